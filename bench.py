@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""bench.py -- frames/s of ORB extract + match (BASELINE.json metric) on 1..N MI355X.
+
+One step = one pass of the hot path over one batch of B synthetic 640x480 frames already
+resident in HBM:  ORBextractor::operator() on every frame (nfeatures 1000, 1.2, 8 levels,
+FAST 20/7) + SearchForTriangulation of frame b against frame b-1 (one BoW node holding all
+features = the BASELINE "BF" configuration) + the cooperative exchange: each agent packs its
+latest keyframe (keypoints + descriptors) and RCCL-all-gathers it, then matches it against
+every agent's slot. One process per GPU = one agent; frames are
+agent-private, so per-GPU work is fixed as N grows ("weak" scaling).
+
+Launch (N>1): python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+              --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cooperative-orb-slam_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def level_sizes(W, H, nlevels=8, scale=1.2):
+    """Level sizes exactly as ComputePyramid (ORBextractor.cc:1111-1112) with float math."""
+    import numpy as np
+    s = [np.float32(1.0)]
+    for _ in range(1, nlevels):
+        s.append(np.float32(np.float64(s[-1]) * np.float64(np.float32(scale))))
+    out = []
+    for sc in s:
+        inv = np.float32(1.0) / sc
+        out.append((int(np.rint(np.float32(W) * inv)), int(np.rint(np.float32(H) * inv))))
+    return out
+
+
+def algorithmic_bytes(W, H, nkp):
+    """Per-frame algorithmic HBM bytes (DESIGN.md "Roofline"): the SURVEY 8(d) figure
+    B_extract = sum_l W_l*H_l (read each level once) + sum_{l>=1} W_l*H_l (write levels 1..7)
+    + 64*N, and the per-stage split used for the dominant-kernel roofline."""
+    ls = level_sizes(W, H)
+    px = [w * h for w, h in ls]
+    total = sum(px) + sum(px[1:]) + 64 * nkp
+    per_stage = {
+        "pyramid": sum(px[:-1]) + sum(px[1:]),   # read level l-1, write level l
+        "fast_cells": sum(px),                   # read every level once
+        "octree": 0,                             # candidate keys only (reported, not priced)
+        "blur": 2 * sum(px),                     # read + write every level
+        "describe": nkp * (31 * 31 + 37 * 37 + 56),  # IC patch + BRIEF patch + 24B kp + 32B desc
+    }
+    return total, per_stage
+
+
+def cpu_baseline(frames, seconds, threads):
+    """Oracle ("port") timed on host cores: extract + BF SearchForTriangulation vs the previous
+    frame, one independent frame stream per thread (ctypes releases the GIL)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle_py
+    import orbamd
+    F12, ex, ey = orbamd.device.default_geometry()
+    count = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(tid):
+        orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+        tabs = orc.tables()
+        prev = None
+        i = tid
+        while time.perf_counter() < stop:
+            img = frames[i % len(frames)]
+            k, d = orc(img)
+            cur = orbamd.KeyFrameView(k, d, tabs["scale"], tabs["sigma2"])
+            if prev is not None:
+                oracle_py.search_for_triangulation(cur, prev, F12, ex, ey, False, False)
+            prev = cur
+            count[tid] += 1
+            i += threads
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    el = time.perf_counter() - t0
+    return sum(count) / el, sum(count), el
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=128, help="frames per step per GPU")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-exchange", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import orbamd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    W, H, B = args.width, args.height, args.batch
+    frames_np = orbamd.synth_frames(rank, 0, B, W, H)  # agent = rank
+    frames = torch.from_numpy(frames_np).to(dev)
+    pipe = orbamd.device.BatchPipeline(torch, W, H, B, device=local)
+    slot_bytes = pipe.slot_bytes()
+    my_slot = torch.zeros(slot_bytes, dtype=torch.uint8, device=dev)
+    all_slots = torch.zeros(world * slot_bytes, dtype=torch.uint8, device=dev)
+    xmatch = torch.empty((world, pipe.stride), dtype=torch.int32, device=dev)
+    xn = torch.zeros(world, dtype=torch.int32, device=dev)
+
+    def step():
+        pipe.step(frames)
+        if not args.no_exchange:
+            pipe.pack(0, my_slot)  # this agent's latest keyframe
+            if world > 1:
+                dist.all_gather_into_tensor(all_slots, my_slot)
+            else:
+                all_slots.copy_(my_slot)
+            pipe.match_packed(0, all_slots, world, xmatch, xn)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    lib = orbamd.load()
+    import ctypes as C
+    lib.orbx_profile_enable(pipe.ext._h, 1)
+    ev_m0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_m1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        pipe.extract(frames)
+        ev_m0[i].record()
+        pipe.match_pairs()
+        ev_m1[i].record()
+        if not args.no_exchange:
+            pipe.pack(0, my_slot)
+            if world > 1:
+                dist.all_gather_into_tensor(all_slots, my_slot)
+            else:
+                all_slots.copy_(my_slot)
+            pipe.match_packed(0, all_slots, world, xmatch, xn)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = (C.c_double * 5)()
+    nc = C.c_int()
+    lib.orbx_profile_read(pipe.ext._h, ms, C.byref(nc))
+    stage_ms = dict(zip(["pyramid", "fast_cells", "octree", "blur", "describe"], [v / max(nc.value, 1) for v in ms]))
+    stage_ms["match"] = sum(a.elapsed_time(b) for a, b in zip(ev_m0, ev_m1)) / args.steps
+    nkp = float(pipe.counts.float().mean().item())
+    nmatch = float(pipe.nmatch.float().mean().item())
+    lib.orbx_profile_enable(pipe.ext._h, 0)
+
+    total_frames = world * B * args.steps
+    value = total_frames / el
+    result = None
+    if rank == 0:
+        b_frame, per_stage = algorithmic_bytes(W, H, nkp)
+        dom = max((k for k in stage_ms if k != "match"), key=lambda k: stage_ms[k])
+        dom_ms = stage_ms[dom]
+        achieved = per_stage[dom] * B / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and per_stage[dom] > 0 else 0.0
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            try:
+                traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        result = {
+            "metric": "frames/sec ORB extract+match, 640x480 mono, 1000 feat/frame",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (deterministic textured pan, SURVEY.md 8(d)); resident in HBM",
+            "config": {"workload": "C2: synthetic %dx%d uint8, nfeatures 1000, scale 1.2, 8 levels, FAST 20/7; "
+                                   "extract + BF SearchForTriangulation vs previous frame + per-step keyframe "
+                                   "all-gather & cross-agent match" % (W, H),
+                       "frames_per_step_per_gpu": B, "parallelism": "agent-per-gpu x%d" % world},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": per_stage[dom] * B,
+                         "launch_ms": round(dom_ms, 4)},
+            "pipeline_hbm": {"bytes_per_frame": b_frame, "achieved_GBs": round(b_frame * value / world / 1e9, 2),
+                             "frac": round(b_frame * value / world / 1e9 / HBM_PEAK_GBS, 5)},
+            "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
+            "kp_per_frame": round(nkp, 1),
+            "matches_per_pair": round(nmatch, 1),
+        }
+    if rank == 0 and not args.no_cpu:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        fps, nfr, sec = cpu_baseline(frames_np, args.cpu_seconds, threads)
+        result["cpu_baseline"] = {"value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+                                  "sample": "%d synthetic 640x480 frames (extract + BF triangulation vs previous) "
+                                            "in %.1f s on %d threads, oracle/orb_oracle.c -O2" % (nfr, sec, threads)}
+        result["speedup_vs_cpu"] = round(value / fps, 1)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    pipe.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

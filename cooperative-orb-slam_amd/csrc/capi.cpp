@@ -1,0 +1,858 @@
+/*
+ * capi.cpp -- host side of the C ABI (include/orbslam_amd.h).
+ *
+ * Owns the per-handle device state, builds the geometry tables once per frame size with
+ * the reference's exact float semantics (ORBextractor.cc:410-470, 765-787, 1107-1112 and
+ * OpenCV 3.x resize coefficients), and sequences the gfx950 kernels on a HIP stream.
+ * There is no CPU fallback: every compute entry point fails with ORBX_EDEVICE when the
+ * device path is unavailable.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/orbslam_amd.h"
+#include "launch.h"
+#include "orb_device.h"
+#include "orb_match.h"
+
+using namespace orbamd;
+
+#define HIPR(expr)                                                                    \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            if (getenv("ORBX_DEBUG")) fprintf(stderr, "HIP error %s at %s:%d\n",     \
+                                              hipGetErrorString(e_), __FILE__, __LINE__); \
+            return ORBX_EDEVICE;                                                      \
+        }                                                                             \
+    } while (0)
+
+namespace {
+
+int cv_round_f(float v) { return (int)lrintf(v); }
+int cv_floor_f(float v) { int i = (int)v; return i - (i > v); }
+int cv_ceil_f(float v) { int i = (int)v; return i + (i < v); }
+short sat_short(float v) {
+    int i = cv_round_f(v);
+    return (short)std::min(32767, std::max(-32768, i));
+}
+long long align_up(long long v, long long a) { return (v + a - 1) / a * a; }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t need) {
+        if (need <= bytes) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, need) != hipSuccess) { p = nullptr; return ORBX_EDEVICE; }
+        bytes = need;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T* as() const { return (T*)p; }
+};
+
+/* ORBextractor constructor tables (ORBextractor.cc:410-470) */
+struct Tables {
+    int nfeatures, nlevels, ini_th, min_th;
+    double scaleFactor;  // double member (ORBextractor.h:100)
+    float scale[kMaxLevels], inv_scale[kMaxLevels], sigma2[kMaxLevels], inv_sigma2[kMaxLevels];
+    int nfeat[kMaxLevels];
+    int umax[16];
+    void build(const orbx_params& p) {
+        nfeatures = p.nfeatures;
+        nlevels = p.nlevels;
+        ini_th = p.ini_th_fast;
+        min_th = p.min_th_fast;
+        scaleFactor = p.scale_factor;
+        scale[0] = 1.0f;
+        sigma2[0] = 1.0f;
+        for (int i = 1; i < nlevels; i++) {
+            scale[i] = (float)(scale[i - 1] * scaleFactor);
+            sigma2[i] = scale[i] * scale[i];
+        }
+        for (int i = 0; i < nlevels; i++) {
+            inv_scale[i] = 1.0f / scale[i];
+            inv_sigma2[i] = 1.0f / sigma2[i];
+        }
+        float factor = (float)(1.0f / scaleFactor);
+        float nDesired = nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)nlevels));
+        int sum = 0;
+        for (int l = 0; l < nlevels - 1; l++) {
+            nfeat[l] = cv_round_f(nDesired);
+            sum += nfeat[l];
+            nDesired *= factor;
+        }
+        nfeat[nlevels - 1] = std::max(nfeatures - sum, 0);
+        int v, v0, vmax = cv_floor_f(kHalfPatch * sqrtf(2.f) / 2 + 1);
+        int vmin = cv_ceil_f(kHalfPatch * sqrtf(2.f) / 2);
+        const double hp2 = kHalfPatch * kHalfPatch;
+        for (v = 0; v <= vmax; ++v) umax[v] = (int)lrint(sqrt(hp2 - v * v));
+        for (v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+            while (umax[v0] == umax[v0 + 1]) ++v0;
+            umax[v] = v0;
+            ++v0;
+        }
+    }
+};
+
+/* Everything that depends on (W, H): host copies + device copies */
+struct Geometry {
+    int W = 0, H = 0;
+    ExtractParams ep{};
+    std::vector<LevelDesc> lv;
+    std::vector<CellDesc> cells;
+    std::vector<int> coef;
+    std::vector<int> tile_begin;
+    int ntiles = 0;
+    int NC = 0, KL = 0, lds_bytes = 0;
+    DevBuf d_lv, d_cells, d_coef, d_tiles;
+
+    int build(const Tables& T, int W_, int H_) {
+        W = W_;
+        H = H_;
+        const int L = T.nlevels;
+        lv.assign(L, LevelDesc{});
+        cells.clear();
+        coef.clear();
+        long long pyr_off = 0, blur_off = 0;
+        int key_begin = 0, kp_off = 0;
+        int maxnode = 0;
+        for (int l = 0; l < L; l++) {
+            LevelDesc& d = lv[l];
+            // ComputePyramid (ORBextractor.cc:1111-1112)
+            d.w = cv_round_f((float)W * T.inv_scale[l]);
+            d.h = cv_round_f((float)H * T.inv_scale[l]);
+            if (d.w < 62 || d.h < 62 || d.w > 4096 || d.h > 4096) return ORBX_EARG;
+            d.pitch = (int)align_up(d.w, 64);
+            d.pyr_off = l == 0 ? 0 : pyr_off;
+            if (l > 0) pyr_off += align_up((long long)d.pitch * d.h, 256);
+            d.blur_off = blur_off;
+            blur_off += align_up((long long)d.pitch * d.h, 256);
+            d.scale = T.scale[l];
+            d.patch_size = (float)(int)(kPatchSize * T.scale[l]);
+            d.blur_vec_end = d.w & ~3;
+            // resize tables from level l-1 (OpenCV resize(), INTER_LINEAR, 8U)
+            if (l > 0) {
+                const int sw = lv[l - 1].w, sh = lv[l - 1].h, dw = d.w, dh = d.h;
+                d.coef_off = (int)coef.size();
+                coef.resize(coef.size() + 2 * dw + 2 * dh);
+                int* xofs = coef.data() + d.coef_off;
+                short* alpha = (short*)(xofs + dw);
+                int* yofs = xofs + 2 * dw;
+                short* beta = (short*)(yofs + dh);
+                const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+                int xmax = dw;
+                for (int dx = 0; dx < dw; dx++) {
+                    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+                    int sx = cv_floor_f(fx);
+                    fx -= sx;
+                    if (sx < 0) { fx = 0; sx = 0; }
+                    if (sx + 1 >= sw) {
+                        xmax = std::min(xmax, dx);
+                        if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+                    }
+                    xofs[dx] = sx;
+                    alpha[2 * dx] = sat_short((1.f - fx) * 2048);
+                    alpha[2 * dx + 1] = sat_short(fx * 2048);
+                }
+                for (int dy = 0; dy < dh; dy++) {
+                    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+                    int sy = cv_floor_f(fy);
+                    fy -= sy;
+                    yofs[dy] = sy;
+                    beta[2 * dy] = sat_short((1.f - fy) * 2048);
+                    beta[2 * dy + 1] = sat_short(fy * 2048);
+                }
+                int se = 0;
+                while (se <= dw - 16) se += 16;
+                while (se < dw - 4) se += 4;
+                d.xmax = xmax;
+                d.simd_end = se;
+                // OpenCV switches INTER_LINEAR to INTER_AREA for exact 2x downscales; unsupported
+                if (std::abs(scale_x - 2.0) < 1e-15 && std::abs(scale_y - 2.0) < 1e-15) return ORBX_EARG;
+            }
+            // FAST cell grid (ORBextractor.cc:769-806)
+            const float Wc = 30;
+            const int minBorderX = kEdgeThreshold - 3, minBorderY = minBorderX;
+            const int maxBorderX = d.w - kEdgeThreshold + 3, maxBorderY = d.h - kEdgeThreshold + 3;
+            const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
+            const int nCols = (int)(width / Wc), nRows = (int)(height / Wc);
+            if (nCols <= 0 || nRows <= 0) return ORBX_EARG;
+            const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+            d.cell_begin = (int)cells.size();
+            d.key_begin = key_begin;
+            int kc = 0;
+            for (int i = 0; i < nRows; i++) {
+                const float iniY = (float)(minBorderY + i * hCell);
+                float maxY = iniY + hCell + 6;
+                if (iniY >= maxBorderY - 3) continue;
+                if (maxY > maxBorderY) maxY = (float)maxBorderY;
+                for (int j = 0; j < nCols; j++) {
+                    const float iniX = (float)(minBorderX + j * wCell);
+                    float maxX = iniX + wCell + 6;
+                    if (iniX >= maxBorderX - 6) continue;
+                    if (maxX > maxBorderX) maxX = (float)maxBorderX;
+                    CellDesc c;
+                    c.level = l;
+                    c.x0 = (int)iniX;
+                    c.y0 = (int)iniY;
+                    c.w = (int)maxX - c.x0;
+                    c.h = (int)maxY - c.y0;
+                    if (c.w > kRoiMax || c.h > kRoiMax) return ORBX_EARG;
+                    c.xoff = j * wCell;
+                    c.yoff = i * hCell;
+                    const int bw = std::max(c.w - 6, 0), bh = std::max(c.h - 6, 0);
+                    c.cap = ((bw + 1) / 2) * ((bh + 1) / 2);
+                    c.slot = key_begin + kc;
+                    kc += c.cap;
+                    cells.push_back(c);
+                }
+            }
+            d.ncells = (int)cells.size() - d.cell_begin;
+            d.key_cap = kc;
+            key_begin += (int)align_up(kc, 64);
+            // DistributeOctTree roots (ORBextractor.cc:542-545)
+            d.minX = minBorderX;
+            d.maxX = maxBorderX;
+            d.minY = minBorderY;
+            d.maxY = maxBorderY;
+            d.nIni = (int)roundf((float)(maxBorderX - minBorderX) / (maxBorderY - minBorderY));
+            if (d.nIni <= 0) return ORBX_EARG;
+            d.hX = (float)(maxBorderX - minBorderX) / d.nIni;
+            d.N = T.nfeat[l];
+            d.node_cap = std::max(d.N + 3, 4 * d.nIni);
+            d.kp_off = kp_off;
+            d.kp_cap = d.node_cap;
+            kp_off += d.kp_cap;
+            maxnode = std::max(maxnode, d.node_cap);
+        }
+        ep.L = L;
+        ep.ncells = (int)cells.size();
+        ep.keys_per_frame = key_begin;
+        ep.kp_per_frame = kp_off;
+        ep.ini_th = T.ini_th;
+        ep.min_th = T.min_th;
+        ep.pyr_frame_bytes = align_up(pyr_off, 256);
+        ep.blur_frame_bytes = align_up(blur_off, 256);
+        for (int v = 0; v < 16; v++) ep.umax[v] = T.umax[v];
+        // blur tiles (64 x 16)
+        tile_begin.assign(L + 1, 0);
+        for (int l = 0; l < L; l++)
+            tile_begin[l + 1] = tile_begin[l] + ((lv[l].w + 63) / 64) * ((lv[l].h + 15) / 16);
+        ntiles = tile_begin[L];
+        // octree LDS: node arrays (92 B/node, NC pow2) + keys (7 B/key)
+        NC = 1;
+        while (NC < maxnode) NC <<= 1;
+        const int node_bytes = 92 * NC;
+        const int budget = 64 * 1024;
+        if (node_bytes + 7 * 256 > 160 * 1024) return ORBX_EARG;
+        int lds = std::max(budget, node_bytes + 7 * 1024);
+        KL = ((lds - node_bytes) / 7) & ~15;
+        lds_bytes = node_bytes + 7 * KL;
+        // upload
+        if (d_lv.ensure(sizeof(LevelDesc) * L) || d_cells.ensure(sizeof(CellDesc) * cells.size()) ||
+            d_coef.ensure(sizeof(int) * std::max<size_t>(coef.size(), 1)) || d_tiles.ensure(sizeof(int) * (L + 1)))
+            return ORBX_EDEVICE;
+        HIPR(hipMemcpy(d_lv.p, lv.data(), sizeof(LevelDesc) * L, hipMemcpyHostToDevice));
+        HIPR(hipMemcpy(d_cells.p, cells.data(), sizeof(CellDesc) * cells.size(), hipMemcpyHostToDevice));
+        if (!coef.empty()) HIPR(hipMemcpy(d_coef.p, coef.data(), sizeof(int) * coef.size(), hipMemcpyHostToDevice));
+        HIPR(hipMemcpy(d_tiles.p, tile_begin.data(), sizeof(int) * (L + 1), hipMemcpyHostToDevice));
+        return 0;
+    }
+    void release() { d_lv.release(); d_cells.release(); d_coef.release(); d_tiles.release(); }
+};
+
+}  // namespace
+
+struct orbx_handle {
+    orbx_params params;
+    Tables T;
+    int device = 0;
+    int max_w = 0, max_h = 0, max_batch = 1;
+    hipStream_t stream = nullptr;
+    Geometry geo;
+    DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
+    // host-path staging
+    DevBuf in_frame, out_kps, out_desc, out_cnt;
+    // last extraction, for orbx_pyramid_level
+    const uint8_t* last_frames = nullptr;
+    long long last_fstride = 0;
+    int last_pitch = 0, last_nframes = 0;
+    bool lds_attr_set = false;
+    // stage profiling (orbx_profile_*)
+    bool prof_on = false;
+    std::vector<hipEvent_t> prof_ev;  // groups of 6
+    int prof_calls = 0;
+    double prof_ms[5] = {0, 0, 0, 0, 0};
+};
+
+static const int kProfMaxCalls = 4096;
+
+static int prof_mark(orbx_handle* h, int k, hipStream_t st) {
+    if (!h->prof_on) return 0;
+    if (h->prof_calls >= kProfMaxCalls) return 0;
+    const size_t need = (size_t)(h->prof_calls + 1) * 6;
+    while (h->prof_ev.size() < need) {
+        hipEvent_t e;
+        HIPR(hipEventCreate(&e));
+        h->prof_ev.push_back(e);
+    }
+    HIPR(hipEventRecord(h->prof_ev[(size_t)h->prof_calls * 6 + k], st));
+    if (k == 5) h->prof_calls++;
+    return 0;
+}
+
+static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
+    if (nframes < 1 || nframes > h->max_batch) return ORBX_EARG;
+    if (h->geo.W != W || h->geo.H != H) {
+        int rc = h->geo.build(h->T, W, H);
+        if (rc) { h->geo.W = h->geo.H = 0; return rc; }
+    }
+    const ExtractParams& ep = h->geo.ep;
+    const size_t B = (size_t)h->max_batch;
+    if (h->pyr.ensure(B * ep.pyr_frame_bytes) || h->blur.ensure(B * ep.blur_frame_bytes) ||
+        h->cellkey.ensure(B * ep.keys_per_frame * 4) || h->cellcnt.ensure(B * ep.ncells * 4) ||
+        h->lvkey.ensure(B * ep.kp_per_frame * 4) || h->lvcnt.ensure(B * ep.L * 4) ||
+        h->gscratch.ensure(B * (size_t)ep.keys_per_frame * 8) || h->err.ensure(256))
+        return ORBX_EDEVICE;
+    if (!h->lds_attr_set) {
+        HIPR(octree_setup(160 * 1024));
+        h->lds_attr_set = true;
+    }
+    return 0;
+}
+
+static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
+                       orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st) {
+    Geometry& g = h->geo;
+    const ExtractParams& ep = g.ep;
+    const LevelDesc* dl = g.d_lv.as<LevelDesc>();
+    if (prof_mark(h, 0, st)) return ORBX_EDEVICE;
+    // pyramid levels 1..L-1 (ORBextractor.cc:1107-1132)
+    for (int l = 1; l < ep.L; l++) {
+        const LevelDesc& s = g.lv[l - 1];
+        const LevelDesc& d = g.lv[l];
+        const uint8_t* src = l == 1 ? d_frames : h->pyr.as<uint8_t>() + s.pyr_off;
+        const long long sfs = l == 1 ? fstride : ep.pyr_frame_bytes;
+        const int sp = l == 1 ? pitch : s.pitch;
+        HIPR(launch_resize(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes, d.pitch,
+                           d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, st));
+    }
+    if (prof_mark(h, 1, st)) return ORBX_EDEVICE;
+    HIPR(launch_fast_cells(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, g.d_cells.as<CellDesc>(),
+                           h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), nframes, st));
+    if (prof_mark(h, 2, st)) return ORBX_EDEVICE;
+    HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
+                       h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
+                       (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, h->err.as<int>(), nframes, st));
+    if (prof_mark(h, 3, st)) return ORBX_EDEVICE;
+    HIPR(launch_blur(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                     g.d_tiles.as<int>(), g.ntiles, h->lvcnt.as<int>(), nframes, st));
+    if (prof_mark(h, 4, st)) return ORBX_EDEVICE;
+    HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                         h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride, nframes,
+                         st));
+    if (prof_mark(h, 5, st)) return ORBX_EDEVICE;
+    h->last_frames = d_frames;
+    h->last_fstride = fstride;
+    h->last_pitch = pitch;
+    h->last_nframes = nframes;
+    return 0;
+}
+
+extern "C" {
+
+const char* orbx_version(void) { return "orbslam-mi355x 0.1 (gfx950)"; }
+
+int orbx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int orbx_create(const orbx_params* p, int device, int max_width, int max_height, int max_batch,
+                orbx_handle** out) {
+    if (!p || !out || p->nlevels < 1 || p->nlevels > kMaxLevels || p->nfeatures < 1 || p->scale_factor <= 1.0f ||
+        max_width <= 0 || max_height <= 0 || max_batch < 1)
+        return ORBX_EARG;
+    *out = nullptr;
+    int ndev = orbx_device_count();
+    if (device < 0 || device >= ndev) return ORBX_EDEVICE;
+    HIPR(hipSetDevice(device));
+    orbx_handle* h = new orbx_handle();
+    h->params = *p;
+    h->T.build(*p);
+    h->device = device;
+    h->max_w = max_width;
+    h->max_h = max_height;
+    h->max_batch = max_batch;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return ORBX_EDEVICE;
+    }
+    int rc = ensure_geometry(h, max_width, max_height, 1);
+    if (rc) {
+        orbx_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return 0;
+}
+
+void orbx_destroy(orbx_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (DevBuf* b : {&h->pyr, &h->blur, &h->cellkey, &h->cellcnt, &h->lvkey, &h->lvcnt, &h->gscratch, &h->err,
+                      &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt})
+        b->release();
+    h->geo.release();
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
+    delete h;
+}
+
+int orbx_profile_enable(orbx_handle* h, int on) {
+    if (!h) return ORBX_EARG;
+    h->prof_on = on != 0;
+    h->prof_calls = 0;
+    for (double& v : h->prof_ms) v = 0;
+    return 0;
+}
+
+int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls) {
+    if (!h) return ORBX_EARG;
+    HIPR(hipSetDevice(h->device));
+    double acc[5] = {0, 0, 0, 0, 0};
+    for (int c = 0; c < h->prof_calls; c++) {
+        HIPR(hipEventSynchronize(h->prof_ev[(size_t)c * 6 + 5]));
+        for (int k = 0; k < 5; k++) {
+            float t = 0;
+            HIPR(hipEventElapsedTime(&t, h->prof_ev[(size_t)c * 6 + k], h->prof_ev[(size_t)c * 6 + k + 1]));
+            acc[k] += t;
+        }
+    }
+    if (ms) for (int k = 0; k < 5; k++) ms[k] = acc[k];
+    if (ncalls) *ncalls = h->prof_calls;
+    return 0;
+}
+
+int orbx_max_keypoints(const orbx_handle* h, int width, int height) {
+    if (!h) return ORBX_EARG;
+    if (h->geo.W == width && h->geo.H == height) return h->geo.ep.kp_per_frame;
+    // host-only computation of the cap (no upload): replicate build's kp accounting
+    int total = 0;
+    for (int l = 0; l < h->T.nlevels; l++) {
+        const int w = cv_round_f((float)width * h->T.inv_scale[l]);
+        const int hh = cv_round_f((float)height * h->T.inv_scale[l]);
+        const int nIni = (int)roundf((float)(w - 32) / (hh - 32));
+        total += std::max(h->T.nfeat[l] + 3, 4 * std::max(nIni, 1));
+    }
+    return total;
+}
+
+int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_frames, size_t frame_stride, int width,
+                              int height, size_t pitch, orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
+                              int kp_stride, void* stream) {
+    if (!h || !d_frames || !d_kps || !d_desc || !d_counts || width <= 0 || height <= 0 || pitch < (size_t)width)
+        return ORBX_EARG;
+    HIPR(hipSetDevice(h->device));
+    int rc = ensure_geometry(h, width, height, nframes);
+    if (rc) return rc;
+    if (kp_stride < h->geo.ep.kp_per_frame) return ORBX_ECAPACITY;
+    return run_extract(h, nframes, d_frames, (long long)frame_stride, (int)pitch, d_kps, d_desc, d_counts, kp_stride,
+                       (hipStream_t)stream);
+}
+
+int orbx_extract(orbx_handle* h, const uint8_t* img, int width, int height, size_t pitch, orbx_kp* kps,
+                 uint8_t* desc, int cap, int* n) {
+    if (!h || !n) return ORBX_EARG;
+    *n = 0;
+    if (width <= 0 || height <= 0 || !img) return 0;  // empty image: outputs untouched (:1046-1047)
+    if (pitch < (size_t)width) return ORBX_EARG;
+    HIPR(hipSetDevice(h->device));
+    int rc = ensure_geometry(h, width, height, 1);
+    if (rc) return rc;
+    const int K = h->geo.ep.kp_per_frame;
+    if (h->in_frame.ensure((size_t)width * height) || h->out_kps.ensure(sizeof(orbx_kp) * K) ||
+        h->out_desc.ensure(32 * (size_t)K) || h->out_cnt.ensure(64))
+        return ORBX_EDEVICE;
+    HIPR(hipMemcpy2DAsync(h->in_frame.p, width, img, pitch, width, height, hipMemcpyHostToDevice, h->stream));
+    rc = run_extract(h, 1, h->in_frame.as<uint8_t>(), (long long)width * height, width, h->out_kps.as<orbx_kp>(),
+                     h->out_desc.as<uint8_t>(), h->out_cnt.as<int32_t>(), K, h->stream);
+    if (rc) return rc;
+    int cnt = 0, errflag = 0;
+    HIPR(hipMemcpyAsync(&cnt, h->out_cnt.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPR(hipMemcpyAsync(&errflag, h->err.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPR(hipStreamSynchronize(h->stream));
+    if (errflag) return ORBX_EDEVICE;
+    if (cnt > cap) return ORBX_ECAPACITY;
+    if (cnt > 0) {
+        if (kps) HIPR(hipMemcpyAsync(kps, h->out_kps.p, sizeof(orbx_kp) * cnt, hipMemcpyDeviceToHost, h->stream));
+        if (desc) HIPR(hipMemcpyAsync(desc, h->out_desc.p, 32 * (size_t)cnt, hipMemcpyDeviceToHost, h->stream));
+        HIPR(hipStreamSynchronize(h->stream));
+    }
+    *n = cnt;
+    return 0;
+}
+
+int orbx_pyramid_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t pitch, int* width, int* height) {
+    if (!h || level < 0 || level >= h->T.nlevels || !h->geo.W) return ORBX_EARG;
+    const LevelDesc& d = h->geo.lv[level];
+    if (width) *width = d.w;
+    if (height) *height = d.h;
+    if (!dst) return 0;
+    if (!h->last_frames || frame < 0 || frame >= h->last_nframes || pitch < (size_t)d.w) return ORBX_EARG;
+    HIPR(hipSetDevice(h->device));
+    HIPR(hipDeviceSynchronize());
+    const uint8_t* src = level == 0 ? h->last_frames + frame * h->last_fstride
+                                    : h->pyr.as<uint8_t>() + frame * h->geo.ep.pyr_frame_bytes + d.pyr_off;
+    const size_t sp = level == 0 ? (size_t)h->last_pitch : (size_t)d.pitch;
+    HIPR(hipMemcpy2D(dst, pitch, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int orbx_get_levels(const orbx_handle* h) { return h ? h->T.nlevels : ORBX_EARG; }
+float orbx_get_scale_factor(const orbx_handle* h) { return h ? (float)h->T.scaleFactor : 0.f; }
+
+int orbx_get_scale_tables(const orbx_handle* h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2) {
+    if (!h) return ORBX_EARG;
+    for (int l = 0; l < h->T.nlevels; l++) {
+        if (scale) scale[l] = h->T.scale[l];
+        if (inv_scale) inv_scale[l] = h->T.inv_scale[l];
+        if (sigma2) sigma2[l] = h->T.sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = h->T.inv_sigma2[l];
+    }
+    return 0;
+}
+
+int orbx_get_feature_split(const orbx_handle* h, int32_t* per_level, int32_t* umax16) {
+    if (!h) return ORBX_EARG;
+    for (int l = 0; l < h->T.nlevels; l++)
+        if (per_level) per_level[l] = h->T.nfeat[l];
+    for (int v = 0; v < 16; v++)
+        if (umax16) umax16[v] = h->T.umax[v];
+    return 0;
+}
+
+size_t orbx_slot_bytes(int cap) {
+    const long long c = (cap + 1) & ~1;
+    return (size_t)align_up(64 + c * (long long)sizeof(orbx_kp) + c * 32, 256);
+}
+
+int orbx_pack_keyframe_device(const orbx_kp* d_kps, const uint8_t* d_desc, const int32_t* d_count, int cap,
+                              uint8_t* d_slot, void* stream) {
+    if (!d_kps || !d_desc || !d_count || !d_slot || cap < 1) return ORBX_EARG;
+    HIPR(launch_pack_slot(d_kps, d_desc, d_count, (cap + 1) & ~1, d_slot, (hipStream_t)stream));
+    return 0;
+}
+
+}  // extern "C"
+
+/* ===================================================================================== */
+/* Matcher                                                                               */
+/* ===================================================================================== */
+struct orbm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf scratch;
+    std::vector<uint8_t> host;
+};
+
+namespace {
+
+void make_geom(MatchGeom& g, const float F12[9], float ex, float ey, int nlevels, const float* scale,
+               const float* sigma2) {
+    for (int i = 0; i < 9; i++) g.F[i] = F12[i];
+    g.ex = ex;
+    g.ey = ey;
+    for (int o = 0; o < 16; o++) {
+        g.th100[o] = o < nlevels ? 100 * scale[o] : 0.f;
+        g.th384[o] = o < nlevels ? 3.84 * (double)sigma2[o] : 0.0;
+    }
+}
+
+/* bump allocator over the ctx scratch buffer (sizes first, then carve) */
+struct Carve {
+    size_t off = 0;
+    size_t take(size_t b) { size_t o = off; off += align_up((long long)b, 256); return o; }
+};
+
+/* merge-walk of two FeatureVectors (DBoW2 std::map iteration with lower_bound jumps,
+ * ORBmatcher.cc:691-789): returns the common (node index 1, node index 2) pairs */
+void common_nodes(const orbm_kf_view* a, const orbm_kf_view* b, std::vector<std::pair<int, int>>& out) {
+    out.clear();
+    int i = 0, j = 0;
+    while (i < a->n_nodes && j < b->n_nodes) {
+        if (a->node_id[i] == b->node_id[j]) {
+            out.emplace_back(i, j);
+            i++;
+            j++;
+        } else if (a->node_id[i] < b->node_id[j]) {
+            i = (int)(std::lower_bound(a->node_id + i, a->node_id + a->n_nodes, b->node_id[j]) - a->node_id);
+        } else {
+            j = (int)(std::lower_bound(b->node_id + j, b->node_id + b->n_nodes, a->node_id[i]) - b->node_id);
+        }
+    }
+}
+
+bool view_ok(const orbm_kf_view* v) {
+    return v && v->n >= 0 && (v->n == 0 || (v->desc && v->x && v->y && v->angle && v->octave)) && v->n_nodes >= 0 &&
+           (v->n_nodes == 0 || (v->node_id && v->node_off && v->node_feat)) && v->nlevels > 0 && v->nlevels <= 16 &&
+           v->scale_factors && v->level_sigma2;
+}
+
+/* upload one view into the scratch at offsets computed by plan_view */
+struct ViewPlan {
+    size_t desc, x, y, angle, octave, uright, has_mp, mp_bad, feat;
+    int nfeat;
+};
+void plan_view(Carve& c, const orbm_kf_view* v, ViewPlan& p) {
+    const size_t n = (size_t)std::max(v->n, 1);
+    p.nfeat = v->n_nodes ? v->node_off[v->n_nodes] : 0;
+    p.desc = c.take(32 * n);
+    p.x = c.take(4 * n);
+    p.y = c.take(4 * n);
+    p.angle = c.take(4 * n);
+    p.octave = c.take(4 * n);
+    p.uright = v->uright ? c.take(4 * n) : (size_t)-1;
+    p.has_mp = v->has_mp ? c.take(n) : (size_t)-1;
+    p.mp_bad = v->mp_bad ? c.take(n) : (size_t)-1;
+    p.feat = c.take(4 * (size_t)std::max(p.nfeat, 1));
+}
+int upload_view(orbm_ctx* ctx, const orbm_kf_view* v, const ViewPlan& p, DevView& d) {
+    uint8_t* base = ctx->scratch.as<uint8_t>();
+    hipStream_t st = ctx->stream;
+    const size_t n = (size_t)v->n;
+    d.n = v->n;
+    d.desc = base + p.desc;
+    d.x = (const float*)(base + p.x);
+    d.y = (const float*)(base + p.y);
+    d.angle = (const float*)(base + p.angle);
+    d.octave = (const int32_t*)(base + p.octave);
+    d.uright = v->uright ? (const float*)(base + p.uright) : nullptr;
+    d.has_mp = v->has_mp ? base + p.has_mp : nullptr;
+    d.mp_bad = v->mp_bad ? base + p.mp_bad : nullptr;
+    d.node_feat = (const int32_t*)(base + p.feat);
+    if (n) {
+        HIPR(hipMemcpyAsync(base + p.desc, v->desc, 32 * n, hipMemcpyHostToDevice, st));
+        HIPR(hipMemcpyAsync(base + p.x, v->x, 4 * n, hipMemcpyHostToDevice, st));
+        HIPR(hipMemcpyAsync(base + p.y, v->y, 4 * n, hipMemcpyHostToDevice, st));
+        HIPR(hipMemcpyAsync(base + p.angle, v->angle, 4 * n, hipMemcpyHostToDevice, st));
+        HIPR(hipMemcpyAsync(base + p.octave, v->octave, 4 * n, hipMemcpyHostToDevice, st));
+        if (v->uright) HIPR(hipMemcpyAsync(base + p.uright, v->uright, 4 * n, hipMemcpyHostToDevice, st));
+        if (v->has_mp) HIPR(hipMemcpyAsync(base + p.has_mp, v->has_mp, n, hipMemcpyHostToDevice, st));
+        if (v->mp_bad) HIPR(hipMemcpyAsync(base + p.mp_bad, v->mp_bad, n, hipMemcpyHostToDevice, st));
+    }
+    if (p.nfeat) HIPR(hipMemcpyAsync(base + p.feat, v->node_feat, 4 * (size_t)p.nfeat, hipMemcpyHostToDevice, st));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbm_create(int device, orbm_ctx** out) {
+    if (!out) return ORBX_EARG;
+    *out = nullptr;
+    if (device < 0 || device >= orbx_device_count()) return ORBX_EDEVICE;
+    HIPR(hipSetDevice(device));
+    orbm_ctx* c = new orbm_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return ORBX_EDEVICE;
+    }
+    *out = c;
+    return 0;
+}
+
+void orbm_destroy(orbm_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->scratch.release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+/* ORBmatcher::DescriptorDistance (ORBmatcher.cc:1647-1663) -- host scalar */
+int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+    if (!a || !b) return ORBX_EARG;
+    int d = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        memcpy(&x, a + 4 * i, 4);
+        memcpy(&y, b + 4 * i, 4);
+        d += __builtin_popcount(x ^ y);
+    }
+    return d;
+}
+
+void orbm_epipole(const float R2w[9], const float t2w[3], const float Cw[3], float fx, float fy, float cx, float cy,
+                  float* ex, float* ey) {
+    float C2[3];
+    for (int i = 0; i < 3; i++) {
+        double s = 0;
+        for (int k = 0; k < 3; k++) s += (double)R2w[3 * i + k] * (double)Cw[k];
+        C2[i] = (float)(s * 1.0 + (double)t2w[i] * 1.0);  // cv::gemm(R, C, 1, t, 1)
+    }
+    const float invz = 1.0f / C2[2];
+    *ex = fx * C2[0] * invz + cx;
+    *ey = fy * C2[1] * invz + cy;
+}
+
+static int count_matches(const int32_t* m, int n) {
+    int c = 0;
+    for (int i = 0; i < n; i++) c += m[i] >= 0;
+    return c;
+}
+
+int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2,
+                                  const float F12[9], float ex, float ey, int only_stereo, int check_ori,
+                                  int32_t* match12, int* nmatches) {
+    if (!ctx || !view_ok(kf1) || !view_ok(kf2) || !F12 || !match12) return ORBX_EARG;
+    HIPR(hipSetDevice(ctx->device));
+    std::vector<std::pair<int, int>> common;
+    common_nodes(kf1, kf2, common);
+    std::vector<NodeTask> tasks;
+    for (auto& c : common) {
+        const int qb = kf1->node_off[c.first], qe = kf1->node_off[c.first + 1];
+        for (int q = qb; q < qe; q += 64)
+            tasks.push_back({q, std::min(q + 64, qe), kf2->node_off[c.second], kf2->node_off[c.second + 1]});
+    }
+    Carve cv;
+    ViewPlan p1, p2;
+    plan_view(cv, kf1, p1);
+    plan_view(cv, kf2, p2);
+    const size_t o_tasks = cv.take(sizeof(NodeTask) * std::max<size_t>(tasks.size(), 1));
+    const size_t o_out = cv.take(4 * (size_t)std::max(kf1->n, 1));
+    if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
+    DevView d1, d2;
+    if (upload_view(ctx, kf1, p1, d1) || upload_view(ctx, kf2, p2, d2)) return ORBX_EDEVICE;
+    uint8_t* base = ctx->scratch.as<uint8_t>();
+    if (!tasks.empty())
+        HIPR(hipMemcpyAsync(base + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size(), hipMemcpyHostToDevice,
+                            ctx->stream));
+    int32_t* dout = (int32_t*)(base + o_out);
+    HIPR(hipMemsetAsync(dout, 0xFF, 4 * (size_t)std::max(kf1->n, 1), ctx->stream));
+    MatchGeom g;
+    make_geom(g, F12, ex, ey, kf2->nlevels, kf2->scale_factors, kf2->level_sigma2);
+    HIPR(launch_tri_nodes(d1, d2, (const NodeTask*)(base + o_tasks), (int)tasks.size(), g, only_stereo, dout,
+                          ctx->stream));
+    if (check_ori) HIPR(launch_rot_filter(kf1->n, dout, d1.angle, d2.angle, 0, nullptr, ctx->stream));
+    if (kf1->n) HIPR(hipMemcpyAsync(match12, dout, 4 * (size_t)kf1->n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    if (nmatches) *nmatches = count_matches(match12, kf1->n);
+    return 0;
+}
+
+static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view* vc, float nnratio, int check_ori,
+                      int mode, int32_t* out, int nout, int* nmatches) {
+    HIPR(hipSetDevice(ctx->device));
+    std::vector<std::pair<int, int>> common;
+    common_nodes(vq, vc, common);
+    std::vector<NodeTask> tasks;
+    int max_nc = 1;
+    for (auto& c : common) {
+        NodeTask t{vq->node_off[c.first], vq->node_off[c.first + 1], vc->node_off[c.second],
+                   vc->node_off[c.second + 1]};
+        max_nc = std::max(max_nc, t.c_end - t.c_begin);
+        tasks.push_back(t);
+    }
+    if (max_nc > 64 * 1024) return ORBX_EARG;
+    Carve cv;
+    ViewPlan pq, pc;
+    plan_view(cv, vq, pq);
+    plan_view(cv, vc, pc);
+    const size_t o_tasks = cv.take(sizeof(NodeTask) * std::max<size_t>(tasks.size(), 1));
+    const size_t o_out = cv.take(4 * (size_t)std::max(nout, 1));
+    if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
+    DevView dq, dc;
+    if (upload_view(ctx, vq, pq, dq) || upload_view(ctx, vc, pc, dc)) return ORBX_EDEVICE;
+    uint8_t* base = ctx->scratch.as<uint8_t>();
+    if (!tasks.empty())
+        HIPR(hipMemcpyAsync(base + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size(), hipMemcpyHostToDevice,
+                            ctx->stream));
+    int32_t* dout = (int32_t*)(base + o_out);
+    HIPR(hipMemsetAsync(dout, 0xFF, 4 * (size_t)std::max(nout, 1), ctx->stream));
+    HIPR(launch_bow(dq, dc, (const NodeTask*)(base + o_tasks), (int)tasks.size(), max_nc, nnratio, mode, dout,
+                    ctx->stream));
+    if (check_ori) {
+        if (mode == 0)  // out indexed by F idx, partner = KF idx: rot = angKF[m] - angF[i]
+            HIPR(launch_rot_filter(nout, dout, dq.angle, dc.angle, 1, nullptr, ctx->stream));
+        else
+            HIPR(launch_rot_filter(nout, dout, dq.angle, dc.angle, 0, nullptr, ctx->stream));
+    }
+    if (nout) HIPR(hipMemcpyAsync(out, dout, 4 * (size_t)nout, hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    if (nmatches) *nmatches = count_matches(out, nout);
+    return 0;
+}
+
+int orbm_search_by_bow_kf_f(orbm_ctx* ctx, const orbm_kf_view* kf, const orbm_kf_view* f, float nnratio,
+                            int check_ori, int32_t* match_f, int* nmatches) {
+    if (!ctx || !view_ok(kf) || !view_ok(f) || !match_f) return ORBX_EARG;
+    return bow_common(ctx, kf, f, nnratio, check_ori, 0, match_f, f->n, nmatches);
+}
+
+int orbm_search_by_bow_kf_kf(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2, float nnratio,
+                             int check_ori, int32_t* match12, int* nmatches) {
+    if (!ctx || !view_ok(kf1) || !view_ok(kf2) || !match12) return ORBX_EARG;
+    return bow_common(ctx, kf1, kf2, nnratio, check_ori, 1, match12, kf1->n, nmatches);
+}
+
+int orbm_triangulation_bf_batch_device(orbm_ctx* ctx, int npairs, const int32_t* d_q1, const int32_t* d_q2,
+                                       const orbx_kp* d_kps, const uint8_t* d_desc, const int32_t* d_counts,
+                                       int kp_stride, const float F12[9], float ex, float ey, int nlevels,
+                                       const float* scale_factors, const float* level_sigma2, int check_ori,
+                                       int32_t* d_match12, int32_t* d_nmatches, void* stream) {
+    if (!ctx || npairs < 0 || !F12 || nlevels < 1 || nlevels > 16 || !scale_factors || !level_sigma2 ||
+        kp_stride < 1)
+        return ORBX_EARG;
+    if (npairs == 0) return 0;
+    HIPR(hipSetDevice(ctx->device));
+    MatchGeom g;
+    make_geom(g, F12, ex, ey, nlevels, scale_factors, level_sigma2);
+    hipStream_t st = (hipStream_t)stream;
+    HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * npairs, st));
+    HIPR(launch_tri_bf(npairs, d_q1, d_q2, d_kps, d_desc, d_counts, kp_stride, g, d_match12, d_nmatches, st));
+    if (check_ori)
+        HIPR(launch_rot_filter_pairs(npairs, d_q1, d_q2, d_kps, d_counts, kp_stride, d_match12, d_nmatches, st));
+    return 0;
+}
+
+int orbm_triangulation_bf_packed_device(orbm_ctx* ctx, const orbx_kp* d_kps1, const uint8_t* d_desc1,
+                                        const int32_t* d_count1, int nref, const uint8_t* d_slots,
+                                        size_t slot_bytes, const float F12[9], float ex, float ey, int nlevels,
+                                        const float* scale_factors, const float* level_sigma2, int32_t* d_match,
+                                        int cap1, int32_t* d_nmatches, void* stream) {
+    if (!ctx || nref < 0 || !F12 || nlevels < 1 || nlevels > 16 || cap1 < 1) return ORBX_EARG;
+    if (nref == 0) return 0;
+    HIPR(hipSetDevice(ctx->device));
+    // slot capacity implied by slot_bytes: 64 + cap*24 + cap*32 <= slot_bytes
+    const int slot_cap = (int)(((long long)slot_bytes - 64) / (long long)(sizeof(orbx_kp) + 32)) & ~1;
+    MatchGeom g;
+    make_geom(g, F12, ex, ey, nlevels, scale_factors, level_sigma2);
+    hipStream_t st = (hipStream_t)stream;
+    HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * nref, st));
+    HIPR(launch_tri_bf_packed(d_kps1, d_desc1, d_count1, nref, d_slots, (long long)slot_bytes, slot_cap, g, d_match,
+                              cap1, d_nmatches, st));
+    return 0;
+}
+
+}  // extern "C"

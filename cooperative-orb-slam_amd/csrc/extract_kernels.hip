@@ -1,0 +1,790 @@
+/*
+ * extract_kernels.hip -- gfx950 kernels for ORBextractor::operator() (ORBextractor.cc:1043-1105).
+ *
+ * One launch per stage over a whole batch of frames (grid.y / grid.z = frame):
+ *   k_resize_level   ComputePyramid, one launch per level 1..L-1      (ORBextractor.cc:1107-1132)
+ *   k_fast_cells     per-cell cv::FAST + 3x3 NMS + threshold fallback (ORBextractor.cc:789-829)
+ *   k_octree         DistributeOctTree, one workgroup per (frame,level) (ORBextractor.cc:539-763)
+ *   k_blur           GaussianBlur 7x7 sigma 2 REFLECT_101 per level   (ORBextractor.cc:1085-1086)
+ *   k_describe       IC_Angle + rBRIEF + output assembly, one wave per keypoint
+ *                    (ORBextractor.cc:77-147, 851-852, 1075-1104)
+ * All of it is integer/byte work bounded by HBM/LDS and VALU issue; no MFMA.
+ * Exact-semantics notes live in DESIGN.md "Pinned semantics".
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbslam_amd.h"
+#include "orb_device.h"
+#include "orb_math.h"
+#include "orb_pattern.h"
+
+namespace orbamd {
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lane_prefix(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
+}
+
+__device__ __forceinline__ int iclamp(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* ----------------------------------------------------------------------------------- */
+/* Pyramid: cv::resize(INTER_LINEAR) 8U fixed point, one output pixel per lane.        */
+/* xofs/alpha/yofs/beta are the host-built tables of resizeGeneric_.       */
+/* ----------------------------------------------------------------------------------- */
+__global__ __launch_bounds__(256) void k_resize_level(
+    const uint8_t* __restrict__ src, long long src_fstride, int src_pitch, int sw, int sh,
+    uint8_t* __restrict__ dst, long long dst_fstride, int dst_pitch, int dw, int dh,
+    const int* __restrict__ xofs, const short2* __restrict__ alpha, const int* __restrict__ yofs,
+    const short2* __restrict__ beta, int xmax, int simd_end) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= dw || y >= dh) return;
+    const uint8_t* S = src + (long long)blockIdx.z * src_fstride;
+    const int sy = yofs[y];
+    const int r0 = iclamp(sy, 0, sh - 1), r1 = iclamp(sy + 1, 0, sh - 1);
+    const uint8_t* S0 = S + (long long)r0 * src_pitch;
+    const uint8_t* S1 = S + (long long)r1 * src_pitch;
+    const short2 b = beta[y];
+    const int sx = xofs[x];
+    int h0, h1;
+    if (x < xmax) {
+        const short2 a = alpha[x];
+        h0 = S0[sx] * a.x + S0[sx + 1] * a.y;
+        h1 = S1[sx] * a.x + S1[sx + 1] * a.y;
+    } else {
+        h0 = S0[sx] * 2048;
+        h1 = S1[sx] * 2048;
+    }
+    int v;
+    if (x < simd_end)  // SSE2 VResizeLinearVec_32s8u: mulhi_epi16 on (h >> 4)
+        v = ((((h0 >> 4) * b.x) >> 16) + (((h1 >> 4) * b.y) >> 16) + 2) >> 2;
+    else  // scalar FixedPtCast<int, uchar, 22>
+        v = (h0 * b.x + h1 * b.y + (1 << 21)) >> 22;
+    dst[(long long)blockIdx.z * dst_fstride + (long long)y * dst_pitch + x] = (uint8_t)iclamp(v, 0, 255);
+}
+
+/* ----------------------------------------------------------------------------------- */
+/* FAST-9/16 "strength": S = max over the 16 cyclic 9-arcs of min(v-ring) or min(ring-v). */
+/* A pixel is a cv::FAST corner at threshold t iff S > t, and then cornerScore<16> = S-1  */
+/* (threshold-independent), so one S map serves both thresholds of the cell fallback.    */
+/* ----------------------------------------------------------------------------------- */
+__device__ __forceinline__ int fast_strength(const uint8_t* p, int P) {
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * P];
+    d[1] = v - p[1 + 3 * P];
+    d[2] = v - p[2 + 2 * P];
+    d[3] = v - p[3 + 1 * P];
+    d[4] = v - p[3];
+    d[5] = v - p[3 - 1 * P];
+    d[6] = v - p[2 - 2 * P];
+    d[7] = v - p[1 - 3 * P];
+    d[8] = v - p[-3 * P];
+    d[9] = v - p[-1 - 3 * P];
+    d[10] = v - p[-2 - 2 * P];
+    d[11] = v - p[-3 - 1 * P];
+    d[12] = v - p[-3];
+    d[13] = v - p[-3 + 1 * P];
+    d[14] = v - p[-2 + 2 * P];
+    d[15] = v - p[-1 + 3 * P];
+    int mn2[16], mx2[16], mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn2[k] = min(d[k], d[(k + 1) & 15]);
+        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    }
+    int A = -1024, Bm = 1024;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+        int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+        A = max(A, mn9);
+        Bm = min(Bm, mx9);
+    }
+    int S = max(A, -Bm);
+    return S < 0 ? 0 : S;
+}
+
+/* NMS survivor test of cv::FAST (FAST_t, nonmax_suppression) at threshold t, on the
+ * cell's S buffer (zero outside the detection band [3, rows-3) x [3, cols-3)). */
+__device__ __forceinline__ bool fast_survivor(const uint8_t* s, int P, int t) {
+    const int c = s[0];
+    if (c <= t) return false;
+    const int sc = c - 1;
+    int n;
+#define NB(off) n = s[off]; if (n > t && n - 1 >= sc) return false;
+    NB(-P - 1) NB(-P) NB(-P + 1) NB(-1) NB(1) NB(P - 1) NB(P) NB(P + 1)
+#undef NB
+    return sc > 0;
+}
+
+/* One wave per FAST cell (4 cells per 256-thread workgroup). ROI staged in LDS; band
+ * pixels are visited in row-major order in 64-lane chunks so ballot+mbcnt reproduce the
+ * reference's emission order (ORBextractor.cc:820-825). */
+__global__ __launch_bounds__(256) void k_fast_cells(
+    const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
+    ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
+    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt) {
+    __shared__ uint8_t s_roi[4][kRoiMax * kRoiPitch];
+    __shared__ uint8_t s_str[4][kRoiMax * kRoiPitch];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int ci = blockIdx.x * 4 + wave;
+    if (ci >= ep.ncells) return;  // wave-uniform; no block barriers below
+    const CellDesc c = cells[ci];
+    const LevelDesc& lv = levels[c.level];
+    const uint8_t* img = c.level == 0 ? frames + (long long)f * fstride
+                                      : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
+    const int pitch = c.level == 0 ? pitch0 : lv.pitch;
+    uint8_t* roi = s_roi[wave];
+    uint8_t* str = s_str[wave];
+    const int P = kRoiPitch;
+    // stage ROI (rows of c.w bytes) and clear the strength buffer
+    for (int idx = lane; idx < c.w * c.h; idx += 64) {
+        const int r = idx / c.w, col = idx - r * c.w;
+        roi[r * P + col] = img[(long long)(c.y0 + r) * pitch + c.x0 + col];
+    }
+    for (int idx = lane; idx < (kRoiMax * kRoiPitch) / 4; idx += 64) ((uint32_t*)str)[idx] = 0u;
+    wave_sync();
+    const int bw = c.w - 6, bh = c.h - 6;
+    int total = 0;
+    if (bw > 0 && bh > 0) {
+        const int rpi = 64 / bw;  // band rows per 64-lane chunk
+        const int lr = lane / bw, lc = lane - lr * bw;
+        const bool lane_ok = lane < rpi * bw;
+        for (int r0 = 0; r0 < bh; r0 += rpi) {
+            const int rr = r0 + lr;
+            if (lane_ok && rr < bh) {
+                const int o = (rr + 3) * P + lc + 3;
+                str[o] = (uint8_t)fast_strength(roi + o, P);
+            }
+        }
+        wave_sync();
+        // pass 1: survivors at iniThFAST; if none, the cell falls back to minThFAST
+        int t = ep.ini_th;
+        int cnt = 0;
+        for (int r0 = 0; r0 < bh; r0 += rpi) {
+            const int rr = r0 + lr;
+            bool keep = false;
+            if (lane_ok && rr < bh) keep = fast_survivor(str + (rr + 3) * P + lc + 3, P, t);
+            cnt += __popcll(__ballot(keep));
+        }
+        if (cnt == 0) t = ep.min_th;
+        // pass 2: emit in row-major order
+        uint32_t* out = cellkey + (long long)f * ep.keys_per_frame + c.slot;
+        for (int r0 = 0; r0 < bh; r0 += rpi) {
+            const int rr = r0 + lr;
+            bool keep = false;
+            int sc = 0;
+            if (lane_ok && rr < bh) {
+                const int o = (rr + 3) * P + lc + 3;
+                keep = fast_survivor(str + o, P, t);
+                sc = str[o] - 1;
+            }
+            const unsigned long long m = __ballot(keep);
+            if (keep) {
+                const int pos = total + lane_prefix(m);
+                const uint32_t xr = (uint32_t)(lc + 3 + c.xoff), yr = (uint32_t)(rr + 3 + c.yoff);
+                if (pos < c.cap) out[pos] = xr | (yr << 12) | ((uint32_t)sc << 24);
+            }
+            total += __popcll(m);
+        }
+        if (total > c.cap) total = c.cap;  // cannot happen: cap >= max NMS survivors
+    }
+    if (lane == 0) cellcnt[(long long)f * ep.ncells + ci] = total;
+}
+
+/* ----------------------------------------------------------------------------------- */
+/* DistributeOctTree, one 256-thread workgroup per (frame, level).                       */
+/*                                                                                       */
+/* Re-formulation (proved equivalent in DESIGN.md): keys never move; each key carries   */
+/* the index of its live node. The std::list order is kept as the node table's order:   */
+/* children of a round are pushed to the front (reverse creation order) ahead of the    */
+/* surviving nodes. Phase 1 divides every node with >1 key in list order; phase 2        */
+/* divides them by (size desc, creation desc) and stops at the first division that      */
+/* reaches N (ORBextractor.cc:676-737; pointer tie-break pinned to creation order).      */
+/* ----------------------------------------------------------------------------------- */
+struct OctScratch {
+    uint32_t* key;     // [n]   x_rel | y_rel<<12 | r<<24
+    uint16_t* label;   // [n]   live node index
+    uint8_t* quad;     // [n]
+};
+
+__device__ int block_scan_excl(int v, int* total, int* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) red[w] = inc;
+    __syncthreads();
+    int woff = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int s = red[i];
+        woff += (i < w) ? s : 0;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return woff + inc - v;
+}
+
+__device__ __forceinline__ int block_sum(int v, int* red) {
+    int tot;
+    block_scan_excl(v, &tot, red);
+    return tot;
+}
+
+/* LDS layout (bytes), NC = node capacity (pow2-rounded for the sort):
+ *   nodes A/B : 2 x NC x {int x0,y0,x1,y1,nk; uint seq}   = 48 NC
+ *   cnt4      : NC x 4 int                                 = 16 NC
+ *   cpos      : NC x 4 u16                                 =  8 NC
+ *   spos, dflag, dbase : 3 x NC int                        = 12 NC
+ *   sortkey   : NC x u64                                   =  8 NC
+ *   keys      : KL x (4 + 2 + 1) (if n <= KL, else global scratch)
+ */
+struct NodeT {
+    int* x0; int* y0; int* x1; int* y1; int* nk; uint32_t* seq;
+};
+
+__global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDesc* __restrict__ levels,
+                                                const CellDesc* __restrict__ cells,
+                                                const uint32_t* __restrict__ cellkey,
+                                                const int* __restrict__ cellcnt, uint32_t* __restrict__ lvkey,
+                                                int* __restrict__ lvcnt, uint8_t* __restrict__ gscratch,
+                                                long long gscratch_frame_bytes, int NC, int KL,
+                                                int* __restrict__ err) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    __shared__ int red[8];
+    __shared__ int sh_n, sh_size, sh_jstar, sh_tc, sh_nexp, sh_ndiv;
+    const int tid = threadIdx.x;
+    const int l = blockIdx.x, f = blockIdx.y;
+    const LevelDesc lv = levels[l];
+    // --- carve LDS
+    uint8_t* p = lds;
+    NodeT A, Bt;
+    A.x0 = (int*)p; p += 4 * NC; A.y0 = (int*)p; p += 4 * NC; A.x1 = (int*)p; p += 4 * NC;
+    A.y1 = (int*)p; p += 4 * NC; A.nk = (int*)p; p += 4 * NC; A.seq = (uint32_t*)p; p += 4 * NC;
+    Bt.x0 = (int*)p; p += 4 * NC; Bt.y0 = (int*)p; p += 4 * NC; Bt.x1 = (int*)p; p += 4 * NC;
+    Bt.y1 = (int*)p; p += 4 * NC; Bt.nk = (int*)p; p += 4 * NC; Bt.seq = (uint32_t*)p; p += 4 * NC;
+    int* cnt4 = (int*)p; p += 16 * NC;
+    int* spos = (int*)p; p += 4 * NC;
+    int* dflag = (int*)p; p += 4 * NC;
+    int* dbase = (int*)p; p += 4 * NC;
+    unsigned long long* skey = (unsigned long long*)p; p += 8 * NC;
+    uint16_t* cpos = (uint16_t*)p; p += 8 * NC;
+    uint8_t* kbase = p;
+
+    // --- 1. gather this level's candidates (cell order = ORBextractor.cc:789-829 order)
+    const int* ccnt = cellcnt + (long long)f * ep.ncells + lv.cell_begin;
+    const uint32_t* ckey = cellkey + (long long)f * ep.keys_per_frame;
+    int carry = 0;
+    // cell offsets -> reuse dbase/spos as temp (ncells may exceed NC: chunked)
+    if (tid == 0) sh_n = 0;
+    __syncthreads();
+    int n = 0;
+    for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
+        const int c = c0 + tid;
+        const int v = c < lv.ncells ? ccnt[c] : 0;
+        int tot;
+        const int off = block_scan_excl(v, &tot, red) + carry;
+        carry += tot;
+        (void)off;
+    }
+    n = carry;
+    OctScratch K;
+    if (n <= KL) {
+        K.key = (uint32_t*)kbase;
+        K.label = (uint16_t*)(kbase + 4 * KL);
+        K.quad = kbase + 6 * KL;
+    } else {
+        uint8_t* g = gscratch + (long long)f * gscratch_frame_bytes + (long long)lv.key_begin * 8;
+        K.key = (uint32_t*)g;
+        K.label = (uint16_t*)(g + 4ll * lv.key_cap);
+        K.quad = g + 6ll * lv.key_cap;
+    }
+    carry = 0;
+    for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
+        const int c = c0 + tid;
+        const int v = c < lv.ncells ? ccnt[c] : 0;
+        int tot;
+        const int off = block_scan_excl(v, &tot, red) + carry;
+        if (c < lv.ncells) {
+            const uint32_t* src = ckey + cells[lv.cell_begin + c].slot;
+            for (int k = 0; k < v; k++) K.key[off + k] = src[k];
+        }
+        carry += tot;
+    }
+    __syncthreads();
+    uint32_t* outk = lvkey + (long long)f * ep.kp_per_frame + lv.kp_off;
+    if (n == 0) {
+        if (tid == 0) lvcnt[f * ep.L + l] = 0;
+        return;
+    }
+    // --- 2. roots (ORBextractor.cc:542-585)
+    const int nIni = lv.nIni;
+    for (int s = tid; s < nIni; s += 256) cnt4[s] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+        const float x = (float)(K.key[i] & 0xFFF);
+        int r = (int)__fdiv_rn(x, lv.hX);
+        if (r >= nIni) { atomicOr(err, 1); r = nIni - 1; }
+        K.label[i] = (uint16_t)r;
+        atomicAdd(&cnt4[r], 1);
+    }
+    __syncthreads();
+    int size = 0;
+    {
+        int carry2 = 0;
+        for (int r0 = 0; r0 < nIni; r0 += 256) {
+            const int r = r0 + tid;
+            const int nonempty = (r < nIni && cnt4[r] > 0) ? 1 : 0;
+            int tot;
+            const int pos = block_scan_excl(nonempty, &tot, red) + carry2;
+            if (nonempty) {
+                spos[r] = pos;
+                A.x0[pos] = (int)__fmul_rn(lv.hX, (float)r);
+                A.x1[pos] = (int)__fmul_rn(lv.hX, (float)(r + 1));
+                A.y0[pos] = 0;
+                A.y1[pos] = lv.maxY - lv.minY;
+                A.nk[pos] = cnt4[r];
+                A.seq[pos] = (uint32_t)r;
+            }
+            carry2 += tot;
+        }
+        size = carry2;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) K.label[i] = (uint16_t)spos[K.label[i]];
+    if (size > NC) { if (tid == 0) atomicOr(err, 2); return; }
+    __syncthreads();
+    uint32_t next_seq = (uint32_t)nIni;
+    int phase = 1;
+    const int N = lv.N;
+    // --- 3. division rounds (ORBextractor.cc:594-739)
+    for (int iter = 0; iter < 100000; iter++) {
+        const int prevSize = size;
+        for (int s = tid; s < size; s += 256) {
+            cnt4[4 * s] = 0; cnt4[4 * s + 1] = 0; cnt4[4 * s + 2] = 0; cnt4[4 * s + 3] = 0;
+        }
+        __syncthreads();
+        for (int i = tid; i < n; i += 256) {
+            const int s = K.label[i];
+            if (A.nk[s] >= 2) {
+                const uint32_t kk = K.key[i];
+                const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF);
+                const int hx = (A.x1[s] - A.x0[s] + 1) >> 1, hy = (A.y1[s] - A.y0[s] + 1) >> 1;
+                const int q = (x >= A.x0[s] + hx ? 1 : 0) + (y >= A.y0[s] + hy ? 2 : 0);
+                K.quad[i] = (uint8_t)q;
+                atomicAdd(&cnt4[4 * s + q], 1);
+            }
+        }
+        __syncthreads();
+        // D = nodes with >1 key; processing order: list order (phase 1) or sorted (phase 2)
+        int nD;
+        {
+            int carry3 = 0;
+            for (int s0 = 0; s0 < size; s0 += 256) {
+                const int s = s0 + tid;
+                const int isD = (s < size && A.nk[s] >= 2) ? 1 : 0;
+                int tot;
+                const int pos = block_scan_excl(isD, &tot, red) + carry3;
+                if (isD) {
+                    dflag[pos] = s;  // D array (slot ids) in list order
+                    skey[pos] = ((unsigned long long)(uint32_t)A.nk[s] << 32) | A.seq[s];
+                }
+                carry3 += tot;
+            }
+            nD = carry3;
+        }
+        __syncthreads();
+        if (nD == 0) break;  // cannot happen while size changes, kept for safety
+        if (phase == 2) {
+            // bitonic sort of skey[0..P) descending; pad with 0
+            int P2 = 1;
+            while (P2 < nD) P2 <<= 1;
+            for (int i = nD + tid; i < P2; i += 256) skey[i] = 0ull;
+            __syncthreads();
+            for (int k = 2; k <= P2; k <<= 1) {
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    for (int i = tid; i < P2; i += 256) {
+                        const int ixj = i ^ j;
+                        if (ixj > i) {
+                            const unsigned long long a = skey[i], b = skey[ixj];
+                            const bool desc = (i & k) == 0;
+                            if (desc ? (a < b) : (a > b)) { skey[i] = b; skey[ixj] = a; }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            // map sorted keys back to slots: seq is unique -> search by seq
+            for (int j = tid; j < nD; j += 256) dbase[j] = 0;
+            __syncthreads();
+            for (int s = tid; s < size; s += 256) spos[s] = -1;
+            __syncthreads();
+            // slot lookup: for each D slot (in dflag), find its rank via binary search over skey
+            for (int j = tid; j < nD; j += 256) {
+                const int s = dflag[j];
+                const unsigned long long key = ((unsigned long long)(uint32_t)A.nk[s] << 32) | A.seq[s];
+                int lo = 0, hi = nD - 1;
+                while (lo < hi) {  // descending array: find index of key
+                    const int mid = (lo + hi) >> 1;
+                    if (skey[mid] > key) lo = mid + 1; else hi = mid;
+                }
+                spos[s] = lo;  // processing rank of slot s
+            }
+            __syncthreads();
+            for (int s = tid; s < size; s += 256)
+                if (spos[s] >= 0) dflag[spos[s]] = s;
+            __syncthreads();
+        }
+        // children counts per processing position; prefix -> creation indices
+        int TC = 0, jstar = nD - 1;
+        {
+            int carry4 = 0, carryG = 0;
+            if (tid == 0) sh_jstar = nD - 1;
+            __syncthreads();
+            for (int j0 = 0; j0 < nD; j0 += 256) {
+                const int j = j0 + tid;
+                int nc = 0;
+                if (j < nD) {
+                    const int s = dflag[j];
+                    nc = (cnt4[4 * s] > 0) + (cnt4[4 * s + 1] > 0) + (cnt4[4 * s + 2] > 0) + (cnt4[4 * s + 3] > 0);
+                }
+                int tot;
+                const int excl = block_scan_excl(nc, &tot, red) + carry4;
+                int tot2;
+                const int excl2 = block_scan_excl(nc - 1, &tot2, red) + carryG;
+                if (j < nD) {
+                    dbase[j] = excl;
+                    if (phase == 2) {
+                        const int after = prevSize + excl2 + (nc - 1);
+                        const int before = prevSize + excl2;
+                        if (after >= N && before < N) sh_jstar = j;  // first crossing (unique)
+                    }
+                }
+                carry4 += tot;
+                carryG += tot2;
+            }
+            __syncthreads();
+            jstar = sh_jstar;
+            TC = (jstar == nD - 1) ? carry4 : dbase[jstar + 1];
+        }
+        const int ndiv = jstar + 1;
+        // survivors = live slots not divided, in list order
+        for (int s = tid; s < size; s += 256) spos[s] = 0;
+        __syncthreads();
+        for (int j = tid; j < ndiv; j += 256) spos[dflag[j]] = -1;  // mark divided
+        __syncthreads();
+        int nsurv;
+        {
+            int carry5 = 0;
+            for (int s0 = 0; s0 < size; s0 += 256) {
+                const int s = s0 + tid;
+                const int sv = (s < size && spos[s] == 0) ? 1 : 0;
+                int tot;
+                const int pos = block_scan_excl(sv, &tot, red) + carry5;
+                __syncthreads();
+                if (s < size) spos[s] = sv ? (TC + pos) : -1;
+                carry5 += tot;
+            }
+            nsurv = carry5;
+        }
+        __syncthreads();
+        const int newSize = TC + nsurv;
+        if (newSize > NC) { if (tid == 0) atomicOr(err, 4); return; }
+        // write new table: survivors copy, children created
+        for (int s = tid; s < size; s += 256) {
+            const int np = spos[s];
+            if (np >= 0) {
+                Bt.x0[np] = A.x0[s]; Bt.y0[np] = A.y0[s]; Bt.x1[np] = A.x1[s]; Bt.y1[np] = A.y1[s];
+                Bt.nk[np] = A.nk[s]; Bt.seq[np] = A.seq[s];
+            }
+        }
+        int nexp_local = 0;
+        for (int j = tid; j < ndiv; j += 256) {
+            const int s = dflag[j];
+            const int x0 = A.x0[s], y0 = A.y0[s], x1 = A.x1[s], y1 = A.y1[s];
+            const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;
+            int ci = dbase[j];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int cn = cnt4[4 * s + q];
+                if (cn > 0) {
+                    const int np = TC - 1 - ci;
+                    const int cx0 = (q & 1) ? x0 + hx : x0, cx1 = (q & 1) ? x1 : x0 + hx;
+                    const int cy0 = (q & 2) ? y0 + hy : y0, cy1 = (q & 2) ? y1 : y0 + hy;
+                    Bt.x0[np] = cx0; Bt.y0[np] = cy0; Bt.x1[np] = cx1; Bt.y1[np] = cy1;
+                    Bt.nk[np] = cn; Bt.seq[np] = next_seq + (uint32_t)ci;
+                    cpos[4 * s + q] = (uint16_t)np;
+                    nexp_local += cn > 1;
+                    ci++;
+                }
+            }
+        }
+        const int nToExpand = block_sum(nexp_local, red);
+        // relabel keys
+        for (int i = tid; i < n; i += 256) {
+            const int s = K.label[i];
+            const int np = spos[s];
+            K.label[i] = (uint16_t)(np >= 0 ? np : cpos[4 * s + K.quad[i]]);
+        }
+        __syncthreads();
+        // swap tables
+        { NodeT t = A; A = Bt; Bt = t; }
+        next_seq += (uint32_t)TC;
+        size = newSize;
+        if (size >= N || size == prevSize) break;
+        if (phase == 1 && size + nToExpand * 3 > N) phase = 2;
+    }
+    // --- 4. keep the best key of each node (first max response, ORBextractor.cc:741-760)
+    uint32_t* best = (uint32_t*)cnt4;
+    for (int s = tid; s < size; s += 256) best[s] = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+        const uint32_t kk = K.key[i];
+        atomicMax(&best[K.label[i]], (kk & 0xFF000000u) | (0xFFFFFFu - (uint32_t)i));
+    }
+    __syncthreads();
+    if (size > lv.kp_cap) { if (tid == 0) atomicOr(err, 8); size = lv.kp_cap; }
+    for (int s = tid; s < size; s += 256) {
+        const int i = (int)(0xFFFFFFu - (best[s] & 0xFFFFFFu));
+        const uint32_t kk = K.key[i];
+        const uint32_t x = (kk & 0xFFF) + (uint32_t)lv.minX, y = ((kk >> 12) & 0xFFF) + (uint32_t)lv.minY;
+        outk[s] = x | (y << 12) | (kk & 0xFF000000u);
+    }
+    if (tid == 0) lvcnt[f * ep.L + l] = size;
+}
+
+/* ----------------------------------------------------------------------------------- */
+/* GaussianBlur 7x7, sigma 2, REFLECT_101, 8U fixed point (kernel 18,34,49,55,...; sum  */
+/* 257). 64x16 output tile per workgroup, tiles of all levels of all frames in one grid. */
+/* ----------------------------------------------------------------------------------- */
+__device__ __forceinline__ int reflect101(int p, int n) {
+    p = p < 0 ? -p : p;
+    p = p >= n ? 2 * n - 2 - p : p;
+    return p;
+}
+
+__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
+                                              const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                              ExtractParams ep, const LevelDesc* __restrict__ levels,
+                                              const int* __restrict__ tile_begin /* L+1 */,
+                                              const int* __restrict__ lvcnt) {
+    __shared__ uint8_t s_in[22][72];
+    __shared__ int s_row[22][64];
+    const int f = blockIdx.y;
+    int t = blockIdx.x, l = 0;
+    while (l + 1 < ep.L && t >= tile_begin[l + 1]) l++;
+    if (lvcnt[f * ep.L + l] == 0) return;  // level without keypoints is never blurred (:1081)
+    t -= tile_begin[l];
+    const LevelDesc& lv = levels[l];
+    const int tilesx = (lv.w + 63) / 64;
+    const int tx = t % tilesx, ty = t / tilesx;
+    const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
+    const int pitch = l == 0 ? pitch0 : lv.pitch;
+    const int gx0 = tx * 64 - 3, gy0 = ty * 16 - 3;
+    for (int idx = threadIdx.x; idx < 22 * 70; idx += 256) {
+        const int r = idx / 70, c = idx - r * 70;
+        const int gy = reflect101(gy0 + r, lv.h), gx = reflect101(gx0 + c, lv.w);
+        s_in[r][c] = img[(long long)gy * pitch + gx];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 22 * 64; idx += 256) {
+        const int r = idx >> 6, c = idx & 63;
+        const uint8_t* s = &s_in[r][c];
+        s_row[r][c] = 18 * (s[0] + s[6]) + 34 * (s[1] + s[5]) + 49 * (s[2] + s[4]) + 55 * s[3];
+    }
+    __syncthreads();
+    const int c = threadIdx.x & 63, rb = (threadIdx.x >> 6) * 4;
+    const int gx = tx * 64 + c;
+    uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int r = rb + k;
+        const int gy = ty * 16 + r;
+        if (gx < lv.w && gy < lv.h) {
+            const int s = 55 * s_row[r + 3][c] + 49 * (s_row[r + 2][c] + s_row[r + 4][c]) +
+                          34 * (s_row[r + 1][c] + s_row[r + 5][c]) + 18 * (s_row[r][c] + s_row[r + 6][c]);
+            int v;
+            if (gx < lv.blur_vec_end)  // SSE2 float path == round half to even (exact)
+                v = (s + 0x7FFF + ((s >> 16) & 1)) >> 16;
+            else  // scalar FixedPtCastEx tail
+                v = (s + (1 << 15)) >> 16;
+            out[(long long)gy * lv.pitch + gx] = (uint8_t)(v > 255 ? 255 : v);
+        }
+    }
+}
+
+/* ----------------------------------------------------------------------------------- */
+/* IC_Angle + rBRIEF + output, one wave per octree output slot.                          */
+/* ----------------------------------------------------------------------------------- */
+__global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
+                                                  const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                                                  ExtractParams ep, const LevelDesc* __restrict__ levels,
+                                                  const uint32_t* __restrict__ lvkey, const int* __restrict__ lvcnt,
+                                                  orbx_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
+                                                  int* __restrict__ out_counts, int kp_stride) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = blockIdx.x * 4 + wave, f = blockIdx.y;
+    if (g >= ep.kp_per_frame) return;
+    const int* cnt = lvcnt + f * ep.L;
+    if (g == 0 && lane == 0) {
+        int tot = 0;
+        for (int l = 0; l < ep.L; l++) tot += cnt[l];
+        out_counts[f] = tot;
+    }
+    int l = 0;
+    while (l + 1 < ep.L && g >= levels[l + 1].kp_off) l++;
+    const LevelDesc& lv = levels[l];
+    const int k = g - lv.kp_off;
+    if (k >= cnt[l]) return;
+    int outidx = k;
+    for (int q = 0; q < l; q++) outidx += cnt[q];
+    const uint32_t kk = lvkey[(long long)f * ep.kp_per_frame + g];
+    const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF), resp = (int)(kk >> 24);
+    const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
+    const int pitch = l == 0 ? pitch0 : lv.pitch;
+    // IC_Angle (ORBextractor.cc:77-104): lanes = columns u, two half-waves split the rows
+    int m10 = 0, m01 = 0;
+    {
+        const int u = (lane & 31) - 15;
+        const int vbeg = (lane < 32) ? -15 : 1, vend = (lane < 32) ? 0 : 15;
+        if ((lane & 31) < 31) {
+            const uint8_t* col = img + (long long)y * pitch + x + u;
+            const int au = u < 0 ? -u : u;
+            for (int v = vbeg; v <= vend; v++) {
+                const int av = v < 0 ? -v : v;
+                if (au <= ep.umax[av]) {
+                    const int I = col[(long long)v * pitch];
+                    m10 += u * I;
+                    m01 += v * I;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            m10 += __shfl_xor(m10, o, 64);
+            m01 += __shfl_xor(m01, o, 64);
+        }
+    }
+    const float angle = fast_atan2((float)m01, (float)m10);
+    // computeOrbDescriptor (ORBextractor.cc:107-147)
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float theta = __fmul_rn(angle, factorPI);
+    float sa, ca;
+    glibc_sincosf(theta, &sa, &ca);
+    const float a = ca, b = sa;
+    const uint8_t* bl = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
+    const uint8_t* center = bl + (long long)y * lv.pitch + x;
+    const signed char* pat = (const signed char*)orbx_pattern_soa_u8;
+    unsigned long long words[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int t = 64 * w + lane;
+        const float px0 = (float)pat[t], py0 = (float)pat[256 + t];
+        const float px1 = (float)pat[512 + t], py1 = (float)pat[768 + t];
+        const int r0 = cv_round(__fadd_rn(__fmul_rn(px0, b), __fmul_rn(py0, a)));
+        const int c0 = cv_round(__fsub_rn(__fmul_rn(px0, a), __fmul_rn(py0, b)));
+        const int r1 = cv_round(__fadd_rn(__fmul_rn(px1, b), __fmul_rn(py1, a)));
+        const int c1 = cv_round(__fsub_rn(__fmul_rn(px1, a), __fmul_rn(py1, b)));
+        const int t0 = center[r0 * lv.pitch + c0];
+        const int t1 = center[r1 * lv.pitch + c1];
+        words[w] = __ballot(t0 < t1);
+    }
+    const long long o = (long long)f * kp_stride + outidx;
+    if (lane == 0) {
+        unsigned long long* d = (unsigned long long*)(out_desc + o * 32);
+        d[0] = words[0]; d[1] = words[1]; d[2] = words[2]; d[3] = words[3];
+        orbx_kp kp;
+        const float fx = (float)x, fy = (float)y;
+        kp.x = l ? __fmul_rn(fx, lv.scale) : fx;
+        kp.y = l ? __fmul_rn(fy, lv.scale) : fy;
+        kp.size = lv.patch_size;
+        kp.angle = angle;
+        kp.response = (float)resp;
+        kp.octave = l;
+        out_kps[o] = kp;
+    }
+}
+
+}  // namespace orbamd
+
+/* ----------------------------------------------------------------------------------- */
+/* host-side launchers (called from capi.cpp)                                           */
+/* ----------------------------------------------------------------------------------- */
+#include "launch.h"
+
+namespace orbamd {
+
+hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
+                         long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
+                         int simd_end, int nframes, hipStream_t st) {
+    const int* xofs = coef;
+    const short2* alpha = (const short2*)(coef + dw);
+    const int* yofs = coef + 2 * dw;
+    const short2* beta = (const short2*)(coef + 2 * dw + dh);
+    dim3 grid((dw + 63) / 64, (dh + 3) / 4, nframes);
+    hipLaunchKernelGGL(k_resize_level, grid, dim3(256), 0, st, src, src_fstride, src_pitch, sw, sh, dst,
+                       dst_fstride, dst_pitch, dw, dh, xofs, alpha, yofs, beta, xmax, simd_end);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                             const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
+                             uint32_t* cellkey, int* cellcnt, int nframes, hipStream_t st) {
+    dim3 grid((ep.ncells + 3) / 4, nframes);
+    hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, ep, levels, cells,
+                       cellkey, cellcnt);
+    return hipGetLastError();
+}
+
+hipError_t octree_setup(int lds_bytes) {
+    return hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+}
+
+hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
+                         const uint32_t* cellkey, const int* cellcnt, uint32_t* lvkey, int* lvcnt,
+                         uint8_t* gscratch, long long gscratch_frame_bytes, int NC, int KL, int lds_bytes,
+                         int* err, int nframes, hipStream_t st) {
+    dim3 grid(ep.L, nframes);
+    hipLaunchKernelGGL(k_octree, grid, dim3(256), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey, lvcnt,
+                       gscratch, gscratch_frame_bytes, NC, KL, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
+                       const ExtractParams& ep, const LevelDesc* levels, const int* tile_begin, int ntiles,
+                       const int* lvcnt, int nframes, hipStream_t st) {
+    dim3 grid(ntiles, nframes);
+    hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, tile_begin,
+                       lvcnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                           const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
+                           const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,
+                           int* out_counts, int kp_stride, int nframes, hipStream_t st) {
+    dim3 grid((ep.kp_per_frame + 3) / 4, nframes);
+    hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, lvkey,
+                       lvcnt, out_kps, out_desc, out_counts, kp_stride);
+    return hipGetLastError();
+}
+
+}  // namespace orbamd

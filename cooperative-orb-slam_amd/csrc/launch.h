@@ -1,0 +1,49 @@
+/* launch.h -- host launchers of the gfx950 kernels (defined next to the kernels). */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbslam_amd.h"
+#include "orb_device.h"
+#include "orb_match.h"
+
+namespace orbamd {
+
+hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
+                         long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
+                         int simd_end, int nframes, hipStream_t st);
+hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                             const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
+                             uint32_t* cellkey, int* cellcnt, int nframes, hipStream_t st);
+hipError_t octree_setup(int lds_bytes);
+hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
+                         const uint32_t* cellkey, const int* cellcnt, uint32_t* lvkey, int* lvcnt,
+                         uint8_t* gscratch, long long gscratch_frame_bytes, int NC, int KL, int lds_bytes,
+                         int* err, int nframes, hipStream_t st);
+hipError_t launch_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
+                       const ExtractParams& ep, const LevelDesc* levels, const int* tile_begin, int ntiles,
+                       const int* lvcnt, int nframes, hipStream_t st);
+hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                           const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
+                           const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,
+                           int* out_counts, int kp_stride, int nframes, hipStream_t st);
+
+hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
+                         const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
+                         int32_t* nmatches, hipStream_t st);
+hipError_t launch_rot_filter_pairs(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps,
+                                   const int32_t* counts, int kp_stride, int32_t* match12, int32_t* nmatches,
+                                   hipStream_t st);
+hipError_t launch_tri_bf_packed(const orbx_kp* kps1, const uint8_t* desc1, const int32_t* count1, int nref,
+                                const uint8_t* slots, long long slot_bytes, int slot_cap, const MatchGeom& g,
+                                int32_t* match, int cap1, int32_t* nmatches, hipStream_t st);
+hipError_t launch_pack_slot(const orbx_kp* kps, const uint8_t* desc, const int32_t* count, int cap, uint8_t* slot,
+                            hipStream_t st);
+hipError_t launch_tri_nodes(const DevView& v1, const DevView& v2, const NodeTask* tasks, int ntasks,
+                            const MatchGeom& g, int only_stereo, int32_t* match12, hipStream_t st);
+hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* tasks, int ntasks, int max_nc,
+                      float nnratio, int mode, int32_t* out, hipStream_t st);
+hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* angB, int swap, int32_t* nout,
+                             hipStream_t st);
+
+}  // namespace orbamd

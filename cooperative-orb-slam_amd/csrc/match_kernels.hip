@@ -1,0 +1,428 @@
+/*
+ * match_kernels.hip -- gfx950 kernels for ORBmatcher (ORBmatcher.cc).
+ *
+ *   k_tri_bf          SearchForTriangulation, one FeatureVector node holding every feature
+ *                     (BASELINE "BF"), batch of frame pairs; lane = query idx1, candidate
+ *                     KF2 tile staged in LDS, descriptors compared as 8 x u32 XOR+popcount
+ *                     (v_bcnt_u32_b32) -- ORBmatcher.cc:657-823, 1647-1663.
+ *   k_tri_nodes       SearchForTriangulation over common BoW nodes (general form).
+ *   k_bow             SearchByBoW(KF,F) / SearchByBoW(KF,KF): per common node, greedy over the
+ *                     node's queries in order, wave-parallel best/second-best over candidates
+ *                     (ORBmatcher.cc:159-288, 522-655).
+ *   k_rot_filter      rotation-histogram consistency + ComputeThreeMaxima
+ *                     (ORBmatcher.cc:236-246, 267-285, 1601-1642).
+ * Candidate order / tie rules are the reference's (DESIGN.md "Matcher semantics").
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbslam_amd.h"
+#include "orb_match.h"
+
+namespace orbamd {
+
+__device__ __forceinline__ int hamming8(const uint32_t* a, const uint32_t* b) {
+    int d = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) d += __popc(a[k] ^ b[k]);
+    return d;
+}
+
+/* CheckDistEpipolarLine (ORBmatcher.cc:140-157) with the line (a,b,c) of kp1 precomputed
+ * (same float ops); compare in double like `dsqr < 3.84*sigma2`. */
+__device__ __forceinline__ bool epi_ok(float a, float b, float c, float x2, float y2, double th384) {
+    const float num = __fadd_rn(__fadd_rn(__fmul_rn(a, x2), __fmul_rn(b, y2)), c);
+    const float den = __fadd_rn(__fmul_rn(a, a), __fmul_rn(b, b));
+    if (den == 0.f) return false;
+    const float dsqr = __fdiv_rn(__fmul_rn(num, num), den);
+    return (double)dsqr < th384;
+}
+
+__device__ __forceinline__ void epi_line(const MatchGeom& g, float x1, float y1, float* a, float* b, float* c) {
+    *a = __fadd_rn(__fadd_rn(__fmul_rn(x1, g.F[0]), __fmul_rn(y1, g.F[3])), g.F[6]);
+    *b = __fadd_rn(__fadd_rn(__fmul_rn(x1, g.F[1]), __fmul_rn(y1, g.F[4])), g.F[7]);
+    *c = __fadd_rn(__fadd_rn(__fmul_rn(x1, g.F[2]), __fmul_rn(y1, g.F[5])), g.F[8]);
+}
+
+/* epipole-radius rejection for mono-mono pairs (ORBmatcher.cc:743-749) */
+__device__ __forceinline__ bool near_epipole(const MatchGeom& g, float x2, float y2, int oct2) {
+    const float dx = __fsub_rn(g.ex, x2), dy = __fsub_rn(g.ey, y2);
+    return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < g.th100[oct2];
+}
+
+constexpr int kTile = 512;
+
+/* Pair p: KF1 = (kps1, desc1, n1), KF2 = (kps2, desc2, n2) resolved by the caller-side
+ * accessor; every keypoint mono, no MapPoints (BF bench configuration). */
+struct PairSrc {
+    const orbx_kp* kps1; const uint8_t* desc1; int n1;
+    const orbx_kp* kps2; const uint8_t* desc2; int n2;
+};
+
+__device__ __forceinline__ void tri_bf_body(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
+                                            int32_t* __restrict__ nmatch) {
+    __shared__ uint4 s_desc[kTile * 2];
+    __shared__ float s_x[kTile], s_y[kTile];
+    __shared__ int s_oct[kTile];
+    const int tid = threadIdx.x;
+    const int idx1 = blockIdx.x * 256 + tid;
+    if ((int)(blockIdx.x * 256) >= s.n1) return;  // block-uniform
+    const bool active = idx1 < s.n1;
+    uint32_t q[8];
+    float a = 0.f, b = 0.f, c = 0.f;
+    if (active) {
+        const uint4* qd = (const uint4*)(s.desc1 + (long long)idx1 * 32);
+        const uint4 q0 = qd[0], q1 = qd[1];
+        q[0] = q0.x; q[1] = q0.y; q[2] = q0.z; q[3] = q0.w;
+        q[4] = q1.x; q[5] = q1.y; q[6] = q1.z; q[7] = q1.w;
+        epi_line(g, s.kps1[idx1].x, s.kps1[idx1].y, &a, &b, &c);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) q[k] = 0;
+    }
+    int bestDist = 50, bestIdx2 = -1;  // TH_LOW (ORBmatcher.cc:715)
+    for (int t0 = 0; t0 < s.n2; t0 += kTile) {
+        const int nt = min(kTile, s.n2 - t0);
+        __syncthreads();
+        for (int j = tid; j < nt; j += 256) {
+            const uint4* cd = (const uint4*)(s.desc2 + (long long)(t0 + j) * 32);
+            s_desc[2 * j] = cd[0];
+            s_desc[2 * j + 1] = cd[1];
+            const orbx_kp kp = s.kps2[t0 + j];
+            s_x[j] = kp.x; s_y[j] = kp.y; s_oct[j] = kp.octave;
+        }
+        __syncthreads();
+        if (active) {
+            for (int j = 0; j < nt; j++) {
+                const uint4 c0 = s_desc[2 * j], c1 = s_desc[2 * j + 1];
+                const int dist = __popc(q[0] ^ c0.x) + __popc(q[1] ^ c0.y) + __popc(q[2] ^ c0.z) +
+                                 __popc(q[3] ^ c0.w) + __popc(q[4] ^ c1.x) + __popc(q[5] ^ c1.y) +
+                                 __popc(q[6] ^ c1.z) + __popc(q[7] ^ c1.w);
+                if (dist > 50 || dist > bestDist) continue;
+                const float x2 = s_x[j], y2 = s_y[j];
+                const int oct2 = s_oct[j];
+                if (near_epipole(g, x2, y2, oct2)) continue;
+                if (epi_ok(a, b, c, x2, y2, g.th384[oct2])) {
+                    bestIdx2 = t0 + j;
+                    bestDist = dist;
+                }
+            }
+        }
+    }
+    if (active) {
+        out[idx1] = bestIdx2;
+        if (bestIdx2 >= 0) atomicAdd(nmatch, 1);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tri_bf(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
+                                                const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
+                                                const int32_t* __restrict__ counts, int kp_stride, MatchGeom g,
+                                                int32_t* __restrict__ match12, int32_t* __restrict__ nmatches) {
+    const int p = blockIdx.y;
+    const int f1 = q1[p], f2 = q2[p];
+    PairSrc s;
+    s.kps1 = kps + (long long)f1 * kp_stride; s.desc1 = desc + (long long)f1 * kp_stride * 32; s.n1 = counts[f1];
+    s.kps2 = kps + (long long)f2 * kp_stride; s.desc2 = desc + (long long)f2 * kp_stride * 32; s.n2 = counts[f2];
+    tri_bf_body(s, g, match12 + (long long)p * kp_stride, nmatches + p);
+}
+
+/* cross-agent: the query frame against nref packed slots (orbx_pack_keyframe_device) */
+__global__ __launch_bounds__(256) void k_tri_bf_packed(const orbx_kp* __restrict__ kps1, const uint8_t* __restrict__ desc1,
+                                                       const int32_t* __restrict__ count1, const uint8_t* __restrict__ slots,
+                                                       long long slot_bytes, int slot_cap, MatchGeom g,
+                                                       int32_t* __restrict__ match, int cap1, int32_t* __restrict__ nmatches) {
+    const int r = blockIdx.y;
+    const uint8_t* slot = slots + (long long)r * slot_bytes;
+    PairSrc s;
+    s.kps1 = kps1; s.desc1 = desc1; s.n1 = *count1;
+    s.n2 = ((const int32_t*)slot)[0];
+    const int cap2 = ((const int32_t*)slot)[1];  // written by k_pack_slot (even)
+    (void)slot_cap;
+    s.kps2 = (const orbx_kp*)(slot + 64);
+    s.desc2 = slot + 64 + (long long)cap2 * sizeof(orbx_kp);
+    tri_bf_body(s, g, match + (long long)r * cap1, nmatches + r);
+}
+
+/* pack one frame's (n, kps, desc) into an exchange slot */
+__global__ __launch_bounds__(256) void k_pack_slot(const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
+                                                   const int32_t* __restrict__ count, int cap, uint8_t* __restrict__ slot) {
+    const int n = *count;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ((int32_t*)slot)[0] = n;
+        ((int32_t*)slot)[1] = cap;
+    }
+    orbx_kp* ok = (orbx_kp*)(slot + 64);
+    uint4* od = (uint4*)(slot + 64 + (long long)cap * sizeof(orbx_kp));
+    const uint4* id = (const uint4*)desc;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        ok[i] = kps[i];
+        od[2 * i] = id[2 * i];
+        od[2 * i + 1] = id[2 * i + 1];
+    }
+}
+
+/* ----------------------------------------------------------------------------------- */
+/* General node-based SearchForTriangulation: one wave per (common node, 64 queries).   */
+/* ----------------------------------------------------------------------------------- */
+__global__ __launch_bounds__(64) void k_tri_nodes(const DevView v1, const DevView v2, const NodeTask* __restrict__ tasks,
+                                                  MatchGeom g, int only_stereo, int32_t* __restrict__ match12) {
+    const NodeTask t = tasks[blockIdx.x];
+    const int i1 = t.q_begin + threadIdx.x;
+    if (i1 >= t.q_end) return;
+    const int idx1 = v1.node_feat[i1];
+    if (v1.has_mp && v1.has_mp[idx1]) return;
+    const bool st1 = v1.uright ? v1.uright[idx1] >= 0.f : false;
+    if (only_stereo && !st1) return;
+    uint32_t q[8];
+    const uint32_t* qd = (const uint32_t*)(v1.desc + (long long)idx1 * 32);
+#pragma unroll
+    for (int k = 0; k < 8; k++) q[k] = qd[k];
+    float a, b, c;
+    epi_line(g, v1.x[idx1], v1.y[idx1], &a, &b, &c);
+    int bestDist = 50, bestIdx2 = -1;
+    for (int i2 = t.c_begin; i2 < t.c_end; i2++) {
+        const int idx2 = v2.node_feat[i2];
+        if (v2.has_mp && v2.has_mp[idx2]) continue;
+        const bool st2 = v2.uright ? v2.uright[idx2] >= 0.f : false;
+        if (only_stereo && !st2) continue;
+        const int dist = hamming8(q, (const uint32_t*)(v2.desc + (long long)idx2 * 32));
+        if (dist > 50 || dist > bestDist) continue;
+        const float x2 = v2.x[idx2], y2 = v2.y[idx2];
+        const int oct2 = v2.octave[idx2];
+        if (!st1 && !st2 && near_epipole(g, x2, y2, oct2)) continue;
+        if (epi_ok(a, b, c, x2, y2, g.th384[oct2])) {
+            bestIdx2 = idx2;
+            bestDist = dist;
+        }
+    }
+    match12[idx1] = bestIdx2;
+}
+
+/* ----------------------------------------------------------------------------------- */
+/* SearchByBoW: one wave per common node. Queries of node1 in order (greedy exclusion of */
+/* already-matched candidates is node-local); per query the wave computes best/second   */
+/* best over node2 with the sequential scan's semantics: best1 = first strict minimum,   */
+/* best2 = second smallest of the multiset.                                              */
+/* mode 0 = (KF,F): accept best1 <= TH_LOW, query needs a good MapPoint, candidates any  */
+/* mode 1 = (KF,KF): accept best1 < TH_LOW, both sides need a good MapPoint.             */
+/* out[idx of the side that is marked] as in the reference (F index / idx1).            */
+/* ----------------------------------------------------------------------------------- */
+struct Top2 { int b1, i1, b2; };
+__device__ __forceinline__ Top2 top2_merge(Top2 A, Top2 B) {
+    Top2 r;
+    const bool takeB = (B.b1 < A.b1) || (B.b1 == A.b1 && B.i1 >= 0 && (A.i1 < 0 || B.i1 < A.i1));
+    r.b1 = takeB ? B.b1 : A.b1;
+    r.i1 = takeB ? B.i1 : A.i1;
+    r.b2 = min(max(A.b1, B.b1), min(A.b2, B.b2));
+    return r;
+}
+
+__global__ __launch_bounds__(64) void k_bow(const DevView vq, const DevView vc, const NodeTask* __restrict__ tasks,
+                                            float nnratio, int mode, int32_t* __restrict__ out) {
+    extern __shared__ uint8_t matched[];  // per candidate position in the node
+    const NodeTask t = tasks[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int nc = t.c_end - t.c_begin;
+    for (int j = lane; j < nc; j += 64) matched[j] = 0;
+    __syncthreads();
+    for (int i1 = t.q_begin; i1 < t.q_end; i1++) {
+        const int idxq = vq.node_feat[i1];
+        if (!(vq.has_mp && vq.has_mp[idxq])) continue;
+        if (vq.mp_bad && vq.mp_bad[idxq]) continue;
+        const uint32_t* qd = (const uint32_t*)(vq.desc + (long long)idxq * 32);
+        uint32_t q[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) q[k] = qd[k];
+        Top2 r = {256, -1, 256};
+        for (int j = lane; j < nc; j += 64) {
+            if (matched[j]) continue;
+            const int idxc = vc.node_feat[t.c_begin + j];
+            if (mode == 1) {
+                if (!(vc.has_mp && vc.has_mp[idxc])) continue;
+                if (vc.mp_bad && vc.mp_bad[idxc]) continue;
+            }
+            const int dist = hamming8(q, (const uint32_t*)(vc.desc + (long long)idxc * 32));
+            if (dist < r.b1) { r.b2 = r.b1; r.b1 = dist; r.i1 = j; }
+            else if (dist < r.b2) { r.b2 = dist; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            Top2 o2;
+            o2.b1 = __shfl_xor(r.b1, o, 64);
+            o2.i1 = __shfl_xor(r.i1, o, 64);
+            o2.b2 = __shfl_xor(r.b2, o, 64);
+            r = top2_merge(r, o2);
+        }
+        const bool ok_th = mode == 0 ? (r.b1 <= 50) : (r.b1 < 50);
+        if (ok_th && r.i1 >= 0 && __fmul_rn(1.0f, (float)r.b1) < __fmul_rn(nnratio, (float)r.b2)) {
+            const int idxc = vc.node_feat[t.c_begin + r.i1];
+            __syncthreads();
+            if (lane == 0) {
+                matched[r.i1] = 1;
+                if (mode == 0) out[idxc] = idxq;  // vpMapPointMatches[bestIdxF] = pMP(KF idx)
+                else out[idxq] = idxc;            // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
+            }
+            __syncthreads();
+        }
+    }
+}
+
+/* Rotation consistency (ORBmatcher.cc:236-246 + 267-285): entries i with m[i] >= 0; rot =
+ * angA[a] - angB[b] where (a,b) = (i, m[i]) or, with swap, (m[i], i). One workgroup. */
+__global__ __launch_bounds__(256) void k_rot_filter(int n, int32_t* __restrict__ m, const float* __restrict__ angA,
+                                                    const float* __restrict__ angB, int swap, int32_t* __restrict__ nout) {
+    __shared__ int hist[30];
+    __shared__ int keep[3];
+    if (threadIdx.x < 30) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const float factor = 1.0f / 30;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int j = m[i];
+        if (j < 0) continue;
+        float rot = swap ? __fsub_rn(angA[j], angB[i]) : __fsub_rn(angA[i], angB[j]);
+        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+        int bin = (int)roundf(__fmul_rn(rot, factor));
+        if (bin == 30) bin = 0;
+        atomicAdd(&hist[bin], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < 30; i++) {
+            const int s = hist[i];
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if (max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
+        else if (max3 < __fmul_rn(0.1f, (float)max1)) { ind3 = -1; }
+        keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
+    }
+    __syncthreads();
+    int local = 0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int j = m[i];
+        if (j < 0) continue;
+        float rot = swap ? __fsub_rn(angA[j], angB[i]) : __fsub_rn(angA[i], angB[j]);
+        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+        int bin = (int)roundf(__fmul_rn(rot, factor));
+        if (bin == 30) bin = 0;
+        if (bin != keep[0] && bin != keep[1] && bin != keep[2]) m[i] = -1;
+        else local++;
+    }
+    if (nout) atomicAdd(nout, local);
+}
+
+/* batch form of the rotation filter for k_tri_bf output: one workgroup per pair */
+__global__ __launch_bounds__(256) void k_rot_filter_pairs(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
+                                                          const orbx_kp* __restrict__ kps, const int32_t* __restrict__ counts,
+                                                          int kp_stride, int32_t* __restrict__ match12,
+                                                          int32_t* __restrict__ nmatches) {
+    __shared__ int hist[30];
+    __shared__ int keep[3];
+    const int p = blockIdx.x;
+    const orbx_kp* k1 = kps + (long long)q1[p] * kp_stride;
+    const orbx_kp* k2 = kps + (long long)q2[p] * kp_stride;
+    int32_t* m = match12 + (long long)p * kp_stride;
+    const int n = counts[q1[p]];
+    if (threadIdx.x < 30) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const float factor = 1.0f / 30;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int j = m[i];
+        if (j < 0) continue;
+        float rot = __fsub_rn(k1[i].angle, k2[j].angle);
+        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+        int bin = (int)roundf(__fmul_rn(rot, factor));
+        if (bin == 30) bin = 0;
+        atomicAdd(&hist[bin], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < 30; i++) {
+            const int s = hist[i];
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if (max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
+        else if (max3 < __fmul_rn(0.1f, (float)max1)) { ind3 = -1; }
+        keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
+        nmatches[p] = 0;
+    }
+    __syncthreads();
+    int local = 0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int j = m[i];
+        if (j < 0) continue;
+        float rot = __fsub_rn(k1[i].angle, k2[j].angle);
+        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+        int bin = (int)roundf(__fmul_rn(rot, factor));
+        if (bin == 30) bin = 0;
+        if (bin != keep[0] && bin != keep[1] && bin != keep[2]) m[i] = -1;
+        else local++;
+    }
+    atomicAdd(&nmatches[p], local);
+}
+
+}  // namespace orbamd
+
+#include "launch.h"
+
+namespace orbamd {
+
+hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
+                         const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
+                         int32_t* nmatches, hipStream_t st) {
+    dim3 grid((kp_stride + 255) / 256, npairs);
+    hipLaunchKernelGGL(k_tri_bf, grid, dim3(256), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12, nmatches);
+    return hipGetLastError();
+}
+
+hipError_t launch_rot_filter_pairs(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps,
+                                   const int32_t* counts, int kp_stride, int32_t* match12, int32_t* nmatches,
+                                   hipStream_t st) {
+    hipLaunchKernelGGL(k_rot_filter_pairs, dim3(npairs), dim3(256), 0, st, q1, q2, kps, counts, kp_stride, match12,
+                       nmatches);
+    return hipGetLastError();
+}
+
+hipError_t launch_tri_bf_packed(const orbx_kp* kps1, const uint8_t* desc1, const int32_t* count1, int nref,
+                                const uint8_t* slots, long long slot_bytes, int slot_cap, const MatchGeom& g,
+                                int32_t* match, int cap1, int32_t* nmatches, hipStream_t st) {
+    dim3 grid((cap1 + 255) / 256, nref);
+    hipLaunchKernelGGL(k_tri_bf_packed, grid, dim3(256), 0, st, kps1, desc1, count1, slots, slot_bytes, slot_cap, g,
+                       match, cap1, nmatches);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_slot(const orbx_kp* kps, const uint8_t* desc, const int32_t* count, int cap, uint8_t* slot,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_slot, dim3((cap + 255) / 256), dim3(256), 0, st, kps, desc, count, cap, slot);
+    return hipGetLastError();
+}
+
+hipError_t launch_tri_nodes(const DevView& v1, const DevView& v2, const NodeTask* tasks, int ntasks,
+                            const MatchGeom& g, int only_stereo, int32_t* match12, hipStream_t st) {
+    if (ntasks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tri_nodes, dim3(ntasks), dim3(64), 0, st, v1, v2, tasks, g, only_stereo, match12);
+    return hipGetLastError();
+}
+
+hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* tasks, int ntasks, int max_nc,
+                      float nnratio, int mode, int32_t* out, hipStream_t st) {
+    if (ntasks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bow, dim3(ntasks), dim3(64), (size_t)(max_nc > 0 ? max_nc : 1), st, vq, vc, tasks,
+                       nnratio, mode, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* angB, int swap, int32_t* nout,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(k_rot_filter, dim3(1), dim3(256), 0, st, n, m, angA, angB, swap, nout);
+    return hipGetLastError();
+}
+
+}  // namespace orbamd

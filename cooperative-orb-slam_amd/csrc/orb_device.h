@@ -1,0 +1,70 @@
+/*
+ * orb_device.h -- geometry tables shared by the host launcher (capi.cpp) and the gfx950
+ * kernels. Everything that depends only on (W, H, ORB params) -- pyramid sizes, resize
+ * coefficients, the FAST cell grid, octree root split -- is computed ONCE on the host with
+ * the reference's exact float semantics and uploaded; kernels do integer work on it.
+ *
+ * HBM layout per frame f of a batch (all offsets in bytes / elements):
+ *   input   : caller's frames, level 0 read in place (frame_stride, pitch)
+ *   pyr     : levels 1..L-1 at pyr + f*pyr_frame_bytes + lv.pyr_off, row pitch lv.pitch
+ *   blur    : levels 0..L-1 at blur + f*blur_frame_bytes + lv.blur_off, row pitch lv.pitch
+ *   cellkey : per FAST cell a fixed slot of `cap` u32 keys: cellkey + f*keys_per_frame +
+ *             cell.slot; key = x_rel | y_rel << 12 | score << 24 (coords relative to the
+ *             16-px border, ORBextractor.cc:822-823)
+ *   cellcnt : cellcnt + f*ncells + c
+ *   lvkey   : octree output per level, u32 key (level coords), lvkey + f*kp_per_frame +
+ *             lv.kp_off, count lvcnt + f*L + l
+ */
+#pragma once
+#include <stdint.h>
+
+namespace orbamd {
+
+constexpr int kMaxLevels = 16;
+constexpr int kEdgeThreshold = 19;  // ORBextractor.cc:74
+constexpr int kPatchSize = 31;      // ORBextractor.cc:72
+constexpr int kHalfPatch = 15;      // ORBextractor.cc:73
+constexpr int kRoiMax = 72;         // max FAST cell ROI side (cells are < 60+6 px)
+constexpr int kRoiPitch = 72;
+
+struct LevelDesc {
+    int w, h, pitch;
+    int pad0;
+    long long pyr_off;   // byte offset inside a frame's pyramid area (levels >= 1)
+    long long blur_off;  // byte offset inside a frame's blurred area
+    int cell_begin, ncells;
+    int N;               // mnFeaturesPerLevel[l]
+    int nIni;            // DistributeOctTree root count
+    float hX;            // root width (float, ORBextractor.cc:545)
+    int minX, maxX, minY, maxY;  // octree bounds (ORBextractor.cc:773-776)
+    int key_begin, key_cap;      // this level's cell-key range inside a frame
+    int kp_off, kp_cap;          // octree output slots inside a frame
+    int node_cap;                // max live octree nodes: max(N+3, 4*nIni)
+    float scale;                 // mvScaleFactor[l]
+    float patch_size;            // (float)(int)(31*scale)
+    int blur_vec_end;            // w & ~3 (SSE2 column-filter span)
+    int xmax, simd_end;          // resize: first column with sx+1>=sw; VResize SSE2 span
+    int coef_off;                // offset of this level's resize tables
+};
+
+struct CellDesc {
+    int level;
+    int x0, y0;  // ROI origin in level coordinates
+    int w, h;    // ROI size (before clipping to the band)
+    int xoff, yoff;  // j*wCell, i*hCell (ORBextractor.cc:822-823)
+    int slot;        // key slot offset inside a frame
+    int cap;         // slot capacity
+};
+
+struct ExtractParams {
+    int L;
+    int ncells;
+    int keys_per_frame;
+    int kp_per_frame;
+    int ini_th, min_th;
+    long long pyr_frame_bytes;
+    long long blur_frame_bytes;
+    int umax[16];
+};
+
+}  // namespace orbamd

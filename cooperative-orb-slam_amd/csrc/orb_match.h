@@ -1,0 +1,38 @@
+/*
+ * orb_match.h -- matcher argument structs shared by capi.cpp and match_kernels.hip.
+ */
+#pragma once
+#include <stdint.h>
+
+namespace orbamd {
+
+/* F12 (row-major, F12.at<float>(r,c)), epipole and per-octave thresholds:
+ * th100[o] = 100*mvScaleFactors[o] (float, ORBmatcher.cc:747),
+ * th384[o] = 3.84*mvLevelSigma2[o] (double, ORBmatcher.cc:156). */
+struct MatchGeom {
+    float F[9];
+    float ex, ey;
+    float th100[16];
+    double th384[16];
+};
+
+/* device-side copy of an orbm_kf_view */
+struct DevView {
+    const uint8_t* desc;
+    const float* x;
+    const float* y;
+    const float* angle;
+    const int32_t* octave;
+    const float* uright;
+    const uint8_t* has_mp;
+    const uint8_t* mp_bad;
+    const int32_t* node_feat;
+    int32_t n;
+};
+
+/* one common BoW node (or a 64-query chunk of it): ranges into node_feat of each side */
+struct NodeTask {
+    int q_begin, q_end, c_begin, c_end;
+};
+
+}  // namespace orbamd

@@ -1,0 +1,113 @@
+"""Device-resident batch pipeline (torch tensors as HBM buffers, HIP stream from torch).
+
+One "step" of the hot path over a batch of B frames already in HBM:
+  orbx_extract_batch_device  -> keypoints/descriptors/counts per frame
+  orbm_triangulation_bf_batch_device -> SearchForTriangulation(frame b, frame b-1 mod B)
+torch is plumbing only (allocation, streams, torch.distributed); all compute is in
+liborbamd.so.
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import check, load
+from .extractor import ORBextractor
+
+# camera of the reference config (ORB_SLAM2/my.yaml:8-11)
+FX, FY, CX, CY = 715.092024, 719.025258, 334.298489, 256.326097
+
+
+def default_geometry():
+    """KF2 pose relative to KF1: R = I, t = (0.05, 0, 0.01); returns (F12, ex, ey)."""
+    from .matcher import compute_f12, epipole
+    K = np.array([[FX, 0, CX], [0, FY, CY], [0, 0, 1]], np.float32)
+    R1 = np.eye(3, dtype=np.float32)
+    t1 = np.zeros(3, np.float32)
+    R2 = np.eye(3, dtype=np.float32)
+    t2 = np.array([0.05, 0.0, 0.01], np.float32)
+    F12 = compute_f12(R1, t1, R2, t2, K, K)
+    Cw = -R1.T @ t1  # KF1 camera centre
+    ex, ey = epipole(R2, t2, Cw, FX, FY, CX, CY)
+    return F12, ex, ey
+
+
+class BatchPipeline:
+    """Extract + match over batches of frames on one GPU."""
+
+    def __init__(self, torch, width=640, height=480, batch=64, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mini=7,
+                 device=0, check_ori=False):
+        self.torch = torch
+        self.W, self.H, self.B = width, height, batch
+        self.ext = ORBextractor(nfeatures, scale, nlevels, ini, mini, device=device, max_width=width,
+                                max_height=height, max_batch=batch)
+        self.lib = load()
+        self.stride = self.ext.max_keypoints(width, height)
+        dev = torch.device("cuda", device)
+        self.dev = dev
+        self.kps = torch.empty((batch, self.stride, 6), dtype=torch.float32, device=dev)
+        self.desc = torch.empty((batch, self.stride, 32), dtype=torch.uint8, device=dev)
+        self.counts = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self.match = torch.empty((batch, self.stride), dtype=torch.int32, device=dev)
+        self.nmatch = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self.q1 = torch.arange(batch, dtype=torch.int32, device=dev)
+        self.q2 = ((self.q1 + batch - 1) % batch).to(torch.int32)
+        h = C.c_void_p()
+        check(self.lib.orbm_create(device, C.byref(h)), "orbm_create")
+        self.mh = h
+        self.F12, self.ex, self.ey = default_geometry()
+        self.scale = self.ext.GetScaleFactors()
+        self.sigma2 = self.ext.GetScaleSigmaSquares()
+        self.check_ori = int(check_ori)
+
+    def stream_ptr(self):
+        return self.torch.cuda.current_stream(self.dev).cuda_stream
+
+    def extract(self, frames, stream=None):
+        st = self.stream_ptr() if stream is None else stream
+        self.ext.extract_batch_device(frames, self.kps, self.desc, self.counts, st)
+
+    def match_pairs(self, stream=None):
+        st = self.stream_ptr() if stream is None else stream
+        F = np.ascontiguousarray(self.F12.reshape(9))
+        check(self.lib.orbm_triangulation_bf_batch_device(
+            self.mh, self.B, self.q1.data_ptr(), self.q2.data_ptr(), self.kps.data_ptr(), self.desc.data_ptr(),
+            self.counts.data_ptr(), self.stride, F.ctypes.data, self.ex, self.ey, len(self.scale),
+            self.scale.ctypes.data, self.sigma2.ctypes.data, self.check_ori, self.match.data_ptr(),
+            self.nmatch.data_ptr(), st), "orbm_triangulation_bf_batch_device")
+
+    def step(self, frames, stream=None):
+        self.extract(frames, stream)
+        self.match_pairs(stream)
+
+    def slot_bytes(self):
+        return int(self.lib.orbx_slot_bytes(self.stride))
+
+    def pack(self, frame_idx, slot, stream=None):
+        st = self.stream_ptr() if stream is None else stream
+        check(self.lib.orbx_pack_keyframe_device(
+            self.kps[frame_idx].data_ptr(), self.desc[frame_idx].data_ptr(), self.counts[frame_idx:].data_ptr(),
+            self.stride, slot.data_ptr(), st), "orbx_pack_keyframe_device")
+
+    def match_packed(self, frame_idx, slots, nref, out_match, out_n, stream=None):
+        st = self.stream_ptr() if stream is None else stream
+        F = np.ascontiguousarray(self.F12.reshape(9))
+        check(self.lib.orbm_triangulation_bf_packed_device(
+            self.mh, self.kps[frame_idx].data_ptr(), self.desc[frame_idx].data_ptr(),
+            self.counts[frame_idx:].data_ptr(), nref, slots.data_ptr(), self.slot_bytes(), F.ctypes.data, self.ex,
+            self.ey, len(self.scale), self.scale.ctypes.data, self.sigma2.ctypes.data, out_match.data_ptr(),
+            self.stride, out_n.data_ptr(), st), "orbm_triangulation_bf_packed_device")
+
+    def host_results(self, b):
+        """(keypoints structured array, descriptors uint8 [n,32], match12 int32 [n]) of frame b."""
+        from .extractor import kp_dtype
+        n = int(self.counts[b].item())
+        k = self.kps[b, :n].cpu().numpy().copy().view(np.uint8).view(kp_dtype).reshape(n)
+        d = self.desc[b, :n].cpu().numpy()
+        m = self.match[b, :n].cpu().numpy()
+        return k, d, m
+
+    def close(self):
+        if getattr(self, "mh", None):
+            self.lib.orbm_destroy(self.mh)
+            self.mh = None
+        self.ext.close()

@@ -1,0 +1,142 @@
+"""ORBmatcher -- Python mirror of ORB_SLAM2::ORBmatcher over the C ABI.
+
+Reference surface: ORB_SLAM2/include/ORBmatcher.h:37-102. A :class:`KeyFrameView` stands
+in for the KeyFrame/Frame accessors the matcher reads (mvKeysUn, mDescriptors, mvuRight,
+GetMapPoint/isBad, mFeatVec, mvScaleFactors, mvLevelSigma2).
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import OrbmKfView, check, load
+
+TH_HIGH = 100  # ORBmatcher.cc:37
+TH_LOW = 50  # ORBmatcher.cc:38
+HISTO_LENGTH = 30  # ORBmatcher.cc:39
+
+
+class KeyFrameView:
+    """What ORBmatcher reads from a KeyFrame / Frame.
+
+    keypoints: structured array with fields x, y, angle, octave (mvKeysUn); descriptors: uint8
+    [N,32]; feat_vec: dict node_id -> list of feature indices (DBoW2::FeatureVector; default
+    one node holding every feature); has_mp / mp_bad: bool [N]; uright: float [N] or None.
+    """
+
+    def __init__(self, keypoints, descriptors, scale_factors, level_sigma2, feat_vec=None, uright=None,
+                 has_mp=None, mp_bad=None):
+        n = len(keypoints)
+        self.n = n
+        self.desc = np.ascontiguousarray(descriptors if descriptors is not None else np.zeros((0, 32), np.uint8),
+                                         dtype=np.uint8).reshape(n, 32)
+        self.x = np.ascontiguousarray(keypoints["x"], np.float32)
+        self.y = np.ascontiguousarray(keypoints["y"], np.float32)
+        self.angle = np.ascontiguousarray(keypoints["angle"], np.float32)
+        self.octave = np.ascontiguousarray(keypoints["octave"], np.int32)
+        self.uright = None if uright is None else np.ascontiguousarray(uright, np.float32)
+        self.has_mp = None if has_mp is None else np.ascontiguousarray(has_mp, np.uint8)
+        self.mp_bad = None if mp_bad is None else np.ascontiguousarray(mp_bad, np.uint8)
+        if feat_vec is None:
+            feat_vec = {0: list(range(n))} if n else {}
+        ids = sorted(feat_vec)
+        self.node_id = np.array(ids, np.uint32)
+        offs = [0]
+        feats = []
+        for i in ids:
+            f = sorted(int(v) for v in feat_vec[i])
+            feats.extend(f)
+            offs.append(len(feats))
+        self.node_off = np.array(offs, np.int32)
+        self.node_feat = np.array(feats if feats else [0], np.int32)
+        self.scale_factors = np.ascontiguousarray(scale_factors, np.float32)
+        self.level_sigma2 = np.ascontiguousarray(level_sigma2, np.float32)
+
+    def cview(self):
+        def p(a):
+            return None if a is None else a.ctypes.data
+        return OrbmKfView(self.n, p(self.desc), p(self.x), p(self.y), p(self.angle), p(self.octave), p(self.uright),
+                          p(self.has_mp), p(self.mp_bad), len(self.node_id), p(self.node_id), p(self.node_off),
+                          p(self.node_feat), len(self.scale_factors), p(self.scale_factors), p(self.level_sigma2))
+
+
+def epipole(R2w, t2w, Cw, fx, fy, cx, cy):
+    """(ex, ey) of KF1's centre in KF2 (ORBmatcher.cc:664-670) via orbm_epipole."""
+    lib = load()
+    R = np.ascontiguousarray(R2w, np.float32).reshape(9)
+    t = np.ascontiguousarray(t2w, np.float32).reshape(3)
+    c = np.ascontiguousarray(Cw, np.float32).reshape(3)
+    ex = C.c_float()
+    ey = C.c_float()
+    lib.orbm_epipole(R.ctypes.data, t.ctypes.data, c.ctypes.data, fx, fy, cx, cy, C.byref(ex), C.byref(ey))
+    return ex.value, ey.value
+
+
+def compute_f12(R1w, t1w, R2w, t2w, K1, K2):
+    """LocalMapping::ComputeF12 (LocalMapping.cc:536-553) in float64, rounded to float32.
+    F12 is an input of the matcher; both the oracle and the device receive the same floats."""
+    R1w, t1w, R2w, t2w, K1, K2 = [np.asarray(a, np.float64) for a in (R1w, t1w, R2w, t2w, K1, K2)]
+    R12 = R1w @ R2w.T
+    t12 = -R1w @ R2w.T @ t2w.reshape(3) + t1w.reshape(3)
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
+    return (np.linalg.inv(K1.T) @ tx @ R12 @ np.linalg.inv(K2)).astype(np.float32)
+
+
+class ORBmatcher:
+    """ORB_SLAM2::ORBmatcher(nnratio=0.6, checkOri=true) -- device-backed."""
+    TH_HIGH = TH_HIGH
+    TH_LOW = TH_LOW
+    HISTO_LENGTH = HISTO_LENGTH
+
+    def __init__(self, nnratio=0.6, checkOri=True, device=0):
+        self._lib = load()
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+        h = C.c_void_p()
+        check(self._lib.orbm_create(device, C.byref(h)), "orbm_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.orbm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def DescriptorDistance(a, b):
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return int(load().orbm_descriptor_distance(a.ctypes.data, b.ctypes.data))
+
+    def SearchForTriangulation(self, kf1, kf2, F12, ex, ey, bOnlyStereo=False):
+        """Returns (nmatches, match12 int32 [kf1.n]) -- vMatchedPairs = [(i, match12[i]) | match12[i] >= 0]."""
+        F = np.ascontiguousarray(F12, np.float32).reshape(9)
+        out = np.empty(max(kf1.n, 1), np.int32)
+        n = C.c_int()
+        v1, v2 = kf1.cview(), kf2.cview()
+        check(self._lib.orbm_search_for_triangulation(self._h, C.byref(v1), C.byref(v2), F.ctypes.data, ex, ey,
+                                                      int(bOnlyStereo), int(self.mbCheckOrientation),
+                                                      out.ctypes.data, C.byref(n)), "orbm_search_for_triangulation")
+        return n.value, out[:kf1.n]
+
+    def SearchByBoW(self, kf, other, other_is_keyframe=False):
+        """SearchByBoW(KeyFrame*, Frame&) (default) or SearchByBoW(KeyFrame*, KeyFrame*).
+        Returns (nmatches, matches): for (KF,F) matches[iF] = KF feature index (or -1);
+        for (KF,KF) matches[i1] = idx2 (or -1)."""
+        v1, v2 = kf.cview(), other.cview()
+        n = C.c_int()
+        if other_is_keyframe:
+            out = np.empty(max(kf.n, 1), np.int32)
+            check(self._lib.orbm_search_by_bow_kf_kf(self._h, C.byref(v1), C.byref(v2), self.mfNNratio,
+                                                     int(self.mbCheckOrientation), out.ctypes.data, C.byref(n)),
+                  "orbm_search_by_bow_kf_kf")
+            return n.value, out[:kf.n]
+        out = np.empty(max(other.n, 1), np.int32)
+        check(self._lib.orbm_search_by_bow_kf_f(self._h, C.byref(v1), C.byref(v2), self.mfNNratio,
+                                                int(self.mbCheckOrientation), out.ctypes.data, C.byref(n)),
+              "orbm_search_by_bow_kf_f")
+        return n.value, out[:other.n]

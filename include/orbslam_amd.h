@@ -1,0 +1,218 @@
+/*
+ * orbslam_amd.h -- C ABI of the MI355X-native ORB front-end + Hamming matcher.
+ *
+ * This is the drop-in boundary underneath the reference's two C++ class surfaces
+ * (ORB_SLAM2/include/ORBextractor.h:45-111, ORB_SLAM2/include/ORBmatcher.h:37-102; the
+ * files are byte-identical in ORB_SLAM2/ and ORB_SLAM2.1/). Every entry point below
+ * names the reference member it replaces. Plain pointers and sizes only; no torch,
+ * OpenCV or HIP types cross it (streams are passed as `void*` = hipStream_t).
+ *
+ * Conventions:
+ *   return 0 = OK, negative = error (ORBX_E*). Nothing throws across the ABI.
+ *   Host entry points take host memory; *_device entry points take device memory and a
+ *   stream and do not synchronise.
+ *   A handle (orbx_handle / orbm_ctx) must not be used by two threads at once; create one
+ *   per thread (the reference creates one ORBextractor per Tracking instance and stack
+ *   ORBmatcher objects per thread: Tracking.cc:119-125, LocalMapping.cc:215).
+ */
+#ifndef ORBSLAM_AMD_H
+#define ORBSLAM_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBX_OK 0
+#define ORBX_EARG (-1)     /* bad argument (null pointer, size out of range)          */
+#define ORBX_EDEVICE (-2)  /* HIP runtime / kernel failure, or no usable device        */
+#define ORBX_ECAPACITY (-3) /* caller buffer too small for the result                  */
+
+/* ------------------------------------------------------------------------------------
+ * Extractor -- replaces ORB_SLAM2::ORBextractor (ORBextractor.h:45-111, .cc:410-1132)
+ * ---------------------------------------------------------------------------------- */
+
+/* ctor arguments of ORBextractor::ORBextractor (ORBextractor.cc:410-411); the values the
+ * reference runs with are my.yaml:31-43 = {1000, 1.2f, 8, 20, 7}. */
+typedef struct orbx_params {
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+} orbx_params;
+
+/* One output keypoint = cv::KeyPoint of ORBextractor::operator() (ORBextractor.cc:1043-1105)
+ * minus class_id (always -1 in the reference). 24 bytes. Coordinates are level-0 pixels
+ * (pt *= mvScaleFactor[level], ORBextractor.cc:1095-1101). */
+typedef struct orbx_kp {
+    float x, y;
+    float size;      /* (int)(PATCH_SIZE * mvScaleFactor[level])  ORBextractor.cc:837,846 */
+    float angle;     /* IC_Angle, degrees in [0,360]               ORBextractor.cc:77-104  */
+    float response;  /* FAST score                                 ORBextractor.cc:809-816 */
+    int32_t octave;  /* pyramid level                              ORBextractor.cc:845     */
+} orbx_kp;
+
+typedef struct orbx_handle orbx_handle;
+
+/* ORBextractor::ORBextractor (ORBextractor.cc:410-470). Device buffers are sized for frames
+ * up to max_width x max_height and batches up to max_batch frames. device = HIP ordinal. */
+int orbx_create(const orbx_params* params, int device, int max_width, int max_height,
+                int max_batch, orbx_handle** out);
+void orbx_destroy(orbx_handle* h);
+
+/* Upper bound on keypoints one frame can produce: sum over levels of
+ * max(N_l + 3, 4*nIni_l) (DistributeOctTree overshoot, ORBextractor.cc:669-735). */
+int orbx_max_keypoints(const orbx_handle* h, int width, int height);
+
+/* ORBextractor::operator()(image, mask(ignored), keypoints, descriptors)
+ * (ORBextractor.cc:1043-1105). Host image (8UC1, row pitch in bytes); outputs written to
+ * host arrays kps[cap], desc[cap*32] in the reference's order (levels 0..L-1, each in
+ * DistributeOctTree order). *n = keypoint count. Empty image (w or h == 0) -> *n = 0,
+ * outputs untouched (ORBextractor.cc:1046-1047). */
+int orbx_extract(orbx_handle* h, const uint8_t* img, int width, int height, size_t pitch,
+                 orbx_kp* kps, uint8_t* desc, int cap, int* n);
+
+/* Batched, device-resident form of operator(): nframes frames at d_frames + f*frame_stride
+ * (each width x height, row pitch `pitch`). Per frame f: kps at d_kps + f*kp_stride,
+ * descriptors at d_desc + f*kp_stride*32, count at d_counts[f]. kp_stride must be
+ * >= orbx_max_keypoints(). Enqueued on `stream` (hipStream_t); no host sync. */
+int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_frames,
+                              size_t frame_stride, int width, int height, size_t pitch,
+                              orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
+                              int kp_stride, void* stream);
+
+/* public ORBextractor::mvImagePyramid (ORBextractor.h:85), materialised lazily: copies
+ * level `level` of frame `frame` of the most recent extraction to host dst (pitch bytes).
+ * Pass dst = NULL to query the size only. */
+int orbx_pyramid_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t pitch,
+                       int* width, int* height);
+
+/* ORBextractor getters (ORBextractor.h:63-81): GetLevels, GetScaleFactor,
+ * GetScaleFactors, GetInverseScaleFactors, GetScaleSigmaSquares,
+ * GetInverseScaleSigmaSquares. Arrays have nlevels entries. */
+int orbx_get_levels(const orbx_handle* h);
+float orbx_get_scale_factor(const orbx_handle* h);
+int orbx_get_scale_tables(const orbx_handle* h, float* scale, float* inv_scale, float* sigma2,
+                          float* inv_sigma2);
+/* mnFeaturesPerLevel (ORBextractor.cc:435-446) and umax (ORBextractor.cc:454-469, 16
+ * entries) -- exposed for tests. */
+int orbx_get_feature_split(const orbx_handle* h, int32_t* per_level, int32_t* umax16);
+
+/* ------------------------------------------------------------------------------------
+ * Matcher -- replaces ORB_SLAM2::ORBmatcher (ORBmatcher.h:37-102, ORBmatcher.cc)
+ * ---------------------------------------------------------------------------------- */
+
+/* One KeyFrame/Frame as the matcher sees it, gathered by the caller under its own
+ * locks (KeyFrame::GetMapPoint/GetMapPointMatches, ORBmatcher.cc:526,699,722).
+ * All arrays have n entries unless noted; host or device memory depending on the call. */
+typedef struct orbm_kf_view {
+    int32_t n;                 /* KeyFrame::N                                              */
+    const uint8_t* desc;       /* mDescriptors, n x 32 contiguous rows                     */
+    const float* x;            /* mvKeysUn[i].pt.x                                         */
+    const float* y;            /* mvKeysUn[i].pt.y                                         */
+    const float* angle;        /* mvKeysUn[i].angle (== mvKeys[i].angle)                   */
+    const int32_t* octave;     /* mvKeysUn[i].octave                                       */
+    const float* uright;       /* mvuRight; NULL = monocular (all -1)                      */
+    const uint8_t* has_mp;     /* GetMapPoint(i) != NULL; NULL = none                      */
+    const uint8_t* mp_bad;     /* that MapPoint's isBad(); NULL = none bad                 */
+    int32_t n_nodes;           /* DBoW2::FeatureVector as CSR, node ids ascending          */
+    const uint32_t* node_id;   /* [n_nodes]                                                */
+    const int32_t* node_off;   /* [n_nodes+1] offsets into node_feat                       */
+    const int32_t* node_feat;  /* feature indices, ascending within a node                 */
+    int32_t nlevels;
+    const float* scale_factors; /* mvScaleFactors[nlevels]                                 */
+    const float* level_sigma2;  /* mvLevelSigma2[nlevels]                                  */
+} orbm_kf_view;
+
+typedef struct orbm_ctx orbm_ctx;
+
+/* ORBmatcher::ORBmatcher(nnratio, checkOri) state lives in the call arguments; the ctx
+ * only owns a device, a stream and scratch (one per thread). */
+int orbm_create(int device, orbm_ctx** out);
+void orbm_destroy(orbm_ctx* ctx);
+
+/* ORBmatcher::DescriptorDistance (ORBmatcher.cc:1647-1663): host, 32-byte rows. */
+int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* ORBmatcher::SearchForTriangulation (ORBmatcher.cc:657-823). F12 = 3x3 row-major float
+ * (F12.at<float>(r,c)); (ex,ey) = epipole of KF1's centre in KF2 (ORBmatcher.cc:664-670,
+ * see orbm_epipole). match12[kf1.n] receives idx2 or -1; *nmatches = pair count. */
+int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2,
+                                  const float F12[9], float ex, float ey, int only_stereo,
+                                  int check_ori, int32_t* match12, int* nmatches);
+
+/* ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (ORBmatcher.cc:159-288).
+ * match_f[f.n] receives the KF feature index whose MapPoint was assigned to that Frame
+ * feature (vpMapPointMatches[i] = pKF->GetMapPointMatches()[match_f[i]]) or -1. */
+int orbm_search_by_bow_kf_f(orbm_ctx* ctx, const orbm_kf_view* kf, const orbm_kf_view* f,
+                            float nnratio, int check_ori, int32_t* match_f, int* nmatches);
+
+/* ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&) (ORBmatcher.cc:522-655).
+ * match12[kf1.n] receives idx2 (vpMatches12[idx1] = vpMapPoints2[idx2]) or -1. */
+int orbm_search_by_bow_kf_kf(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2,
+                             float nnratio, int check_ori, int32_t* match12, int* nmatches);
+
+/* Device batch of SearchForTriangulation with one FeatureVector node holding every
+ * feature of both keyframes (the BASELINE "BF" configuration): pair p
+ * matches frame q1[p] (KF1) against frame q2[p] (KF2) of an orbx_extract_batch_device
+ * output (kps/desc/counts/kp_stride as produced there). All keypoints monocular, no
+ * MapPoints, one F12/(ex,ey) and one scale table for all pairs. match12[p*kp_stride+i]. */
+int orbm_triangulation_bf_batch_device(orbm_ctx* ctx, int npairs, const int32_t* d_q1,
+                                       const int32_t* d_q2, const orbx_kp* d_kps,
+                                       const uint8_t* d_desc, const int32_t* d_counts,
+                                       int kp_stride, const float F12[9], float ex, float ey,
+                                       int nlevels, const float* scale_factors,
+                                       const float* level_sigma2, int check_ori,
+                                       int32_t* d_match12, int32_t* d_nmatches, void* stream);
+
+/* Cross-agent variant: one query frame (kps/desc/count on device, e.g. this rank's latest
+ * keyframe) against nref reference slots packed by orbx_pack_keyframe (e.g. the RCCL
+ * all-gather receive buffer). Same BF SearchForTriangulation semantics per slot. */
+int orbm_triangulation_bf_packed_device(orbm_ctx* ctx, const orbx_kp* d_kps1,
+                                        const uint8_t* d_desc1, const int32_t* d_count1,
+                                        int nref, const uint8_t* d_slots, size_t slot_bytes,
+                                        const float F12[9], float ex, float ey, int nlevels,
+                                        const float* scale_factors, const float* level_sigma2,
+                                        int32_t* d_match /* nref x cap1 */, int cap1,
+                                        int32_t* d_nmatches /* nref */, void* stream);
+
+/* Epipole helper (ORBmatcher.cc:664-670): C2 = R2w*Cw + t2w with cv::Mat float GEMM
+ * semantics (double accumulation, one rounding), ex = fx*C2.x*invz + cx, ey likewise. */
+void orbm_epipole(const float R2w[9], const float t2w[3], const float Cw[3], float fx, float fy,
+                  float cx, float cy, float* ex, float* ey);
+
+/* ------------------------------------------------------------------------------------
+ * Cross-agent exchange slot (replaces the LCM KeyFrameexample message,
+ * ORB_SLAM2.1/Examples/ROS/ORB_SLAM2/src/ros_mono.cc:1907-2410).
+ * slot = [u32 n | u32 pad[15] | n x orbx_kp (24 B) | n x 32 B descriptors], fixed size
+ * orbx_slot_bytes(cap). */
+size_t orbx_slot_bytes(int cap);
+int orbx_pack_keyframe_device(const orbx_kp* d_kps, const uint8_t* d_desc,
+                              const int32_t* d_count, int cap, uint8_t* d_slot, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Synthetic input: deterministic frame t of agent a, width x height,
+ * written to host out (pitch = width). Identical on every machine (integer-only).
+ * ---------------------------------------------------------------------------------- */
+int orbx_synth_frame(int agent, int t, int width, int height, uint8_t* out);
+/* frames t0 .. t0+count-1 of agent a, back to back (frame stride width*height). */
+int orbx_synth_frames(int agent, int t0, int count, int width, int height, uint8_t* out);
+
+/* Stage profiling with HIP events recorded on the extraction stream between kernels:
+ * stages = {pyramid, fast_cells, octree, blur, describe}. orbx_profile_enable resets the
+ * accumulators; orbx_profile_read waits for the recorded events and returns the summed
+ * milliseconds per stage (ms[5]) and the number of profiled extraction calls. */
+int orbx_profile_enable(orbx_handle* h, int on);
+int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls);
+
+/* Library/version and device probe. */
+const char* orbx_version(void);
+int orbx_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBSLAM_AMD_H */

@@ -1,0 +1,215 @@
+"""ctypes binding of the CPU oracle (oracle/build/liborb_oracle.so).
+
+TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+may import this module. Parity status: "parity unpinned" at the OpenCV boundary (see
+orb_oracle.h and DESIGN.md).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liborb_oracle.so")
+
+KP_FIELDS = [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"), ("octave", "<i4")]
+kp_dtype = np.dtype(KP_FIELDS)
+
+
+class _Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+class _View(C.Structure):
+    _fields_ = [("n", C.c_int32), ("desc", C.c_void_p), ("x", C.c_void_p), ("y", C.c_void_p),
+                ("angle", C.c_void_p), ("octave", C.c_void_p), ("uright", C.c_void_p),
+                ("has_mp", C.c_void_p), ("mp_bad", C.c_void_p), ("n_nodes", C.c_int32),
+                ("node_id", C.c_void_p), ("node_off", C.c_void_p), ("node_feat", C.c_void_p),
+                ("nlevels", C.c_int32), ("scale_factors", C.c_void_p), ("level_sigma2", C.c_void_p)]
+
+
+_P, _I, _F, _SZ = C.c_void_p, C.c_int, C.c_float, C.c_size_t
+_SIG = {
+    "oc_create": (_P, [C.POINTER(_Params)]),
+    "oc_destroy": (None, [_P]),
+    "oc_extract": (_I, [_P, _P, _I, _I, _SZ, _P, _P, _I, C.POINTER(_I)]),
+    "oc_level_size": (_I, [_P, _I, C.POINTER(_I), C.POINTER(_I)]),
+    "oc_pyramid": (C.POINTER(C.c_uint8), [_P, _I]),
+    "oc_blurred": (C.POINTER(C.c_uint8), [_P, _I]),
+    "oc_level_candidates": (_I, [_P, _I, _P, _I]),
+    "oc_level_octree": (_I, [_P, _I, _P, _I]),
+    "oc_get_tables": (None, [_P, _P, _P, _P, _P, _P, _P]),
+    "oc_fast_atan2": (_F, [_F, _F]),
+    "oc_gauss_kernel_q8": (_I, [_P]),
+    "oc_resize_linear": (None, [_P, _I, _I, _SZ, _P, _I, _I, _SZ]),
+    "oc_gauss7": (None, [_P, _I, _I, _SZ, _P, _SZ]),
+    "oc_fast": (_I, [_P, _I, _I, _SZ, _I, _P, _I]),
+    "oc_descriptor_distance": (_I, [_P, _P]),
+    "oc_search_for_triangulation": (_I, [C.POINTER(_View), C.POINTER(_View), _P, _F, _F, _I, _I, _P]),
+    "oc_search_by_bow_kf_f": (_I, [C.POINTER(_View), C.POINTER(_View), _F, _I, _P]),
+    "oc_search_by_bow_kf_kf": (_I, [C.POINTER(_View), C.POINTER(_View), _F, _I, _P]),
+}
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        lib = C.CDLL(LIB_PATH)
+        for k, (r, a) in _SIG.items():
+            f = getattr(lib, k)
+            f.restype = r
+            f.argtypes = a
+        _lib = lib
+    return _lib
+
+
+class OracleExtractor:
+    """CPU restatement of ORBextractor (ORBextractor.cc:410-1132)."""
+
+    def __init__(self, nfeatures=1000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7):
+        self.lib = load()
+        p = _Params(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+        self.h = self.lib.oc_create(C.byref(p))
+        if not self.h:
+            raise ValueError("bad ORBextractor parameters")
+        self.nlevels = nlevels
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.oc_destroy(self.h)
+        except Exception:
+            pass
+
+    def __call__(self, img, cap=None):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        cap = cap or 64 * 1024
+        kps = np.empty(cap, kp_dtype)
+        desc = np.empty((cap, 32), np.uint8)
+        n = C.c_int()
+        rc = self.lib.oc_extract(self.h, img.ctypes.data, w, h, img.strides[0], kps.ctypes.data, desc.ctypes.data,
+                                 cap, C.byref(n))
+        if rc != 0:
+            raise RuntimeError("oc_extract rc=%d" % rc)
+        n = n.value
+        return kps[:n].copy(), desc[:n].copy()
+
+    def level_size(self, l):
+        w, h = C.c_int(), C.c_int()
+        self.lib.oc_level_size(self.h, l, C.byref(w), C.byref(h))
+        return w.value, h.value
+
+    def pyramid(self, l):
+        w, h = self.level_size(l)
+        p = self.lib.oc_pyramid(self.h, l)
+        return np.ctypeslib.as_array(p, shape=(h * w,)).reshape(h, w).copy()
+
+    def blurred(self, l):
+        w, h = self.level_size(l)
+        p = self.lib.oc_blurred(self.h, l)
+        if not p:
+            return None
+        return np.ctypeslib.as_array(p, shape=(h * w,)).reshape(h, w).copy()
+
+    def _xyr(self, fn, l):
+        n = fn(self.h, l, None, 0)
+        out = np.empty((max(n, 1), 3), np.float32)
+        fn(self.h, l, out.ctypes.data, n)
+        return out[:n]
+
+    def candidates(self, l):
+        return self._xyr(self.lib.oc_level_candidates, l)
+
+    def octree(self, l):
+        return self._xyr(self.lib.oc_level_octree, l)
+
+    def tables(self):
+        L = self.nlevels
+        a = [np.empty(L, np.float32) for _ in range(4)]
+        nf = np.empty(L, np.int32)
+        um = np.empty(16, np.int32)
+        self.lib.oc_get_tables(self.h, *[x.ctypes.data for x in a], nf.ctypes.data, um.ctypes.data)
+        return {"scale": a[0], "inv_scale": a[1], "sigma2": a[2], "inv_sigma2": a[3], "nfeat": nf, "umax": um}
+
+
+def fast(img, threshold, cap=100000):
+    lib = load()
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.empty((cap, 3), np.float32)
+    n = lib.oc_fast(img.ctypes.data, w, h, img.strides[0], threshold, out.ctypes.data, cap)
+    return out[:n].copy()
+
+
+def resize_linear(src, dw, dh):
+    lib = load()
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.empty((dh, dw), np.uint8)
+    lib.oc_resize_linear(src.ctypes.data, src.shape[1], src.shape[0], src.strides[0], dst.ctypes.data, dw, dh, dw)
+    return dst
+
+
+def gauss7(src):
+    lib = load()
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.empty_like(src)
+    lib.oc_gauss7(src.ctypes.data, src.shape[1], src.shape[0], src.strides[0], dst.ctypes.data, dst.strides[0])
+    return dst
+
+
+def gauss_kernel_q8():
+    k = np.empty(7, np.int32)
+    s = load().oc_gauss_kernel_q8(k.ctypes.data)
+    return k, s
+
+
+def fast_atan2(y, x):
+    return load().oc_fast_atan2(y, x)
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return load().oc_descriptor_distance(a.ctypes.data, b.ctypes.data)
+
+
+def _cview(v):
+    """v: an object with the KeyFrameView attributes (orbamd.matcher.KeyFrameView)."""
+    def p(a):
+        return None if a is None else a.ctypes.data
+    return _View(v.n, p(v.desc), p(v.x), p(v.y), p(v.angle), p(v.octave), p(v.uright), p(v.has_mp), p(v.mp_bad),
+                 len(v.node_id), p(v.node_id), p(v.node_off), p(v.node_feat), len(v.scale_factors),
+                 p(v.scale_factors), p(v.level_sigma2))
+
+
+def search_for_triangulation(kf1, kf2, F12, ex, ey, only_stereo=False, check_ori=False):
+    lib = load()
+    F = np.ascontiguousarray(F12, np.float32).reshape(9)
+    out = np.empty(max(kf1.n, 1), np.int32)
+    a, b = _cview(kf1), _cview(kf2)
+    n = lib.oc_search_for_triangulation(C.byref(a), C.byref(b), F.ctypes.data, ex, ey, int(only_stereo),
+                                        int(check_ori), out.ctypes.data)
+    return n, out[:kf1.n]
+
+
+def search_by_bow(kf, other, nnratio, check_ori, other_is_keyframe=False):
+    lib = load()
+    a, b = _cview(kf), _cview(other)
+    if other_is_keyframe:
+        out = np.empty(max(kf.n, 1), np.int32)
+        n = lib.oc_search_by_bow_kf_kf(C.byref(a), C.byref(b), nnratio, int(check_ori), out.ctypes.data)
+        return n, out[:kf.n]
+    out = np.empty(max(other.n, 1), np.int32)
+    n = lib.oc_search_by_bow_kf_f(C.byref(a), C.byref(b), nnratio, int(check_ori), out.ctypes.data)
+    return n, out[:other.n]

@@ -1,0 +1,72 @@
+/*
+ * orb_oracle.h -- CPU restatement of the reference hot path. TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
+ * The product (liborbamd.so) never links or calls it.
+ *
+ * PARITY STATUS: "parity unpinned" at the OpenCV boundary. The reference
+ * (ORB_SLAM2/src/ORBextractor.cc, ORBmatcher.cc) cannot be built here without writing
+ * stand-ins for OpenCV/DBoW2 headers (forbidden), and it ships no tests or golden
+ * vectors. Everything ORB-SLAM2 authored is restated literally with file:line
+ * citations; the OpenCV 3.x primitives it calls (resize INTER_LINEAR, FAST-9/16 + NMS,
+ * GaussianBlur 7x7 sigma 2, fastAtan2, cvRound) are restated from OpenCV 3.3's published
+ * algorithm (DESIGN.md "Pinned semantics"). glibc cosf/sinf are called
+ * directly (as the reference does). Pinned by: constant tables derived from the reference
+ * source (tests/test_oracle_tables.py) and committed regression vectors (tests/golden/).
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+#include "../include/orbslam_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oc_extractor oc_extractor;
+
+oc_extractor* oc_create(const orbx_params* p);
+void oc_destroy(oc_extractor* e);
+/* ORBextractor::operator() (ORBextractor.cc:1043-1105). Returns 0, or ORBX_ECAPACITY. */
+int oc_extract(oc_extractor* e, const uint8_t* img, int w, int h, size_t pitch, orbx_kp* kps,
+               uint8_t* desc, int cap, int* n);
+
+/* stage access for stage-isolated parity tests (valid after oc_extract) */
+int oc_level_size(const oc_extractor* e, int level, int* w, int* h);
+const uint8_t* oc_pyramid(const oc_extractor* e, int level);
+const uint8_t* oc_blurred(const oc_extractor* e, int level); /* NULL if level had no kps */
+/* vToDistributeKeys of a level (ORBextractor.cc:778-829): xyr triplets (x, y relative to
+ * minBorder, response). Returns the count (copies min(count, cap)). */
+int oc_level_candidates(const oc_extractor* e, int level, float* xyr, int cap);
+/* DistributeOctTree output of a level before orientation, level coordinates (+minBorder),
+ * xyr triplets. Returns the count. */
+int oc_level_octree(const oc_extractor* e, int level, float* xyr, int cap);
+
+/* constructor tables (ORBextractor.cc:410-470) */
+void oc_get_tables(const oc_extractor* e, float* scale, float* inv_scale, float* sigma2,
+                   float* inv_sigma2, int32_t* nfeat_per_level, int32_t* umax16);
+
+/* primitives, exposed for unit tests */
+float oc_fast_atan2(float y, float x);
+int oc_gauss_kernel_q8(int32_t* k7); /* fixed-point 7-tap kernel (sum returned) */
+void oc_resize_linear(const uint8_t* src, int sw, int sh, size_t sstep, uint8_t* dst, int dw,
+                      int dh, size_t dstep);
+void oc_gauss7(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst, size_t dstep);
+/* cv::FAST(img, kps, th, true) on a w x h view: xyr triplets, returns count */
+int oc_fast(const uint8_t* img, int w, int h, size_t step, int threshold, float* xyr, int cap);
+
+/* matcher (ORBmatcher.cc) -- host views */
+int oc_descriptor_distance(const uint8_t* a, const uint8_t* b);
+int oc_search_for_triangulation(const orbm_kf_view* kf1, const orbm_kf_view* kf2,
+                                const float F12[9], float ex, float ey, int only_stereo,
+                                int check_ori, int32_t* match12);
+int oc_search_by_bow_kf_f(const orbm_kf_view* kf, const orbm_kf_view* f, float nnratio,
+                          int check_ori, int32_t* match_f);
+int oc_search_by_bow_kf_kf(const orbm_kf_view* kf1, const orbm_kf_view* kf2, float nnratio,
+                           int check_ori, int32_t* match12);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,120 @@
+"""GPU parity: ORBmatcher on the HIP path vs the CPU oracle (exact index equality)."""
+import numpy as np
+import pytest
+
+import oracle_py
+import orbamd
+from orbamd.matcher import KeyFrameView
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames_kf(agent, t, n=2, W=640, H=480, nf=1000):
+    orc = oracle_py.OracleExtractor(nf, 1.2, 8, 20, 7)
+    tabs = orc.tables()
+    out = []
+    for img in orbamd.synth_frames(agent, t, n, W, H):
+        k, d = orc(img)
+        out.append((k, d))
+    return out, tabs
+
+
+def _view(k, d, tabs, **kw):
+    return KeyFrameView(k, d, tabs["scale"], tabs["sigma2"], **kw)
+
+
+def _random_featvec(rng, n, nodes):
+    ids = rng.choice(10000, size=nodes, replace=False)
+    assign = rng.integers(0, nodes, n)
+    return {int(ids[a]): [] for a in range(nodes)} | {int(ids[a]): list(np.nonzero(assign == a)[0])
+                                                    for a in range(nodes)}
+
+
+@pytest.mark.parametrize("check_ori", [False, True])
+def test_triangulation_bf(check_ori):
+    (k1, d1), (k2, d2) = _frames_kf(0, 0)[0]
+    tabs = _frames_kf(0, 0, 1)[1]
+    F12, ex, ey = orbamd.device.default_geometry()
+    v1, v2 = _view(k1, d1, tabs), _view(k2, d2, tabs)
+    m = orbamd.ORBmatcher(0.6, check_ori)
+    ng, mg = m.SearchForTriangulation(v1, v2, F12, ex, ey)
+    no, mo = oracle_py.search_for_triangulation(v1, v2, F12, ex, ey, False, check_ori)
+    assert ng == no and no > 0
+    np.testing.assert_array_equal(mg, mo)
+
+
+def test_triangulation_nodes_mappoints_stereo():
+    rng = np.random.default_rng(3)
+    (k1, d1), (k2, d2) = _frames_kf(1, 4)[0]
+    tabs = _frames_kf(1, 4, 1)[1]
+    F12, ex, ey = orbamd.device.default_geometry()
+    nodes = 40
+    ids = np.sort(rng.choice(5000, nodes, replace=False))
+    fv1 = {int(i): [] for i in ids}
+    fv2 = {int(i): [] for i in ids[::2]} | {int(i) + 5000: [] for i in ids[1::2]}  # partial overlap
+    for i in range(len(k1)):
+        fv1[int(ids[rng.integers(0, nodes)])].append(i)
+    keys2 = sorted(fv2)
+    for i in range(len(k2)):
+        fv2[keys2[rng.integers(0, len(keys2))]].append(i)
+    ur1 = np.where(rng.random(len(k1)) < 0.3, rng.random(len(k1)) * 600, -1).astype(np.float32)
+    ur2 = np.where(rng.random(len(k2)) < 0.3, rng.random(len(k2)) * 600, -1).astype(np.float32)
+    mp1 = rng.random(len(k1)) < 0.2
+    mp2 = rng.random(len(k2)) < 0.2
+    v1 = _view(k1, d1, tabs, feat_vec=fv1, uright=ur1, has_mp=mp1)
+    v2 = _view(k2, d2, tabs, feat_vec=fv2, uright=ur2, has_mp=mp2)
+    for only_stereo in (False, True):
+        for check_ori in (False, True):
+            m = orbamd.ORBmatcher(0.6, check_ori)
+            ng, mg = m.SearchForTriangulation(v1, v2, F12, ex, ey, only_stereo)
+            no, mo = oracle_py.search_for_triangulation(v1, v2, F12, ex, ey, only_stereo, check_ori)
+            assert ng == no
+            np.testing.assert_array_equal(mg, mo)
+
+
+@pytest.mark.parametrize("kfkf", [False, True])
+@pytest.mark.parametrize("nodes", [1, 8, 60])
+def test_search_by_bow(kfkf, nodes):
+    rng = np.random.default_rng(11 + nodes)
+    (k1, d1), (k2, d2) = _frames_kf(2, 9)[0]
+    tabs = _frames_kf(2, 9, 1)[1]
+    ids = np.sort(rng.choice(100000, nodes, replace=False))
+    fv1 = {int(i): [] for i in ids}
+    fv2 = {int(i): [] for i in ids}
+    for i in range(len(k1)):
+        fv1[int(ids[rng.integers(0, nodes)])].append(i)
+    for i in range(len(k2)):
+        fv2[int(ids[rng.integers(0, nodes)])].append(i)
+    mp1 = rng.random(len(k1)) < 0.8
+    bad1 = rng.random(len(k1)) < 0.1
+    mp2 = rng.random(len(k2)) < 0.8
+    bad2 = rng.random(len(k2)) < 0.1
+    v1 = _view(k1, d1, tabs, feat_vec=fv1, has_mp=mp1, mp_bad=bad1)
+    v2 = _view(k2, d2, tabs, feat_vec=fv2, has_mp=mp2, mp_bad=bad2)
+    for ratio, ori in ((0.75, True), (0.7, True), (0.9, False), (0.6, True)):
+        m = orbamd.ORBmatcher(ratio, ori)
+        ng, mg = m.SearchByBoW(v1, v2, other_is_keyframe=kfkf)
+        no, mo = oracle_py.search_by_bow(v1, v2, ratio, ori, other_is_keyframe=kfkf)
+        assert ng == no
+        np.testing.assert_array_equal(mg, mo)
+
+
+def test_batch_pairs_match_oracle():
+    torch = pytest.importorskip("torch")
+    W, H, B = 640, 480, 4
+    frames = orbamd.synth_frames(0, 0, B, W, H)
+    pipe = orbamd.device.BatchPipeline(torch, W, H, B)
+    pipe.step(torch.from_numpy(frames).cuda())
+    torch.cuda.synchronize()
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    tabs = orc.tables()
+    res = [orc(frames[b]) for b in range(B)]
+    for b in range(B):
+        kg, dg, mg = pipe.host_results(b)
+        pb = (b + B - 1) % B
+        v1 = _view(res[b][0], res[b][1], tabs)
+        v2 = _view(res[pb][0], res[pb][1], tabs)
+        no, mo = oracle_py.search_for_triangulation(v1, v2, pipe.F12, pipe.ex, pipe.ey, False, False)
+        np.testing.assert_array_equal(mg, mo)
+        assert int(pipe.nmatch[b].item()) == no
+    pipe.close()
