@@ -329,8 +329,8 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
         h->lvkey.ensure(B * ep.kp_per_frame * 4) || h->lvcnt.ensure(B * ep.L * 4) ||
         h->gscratch.ensure(B * (size_t)ep.keys_per_frame * 8) || h->err.ensure(256))
         return ORBX_EDEVICE;
-    if (!h->lds_attr_set) {
-        HIPR(octree_setup(160 * 1024));
+    if (h->geo.lds_bytes > 64 * 1024 && !h->lds_attr_set) {
+        HIPR(octree_setup(h->geo.lds_bytes));
         h->lds_attr_set = true;
     }
     return 0;
@@ -341,6 +341,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     Geometry& g = h->geo;
     const ExtractParams& ep = g.ep;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
+    HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), st));
     if (prof_mark(h, 0, st)) return ORBX_EDEVICE;
     // pyramid levels 1..L-1 (ORBextractor.cc:1107-1132)
     for (int l = 1; l < ep.L; l++) {
@@ -424,6 +425,15 @@ void orbx_destroy(orbx_handle* h) {
     if (h->stream) (void)hipStreamDestroy(h->stream);
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
     delete h;
+}
+
+int orbx_check_error(orbx_handle* h, void* stream) {
+    if (!h) return ORBX_EARG;
+    HIPR(hipSetDevice(h->device));
+    int flag = 0;
+    HIPR(hipMemcpyAsync(&flag, h->err.p, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIPR(hipStreamSynchronize((hipStream_t)stream));
+    return flag ? ORBX_EDEVICE : 0;
 }
 
 int orbx_profile_enable(orbx_handle* h, int on) {

@@ -70,6 +70,7 @@ SIGNATURES = {
     "orbx_pack_keyframe_device": (_I, [_P, _P, _P, _I, _P, _P]),
     "orbx_synth_frame": (_I, [_I, _I, _I, _I, _P]),
     "orbx_synth_frames": (_I, [_I, _I, _I, _I, _I, _P]),
+    "orbx_check_error": (_I, [_P, _P]),
     "orbx_profile_enable": (_I, [_P, _I]),
     "orbx_profile_read": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_I)]),
     "orbx_version": (C.c_char_p, []),
@@ -79,6 +80,26 @@ SIGNATURES = {
 _lib = None
 
 
+def _bind_runtime():
+    """One HIP runtime per process: if torch is importable, import it first so liborbamd.so's
+    DT_NEEDED `libamdhip64.so` binds to the runtime torch loaded (device pointers and streams
+    from torch are then valid in our kernels); otherwise RUNPATH picks /opt/rocm/lib's."""
+    if os.environ.get("ORBAMD_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def runtime_path():
+    """Path of the libamdhip64 this process uses (for diagnostics/tests)."""
+    for line in open("/proc/self/maps"):
+        if "libamdhip64" in line:
+            return line.split()[-1]
+    return None
+
+
 def load():
     """Load liborbamd.so (raises OSError when it has not been built)."""
     global _lib
@@ -86,6 +107,7 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise OSError("liborbamd.so not built: run `make -C cooperative-orb-slam_amd` "
                           "(or __graft_entry__.build()); expected at %s" % LIB_PATH)
+        _bind_runtime()
         lib = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

@@ -66,6 +66,10 @@ class BatchPipeline:
         st = self.stream_ptr() if stream is None else stream
         self.ext.extract_batch_device(frames, self.kps, self.desc, self.counts, st)
 
+    def check_error(self, stream=None):
+        st = self.stream_ptr() if stream is None else stream
+        check(self.lib.orbx_check_error(self.ext._h, st), "orbx_check_error")
+
     def match_pairs(self, stream=None):
         st = self.stream_ptr() if stream is None else stream
         F = np.ascontiguousarray(self.F12.reshape(9))

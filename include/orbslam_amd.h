@@ -84,6 +84,10 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
                               orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
                               int kp_stride, void* stream);
 
+/* Waits for `stream` and reports a device-side consistency failure of the last batched
+ * extraction (octree capacity or root-index overflow): 0 = OK, ORBX_EDEVICE otherwise. */
+int orbx_check_error(orbx_handle* h, void* stream);
+
 /* public ORBextractor::mvImagePyramid (ORBextractor.h:85), materialised lazily: copies
  * level `level` of frame `frame` of the most recent extraction to host dst (pitch bytes).
  * Pass dst = NULL to query the size only. */
