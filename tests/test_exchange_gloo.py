@@ -1,0 +1,84 @@
+"""Multi-agent exchange on CPU: world_size-2 gloo all-gather of packed keyframe slots and the
+cross-agent SearchForTriangulation (oracle as the matcher) equal a single-process run that
+matches the concatenated buffers."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytest.importorskip("torch")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _agent_keyframe(agent):
+    import oracle_py
+    import orbamd
+    img = orbamd.synth_frames(agent, 0, 1, 640, 480)[0]
+    orc = oracle_py.OracleExtractor()
+    k, d = orc(img)
+    return k, d, orc.tables()
+
+
+def _cross_match(kq, dq, tabs, slots):
+    import oracle_py
+    import orbamd
+    from orbamd import exchange
+    F12, ex, ey = orbamd.device.default_geometry()
+    out = []
+    vq = orbamd.KeyFrameView(kq, dq, tabs["scale"], tabs["sigma2"])
+    for buf in slots:
+        k2, d2 = exchange.unpack_slot_host(buf)
+        v2 = orbamd.KeyFrameView(k2, d2, tabs["scale"], tabs["sigma2"])
+        out.append(oracle_py.search_for_triangulation(vq, v2, F12, ex, ey, False, False)[1])
+    return out
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "cooperative-orb-slam_amd"), os.path.join(root, "oracle")]
+    import torch
+    import torch.distributed as dist
+    from orbamd import exchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    k, d, tabs = _agent_keyframe(rank)
+    cap = 1031
+    mine = torch.from_numpy(exchange.pack_slot_host(k, d, cap))
+    allb = torch.empty(world * mine.numel(), dtype=torch.uint8)
+    dist.all_gather_into_tensor(allb, mine)
+    slots = allb.numpy().reshape(world, -1)
+    res = _cross_match(k, d, tabs, slots)
+    q.put((rank, [r.tolist() for r in res]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_allgather_cross_agent_match():
+    import torch.multiprocessing as mp
+    from orbamd import exchange
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    kfs = [_agent_keyframe(a) for a in range(world)]
+    slots = [exchange.pack_slot_host(k, d, 1031) for k, d, _ in kfs]
+    for r in range(world):
+        exp = _cross_match(kfs[r][0], kfs[r][1], kfs[r][2], slots)
+        assert [e.tolist() for e in exp] == got[r]
+        assert sum(x >= 0 for x in got[r][r]) > 0.5 * len(kfs[r][0])  # self-match sanity
