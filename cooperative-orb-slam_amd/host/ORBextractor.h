@@ -1,0 +1,69 @@
+/*
+ * ORBextractor.h -- drop-in replacement of ORB_SLAM2/include/ORBextractor.h (public surface of
+ * ORBextractor.h:45-85 kept verbatim in meaning: ctor, operator(), the six getters, public
+ * mvImagePyramid). The work runs on an MI355X through include/orbslam_amd.h; protected state is
+ * a device handle instead of the reference's tables (callers never touch it: Frame.cc:69-75,
+ * 252-258; Tracking.cc:119-125).
+ *
+ * Error behaviour: like the reference, an empty image returns with outputs untouched and a
+ * non-8UC1 image asserts (ORBextractor.cc:1046-1050); a device failure throws
+ * std::runtime_error (the reference has no failure mode there; there is no CPU fallback).
+ *
+ * mvImagePyramid is materialised from the device after every call (needed by
+ * Frame::ComputeStereoMatches, A1 Frame.cc:474-581); set ORBAMD_NO_HOST_PYRAMID=1 in
+ * monocular deployments to skip that PCIe copy.
+ */
+#ifndef ORBEXTRACTOR_H
+#define ORBEXTRACTOR_H
+
+#include <opencv2/core/core.hpp>
+#include <opencv2/features2d/features2d.hpp>
+#include <vector>
+
+struct orbx_handle;
+
+namespace ORB_SLAM2 {
+
+class ORBextractor {
+public:
+    enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
+
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST);
+    ~ORBextractor();
+
+    // Compute the ORB features and descriptors on an image (mask ignored, as in the reference).
+    void operator()(cv::InputArray image, cv::InputArray mask, std::vector<cv::KeyPoint>& keypoints,
+                    cv::OutputArray descriptors);
+
+    int inline GetLevels() { return nlevels; }
+    float inline GetScaleFactor() { return (float)scaleFactor; }
+    std::vector<float> inline GetScaleFactors() { return mvScaleFactor; }
+    std::vector<float> inline GetInverseScaleFactors() { return mvInvScaleFactor; }
+    std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2; }
+    std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
+
+    std::vector<cv::Mat> mvImagePyramid;
+
+protected:
+    void ensureHandle(int width, int height);
+
+    int nfeatures;
+    double scaleFactor;
+    int nlevels;
+    int iniThFAST;
+    int minThFAST;
+    std::vector<float> mvScaleFactor;
+    std::vector<float> mvInvScaleFactor;
+    std::vector<float> mvLevelSigma2;
+    std::vector<float> mvInvLevelSigma2;
+
+    orbx_handle* mpHandle;
+    int mHandleW, mHandleH;
+    int mDevice;
+    bool mbHostPyramid;
+    std::vector<unsigned char> mKpBuf, mDescBuf;
+};
+
+}  // namespace ORB_SLAM2
+
+#endif

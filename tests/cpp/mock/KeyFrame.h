@@ -1,0 +1,31 @@
+/* TEST-ONLY mock of the KeyFrame members ORBmatcher reads (names as in ORB_SLAM2/include/KeyFrame.h). */
+#ifndef KEYFRAME_H
+#define KEYFRAME_H
+#include <map>
+#include <opencv2/core/core.hpp>
+#include <opencv2/features2d/features2d.hpp>
+#include <vector>
+#include "MapPoint.h"
+namespace DBoW2 {
+typedef std::map<unsigned int, std::vector<unsigned int> > FeatureVector;
+}
+namespace ORB_SLAM2 {
+class KeyFrame {
+public:
+    int N = 0;
+    float fx = 0, fy = 0, cx = 0, cy = 0;
+    std::vector<cv::KeyPoint> mvKeys, mvKeysUn;
+    std::vector<float> mvuRight;
+    cv::Mat mDescriptors;
+    DBoW2::FeatureVector mFeatVec;
+    std::vector<float> mvScaleFactors, mvLevelSigma2;
+    std::vector<MapPoint*> mvpMapPoints;
+    cv::Mat Rcw, tcw, Ow;
+    std::vector<MapPoint*> GetMapPointMatches() { return mvpMapPoints; }
+    MapPoint* GetMapPoint(const size_t& i) { return mvpMapPoints[i]; }
+    cv::Mat GetRotation() { return Rcw.clone(); }
+    cv::Mat GetTranslation() { return tcw.clone(); }
+    cv::Mat GetCameraCenter() { return Ow.clone(); }
+};
+}  // namespace ORB_SLAM2
+#endif

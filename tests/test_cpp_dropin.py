@@ -1,0 +1,27 @@
+"""The C++ drop-in classes (host/ORBextractor.*, host/ORBmatcher*) build with g++ against
+the C ABI, and (GPU) reproduce the oracle bit-exactly when called like ORB-SLAM2 does."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "cpp", "build", "test_dropin")
+
+
+def _build():
+    subprocess.check_call([os.path.join(ROOT, "tests", "cpp", "build.sh")])
+
+
+def test_dropin_builds():
+    _build()
+    assert os.path.exists(BIN)
+
+
+@pytest.mark.gpu
+def test_dropin_bit_exact_on_gpu():
+    _build()
+    env = dict(os.environ)
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=600, env=env)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0 and "ALL PASS" in r.stdout
