@@ -118,7 +118,10 @@ struct Geometry {
     std::vector<int> coef;
     std::vector<int> tile_begin;
     int ntiles = 0;
+    std::vector<int> bjob_begin;  // blur strip jobs (256 cols x 64 rows) per level
+    int nbjobs = 0;
     int NC = 0, KL = 0, lds_bytes = 0;
+    int roi_pitch = 0, roi_rows = 0;  // FAST cell LDS staging (max cell ROI)
     DevBuf d_lv, d_cells, d_coef, d_tiles;
 
     int build(const Tables& T, int W_, int H_) {
@@ -240,6 +243,12 @@ struct Geometry {
             kp_off += d.kp_cap;
             maxnode = std::max(maxnode, d.node_cap);
         }
+        roi_pitch = 4;
+        roi_rows = 1;
+        for (const CellDesc& c : cells) {
+            roi_pitch = std::max(roi_pitch, (int)align_up(c.w, 4));
+            roi_rows = std::max(roi_rows, c.h);
+        }
         ep.L = L;
         ep.ncells = (int)cells.size();
         ep.keys_per_frame = key_begin;
@@ -254,6 +263,10 @@ struct Geometry {
         for (int l = 0; l < L; l++)
             tile_begin[l + 1] = tile_begin[l] + ((lv[l].w + 63) / 64) * ((lv[l].h + 15) / 16);
         ntiles = tile_begin[L];
+        bjob_begin.assign(L + 1, 0);
+        for (int l = 0; l < L; l++)
+            bjob_begin[l + 1] = bjob_begin[l] + ((lv[l].w + 255) / 256) * ((lv[l].h + 63) / 64);
+        nbjobs = bjob_begin[L];
         // octree LDS: node arrays (92 B/node, NC pow2) + keys (7 B/key)
         NC = 1;
         while (NC < maxnode) NC <<= 1;
@@ -265,12 +278,13 @@ struct Geometry {
         lds_bytes = node_bytes + 7 * KL;
         // upload
         if (d_lv.ensure(sizeof(LevelDesc) * L) || d_cells.ensure(sizeof(CellDesc) * cells.size()) ||
-            d_coef.ensure(sizeof(int) * std::max<size_t>(coef.size(), 1)) || d_tiles.ensure(sizeof(int) * (L + 1)))
+            d_coef.ensure(sizeof(int) * std::max<size_t>(coef.size(), 1)) || d_tiles.ensure(sizeof(int) * 2 * (L + 1)))
             return ORBX_EDEVICE;
         HIPR(hipMemcpy(d_lv.p, lv.data(), sizeof(LevelDesc) * L, hipMemcpyHostToDevice));
         HIPR(hipMemcpy(d_cells.p, cells.data(), sizeof(CellDesc) * cells.size(), hipMemcpyHostToDevice));
         if (!coef.empty()) HIPR(hipMemcpy(d_coef.p, coef.data(), sizeof(int) * coef.size(), hipMemcpyHostToDevice));
         HIPR(hipMemcpy(d_tiles.p, tile_begin.data(), sizeof(int) * (L + 1), hipMemcpyHostToDevice));
+        HIPR(hipMemcpy(d_tiles.as<int>() + (L + 1), bjob_begin.data(), sizeof(int) * (L + 1), hipMemcpyHostToDevice));
         return 0;
     }
     void release() { d_lv.release(); d_cells.release(); d_coef.release(); d_tiles.release(); }
@@ -354,15 +368,24 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
                            d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, st));
     }
     if (prof_mark(h, 1, st)) return ORBX_EDEVICE;
-    HIPR(launch_fast_cells(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, g.d_cells.as<CellDesc>(),
-                           h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), nframes, st));
+    if (getenv("ORBX_FAST_DENSE"))
+        HIPR(launch_fast_cells(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, g.d_cells.as<CellDesc>(),
+                               h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), nframes, st));
+    else
+        HIPR(launch_fast_cells2(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, g.d_cells.as<CellDesc>(),
+                                h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), g.roi_pitch, g.roi_rows, nframes,
+                                st));
     if (prof_mark(h, 2, st)) return ORBX_EDEVICE;
     HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                        h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
                        (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, h->err.as<int>(), nframes, st));
     if (prof_mark(h, 3, st)) return ORBX_EDEVICE;
-    HIPR(launch_blur(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                     g.d_tiles.as<int>(), g.ntiles, h->lvcnt.as<int>(), nframes, st));
+    if (getenv("ORBX_BLUR_TILES"))
+        HIPR(launch_blur(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                         g.d_tiles.as<int>(), g.ntiles, h->lvcnt.as<int>(), nframes, st));
+    else
+        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                                g.d_tiles.as<int>() + (ep.L + 1), g.nbjobs, h->lvcnt.as<int>(), nframes, st));
     if (prof_mark(h, 4, st)) return ORBX_EDEVICE;
     HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                          h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride, nframes,

@@ -37,20 +37,8 @@ __device__ __forceinline__ int iclamp(int v, int lo, int hi) { return v < lo ? l
 /* Pyramid: cv::resize(INTER_LINEAR) 8U fixed point, one output pixel per lane.        */
 /* xofs/alpha/yofs/beta are the host-built tables of resizeGeneric_.       */
 /* ----------------------------------------------------------------------------------- */
-__global__ __launch_bounds__(256) void k_resize_level(
-    const uint8_t* __restrict__ src, long long src_fstride, int src_pitch, int sw, int sh,
-    uint8_t* __restrict__ dst, long long dst_fstride, int dst_pitch, int dw, int dh,
-    const int* __restrict__ xofs, const short2* __restrict__ alpha, const int* __restrict__ yofs,
-    const short2* __restrict__ beta, int xmax, int simd_end) {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= dw || y >= dh) return;
-    const uint8_t* S = src + (long long)blockIdx.z * src_fstride;
-    const int sy = yofs[y];
-    const int r0 = iclamp(sy, 0, sh - 1), r1 = iclamp(sy + 1, 0, sh - 1);
-    const uint8_t* S0 = S + (long long)r0 * src_pitch;
-    const uint8_t* S1 = S + (long long)r1 * src_pitch;
-    const short2 b = beta[y];
+__device__ __forceinline__ int resize_px(const uint8_t* S0, const uint8_t* S1, int x, int xmax, int simd_end,
+                                         const int* __restrict__ xofs, const short2* __restrict__ alpha, short2 b) {
     const int sx = xofs[x];
     int h0, h1;
     if (x < xmax) {
@@ -66,7 +54,33 @@ __global__ __launch_bounds__(256) void k_resize_level(
         v = ((((h0 >> 4) * b.x) >> 16) + (((h1 >> 4) * b.y) >> 16) + 2) >> 2;
     else  // scalar FixedPtCast<int, uchar, 22>
         v = (h0 * b.x + h1 * b.y + (1 << 21)) >> 22;
-    dst[(long long)blockIdx.z * dst_fstride + (long long)y * dst_pitch + x] = (uint8_t)iclamp(v, 0, 255);
+    return iclamp(v, 0, 255);
+}
+
+/* 4 adjacent output pixels per lane, one dword store (rows are 64-B aligned). */
+__global__ __launch_bounds__(256) void k_resize_level(
+    const uint8_t* __restrict__ src, long long src_fstride, int src_pitch, int sw, int sh,
+    uint8_t* __restrict__ dst, long long dst_fstride, int dst_pitch, int dw, int dh,
+    const int* __restrict__ xofs, const short2* __restrict__ alpha, const int* __restrict__ yofs,
+    const short2* __restrict__ beta, int xmax, int simd_end) {
+    const int x0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x0 >= dw || y >= dh) return;
+    const uint8_t* S = src + (long long)blockIdx.z * src_fstride;
+    const int sy = yofs[y];
+    const int r0 = iclamp(sy, 0, sh - 1), r1 = iclamp(sy + 1, 0, sh - 1);
+    const uint8_t* S0 = S + (long long)r0 * src_pitch;
+    const uint8_t* S1 = S + (long long)r1 * src_pitch;
+    const short2 b = beta[y];
+    uint8_t* D = dst + (long long)blockIdx.z * dst_fstride + (long long)y * dst_pitch;
+    if (x0 + 4 <= dw) {
+        uint32_t packed = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) packed |= (uint32_t)resize_px(S0, S1, x0 + i, xmax, simd_end, xofs, alpha, b) << (8 * i);
+        *(uint32_t*)(D + x0) = packed;
+    } else {
+        for (int x = x0; x < dw; x++) D[x] = (uint8_t)resize_px(S0, S1, x, xmax, simd_end, xofs, alpha, b);
+    }
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -201,6 +215,104 @@ __global__ __launch_bounds__(256) void k_fast_cells(
             total += __popcll(m);
         }
         if (total > c.cap) total = c.cap;  // cannot happen: cap >= max NMS survivors
+    }
+    if (lane == 0) cellcnt[(long long)f * ep.ncells + ci] = total;
+}
+
+/* Candidate form (k_fast_cells2): a necessary condition for S > t_lo (any 9-arc contains two
+ * cyclically adjacent cardinal ring points 0/4/8/12, so both are brighter or both darker) is
+ * tested on every band pixel; survivors are compacted in row-major order with ballot+mbcnt
+ * into an LDS list; S is computed only for them (full lanes), and the NMS/emission passes walk
+ * the list, so emission order is still the reference's row-major order. Pixels that fail the
+ * test have S <= t_lo <= t and are zero in the NMS buffer, exactly as in cv::FAST. */
+__device__ __forceinline__ bool fast_pretest(const uint8_t* p, int P, int t) {
+    const int v = p[0];
+    const int c0 = p[3 * P], c4 = p[3], c8 = p[-3 * P], c12 = p[-3];
+    const int hi = v + t, lo = v - t;
+    const bool b0 = c0 > hi, b4 = c4 > hi, b8 = c8 > hi, b12 = c12 > hi;
+    const bool d0 = c0 < lo, d4 = c4 < lo, d8 = c8 < lo, d12 = c12 < lo;
+    return (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
+}
+
+__global__ __launch_bounds__(256) void k_fast_cells2(
+    const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
+    ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
+    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP, int RH) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int ci = blockIdx.x * 4 + wave;
+    if (ci >= ep.ncells) return;  // wave-uniform; no block barriers in this kernel
+    const int roi_bytes = RP * RH;
+    uint8_t* roi = lds + wave * (4 * roi_bytes);
+    uint8_t* str = roi + roi_bytes;
+    uint16_t* clist = (uint16_t*)(str + roi_bytes);  // <= roi_bytes entries (band < ROI)
+    const CellDesc c = cells[ci];
+    const LevelDesc& lv = levels[c.level];
+    const uint8_t* img = c.level == 0 ? frames + (long long)f * fstride
+                                      : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
+    const int pitch = c.level == 0 ? pitch0 : lv.pitch;
+    const uint8_t* src = img + (long long)c.y0 * pitch + c.x0;
+    for (int r = 0; r < c.h; r++) {
+        for (int col = lane; col < c.w; col += 64) roi[r * RP + col] = src[(long long)r * pitch + col];
+        for (int col = lane; col < RP / 4; col += 64) ((uint32_t*)(str + r * RP))[col] = 0u;
+    }
+    wave_sync();
+    const int bw = c.w - 6, bh = c.h - 6;
+    int total = 0;
+    if (bw > 0 && bh > 0) {
+        const int t_lo = min(ep.ini_th, ep.min_th);
+        const int rpi = 64 / bw;
+        const int lr = lane / bw, lc = lane - lr * bw;
+        const bool lane_ok = lane < rpi * bw;
+        int ncand = 0;
+        for (int r0 = 0; r0 < bh; r0 += rpi) {
+            const int rr = r0 + lr;
+            bool cand = false;
+            if (lane_ok && rr < bh) cand = fast_pretest(roi + (rr + 3) * RP + lc + 3, RP, t_lo);
+            const unsigned long long m = __ballot(cand);
+            if (cand) clist[ncand + lane_prefix(m)] = (uint16_t)(((rr + 3) << 8) | (lc + 3));
+            ncand += __popcll(m);
+        }
+        wave_sync();
+        for (int i = lane; i < ncand; i += 64) {
+            const int e = clist[i];
+            const int o = (e >> 8) * RP + (e & 0xFF);
+            const int S = fast_strength(roi + o, RP);
+            if (S > t_lo) str[o] = (uint8_t)S;
+        }
+        wave_sync();
+        int t = ep.ini_th;
+        int cnt = 0;
+        for (int i0 = 0; i0 < ncand; i0 += 64) {
+            const int i = i0 + lane;
+            bool keep = false;
+            if (i < ncand) {
+                const int e = clist[i];
+                keep = fast_survivor(str + (e >> 8) * RP + (e & 0xFF), RP, t);
+            }
+            cnt += __popcll(__ballot(keep));
+        }
+        if (cnt == 0) t = ep.min_th;
+        uint32_t* out = cellkey + (long long)f * ep.keys_per_frame + c.slot;
+        for (int i0 = 0; i0 < ncand; i0 += 64) {
+            const int i = i0 + lane;
+            bool keep = false;
+            int e = 0;
+            if (i < ncand) {
+                e = clist[i];
+                keep = fast_survivor(str + (e >> 8) * RP + (e & 0xFF), RP, t);
+            }
+            const unsigned long long m = __ballot(keep);
+            if (keep) {
+                const int pos = total + lane_prefix(m);
+                const int sc = str[(e >> 8) * RP + (e & 0xFF)] - 1;
+                const uint32_t xr = (uint32_t)((e & 0xFF) + c.xoff), yr = (uint32_t)((e >> 8) + c.yoff);
+                if (pos < c.cap) out[pos] = xr | (yr << 12) | ((uint32_t)sc << 24);
+            }
+            total += __popcll(m);
+        }
+        if (total > c.cap) total = c.cap;
     }
     if (lane == 0) cellcnt[(long long)f * ep.ncells + ci] = total;
 }
@@ -631,6 +743,89 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames
     }
 }
 
+/* Strip form: one wave per (frame, level, 256-column strip, 64-row chunk); each lane owns 4
+ * adjacent output columns, loads 3 dwords per source row, keeps the 7 row sums of the vertical
+ * window in registers and writes one dword per output row. Same arithmetic as k_blur. */
+constexpr int kBlurRows = 64;
+
+__device__ __forceinline__ void blur_rowsum4(const uint8_t* row, int x0, int w, int rs[4]) {
+    int b[10];
+    if (x0 >= 4 && x0 + 8 <= w) {
+        const uint32_t w0 = *(const uint32_t*)(row + x0 - 4);
+        const uint32_t w1 = *(const uint32_t*)(row + x0);
+        const uint32_t w2 = *(const uint32_t*)(row + x0 + 4);
+        b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
+        b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
+        b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 10; j++) {
+            int x = x0 - 3 + j;
+            x = x < 0 ? -x : x;
+            x = x >= w ? 2 * w - 2 - x : x;
+            x = x < 0 ? 0 : x;  // lanes past the right edge (outputs discarded)
+            b[j] = row[x];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        rs[i] = 18 * (b[i] + b[i + 6]) + 34 * (b[i + 1] + b[i + 5]) + 49 * (b[i + 2] + b[i + 4]) + 55 * b[i + 3];
+}
+
+__global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
+                                                     const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                     ExtractParams ep, const LevelDesc* __restrict__ levels,
+                                                     const int* __restrict__ job_begin /* L+1 */,
+                                                     const int* __restrict__ lvcnt) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    int j = blockIdx.x * 4 + wave;
+    if (j >= job_begin[ep.L]) return;
+    int l = 0;
+    while (l + 1 < ep.L && j >= job_begin[l + 1]) l++;
+    if (lvcnt[f * ep.L + l] == 0) return;  // a level without keypoints is never blurred (:1081)
+    j -= job_begin[l];
+    const LevelDesc& lv = levels[l];
+    const int nstrips = (lv.w + 255) / 256;
+    const int strip = j % nstrips, chunk = j / nstrips;
+    const int x0 = strip * 256 + lane * 4;
+    const int ya = chunk * kBlurRows, yb = min(lv.h, ya + kBlurRows);
+    const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
+    const int pitch = l == 0 ? pitch0 : lv.pitch;
+    uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
+    const bool lane_on = x0 < lv.w;
+    int r[7][4];
+    // prime the window with rows ya-3 .. ya+2 (REFLECT_101 rows)
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        const int yy = reflect101(ya - 3 + k, lv.h);
+        blur_rowsum4(img + (long long)yy * pitch, lane_on ? x0 : 0, lv.w, r[k + 1]);
+    }
+    for (int y = ya; y < yb; y++) {
+#pragma unroll
+        for (int k = 0; k < 6; k++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) r[k][i] = r[k + 1][i];
+        const int yy = reflect101(y + 3, lv.h);
+        blur_rowsum4(img + (long long)yy * pitch, lane_on ? x0 : 0, lv.w, r[6]);
+        if (!lane_on) continue;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int s = 55 * r[3][i] + 49 * (r[2][i] + r[4][i]) + 34 * (r[1][i] + r[5][i]) + 18 * (r[0][i] + r[6][i]);
+            int v = (x0 + i < lv.blur_vec_end) ? (s + 0x7FFF + ((s >> 16) & 1)) >> 16 : (s + (1 << 15)) >> 16;
+            v = v > 255 ? 255 : v;
+            packed |= (uint32_t)v << (8 * i);
+        }
+        uint8_t* o = out + (long long)y * lv.pitch + x0;
+        if (x0 + 4 <= lv.w) {
+            *(uint32_t*)o = packed;
+        } else {
+            for (int i = 0; i < 4 && x0 + i < lv.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+        }
+    }
+}
+
 /* ----------------------------------------------------------------------------------- */
 /* IC_Angle + rBRIEF + output, one wave per octree output slot.                          */
 /* ----------------------------------------------------------------------------------- */
@@ -739,7 +934,7 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
     const short2* alpha = (const short2*)(coef + dw);
     const int* yofs = coef + 2 * dw;
     const short2* beta = (const short2*)(coef + 2 * dw + dh);
-    dim3 grid((dw + 63) / 64, (dh + 3) / 4, nframes);
+    dim3 grid((dw + 255) / 256, (dh + 3) / 4, nframes);
     hipLaunchKernelGGL(k_resize_level, grid, dim3(256), 0, st, src, src_fstride, src_pitch, sw, sh, dst,
                        dst_fstride, dst_pitch, dw, dh, xofs, alpha, yofs, beta, xmax, simd_end);
     return hipGetLastError();
@@ -751,6 +946,16 @@ hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch
     dim3 grid((ep.ncells + 3) / 4, nframes);
     hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, ep, levels, cells,
                        cellkey, cellcnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                              const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
+                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int nframes, hipStream_t st) {
+    dim3 grid((ep.ncells + 3) / 4, nframes);
+    const size_t lds = 4 * 4 * (size_t)RP * RH;
+    hipLaunchKernelGGL(k_fast_cells2, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
+                       cellkey, cellcnt, RP, RH);
     return hipGetLastError();
 }
 
@@ -774,6 +979,15 @@ hipError_t launch_blur(const uint8_t* frames, long long fstride, int pitch0, con
     dim3 grid(ntiles, nframes);
     hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, tile_begin,
                        lvcnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
+                              const ExtractParams& ep, const LevelDesc* levels, const int* job_begin, int njobs,
+                              const int* lvcnt, int nframes, hipStream_t st) {
+    dim3 grid((njobs + 3) / 4, nframes);
+    hipLaunchKernelGGL(k_blur_strips, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
+                       job_begin, lvcnt);
     return hipGetLastError();
 }
 

@@ -15,6 +15,9 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                              const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                              uint32_t* cellkey, int* cellcnt, int nframes, hipStream_t st);
+hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                              const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
+                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int nframes, hipStream_t st);
 hipError_t octree_setup(int lds_bytes);
 hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                          const uint32_t* cellkey, const int* cellcnt, uint32_t* lvkey, int* lvcnt,
@@ -23,6 +26,9 @@ hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const
 hipError_t launch_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
                        const ExtractParams& ep, const LevelDesc* levels, const int* tile_begin, int ntiles,
                        const int* lvcnt, int nframes, hipStream_t st);
+hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
+                              const ExtractParams& ep, const LevelDesc* levels, const int* job_begin, int njobs,
+                              const int* lvcnt, int nframes, hipStream_t st);
 hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                            const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
                            const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,

@@ -59,22 +59,32 @@ struct PairSrc {
     const orbx_kp* kps2; const uint8_t* desc2; int n2;
 };
 
+/* 256 threads = SPLIT parts x Q queries (Q = 256/SPLIT). Part k scans the k-th slice of
+ * every candidate tile in order with the reference's rule (accept dist <= best, so ties go to
+ * the later candidate); slices are merged with min distance, ties -> larger idx2, which is
+ * exactly the sequential scan's result (DESIGN.md "Matcher semantics"). */
+template <int SPLIT>
 __device__ __forceinline__ void tri_bf_body(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
                                             int32_t* __restrict__ nmatch) {
+    constexpr int Q = 256 / SPLIT;
+    constexpr int SL = kTile / SPLIT;
     __shared__ uint4 s_desc[kTile * 2];
     __shared__ float s_x[kTile], s_y[kTile];
     __shared__ int s_oct[kTile];
+    __shared__ int s_bd[SPLIT > 1 ? SPLIT : 1][Q], s_bi[SPLIT > 1 ? SPLIT : 1][Q];
     const int tid = threadIdx.x;
-    const int idx1 = blockIdx.x * 256 + tid;
-    if ((int)(blockIdx.x * 256) >= s.n1) return;  // block-uniform
+    const int ql = tid % Q, part = tid / Q;
+    const int q0 = blockIdx.x * Q;
+    if (q0 >= s.n1) return;  // block-uniform
+    const int idx1 = q0 + ql;
     const bool active = idx1 < s.n1;
     uint32_t q[8];
     float a = 0.f, b = 0.f, c = 0.f;
     if (active) {
         const uint4* qd = (const uint4*)(s.desc1 + (long long)idx1 * 32);
-        const uint4 q0 = qd[0], q1 = qd[1];
-        q[0] = q0.x; q[1] = q0.y; q[2] = q0.z; q[3] = q0.w;
-        q[4] = q1.x; q[5] = q1.y; q[6] = q1.z; q[7] = q1.w;
+        const uint4 q0v = qd[0], q1v = qd[1];
+        q[0] = q0v.x; q[1] = q0v.y; q[2] = q0v.z; q[3] = q0v.w;
+        q[4] = q1v.x; q[5] = q1v.y; q[6] = q1v.z; q[7] = q1v.w;
         epi_line(g, s.kps1[idx1].x, s.kps1[idx1].y, &a, &b, &c);
     } else {
 #pragma unroll
@@ -93,7 +103,8 @@ __device__ __forceinline__ void tri_bf_body(const PairSrc& s, const MatchGeom& g
         }
         __syncthreads();
         if (active) {
-            for (int j = 0; j < nt; j++) {
+            const int jb = part * SL, je = min(nt, jb + SL);
+            for (int j = jb; j < je; j++) {
                 const uint4 c0 = s_desc[2 * j], c1 = s_desc[2 * j + 1];
                 const int dist = __popc(q[0] ^ c0.x) + __popc(q[1] ^ c0.y) + __popc(q[2] ^ c0.z) +
                                  __popc(q[3] ^ c0.w) + __popc(q[4] ^ c1.x) + __popc(q[5] ^ c1.y) +
@@ -109,12 +120,26 @@ __device__ __forceinline__ void tri_bf_body(const PairSrc& s, const MatchGeom& g
             }
         }
     }
+    if (SPLIT > 1) {
+        s_bd[part][ql] = bestDist;
+        s_bi[part][ql] = bestIdx2;
+        __syncthreads();
+        if (part != 0) return;
+        for (int k = 1; k < SPLIT; k++) {
+            const int d = s_bd[k][ql], i = s_bi[k][ql];
+            if (i >= 0 && (bestIdx2 < 0 || d < bestDist || (d == bestDist && i > bestIdx2))) {
+                bestDist = d;
+                bestIdx2 = i;
+            }
+        }
+    }
     if (active) {
         out[idx1] = bestIdx2;
         if (bestIdx2 >= 0) atomicAdd(nmatch, 1);
     }
 }
 
+template <int SPLIT>
 __global__ __launch_bounds__(256) void k_tri_bf(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
                                                 const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
                                                 const int32_t* __restrict__ counts, int kp_stride, MatchGeom g,
@@ -124,7 +149,7 @@ __global__ __launch_bounds__(256) void k_tri_bf(const int32_t* __restrict__ q1, 
     PairSrc s;
     s.kps1 = kps + (long long)f1 * kp_stride; s.desc1 = desc + (long long)f1 * kp_stride * 32; s.n1 = counts[f1];
     s.kps2 = kps + (long long)f2 * kp_stride; s.desc2 = desc + (long long)f2 * kp_stride * 32; s.n2 = counts[f2];
-    tri_bf_body(s, g, match12 + (long long)p * kp_stride, nmatches + p);
+    tri_bf_body<SPLIT>(s, g, match12 + (long long)p * kp_stride, nmatches + p);
 }
 
 /* cross-agent: the query frame against nref packed slots (orbx_pack_keyframe_device) */
@@ -141,7 +166,7 @@ __global__ __launch_bounds__(256) void k_tri_bf_packed(const orbx_kp* __restrict
     (void)slot_cap;
     s.kps2 = (const orbx_kp*)(slot + 64);
     s.desc2 = slot + 64 + (long long)cap2 * sizeof(orbx_kp);
-    tri_bf_body(s, g, match + (long long)r * cap1, nmatches + r);
+    tri_bf_body<4>(s, g, match + (long long)r * cap1, nmatches + r);
 }
 
 /* pack one frame's (n, kps, desc) into an exchange slot */
@@ -376,8 +401,16 @@ namespace orbamd {
 hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
                          int32_t* nmatches, hipStream_t st) {
-    dim3 grid((kp_stride + 255) / 256, npairs);
-    hipLaunchKernelGGL(k_tri_bf, grid, dim3(256), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12, nmatches);
+    // few pairs: split the candidate scan over 4 parts for more waves; many pairs: 256 queries per block
+    if (npairs * ((kp_stride + 255) / 256) < 2048) {
+        dim3 grid((kp_stride + 63) / 64, npairs);
+        hipLaunchKernelGGL(k_tri_bf<4>, grid, dim3(256), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
+                           nmatches);
+    } else {
+        dim3 grid((kp_stride + 255) / 256, npairs);
+        hipLaunchKernelGGL(k_tri_bf<1>, grid, dim3(256), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
+                           nmatches);
+    }
     return hipGetLastError();
 }
 
@@ -392,7 +425,7 @@ hipError_t launch_rot_filter_pairs(int npairs, const int32_t* q1, const int32_t*
 hipError_t launch_tri_bf_packed(const orbx_kp* kps1, const uint8_t* desc1, const int32_t* count1, int nref,
                                 const uint8_t* slots, long long slot_bytes, int slot_cap, const MatchGeom& g,
                                 int32_t* match, int cap1, int32_t* nmatches, hipStream_t st) {
-    dim3 grid((cap1 + 255) / 256, nref);
+    dim3 grid((cap1 + 63) / 64, nref);
     hipLaunchKernelGGL(k_tri_bf_packed, grid, dim3(256), 0, st, kps1, desc1, count1, slots, slot_bytes, slot_cap, g,
                        match, cap1, nmatches);
     return hipGetLastError();
