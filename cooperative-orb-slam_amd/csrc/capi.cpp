@@ -122,6 +122,7 @@ struct Geometry {
     int nbjobs = 0;
     int NC = 0, KL = 0, lds_bytes = 0;
     int roi_pitch = 0, roi_rows = 0;  // FAST cell LDS staging (max cell ROI)
+    int tiled_ok[kMaxLevels] = {0};   // level's resize fits the LDS-tiled kernel
     DevBuf d_lv, d_cells, d_coef, d_tiles;
 
     int build(const Tables& T, int W_, int H_) {
@@ -185,6 +186,7 @@ struct Geometry {
                 while (se < dw - 4) se += 4;
                 d.xmax = xmax;
                 d.simd_end = se;
+                tiled_ok[l] = resize_tile_fits(xofs, yofs, sw, sh, dw, dh);
                 // OpenCV switches INTER_LINEAR to INTER_AREA for exact 2x downscales; unsupported
                 if (std::abs(scale_x - 2.0) < 1e-15 && std::abs(scale_y - 2.0) < 1e-15) return ORBX_EARG;
             }
@@ -364,8 +366,13 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         const uint8_t* src = l == 1 ? d_frames : h->pyr.as<uint8_t>() + s.pyr_off;
         const long long sfs = l == 1 ? fstride : ep.pyr_frame_bytes;
         const int sp = l == 1 ? pitch : s.pitch;
-        HIPR(launch_resize(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes, d.pitch,
-                           d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, st));
+        if (g.tiled_ok[l] && !getenv("ORBX_RESIZE_SIMPLE"))
+            HIPR(launch_resize_tiled(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes,
+                                     d.pitch, d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes,
+                                     st));
+        else
+            HIPR(launch_resize(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes, d.pitch,
+                               d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, st));
     }
     if (prof_mark(h, 1, st)) return ORBX_EDEVICE;
     if (getenv("ORBX_FAST_DENSE"))

@@ -32,6 +32,22 @@ __device__ __forceinline__ int lane_prefix(unsigned long long mask) {
 }
 
 __device__ __forceinline__ int iclamp(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+static inline int iclamp_host(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* n consecutive little-endian dwords starting at an arbitrary byte address, from n+1 aligned
+ * dword loads + v_alignbyte (rows of the input frame need not be 4-byte aligned). The caller
+ * guarantees the 4 bytes after the span are readable. */
+template <int N>
+__device__ __forceinline__ void load_u32_unaligned(const uint8_t* p, uint32_t out[N]) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    const unsigned sh = (unsigned)(a & 3);
+    uint32_t w[N + 1];
+#pragma unroll
+    for (int i = 0; i <= N; i++) w[i] = q[i];
+#pragma unroll
+    for (int i = 0; i < N; i++) out[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+}
 
 /* ----------------------------------------------------------------------------------- */
 /* Pyramid: cv::resize(INTER_LINEAR) 8U fixed point, one output pixel per lane.        */
@@ -81,6 +97,82 @@ __global__ __launch_bounds__(256) void k_resize_level(
     } else {
         for (int x = x0; x < dw; x++) D[x] = (uint8_t)resize_px(S0, S1, x, xmax, simd_end, xofs, alpha, b);
     }
+}
+
+/* Tiled form: a 64 x 16 output tile per workgroup; its source window (<= kRsW x kRsH bytes,
+ * checked on the host) is staged in LDS with aligned dword loads, then each thread produces 4
+ * rows of one column from LDS. */
+constexpr int kRsTW = 64, kRsTH = 16, kRsW = 144, kRsH = 40;
+
+__global__ __launch_bounds__(256) void k_resize_tiled(
+    const uint8_t* __restrict__ src, long long src_fstride, int src_pitch, int sw, int sh,
+    uint8_t* __restrict__ dst, long long dst_fstride, int dst_pitch, int dw, int dh,
+    const int* __restrict__ xofs, const short2* __restrict__ alpha, const int* __restrict__ yofs,
+    const short2* __restrict__ beta, int xmax, int simd_end) {
+    __shared__ __align__(16) uint8_t tile[kRsH][kRsW];
+    const int c0 = blockIdx.x * kRsTW, r0 = blockIdx.y * kRsTH;
+    const int c1 = min(c0 + kRsTW, dw), r1 = min(r0 + kRsTH, dh);
+    const uint8_t* S = src + (long long)blockIdx.z * src_fstride;
+    // source window (uniform): columns [xb, xe], rows [yb, ye]
+    const int sx_lo = xofs[c0];
+    const int sx_hi = min(sw - 1, xofs[c1 - 1] + 1);
+    const int yb = iclamp(yofs[r0], 0, sh - 1), ye = iclamp(yofs[r1 - 1] + 1, 0, sh - 1);
+    const uintptr_t rowbase0 = (uintptr_t)(S + (long long)yb * src_pitch + sx_lo);
+    const int nrows = ye - yb + 1;
+    // aligned dwords per row: cover [sx_lo - mis, sx_hi]
+    const int tid = threadIdx.x;
+    {
+        constexpr int kPer = (kRsH * (kRsW / 4) + 255) / 256;
+        uint32_t v[kPer];
+        int slot[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int i = tid + k * 256;
+            const int r = i / (kRsW / 4), d = i - r * (kRsW / 4);
+            slot[k] = -1;
+            v[k] = 0;
+            if (r < nrows) {
+                const uintptr_t rb = (uintptr_t)(S + (long long)(yb + r) * src_pitch + sx_lo);
+                const uintptr_t ab = rb & ~(uintptr_t)3;
+                const int span = (int)(rb - ab) + (sx_hi - sx_lo + 1);
+                if (4 * d < span) {
+                    v[k] = *(const uint32_t*)(ab + 4 * d);
+                    slot[k] = r * kRsW + 4 * d;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++)
+            if (slot[k] >= 0) *(uint32_t*)(&tile[0][0] + slot[k]) = v[k];
+    }
+    __syncthreads();
+    const int c = c0 + (tid & 63);
+    if (c >= c1) return;
+    // LDS column of source x in row r: (x - sx_lo) + mis(r), mis = misalignment of that row's start
+    const int sx = xofs[c];
+    int a0 = 2048, a1 = 0;
+    if (c < xmax) { const short2 a = alpha[c]; a0 = a.x; a1 = a.y; }
+    const int sxn = c < xmax ? sx + 1 : sx;
+    uint8_t* D = dst + (long long)blockIdx.z * dst_fstride;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int y = r0 + (tid >> 6) * 4 + k;
+        if (y >= r1) break;
+        const int sy = yofs[y];
+        const int q0 = iclamp(sy, 0, sh - 1) - yb, q1 = iclamp(sy + 1, 0, sh - 1) - yb;
+        const int m0 = (int)(((uintptr_t)(S + (long long)(yb + q0) * src_pitch + sx_lo)) & 3);
+        const int m1 = (int)(((uintptr_t)(S + (long long)(yb + q1) * src_pitch + sx_lo)) & 3);
+        const int h0 = tile[q0][sx - sx_lo + m0] * a0 + tile[q0][sxn - sx_lo + m0] * a1;
+        const int h1 = tile[q1][sx - sx_lo + m1] * a0 + tile[q1][sxn - sx_lo + m1] * a1;
+        const short2 b = beta[y];
+        int v;
+        if (c < simd_end)
+            v = ((((h0 >> 4) * b.x) >> 16) + (((h1 >> 4) * b.y) >> 16) + 2) >> 2;
+        else
+            v = (h0 * b.x + h1 * b.y + (1 << 21)) >> 22;
+        D[(long long)y * dst_pitch + c] = (uint8_t)iclamp(v, 0, 255);
+    }
+    (void)rowbase0;
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -253,9 +345,32 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
                                       : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
     const int pitch = c.level == 0 ? pitch0 : lv.pitch;
     const uint8_t* src = img + (long long)c.y0 * pitch + c.x0;
-    for (int r = 0; r < c.h; r++) {
-        for (int col = lane; col < c.w; col += 64) roi[r * RP + col] = src[(long long)r * pitch + col];
-        for (int col = lane; col < RP / 4; col += 64) ((uint32_t*)(str + r * RP))[col] = 0u;
+    {
+        // D dwords per ROI row, 64/D rows per pass; all passes' loads issued before the LDS writes
+        const int D = (c.w + 3) >> 2;
+        const int rpp = 64 / D;
+        const int lr = lane / D, ld = lane - lr * D;
+        const bool on = lane < rpp * D;
+        constexpr int kMaxPass = 24;  // ROI rows <= 72, >= 3 rows per pass
+        uint32_t v[kMaxPass];
+#pragma unroll
+        for (int k = 0; k < kMaxPass; k++) {
+            const int r = k * rpp + lr;
+            v[k] = 0u;
+            if (on && r < c.h) {
+                uint32_t t[1];
+                load_u32_unaligned<1>(src + (long long)r * pitch + 4 * ld, t);
+                v[k] = t[0];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kMaxPass; k++) {
+            const int r = k * rpp + lr;
+            if (on && r < c.h) {
+                ((uint32_t*)(roi + r * RP))[ld] = v[k];
+                ((uint32_t*)(str + r * RP))[ld] = 0u;
+            }
+        }
     }
     wave_sync();
     const int bw = c.w - 6, bh = c.h - 6;
@@ -748,12 +863,11 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames
  * window in registers and writes one dword per output row. Same arithmetic as k_blur. */
 constexpr int kBlurRows = 64;
 
-__device__ __forceinline__ void blur_rowsum4(const uint8_t* row, int x0, int w, int rs[4]) {
-    int b[10];
-    if (x0 >= 4 && x0 + 8 <= w) {
-        const uint32_t w0 = *(const uint32_t*)(row + x0 - 4);
-        const uint32_t w1 = *(const uint32_t*)(row + x0);
-        const uint32_t w2 = *(const uint32_t*)(row + x0 + 4);
+__device__ __forceinline__ void blur_load10(const uint8_t* row, int x0, int w, int b[10]) {
+    if (x0 >= 4 && x0 + 12 <= w) {
+        uint32_t t[3];
+        load_u32_unaligned<3>(row + x0 - 4, t);
+        const uint32_t w0 = t[0], w1 = t[1], w2 = t[2];
         b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
         b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
         b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
@@ -767,10 +881,15 @@ __device__ __forceinline__ void blur_rowsum4(const uint8_t* row, int x0, int w, 
             b[j] = row[x];
         }
     }
+}
+
+__device__ __forceinline__ void blur_rowsum4(const int b[10], int rs[4]) {
 #pragma unroll
     for (int i = 0; i < 4; i++)
         rs[i] = 18 * (b[i] + b[i + 6]) + 34 * (b[i + 1] + b[i + 5]) + 49 * (b[i + 2] + b[i + 4]) + 55 * b[i + 3];
 }
+
+constexpr int kBlurG = 4;  // source rows loaded per batch (issued before any compute)
 
 __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                      const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
@@ -794,34 +913,45 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     const int pitch = l == 0 ? pitch0 : lv.pitch;
     uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
     const bool lane_on = x0 < lv.w;
+    const int xl = lane_on ? x0 : 0;
     int r[7][4];
-    // prime the window with rows ya-3 .. ya+2 (REFLECT_101 rows)
+    {
+        int b[6][10];
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-        const int yy = reflect101(ya - 3 + k, lv.h);
-        blur_rowsum4(img + (long long)yy * pitch, lane_on ? x0 : 0, lv.w, r[k + 1]);
+        for (int k = 0; k < 6; k++) blur_load10(img + (long long)reflect101(ya - 3 + k, lv.h) * pitch, xl, lv.w, b[k]);
+#pragma unroll
+        for (int k = 0; k < 6; k++) blur_rowsum4(b[k], r[k + 1]);
     }
-    for (int y = ya; y < yb; y++) {
+    for (int y = ya; y < yb; y += kBlurG) {
+        int b[kBlurG][10];
 #pragma unroll
-        for (int k = 0; k < 6; k++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) r[k][i] = r[k + 1][i];
-        const int yy = reflect101(y + 3, lv.h);
-        blur_rowsum4(img + (long long)yy * pitch, lane_on ? x0 : 0, lv.w, r[6]);
-        if (!lane_on) continue;
-        uint32_t packed = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int s = 55 * r[3][i] + 49 * (r[2][i] + r[4][i]) + 34 * (r[1][i] + r[5][i]) + 18 * (r[0][i] + r[6][i]);
-            int v = (x0 + i < lv.blur_vec_end) ? (s + 0x7FFF + ((s >> 16) & 1)) >> 16 : (s + (1 << 15)) >> 16;
-            v = v > 255 ? 255 : v;
-            packed |= (uint32_t)v << (8 * i);
+        for (int g = 0; g < kBlurG; g++) {
+            const int yy = min(y + g + 3, yb + 2);  // rows past the chunk are clamped (outputs skipped)
+            blur_load10(img + (long long)reflect101(yy, lv.h) * pitch, xl, lv.w, b[g]);
         }
-        uint8_t* o = out + (long long)y * lv.pitch + x0;
-        if (x0 + 4 <= lv.w) {
-            *(uint32_t*)o = packed;
-        } else {
-            for (int i = 0; i < 4 && x0 + i < lv.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+#pragma unroll
+        for (int g = 0; g < kBlurG; g++) {
+#pragma unroll
+            for (int k = 0; k < 6; k++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) r[k][i] = r[k + 1][i];
+            blur_rowsum4(b[g], r[6]);
+            const int yo = y + g;
+            if (!lane_on || yo >= yb) continue;
+            uint32_t packed = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int s = 55 * r[3][i] + 49 * (r[2][i] + r[4][i]) + 34 * (r[1][i] + r[5][i]) + 18 * (r[0][i] + r[6][i]);
+                int v = (x0 + i < lv.blur_vec_end) ? (s + 0x7FFF + ((s >> 16) & 1)) >> 16 : (s + (1 << 15)) >> 16;
+                v = v > 255 ? 255 : v;
+                packed |= (uint32_t)v << (8 * i);
+            }
+            uint8_t* o = out + (long long)yo * lv.pitch + x0;
+            if (x0 + 4 <= lv.w) {
+                *(uint32_t*)o = packed;
+            } else {
+                for (int i = 0; i < 4 && x0 + i < lv.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+            }
         }
     }
 }
@@ -859,17 +989,21 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     int m10 = 0, m01 = 0;
     {
         const int u = (lane & 31) - 15;
-        const int vbeg = (lane < 32) ? -15 : 1, vend = (lane < 32) ? 0 : 15;
+        const int vbeg = (lane < 32) ? -15 : 1;  // half 0: v = -15..0, half 1: v = 1..15 (16th row masked)
         if ((lane & 31) < 31) {
             const uint8_t* col = img + (long long)y * pitch + x + u;
             const int au = u < 0 ? -u : u;
-            for (int v = vbeg; v <= vend; v++) {
+            int I[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int v = vbeg + k;
                 const int av = v < 0 ? -v : v;
-                if (au <= ep.umax[av]) {
-                    const int I = col[(long long)v * pitch];
-                    m10 += u * I;
-                    m01 += v * I;
-                }
+                I[k] = (v <= 15 && au <= ep.umax[av < 16 ? av : 15]) ? col[(long long)v * pitch] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                m10 += u * I[k];
+                m01 += (vbeg + k) * I[k];
             }
         }
 #pragma unroll
@@ -938,6 +1072,33 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
     hipLaunchKernelGGL(k_resize_level, grid, dim3(256), 0, st, src, src_fstride, src_pitch, sw, sh, dst,
                        dst_fstride, dst_pitch, dw, dh, xofs, alpha, yofs, beta, xmax, simd_end);
     return hipGetLastError();
+}
+
+hipError_t launch_resize_tiled(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
+                               long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
+                               int simd_end, int nframes, hipStream_t st) {
+    const int* xofs = coef;
+    const short2* alpha = (const short2*)(coef + dw);
+    const int* yofs = coef + 2 * dw;
+    const short2* beta = (const short2*)(coef + 2 * dw + dh);
+    dim3 grid((dw + kRsTW - 1) / kRsTW, (dh + kRsTH - 1) / kRsTH, nframes);
+    hipLaunchKernelGGL(k_resize_tiled, grid, dim3(256), 0, st, src, src_fstride, src_pitch, sw, sh, dst, dst_fstride,
+                       dst_pitch, dw, dh, xofs, alpha, yofs, beta, xmax, simd_end);
+    return hipGetLastError();
+}
+
+int resize_tile_fits(const int* xofs, const int* yofs, int sw, int sh, int dw, int dh) {
+    for (int c0 = 0; c0 < dw; c0 += kRsTW) {
+        const int c1 = c0 + kRsTW < dw ? c0 + kRsTW : dw;
+        const int hi = xofs[c1 - 1] + 1 < sw - 1 ? xofs[c1 - 1] + 1 : sw - 1;
+        if (hi - xofs[c0] + 1 + 3 + 4 > kRsW) return 0;
+    }
+    for (int r0 = 0; r0 < dh; r0 += kRsTH) {
+        const int r1 = r0 + kRsTH < dh ? r0 + kRsTH : dh;
+        const int lo = iclamp_host(yofs[r0], 0, sh - 1), hi = iclamp_host(yofs[r1 - 1] + 1, 0, sh - 1);
+        if (hi - lo + 1 > kRsH) return 0;
+    }
+    return 1;
 }
 
 hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,

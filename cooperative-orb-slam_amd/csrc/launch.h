@@ -12,6 +12,10 @@ namespace orbamd {
 hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
                          long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
                          int simd_end, int nframes, hipStream_t st);
+hipError_t launch_resize_tiled(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
+                               long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
+                               int simd_end, int nframes, hipStream_t st);
+int resize_tile_fits(const int* xofs, const int* yofs, int sw, int sh, int dw, int dh);
 hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                              const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                              uint32_t* cellkey, int* cellcnt, int nframes, hipStream_t st);
