@@ -269,6 +269,10 @@ struct Geometry {
         for (int l = 0; l < L; l++)
             bjob_begin[l + 1] = bjob_begin[l] + ((lv[l].w + 255) / 256) * ((lv[l].h + 63) / 64);
         nbjobs = bjob_begin[L];
+        for (int l = 0; l <= kMaxLevels; l++) {
+            ep.kp_off[l] = l < L ? lv[l].kp_off : kp_off;
+            ep.bjob_begin[l] = l <= L ? bjob_begin[l] : nbjobs;
+        }
         // octree LDS: node arrays (92 B/node, NC pow2) + keys (7 B/key)
         NC = 1;
         while (NC < maxnode) NC <<= 1;

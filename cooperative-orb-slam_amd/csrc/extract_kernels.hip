@@ -35,8 +35,8 @@ __device__ __forceinline__ int iclamp(int v, int lo, int hi) { return v < lo ? l
 static inline int iclamp_host(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 /* n consecutive little-endian dwords starting at an arbitrary byte address, from n+1 aligned
- * dword loads + v_alignbyte (rows of the input frame need not be 4-byte aligned). The caller
- * guarantees the 4 bytes after the span are readable. */
+ * dword loads + v_alignbyte (rows of the input frame need not be 4-byte aligned). Reads only
+ * dwords that overlap the span, so it never touches memory past the span's last byte's dword. */
 template <int N>
 __device__ __forceinline__ void load_u32_unaligned(const uint8_t* p, uint32_t out[N]) {
     const uintptr_t a = (uintptr_t)p;
@@ -44,7 +44,8 @@ __device__ __forceinline__ void load_u32_unaligned(const uint8_t* p, uint32_t ou
     const unsigned sh = (unsigned)(a & 3);
     uint32_t w[N + 1];
 #pragma unroll
-    for (int i = 0; i <= N; i++) w[i] = q[i];
+    for (int i = 0; i < N; i++) w[i] = q[i];
+    w[N] = sh ? q[N] : 0u;  // an aligned span never touches the dword after it
 #pragma unroll
     for (int i = 0; i < N; i++) out[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
@@ -889,53 +890,112 @@ __device__ __forceinline__ void blur_rowsum4(const int b[10], int rs[4]) {
         rs[i] = 18 * (b[i] + b[i + 6]) + 34 * (b[i + 1] + b[i + 5]) + 49 * (b[i + 2] + b[i + 4]) + 55 * b[i + 3];
 }
 
-constexpr int kBlurG = 4;  // source rows loaded per batch (issued before any compute)
+constexpr int kBlurG = 4;     // source rows staged per batch
+constexpr int kBlurSeg = 264; // bytes of one staged row segment: strip (256) + 4 left + 4 right
 
+/* One wave per (frame, level, 256-column strip, 64-row chunk). Each source row segment
+ * [sx-4, sx+260) is loaded once per wave with coalesced dword loads into LDS, REFLECT_101
+ * halo bytes are patched in LDS by three lanes, and every lane reads its 10 bytes
+ * (x0-3 .. x0+6 for its 4 outputs) as three aligned LDS dwords. The vertical 7-row window
+ * lives in registers. Arithmetic identical to k_blur. */
 __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                      const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                      ExtractParams ep, const LevelDesc* __restrict__ levels,
-                                                     const int* __restrict__ job_begin /* L+1 */,
+                                                     const int* __restrict__ job_begin_unused,
                                                      const int* __restrict__ lvcnt) {
+    __shared__ __align__(16) uint8_t s_rows[4][kBlurG][kBlurSeg];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     int j = blockIdx.x * 4 + wave;
-    if (j >= job_begin[ep.L]) return;
-    int l = 0;
-    while (l + 1 < ep.L && j >= job_begin[l + 1]) l++;
+    if (j >= ep.bjob_begin[ep.L]) return;
+    const int l = level_of(ep.bjob_begin, ep.L, j);
+    j -= ep.bjob_begin[l];
     if (lvcnt[f * ep.L + l] == 0) return;  // a level without keypoints is never blurred (:1081)
-    j -= job_begin[l];
     const LevelDesc& lv = levels[l];
-    const int nstrips = (lv.w + 255) / 256;
+    const int w = lv.w, h = lv.h;
+    const int nstrips = (w + 255) / 256;
     const int strip = j % nstrips, chunk = j / nstrips;
-    const int x0 = strip * 256 + lane * 4;
-    const int ya = chunk * kBlurRows, yb = min(lv.h, ya + kBlurRows);
+    const int sx = strip * 256;
+    const int x0 = sx + lane * 4;
+    const int ya = chunk * kBlurRows, yb = min(h, ya + kBlurRows);
     const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
     const int pitch = l == 0 ? pitch0 : lv.pitch;
     uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
-    const bool lane_on = x0 < lv.w;
-    const int xl = lane_on ? x0 : 0;
+    const bool lane_on = x0 < w;
+    const int seg0 = sx - 4;                      // segment byte 0 = column seg0
+    const int need_hi = min(sx + 256, w) + 3;     // columns [sx-3, need_hi) are read
+    // stage source row yy (reflected) into buffer k: dword i covers columns seg0+4i .. +3
+    auto stage = [&](int k, int yy) {
+        const uint8_t* row = img + (long long)reflect101(yy, h) * pitch;
+        uint8_t* dstrow = s_rows[wave][k];
+#pragma unroll
+        for (int part = 0; part < 2; part++) {
+            const int i = lane + part * 64;
+            const int c = seg0 + 4 * i;
+            if (i < kBlurSeg / 4 && c + 3 >= 0 && c < w && c < need_hi) {
+                uint32_t v;
+                if (c >= 0 && c + 4 <= w) {
+                    uint32_t t[1];
+                    load_u32_unaligned<1>(row + c, t);  // 4 bytes after: inside the row or its pitch
+                    v = t[0];
+                } else {
+                    v = 0;
+                    for (int b = 0; b < 4; b++)
+                        if (c + b >= 0 && c + b < w) v |= (uint32_t)row[c + b] << (8 * b);
+                }
+                ((uint32_t*)dstrow)[i] = v;
+            }
+        }
+    };
+    auto patch = [&](int k) {
+        uint8_t* dstrow = s_rows[wave][k];
+        // REFLECT_101 halo: column -1-q <- 1+q (left strip), column w+q <- w-2-q (right)
+        if (lane < 3) {
+            const int q = lane;
+            if (sx == 0) dstrow[(-1 - q) - seg0] = dstrow[(1 + q) - seg0];
+            const int xr = w + q;
+            if (xr >= sx && xr < need_hi) dstrow[xr - seg0] = dstrow[(w - 2 - q) - seg0];
+        }
+    };
+    auto rowsum = [&](int k, int rs[4]) {
+        const uint32_t* d = (const uint32_t*)s_rows[wave][k] + lane;
+        const uint32_t w0 = d[0], w1 = d[1], w2 = d[2];  // columns x0-4 .. x0+7
+        int b[10];
+        b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
+        b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
+        b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            rs[i] = 18 * (b[i] + b[i + 6]) + 34 * (b[i + 1] + b[i + 5]) + 49 * (b[i + 2] + b[i + 4]) + 55 * b[i + 3];
+    };
     int r[7][4];
-    {
-        int b[6][10];
+    // prime rows ya-3 .. ya+2 (two batches of 3)
 #pragma unroll
-        for (int k = 0; k < 6; k++) blur_load10(img + (long long)reflect101(ya - 3 + k, lv.h) * pitch, xl, lv.w, b[k]);
+    for (int half = 0; half < 2; half++) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) blur_rowsum4(b[k], r[k + 1]);
+        for (int k = 0; k < 3; k++) stage(k, ya - 3 + 3 * half + k);
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < 3; k++) patch(k);
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < 3; k++) rowsum(k, r[1 + 3 * half + k]);
+        wave_sync();
     }
     for (int y = ya; y < yb; y += kBlurG) {
-        int b[kBlurG][10];
 #pragma unroll
-        for (int g = 0; g < kBlurG; g++) {
-            const int yy = min(y + g + 3, yb + 2);  // rows past the chunk are clamped (outputs skipped)
-            blur_load10(img + (long long)reflect101(yy, lv.h) * pitch, xl, lv.w, b[g]);
-        }
+        for (int g = 0; g < kBlurG; g++) stage(g, min(y + g + 3, yb + 2));
+        wave_sync();
+#pragma unroll
+        for (int g = 0; g < kBlurG; g++) patch(g);
+        wave_sync();
 #pragma unroll
         for (int g = 0; g < kBlurG; g++) {
 #pragma unroll
             for (int k = 0; k < 6; k++)
 #pragma unroll
                 for (int i = 0; i < 4; i++) r[k][i] = r[k + 1][i];
-            blur_rowsum4(b[g], r[6]);
+            rowsum(g, r[6]);
             const int yo = y + g;
             if (!lane_on || yo >= yb) continue;
             uint32_t packed = 0;
@@ -947,12 +1007,13 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
                 packed |= (uint32_t)v << (8 * i);
             }
             uint8_t* o = out + (long long)yo * lv.pitch + x0;
-            if (x0 + 4 <= lv.w) {
+            if (x0 + 4 <= w) {
                 *(uint32_t*)o = packed;
             } else {
-                for (int i = 0; i < 4 && x0 + i < lv.w; i++) o[i] = (uint8_t)(packed >> (8 * i));
+                for (int i = 0; i < 4 && x0 + i < w; i++) o[i] = (uint8_t)(packed >> (8 * i));
             }
         }
+        wave_sync();
     }
 }
 
@@ -974,13 +1035,16 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
         for (int l = 0; l < ep.L; l++) tot += cnt[l];
         out_counts[f] = tot;
     }
-    int l = 0;
-    while (l + 1 < ep.L && g >= levels[l + 1].kp_off) l++;
-    const LevelDesc& lv = levels[l];
-    const int k = g - lv.kp_off;
-    if (k >= cnt[l]) return;
+    const int l = level_of(ep.kp_off, ep.L, g);
+    const int k = g - ep.kp_off[l];
+    int cl[kMaxLevels];
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;  // independent loads
+    if (k >= cl[l]) return;
     int outidx = k;
-    for (int q = 0; q < l; q++) outidx += cnt[q];
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; q++) outidx += q < l ? cl[q] : 0;
+    const LevelDesc& lv = levels[l];
     const uint32_t kk = lvkey[(long long)f * ep.kp_per_frame + g];
     const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF), resp = (int)(kk >> 24);
     const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;

@@ -65,6 +65,17 @@ struct ExtractParams {
     long long pyr_frame_bytes;
     long long blur_frame_bytes;
     int umax[16];
+    int kp_off[kMaxLevels + 1];      // level l's octree output slots start (kp_off[L] = kp_per_frame)
+    int bjob_begin[kMaxLevels + 1];  // blur strip jobs prefix
 };
+
+/* level containing index g of a per-level prefix table (no dependent loads: unrolled compares
+ * against kernel-argument values) */
+__host__ __device__ inline int level_of(const int* begin, int L, int g) {
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxLevels; k++) l += (k < L && g >= begin[k]) ? 1 : 0;
+    return l;
+}
 
 }  // namespace orbamd
