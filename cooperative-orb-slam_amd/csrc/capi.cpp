@@ -259,7 +259,11 @@ struct Geometry {
         ep.min_th = T.min_th;
         ep.pyr_frame_bytes = align_up(pyr_off, 256);
         ep.blur_frame_bytes = align_up(blur_off, 256);
-        for (int v = 0; v < 16; v++) ep.umax[v] = T.umax[v];
+        ep.umax_packed = 0;
+        for (int v = 0; v < 16; v++) {
+            ep.umax[v] = T.umax[v];
+            ep.umax_packed |= (unsigned long long)(T.umax[v] & 15) << (4 * v);
+        }
         // blur tiles (64 x 16)
         tile_begin.assign(L + 1, 0);
         for (int l = 0; l < L; l++)
@@ -346,7 +350,7 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
     const size_t B = (size_t)h->max_batch;
     if (h->pyr.ensure(B * ep.pyr_frame_bytes) || h->blur.ensure(B * ep.blur_frame_bytes) ||
         h->cellkey.ensure(B * ep.keys_per_frame * 4) || h->cellcnt.ensure(B * ep.ncells * 4) ||
-        h->lvkey.ensure(B * ep.kp_per_frame * 4) || h->lvcnt.ensure(B * ep.L * 4) ||
+        h->lvkey.ensure(B * ep.kp_per_frame * 4) || h->lvcnt.ensure((B * ep.L + kMaxLevels) * 4) ||
         h->gscratch.ensure(B * (size_t)ep.keys_per_frame * 8) || h->err.ensure(256))
         return ORBX_EDEVICE;
     if (h->geo.lds_bytes > 64 * 1024 && !h->lds_attr_set) {

@@ -37,6 +37,20 @@ static inline int iclamp_host(int v, int lo, int hi) { return v < lo ? lo : (v >
 /* n consecutive little-endian dwords starting at an arbitrary byte address, from n+1 aligned
  * dword loads + v_alignbyte (rows of the input frame need not be 4-byte aligned). Reads only
  * dwords that overlap the span, so it never touches memory past the span's last byte's dword. */
+/* dword of bytes [c, c+4) of a row whose valid bytes are [0, w): two aligned dword loads,
+ * addresses clamped into the row's valid dwords (always issued, never out of bounds); bytes
+ * outside [0, w) come back as garbage and must be overwritten by the caller. */
+__device__ __forceinline__ uint32_t load_row_u32_clamped(const uint8_t* row, int c, int w) {
+    const uintptr_t lo = (uintptr_t)row & ~(uintptr_t)3;
+    const uintptr_t hi = ((uintptr_t)row + (uintptr_t)(w - 1)) & ~(uintptr_t)3;
+    const intptr_t a = (intptr_t)row + c;
+    uintptr_t a0 = (uintptr_t)a & ~(uintptr_t)3;
+    a0 = a0 < lo ? lo : (a0 > hi ? hi : a0);
+    uintptr_t a1 = a0 + 4 > hi ? hi : a0 + 4;
+    const uint32_t w0 = *(const uint32_t*)a0, w1 = *(const uint32_t*)a1;
+    return __builtin_amdgcn_alignbyte(w1, w0, (unsigned)(a & 3));
+}
+
 template <int N>
 __device__ __forceinline__ void load_u32_unaligned(const uint8_t* p, uint32_t out[N]) {
     const uintptr_t a = (uintptr_t)p;
@@ -126,21 +140,18 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
         constexpr int kPer = (kRsH * (kRsW / 4) + 255) / 256;
         uint32_t v[kPer];
         int slot[kPer];
+        // unconditional loads (row and dword clamped into the source window), stores masked
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const int i = tid + k * 256;
             const int r = i / (kRsW / 4), d = i - r * (kRsW / 4);
-            slot[k] = -1;
-            v[k] = 0;
-            if (r < nrows) {
-                const uintptr_t rb = (uintptr_t)(S + (long long)(yb + r) * src_pitch + sx_lo);
-                const uintptr_t ab = rb & ~(uintptr_t)3;
-                const int span = (int)(rb - ab) + (sx_hi - sx_lo + 1);
-                if (4 * d < span) {
-                    v[k] = *(const uint32_t*)(ab + 4 * d);
-                    slot[k] = r * kRsW + 4 * d;
-                }
-            }
+            const int rr = min(r, nrows - 1);
+            const uintptr_t rb = (uintptr_t)(S + (long long)(yb + rr) * src_pitch + sx_lo);
+            const uintptr_t ab = rb & ~(uintptr_t)3;
+            const int span = (int)(rb - ab) + (sx_hi - sx_lo + 1);
+            const int dmax = (span - 1) >> 2;
+            v[k] = *(const uint32_t*)(ab + 4 * (d < dmax ? d : dmax));
+            slot[k] = (r < nrows && d <= dmax) ? r * kRsW + 4 * d : -1;
         }
 #pragma unroll
         for (int k = 0; k < kPer; k++)
@@ -354,15 +365,11 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
         const bool on = lane < rpp * D;
         constexpr int kMaxPass = 24;  // ROI rows <= 72, >= 3 rows per pass
         uint32_t v[kMaxPass];
+        const int ldc = on ? ld : 0;
 #pragma unroll
         for (int k = 0; k < kMaxPass; k++) {
-            const int r = k * rpp + lr;
-            v[k] = 0u;
-            if (on && r < c.h) {
-                uint32_t t[1];
-                load_u32_unaligned<1>(src + (long long)r * pitch + 4 * ld, t);
-                v[k] = t[0];
-            }
+            const int r = min(k * rpp + lr, c.h - 1);  // clamped: loads always valid, issued back to back
+            v[k] = load_row_u32_clamped(img + (long long)(c.y0 + r) * pitch, c.x0 + 4 * ldc, lv.w);
         }
 #pragma unroll
         for (int k = 0; k < kMaxPass; k++) {
@@ -928,28 +935,15 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     auto stage = [&](int k, int yy) {
         const uint8_t* row = img + (long long)reflect101(yy, h) * pitch;
         uint8_t* dstrow = s_rows[wave][k];
-#pragma unroll
-        for (int part = 0; part < 2; part++) {
-            const int i = lane + part * 64;
-            const int c = seg0 + 4 * i;
-            if (i < kBlurSeg / 4 && c + 3 >= 0 && c < w && c < need_hi) {
-                uint32_t v;
-                if (c >= 0 && c + 4 <= w) {
-                    uint32_t t[1];
-                    load_u32_unaligned<1>(row + c, t);  // 4 bytes after: inside the row or its pitch
-                    v = t[0];
-                } else {
-                    v = 0;
-                    for (int b = 0; b < 4; b++)
-                        if (c + b >= 0 && c + b < w) v |= (uint32_t)row[c + b] << (8 * b);
-                }
-                ((uint32_t*)dstrow)[i] = v;
-            }
-        }
+        // 66 dwords per segment: lanes 0..63 and lanes 0..1 again; loads unconditional
+        const uint32_t v0 = load_row_u32_clamped(row, seg0 + 4 * lane, w);
+        const uint32_t v1 = load_row_u32_clamped(row, seg0 + 4 * (lane + 64), w);
+        ((uint32_t*)dstrow)[lane] = v0;
+        if (lane < kBlurSeg / 4 - 64) ((uint32_t*)dstrow)[lane + 64] = v1;
     };
     auto patch = [&](int k) {
         uint8_t* dstrow = s_rows[wave][k];
-        // REFLECT_101 halo: column -1-q <- 1+q (left strip), column w+q <- w-2-q (right)
+        // REFLECT_101 halo over the garbage bytes: column -1-q <- 1+q, column w+q <- w-2-q
         if (lane < 3) {
             const int q = lane;
             if (sx == 0) dstrow[(-1 - q) - seg0] = dstrow[(1 + q) - seg0];
@@ -1029,21 +1023,29 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = blockIdx.x * 4 + wave, f = blockIdx.y;
     if (g >= ep.kp_per_frame) return;
+    // per-level counts of this frame: kMaxLevels unconditional loads (lvcnt is padded by
+    // kMaxLevels ints), issued together; entries >= L masked
     const int* cnt = lvcnt + f * ep.L;
+    int cl[kMaxLevels];
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; q++) cl[q] = cnt[q];
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cl[q] : 0;
     if (g == 0 && lane == 0) {
         int tot = 0;
-        for (int l = 0; l < ep.L; l++) tot += cnt[l];
+#pragma unroll
+        for (int q = 0; q < kMaxLevels; q++) tot += cl[q];
         out_counts[f] = tot;
     }
     const int l = level_of(ep.kp_off, ep.L, g);
     const int k = g - ep.kp_off[l];
-    int cl[kMaxLevels];
+    int mycnt = 0, outidx = k;
 #pragma unroll
-    for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;  // independent loads
-    if (k >= cl[l]) return;
-    int outidx = k;
-#pragma unroll
-    for (int q = 0; q < kMaxLevels; q++) outidx += q < l ? cl[q] : 0;
+    for (int q = 0; q < kMaxLevels; q++) {
+        mycnt = q == l ? cl[q] : mycnt;
+        outidx += q < l ? cl[q] : 0;
+    }
+    if (k >= mycnt) return;
     const LevelDesc& lv = levels[l];
     const uint32_t kk = lvkey[(long long)f * ep.kp_per_frame + g];
     const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF), resp = (int)(kk >> 24);
@@ -1052,23 +1054,29 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     // IC_Angle (ORBextractor.cc:77-104): lanes = columns u, two half-waves split the rows
     int m10 = 0, m01 = 0;
     {
-        const int u = (lane & 31) - 15;
-        const int vbeg = (lane < 32) ? -15 : 1;  // half 0: v = -15..0, half 1: v = 1..15 (16th row masked)
-        if ((lane & 31) < 31) {
-            const uint8_t* col = img + (long long)y * pitch + x + u;
-            const int au = u < 0 ? -u : u;
-            int I[16];
+        // lanes = patch columns u (lane 31/63 duplicate u = 15, masked); half-waves split the rows.
+        // All 16 loads are unconditional and in bounds (keypoints are >= 19 px from the level
+        // border), so they issue back to back; the circular mask is applied afterwards.
+        const int lu = lane & 31;
+        const int u = (lu < 31 ? lu : 30) - 15;
+        const int vbeg = (lane < 32) ? -15 : 1;  // half 0: v = -15..0, half 1: v = 1..15 (+1 masked)
+        const uint8_t* col = img + (long long)y * pitch + x + u;
+        const int au = u < 0 ? -u : u;
+        int I[16];
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const int v = vbeg + k;
-                const int av = v < 0 ? -v : v;
-                I[k] = (v <= 15 && au <= ep.umax[av < 16 ? av : 15]) ? col[(long long)v * pitch] : 0;
-            }
+        for (int k = 0; k < 16; k++) {
+            const int v = min(vbeg + k, 15);
+            I[k] = col[(long long)v * pitch];
+        }
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                m10 += u * I[k];
-                m01 += (vbeg + k) * I[k];
-            }
+        for (int k = 0; k < 16; k++) {
+            const int v = vbeg + k;
+            const int av = v < 0 ? -v : v;
+            const int um = (int)((ep.umax_packed >> (4 * (av & 15))) & 15);
+            const bool use = lu < 31 && v <= 15 && au <= um;
+            const int Iv = use ? I[k] : 0;
+            m10 += u * Iv;
+            m01 += v * Iv;
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {

@@ -94,12 +94,28 @@ __device__ __forceinline__ void tri_bf_body(const PairSrc& s, const MatchGeom& g
     for (int t0 = 0; t0 < s.n2; t0 += kTile) {
         const int nt = min(kTile, s.n2 - t0);
         __syncthreads();
-        for (int j = tid; j < nt; j += 256) {
-            const uint4* cd = (const uint4*)(s.desc2 + (long long)(t0 + j) * 32);
-            s_desc[2 * j] = cd[0];
-            s_desc[2 * j + 1] = cd[1];
-            const orbx_kp kp = s.kps2[t0 + j];
-            s_x[j] = kp.x; s_y[j] = kp.y; s_oct[j] = kp.octave;
+        {
+            // kTile/256 candidates per thread: unconditional clamped loads, masked LDS stores
+            constexpr int kPerT = kTile / 256;
+            uint4 d0[kPerT], d1[kPerT];
+            orbx_kp kp[kPerT];
+#pragma unroll
+            for (int u = 0; u < kPerT; u++) {
+                const int j = min(tid + u * 256, nt - 1);
+                const uint4* cd = (const uint4*)(s.desc2 + (long long)(t0 + j) * 32);
+                d0[u] = cd[0];
+                d1[u] = cd[1];
+                kp[u] = s.kps2[t0 + j];
+            }
+#pragma unroll
+            for (int u = 0; u < kPerT; u++) {
+                const int j = tid + u * 256;
+                if (j < nt) {
+                    s_desc[2 * j] = d0[u];
+                    s_desc[2 * j + 1] = d1[u];
+                    s_x[j] = kp[u].x; s_y[j] = kp[u].y; s_oct[j] = kp[u].octave;
+                }
+            }
         }
         __syncthreads();
         if (active) {

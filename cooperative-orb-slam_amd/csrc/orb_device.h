@@ -65,6 +65,7 @@ struct ExtractParams {
     long long pyr_frame_bytes;
     long long blur_frame_bytes;
     int umax[16];
+    unsigned long long umax_packed;  // umax[v] in bits 4v..4v+3 (all values <= 15)
     int kp_off[kMaxLevels + 1];      // level l's octree output slots start (kp_off[L] = kp_per_frame)
     int bjob_begin[kMaxLevels + 1];  // blur strip jobs prefix
 };

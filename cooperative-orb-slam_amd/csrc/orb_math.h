@@ -40,37 +40,37 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
     return a;
 }
 
-/* glibc 2.35 __sincosf_table[2] (values from libm.so.6 .rodata), fields:
- * sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4 */
-struct SinCosTab {
-    double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
-};
-__device__ __forceinline__ const SinCosTab& sctab(int i) {
-    static const __device__ SinCosTab t[2] = {
-        {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 1.0,
-         -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
-         0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13,
-         0x1.99343027bf8c3p-16},
-        {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -1.0,
-         0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,
-         0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13,
-         -0x1.99343027bf8c3p-16}};
-    return t[i];
-}
-__device__ __forceinline__ float sinf_poly(double xs, double x2, const SinCosTab& p) {
+/* glibc 2.35 __sincosf_table (values read from libm.so.6 .rodata). Table 1 is table 0 with the
+ * cosine coefficients negated and identical sine coefficients, and sign[n&3] = -1 for n&3 in
+ * {1,2}; all constants are immediates (no memory loads on the hot path). */
+#define SC_HPI_INV 0x1.45f306dc9c883p+23
+#define SC_HPI 0x1.921fb54442d18p+0
+#define SC_C0 1.0
+#define SC_C1 -0x1.ffffffd0c621cp-2
+#define SC_S1 -0x1.555545995a603p-3
+#define SC_C2 0x1.55553e1068f19p-5
+#define SC_S2 0x1.1107605230bc4p-7
+#define SC_C3 -0x1.6c087e89a359dp-10
+#define SC_S3 -0x1.994eb3774cf24p-13
+#define SC_C4 0x1.99343027bf8c3p-16
+
+__device__ __forceinline__ float sinf_poly(double xs, double x2) {
     double x3 = __dmul_rn(x2, xs);
-    double a = __fma_rn(x2, p.s3, p.s2);
+    double a = __fma_rn(x2, SC_S3, SC_S2);
     double x5 = __dmul_rn(x3, x2);
-    double s = __fma_rn(x3, p.s1, xs);
+    double s = __fma_rn(x3, SC_S1, xs);
     return __double2float_rn(__fma_rn(a, x5, s));
 }
-__device__ __forceinline__ float cosf_poly(double x2, const SinCosTab& p) {
+/* neg = 1 selects table 1 (cosine coefficients negated) */
+__device__ __forceinline__ float cosf_poly(double x2, bool neg) {
+    const double c0 = neg ? -SC_C0 : SC_C0, c1 = neg ? -SC_C1 : SC_C1, c2 = neg ? -SC_C2 : SC_C2;
+    const double c3 = neg ? -SC_C3 : SC_C3, c4 = neg ? -SC_C4 : SC_C4;
     double x4 = __dmul_rn(x2, x2);
-    double c1 = __fma_rn(x2, p.c1, p.c0);
-    double c2 = __fma_rn(x2, p.c4, p.c3);
+    double t1 = __fma_rn(x2, c1, c0);
+    double t2 = __fma_rn(x2, c4, c3);
     double x6 = __dmul_rn(x2, x4);
-    double c = __fma_rn(x4, p.c2, c1);
-    return __double2float_rn(__fma_rn(c2, x6, c));
+    double c = __fma_rn(x4, c2, t1);
+    return __double2float_rn(__fma_rn(t2, x6, c));
 }
 __device__ __forceinline__ unsigned top12(float y) { return (__float_as_uint(y) >> 20) & 0x7ff; }
 /* valid for |y| < 120 (all ORB angles are in [0, 2*pi]) */
@@ -83,22 +83,23 @@ __device__ __forceinline__ void glibc_sincosf(float y, float* s_out, float* c_ou
             *c_out = 1.0f;
             return;
         }
-        *s_out = sinf_poly(x, x2, sctab(0));
-        *c_out = cosf_poly(x2, sctab(0));
+        *s_out = sinf_poly(x, x2);
+        *c_out = cosf_poly(x2, false);
         return;
     }
-    double r = __dmul_rn(x, sctab(0).hpi_inv);
+    double r = __dmul_rn(x, SC_HPI_INV);
     int n = ((int)r + 0x800000) >> 24;
-    double xr = __fma_rn(-(double)n, sctab(0).hpi, x);
-    const SinCosTab& p = sctab((n & 2) ? 1 : 0);
+    double xr = __fma_rn(-(double)n, SC_HPI, x);
+    const bool neg = (n & 2) != 0;
     double x2 = __dmul_rn(xr, xr);
-    double xs = __dmul_rn(xr, sctab(0).sign[n & 3]);
+    const int q = n & 3;
+    double xs = (q == 1 || q == 2) ? -xr : xr;  // xr * sign[n&3], exact
     if (n & 1) {
-        *s_out = cosf_poly(x2, p);
-        *c_out = sinf_poly(xs, x2, p);
+        *s_out = cosf_poly(x2, neg);
+        *c_out = sinf_poly(xs, x2);
     } else {
-        *s_out = sinf_poly(xs, x2, p);
-        *c_out = cosf_poly(x2, p);
+        *s_out = sinf_poly(xs, x2);
+        *c_out = cosf_poly(x2, neg);
     }
 }
 
