@@ -474,6 +474,13 @@ int orbx_check_error(orbx_handle* h, void* stream) {
     return flag ? ORBX_EDEVICE : 0;
 }
 
+int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, void* stream) {
+    if (!d_in || !d_sin || !d_cos || n < 0) return ORBX_EARG;
+    if (n == 0) return 0;
+    HIPR(launch_sincos_selftest(d_in, d_sin, d_cos, n, (hipStream_t)stream));
+    return 0;
+}
+
 int orbx_profile_enable(orbx_handle* h, int on) {
     if (!h) return ORBX_EARG;
     h->prof_on = on != 0;

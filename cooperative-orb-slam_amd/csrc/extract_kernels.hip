@@ -1124,6 +1124,12 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     }
 }
 
+/* self-test hook: the device restatement of glibc sinf/cosf on an array (tests only) */
+__global__ void k_sincos_selftest(const float* __restrict__ in, float* __restrict__ s, float* __restrict__ c, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) glibc_sincosf(in[i], s + i, c + i);
+}
+
 }  // namespace orbamd
 
 /* ----------------------------------------------------------------------------------- */
@@ -1189,6 +1195,11 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
     const size_t lds = 4 * 4 * (size_t)RP * RH;
     hipLaunchKernelGGL(k_fast_cells2, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
                        cellkey, cellcnt, RP, RH);
+    return hipGetLastError();
+}
+
+hipError_t launch_sincos_selftest(const float* in, float* so, float* co, int n, hipStream_t st) {
+    hipLaunchKernelGGL(k_sincos_selftest, dim3((n + 255) / 256), dim3(256), 0, st, in, so, co, n);
     return hipGetLastError();
 }
 

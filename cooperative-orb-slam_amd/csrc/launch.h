@@ -23,6 +23,7 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
                               const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                               uint32_t* cellkey, int* cellcnt, int RP, int RH, int nframes, hipStream_t st);
 hipError_t octree_setup(int lds_bytes);
+hipError_t launch_sincos_selftest(const float* in, float* so, float* co, int n, hipStream_t st);
 hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                          const uint32_t* cellkey, const int* cellcnt, uint32_t* lvkey, int* lvcnt,
                          uint8_t* gscratch, long long gscratch_frame_bytes, int NC, int KL, int lds_bytes,

@@ -71,6 +71,7 @@ SIGNATURES = {
     "orbx_synth_frame": (_I, [_I, _I, _I, _I, _P]),
     "orbx_synth_frames": (_I, [_I, _I, _I, _I, _I, _P]),
     "orbx_check_error": (_I, [_P, _P]),
+    "orbx_selftest_sincosf": (_I, [_P, _P, _P, _I, _P]),
     "orbx_profile_enable": (_I, [_P, _I]),
     "orbx_profile_read": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_I)]),
     "orbx_version": (C.c_char_p, []),

@@ -212,6 +212,10 @@ int orbx_synth_frames(int agent, int t0, int count, int width, int height, uint8
 int orbx_profile_enable(orbx_handle* h, int on);
 int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls);
 
+/* Test hook: the device's restatement of glibc sinf/cosf (used by computeOrbDescriptor,
+ * ORBextractor.cc:113) applied to n device floats; lets tests compare against host libm. */
+int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, void* stream);
+
 /* Library/version and device probe. */
 const char* orbx_version(void);
 int orbx_device_count(void);

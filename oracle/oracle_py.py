@@ -47,6 +47,7 @@ _SIG = {
     "oc_gauss7": (None, [_P, _I, _I, _SZ, _P, _SZ]),
     "oc_fast": (_I, [_P, _I, _I, _SZ, _I, _P, _I]),
     "oc_descriptor_distance": (_I, [_P, _P]),
+    "oc_sincosf_batch": (None, [_P, _P, _P, _I]),
     "oc_search_for_triangulation": (_I, [C.POINTER(_View), C.POINTER(_View), _P, _F, _F, _I, _I, _P]),
     "oc_search_by_bow_kf_f": (_I, [C.POINTER(_View), C.POINTER(_View), _F, _I, _P]),
     "oc_search_by_bow_kf_kf": (_I, [C.POINTER(_View), C.POINTER(_View), _F, _I, _P]),
@@ -176,6 +177,14 @@ def gauss_kernel_q8():
 
 def fast_atan2(y, x):
     return load().oc_fast_atan2(y, x)
+
+
+def sincosf(x):
+    x = np.ascontiguousarray(x, np.float32)
+    s = np.empty_like(x)
+    c = np.empty_like(x)
+    load().oc_sincosf_batch(x.ctypes.data, s.ctypes.data, c.ctypes.data, x.size)
+    return s, c
 
 
 def descriptor_distance(a, b):

@@ -7,7 +7,7 @@
  * threshold fallback, ...) so that the GPU's re-formulations are checked against an
  * independent statement. PARITY UNPINNED at the OpenCV boundary (see header).
  *
- * Citations are to /root/reference/ORB_SLAM2/src/*.cc (identical to ORB_SLAM2.1/).
+ * Citations are to files under /root/reference/ORB_SLAM2/src (identical to ORB_SLAM2.1).
  * Build: -O2 -ffp-contract=off (no FMA contraction: the pinned float semantics).
  */
 #include "orb_oracle.h"
@@ -793,6 +793,14 @@ void oc_get_tables(const oc_extractor* e, float* scale, float* inv_scale, float*
         if (nfeat) nfeat[l] = e->nfeat[l];
     }
     if (umax16) for (int v = 0; v <= HALF_PATCH_SIZE; v++) umax16[v] = e->umax[v];
+}
+
+/* host libm sinf/cosf over an array (what computeOrbDescriptor calls, ORBextractor.cc:113) */
+void oc_sincosf_batch(const float* in, float* s, float* c, int n) {
+    for (int i = 0; i < n; i++) {
+        s[i] = sinf(in[i]);
+        c[i] = cosf(in[i]);
+    }
 }
 
 /* ------------------------------------------------------------------- matcher ------ */

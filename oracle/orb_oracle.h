@@ -56,6 +56,8 @@ void oc_gauss7(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst, siz
 /* cv::FAST(img, kps, th, true) on a w x h view: xyr triplets, returns count */
 int oc_fast(const uint8_t* img, int w, int h, size_t step, int threshold, float* xyr, int cap);
 
+void oc_sincosf_batch(const float* in, float* s, float* c, int n);
+
 /* matcher (ORBmatcher.cc) -- host views */
 int oc_descriptor_distance(const uint8_t* a, const uint8_t* b);
 int oc_search_for_triangulation(const orbm_kf_view* kf1, const orbm_kf_view* kf2,
