@@ -122,6 +122,7 @@ struct Geometry {
     int nbjobs = 0;
     int NC = 0, KL = 0, lds_bytes = 0;
     int roi_pitch = 0, roi_rows = 0;  // FAST cell LDS staging (max cell ROI)
+    int max_pass = 1;                 // ROI staging passes (rows per 64-lane dword pass)
     int tiled_ok[kMaxLevels] = {0};   // level's resize fits the LDS-tiled kernel
     DevBuf d_lv, d_cells, d_coef, d_tiles;
 
@@ -247,10 +248,14 @@ struct Geometry {
         }
         roi_pitch = 4;
         roi_rows = 1;
+        max_pass = 1;
         for (const CellDesc& c : cells) {
             roi_pitch = std::max(roi_pitch, (int)align_up(c.w, 4));
             roi_rows = std::max(roi_rows, c.h);
+            const int D = (c.w + 3) / 4, rpp = 64 / D;
+            max_pass = std::max(max_pass, (c.h + rpp - 1) / rpp);
         }
+        if (max_pass > 24) return ORBX_EARG;
         ep.L = L;
         ep.ncells = (int)cells.size();
         ep.keys_per_frame = key_begin;
@@ -388,8 +393,8 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
                                h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), nframes, st));
     else
         HIPR(launch_fast_cells2(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, g.d_cells.as<CellDesc>(),
-                                h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), g.roi_pitch, g.roi_rows, nframes,
-                                st));
+                                h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), g.roi_pitch, g.roi_rows, g.max_pass,
+                                nframes, st));
     if (prof_mark(h, 2, st)) return ORBX_EDEVICE;
     HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                        h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),

@@ -41,14 +41,15 @@ static inline int iclamp_host(int v, int lo, int hi) { return v < lo ? lo : (v >
  * addresses clamped into the row's valid dwords (always issued, never out of bounds); bytes
  * outside [0, w) come back as garbage and must be overwritten by the caller. */
 __device__ __forceinline__ uint32_t load_row_u32_clamped(const uint8_t* row, int c, int w) {
-    const uintptr_t lo = (uintptr_t)row & ~(uintptr_t)3;
-    const uintptr_t hi = ((uintptr_t)row + (uintptr_t)(w - 1)) & ~(uintptr_t)3;
-    const intptr_t a = (intptr_t)row + c;
-    uintptr_t a0 = (uintptr_t)a & ~(uintptr_t)3;
-    a0 = a0 < lo ? lo : (a0 > hi ? hi : a0);
-    uintptr_t a1 = a0 + 4 > hi ? hi : a0 + 4;
-    const uint32_t w0 = *(const uint32_t*)a0, w1 = *(const uint32_t*)a1;
-    return __builtin_amdgcn_alignbyte(w1, w0, (unsigned)(a & 3));
+    // offsets stay relative to `row` (pointer arithmetic keeps the global address space, so
+    // these become global_load_dword, not flat loads)
+    const int mr = (int)((uintptr_t)row & 3);
+    const int lo = -mr, hi = ((mr + w - 1) & ~3) - mr;
+    int o0 = ((mr + c) & ~3) - mr;
+    o0 = o0 < lo ? lo : (o0 > hi ? hi : o0);
+    const int o1 = o0 + 4 > hi ? hi : o0 + 4;
+    const uint32_t w0 = *(const uint32_t*)(row + o0), w1 = *(const uint32_t*)(row + o1);
+    return __builtin_amdgcn_alignbyte(w1, w0, (unsigned)((mr + c) & 3));
 }
 
 template <int N>
@@ -146,11 +147,11 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
             const int i = tid + k * 256;
             const int r = i / (kRsW / 4), d = i - r * (kRsW / 4);
             const int rr = min(r, nrows - 1);
-            const uintptr_t rb = (uintptr_t)(S + (long long)(yb + rr) * src_pitch + sx_lo);
-            const uintptr_t ab = rb & ~(uintptr_t)3;
-            const int span = (int)(rb - ab) + (sx_hi - sx_lo + 1);
+            const uint8_t* rp = S + (long long)(yb + rr) * src_pitch + sx_lo;
+            const int mis = (int)((uintptr_t)rp & 3);
+            const int span = mis + (sx_hi - sx_lo + 1);
             const int dmax = (span - 1) >> 2;
-            v[k] = *(const uint32_t*)(ab + 4 * (d < dmax ? d : dmax));
+            v[k] = *(const uint32_t*)(rp - mis + 4 * (d < dmax ? d : dmax));
             slot[k] = (r < nrows && d <= dmax) ? r * kRsW + 4 * d : -1;
         }
 #pragma unroll
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(
     const int ci = blockIdx.x * 4 + wave;
     if (ci >= ep.ncells) return;  // wave-uniform; no block barriers below
     const CellDesc c = cells[ci];
-    const LevelDesc& lv = levels[c.level];
+    const LevelDesc lv = levels[c.level];
     const uint8_t* img = c.level == 0 ? frames + (long long)f * fstride
                                       : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
     const int pitch = c.level == 0 ? pitch0 : lv.pitch;
@@ -338,6 +339,7 @@ __device__ __forceinline__ bool fast_pretest(const uint8_t* p, int P, int t) {
     return (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
 }
 
+template <int kMaxPass>
 __global__ __launch_bounds__(256) void k_fast_cells2(
     const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
     ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
@@ -352,7 +354,7 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
     uint8_t* str = roi + roi_bytes;
     uint16_t* clist = (uint16_t*)(str + roi_bytes);  // <= roi_bytes entries (band < ROI)
     const CellDesc c = cells[ci];
-    const LevelDesc& lv = levels[c.level];
+    const LevelDesc lv = levels[c.level];
     const uint8_t* img = c.level == 0 ? frames + (long long)f * fstride
                                       : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
     const int pitch = c.level == 0 ? pitch0 : lv.pitch;
@@ -363,8 +365,7 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
         const int rpp = 64 / D;
         const int lr = lane / D, ld = lane - lr * D;
         const bool on = lane < rpp * D;
-        constexpr int kMaxPass = 24;  // ROI rows <= 72, >= 3 rows per pass
-        uint32_t v[kMaxPass];
+        uint32_t v[kMaxPass];  // kMaxPass >= ceil(h / rpp) for every cell (host-chosen)
         const int ldc = on ? ld : 0;
 #pragma unroll
         for (int k = 0; k < kMaxPass; k++) {
@@ -828,7 +829,7 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames
     while (l + 1 < ep.L && t >= tile_begin[l + 1]) l++;
     if (lvcnt[f * ep.L + l] == 0) return;  // level without keypoints is never blurred (:1081)
     t -= tile_begin[l];
-    const LevelDesc& lv = levels[l];
+    const LevelDesc lv = levels[l];
     const int tilesx = (lv.w + 63) / 64;
     const int tx = t % tilesx, ty = t / tilesx;
     const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
@@ -918,7 +919,7 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     const int l = level_of(ep.bjob_begin, ep.L, j);
     j -= ep.bjob_begin[l];
     if (lvcnt[f * ep.L + l] == 0) return;  // a level without keypoints is never blurred (:1081)
-    const LevelDesc& lv = levels[l];
+    const LevelDesc lv = levels[l];
     const int w = lv.w, h = lv.h;
     const int nstrips = (w + 255) / 256;
     const int strip = j % nstrips, chunk = j / nstrips;
@@ -1046,7 +1047,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
         outidx += q < l ? cl[q] : 0;
     }
     if (k >= mycnt) return;
-    const LevelDesc& lv = levels[l];
+    const LevelDesc lv = levels[l];
     const uint32_t kk = lvkey[(long long)f * ep.kp_per_frame + g];
     const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF), resp = (int)(kk >> 24);
     const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
@@ -1190,11 +1191,19 @@ hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch
 
 hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                               const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
-                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int nframes, hipStream_t st) {
+                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int max_pass, int nframes,
+                              hipStream_t st) {
     dim3 grid((ep.ncells + 3) / 4, nframes);
     const size_t lds = 4 * 4 * (size_t)RP * RH;
-    hipLaunchKernelGGL(k_fast_cells2, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
-                       cellkey, cellcnt, RP, RH);
+    if (max_pass <= 8)
+        hipLaunchKernelGGL(k_fast_cells2<8>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
+                           cellkey, cellcnt, RP, RH);
+    else if (max_pass <= 12)
+        hipLaunchKernelGGL(k_fast_cells2<12>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
+                           cellkey, cellcnt, RP, RH);
+    else
+        hipLaunchKernelGGL(k_fast_cells2<24>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
+                           cellkey, cellcnt, RP, RH);
     return hipGetLastError();
 }
 

@@ -21,7 +21,8 @@ hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch
                              uint32_t* cellkey, int* cellcnt, int nframes, hipStream_t st);
 hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                               const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
-                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int nframes, hipStream_t st);
+                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int max_pass, int nframes,
+                              hipStream_t st);
 hipError_t octree_setup(int lds_bytes);
 hipError_t launch_sincos_selftest(const float* in, float* so, float* co, int n, hipStream_t st);
 hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
