@@ -115,10 +115,12 @@ __global__ __launch_bounds__(256) void k_resize_level(
     }
 }
 
-/* Tiled form: a 64 x 16 output tile per workgroup; its source window (<= kRsW x kRsH bytes,
- * checked on the host) is staged in LDS with aligned dword loads, then each thread produces 4
- * rows of one column from LDS. */
-constexpr int kRsTW = 64, kRsTH = 16, kRsW = 144, kRsH = 40;
+/* Tiled form: a 64 x kRsTH output tile per workgroup; its source window (<= kRsW x kRsH
+ * bytes, checked on the host by resize_tile_fits) is staged in LDS with aligned dword loads,
+ * then each thread produces kRsTH/4 rows of one column from LDS. Every table load (window
+ * bounds, xofs/alpha of the thread's column, yofs/beta of its rows) is issued before the
+ * staging loads, so a tile costs two memory round trips (tables, source). */
+constexpr int kRsTW = 64, kRsTH = 32, kRsW = 144, kRsH = 48, kRsRows = kRsTH / 4;
 
 __global__ __launch_bounds__(256) void k_resize_tiled(
     const uint8_t* __restrict__ src, long long src_fstride, int src_pitch, int sw, int sh,
@@ -129,14 +131,26 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
     const int c0 = blockIdx.x * kRsTW, r0 = blockIdx.y * kRsTH;
     const int c1 = min(c0 + kRsTW, dw), r1 = min(r0 + kRsTH, dh);
     const uint8_t* S = src + (long long)blockIdx.z * src_fstride;
-    // source window (uniform): columns [xb, xe], rows [yb, ye]
+    const int tid = threadIdx.x;
+    // this thread's column and rows (indices clamped so every load is unconditional)
+    const int c = c0 + (tid & 63);
+    const int cc = min(c, dw - 1);
+    const int yr0 = r0 + (tid >> 6) * kRsRows;
+    const int sx = xofs[cc];
+    const short2 al = alpha[cc];
+    int syv[kRsRows];
+    short2 bv[kRsRows];
+#pragma unroll
+    for (int k = 0; k < kRsRows; k++) {
+        const int y = min(yr0 + k, dh - 1);
+        syv[k] = yofs[y];
+        bv[k] = beta[y];
+    }
+    // source window (uniform): columns [sx_lo, sx_hi], rows [yb, ye]
     const int sx_lo = xofs[c0];
     const int sx_hi = min(sw - 1, xofs[c1 - 1] + 1);
     const int yb = iclamp(yofs[r0], 0, sh - 1), ye = iclamp(yofs[r1 - 1] + 1, 0, sh - 1);
-    const uintptr_t rowbase0 = (uintptr_t)(S + (long long)yb * src_pitch + sx_lo);
     const int nrows = ye - yb + 1;
-    // aligned dwords per row: cover [sx_lo - mis, sx_hi]
-    const int tid = threadIdx.x;
     {
         constexpr int kPer = (kRsH * (kRsW / 4) + 255) / 256;
         uint32_t v[kPer];
@@ -159,25 +173,23 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
             if (slot[k] >= 0) *(uint32_t*)(&tile[0][0] + slot[k]) = v[k];
     }
     __syncthreads();
-    const int c = c0 + (tid & 63);
     if (c >= c1) return;
     // LDS column of source x in row r: (x - sx_lo) + mis(r), mis = misalignment of that row's start
-    const int sx = xofs[c];
-    int a0 = 2048, a1 = 0;
-    if (c < xmax) { const short2 a = alpha[c]; a0 = a.x; a1 = a.y; }
+    const int a0 = c < xmax ? al.x : 2048, a1 = c < xmax ? al.y : 0;
     const int sxn = c < xmax ? sx + 1 : sx;
+    const int mis0 = (int)((uintptr_t)(S + sx_lo) & 3);
     uint8_t* D = dst + (long long)blockIdx.z * dst_fstride;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int y = r0 + (tid >> 6) * 4 + k;
+    for (int k = 0; k < kRsRows; k++) {
+        const int y = yr0 + k;
         if (y >= r1) break;
-        const int sy = yofs[y];
+        const int sy = syv[k];
         const int q0 = iclamp(sy, 0, sh - 1) - yb, q1 = iclamp(sy + 1, 0, sh - 1) - yb;
-        const int m0 = (int)(((uintptr_t)(S + (long long)(yb + q0) * src_pitch + sx_lo)) & 3);
-        const int m1 = (int)(((uintptr_t)(S + (long long)(yb + q1) * src_pitch + sx_lo)) & 3);
+        const int m0 = (mis0 + (yb + q0) * src_pitch) & 3;
+        const int m1 = (mis0 + (yb + q1) * src_pitch) & 3;
         const int h0 = tile[q0][sx - sx_lo + m0] * a0 + tile[q0][sxn - sx_lo + m0] * a1;
         const int h1 = tile[q1][sx - sx_lo + m1] * a0 + tile[q1][sxn - sx_lo + m1] * a1;
-        const short2 b = beta[y];
+        const short2 b = bv[k];
         int v;
         if (c < simd_end)
             v = ((((h0 >> 4) * b.x) >> 16) + (((h1 >> 4) * b.y) >> 16) + 2) >> 2;
@@ -185,7 +197,6 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
             v = (h0 * b.x + h1 * b.y + (1 << 21)) >> 22;
         D[(long long)y * dst_pitch + c] = (uint8_t)iclamp(v, 0, 255);
     }
-    (void)rowbase0;
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -506,7 +517,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                                                 int* __restrict__ err) {
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int red[8];
-    __shared__ int sh_n, sh_size, sh_jstar, sh_tc, sh_nexp, sh_ndiv;
+    __shared__ int sh_size, sh_jstar, sh_tc, sh_nexp, sh_ndiv;
     const int tid = threadIdx.x;
     const int l = blockIdx.x, f = blockIdx.y;
     const LevelDesc lv = levels[l];
@@ -530,7 +541,6 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
     const uint32_t* ckey = cellkey + (long long)f * ep.keys_per_frame;
     int carry = 0;
     // cell offsets -> reuse dbase/spos as temp (ncells may exceed NC: chunked)
-    if (tid == 0) sh_n = 0;
     __syncthreads();
     int n = 0;
     for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
@@ -898,20 +908,24 @@ __device__ __forceinline__ void blur_rowsum4(const int b[10], int rs[4]) {
         rs[i] = 18 * (b[i] + b[i + 6]) + 34 * (b[i + 1] + b[i + 5]) + 49 * (b[i + 2] + b[i + 4]) + 55 * b[i + 3];
 }
 
-constexpr int kBlurG = 4;     // source rows staged per batch
 constexpr int kBlurSeg = 264; // bytes of one staged row segment: strip (256) + 4 left + 4 right
 
 /* One wave per (frame, level, 256-column strip, 64-row chunk). Each source row segment
- * [sx-4, sx+260) is loaded once per wave with coalesced dword loads into LDS, REFLECT_101
- * halo bytes are patched in LDS by three lanes, and every lane reads its 10 bytes
- * (x0-3 .. x0+6 for its 4 outputs) as three aligned LDS dwords. The vertical 7-row window
- * lives in registers. Arithmetic identical to k_blur. */
+ * [sx-4, sx+260) is fetched once per wave with coalesced dword loads, REFLECT_101 halo bytes are
+ * patched in LDS by three lanes, and every lane reads its 10 bytes (x0-3 .. x0+6 for its 4
+ * outputs) as three aligned LDS dwords. The loads of batch i+1 are issued into registers
+ * before batch i is computed (register double buffering), so memory latency overlaps VALU
+ * work. The vertical 7-row window lives in registers. Arithmetic identical to k_blur. */
+constexpr int kBlurG = 2;  // rows per prefetch batch (A/B on MI355X: 2 > 4 > 8, occupancy-limited)
+
+template <int G>
 __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                      const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                      ExtractParams ep, const LevelDesc* __restrict__ levels,
                                                      const int* __restrict__ job_begin_unused,
                                                      const int* __restrict__ lvcnt) {
-    __shared__ __align__(16) uint8_t s_rows[4][kBlurG][kBlurSeg];
+    constexpr int kSlots = G > 6 ? G : 6;
+    __shared__ __align__(16) uint8_t s_rows[4][kSlots][kBlurSeg];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     int j = blockIdx.x * 4 + wave;
@@ -932,28 +946,28 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     const bool lane_on = x0 < w;
     const int seg0 = sx - 4;                      // segment byte 0 = column seg0
     const int need_hi = min(sx + 256, w) + 3;     // columns [sx-3, need_hi) are read
-    // stage source row yy (reflected) into buffer k: dword i covers columns seg0+4i .. +3
-    auto stage = [&](int k, int yy) {
+    uint8_t(*rows)[kBlurSeg] = s_rows[wave];
+    // dword `lane` (and `lane+64`, lanes 0..1) of source row yy: unconditional clamped loads
+    auto fetch = [&](int yy, uint32_t& v0, uint32_t& v1) {
         const uint8_t* row = img + (long long)reflect101(yy, h) * pitch;
-        uint8_t* dstrow = s_rows[wave][k];
-        // 66 dwords per segment: lanes 0..63 and lanes 0..1 again; loads unconditional
-        const uint32_t v0 = load_row_u32_clamped(row, seg0 + 4 * lane, w);
-        const uint32_t v1 = load_row_u32_clamped(row, seg0 + 4 * (lane + 64), w);
-        ((uint32_t*)dstrow)[lane] = v0;
-        if (lane < kBlurSeg / 4 - 64) ((uint32_t*)dstrow)[lane + 64] = v1;
+        v0 = load_row_u32_clamped(row, seg0 + 4 * lane, w);
+        v1 = load_row_u32_clamped(row, seg0 + 4 * (lane + 64), w);
+    };
+    auto put = [&](int k, uint32_t v0, uint32_t v1) {
+        ((uint32_t*)rows[k])[lane] = v0;
+        if (lane < kBlurSeg / 4 - 64) ((uint32_t*)rows[k])[lane + 64] = v1;
     };
     auto patch = [&](int k) {
-        uint8_t* dstrow = s_rows[wave][k];
         // REFLECT_101 halo over the garbage bytes: column -1-q <- 1+q, column w+q <- w-2-q
         if (lane < 3) {
             const int q = lane;
-            if (sx == 0) dstrow[(-1 - q) - seg0] = dstrow[(1 + q) - seg0];
+            if (sx == 0) rows[k][(-1 - q) - seg0] = rows[k][(1 + q) - seg0];
             const int xr = w + q;
-            if (xr >= sx && xr < need_hi) dstrow[xr - seg0] = dstrow[(w - 2 - q) - seg0];
+            if (xr >= sx && xr < need_hi) rows[k][xr - seg0] = rows[k][(w - 2 - q) - seg0];
         }
     };
     auto rowsum = [&](int k, int rs[4]) {
-        const uint32_t* d = (const uint32_t*)s_rows[wave][k] + lane;
+        const uint32_t* d = (const uint32_t*)rows[k] + lane;
         const uint32_t w0 = d[0], w1 = d[1], w2 = d[2];  // columns x0-4 .. x0+7
         int b[10];
         b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
@@ -964,28 +978,37 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
             rs[i] = 18 * (b[i] + b[i + 6]) + 34 * (b[i + 1] + b[i + 5]) + 49 * (b[i + 2] + b[i + 4]) + 55 * b[i + 3];
     };
     int r[7][4];
-    // prime rows ya-3 .. ya+2 (two batches of 3)
+    uint32_t A0[G], A1[G];
+    {  // prime: rows ya-3 .. ya+2 into window slots 1..6
+        uint32_t P0[6], P1[6];
 #pragma unroll
-    for (int half = 0; half < 2; half++) {
+        for (int k = 0; k < 6; k++) fetch(ya - 3 + k, P0[k], P1[k]);
 #pragma unroll
-        for (int k = 0; k < 3; k++) stage(k, ya - 3 + 3 * half + k);
-        wave_sync();
-#pragma unroll
-        for (int k = 0; k < 3; k++) patch(k);
-        wave_sync();
-#pragma unroll
-        for (int k = 0; k < 3; k++) rowsum(k, r[1 + 3 * half + k]);
-        wave_sync();
+        for (int k = 0; k < 6; k++) put(k, P0[k], P1[k]);
     }
-    for (int y = ya; y < yb; y += kBlurG) {
+    wave_sync();
 #pragma unroll
-        for (int g = 0; g < kBlurG; g++) stage(g, min(y + g + 3, yb + 2));
+    for (int k = 0; k < 6; k++) patch(k);
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 6; k++) rowsum(k, r[1 + k]);
+    wave_sync();
+    // first batch in flight
+#pragma unroll
+    for (int g = 0; g < G; g++) fetch(min(ya + g + 3, yb + 2), A0[g], A1[g]);
+    for (int y = ya; y < yb; y += G) {
+#pragma unroll
+        for (int g = 0; g < G; g++) put(g, A0[g], A1[g]);
         wave_sync();
 #pragma unroll
-        for (int g = 0; g < kBlurG; g++) patch(g);
+        for (int g = 0; g < G; g++) patch(g);
         wave_sync();
+        if (y + G < yb) {  // next batch's loads overlap this batch's arithmetic
 #pragma unroll
-        for (int g = 0; g < kBlurG; g++) {
+            for (int g = 0; g < G; g++) fetch(min(y + G + g + 3, yb + 2), A0[g], A1[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
 #pragma unroll
             for (int k = 0; k < 6; k++)
 #pragma unroll
@@ -1239,7 +1262,7 @@ hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitc
                               const ExtractParams& ep, const LevelDesc* levels, const int* job_begin, int njobs,
                               const int* lvcnt, int nframes, hipStream_t st) {
     dim3 grid((njobs + 3) / 4, nframes);
-    hipLaunchKernelGGL(k_blur_strips, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
+    hipLaunchKernelGGL(k_blur_strips<kBlurG>, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
                        job_begin, lvcnt);
     return hipGetLastError();
 }
