@@ -23,12 +23,6 @@
 
 namespace ORB_SLAM2 {
 
-const int ORBmatcher::TH_HIGH = 100;
-const int ORBmatcher::TH_LOW = 50;
-const int ORBmatcher::HISTO_LENGTH = 30;
-
-ORBmatcher::ORBmatcher(float nnratio, bool checkOri) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
-
 namespace {
 
 void amd_ok(int rc, const char* what) {
