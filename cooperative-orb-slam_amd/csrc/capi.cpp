@@ -111,20 +111,56 @@ struct Tables {
 
 /* Everything that depends on (W, H): host copies + device copies */
 struct Geometry {
+    /* k_pyramid_frames tables for one level (see PyrColGroup in extract_kernels.hip): per 4-column
+     * group the 8-byte source window W and per output a v_perm selector + tap weights; per row
+     * (r0, r1, beta). Returns false if some group's taps do not fit an 8-byte window. */
+    bool build_pyr_tables(LevelDesc& d, const int* xofs, const short* alpha, const int* yofs, const short* beta,
+                          int xmax, int sw, int sh, int dw, int dh) {
+        bool ok = dh <= kPyrMaxRows && (dw + 3) / 4 <= 1024 && sw >= 12;
+        const int AU = (int)align_up(sw, 4);
+        const int gw = (dw + 3) / 4;
+        d.cg_off = (int)ptab.size();
+        for (int gi = 0; gi < gw; gi++) {
+            int e[12] = {0};
+            const int W = std::min(xofs[4 * gi], AU - 8);
+            for (int i = 0; i < 4; i++) {
+                const int x = std::min(4 * gi + i, dw - 1);
+                const int o = xofs[x] - W;
+                const bool two = x < xmax;  // second tap has a non-zero weight
+                if (o < 0 || o > 7 || (two && o + 1 > 7)) ok = false;
+                const int o1 = std::min(o + 1, 7);
+                e[i] = (o & 7) | (0x0c << 8) | (o1 << 16) | (0x0c << 24);
+                const short a0 = two ? alpha[2 * x] : (short)2048, a1 = two ? alpha[2 * x + 1] : (short)0;
+                e[4 + i] = (int)(((uint32_t)(uint16_t)a1 << 16) | (uint16_t)a0);
+            }
+            e[8] = W;
+            e[9] = AU - 4;  // last dword of the row (clamp of the window's third dword)
+            ptab.insert(ptab.end(), e, e + 12);
+        }
+        d.rt_off = (int)ptab.size();
+        for (int y = 0; y < dh; y++) {
+            const int r0 = std::min(std::max(yofs[y], 0), sh - 1), r1 = std::min(std::max(yofs[y] + 1, 0), sh - 1);
+            const int b = (int)(((uint32_t)(uint16_t)beta[2 * y + 1] << 16) | (uint16_t)beta[2 * y]);
+            const int e[4] = {r0, r1, b, 0};
+            ptab.insert(ptab.end(), e, e + 4);
+        }
+        return ok;
+    }
+
     int W = 0, H = 0;
     ExtractParams ep{};
     std::vector<LevelDesc> lv;
     std::vector<CellDesc> cells;
     std::vector<int> coef;
-    std::vector<int> tile_begin;
-    int ntiles = 0;
     std::vector<int> bjob_begin;  // blur strip jobs (256 cols x 64 rows) per level
     int nbjobs = 0;
     int NC = 0, KL = 0, lds_bytes = 0;
     int roi_pitch = 0, roi_rows = 0;  // FAST cell LDS staging (max cell ROI)
     int max_pass = 1;                 // ROI staging passes (rows per 64-lane dword pass)
     int tiled_ok[kMaxLevels] = {0};   // level's resize fits the LDS-tiled kernel
-    DevBuf d_lv, d_cells, d_coef, d_tiles;
+    std::vector<int> ptab;            // k_pyramid_frames column-group / row tables
+    bool frames_ok = true;            // every level fits k_pyramid_frames
+    DevBuf d_lv, d_cells, d_coef, d_ptab;
 
     int build(const Tables& T, int W_, int H_) {
         W = W_;
@@ -133,6 +169,8 @@ struct Geometry {
         lv.assign(L, LevelDesc{});
         cells.clear();
         coef.clear();
+        ptab.clear();
+        frames_ok = true;
         long long pyr_off = 0, blur_off = 0;
         int key_begin = 0, kp_off = 0;
         int maxnode = 0;
@@ -188,6 +226,7 @@ struct Geometry {
                 d.xmax = xmax;
                 d.simd_end = se;
                 tiled_ok[l] = resize_tile_fits(xofs, yofs, sw, sh, dw, dh);
+                frames_ok = frames_ok && build_pyr_tables(d, xofs, alpha, yofs, beta, xmax, sw, sh, dw, dh);
                 // OpenCV switches INTER_LINEAR to INTER_AREA for exact 2x downscales; unsupported
                 if (std::abs(scale_x - 2.0) < 1e-15 && std::abs(scale_y - 2.0) < 1e-15) return ORBX_EARG;
             }
@@ -269,11 +308,6 @@ struct Geometry {
             ep.umax[v] = T.umax[v];
             ep.umax_packed |= (unsigned long long)(T.umax[v] & 15) << (4 * v);
         }
-        // blur tiles (64 x 16)
-        tile_begin.assign(L + 1, 0);
-        for (int l = 0; l < L; l++)
-            tile_begin[l + 1] = tile_begin[l] + ((lv[l].w + 63) / 64) * ((lv[l].h + 15) / 16);
-        ntiles = tile_begin[L];
         bjob_begin.assign(L + 1, 0);
         for (int l = 0; l < L; l++)
             bjob_begin[l + 1] = bjob_begin[l] + ((lv[l].w + 255) / 256) * ((lv[l].h + 63) / 64);
@@ -293,16 +327,16 @@ struct Geometry {
         lds_bytes = node_bytes + 7 * KL;
         // upload
         if (d_lv.ensure(sizeof(LevelDesc) * L) || d_cells.ensure(sizeof(CellDesc) * cells.size()) ||
-            d_coef.ensure(sizeof(int) * std::max<size_t>(coef.size(), 1)) || d_tiles.ensure(sizeof(int) * 2 * (L + 1)))
+            d_coef.ensure(sizeof(int) * std::max<size_t>(coef.size(), 1)) ||
+            d_ptab.ensure(sizeof(int) * std::max<size_t>(ptab.size(), 4)))
             return ORBX_EDEVICE;
         HIPR(hipMemcpy(d_lv.p, lv.data(), sizeof(LevelDesc) * L, hipMemcpyHostToDevice));
         HIPR(hipMemcpy(d_cells.p, cells.data(), sizeof(CellDesc) * cells.size(), hipMemcpyHostToDevice));
         if (!coef.empty()) HIPR(hipMemcpy(d_coef.p, coef.data(), sizeof(int) * coef.size(), hipMemcpyHostToDevice));
-        HIPR(hipMemcpy(d_tiles.p, tile_begin.data(), sizeof(int) * (L + 1), hipMemcpyHostToDevice));
-        HIPR(hipMemcpy(d_tiles.as<int>() + (L + 1), bjob_begin.data(), sizeof(int) * (L + 1), hipMemcpyHostToDevice));
+        if (!ptab.empty()) HIPR(hipMemcpy(d_ptab.p, ptab.data(), sizeof(int) * ptab.size(), hipMemcpyHostToDevice));
         return 0;
     }
-    void release() { d_lv.release(); d_cells.release(); d_coef.release(); d_tiles.release(); }
+    void release() { d_lv.release(); d_cells.release(); d_coef.release(); d_ptab.release(); }
 };
 
 }  // namespace
@@ -313,6 +347,9 @@ struct orbx_handle {
     int device = 0;
     int max_w = 0, max_h = 0, max_batch = 1;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
+    hipStream_t pyr_stream = nullptr;  // high priority: the latency-bound pyramid chain
+    hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_fast0 = nullptr, ev_fast = nullptr, ev_blur = nullptr;
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
     // host-path staging
@@ -365,21 +402,32 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
     return 0;
 }
 
-static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
-                       orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st) {
+static hipError_t create_priority_stream(hipStream_t* s) {
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}
+
+static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fstride, int pitch, int nframes,
+                          hipStream_t st) {
     Geometry& g = h->geo;
     const ExtractParams& ep = g.ep;
-    const LevelDesc* dl = g.d_lv.as<LevelDesc>();
-    HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), st));
-    if (prof_mark(h, 0, st)) return ORBX_EDEVICE;
-    // pyramid levels 1..L-1 (ORBextractor.cc:1107-1132)
+    // pyramid levels 1..L-1 (ORBextractor.cc:1107-1132): whole-frame kernel for large batches of
+    // 4-byte-aligned frames, per-level kernels otherwise
+    const bool aligned = ((uintptr_t)d_frames & 3) == 0 && (fstride & 3) == 0 && (pitch & 3) == 0;
+    if (g.frames_ok && aligned && nframes >= kPyrFramesMinBatch && ep.L > 1) {
+        HIPR(launch_pyramid_frames(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, g.d_lv.as<LevelDesc>(),
+                                   g.d_ptab.as<int>(), nframes, st));
+        return 0;
+    }
     for (int l = 1; l < ep.L; l++) {
         const LevelDesc& s = g.lv[l - 1];
         const LevelDesc& d = g.lv[l];
         const uint8_t* src = l == 1 ? d_frames : h->pyr.as<uint8_t>() + s.pyr_off;
         const long long sfs = l == 1 ? fstride : ep.pyr_frame_bytes;
         const int sp = l == 1 ? pitch : s.pitch;
-        if (g.tiled_ok[l] && !getenv("ORBX_RESIZE_SIMPLE"))
+        if (g.tiled_ok[l])
             HIPR(launch_resize_tiled(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes,
                                      d.pitch, d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes,
                                      st));
@@ -387,25 +435,73 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
             HIPR(launch_resize(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes, d.pitch,
                                d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, st));
     }
+    return 0;
+}
+
+static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstride, int pitch, int cell_lo,
+                       int cell_hi, int nframes, hipStream_t st) {
+    Geometry& g = h->geo;
+    HIPR(launch_fast_cells2(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), g.ep, g.d_lv.as<LevelDesc>(),
+                            g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), g.roi_pitch,
+                            g.roi_rows, g.max_pass, cell_lo, cell_hi, nframes, st));
+    return 0;
+}
+
+/* ORBextractor::operator() for a batch. Dependencies between the stages:
+ *
+ *   pyr  (high priority) : [fork] pyramid(1..L-1) -> [ev_pyr]
+ *   side                 : [fork] FAST(level 0) -> [ev_fast0] ......... [ev_fast] blur(all levels) -> [ev_blur]
+ *   st   (caller)        : memset(err) [fork] ... [ev_pyr] FAST(levels>=1) [ev_fast] [ev_fast0] octree [ev_blur] describe
+ *
+ * FAST on level 0 needs only the input frames, so it fills the GPU around the seven small,
+ * dependent pyramid launches (which get stream priority so they are not starved); the blur
+ * runs beside the octree, whose workgroups are LDS/barrier-bound and leave VALU idle. (The
+ * reference blurs only levels that kept keypoints (ORBextractor.cc:1081); blurring every
+ * level changes no output, since describe reads only levels with keypoints.)
+ * With stage profiling on, everything runs in order on `st` between timing events. */
+static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
+                       orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st) {
+    Geometry& g = h->geo;
+    const ExtractParams& ep = g.ep;
+    const LevelDesc* dl = g.d_lv.as<LevelDesc>();
+    const int ncell0 = g.lv[0].ncells;
+    HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), st));
+    const bool serial = h->prof_on;
+    hipStream_t sd = serial ? st : h->side;
+    hipStream_t sp = serial ? st : h->pyr_stream;
+    if (!serial) {
+        HIPR(hipEventRecord(h->ev_fork, st));
+        HIPR(hipStreamWaitEvent(sp, h->ev_fork, 0));
+        HIPR(hipStreamWaitEvent(sd, h->ev_fork, 0));
+    }
+    if (prof_mark(h, 0, st)) return ORBX_EDEVICE;
+    if (launch_pyramid(h, d_frames, fstride, pitch, nframes, sp)) return ORBX_EDEVICE;
+    if (!serial) {
+        HIPR(hipEventRecord(h->ev_pyr, sp));
+        if (launch_fast(h, d_frames, fstride, pitch, 0, ncell0, nframes, sd)) return ORBX_EDEVICE;
+        HIPR(hipEventRecord(h->ev_fast0, sd));
+        HIPR(hipStreamWaitEvent(st, h->ev_pyr, 0));
+    }
     if (prof_mark(h, 1, st)) return ORBX_EDEVICE;
-    if (getenv("ORBX_FAST_DENSE"))
-        HIPR(launch_fast_cells(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, g.d_cells.as<CellDesc>(),
-                               h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), nframes, st));
-    else
-        HIPR(launch_fast_cells2(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, g.d_cells.as<CellDesc>(),
-                                h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), g.roi_pitch, g.roi_rows, g.max_pass,
-                                nframes, st));
+    if (launch_fast(h, d_frames, fstride, pitch, serial ? 0 : ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
+    if (!serial) {
+        HIPR(hipEventRecord(h->ev_fast, st));
+        HIPR(hipStreamWaitEvent(sd, h->ev_fast, 0));
+        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                                nullptr, g.nbjobs, nullptr, nframes, sd));
+        HIPR(hipEventRecord(h->ev_blur, sd));
+        HIPR(hipStreamWaitEvent(st, h->ev_fast0, 0));
+    }
     if (prof_mark(h, 2, st)) return ORBX_EDEVICE;
     HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                        h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
                        (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, h->err.as<int>(), nframes, st));
     if (prof_mark(h, 3, st)) return ORBX_EDEVICE;
-    if (getenv("ORBX_BLUR_TILES"))
-        HIPR(launch_blur(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                         g.d_tiles.as<int>(), g.ntiles, h->lvcnt.as<int>(), nframes, st));
-    else
+    if (serial)
         HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                                g.d_tiles.as<int>() + (ep.L + 1), g.nbjobs, h->lvcnt.as<int>(), nframes, st));
+                                nullptr, g.nbjobs, nullptr, nframes, st));
+    else
+        HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     if (prof_mark(h, 4, st)) return ORBX_EDEVICE;
     HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                          h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride, nframes,
@@ -444,8 +540,15 @@ int orbx_create(const orbx_params* p, int device, int max_width, int max_height,
     h->max_w = max_width;
     h->max_h = max_height;
     h->max_batch = max_batch;
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete h;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
+        create_priority_stream(&h->pyr_stream) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_fast0, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_fast, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_blur, hipEventDisableTiming) != hipSuccess) {
+        orbx_destroy(h);
         return ORBX_EDEVICE;
     }
     int rc = ensure_geometry(h, max_width, max_height, 1);
@@ -461,11 +564,17 @@ void orbx_destroy(orbx_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->pyr_stream) (void)hipStreamSynchronize(h->pyr_stream);
     for (DevBuf* b : {&h->pyr, &h->blur, &h->cellkey, &h->cellcnt, &h->lvkey, &h->lvcnt, &h->gscratch, &h->err,
                       &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt})
         b->release();
     h->geo.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->side) (void)hipStreamDestroy(h->side);
+    if (h->pyr_stream) (void)hipStreamDestroy(h->pyr_stream);
+    for (hipEvent_t e : {h->ev_fork, h->ev_pyr, h->ev_fast0, h->ev_fast, h->ev_blur})
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
     delete h;
 }

@@ -2,12 +2,14 @@
  * extract_kernels.hip -- gfx950 kernels for ORBextractor::operator() (ORBextractor.cc:1043-1105).
  *
  * One launch per stage over a whole batch of frames (grid.y / grid.z = frame):
- *   k_resize_level   ComputePyramid, one launch per level 1..L-1      (ORBextractor.cc:1107-1132)
- *   k_fast_cells     per-cell cv::FAST + 3x3 NMS + threshold fallback (ORBextractor.cc:789-829)
+ *   k_resize_tiled   ComputePyramid, one launch per level 1..L-1      (ORBextractor.cc:1107-1132)
+ *                    (k_resize_level: untiled form for windows that do not fit the LDS tile)
+ *   k_fast_cells2    per-cell cv::FAST + 3x3 NMS + threshold fallback (ORBextractor.cc:789-829)
  *   k_octree         DistributeOctTree, one workgroup per (frame,level) (ORBextractor.cc:539-763)
- *   k_blur           GaussianBlur 7x7 sigma 2 REFLECT_101 per level   (ORBextractor.cc:1085-1086)
+ *   k_blur_strips    GaussianBlur 7x7 sigma 2 REFLECT_101 per level   (ORBextractor.cc:1085-1086)
  *   k_describe       IC_Angle + rBRIEF + output assembly, one wave per keypoint
  *                    (ORBextractor.cc:77-147, 851-852, 1075-1104)
+ * capi.cpp runs them as a fork/join graph on two streams (DESIGN.md "Schedule").
  * All of it is integer/byte work bounded by HBM/LDS and VALU issue; no MFMA.
  * Exact-semantics notes live in DESIGN.md "Pinned semantics".
  */
@@ -32,6 +34,8 @@ __device__ __forceinline__ int lane_prefix(unsigned long long mask) {
 }
 
 __device__ __forceinline__ int iclamp(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+typedef short short2v __attribute__((ext_vector_type(2)));
 static inline int iclamp_host(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 /* n consecutive little-endian dwords starting at an arbitrary byte address, from n+1 aligned
@@ -199,6 +203,102 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
     }
 }
 
+/* Whole-pyramid form: one 1024-thread workgroup per frame builds levels 1..L-1 in order
+ * (level l+1 is read back from L2 right after this CU wrote level l; a workgroup barrier
+ * separates the levels). A batch of >= 256 frames fills every CU with equal work, and the
+ * seven dependent per-level launches (each too small to hide its own latency) become one.
+ *
+ * Per level each thread owns one 4-column output group (column table in registers) and walks
+ * rows. For a group the host precomputed (PyrColGroup): the 8-byte source window start W
+ * (relative to the row; all 4 outputs' taps lie in [W, W+8)), per output a v_perm selector
+ * that extracts the tap pair as two u16 lanes, and the tap weights as a short2 (alpha, with
+ * (2048, 0) past xmax). Horizontal = one v_dot2 per output and source row; vertical = the
+ * SSE2 VResizeLinearVec_32s8u formula, scalar FixedPtCast for x >= simd_end (as k_resize_*).
+ * Rows' (r0, r1, beta) come from an LDS copy of the level's row table. */
+struct PyrColGroup {
+    int sel[4];
+    int alpha[4];  // short2 bit patterns
+    int W;
+    int pad[3];
+};
+static_assert(sizeof(PyrColGroup) == 48, "PyrColGroup layout");
+
+template <int U>
+__global__ __launch_bounds__(1024) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
+                                                         int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
+                                                         const LevelDesc* __restrict__ levels,
+                                                         const int* __restrict__ ptab) {
+    __shared__ int4 s_rt[kPyrMaxRows];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    uint8_t* P = pyr + (long long)f * ep.pyr_frame_bytes;
+    for (int l = 1; l < ep.L; l++) {
+        const LevelDesc sv = levels[l - 1];
+        const LevelDesc lv = levels[l];
+        const uint8_t* src = l == 1 ? frames + (long long)f * fstride : P + sv.pyr_off;
+        const int sp = l == 1 ? pitch0 : sv.pitch;
+        uint8_t* dst = P + lv.pyr_off;
+        const int dh = lv.h;
+        const int4* rt = (const int4*)(ptab + lv.rt_off);
+        for (int i = tid; i < dh; i += 1024) s_rt[i] = rt[i];
+        const int gw = (lv.w + 3) >> 2;
+        const int R = 1024 / gw;  // rows per pass
+        const int ry = tid / gw, xg = tid - ry * gw;
+        const PyrColGroup cg = ((const PyrColGroup*)(ptab + lv.cg_off))[min(xg, gw - 1)];
+        const int A = cg.W & ~3, k = cg.W & 3;
+        const int x0 = 4 * xg;
+        const bool tail = x0 + 3 >= lv.simd_end;
+        __syncthreads();
+        if (ry < R) {
+            for (int y0 = ry; y0 < dh; y0 += U * R) {
+                uint32_t w[U][2][3];
+                int4 rr[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    rr[u] = s_rt[min(y0 + u * R, dh - 1)];
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const unsigned off = (unsigned)((q ? rr[u].y : rr[u].x) * sp + A);
+                        const uint2 lo = *(const uint2*)(src + off);
+                        w[u][q][0] = lo.x;
+                        w[u][q][1] = lo.y;
+                        w[u][q][2] = *(const uint32_t*)(src + min(off + 8u, (unsigned)((q ? rr[u].y : rr[u].x) * sp + cg.pad[0])));
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int y = y0 + u * R;
+                    if (y >= dh) break;
+                    const short2 b = __builtin_bit_cast(short2, rr[u].z);
+                    int h[2][4];
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const uint32_t lo = __builtin_amdgcn_alignbyte(w[u][q][1], w[u][q][0], k);
+                        const uint32_t hi = __builtin_amdgcn_alignbyte(w[u][q][2], w[u][q][1], k);
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const uint32_t pr = __builtin_amdgcn_perm(hi, lo, cg.sel[i]);
+                            h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
+                                                             __builtin_bit_cast(short2v, cg.alpha[i]), 0, false);
+                        }
+                    }
+                    uint32_t packed = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        int v = ((((h[0][i] >> 4) * b.x) >> 16) + (((h[1][i] >> 4) * b.y) >> 16) + 2) >> 2;
+                        if (tail && x0 + i >= lv.simd_end) v = (h[0][i] * b.x + h[1][i] * b.y + (1 << 21)) >> 22;
+                        packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
+                    }
+                    if (xg < gw) *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 /* ----------------------------------------------------------------------------------- */
 /* FAST-9/16 "strength": S = max over the 16 cyclic 9-arcs of min(v-ring) or min(ring-v). */
 /* A pixel is a cv::FAST corner at threshold t iff S > t, and then cornerScore<16> = S-1  */
@@ -259,82 +359,6 @@ __device__ __forceinline__ bool fast_survivor(const uint8_t* s, int P, int t) {
     return sc > 0;
 }
 
-/* One wave per FAST cell (4 cells per 256-thread workgroup). ROI staged in LDS; band
- * pixels are visited in row-major order in 64-lane chunks so ballot+mbcnt reproduce the
- * reference's emission order (ORBextractor.cc:820-825). */
-__global__ __launch_bounds__(256) void k_fast_cells(
-    const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
-    ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
-    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt) {
-    __shared__ uint8_t s_roi[4][kRoiMax * kRoiPitch];
-    __shared__ uint8_t s_str[4][kRoiMax * kRoiPitch];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int f = blockIdx.y;
-    const int ci = blockIdx.x * 4 + wave;
-    if (ci >= ep.ncells) return;  // wave-uniform; no block barriers below
-    const CellDesc c = cells[ci];
-    const LevelDesc lv = levels[c.level];
-    const uint8_t* img = c.level == 0 ? frames + (long long)f * fstride
-                                      : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
-    const int pitch = c.level == 0 ? pitch0 : lv.pitch;
-    uint8_t* roi = s_roi[wave];
-    uint8_t* str = s_str[wave];
-    const int P = kRoiPitch;
-    // stage ROI (rows of c.w bytes) and clear the strength buffer
-    for (int idx = lane; idx < c.w * c.h; idx += 64) {
-        const int r = idx / c.w, col = idx - r * c.w;
-        roi[r * P + col] = img[(long long)(c.y0 + r) * pitch + c.x0 + col];
-    }
-    for (int idx = lane; idx < (kRoiMax * kRoiPitch) / 4; idx += 64) ((uint32_t*)str)[idx] = 0u;
-    wave_sync();
-    const int bw = c.w - 6, bh = c.h - 6;
-    int total = 0;
-    if (bw > 0 && bh > 0) {
-        const int rpi = 64 / bw;  // band rows per 64-lane chunk
-        const int lr = lane / bw, lc = lane - lr * bw;
-        const bool lane_ok = lane < rpi * bw;
-        for (int r0 = 0; r0 < bh; r0 += rpi) {
-            const int rr = r0 + lr;
-            if (lane_ok && rr < bh) {
-                const int o = (rr + 3) * P + lc + 3;
-                str[o] = (uint8_t)fast_strength(roi + o, P);
-            }
-        }
-        wave_sync();
-        // pass 1: survivors at iniThFAST; if none, the cell falls back to minThFAST
-        int t = ep.ini_th;
-        int cnt = 0;
-        for (int r0 = 0; r0 < bh; r0 += rpi) {
-            const int rr = r0 + lr;
-            bool keep = false;
-            if (lane_ok && rr < bh) keep = fast_survivor(str + (rr + 3) * P + lc + 3, P, t);
-            cnt += __popcll(__ballot(keep));
-        }
-        if (cnt == 0) t = ep.min_th;
-        // pass 2: emit in row-major order
-        uint32_t* out = cellkey + (long long)f * ep.keys_per_frame + c.slot;
-        for (int r0 = 0; r0 < bh; r0 += rpi) {
-            const int rr = r0 + lr;
-            bool keep = false;
-            int sc = 0;
-            if (lane_ok && rr < bh) {
-                const int o = (rr + 3) * P + lc + 3;
-                keep = fast_survivor(str + o, P, t);
-                sc = str[o] - 1;
-            }
-            const unsigned long long m = __ballot(keep);
-            if (keep) {
-                const int pos = total + lane_prefix(m);
-                const uint32_t xr = (uint32_t)(lc + 3 + c.xoff), yr = (uint32_t)(rr + 3 + c.yoff);
-                if (pos < c.cap) out[pos] = xr | (yr << 12) | ((uint32_t)sc << 24);
-            }
-            total += __popcll(m);
-        }
-        if (total > c.cap) total = c.cap;  // cannot happen: cap >= max NMS survivors
-    }
-    if (lane == 0) cellcnt[(long long)f * ep.ncells + ci] = total;
-}
-
 /* Candidate form (k_fast_cells2): a necessary condition for S > t_lo (any 9-arc contains two
  * cyclically adjacent cardinal ring points 0/4/8/12, so both are brighter or both darker) is
  * tested on every band pixel; survivors are compacted in row-major order with ballot+mbcnt
@@ -354,12 +378,12 @@ template <int kMaxPass>
 __global__ __launch_bounds__(256) void k_fast_cells2(
     const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
     ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
-    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP, int RH) {
+    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP, int RH, int cell_lo, int cell_hi) {
     extern __shared__ __align__(16) uint8_t lds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
-    const int ci = blockIdx.x * 4 + wave;
-    if (ci >= ep.ncells) return;  // wave-uniform; no block barriers in this kernel
+    const int ci = cell_lo + blockIdx.x * 4 + wave;
+    if (ci >= cell_hi) return;  // wave-uniform; no block barriers in this kernel
     const int roi_bytes = RP * RH;
     uint8_t* roi = lds + wave * (4 * roi_bytes);
     uint8_t* str = roi + roi_bytes;
@@ -819,7 +843,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
 
 /* ----------------------------------------------------------------------------------- */
 /* GaussianBlur 7x7, sigma 2, REFLECT_101, 8U fixed point (kernel 18,34,49,55,...; sum  */
-/* 257). 64x16 output tile per workgroup, tiles of all levels of all frames in one grid. */
+/* 257). Row strips of all levels of all frames in one grid.                            */
 /* ----------------------------------------------------------------------------------- */
 __device__ __forceinline__ int reflect101(int p, int n) {
     p = p < 0 ? -p : p;
@@ -827,87 +851,7 @@ __device__ __forceinline__ int reflect101(int p, int n) {
     return p;
 }
 
-__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
-                                              const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                              ExtractParams ep, const LevelDesc* __restrict__ levels,
-                                              const int* __restrict__ tile_begin /* L+1 */,
-                                              const int* __restrict__ lvcnt) {
-    __shared__ uint8_t s_in[22][72];
-    __shared__ int s_row[22][64];
-    const int f = blockIdx.y;
-    int t = blockIdx.x, l = 0;
-    while (l + 1 < ep.L && t >= tile_begin[l + 1]) l++;
-    if (lvcnt[f * ep.L + l] == 0) return;  // level without keypoints is never blurred (:1081)
-    t -= tile_begin[l];
-    const LevelDesc lv = levels[l];
-    const int tilesx = (lv.w + 63) / 64;
-    const int tx = t % tilesx, ty = t / tilesx;
-    const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
-    const int pitch = l == 0 ? pitch0 : lv.pitch;
-    const int gx0 = tx * 64 - 3, gy0 = ty * 16 - 3;
-    for (int idx = threadIdx.x; idx < 22 * 70; idx += 256) {
-        const int r = idx / 70, c = idx - r * 70;
-        const int gy = reflect101(gy0 + r, lv.h), gx = reflect101(gx0 + c, lv.w);
-        s_in[r][c] = img[(long long)gy * pitch + gx];
-    }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < 22 * 64; idx += 256) {
-        const int r = idx >> 6, c = idx & 63;
-        const uint8_t* s = &s_in[r][c];
-        s_row[r][c] = 18 * (s[0] + s[6]) + 34 * (s[1] + s[5]) + 49 * (s[2] + s[4]) + 55 * s[3];
-    }
-    __syncthreads();
-    const int c = threadIdx.x & 63, rb = (threadIdx.x >> 6) * 4;
-    const int gx = tx * 64 + c;
-    uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int r = rb + k;
-        const int gy = ty * 16 + r;
-        if (gx < lv.w && gy < lv.h) {
-            const int s = 55 * s_row[r + 3][c] + 49 * (s_row[r + 2][c] + s_row[r + 4][c]) +
-                          34 * (s_row[r + 1][c] + s_row[r + 5][c]) + 18 * (s_row[r][c] + s_row[r + 6][c]);
-            int v;
-            if (gx < lv.blur_vec_end)  // SSE2 float path == round half to even (exact)
-                v = (s + 0x7FFF + ((s >> 16) & 1)) >> 16;
-            else  // scalar FixedPtCastEx tail
-                v = (s + (1 << 15)) >> 16;
-            out[(long long)gy * lv.pitch + gx] = (uint8_t)(v > 255 ? 255 : v);
-        }
-    }
-}
-
-/* Strip form: one wave per (frame, level, 256-column strip, 64-row chunk); each lane owns 4
- * adjacent output columns, loads 3 dwords per source row, keeps the 7 row sums of the vertical
- * window in registers and writes one dword per output row. Same arithmetic as k_blur. */
 constexpr int kBlurRows = 64;
-
-__device__ __forceinline__ void blur_load10(const uint8_t* row, int x0, int w, int b[10]) {
-    if (x0 >= 4 && x0 + 12 <= w) {
-        uint32_t t[3];
-        load_u32_unaligned<3>(row + x0 - 4, t);
-        const uint32_t w0 = t[0], w1 = t[1], w2 = t[2];
-        b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
-        b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
-        b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
-    } else {
-#pragma unroll
-        for (int j = 0; j < 10; j++) {
-            int x = x0 - 3 + j;
-            x = x < 0 ? -x : x;
-            x = x >= w ? 2 * w - 2 - x : x;
-            x = x < 0 ? 0 : x;  // lanes past the right edge (outputs discarded)
-            b[j] = row[x];
-        }
-    }
-}
-
-__device__ __forceinline__ void blur_rowsum4(const int b[10], int rs[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-        rs[i] = 18 * (b[i] + b[i + 6]) + 34 * (b[i + 1] + b[i + 5]) + 49 * (b[i + 2] + b[i + 4]) + 55 * b[i + 3];
-}
-
 constexpr int kBlurSeg = 264; // bytes of one staged row segment: strip (256) + 4 left + 4 right
 
 /* One wave per (frame, level, 256-column strip, 64-row chunk). Each source row segment
@@ -915,7 +859,9 @@ constexpr int kBlurSeg = 264; // bytes of one staged row segment: strip (256) + 
  * patched in LDS by three lanes, and every lane reads its 10 bytes (x0-3 .. x0+6 for its 4
  * outputs) as three aligned LDS dwords. The loads of batch i+1 are issued into registers
  * before batch i is computed (register double buffering), so memory latency overlaps VALU
- * work. The vertical 7-row window lives in registers. Arithmetic identical to k_blur. */
+ * work. The vertical 7-row window (row sums) lives in registers.
+ * Rounding: columns x < w&~3 take the SSE2 float column path of OpenCV's fixed-point filter,
+ * which equals round-half-to-even of s/2^16; the scalar tail rounds half up. */
 constexpr int kBlurG = 2;  // rows per prefetch batch (A/B on MI355X: 2 > 4 > 8, occupancy-limited)
 
 template <int G>
@@ -932,7 +878,9 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     if (j >= ep.bjob_begin[ep.L]) return;
     const int l = level_of(ep.bjob_begin, ep.L, j);
     j -= ep.bjob_begin[l];
-    if (lvcnt[f * ep.L + l] == 0) return;  // a level without keypoints is never blurred (:1081)
+    // the reference blurs only levels with keypoints (:1081); lvcnt == nullptr blurs every level
+    // (the result of an unused level is never read), so the blur can run before the octree
+    if (lvcnt && lvcnt[f * ep.L + l] == 0) return;
     const LevelDesc lv = levels[l];
     const int w = lv.w, h = lv.h;
     const int nstrips = (w + 255) / 256;
@@ -1176,6 +1124,14 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
     return hipGetLastError();
 }
 
+hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
+                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int nframes,
+                                 hipStream_t st) {
+    hipLaunchKernelGGL(k_pyramid_frames<kPyrU>, dim3(nframes), dim3(1024), 0, st, frames, fstride, pitch0, pyr, ep,
+                       levels, ptab);
+    return hipGetLastError();
+}
+
 hipError_t launch_resize_tiled(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
                                long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
                                int simd_end, int nframes, hipStream_t st) {
@@ -1203,30 +1159,22 @@ int resize_tile_fits(const int* xofs, const int* yofs, int sw, int sh, int dw, i
     return 1;
 }
 
-hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
-                             const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
-                             uint32_t* cellkey, int* cellcnt, int nframes, hipStream_t st) {
-    dim3 grid((ep.ncells + 3) / 4, nframes);
-    hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, ep, levels, cells,
-                       cellkey, cellcnt);
-    return hipGetLastError();
-}
-
 hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                               const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
-                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int max_pass, int nframes,
-                              hipStream_t st) {
-    dim3 grid((ep.ncells + 3) / 4, nframes);
+                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int max_pass, int cell_lo,
+                              int cell_hi, int nframes, hipStream_t st) {
+    if (cell_hi <= cell_lo) return hipSuccess;
+    dim3 grid((cell_hi - cell_lo + 3) / 4, nframes);
     const size_t lds = 4 * 4 * (size_t)RP * RH;
     if (max_pass <= 8)
         hipLaunchKernelGGL(k_fast_cells2<8>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
-                           cellkey, cellcnt, RP, RH);
+                           cellkey, cellcnt, RP, RH, cell_lo, cell_hi);
     else if (max_pass <= 12)
         hipLaunchKernelGGL(k_fast_cells2<12>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
-                           cellkey, cellcnt, RP, RH);
+                           cellkey, cellcnt, RP, RH, cell_lo, cell_hi);
     else
         hipLaunchKernelGGL(k_fast_cells2<24>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
-                           cellkey, cellcnt, RP, RH);
+                           cellkey, cellcnt, RP, RH, cell_lo, cell_hi);
     return hipGetLastError();
 }
 
@@ -1246,15 +1194,6 @@ hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const
     dim3 grid(ep.L, nframes);
     hipLaunchKernelGGL(k_octree, grid, dim3(256), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey, lvcnt,
                        gscratch, gscratch_frame_bytes, NC, KL, err);
-    return hipGetLastError();
-}
-
-hipError_t launch_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
-                       const ExtractParams& ep, const LevelDesc* levels, const int* tile_begin, int ntiles,
-                       const int* lvcnt, int nframes, hipStream_t st) {
-    dim3 grid(ntiles, nframes);
-    hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, tile_begin,
-                       lvcnt);
     return hipGetLastError();
 }
 

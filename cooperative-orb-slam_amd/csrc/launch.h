@@ -12,26 +12,23 @@ namespace orbamd {
 hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
                          long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
                          int simd_end, int nframes, hipStream_t st);
+hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
+                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int nframes,
+                                 hipStream_t st);
 hipError_t launch_resize_tiled(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
                                long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
                                int simd_end, int nframes, hipStream_t st);
 int resize_tile_fits(const int* xofs, const int* yofs, int sw, int sh, int dw, int dh);
-hipError_t launch_fast_cells(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
-                             const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
-                             uint32_t* cellkey, int* cellcnt, int nframes, hipStream_t st);
 hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                               const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
-                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int max_pass, int nframes,
-                              hipStream_t st);
+                              uint32_t* cellkey, int* cellcnt, int RP, int RH, int max_pass, int cell_lo,
+                              int cell_hi, int nframes, hipStream_t st);
 hipError_t octree_setup(int lds_bytes);
 hipError_t launch_sincos_selftest(const float* in, float* so, float* co, int n, hipStream_t st);
 hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                          const uint32_t* cellkey, const int* cellcnt, uint32_t* lvkey, int* lvcnt,
                          uint8_t* gscratch, long long gscratch_frame_bytes, int NC, int KL, int lds_bytes,
                          int* err, int nframes, hipStream_t st);
-hipError_t launch_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
-                       const ExtractParams& ep, const LevelDesc* levels, const int* tile_begin, int ntiles,
-                       const int* lvcnt, int nframes, hipStream_t st);
 hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
                               const ExtractParams& ep, const LevelDesc* levels, const int* job_begin, int njobs,
                               const int* lvcnt, int nframes, hipStream_t st);

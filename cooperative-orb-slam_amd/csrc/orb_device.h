@@ -26,6 +26,9 @@ constexpr int kPatchSize = 31;      // ORBextractor.cc:72
 constexpr int kHalfPatch = 15;      // ORBextractor.cc:73
 constexpr int kRoiMax = 72;         // max FAST cell ROI side (cells are < 60+6 px)
 constexpr int kRoiPitch = 72;
+constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity (levels >= 1)
+constexpr int kPyrU = 4;            // k_pyramid_frames: rows in flight per thread
+constexpr int kPyrFramesMinBatch = 64;  // batches below this use the per-level pyramid kernels
 
 struct LevelDesc {
     int w, h, pitch;
@@ -45,6 +48,7 @@ struct LevelDesc {
     int blur_vec_end;            // w & ~3 (SSE2 column-filter span)
     int xmax, simd_end;          // resize: first column with sx+1>=sw; VResize SSE2 span
     int coef_off;                // offset of this level's resize tables
+    int cg_off, rt_off;          // k_pyramid_frames tables (ints into ptab): column groups, rows
 };
 
 struct CellDesc {

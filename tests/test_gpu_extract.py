@@ -94,3 +94,26 @@ def test_batch_device_matches_host_path():
         ko, do = orc(frames[b])
         _compare(kg, dg, ko, do)
     pipe.close()
+
+
+@pytest.mark.parametrize("W,H,nf", CONFIGS[:3])
+def test_large_batch_whole_frame_pyramid(W, H, nf):
+    """Batches >= kPyrFramesMinBatch (64) build the pyramid with one workgroup per frame
+    (k_pyramid_frames); pyramid levels and keypoints must still match the oracle bit for bit."""
+    torch = pytest.importorskip("torch")
+    B = 64
+    frames = orbamd.synth_frames(5, 3, B, W, H)
+    pipe = orbamd.device.BatchPipeline(torch, W, H, B, nfeatures=nf)
+    fr = torch.from_numpy(frames).cuda()
+    pipe.extract(fr)
+    pipe.check_error()
+    torch.cuda.synchronize()
+    orc = oracle_py.OracleExtractor(nf, 1.2, 8, 20, 7)
+    for b in (0, 37, B - 1):
+        kg, dg, _ = pipe.host_results(b)
+        ko, do = orc(frames[b])
+        _compare(kg, dg, ko, do)
+        for l in range(8):
+            np.testing.assert_array_equal(pipe.ext.pyramid_level(l, frame=b), orc.pyramid(l),
+                                          err_msg="frame %d pyramid level %d" % (b, l))
+    pipe.close()

@@ -15,6 +15,9 @@ for k, v in agg.items():
     w = d.get("SQ_WAVES", 0)
     if not w:
         continue
-    print("%-22s waves %7d cyc/wave %8.0f valu/wave %6.0f vmem/wave %5.1f lds/wave %6.1f wait %.2f waitinst %.2f"
-          % (k[:22], w, 4 * d["SQ_WAVE_CYCLES"] / w, d["SQ_INSTS_VALU"] / w, d["SQ_INSTS_VMEM_RD"] / w,
-             d["SQ_INSTS_LDS"] / w, d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"], d["SQ_WAIT_INST_ANY"] / d["SQ_WAVE_CYCLES"]))
+    g = lambda c: d.get(c, float("nan"))
+    # SQ_WAVE_CYCLES / SQ_BUSY_CYCLES count in quad-cycles on gfx950 (x4)
+    print("%-22s waves %7d cyc/wave %8.0f valu/wave %6.0f valu_total(M) %7.1f vmem/wave %5.1f lds/wave %6.1f wait %.2f waitinst %.2f"
+          % (k[:22], w, 4 * g("SQ_WAVE_CYCLES") / w, g("SQ_INSTS_VALU") / w, g("SQ_INSTS_VALU") / 1e6,
+             g("SQ_INSTS_VMEM_RD") / w, g("SQ_INSTS_LDS") / w, g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES"),
+             g("SQ_WAIT_INST_ANY") / g("SQ_WAVE_CYCLES")))
