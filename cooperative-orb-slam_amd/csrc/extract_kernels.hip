@@ -347,16 +347,16 @@ __device__ __forceinline__ int fast_strength(const uint8_t* p, int P) {
 }
 
 /* NMS survivor test of cv::FAST (FAST_t, nonmax_suppression) at threshold t, on the
- * cell's S buffer (zero outside the detection band [3, rows-3) x [3, cols-3)). */
+ * cell's S buffer (zero outside the detection band [3, rows-3) x [3, cols-3)).
+ * cv::FAST keeps a corner (S > t, score S-1) iff its score is strictly greater than the score of
+ * every neighbouring corner. A neighbour with S_n >= S_c > t is a corner, and one with
+ * S_n < S_c never suppresses, so the test is S_c > t && S_c > 1 && max8(S_n) < S_c. */
 __device__ __forceinline__ bool fast_survivor(const uint8_t* s, int P, int t) {
     const int c = s[0];
-    if (c <= t) return false;
-    const int sc = c - 1;
-    int n;
-#define NB(off) n = s[off]; if (n > t && n - 1 >= sc) return false;
-    NB(-P - 1) NB(-P) NB(-P + 1) NB(-1) NB(1) NB(P - 1) NB(P) NB(P + 1)
-#undef NB
-    return sc > 0;
+    const int n0 = s[-P - 1], n1 = s[-P], n2 = s[-P + 1], n3 = s[-1], n4 = s[1], n5 = s[P - 1], n6 = s[P],
+              n7 = s[P + 1];
+    const int mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
+    return c > t && c > 1 && mx < c;
 }
 
 /* Candidate form (k_fast_cells2): a necessary condition for S > t_lo (any 9-arc contains two
@@ -393,7 +393,6 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
     const uint8_t* img = c.level == 0 ? frames + (long long)f * fstride
                                       : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
     const int pitch = c.level == 0 ? pitch0 : lv.pitch;
-    const uint8_t* src = img + (long long)c.y0 * pitch + c.x0;
     {
         // D dwords per ROI row, 64/D rows per pass; all passes' loads issued before the LDS writes
         const int D = (c.w + 3) >> 2;
@@ -402,16 +401,31 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
         const bool on = lane < rpp * D;
         uint32_t v[kMaxPass];  // kMaxPass >= ceil(h / rpp) for every cell (host-chosen)
         const int ldc = on ? ld : 0;
+        const bool rows_aligned = (((uintptr_t)img | (uintptr_t)pitch) & 3) == 0;  // wave-uniform
+        if (rows_aligned) {
+            // every row starts 4-aligned: one column schedule for all rows (two clamped dwords + alignbyte)
+            const int k = c.x0 & 3;
+            const int lastd = (lv.w - 1) & ~3;
+            const int o0 = min((c.x0 & ~3) + 4 * ldc, lastd), o1 = min(o0 + 4, lastd);
+            const uint8_t* base = img + (long long)c.y0 * pitch;
 #pragma unroll
-        for (int k = 0; k < kMaxPass; k++) {
-            const int r = min(k * rpp + lr, c.h - 1);  // clamped: loads always valid, issued back to back
-            v[k] = load_row_u32_clamped(img + (long long)(c.y0 + r) * pitch, c.x0 + 4 * ldc, lv.w);
+            for (int kk = 0; kk < kMaxPass; kk++) {
+                const unsigned ro = (unsigned)(min(kk * rpp + lr, c.h - 1) * pitch);
+                const uint32_t w0 = *(const uint32_t*)(base + (ro + o0)), w1 = *(const uint32_t*)(base + (ro + o1));
+                v[kk] = __builtin_amdgcn_alignbyte(w1, w0, k);
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < kMaxPass; kk++) {
+                const int r = min(kk * rpp + lr, c.h - 1);  // clamped: loads always valid, issued back to back
+                v[kk] = load_row_u32_clamped(img + (long long)(c.y0 + r) * pitch, c.x0 + 4 * ldc, lv.w);
+            }
         }
 #pragma unroll
-        for (int k = 0; k < kMaxPass; k++) {
-            const int r = k * rpp + lr;
+        for (int kk = 0; kk < kMaxPass; kk++) {
+            const int r = kk * rpp + lr;
             if (on && r < c.h) {
-                ((uint32_t*)(roi + r * RP))[ld] = v[k];
+                ((uint32_t*)(roi + r * RP))[ld] = v[kk];
                 ((uint32_t*)(str + r * RP))[ld] = 0u;
             }
         }
@@ -421,17 +435,79 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
     int total = 0;
     if (bw > 0 && bh > 0) {
         const int t_lo = min(ep.ini_th, ep.min_th);
-        const int rpi = 64 / bw;
-        const int lr = lane / bw, lc = lane - lr * bw;
-        const bool lane_ok = lane < rpi * bw;
         int ncand = 0;
-        for (int r0 = 0; r0 < bh; r0 += rpi) {
-            const int rr = r0 + lr;
-            bool cand = false;
-            if (lane_ok && rr < bh) cand = fast_pretest(roi + (rr + 3) * RP + lc + 3, RP, t_lo);
-            const unsigned long long m = __ballot(cand);
-            if (cand) clist[ncand + lane_prefix(m)] = (uint16_t)(((rr + 3) << 8) | (lc + 3));
-            ncand += __popcll(m);
+        {
+            // SWAR pretest: each lane tests the 4 pixels of one aligned ROI dword (band columns
+            // [3, 3+bw)), as two u16 pairs (pixels 0,2 and 1,3) with packed 16-bit arithmetic.
+            const int G = (bw + 6) >> 2;  // dword groups covering columns [0, bw+3)
+            const int rpc = 64 / G;
+            const int lr = lane / G, j = lane - lr * G;
+            const bool lane_ok = lane < rpc * G;
+            int colmask = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) colmask |= (4 * j + i >= 3 && 4 * j + i < 3 + bw) ? (1 << i) : 0;
+            const uint32_t tq = (uint32_t)(t_lo + 1) * 0x00010001u;
+            for (int r0 = 0; r0 < bh; r0 += rpc) {
+                const int rr = 3 + r0 + lr;
+                const int rrc = min(rr, bh + 2);
+                const uint8_t* q = roi + rrc * RP + 4 * j;
+                const uint32_t xv = *(const uint32_t*)q;
+                const uint32_t xn = *(const uint32_t*)(q + 4);
+                const uint32_t xp = *(const uint32_t*)(q - 4);
+                const uint32_t xd = *(const uint32_t*)(q + 3 * RP);  // ring 0 (row + 3)
+                const uint32_t xu = *(const uint32_t*)(q - 3 * RP);  // ring 8 (row - 3)
+                const uint32_t xr = __builtin_amdgcn_alignbyte(xn, xv, 3);  // ring 4 (col + 3)
+                const uint32_t xl = __builtin_amdgcn_alignbyte(xv, xp, 1);  // ring 12 (col - 3)
+                uint32_t keep2[2];
+#pragma unroll
+                for (int half = 0; half < 2; half++) {
+                    const uint32_t sel = half ? 0x0c030c01u : 0x0c020c00u;
+                    const short2v pv = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xv, sel));
+                    const short2v c0 = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xd, sel));
+                    const short2v c4 = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xr, sel));
+                    const short2v c8 = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xu, sel));
+                    const short2v c12 = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xl, sel));
+                    const short2v tv = __builtin_bit_cast(short2v, tq);
+                    const short2v hv = pv + tv, lv2 = pv - tv;
+                    // sign bit set = NOT brighter (c < v+t+1) / NOT darker (c > v-t-1)
+                    const uint32_t b0 = __builtin_bit_cast(uint32_t, (short2v)(c0 - hv));
+                    const uint32_t b4 = __builtin_bit_cast(uint32_t, (short2v)(c4 - hv));
+                    const uint32_t b8 = __builtin_bit_cast(uint32_t, (short2v)(c8 - hv));
+                    const uint32_t b12 = __builtin_bit_cast(uint32_t, (short2v)(c12 - hv));
+                    const uint32_t d0 = __builtin_bit_cast(uint32_t, (short2v)(lv2 - c0));
+                    const uint32_t d4 = __builtin_bit_cast(uint32_t, (short2v)(lv2 - c4));
+                    const uint32_t d8 = __builtin_bit_cast(uint32_t, (short2v)(lv2 - c8));
+                    const uint32_t d12 = __builtin_bit_cast(uint32_t, (short2v)(lv2 - c12));
+                    // candidate iff two cyclically adjacent cardinals agree: (b0|b8)&(b4|b12) in
+                    // "is brighter" terms = NOT((nb0&nb8)|(nb4&nb12)) in sign terms
+                    const uint32_t xb = (b0 & b8) | (b4 & b12);
+                    const uint32_t xdk = (d0 & d8) | (d4 & d12);
+                    keep2[half] = ~(xb & xdk);  // bits 15 / 31 set = candidate
+                }
+                int m = (int)(((keep2[0] >> 15) & 1u) | ((keep2[1] >> 14) & 2u) | ((keep2[0] >> 29) & 4u) |
+                              ((keep2[1] >> 28) & 8u));
+                m &= (lane_ok && rr < 3 + bh) ? colmask : 0;
+                // ordered compaction: row-major = (lane, pixel) lexicographic
+                int pre = 0, tot = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const unsigned long long bi = __ballot((m >> i) & 1);
+                    pre = __builtin_amdgcn_mbcnt_hi((unsigned)(bi >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bi, pre));
+                    tot += __popcll(bi);
+                }
+                if (m) {
+                    int pos = ncand + pre;
+                    const int e = (rr << 8) | (4 * j);
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        if ((m >> i) & 1) {
+                            clist[pos] = (uint16_t)(e + i);
+                            pos++;
+                        }
+                    }
+                }
+                ncand += tot;
+            }
         }
         wave_sync();
         for (int i = lane; i < ncand; i += 64) {
