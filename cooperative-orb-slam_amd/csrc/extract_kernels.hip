@@ -36,6 +36,7 @@ __device__ __forceinline__ int lane_prefix(unsigned long long mask) {
 __device__ __forceinline__ int iclamp(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 typedef short short2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
 static inline int iclamp_host(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 /* n consecutive little-endian dwords starting at an arbitrary byte address, from n+1 aligned
@@ -930,24 +931,37 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 constexpr int kBlurRows = 64;
 constexpr int kBlurSeg = 264; // bytes of one staged row segment: strip (256) + 4 left + 4 right
 
-/* One wave per (frame, level, 256-column strip, 64-row chunk). Each source row segment
- * [sx-4, sx+260) is fetched once per wave with coalesced dword loads, REFLECT_101 halo bytes are
- * patched in LDS by three lanes, and every lane reads its 10 bytes (x0-3 .. x0+6 for its 4
- * outputs) as three aligned LDS dwords. The loads of batch i+1 are issued into registers
- * before batch i is computed (register double buffering), so memory latency overlaps VALU
- * work. The vertical 7-row window (row sums) lives in registers.
- * Rounding: columns x < w&~3 take the SSE2 float column path of OpenCV's fixed-point filter,
- * which equals round-half-to-even of s/2^16; the scalar tail rounds half up. */
-constexpr int kBlurG = 2;  // rows per prefetch batch (A/B on MI355X: 2 > 4 > 8, occupancy-limited)
+/* One wave per (frame, level, 256-column strip, 64-row chunk); each lane owns 4 adjacent output
+ * columns x0 = sx + 4*lane.
+ *  - Source row segment [sx-4, sx+260) is fetched once per wave with coalesced dword loads
+ *    (addresses clamped into the row), staged in LDS, and the REFLECT_101 halo bytes are
+ *    patched there by three lanes. Rows are prefetched 7 rows ahead into a register ring.
+ *  - Horizontal: the lane's 12 bytes are three LDS dwords; output i's taps are two byte
+ *    windows (alignbyte) dotted with the packed kernel by v_dot4_u32_u8.
+ *  - Vertical: the 7 row sums of the window live in registers as float pairs; the loop is
+ *    unrolled by 7 so the window rotates by renaming. All values are integers < 2^24 and the
+ *    weights are k/2^16, so every packed fma is exact: sf = s / 2^16 exactly.
+ *  - Rounding: OpenCV's SSE2 column path (x < w&~3) rounds s/2^16 half to even = rint(sf),
+ *    v_cvt_pk_u8_f32 (round-to-nearest-even, saturating); the scalar tail rounds half up,
+ *    floor(sf + 0.5) (DESIGN.md "Pinned semantics"; checked by tools/check_cvtpk.hip). */
+__device__ __forceinline__ float2v blur_vsum(const float2v r0, const float2v r1, const float2v r2, const float2v r3,
+                                            const float2v r4, const float2v r5, const float2v r6) {
+    const float k18 = 18.f / 65536.f, k34 = 34.f / 65536.f, k49 = 49.f / 65536.f, k55 = 55.f / 65536.f;
+    float2v v = r3 * (float2v){k55, k55};
+    v = __builtin_elementwise_fma(r2, (float2v){k49, k49}, v);
+    v = __builtin_elementwise_fma(r4, (float2v){k49, k49}, v);
+    v = __builtin_elementwise_fma(r1, (float2v){k34, k34}, v);
+    v = __builtin_elementwise_fma(r5, (float2v){k34, k34}, v);
+    v = __builtin_elementwise_fma(r0, (float2v){k18, k18}, v);
+    v = __builtin_elementwise_fma(r6, (float2v){k18, k18}, v);
+    return v;
+}
 
-template <int G>
 __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                      const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                      ExtractParams ep, const LevelDesc* __restrict__ levels,
-                                                     const int* __restrict__ job_begin_unused,
                                                      const int* __restrict__ lvcnt) {
-    constexpr int kSlots = G > 6 ? G : 6;
-    __shared__ __align__(16) uint8_t s_rows[4][kSlots][kBlurSeg];
+    __shared__ __align__(16) uint8_t s_rows[4][7][kBlurSeg];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     int j = blockIdx.x * 4 + wave;
@@ -968,20 +982,30 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     const int pitch = l == 0 ? pitch0 : lv.pitch;
     uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
     const bool lane_on = x0 < w;
+    const bool tail = x0 + 3 >= lv.blur_vec_end;  // some of this lane's columns take the scalar path
     const int seg0 = sx - 4;                      // segment byte 0 = column seg0
     const int need_hi = min(sx + 256, w) + 3;     // columns [sx-3, need_hi) are read
     uint8_t(*rows)[kBlurSeg] = s_rows[wave];
-    // dword `lane` (and `lane+64`, lanes 0..1) of source row yy: unconditional clamped loads
+    const bool aligned = ((((uintptr_t)img) | (uintptr_t)pitch) & 3) == 0;  // wave-uniform
+    const int lastd = (w - 1) & ~3;
+    const int dA = iclamp(seg0 + 4 * lane, 0, lastd);
+    const int dB = lane < 2 ? iclamp(seg0 + 4 * (lane + 64), 0, lastd) : dA;
+    // dwords `lane` and `lane+64` (lanes 0..1) of source row yy's segment
     auto fetch = [&](int yy, uint32_t& v0, uint32_t& v1) {
         const uint8_t* row = img + (long long)reflect101(yy, h) * pitch;
-        v0 = load_row_u32_clamped(row, seg0 + 4 * lane, w);
-        v1 = load_row_u32_clamped(row, seg0 + 4 * (lane + 64), w);
+        if (aligned) {
+            v0 = *(const uint32_t*)(row + dA);
+            v1 = *(const uint32_t*)(row + dB);
+        } else {
+            v0 = load_row_u32_clamped(row, seg0 + 4 * lane, w);
+            v1 = load_row_u32_clamped(row, seg0 + 4 * (lane + 64), w);
+        }
     };
-    auto put = [&](int k, uint32_t v0, uint32_t v1) {
+    // stage one row into LDS slot k, patch its halo, return the lane's 4 row sums (as floats)
+    auto rowsum = [&](int k, uint32_t v0, uint32_t v1, float2v& lo, float2v& hi) {
         ((uint32_t*)rows[k])[lane] = v0;
-        if (lane < kBlurSeg / 4 - 64) ((uint32_t*)rows[k])[lane + 64] = v1;
-    };
-    auto patch = [&](int k) {
+        if (lane < 2) ((uint32_t*)rows[k])[lane + 64] = v1;
+        wave_sync();
         // REFLECT_101 halo over the garbage bytes: column -1-q <- 1+q, column w+q <- w-2-q
         if (lane < 3) {
             const int q = lane;
@@ -989,73 +1013,62 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
             const int xr = w + q;
             if (xr >= sx && xr < need_hi) rows[k][xr - seg0] = rows[k][(w - 2 - q) - seg0];
         }
-    };
-    auto rowsum = [&](int k, int rs[4]) {
+        wave_sync();
         const uint32_t* d = (const uint32_t*)rows[k] + lane;
         const uint32_t w0 = d[0], w1 = d[1], w2 = d[2];  // columns x0-4 .. x0+7
-        int b[10];
-        b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
-        b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
-        b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            rs[i] = 18 * (b[i] + b[i + 6]) + 34 * (b[i + 1] + b[i + 5]) + 49 * (b[i + 2] + b[i + 4]) + 55 * b[i + 3];
+        const uint32_t K1 = 18u | 34u << 8 | 49u << 16 | 55u << 24, K2 = 49u | 34u << 8 | 18u << 16;
+        const uint32_t r0 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), K1,
+                                                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), K2, 0u, false), false);
+        const uint32_t r1 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), K1,
+                                                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), K2, 0u, false), false);
+        const uint32_t r2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), K1,
+                                                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), K2, 0u, false), false);
+        const uint32_t r3 = __builtin_amdgcn_udot4(w1, K1, __builtin_amdgcn_udot4(w2, K2, 0u, false), false);
+        lo = (float2v){(float)r0, (float)r1};
+        hi = (float2v){(float)r2, (float)r3};
     };
-    int r[7][4];
-    uint32_t A0[G], A1[G];
-    {  // prime: rows ya-3 .. ya+2 into window slots 1..6
-        uint32_t P0[6], P1[6];
+    auto emit = [&](int yo, float2v a, float2v b) {
+        if (!lane_on) return;
+        float o[4] = {a.x, a.y, b.x, b.y};
+        if (tail) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) fetch(ya - 3 + k, P0[k], P1[k]);
-#pragma unroll
-        for (int k = 0; k < 6; k++) put(k, P0[k], P1[k]);
-    }
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < 6; k++) patch(k);
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < 6; k++) rowsum(k, r[1 + k]);
-    wave_sync();
-    // first batch in flight
-#pragma unroll
-    for (int g = 0; g < G; g++) fetch(min(ya + g + 3, yb + 2), A0[g], A1[g]);
-    for (int y = ya; y < yb; y += G) {
-#pragma unroll
-        for (int g = 0; g < G; g++) put(g, A0[g], A1[g]);
-        wave_sync();
-#pragma unroll
-        for (int g = 0; g < G; g++) patch(g);
-        wave_sync();
-        if (y + G < yb) {  // next batch's loads overlap this batch's arithmetic
-#pragma unroll
-            for (int g = 0; g < G; g++) fetch(min(y + G + g + 3, yb + 2), A0[g], A1[g]);
+            for (int i = 0; i < 4; i++)
+                if (x0 + i >= lv.blur_vec_end) o[i] = floorf(o[i] + 0.5f);
         }
+        uint32_t packed = 0;
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-#pragma unroll
-            for (int k = 0; k < 6; k++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) r[k][i] = r[k + 1][i];
-            rowsum(g, r[6]);
-            const int yo = y + g;
-            if (!lane_on || yo >= yb) continue;
-            uint32_t packed = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int s = 55 * r[3][i] + 49 * (r[2][i] + r[4][i]) + 34 * (r[1][i] + r[5][i]) + 18 * (r[0][i] + r[6][i]);
-                int v = (x0 + i < lv.blur_vec_end) ? (s + 0x7FFF + ((s >> 16) & 1)) >> 16 : (s + (1 << 15)) >> 16;
-                v = v > 255 ? 255 : v;
-                packed |= (uint32_t)v << (8 * i);
-            }
-            uint8_t* o = out + (long long)yo * lv.pitch + x0;
-            if (x0 + 4 <= w) {
-                *(uint32_t*)o = packed;
-            } else {
-                for (int i = 0; i < 4 && x0 + i < w; i++) o[i] = (uint8_t)(packed >> (8 * i));
-            }
+        for (int i = 0; i < 4; i++) packed = __builtin_amdgcn_cvt_pk_u8_f32(o[i], (unsigned)i, packed);
+        uint8_t* p = out + (long long)yo * lv.pitch + x0;
+        if (x0 + 4 <= w) {
+            *(uint32_t*)p = packed;
+        } else {
+            for (int i = 0; i < 4 && x0 + i < w; i++) p[i] = (uint8_t)(packed >> (8 * i));
         }
-        wave_sync();
+    };
+    // window: rows y-3 .. y+3 of output row y live in slots (y - ya) .. (y - ya + 6) mod 7
+    float2v WL[7], WH[7];
+    uint32_t D0[7], D1[7];  // prefetched source rows: row ya+3+m in D[m mod 7]
+#pragma unroll
+    for (int m = 0; m < 6; m++) fetch(ya - 3 + m, D0[m], D1[m]);
+#pragma unroll
+    for (int m = 0; m < 6; m++) rowsum(m, D0[m], D1[m], WL[m], WH[m]);
+#pragma unroll
+    for (int m = 0; m < 7; m++)
+        if (ya + 3 + m <= yb + 2) fetch(ya + 3 + m, D0[m], D1[m]);
+    for (int yi = ya; yi < yb; yi += 7) {
+#pragma unroll
+        for (int s = 0; s < 7; s++) {
+            const int y = yi + s;
+            if (y >= yb) break;
+            const int ns = (s + 6) % 7;  // slot of the new row y+3
+            rowsum(ns, D0[s], D1[s], WL[ns], WH[ns]);
+            if (y + 10 <= yb + 2) fetch(y + 10, D0[s], D1[s]);
+            const float2v a = blur_vsum(WL[s], WL[(s + 1) % 7], WL[(s + 2) % 7], WL[(s + 3) % 7], WL[(s + 4) % 7],
+                                       WL[(s + 5) % 7], WL[ns]);
+            const float2v b = blur_vsum(WH[s], WH[(s + 1) % 7], WH[(s + 2) % 7], WH[(s + 3) % 7], WH[(s + 4) % 7],
+                                       WH[(s + 5) % 7], WH[ns]);
+            emit(y, a, b);
+        }
     }
 }
 
@@ -1277,8 +1290,7 @@ hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitc
                               const ExtractParams& ep, const LevelDesc* levels, const int* job_begin, int njobs,
                               const int* lvcnt, int nframes, hipStream_t st) {
     dim3 grid((njobs + 3) / 4, nframes);
-    hipLaunchKernelGGL(k_blur_strips<kBlurG>, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
-                       job_begin, lvcnt);
+    hipLaunchKernelGGL(k_blur_strips, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, lvcnt);
     return hipGetLastError();
 }
 
