@@ -308,9 +308,27 @@ struct Geometry {
             ep.umax[v] = T.umax[v];
             ep.umax_packed |= (unsigned long long)(T.umax[v] & 15) << (4 * v);
         }
+        // IC_Angle lane masks (k_describe): row ri = v + 15 (0..31), column group g (u = -15+4g+i):
+        // {packed (u+15) inside the circular patch, packed 1 inside} (ORBextractor.cc:77-104)
+        ep.ic_off = (int)ptab.size();
+        for (int ri = 0; ri < 32; ri++) {
+            const int v = ri - 15, av = v < 0 ? -v : v;
+            for (int gq = 0; gq < 8; gq++) {
+                uint32_t uw = 0, m1 = 0;
+                for (int i = 0; i < 4; i++) {
+                    const int u = -15 + 4 * gq + i, au = u < 0 ? -u : u;
+                    if (av <= 15 && au <= 15 && au <= T.umax[av]) {
+                        uw |= (uint32_t)(u + 15) << (8 * i);
+                        m1 |= 1u << (8 * i);
+                    }
+                }
+                ptab.push_back((int)uw);
+                ptab.push_back((int)m1);
+            }
+        }
         bjob_begin.assign(L + 1, 0);
         for (int l = 0; l < L; l++)
-            bjob_begin[l + 1] = bjob_begin[l] + ((lv[l].w + 255) / 256) * ((lv[l].h + 63) / 64);
+            bjob_begin[l + 1] = bjob_begin[l] + ((lv[l].w + 255) / 256) * ((lv[l].h + kBlurRows - 1) / kBlurRows);
         nbjobs = bjob_begin[L];
         for (int l = 0; l <= kMaxLevels; l++) {
             ep.kp_off[l] = l < L ? lv[l].kp_off : kp_off;
@@ -320,10 +338,10 @@ struct Geometry {
         NC = 1;
         while (NC < maxnode) NC <<= 1;
         const int node_bytes = 92 * NC;
-        const int budget = 64 * 1024;
+        // keys of a level stay in LDS up to KL (2048 covers a 640x480 / 1000-feature level 0);
+        // larger levels use global scratch. ~38 KB per workgroup -> 4 workgroups per CU.
         if (node_bytes + 7 * 256 > 160 * 1024) return ORBX_EARG;
-        int lds = std::max(budget, node_bytes + 7 * 1024);
-        KL = ((lds - node_bytes) / 7) & ~15;
+        KL = std::min(2048, ((160 * 1024 - node_bytes) / 7) & ~15);
         lds_bytes = node_bytes + 7 * KL;
         // upload
         if (d_lv.ensure(sizeof(LevelDesc) * L) || d_cells.ensure(sizeof(CellDesc) * cells.size()) ||
@@ -504,8 +522,8 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     if (prof_mark(h, 4, st)) return ORBX_EDEVICE;
     HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                         h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride, nframes,
-                         st));
+                         h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
+                         g.d_ptab.as<int>(), nframes, st));
     if (prof_mark(h, 5, st)) return ORBX_EDEVICE;
     h->last_frames = d_frames;
     h->last_fstride = fstride;

@@ -563,12 +563,6 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
 /* divides them by (size desc, creation desc) and stops at the first division that      */
 /* reaches N (ORBextractor.cc:676-737; pointer tie-break pinned to creation order).      */
 /* ----------------------------------------------------------------------------------- */
-struct OctScratch {
-    uint32_t* key;     // [n]   x_rel | y_rel<<12 | r<<24
-    uint16_t* label;   // [n]   live node index
-    uint8_t* quad;     // [n]
-};
-
 __device__ int block_scan_excl(int v, int* total, int* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int inc = v;
@@ -653,269 +647,271 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         (void)off;
     }
     n = carry;
-    OctScratch K;
-    if (n <= KL) {
-        K.key = (uint32_t*)kbase;
-        K.label = (uint16_t*)(kbase + 4 * KL);
-        K.quad = kbase + 6 * KL;
-    } else {
-        uint8_t* g = gscratch + (long long)f * gscratch_frame_bytes + (long long)lv.key_begin * 8;
-        K.key = (uint32_t*)g;
-        K.label = (uint16_t*)(g + 4ll * lv.key_cap);
-        K.quad = g + 6ll * lv.key_cap;
-    }
-    carry = 0;
-    for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
-        const int c = c0 + tid;
-        const int v = c < lv.ncells ? ccnt[c] : 0;
-        int tot;
-        const int off = block_scan_excl(v, &tot, red) + carry;
-        if (c < lv.ncells) {
-            const uint32_t* src = ckey + cells[lv.cell_begin + c].slot;
-            for (int k = 0; k < v; k++) K.key[off + k] = src[k];
-        }
-        carry += tot;
-    }
-    __syncthreads();
-    uint32_t* outk = lvkey + (long long)f * ep.kp_per_frame + lv.kp_off;
-    if (n == 0) {
-        if (tid == 0) lvcnt[f * ep.L + l] = 0;
-        return;
-    }
-    // --- 2. roots (ORBextractor.cc:542-585)
-    const int nIni = lv.nIni;
-    for (int s = tid; s < nIni; s += 256) cnt4[s] = 0;
-    __syncthreads();
-    for (int i = tid; i < n; i += 256) {
-        const float x = (float)(K.key[i] & 0xFFF);
-        int r = (int)__fdiv_rn(x, lv.hX);
-        if (r >= nIni) { atomicOr(err, 1); r = nIni - 1; }
-        K.label[i] = (uint16_t)r;
-        atomicAdd(&cnt4[r], 1);
-    }
-    __syncthreads();
-    int size = 0;
-    {
-        int carry2 = 0;
-        for (int r0 = 0; r0 < nIni; r0 += 256) {
-            const int r = r0 + tid;
-            const int nonempty = (r < nIni && cnt4[r] > 0) ? 1 : 0;
+    // The rest runs with the keys either in LDS (n <= KL) or in global scratch; the two
+    // instantiations keep every key access a plain ds_* or global_* instruction (a pointer
+    // that may be either would make all of them flat accesses).
+    struct KeysLds { uint32_t* key; uint16_t* label; uint8_t* quad; };
+    struct KeysGlobal { uint32_t* key; uint16_t* label; uint8_t* quad; };
+    auto tail = [&](auto K) {
+        carry = 0;
+        for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
+            const int c = c0 + tid;
+            const int v = c < lv.ncells ? ccnt[c] : 0;
             int tot;
-            const int pos = block_scan_excl(nonempty, &tot, red) + carry2;
-            if (nonempty) {
-                spos[r] = pos;
-                A.x0[pos] = (int)__fmul_rn(lv.hX, (float)r);
-                A.x1[pos] = (int)__fmul_rn(lv.hX, (float)(r + 1));
-                A.y0[pos] = 0;
-                A.y1[pos] = lv.maxY - lv.minY;
-                A.nk[pos] = cnt4[r];
-                A.seq[pos] = (uint32_t)r;
+            const int off = block_scan_excl(v, &tot, red) + carry;
+            if (c < lv.ncells) {
+                const uint32_t* src = ckey + cells[lv.cell_begin + c].slot;
+                for (int k = 0; k < v; k++) K.key[off + k] = src[k];
             }
-            carry2 += tot;
+            carry += tot;
         }
-        size = carry2;
-    }
-    __syncthreads();
-    for (int i = tid; i < n; i += 256) K.label[i] = (uint16_t)spos[K.label[i]];
-    if (size > NC) { if (tid == 0) atomicOr(err, 2); return; }
-    __syncthreads();
-    uint32_t next_seq = (uint32_t)nIni;
-    int phase = 1;
-    const int N = lv.N;
-    // --- 3. division rounds (ORBextractor.cc:594-739)
-    for (int iter = 0; iter < 100000; iter++) {
-        const int prevSize = size;
-        for (int s = tid; s < size; s += 256) {
-            cnt4[4 * s] = 0; cnt4[4 * s + 1] = 0; cnt4[4 * s + 2] = 0; cnt4[4 * s + 3] = 0;
+        __syncthreads();
+        uint32_t* outk = lvkey + (long long)f * ep.kp_per_frame + lv.kp_off;
+        if (n == 0) {
+            if (tid == 0) lvcnt[f * ep.L + l] = 0;
+            return;
         }
+        // --- 2. roots (ORBextractor.cc:542-585)
+        const int nIni = lv.nIni;
+        for (int s = tid; s < nIni; s += 256) cnt4[s] = 0;
         __syncthreads();
         for (int i = tid; i < n; i += 256) {
-            const int s = K.label[i];
-            if (A.nk[s] >= 2) {
-                const uint32_t kk = K.key[i];
-                const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF);
-                const int hx = (A.x1[s] - A.x0[s] + 1) >> 1, hy = (A.y1[s] - A.y0[s] + 1) >> 1;
-                const int q = (x >= A.x0[s] + hx ? 1 : 0) + (y >= A.y0[s] + hy ? 2 : 0);
-                K.quad[i] = (uint8_t)q;
-                atomicAdd(&cnt4[4 * s + q], 1);
-            }
+            const float x = (float)(K.key[i] & 0xFFF);
+            int r = (int)__fdiv_rn(x, lv.hX);
+            if (r >= nIni) { atomicOr(err, 1); r = nIni - 1; }
+            K.label[i] = (uint16_t)r;
+            atomicAdd(&cnt4[r], 1);
         }
         __syncthreads();
-        // D = nodes with >1 key; processing order: list order (phase 1) or sorted (phase 2)
-        int nD;
+        int size = 0;
         {
-            int carry3 = 0;
-            for (int s0 = 0; s0 < size; s0 += 256) {
-                const int s = s0 + tid;
-                const int isD = (s < size && A.nk[s] >= 2) ? 1 : 0;
+            int carry2 = 0;
+            for (int r0 = 0; r0 < nIni; r0 += 256) {
+                const int r = r0 + tid;
+                const int nonempty = (r < nIni && cnt4[r] > 0) ? 1 : 0;
                 int tot;
-                const int pos = block_scan_excl(isD, &tot, red) + carry3;
-                if (isD) {
-                    dflag[pos] = s;  // D array (slot ids) in list order
-                    skey[pos] = ((unsigned long long)(uint32_t)A.nk[s] << 32) | A.seq[s];
+                const int pos = block_scan_excl(nonempty, &tot, red) + carry2;
+                if (nonempty) {
+                    spos[r] = pos;
+                    A.x0[pos] = (int)__fmul_rn(lv.hX, (float)r);
+                    A.x1[pos] = (int)__fmul_rn(lv.hX, (float)(r + 1));
+                    A.y0[pos] = 0;
+                    A.y1[pos] = lv.maxY - lv.minY;
+                    A.nk[pos] = cnt4[r];
+                    A.seq[pos] = (uint32_t)r;
                 }
-                carry3 += tot;
+                carry2 += tot;
             }
-            nD = carry3;
+            size = carry2;
         }
         __syncthreads();
-        if (nD == 0) break;  // cannot happen while size changes, kept for safety
-        if (phase == 2) {
-            // bitonic sort of skey[0..P) descending; pad with 0
-            int P2 = 1;
-            while (P2 < nD) P2 <<= 1;
-            for (int i = nD + tid; i < P2; i += 256) skey[i] = 0ull;
+        for (int i = tid; i < n; i += 256) K.label[i] = (uint16_t)spos[K.label[i]];
+        if (size > NC) { if (tid == 0) atomicOr(err, 2); return; }
+        __syncthreads();
+        uint32_t next_seq = (uint32_t)nIni;
+        int phase = 1;
+        const int N = lv.N;
+        // --- 3. division rounds (ORBextractor.cc:594-739)
+        for (int iter = 0; iter < 100000; iter++) {
+            const int prevSize = size;
+            for (int s = tid; s < size; s += 256) {
+                cnt4[4 * s] = 0; cnt4[4 * s + 1] = 0; cnt4[4 * s + 2] = 0; cnt4[4 * s + 3] = 0;
+            }
             __syncthreads();
-            for (int k = 2; k <= P2; k <<= 1) {
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                    for (int i = tid; i < P2; i += 256) {
-                        const int ixj = i ^ j;
-                        if (ixj > i) {
-                            const unsigned long long a = skey[i], b = skey[ixj];
-                            const bool desc = (i & k) == 0;
-                            if (desc ? (a < b) : (a > b)) { skey[i] = b; skey[ixj] = a; }
+            for (int i = tid; i < n; i += 256) {
+                const int s = K.label[i];
+                if (A.nk[s] >= 2) {
+                    const uint32_t kk = K.key[i];
+                    const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF);
+                    const int hx = (A.x1[s] - A.x0[s] + 1) >> 1, hy = (A.y1[s] - A.y0[s] + 1) >> 1;
+                    const int q = (x >= A.x0[s] + hx ? 1 : 0) + (y >= A.y0[s] + hy ? 2 : 0);
+                    K.quad[i] = (uint8_t)q;
+                    atomicAdd(&cnt4[4 * s + q], 1);
+                }
+            }
+            __syncthreads();
+            // D = nodes with >1 key; processing order: list order (phase 1) or sorted (phase 2)
+            int nD;
+            {
+                int carry3 = 0;
+                for (int s0 = 0; s0 < size; s0 += 256) {
+                    const int s = s0 + tid;
+                    const int isD = (s < size && A.nk[s] >= 2) ? 1 : 0;
+                    int tot;
+                    const int pos = block_scan_excl(isD, &tot, red) + carry3;
+                    if (isD) {
+                        dflag[pos] = s;  // D array (slot ids) in list order
+                        skey[pos] = ((unsigned long long)(uint32_t)A.nk[s] << 32) | A.seq[s];
+                    }
+                    carry3 += tot;
+                }
+                nD = carry3;
+            }
+            __syncthreads();
+            if (nD == 0) break;  // cannot happen while size changes, kept for safety
+            if (phase == 2) {
+                // bitonic sort of skey[0..P) descending; pad with 0
+                int P2 = 1;
+                while (P2 < nD) P2 <<= 1;
+                for (int i = nD + tid; i < P2; i += 256) skey[i] = 0ull;
+                __syncthreads();
+                for (int k = 2; k <= P2; k <<= 1) {
+                    for (int j = k >> 1; j > 0; j >>= 1) {
+                        for (int i = tid; i < P2; i += 256) {
+                            const int ixj = i ^ j;
+                            if (ixj > i) {
+                                const unsigned long long a = skey[i], b = skey[ixj];
+                                const bool desc = (i & k) == 0;
+                                if (desc ? (a < b) : (a > b)) { skey[i] = b; skey[ixj] = a; }
+                            }
+                        }
+                        __syncthreads();
+                    }
+                }
+                // map sorted keys back to slots: seq is unique -> search by seq
+                for (int j = tid; j < nD; j += 256) dbase[j] = 0;
+                __syncthreads();
+                for (int s = tid; s < size; s += 256) spos[s] = -1;
+                __syncthreads();
+                // slot lookup: for each D slot (in dflag), find its rank via binary search over skey
+                for (int j = tid; j < nD; j += 256) {
+                    const int s = dflag[j];
+                    const unsigned long long key = ((unsigned long long)(uint32_t)A.nk[s] << 32) | A.seq[s];
+                    int lo = 0, hi = nD - 1;
+                    while (lo < hi) {  // descending array: find index of key
+                        const int mid = (lo + hi) >> 1;
+                        if (skey[mid] > key) lo = mid + 1; else hi = mid;
+                    }
+                    spos[s] = lo;  // processing rank of slot s
+                }
+                __syncthreads();
+                for (int s = tid; s < size; s += 256)
+                    if (spos[s] >= 0) dflag[spos[s]] = s;
+                __syncthreads();
+            }
+            // children counts per processing position; prefix -> creation indices
+            int TC = 0, jstar = nD - 1;
+            {
+                int carry4 = 0, carryG = 0;
+                if (tid == 0) sh_jstar = nD - 1;
+                __syncthreads();
+                for (int j0 = 0; j0 < nD; j0 += 256) {
+                    const int j = j0 + tid;
+                    int nc = 0;
+                    if (j < nD) {
+                        const int s = dflag[j];
+                        nc = (cnt4[4 * s] > 0) + (cnt4[4 * s + 1] > 0) + (cnt4[4 * s + 2] > 0) + (cnt4[4 * s + 3] > 0);
+                    }
+                    int tot;
+                    const int excl = block_scan_excl(nc, &tot, red) + carry4;
+                    int tot2;
+                    const int excl2 = block_scan_excl(nc - 1, &tot2, red) + carryG;
+                    if (j < nD) {
+                        dbase[j] = excl;
+                        if (phase == 2) {
+                            const int after = prevSize + excl2 + (nc - 1);
+                            const int before = prevSize + excl2;
+                            if (after >= N && before < N) sh_jstar = j;  // first crossing (unique)
                         }
                     }
+                    carry4 += tot;
+                    carryG += tot2;
+                }
+                __syncthreads();
+                jstar = sh_jstar;
+                TC = (jstar == nD - 1) ? carry4 : dbase[jstar + 1];
+            }
+            const int ndiv = jstar + 1;
+            // survivors = live slots not divided, in list order
+            for (int s = tid; s < size; s += 256) spos[s] = 0;
+            __syncthreads();
+            for (int j = tid; j < ndiv; j += 256) spos[dflag[j]] = -1;  // mark divided
+            __syncthreads();
+            int nsurv;
+            {
+                int carry5 = 0;
+                for (int s0 = 0; s0 < size; s0 += 256) {
+                    const int s = s0 + tid;
+                    const int sv = (s < size && spos[s] == 0) ? 1 : 0;
+                    int tot;
+                    const int pos = block_scan_excl(sv, &tot, red) + carry5;
                     __syncthreads();
+                    if (s < size) spos[s] = sv ? (TC + pos) : -1;
+                    carry5 += tot;
+                }
+                nsurv = carry5;
+            }
+            __syncthreads();
+            const int newSize = TC + nsurv;
+            if (newSize > NC) { if (tid == 0) atomicOr(err, 4); return; }
+            // write new table: survivors copy, children created
+            for (int s = tid; s < size; s += 256) {
+                const int np = spos[s];
+                if (np >= 0) {
+                    Bt.x0[np] = A.x0[s]; Bt.y0[np] = A.y0[s]; Bt.x1[np] = A.x1[s]; Bt.y1[np] = A.y1[s];
+                    Bt.nk[np] = A.nk[s]; Bt.seq[np] = A.seq[s];
                 }
             }
-            // map sorted keys back to slots: seq is unique -> search by seq
-            for (int j = tid; j < nD; j += 256) dbase[j] = 0;
-            __syncthreads();
-            for (int s = tid; s < size; s += 256) spos[s] = -1;
-            __syncthreads();
-            // slot lookup: for each D slot (in dflag), find its rank via binary search over skey
-            for (int j = tid; j < nD; j += 256) {
+            int nexp_local = 0;
+            for (int j = tid; j < ndiv; j += 256) {
                 const int s = dflag[j];
-                const unsigned long long key = ((unsigned long long)(uint32_t)A.nk[s] << 32) | A.seq[s];
-                int lo = 0, hi = nD - 1;
-                while (lo < hi) {  // descending array: find index of key
-                    const int mid = (lo + hi) >> 1;
-                    if (skey[mid] > key) lo = mid + 1; else hi = mid;
-                }
-                spos[s] = lo;  // processing rank of slot s
-            }
-            __syncthreads();
-            for (int s = tid; s < size; s += 256)
-                if (spos[s] >= 0) dflag[spos[s]] = s;
-            __syncthreads();
-        }
-        // children counts per processing position; prefix -> creation indices
-        int TC = 0, jstar = nD - 1;
-        {
-            int carry4 = 0, carryG = 0;
-            if (tid == 0) sh_jstar = nD - 1;
-            __syncthreads();
-            for (int j0 = 0; j0 < nD; j0 += 256) {
-                const int j = j0 + tid;
-                int nc = 0;
-                if (j < nD) {
-                    const int s = dflag[j];
-                    nc = (cnt4[4 * s] > 0) + (cnt4[4 * s + 1] > 0) + (cnt4[4 * s + 2] > 0) + (cnt4[4 * s + 3] > 0);
-                }
-                int tot;
-                const int excl = block_scan_excl(nc, &tot, red) + carry4;
-                int tot2;
-                const int excl2 = block_scan_excl(nc - 1, &tot2, red) + carryG;
-                if (j < nD) {
-                    dbase[j] = excl;
-                    if (phase == 2) {
-                        const int after = prevSize + excl2 + (nc - 1);
-                        const int before = prevSize + excl2;
-                        if (after >= N && before < N) sh_jstar = j;  // first crossing (unique)
+                const int x0 = A.x0[s], y0 = A.y0[s], x1 = A.x1[s], y1 = A.y1[s];
+                const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;
+                int ci = dbase[j];
+    #pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int cn = cnt4[4 * s + q];
+                    if (cn > 0) {
+                        const int np = TC - 1 - ci;
+                        const int cx0 = (q & 1) ? x0 + hx : x0, cx1 = (q & 1) ? x1 : x0 + hx;
+                        const int cy0 = (q & 2) ? y0 + hy : y0, cy1 = (q & 2) ? y1 : y0 + hy;
+                        Bt.x0[np] = cx0; Bt.y0[np] = cy0; Bt.x1[np] = cx1; Bt.y1[np] = cy1;
+                        Bt.nk[np] = cn; Bt.seq[np] = next_seq + (uint32_t)ci;
+                        cpos[4 * s + q] = (uint16_t)np;
+                        nexp_local += cn > 1;
+                        ci++;
                     }
                 }
-                carry4 += tot;
-                carryG += tot2;
+            }
+            const int nToExpand = block_sum(nexp_local, red);
+            // relabel keys
+            for (int i = tid; i < n; i += 256) {
+                const int s = K.label[i];
+                const int np = spos[s];
+                K.label[i] = (uint16_t)(np >= 0 ? np : cpos[4 * s + K.quad[i]]);
             }
             __syncthreads();
-            jstar = sh_jstar;
-            TC = (jstar == nD - 1) ? carry4 : dbase[jstar + 1];
+            // swap tables
+            { NodeT t = A; A = Bt; Bt = t; }
+            next_seq += (uint32_t)TC;
+            size = newSize;
+            if (size >= N || size == prevSize) break;
+            if (phase == 1 && size + nToExpand * 3 > N) phase = 2;
         }
-        const int ndiv = jstar + 1;
-        // survivors = live slots not divided, in list order
-        for (int s = tid; s < size; s += 256) spos[s] = 0;
+        // --- 4. keep the best key of each node (first max response, ORBextractor.cc:741-760)
+        uint32_t* best = (uint32_t*)cnt4;
+        for (int s = tid; s < size; s += 256) best[s] = 0u;
         __syncthreads();
-        for (int j = tid; j < ndiv; j += 256) spos[dflag[j]] = -1;  // mark divided
-        __syncthreads();
-        int nsurv;
-        {
-            int carry5 = 0;
-            for (int s0 = 0; s0 < size; s0 += 256) {
-                const int s = s0 + tid;
-                const int sv = (s < size && spos[s] == 0) ? 1 : 0;
-                int tot;
-                const int pos = block_scan_excl(sv, &tot, red) + carry5;
-                __syncthreads();
-                if (s < size) spos[s] = sv ? (TC + pos) : -1;
-                carry5 += tot;
-            }
-            nsurv = carry5;
-        }
-        __syncthreads();
-        const int newSize = TC + nsurv;
-        if (newSize > NC) { if (tid == 0) atomicOr(err, 4); return; }
-        // write new table: survivors copy, children created
-        for (int s = tid; s < size; s += 256) {
-            const int np = spos[s];
-            if (np >= 0) {
-                Bt.x0[np] = A.x0[s]; Bt.y0[np] = A.y0[s]; Bt.x1[np] = A.x1[s]; Bt.y1[np] = A.y1[s];
-                Bt.nk[np] = A.nk[s]; Bt.seq[np] = A.seq[s];
-            }
-        }
-        int nexp_local = 0;
-        for (int j = tid; j < ndiv; j += 256) {
-            const int s = dflag[j];
-            const int x0 = A.x0[s], y0 = A.y0[s], x1 = A.x1[s], y1 = A.y1[s];
-            const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;
-            int ci = dbase[j];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int cn = cnt4[4 * s + q];
-                if (cn > 0) {
-                    const int np = TC - 1 - ci;
-                    const int cx0 = (q & 1) ? x0 + hx : x0, cx1 = (q & 1) ? x1 : x0 + hx;
-                    const int cy0 = (q & 2) ? y0 + hy : y0, cy1 = (q & 2) ? y1 : y0 + hy;
-                    Bt.x0[np] = cx0; Bt.y0[np] = cy0; Bt.x1[np] = cx1; Bt.y1[np] = cy1;
-                    Bt.nk[np] = cn; Bt.seq[np] = next_seq + (uint32_t)ci;
-                    cpos[4 * s + q] = (uint16_t)np;
-                    nexp_local += cn > 1;
-                    ci++;
-                }
-            }
-        }
-        const int nToExpand = block_sum(nexp_local, red);
-        // relabel keys
         for (int i = tid; i < n; i += 256) {
-            const int s = K.label[i];
-            const int np = spos[s];
-            K.label[i] = (uint16_t)(np >= 0 ? np : cpos[4 * s + K.quad[i]]);
+            const uint32_t kk = K.key[i];
+            atomicMax(&best[K.label[i]], (kk & 0xFF000000u) | (0xFFFFFFu - (uint32_t)i));
         }
         __syncthreads();
-        // swap tables
-        { NodeT t = A; A = Bt; Bt = t; }
-        next_seq += (uint32_t)TC;
-        size = newSize;
-        if (size >= N || size == prevSize) break;
-        if (phase == 1 && size + nToExpand * 3 > N) phase = 2;
+        if (size > lv.kp_cap) { if (tid == 0) atomicOr(err, 8); size = lv.kp_cap; }
+        for (int s = tid; s < size; s += 256) {
+            const int i = (int)(0xFFFFFFu - (best[s] & 0xFFFFFFu));
+            const uint32_t kk = K.key[i];
+            const uint32_t x = (kk & 0xFFF) + (uint32_t)lv.minX, y = ((kk >> 12) & 0xFFF) + (uint32_t)lv.minY;
+            outk[s] = x | (y << 12) | (kk & 0xFF000000u);
+        }
+        if (tid == 0) lvcnt[f * ep.L + l] = size;
+    };
+    if (n <= KL) {
+        tail(KeysLds{(uint32_t*)kbase, (uint16_t*)(kbase + 4 * KL), kbase + 6 * KL});
+    } else {
+        uint8_t* g = gscratch + (long long)f * gscratch_frame_bytes + (long long)lv.key_begin * 8;
+        tail(KeysGlobal{(uint32_t*)g, (uint16_t*)(g + 4ll * lv.key_cap), g + 6ll * lv.key_cap});
     }
-    // --- 4. keep the best key of each node (first max response, ORBextractor.cc:741-760)
-    uint32_t* best = (uint32_t*)cnt4;
-    for (int s = tid; s < size; s += 256) best[s] = 0u;
-    __syncthreads();
-    for (int i = tid; i < n; i += 256) {
-        const uint32_t kk = K.key[i];
-        atomicMax(&best[K.label[i]], (kk & 0xFF000000u) | (0xFFFFFFu - (uint32_t)i));
-    }
-    __syncthreads();
-    if (size > lv.kp_cap) { if (tid == 0) atomicOr(err, 8); size = lv.kp_cap; }
-    for (int s = tid; s < size; s += 256) {
-        const int i = (int)(0xFFFFFFu - (best[s] & 0xFFFFFFu));
-        const uint32_t kk = K.key[i];
-        const uint32_t x = (kk & 0xFFF) + (uint32_t)lv.minX, y = ((kk >> 12) & 0xFFF) + (uint32_t)lv.minY;
-        outk[s] = x | (y << 12) | (kk & 0xFF000000u);
-    }
-    if (tid == 0) lvcnt[f * ep.L + l] = size;
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -928,7 +924,6 @@ __device__ __forceinline__ int reflect101(int p, int n) {
     return p;
 }
 
-constexpr int kBlurRows = 64;
 constexpr int kBlurSeg = 264; // bytes of one staged row segment: strip (256) + 4 left + 4 right
 
 /* One wave per (frame, level, 256-column strip, 64-row chunk); each lane owns 4 adjacent output
@@ -957,6 +952,7 @@ __device__ __forceinline__ float2v blur_vsum(const float2v r0, const float2v r1,
     return v;
 }
 
+template <bool kAligned>
 __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                      const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                      ExtractParams ep, const LevelDesc* __restrict__ levels,
@@ -986,14 +982,15 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     const int seg0 = sx - 4;                      // segment byte 0 = column seg0
     const int need_hi = min(sx + 256, w) + 3;     // columns [sx-3, need_hi) are read
     uint8_t(*rows)[kBlurSeg] = s_rows[wave];
-    const bool aligned = ((((uintptr_t)img) | (uintptr_t)pitch) & 3) == 0;  // wave-uniform
+    // kAligned: every row of every level starts 4-aligned (pyramid levels always do; the
+    // caller's frames are checked at launch), so segment dwords are plain clamped loads
     const int lastd = (w - 1) & ~3;
     const int dA = iclamp(seg0 + 4 * lane, 0, lastd);
     const int dB = lane < 2 ? iclamp(seg0 + 4 * (lane + 64), 0, lastd) : dA;
     // dwords `lane` and `lane+64` (lanes 0..1) of source row yy's segment
     auto fetch = [&](int yy, uint32_t& v0, uint32_t& v1) {
         const uint8_t* row = img + (long long)reflect101(yy, h) * pitch;
-        if (aligned) {
+        if (kAligned) {
             v0 = *(const uint32_t*)(row + dA);
             v1 = *(const uint32_t*)(row + dB);
         } else {
@@ -1028,7 +1025,7 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
         hi = (float2v){(float)r2, (float)r3};
     };
     auto emit = [&](int yo, float2v a, float2v b) {
-        if (!lane_on) return;
+        if (!lane_on || yo >= yb) return;
         float o[4] = {a.x, a.y, b.x, b.y};
         if (tail) {
 #pragma unroll
@@ -1053,16 +1050,16 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
 #pragma unroll
     for (int m = 0; m < 6; m++) rowsum(m, D0[m], D1[m], WL[m], WH[m]);
 #pragma unroll
-    for (int m = 0; m < 7; m++)
-        if (ya + 3 + m <= yb + 2) fetch(ya + 3 + m, D0[m], D1[m]);
+    for (int m = 0; m < 7; m++) fetch(ya + 3 + m, D0[m], D1[m]);
+    // straight-line body: every step fetches (rows past the chunk are reflected, valid rows)
+    // and computes; only the stores are masked, so the prefetch waits stay counted (vmcnt(N))
     for (int yi = ya; yi < yb; yi += 7) {
 #pragma unroll
         for (int s = 0; s < 7; s++) {
             const int y = yi + s;
-            if (y >= yb) break;
             const int ns = (s + 6) % 7;  // slot of the new row y+3
             rowsum(ns, D0[s], D1[s], WL[ns], WH[ns]);
-            if (y + 10 <= yb + 2) fetch(y + 10, D0[s], D1[s]);
+            fetch(y + 10, D0[s], D1[s]);
             const float2v a = blur_vsum(WL[s], WL[(s + 1) % 7], WL[(s + 2) % 7], WL[(s + 3) % 7], WL[(s + 4) % 7],
                                        WL[(s + 5) % 7], WL[ns]);
             const float2v b = blur_vsum(WH[s], WH[(s + 1) % 7], WH[(s + 2) % 7], WH[(s + 3) % 7], WH[(s + 4) % 7],
@@ -1072,78 +1069,111 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     }
 }
 
+/* rBRIEF test pairs as floats (x0, y0, x1, y1), one 16-byte load per test */
+struct PatPt {
+    float x0, y0, x1, y1;
+};
+struct PatTable {
+    PatPt t[256];
+};
+constexpr float pat_s8(unsigned char c) { return (float)(c < 128 ? (int)c : (int)c - 256); }
+constexpr PatTable make_pattern_table() {
+    PatTable p{};
+    for (int t = 0; t < 256; t++)
+        p.t[t] = PatPt{pat_s8(orbx_pattern_soa_u8[t]), pat_s8(orbx_pattern_soa_u8[256 + t]),
+                       pat_s8(orbx_pattern_soa_u8[512 + t]), pat_s8(orbx_pattern_soa_u8[768 + t])};
+    return p;
+}
+__device__ constexpr PatTable kPatternF = make_pattern_table();
+
 /* ----------------------------------------------------------------------------------- */
-/* IC_Angle + rBRIEF + output, one wave per octree output slot.                          */
+/* IC_Angle + rBRIEF + output: 16 lanes per keypoint, 4 keypoints per wave.               */
+/*                                                                                       */
+/*  - IC_Angle (ORBextractor.cc:77-104): lane (column group g4 = ln&7, row parity ln>>3)  */
+/*    takes rows ri = (ln>>3) + 2p, p = 0..15 (v = ri - 15 in -15..16, 16 masked); its 4  */
+/*    pixels are one dword (8-byte aligned load + alignbyte); the circular mask and the   */
+/*    column weights u+15 are packed bytes of a host table (LDS copy), so per row two     */
+/*    v_dot4 give sum (u+15)*I and sum I: m10 = sum (u+15)I - 15 sum I, m01 = sum v*I.     */
+/*  - fastAtan2 + glibc sincosf once per 16 lanes (orb_math.h).                           */
+/*  - rBRIEF (ORBextractor.cc:107-147): test t = 16k + ln, k = 0..15, pattern from LDS;   */
+/*    bit t%8 of byte t/8 = ballot bit (16 sub + ln) of round k.                          */
 /* ----------------------------------------------------------------------------------- */
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                   const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   ExtractParams ep, const LevelDesc* __restrict__ levels,
                                                   const uint32_t* __restrict__ lvkey, const int* __restrict__ lvcnt,
                                                   orbx_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
-                                                  int* __restrict__ out_counts, int kp_stride) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int g = blockIdx.x * 4 + wave, f = blockIdx.y;
-    if (g >= ep.kp_per_frame) return;
-    // per-level counts of this frame: kMaxLevels unconditional loads (lvcnt is padded by
-    // kMaxLevels ints), issued together; entries >= L masked
+                                                  int* __restrict__ out_counts, int kp_stride,
+                                                  const int* __restrict__ ptab) {
+    __shared__ PatPt s_pat[256];
+    __shared__ int2 s_ic[256];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int sub = lane >> 4, ln = lane & 15;
+    const int f = blockIdx.y;
+    s_pat[tid] = kPatternF.t[tid];
+    s_ic[tid] = ((const int2*)(ptab + ep.ic_off))[tid];
+    // per-level counts of this frame (lvcnt is padded by kMaxLevels ints; entries >= L masked)
     const int* cnt = lvcnt + f * ep.L;
     int cl[kMaxLevels];
 #pragma unroll
-    for (int q = 0; q < kMaxLevels; q++) cl[q] = cnt[q];
-#pragma unroll
-    for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cl[q] : 0;
-    if (g == 0 && lane == 0) {
+    for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;
+    if (blockIdx.x == 0 && tid == 0) {
         int tot = 0;
 #pragma unroll
         for (int q = 0; q < kMaxLevels; q++) tot += cl[q];
         out_counts[f] = tot;
     }
-    const int l = level_of(ep.kp_off, ep.L, g);
-    const int k = g - ep.kp_off[l];
+    __syncthreads();
+    const int g = (blockIdx.x * 4 + wave) * 4 + sub;  // octree output slot of this lane group
+    if (__ballot(g < ep.kp_per_frame) == 0) return;   // wave-uniform
+    const int gc = min(g, ep.kp_per_frame - 1);
+    const int l = level_of(ep.kp_off, ep.L, gc);
+    const int k = gc - ep.kp_off[l];
     int mycnt = 0, outidx = k;
 #pragma unroll
     for (int q = 0; q < kMaxLevels; q++) {
         mycnt = q == l ? cl[q] : mycnt;
         outidx += q < l ? cl[q] : 0;
     }
-    if (k >= mycnt) return;
+    const bool valid = g < ep.kp_per_frame && k < mycnt;
+    if (__ballot(valid) == 0) return;  // wave-uniform
     const LevelDesc lv = levels[l];
-    const uint32_t kk = lvkey[(long long)f * ep.kp_per_frame + g];
-    const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF), resp = (int)(kk >> 24);
+    const uint32_t kk = valid ? lvkey[(long long)f * ep.kp_per_frame + gc] : 0u;
+    // invalid groups run on a safe dummy position (results discarded)
+    const int x = valid ? (int)(kk & 0xFFF) : 32, y = valid ? (int)((kk >> 12) & 0xFFF) : 32;
+    const int resp = (int)(kk >> 24);
     const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
     const int pitch = l == 0 ? pitch0 : lv.pitch;
-    // IC_Angle (ORBextractor.cc:77-104): lanes = columns u, two half-waves split the rows
-    int m10 = 0, m01 = 0;
+    int m10, m01;
     {
-        // lanes = patch columns u (lane 31/63 duplicate u = 15, masked); half-waves split the rows.
-        // All 16 loads are unconditional and in bounds (keypoints are >= 19 px from the level
-        // border), so they issue back to back; the circular mask is applied afterwards.
-        const int lu = lane & 31;
-        const int u = (lu < 31 ? lu : 30) - 15;
-        const int vbeg = (lane < 32) ? -15 : 1;  // half 0: v = -15..0, half 1: v = 1..15 (+1 masked)
-        const uint8_t* col = img + (long long)y * pitch + x + u;
-        const int au = u < 0 ? -u : u;
-        int I[16];
+        const int g4 = ln & 7, r = ln >> 3;
+        const int off0 = (y + r - 15) * pitch + x - 15 + 4 * g4;
+        const uint32_t mis = ((uint32_t)(uintptr_t)img + (uint32_t)off0) & 3u;
+        const uint32_t dmis = (uint32_t)(2 * pitch) & 3u;  // misalignment step between a lane's rows
+        uint2 wv[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int v = min(vbeg + k, 15);
-            I[k] = col[(long long)v * pitch];
+        for (int p = 0; p < 16; p++) {
+            const uint32_t al = (mis + (uint32_t)p * dmis) & 3u;
+            wv[p] = *(const uint2*)(img + (off0 + 2 * p * pitch - (int)al));
+        }
+        int A = 0, M = 0;
+#pragma unroll
+        for (int p = 0; p < 16; p++) {
+            const int ri = r + 2 * p;
+            const uint32_t al = (mis + (uint32_t)p * dmis) & 3u;
+            const uint32_t I4 = __builtin_amdgcn_alignbyte(wv[p].y, wv[p].x, al);
+            const int2 msk = s_ic[ri * 8 + g4];
+            const int sI = (int)__builtin_amdgcn_udot4(I4, (uint32_t)msk.y, 0u, false);
+            A += (int)__builtin_amdgcn_udot4(I4, (uint32_t)msk.x, 0u, false) - 15 * sI;
+            M += (ri - 15) * sI;
         }
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int v = vbeg + k;
-            const int av = v < 0 ? -v : v;
-            const int um = (int)((ep.umax_packed >> (4 * (av & 15))) & 15);
-            const bool use = lu < 31 && v <= 15 && au <= um;
-            const int Iv = use ? I[k] : 0;
-            m10 += u * Iv;
-            m01 += v * Iv;
+        for (int o = 8; o > 0; o >>= 1) {
+            A += __shfl_xor(A, o, 16);
+            M += __shfl_xor(M, o, 16);
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            m10 += __shfl_xor(m10, o, 64);
-            m01 += __shfl_xor(m01, o, 64);
-        }
+        m10 = A;
+        m01 = M;
     }
     const float angle = fast_atan2((float)m01, (float)m10);
     // computeOrbDescriptor (ORBextractor.cc:107-147)
@@ -1152,36 +1182,35 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     float sa, ca;
     glibc_sincosf(theta, &sa, &ca);
     const float a = ca, b = sa;
-    const uint8_t* bl = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
-    const uint8_t* center = bl + (long long)y * lv.pitch + x;
-    const signed char* pat = (const signed char*)orbx_pattern_soa_u8;
-    unsigned long long words[4];
+    const uint8_t* center = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off + (y * lv.pitch + x);
+    uint32_t myword = 0;  // descriptor bytes 2ln, 2ln+1 of this lane's keypoint
 #pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const int t = 64 * w + lane;
-        const float px0 = (float)pat[t], py0 = (float)pat[256 + t];
-        const float px1 = (float)pat[512 + t], py1 = (float)pat[768 + t];
-        const int r0 = cv_round(__fadd_rn(__fmul_rn(px0, b), __fmul_rn(py0, a)));
-        const int c0 = cv_round(__fsub_rn(__fmul_rn(px0, a), __fmul_rn(py0, b)));
-        const int r1 = cv_round(__fadd_rn(__fmul_rn(px1, b), __fmul_rn(py1, a)));
-        const int c1 = cv_round(__fsub_rn(__fmul_rn(px1, a), __fmul_rn(py1, b)));
+    for (int kq = 0; kq < 16; kq++) {
+        const PatPt pp = s_pat[16 * kq + ln];
+        const int r0 = cv_round(__fadd_rn(__fmul_rn(pp.x0, b), __fmul_rn(pp.y0, a)));
+        const int c0 = cv_round(__fsub_rn(__fmul_rn(pp.x0, a), __fmul_rn(pp.y0, b)));
+        const int r1 = cv_round(__fadd_rn(__fmul_rn(pp.x1, b), __fmul_rn(pp.y1, a)));
+        const int c1 = cv_round(__fsub_rn(__fmul_rn(pp.x1, a), __fmul_rn(pp.y1, b)));
         const int t0 = center[r0 * lv.pitch + c0];
         const int t1 = center[r1 * lv.pitch + c1];
-        words[w] = __ballot(t0 < t1);
+        const unsigned long long bal = __ballot(t0 < t1);
+        const uint32_t w16 = (uint32_t)(bal >> (16 * sub)) & 0xFFFFu;
+        myword = ln == kq ? w16 : myword;
     }
-    const long long o = (long long)f * kp_stride + outidx;
-    if (lane == 0) {
-        unsigned long long* d = (unsigned long long*)(out_desc + o * 32);
-        d[0] = words[0]; d[1] = words[1]; d[2] = words[2]; d[3] = words[3];
-        orbx_kp kp;
-        const float fx = (float)x, fy = (float)y;
-        kp.x = l ? __fmul_rn(fx, lv.scale) : fx;
-        kp.y = l ? __fmul_rn(fy, lv.scale) : fy;
-        kp.size = lv.patch_size;
-        kp.angle = angle;
-        kp.response = (float)resp;
-        kp.octave = l;
-        out_kps[o] = kp;
+    if (valid) {
+        const long long o = (long long)f * kp_stride + outidx;
+        ((uint16_t*)(out_desc + o * 32))[ln] = (uint16_t)myword;
+        if (ln == 0) {
+            orbx_kp kp;
+            const float fx = (float)x, fy = (float)y;
+            kp.x = l ? __fmul_rn(fx, lv.scale) : fx;
+            kp.y = l ? __fmul_rn(fy, lv.scale) : fy;
+            kp.size = lv.patch_size;
+            kp.angle = angle;
+            kp.response = (float)resp;
+            kp.octave = l;
+            out_kps[o] = kp;
+        }
     }
 }
 
@@ -1290,17 +1319,23 @@ hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitc
                               const ExtractParams& ep, const LevelDesc* levels, const int* job_begin, int njobs,
                               const int* lvcnt, int nframes, hipStream_t st) {
     dim3 grid((njobs + 3) / 4, nframes);
-    hipLaunchKernelGGL(k_blur_strips, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, lvcnt);
+    const bool aligned = (((uintptr_t)frames | (uintptr_t)fstride | (uintptr_t)pitch0) & 3) == 0;
+    if (aligned)
+        hipLaunchKernelGGL(k_blur_strips<true>, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
+                           lvcnt);
+    else
+        hipLaunchKernelGGL(k_blur_strips<false>, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
+                           lvcnt);
     return hipGetLastError();
 }
 
 hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                            const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
                            const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,
-                           int* out_counts, int kp_stride, int nframes, hipStream_t st) {
-    dim3 grid((ep.kp_per_frame + 3) / 4, nframes);
+                           int* out_counts, int kp_stride, const int* ptab, int nframes, hipStream_t st) {
+    dim3 grid((ep.kp_per_frame + 15) / 16, nframes);
     hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, lvkey,
-                       lvcnt, out_kps, out_desc, out_counts, kp_stride);
+                       lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
     return hipGetLastError();
 }
 

@@ -35,7 +35,7 @@ hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitc
 hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                            const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
                            const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,
-                           int* out_counts, int kp_stride, int nframes, hipStream_t st);
+                           int* out_counts, int kp_stride, const int* ptab, int nframes, hipStream_t st);
 
 hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,

@@ -155,6 +155,164 @@ __device__ __forceinline__ void tri_bf_body(const PairSrc& s, const MatchGeom& g
     }
 }
 
+/* ----------------------------------------------------------------------------------- */
+/* MFMA form of the BF SearchForTriangulation scan.                                       */
+/*                                                                                       */
+/* Hamming distance as an int8 GEMM: with candidate bits a in {0,1} and query bits mapped  */
+/* to b' = 2b-1 in {-1,+1},  sum_k a_k b'_k = 2|a&b| - |a|, so                             */
+/*     D(a, b) = |a| + |b| - 2|a&b| = |b| - dot(a, b')                                     */
+/* and |b| is a per-query (per-lane) constant. v_mfma_i32_32x32x32_i8 computes a 32        */
+/* candidate x 32 query tile of dot(a, b') per 32 descriptor bits; 8 steps cover 256 bits. */
+/* Lane l holds query (l & 31) and candidates (reg&3) + 8(reg>>2) + 4(l>>5) of the tile.  */
+/* Both operands map fragment element j of lane half h to descriptor bit 32s + 16h + j,    */
+/* so the k order inside the instruction is irrelevant (a dot product).                    */
+/*                                                                                       */
+/* Selection: key = D << 16 | (65535 - idx2); the reference's scan (accept dist <= best,   */
+/* geometric checks only for those) returns the valid candidate of minimum key             */
+/* (DESIGN.md "Matcher semantics"). Per tile each lane takes its minimum key; only if it    */
+/* beats the running best with D <= TH_LOW are the candidate's checks evaluated (epipole   */
+/* radius, CheckDistEpipolarLine), walking up the lane's keys until one passes.           */
+/* ----------------------------------------------------------------------------------- */
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint32_t spread01(uint32_t nib) {  // 4 bits -> 4 bytes of 0/1
+    return (nib * 0x00204081u) & 0x01010101u;
+}
+__device__ __forceinline__ uint32_t spread_pm1(uint32_t nib) {  // 4 bits -> 4 bytes of +1/-1
+    return ~(spread01(nib) * 0xFEu);
+}
+
+constexpr int kMfChunk = 64;  // candidates staged per step (two 32-row tiles)
+
+__device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
+                                              int32_t* __restrict__ nmatch) {
+    __shared__ v4i s_frag[2][8][64];  // [tile][step][lane] candidate fragments (0/1 bytes)
+    __shared__ float s_x[kMfChunk], s_y[kMfChunk];
+    __shared__ int s_oct[kMfChunk], s_ok[kMfChunk];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int qblk = blockIdx.x * 128;
+    if (qblk >= s.n1) return;  // block-uniform
+    const int h = lane >> 5;
+    const int qi = qblk + wave * 32 + (lane & 31);
+    const bool qon = qi < s.n1;
+    // query fragments (+1/-1 bytes), popcount and epipolar line
+    v4i bq[8];
+    int pb = 0;
+    float la = 0.f, lb = 0.f, lc = 0.f;
+    {
+        const int qc = qon ? qi : 0;
+        const uint4* qd = (const uint4*)(s.desc1 + (long long)qc * 32);
+        const uint4 d0 = qd[0], d1 = qd[1];
+        const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int st = 0; st < 8; st++) {
+            pb += __popc(dw[st]);
+            const uint32_t b16 = dw[st] >> (16 * h);
+            bq[st] = (v4i){(int)spread_pm1(b16 & 15), (int)spread_pm1((b16 >> 4) & 15),
+                           (int)spread_pm1((b16 >> 8) & 15), (int)spread_pm1((b16 >> 12) & 15)};
+        }
+        const orbx_kp k1 = s.kps1[qc];
+        epi_line(g, k1.x, k1.y, &la, &lb, &lc);
+    }
+    uint32_t best = 0xFFFFFFFFu;
+    // expansion role of this thread: candidate c = tid >> 2 of the chunk, descriptor bytes 8q..8q+7;
+    // the next chunk's bytes (and, for tid < 64, keypoint) are prefetched into registers while
+    // the current chunk is multiplied
+    const int ec = tid >> 2, eq = tid & 3;
+    auto load_chunk = [&](int cb, uint2& d, orbx_kp& k2) {
+        const int c = min(cb + ec, s.n2 - 1);
+        d = *(const uint2*)(s.desc2 + (long long)c * 32 + 8 * eq);
+        k2 = s.kps2[min(cb + (tid & (kMfChunk - 1)), s.n2 - 1)];
+    };
+    uint2 pd;
+    orbx_kp pk;
+    load_chunk(0, pd, pk);
+    for (int cb = 0; cb < s.n2; cb += kMfChunk) {
+        {
+            const bool on = cb + ec < s.n2;
+            const int tile = ec >> 5, r = ec & 31;
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const uint32_t w = on ? (k ? pd.y : pd.x) : 0u;
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    const uint32_t b16 = w >> (16 * hh);
+                    s_frag[tile][2 * eq + k][32 * hh + r] =
+                        (v4i){(int)spread01(b16 & 15), (int)spread01((b16 >> 4) & 15), (int)spread01((b16 >> 8) & 15),
+                              (int)spread01((b16 >> 12) & 15)};
+                }
+            }
+            if (tid < kMfChunk) {
+                const bool on2 = cb + tid < s.n2;
+                s_x[tid] = pk.x;
+                s_y[tid] = pk.y;
+                s_oct[tid] = pk.octave;
+                s_ok[tid] = on2 && !near_epipole(g, pk.x, pk.y, pk.octave);
+            }
+        }
+        __syncthreads();
+        if (cb + kMfChunk < s.n2) load_chunk(cb + kMfChunk, pd, pk);
+        v16i acc0 = (v16i)0, acc1 = (v16i)0;
+#pragma unroll
+        for (int st = 0; st < 8; st++) {
+            acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(s_frag[0][st][lane], bq[st], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(s_frag[1][st][lane], bq[st], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int tile = 0; tile < 2; tile++) {
+            const v16i acc = tile ? acc1 : acc0;
+            // cheap filter: the lane's best dot in this tile (D = pb - dot)
+            int amax = acc[0];
+#pragma unroll
+            for (int rg = 1; rg < 16; rg++) amax = max(amax, acc[rg]);
+            const int lim = min(50, (int)(best >> 16));  // TH_LOW (ORBmatcher.cc:715)
+            if (pb - amax > lim) continue;
+            // key = D << 16 | (65535 - idx2) = kbase - (acc << 16 | row)
+            const uint32_t kbase = ((uint32_t)pb << 16) + 65535u - (uint32_t)(cb + 32 * tile + 4 * h);
+            uint32_t key[16];
+            uint32_t kmin = 0xFFFFFFFFu;
+#pragma unroll
+            for (int rg = 0; rg < 16; rg++) {
+                const uint32_t row = (uint32_t)((rg & 3) + 8 * (rg >> 2));
+                key[rg] = kbase - (((uint32_t)acc[rg] << 16) + row);
+                kmin = min(kmin, key[rg]);
+            }
+            uint32_t km = kmin;
+            while (km < best && (km >> 16) <= 50u) {
+                const int jl = (int)(65535u - (km & 0xFFFFu)) - cb;
+                if (s_ok[jl] && epi_ok(la, lb, lc, s_x[jl], s_y[jl], g.th384[s_oct[jl]])) {
+                    best = km;
+                    break;
+                }
+                uint32_t nx = 0xFFFFFFFFu;
+#pragma unroll
+                for (int rg = 0; rg < 16; rg++) nx = key[rg] > km ? min(nx, key[rg]) : nx;
+                km = nx;
+            }
+        }
+        __syncthreads();
+    }
+    best = min(best, (uint32_t)__shfl_xor((int)best, 32, 64));
+    if (qon && h == 0) {
+        const int idx2 = (best >> 16) <= 50u ? (int)(65535u - (best & 0xFFFFu)) : -1;
+        out[qi] = idx2;
+        if (idx2 >= 0) atomicAdd(nmatch, 1);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tri_mfma(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
+                                                  const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
+                                                  const int32_t* __restrict__ counts, int kp_stride, MatchGeom g,
+                                                  int32_t* __restrict__ match12, int32_t* __restrict__ nmatches) {
+    const int p = blockIdx.y;
+    const int f1 = q1[p], f2 = q2[p];
+    PairSrc s;
+    s.kps1 = kps + (long long)f1 * kp_stride; s.desc1 = desc + (long long)f1 * kp_stride * 32; s.n1 = counts[f1];
+    s.kps2 = kps + (long long)f2 * kp_stride; s.desc2 = desc + (long long)f2 * kp_stride * 32; s.n2 = counts[f2];
+    tri_mfma_body(s, g, match12 + (long long)p * kp_stride, nmatches + p);
+}
+
 template <int SPLIT>
 __global__ __launch_bounds__(256) void k_tri_bf(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
                                                 const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
@@ -417,6 +575,12 @@ namespace orbamd {
 hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
                          int32_t* nmatches, hipStream_t st) {
+    if (!getenv("ORBX_TRI_SIMT")) {
+        dim3 grid((kp_stride + 127) / 128, npairs);
+        hipLaunchKernelGGL(k_tri_mfma, grid, dim3(256), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
+                           nmatches);
+        return hipGetLastError();
+    }
     // few pairs: split the candidate scan over 4 parts for more waves; many pairs: 256 queries per block
     if (npairs * ((kp_stride + 255) / 256) < 2048) {
         dim3 grid((kp_stride + 63) / 64, npairs);

@@ -26,6 +26,7 @@ constexpr int kPatchSize = 31;      // ORBextractor.cc:72
 constexpr int kHalfPatch = 15;      // ORBextractor.cc:73
 constexpr int kRoiMax = 72;         // max FAST cell ROI side (cells are < 60+6 px)
 constexpr int kRoiPitch = 72;
+constexpr int kBlurRows = 63;      // blur strip chunk height: 9 x 7 (the 7-row window loop has no partial step)
 constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity (levels >= 1)
 constexpr int kPyrU = 4;            // k_pyramid_frames: rows in flight per thread
 constexpr int kPyrFramesMinBatch = 64;  // batches below this use the per-level pyramid kernels
@@ -72,6 +73,7 @@ struct ExtractParams {
     unsigned long long umax_packed;  // umax[v] in bits 4v..4v+3 (all values <= 15)
     int kp_off[kMaxLevels + 1];      // level l's octree output slots start (kp_off[L] = kp_per_frame)
     int bjob_begin[kMaxLevels + 1];  // blur strip jobs prefix
+    int ic_off;                      // IC_Angle mask table (int2 pairs) inside the ptab buffer
 };
 
 /* level containing index g of a per-level prefix table (no dependent loads: unrolled compares
