@@ -375,6 +375,12 @@ __device__ __forceinline__ bool fast_pretest(const uint8_t* p, int P, int t) {
     return (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
 }
 
+/* LDS bytes per wave of k_fast_cells2: ROI + S map (RP x RH each) + candidate list (u16 per
+ * band pixel; a band is at most (RP-6) x (RH-6)) */
+__host__ __device__ inline int fast_wave_lds(int RP, int RH) {
+    return 2 * RP * RH + ((2 * (RP - 6) * (RH - 6) + 15) & ~15);
+}
+
 template <int kMaxPass>
 __global__ __launch_bounds__(256) void k_fast_cells2(
     const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
@@ -386,9 +392,9 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
     const int ci = cell_lo + blockIdx.x * 4 + wave;
     if (ci >= cell_hi) return;  // wave-uniform; no block barriers in this kernel
     const int roi_bytes = RP * RH;
-    uint8_t* roi = lds + wave * (4 * roi_bytes);
+    uint8_t* roi = lds + wave * fast_wave_lds(RP, RH);
     uint8_t* str = roi + roi_bytes;
-    uint16_t* clist = (uint16_t*)(str + roi_bytes);  // <= roi_bytes entries (band < ROI)
+    uint16_t* clist = (uint16_t*)(str + roi_bytes);  // <= (RP-6)(RH-6) entries (band pixels)
     const CellDesc c = cells[ci];
     const LevelDesc lv = levels[c.level];
     const uint8_t* img = c.level == 0 ? frames + (long long)f * fstride
@@ -1283,7 +1289,7 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
                               int cell_hi, int nframes, hipStream_t st) {
     if (cell_hi <= cell_lo) return hipSuccess;
     dim3 grid((cell_hi - cell_lo + 3) / 4, nframes);
-    const size_t lds = 4 * 4 * (size_t)RP * RH;
+    const size_t lds = 4 * (size_t)fast_wave_lds(RP, RH);
     if (max_pass <= 8)
         hipLaunchKernelGGL(k_fast_cells2<8>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
                            cellkey, cellcnt, RP, RH, cell_lo, cell_hi);
