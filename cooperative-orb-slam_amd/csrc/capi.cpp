@@ -264,6 +264,15 @@ struct Geometry {
                     c.cap = ((bw + 1) / 2) * ((bh + 1) / 2);
                     c.slot = key_begin + kc;
                     kc += c.cap;
+                    c.D = (c.w + 3) / 4;
+                    c.rpp = 64 / c.D;
+                    c.magD = (65536 + c.D - 1) / c.D;
+                    c.G = (bw + 6) / 4;
+                    c.rpc = c.G > 0 ? 64 / c.G : 1;
+                    c.magG = c.G > 0 ? (65536 + c.G - 1) / c.G : 0;
+                    for (int ln = 0; ln < 64; ln++)  // the magic divisions are exact (checked)
+                        if ((ln * c.magD) >> 16 != ln / c.D || (c.G > 0 && (ln * c.magG) >> 16 != ln / c.G))
+                            return ORBX_EARG;
                     cells.push_back(c);
                 }
             }

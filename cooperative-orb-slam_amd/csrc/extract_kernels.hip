@@ -402,9 +402,9 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
     const int pitch = c.level == 0 ? pitch0 : lv.pitch;
     {
         // D dwords per ROI row, 64/D rows per pass; all passes' loads issued before the LDS writes
-        const int D = (c.w + 3) >> 2;
-        const int rpp = 64 / D;
-        const int lr = lane / D, ld = lane - lr * D;
+        const int D = c.D;
+        const int rpp = c.rpp;
+        const int lr = (lane * c.magD) >> 16, ld = lane - lr * D;
         const bool on = lane < rpp * D;
         uint32_t v[kMaxPass];  // kMaxPass >= ceil(h / rpp) for every cell (host-chosen)
         const int ldc = on ? ld : 0;
@@ -446,9 +446,9 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
         {
             // SWAR pretest: each lane tests the 4 pixels of one aligned ROI dword (band columns
             // [3, 3+bw)), as two u16 pairs (pixels 0,2 and 1,3) with packed 16-bit arithmetic.
-            const int G = (bw + 6) >> 2;  // dword groups covering columns [0, bw+3)
-            const int rpc = 64 / G;
-            const int lr = lane / G, j = lane - lr * G;
+            const int G = c.G;  // dword groups covering columns [0, bw+3): (bw + 6) / 4
+            const int rpc = c.rpc;
+            const int lr = (lane * c.magG) >> 16, j = lane - lr * G;
             const bool lane_ok = lane < rpc * G;
             int colmask = 0;
 #pragma unroll
@@ -1104,6 +1104,10 @@ __device__ constexpr PatTable kPatternF = make_pattern_table();
 /*  - rBRIEF (ORBextractor.cc:107-147): test t = 16k + ln, k = 0..15, pattern from LDS;   */
 /*    bit t%8 of byte t/8 = ballot bit (16 sub + ln) of round k.                          */
 /* ----------------------------------------------------------------------------------- */
+constexpr int kDescPatchR = 18;                   // |round(rotated pattern coordinate)| <= 13*sqrt(2)
+constexpr int kDescPatchRows = 2 * kDescPatchR + 1;  // 37
+constexpr int kDescPatchPitch = 40;                 // 10 dwords: 37 columns + up to 3 bytes misalignment
+
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                   const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   ExtractParams ep, const LevelDesc* __restrict__ levels,
@@ -1113,16 +1117,23 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
                                                   const int* __restrict__ ptab) {
     __shared__ PatPt s_pat[256];
     __shared__ int2 s_ic[256];
+    __shared__ __align__(8) uint8_t s_patch[16][kDescPatchRows * kDescPatchPitch];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int sub = lane >> 4, ln = lane & 15;
     const int f = blockIdx.y;
-    s_pat[tid] = kPatternF.t[tid];
-    s_ic[tid] = ((const int2*)(ptab + ep.ic_off))[tid];
+    // everything that depends only on the slot is issued before the table barrier
+    const PatPt my_pat = kPatternF.t[tid];
+    const int2 my_ic = ((const int2*)(ptab + ep.ic_off))[tid];
+    const int g = (blockIdx.x * 4 + wave) * 4 + sub;  // octree output slot of this lane group
+    const int gc = min(g, ep.kp_per_frame - 1);
+    const uint32_t kk_raw = lvkey[(long long)f * ep.kp_per_frame + gc];
     // per-level counts of this frame (lvcnt is padded by kMaxLevels ints; entries >= L masked)
     const int* cnt = lvcnt + f * ep.L;
     int cl[kMaxLevels];
 #pragma unroll
     for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;
+    s_pat[tid] = my_pat;
+    s_ic[tid] = my_ic;
     if (blockIdx.x == 0 && tid == 0) {
         int tot = 0;
 #pragma unroll
@@ -1130,9 +1141,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
         out_counts[f] = tot;
     }
     __syncthreads();
-    const int g = (blockIdx.x * 4 + wave) * 4 + sub;  // octree output slot of this lane group
-    if (__ballot(g < ep.kp_per_frame) == 0) return;   // wave-uniform
-    const int gc = min(g, ep.kp_per_frame - 1);
+    if (__ballot(g < ep.kp_per_frame) == 0) return;  // wave-uniform
     const int l = level_of(ep.kp_off, ep.L, gc);
     const int k = gc - ep.kp_off[l];
     int mycnt = 0, outidx = k;
@@ -1144,24 +1153,48 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     const bool valid = g < ep.kp_per_frame && k < mycnt;
     if (__ballot(valid) == 0) return;  // wave-uniform
     const LevelDesc lv = levels[l];
-    const uint32_t kk = valid ? lvkey[(long long)f * ep.kp_per_frame + gc] : 0u;
+    const uint32_t kk = valid ? kk_raw : 0u;
     // invalid groups run on a safe dummy position (results discarded)
     const int x = valid ? (int)(kk & 0xFFF) : 32, y = valid ? (int)((kk >> 12) & 0xFFF) : 32;
     const int resp = (int)(kk >> 24);
     const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
     const int pitch = l == 0 ? pitch0 : lv.pitch;
+    const uint8_t* bl = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
+    // one memory round trip: the IC_Angle rows of the level image and the blurred 37x37 patch
+    // around the keypoint (staged in LDS for the 512 rBRIEF samples)
+    const int g4 = ln & 7, r = ln >> 3;
+    const int off0 = (y + r - 15) * pitch + x - 15 + 4 * g4;
+    const uint32_t mis = ((uint32_t)(uintptr_t)img + (uint32_t)off0) & 3u;
+    const uint32_t dmis = (uint32_t)(2 * pitch) & 3u;  // misalignment step between a lane's rows
+    uint2 wv[16];
+#pragma unroll
+    for (int p = 0; p < 16; p++) {
+        const uint32_t al = (mis + (uint32_t)p * dmis) & 3u;
+        wv[p] = *(const uint2*)(img + (off0 + 2 * p * pitch - (int)al));
+    }
+    // patch: 37 rows x 5 aligned 8-byte words (row start rounded down to 4; patch column 0 =
+    // image column x-18-pmis[row])
+    const int bp = lv.pitch;  // blurred rows are 64-aligned: one misalignment for every row
+    const int pmis = (int)((uint32_t)(x - kDescPatchR) & 3u);
+    const int pbase = (y - kDescPatchR) * bp + x - kDescPatchR - pmis;
+    uint2 pw[12];
+#pragma unroll
+    for (int q = 0; q < 12; q++) {
+        const int it = min(ln + 16 * q, kDescPatchRows * 5 - 1);
+        const int pr = it / 5, pc = it - pr * 5;
+        pw[q] = *(const uint2*)(bl + (pbase + pr * bp + 8 * pc));
+    }
+    uint8_t* patch = s_patch[wave * 4 + sub];
+#pragma unroll
+    for (int q = 0; q < 12; q++) {
+        const int it = ln + 16 * q;
+        if (it < kDescPatchRows * 5) {
+            const int pr = it / 5, pc = it - pr * 5;
+            *(uint2*)(patch + pr * kDescPatchPitch + 8 * pc) = pw[q];
+        }
+    }
     int m10, m01;
     {
-        const int g4 = ln & 7, r = ln >> 3;
-        const int off0 = (y + r - 15) * pitch + x - 15 + 4 * g4;
-        const uint32_t mis = ((uint32_t)(uintptr_t)img + (uint32_t)off0) & 3u;
-        const uint32_t dmis = (uint32_t)(2 * pitch) & 3u;  // misalignment step between a lane's rows
-        uint2 wv[16];
-#pragma unroll
-        for (int p = 0; p < 16; p++) {
-            const uint32_t al = (mis + (uint32_t)p * dmis) & 3u;
-            wv[p] = *(const uint2*)(img + (off0 + 2 * p * pitch - (int)al));
-        }
         int A = 0, M = 0;
 #pragma unroll
         for (int p = 0; p < 16; p++) {
@@ -1188,7 +1221,8 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     float sa, ca;
     glibc_sincosf(theta, &sa, &ca);
     const float a = ca, b = sa;
-    const uint8_t* center = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off + (y * lv.pitch + x);
+    wave_sync();  // patch stores of the other lanes of this group
+    const uint8_t* pc0 = patch + kDescPatchR * kDescPatchPitch + kDescPatchR + pmis;  // keypoint
     uint32_t myword = 0;  // descriptor bytes 2ln, 2ln+1 of this lane's keypoint
 #pragma unroll
     for (int kq = 0; kq < 16; kq++) {
@@ -1197,8 +1231,8 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
         const int c0 = cv_round(__fsub_rn(__fmul_rn(pp.x0, a), __fmul_rn(pp.y0, b)));
         const int r1 = cv_round(__fadd_rn(__fmul_rn(pp.x1, b), __fmul_rn(pp.y1, a)));
         const int c1 = cv_round(__fsub_rn(__fmul_rn(pp.x1, a), __fmul_rn(pp.y1, b)));
-        const int t0 = center[r0 * lv.pitch + c0];
-        const int t1 = center[r1 * lv.pitch + c1];
+        const int t0 = pc0[r0 * kDescPatchPitch + c0];
+        const int t1 = pc0[r1 * kDescPatchPitch + c1];
         const unsigned long long bal = __ballot(t0 < t1);
         const uint32_t w16 = (uint32_t)(bal >> (16 * sub)) & 0xFFFFu;
         myword = ln == kq ? w16 : myword;

@@ -59,6 +59,11 @@ struct CellDesc {
     int xoff, yoff;  // j*wCell, i*hCell (ORBextractor.cc:822-823)
     int slot;        // key slot offset inside a frame
     int cap;         // slot capacity
+    // k_fast_cells2 lane schedules (wave-uniform divisions done on the host):
+    // staging: D = dwords per ROI row, rpp = 64 / D rows per pass; pretest: G = dword groups per
+    // band row, rpc = 64 / G rows per chunk; lane / n == (lane * mag_n) >> 16 (exact for lane < 64)
+    int D, rpp, magD;
+    int G, rpc, magG;
 };
 
 struct ExtractParams {
