@@ -375,8 +375,7 @@ struct orbx_handle {
     int max_w = 0, max_h = 0, max_batch = 1;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
-    hipStream_t pyr_stream = nullptr;  // high priority: the latency-bound pyramid chain
-    hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_fast0 = nullptr, ev_fast = nullptr, ev_blur = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_blur = nullptr;
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
     // host-path staging
@@ -388,24 +387,26 @@ struct orbx_handle {
     bool lds_attr_set = false;
     // stage profiling (orbx_profile_*)
     bool prof_on = false;
-    std::vector<hipEvent_t> prof_ev;  // groups of 6
+    int prof_mask = 0;  // stages with event pairs (bit k = stage k)
+    std::vector<hipEvent_t> prof_ev;  // per profiled call: 5 stages x {start, end}
     int prof_calls = 0;
     double prof_ms[5] = {0, 0, 0, 0, 0};
 };
 
 static const int kProfMaxCalls = 4096;
 
-static int prof_mark(orbx_handle* h, int k, hipStream_t st) {
-    if (!h->prof_on) return 0;
+/* stage k = {pyramid, fast_cells, octree, blur, describe}; e = 0 start / 1 end, recorded on the
+ * stream the stage's kernel is launched on (the overlapped schedule is kept) */
+static int prof_mark(orbx_handle* h, int k, int e, hipStream_t st) {
+    if (!h->prof_on || !((h->prof_mask >> k) & 1)) return 0;
     if (h->prof_calls >= kProfMaxCalls) return 0;
-    const size_t need = (size_t)(h->prof_calls + 1) * 6;
+    const size_t need = (size_t)(h->prof_calls + 1) * 10;
     while (h->prof_ev.size() < need) {
-        hipEvent_t e;
-        HIPR(hipEventCreate(&e));
-        h->prof_ev.push_back(e);
+        hipEvent_t ev;
+        HIPR(hipEventCreate(&ev));
+        h->prof_ev.push_back(ev);
     }
-    HIPR(hipEventRecord(h->prof_ev[(size_t)h->prof_calls * 6 + k], st));
-    if (k == 5) h->prof_calls++;
+    HIPR(hipEventRecord(h->prof_ev[(size_t)h->prof_calls * 10 + 2 * k + e], st));
     return 0;
 }
 
@@ -427,13 +428,6 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
         h->lds_attr_set = true;
     }
     return 0;
-}
-
-static hipError_t create_priority_stream(hipStream_t* s) {
-    int least = 0, greatest = 0;
-    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (e != hipSuccess) return e;
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
 }
 
 static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fstride, int pitch, int nframes,
@@ -476,64 +470,67 @@ static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstrid
 
 /* ORBextractor::operator() for a batch. Dependencies between the stages:
  *
- *   pyr  (high priority) : [fork] pyramid(1..L-1) -> [ev_pyr]
- *   side                 : [fork] FAST(level 0) -> [ev_fast0] ......... [ev_fast] blur(all levels) -> [ev_blur]
- *   st   (caller)        : memset(err) [fork] ... [ev_pyr] FAST(levels>=1) [ev_fast] [ev_fast0] octree [ev_blur] describe
+ *   st   (caller): memset(err) -> pyramid(1..L-1) -> [ev_pyr] FAST(all cells) -> octree -> [ev_blur] describe
+ *   side         :                                 [ev_pyr] blur(all levels) ---------> [ev_blur]
  *
- * FAST on level 0 needs only the input frames, so it fills the GPU around the seven small,
- * dependent pyramid launches (which get stream priority so they are not starved); the blur
- * runs beside the octree, whose workgroups are LDS/barrier-bound and leave VALU idle. (The
- * reference blurs only levels that kept keypoints (ORBextractor.cc:1081); blurring every
- * level changes no output, since describe reads only levels with keypoints.)
+ * The blur needs only the pyramid, so it runs beside FAST and the octree (whose workgroups are
+ * barrier/latency-bound); describe joins both. (The reference blurs only levels that kept
+ * keypoints (ORBextractor.cc:1081); blurring every level changes no output, since describe
+ * reads only levels with keypoints.) ORBX_SCHED=split also starts FAST on level 0 (which needs
+ * only the input) beside the pyramid; ORBX_SCHED=serial runs everything on `st` (A/B only).
  * With stage profiling on, everything runs in order on `st` between timing events. */
 static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
                        orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st) {
     Geometry& g = h->geo;
     const ExtractParams& ep = g.ep;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
-    const int ncell0 = g.lv[0].ncells;
-    HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), st));
-    const bool serial = h->prof_on;
+    static const int sched = [] {
+        const char* e = getenv("ORBX_SCHED");
+        return !e ? 0 : (!strcmp(e, "split") ? 1 : (!strcmp(e, "serial") ? 2 : 0));
+    }();
+    const bool serial = sched == 2;
+    const bool split = !serial && sched == 1;
+    const int ncell0 = split ? g.lv[0].ncells : 0;
     hipStream_t sd = serial ? st : h->side;
-    hipStream_t sp = serial ? st : h->pyr_stream;
-    if (!serial) {
+    HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), st));
+    if (split) {
         HIPR(hipEventRecord(h->ev_fork, st));
-        HIPR(hipStreamWaitEvent(sp, h->ev_fork, 0));
         HIPR(hipStreamWaitEvent(sd, h->ev_fork, 0));
-    }
-    if (prof_mark(h, 0, st)) return ORBX_EDEVICE;
-    if (launch_pyramid(h, d_frames, fstride, pitch, nframes, sp)) return ORBX_EDEVICE;
-    if (!serial) {
-        HIPR(hipEventRecord(h->ev_pyr, sp));
         if (launch_fast(h, d_frames, fstride, pitch, 0, ncell0, nframes, sd)) return ORBX_EDEVICE;
-        HIPR(hipEventRecord(h->ev_fast0, sd));
-        HIPR(hipStreamWaitEvent(st, h->ev_pyr, 0));
     }
-    if (prof_mark(h, 1, st)) return ORBX_EDEVICE;
-    if (launch_fast(h, d_frames, fstride, pitch, serial ? 0 : ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
-    if (!serial) {
-        HIPR(hipEventRecord(h->ev_fast, st));
-        HIPR(hipStreamWaitEvent(sd, h->ev_fast, 0));
+    if (prof_mark(h, 0, 0, st)) return ORBX_EDEVICE;
+    if (launch_pyramid(h, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
+    if (prof_mark(h, 0, 1, st)) return ORBX_EDEVICE;
+    auto blur = [&](hipStream_t bs) -> int {
+        if (prof_mark(h, 3, 0, bs)) return ORBX_EDEVICE;
         HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                                nullptr, g.nbjobs, nullptr, nframes, sd));
+                                nullptr, g.nbjobs, nullptr, nframes, bs));
+        return prof_mark(h, 3, 1, bs);
+    };
+    if (!serial) {
+        HIPR(hipEventRecord(h->ev_pyr, st));
+        HIPR(hipStreamWaitEvent(sd, h->ev_pyr, 0));
+        if (blur(sd)) return ORBX_EDEVICE;
         HIPR(hipEventRecord(h->ev_blur, sd));
-        HIPR(hipStreamWaitEvent(st, h->ev_fast0, 0));
     }
-    if (prof_mark(h, 2, st)) return ORBX_EDEVICE;
+    if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
+    if (launch_fast(h, d_frames, fstride, pitch, ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
+    if (prof_mark(h, 1, 1, st) || prof_mark(h, 2, 0, st)) return ORBX_EDEVICE;
     HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                        h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
                        (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, h->err.as<int>(), nframes, st));
-    if (prof_mark(h, 3, st)) return ORBX_EDEVICE;
-    if (serial)
-        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                                nullptr, g.nbjobs, nullptr, nframes, st));
-    else
+    if (prof_mark(h, 2, 1, st)) return ORBX_EDEVICE;
+    if (serial) {
+        if (blur(st)) return ORBX_EDEVICE;
+    } else {
         HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
-    if (prof_mark(h, 4, st)) return ORBX_EDEVICE;
+    }
+    if (prof_mark(h, 4, 0, st)) return ORBX_EDEVICE;
     HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                          h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
                          g.d_ptab.as<int>(), nframes, st));
-    if (prof_mark(h, 5, st)) return ORBX_EDEVICE;
+    if (prof_mark(h, 4, 1, st)) return ORBX_EDEVICE;
+    if (h->prof_on && h->prof_calls < kProfMaxCalls) h->prof_calls++;
     h->last_frames = d_frames;
     h->last_fstride = fstride;
     h->last_pitch = pitch;
@@ -569,11 +566,8 @@ int orbx_create(const orbx_params* p, int device, int max_width, int max_height,
     h->max_batch = max_batch;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
-        create_priority_stream(&h->pyr_stream) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_fast0, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_fast, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_blur, hipEventDisableTiming) != hipSuccess) {
         orbx_destroy(h);
         return ORBX_EDEVICE;
@@ -592,15 +586,13 @@ void orbx_destroy(orbx_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->side) (void)hipStreamSynchronize(h->side);
-    if (h->pyr_stream) (void)hipStreamSynchronize(h->pyr_stream);
     for (DevBuf* b : {&h->pyr, &h->blur, &h->cellkey, &h->cellcnt, &h->lvkey, &h->lvcnt, &h->gscratch, &h->err,
                       &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt})
         b->release();
     h->geo.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     if (h->side) (void)hipStreamDestroy(h->side);
-    if (h->pyr_stream) (void)hipStreamDestroy(h->pyr_stream);
-    for (hipEvent_t e : {h->ev_fork, h->ev_pyr, h->ev_fast0, h->ev_fast, h->ev_blur})
+    for (hipEvent_t e : {h->ev_fork, h->ev_pyr, h->ev_blur})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
     delete h;
@@ -625,6 +617,7 @@ int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, 
 int orbx_profile_enable(orbx_handle* h, int on) {
     if (!h) return ORBX_EARG;
     h->prof_on = on != 0;
+    h->prof_mask = on & 0x1F;
     h->prof_calls = 0;
     for (double& v : h->prof_ms) v = 0;
     return 0;
@@ -635,10 +628,12 @@ int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls) {
     HIPR(hipSetDevice(h->device));
     double acc[5] = {0, 0, 0, 0, 0};
     for (int c = 0; c < h->prof_calls; c++) {
-        HIPR(hipEventSynchronize(h->prof_ev[(size_t)c * 6 + 5]));
         for (int k = 0; k < 5; k++) {
+            const size_t e0 = (size_t)c * 10 + 2 * k;
+            if (!((h->prof_mask >> k) & 1)) continue;
+            HIPR(hipEventSynchronize(h->prof_ev[e0 + 1]));
             float t = 0;
-            HIPR(hipEventElapsedTime(&t, h->prof_ev[(size_t)c * 6 + k], h->prof_ev[(size_t)c * 6 + k + 1]));
+            HIPR(hipEventElapsedTime(&t, h->prof_ev[e0], h->prof_ev[e0 + 1]));
             acc[k] += t;
         }
     }

@@ -205,10 +205,13 @@ int orbx_synth_frame(int agent, int t, int width, int height, uint8_t* out);
 /* frames t0 .. t0+count-1 of agent a, back to back (frame stride width*height). */
 int orbx_synth_frames(int agent, int t0, int count, int width, int height, uint8_t* out);
 
-/* Stage profiling with HIP events recorded on the extraction stream between kernels:
- * stages = {pyramid, fast_cells, octree, blur, describe}. orbx_profile_enable resets the
- * accumulators; orbx_profile_read waits for the recorded events and returns the summed
- * milliseconds per stage (ms[5]) and the number of profiled extraction calls. */
+/* Stage profiling: a pair of HIP events brackets each stage's kernel on the stream it is
+ * launched on (the overlapped schedule is kept, so a stage's time includes sharing the GPU
+ * with the stage that runs beside it): stages = {pyramid, fast_cells, octree, blur, describe}.
+ * orbx_profile_enable(h, mask) resets the accumulators and brackets the stages in `mask`
+ * (bit k = stage k, 0x1F = all, 0 = off); orbx_profile_read waits for the recorded events and
+ * returns the summed milliseconds per stage (ms[5], 0 for stages not in the mask) and the
+ * number of profiled extraction calls. */
 int orbx_profile_enable(orbx_handle* h, int on);
 int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls);
 
