@@ -380,6 +380,9 @@ struct orbx_handle {
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
     // host-path staging
     DevBuf in_frame, out_kps, out_desc, out_cnt;
+    // orbx_compute_stereo_matches staging (host path) and k_stereo's LDS attribute
+    DevBuf st_buf;
+    int stereo_lds_set = 0;
     // last extraction, for orbx_pyramid_level
     const uint8_t* last_frames = nullptr;
     long long last_fstride = 0;
@@ -587,7 +590,7 @@ void orbx_destroy(orbx_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->side) (void)hipStreamSynchronize(h->side);
     for (DevBuf* b : {&h->pyr, &h->blur, &h->cellkey, &h->cellcnt, &h->lvkey, &h->lvcnt, &h->gscratch, &h->err,
-                      &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt})
+                      &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt, &h->st_buf})
         b->release();
     h->geo.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -749,6 +752,129 @@ int orbx_pack_keyframe_device(const orbx_kp* d_kps, const uint8_t* d_desc, const
                               uint8_t* d_slot, void* stream) {
     if (!d_kps || !d_desc || !d_count || !d_slot || cap < 1) return ORBX_EARG;
     HIPR(launch_pack_slot(d_kps, d_desc, d_count, (cap + 1) & ~1, d_slot, (hipStream_t)stream));
+    return 0;
+}
+
+}  // extern "C"
+
+/* ===================================================================================== */
+/* Frame::ComputeStereoMatches (ORB_SLAM2.1/src/Frame.cc:470-641)                         */
+/* ===================================================================================== */
+static int stereo_args(orbx_handle* hl, orbx_handle* hr, float bf, float b, StereoArgs* a) {
+    if (!hl || !hr || !hl->last_frames || !hr->last_frames || hl->geo.W != hr->geo.W || hl->geo.H != hr->geo.H ||
+        hl->T.nlevels != hr->T.nlevels || hl->device != hr->device)
+        return ORBX_EARG;
+    for (int l = 0; l < hl->T.nlevels; l++)
+        if (hl->T.scale[l] != hr->T.scale[l]) return ORBX_EARG;
+    const Geometry& g = hl->geo;
+    const int L = hl->T.nlevels;
+    memset(a, 0, sizeof(*a));
+    a->left = PyrSide{hl->last_frames, hl->last_fstride, hl->pyr.as<uint8_t>(), g.ep.pyr_frame_bytes, hl->last_pitch,
+                      hl->last_nframes};
+    a->right = PyrSide{hr->last_frames, hr->last_fstride, hr->pyr.as<uint8_t>(), hr->geo.ep.pyr_frame_bytes,
+                       hr->last_pitch, hr->last_nframes};
+    a->L = L;
+    a->nrows = g.H;
+    // maxr - minr = ceil(y + r) - floor(y - r) <= 2r + 2, r = 2*mvScaleFactors[octave]
+    a->rspan = (int)std::ceil(4.0 * hl->T.scale[L - 1]) + 3;
+    const float minZ = b;  // Frame.cc:501-503
+    a->maxD = bf / minZ;
+    a->bf = bf;
+    volatile float c15 = 1.5f, c14 = 1.4f;
+    a->thc = c15 * c14;  // 1.5f*1.4f (Frame.cc:639)
+    for (int l = 0; l < L; l++) {
+        a->scale[l] = hl->T.scale[l];
+        a->inv_scale[l] = hl->T.inv_scale[l];
+        a->lw[l] = g.lv[l].w;
+        a->lh[l] = g.lv[l].h;
+        a->lpitch[l] = g.lv[l].pitch;
+        a->pyr_off[l] = g.lv[l].pyr_off;
+    }
+    return 0;
+}
+
+static int stereo_prepare(orbx_handle* hl, int stride) {
+    if (stride < 1 || stride > 65535) return ORBX_EARG;
+    const int lds = stereo_lds_bytes(stride, hl->geo.H);
+    if (lds > 160 * 1024) return ORBX_EARG;
+    if (lds > 64 * 1024 && lds > hl->stereo_lds_set) {
+        HIPR(stereo_setup(lds));
+        hl->stereo_lds_set = lds;
+    }
+    return 0;
+}
+
+extern "C" {
+
+int orbx_stereo_matches_batch_device(orbx_handle* left, orbx_handle* right, int npairs, const int32_t* d_fl,
+                                     const int32_t* d_fr, const orbx_kp* d_kpsL, const uint8_t* d_descL,
+                                     const int32_t* d_cntL, const orbx_kp* d_kpsR, const uint8_t* d_descR,
+                                     const int32_t* d_cntR, int kp_stride, float bf, float b, float* d_uright,
+                                     float* d_depth, int32_t* d_nstereo, void* stream) {
+    if (npairs < 0 || !d_fl || !d_fr || !d_kpsL || !d_descL || !d_cntL || !d_kpsR || !d_descR || !d_cntR ||
+        !d_uright || !d_depth || !d_nstereo || !(b > 0.f))
+        return ORBX_EARG;
+    StereoArgs a;
+    int rc = stereo_args(left, right, bf, b, &a);
+    if (rc) return rc;
+    if (npairs == 0) return 0;
+    HIPR(hipSetDevice(left->device));
+    if ((rc = stereo_prepare(left, kp_stride))) return rc;
+    HIPR(launch_stereo(a, npairs, d_fl, d_fr, d_kpsL, d_descL, d_cntL, d_kpsR, d_descR, d_cntR, kp_stride, d_uright,
+                       d_depth, d_nstereo, left->err.as<int>(), (hipStream_t)stream));
+    return 0;
+}
+
+int orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orbx_kp* kpsL, const uint8_t* descL,
+                                int nL, const orbx_kp* kpsR, const uint8_t* descR, int nR, float bf, float b,
+                                float* uright, float* depth, int* nstereo) {
+    if (!left || !right || left == right || nL < 0 || nR < 0 || (nL && (!kpsL || !descL || !uright || !depth)) ||
+        (nR && (!kpsR || !descR)) || !(b > 0.f))
+        return ORBX_EARG;
+    StereoArgs a;
+    int rc = stereo_args(left, right, bf, b, &a);
+    if (rc) return rc;
+    if (left->last_nframes < 1 || right->last_nframes < 1) return ORBX_EARG;
+    if (nstereo) *nstereo = 0;
+    if (nL == 0) return 0;
+    HIPR(hipSetDevice(left->device));
+    const int stride = (int)align_up(std::max(nL, nR), 4);
+    if ((rc = stereo_prepare(left, stride))) return rc;
+    // staging: kpsL | kpsR | descL | descR | uright | depth | {fl=0, fr=0, cntL, cntR, nstereo}
+    const size_t kb = sizeof(orbx_kp) * stride, db = 32 * (size_t)stride, fb = 4 * (size_t)stride;
+    if (left->st_buf.ensure(2 * kb + 2 * db + 2 * fb + 64)) return ORBX_EDEVICE;
+    uint8_t* base = left->st_buf.as<uint8_t>();
+    orbx_kp* dkL = (orbx_kp*)base;
+    orbx_kp* dkR = (orbx_kp*)(base + kb);
+    uint8_t* ddL = base + 2 * kb;
+    uint8_t* ddR = ddL + db;
+    float* dur = (float*)(ddR + db);
+    float* ddp = dur + stride;
+    int32_t* misc = (int32_t*)(ddp + stride);
+    const int32_t hm[4] = {0, 0, nL, nR};
+    hipStream_t st = left->stream;
+    // the right extraction ran on the right handle's stream
+    HIPR(hipStreamSynchronize(right->stream));
+    HIPR(hipMemcpyAsync(dkL, kpsL, sizeof(orbx_kp) * nL, hipMemcpyHostToDevice, st));
+    HIPR(hipMemcpyAsync(ddL, descL, 32 * (size_t)nL, hipMemcpyHostToDevice, st));
+    if (nR) {
+        HIPR(hipMemcpyAsync(dkR, kpsR, sizeof(orbx_kp) * nR, hipMemcpyHostToDevice, st));
+        HIPR(hipMemcpyAsync(ddR, descR, 32 * (size_t)nR, hipMemcpyHostToDevice, st));
+    }
+    HIPR(hipMemcpyAsync(misc, hm, sizeof(hm), hipMemcpyHostToDevice, st));
+    HIPR(hipMemsetAsync(left->err.p, 0, sizeof(int), st));
+    a.left.nframes = a.right.nframes = 1;
+    HIPR(launch_stereo(a, 1, misc, misc + 1, dkL, ddL, misc + 2, dkR, ddR, misc + 3, stride, dur, ddp, misc + 4,
+                       left->err.as<int>(), st));
+    int flag = 0, ns = 0;
+    HIPR(hipMemcpyAsync(uright, dur, 4 * (size_t)nL, hipMemcpyDeviceToHost, st));
+    HIPR(hipMemcpyAsync(depth, ddp, 4 * (size_t)nL, hipMemcpyDeviceToHost, st));
+    HIPR(hipMemcpyAsync(&ns, misc + 4, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPR(hipMemcpyAsync(&flag, left->err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPR(hipStreamSynchronize(st));
+    if (flag & 2) return ORBX_EARG;
+    if (flag) return ORBX_EDEVICE;
+    if (nstereo) *nstereo = ns;
     return 0;
 }
 

@@ -5,6 +5,7 @@
 
 #include "../../include/orbslam_amd.h"
 #include "orb_device.h"
+#include "orb_frame.h"
 #include "orb_match.h"
 
 namespace orbamd {
@@ -54,5 +55,12 @@ hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* task
                       float nnratio, int mode, int32_t* out, hipStream_t st);
 hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* angB, int swap, int32_t* nout,
                              hipStream_t st);
+
+int stereo_lds_bytes(int cap, int nrows);
+hipError_t stereo_setup(int lds_bytes);
+hipError_t launch_stereo(const StereoArgs& a, int npairs, const int32_t* fl, const int32_t* fr, const orbx_kp* kpsL,
+                         const uint8_t* descL, const int32_t* cntL, const orbx_kp* kpsR, const uint8_t* descR,
+                         const int32_t* cntR, int stride, float* uright, float* depth, int32_t* nstereo, int* err,
+                         hipStream_t st);
 
 }  // namespace orbamd

@@ -65,19 +65,24 @@ static uint8_t* make_texture(int agent, int tw, int th) {
     return t;
 }
 
-int orbx_synth_frames(int agent, int t0, int count, int width, int height, uint8_t* out) {
-    if (width <= 0 || height <= 0 || count < 0 || !out || agent < 0 || t0 < 0) return ORBX_EARG;
+int orbx_synth_frames_shifted(int agent, int t0, int count, int width, int height, int dx, uint8_t* out) {
+    if (width <= 0 || height <= 0 || count < 0 || !out || agent < 0 || t0 < 0 || dx < 0 || dx > 26)
+        return ORBX_EARG;
     const int tw = width + 640, th = height + 32;
     uint8_t* tex = make_texture(agent, tw, th);
     if (!tex) return ORBX_EARG;
     for (int f = 0; f < count; f++) {
         int t = t0 + f;
-        int ox = 16 + (2 * t) % 600, oy = 8 + t % 7;
+        int ox = 16 + (2 * t) % 600 + dx, oy = 8 + t % 7;
         for (int y = 0; y < height; y++)
             memcpy(out + ((size_t)f * height + y) * width, tex + (size_t)(oy + y) * tw + ox, (size_t)width);
     }
     free(tex);
     return ORBX_OK;
+}
+
+int orbx_synth_frames(int agent, int t0, int count, int width, int height, uint8_t* out) {
+    return orbx_synth_frames_shifted(agent, t0, count, width, height, 0, out);
 }
 
 int orbx_synth_frame(int agent, int t, int width, int height, uint8_t* out) {

@@ -70,6 +70,10 @@ SIGNATURES = {
     "orbx_pack_keyframe_device": (_I, [_P, _P, _P, _I, _P, _P]),
     "orbx_synth_frame": (_I, [_I, _I, _I, _I, _P]),
     "orbx_synth_frames": (_I, [_I, _I, _I, _I, _I, _P]),
+    "orbx_synth_frames_shifted": (_I, [_I, _I, _I, _I, _I, _I, _P]),
+    "orbx_compute_stereo_matches": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _P, _P, C.POINTER(_I)]),
+    "orbx_stereo_matches_batch_device": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _P, _P, _P,
+                                              _P]),
     "orbx_check_error": (_I, [_P, _P]),
     "orbx_selftest_sincosf": (_I, [_P, _P, _P, _I, _P]),
     "orbx_profile_enable": (_I, [_P, _I]),

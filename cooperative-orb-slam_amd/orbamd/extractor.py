@@ -14,11 +14,13 @@ from ._lib import KP_FIELDS, OrbxParams, check, load
 kp_dtype = np.dtype(KP_FIELDS)
 
 
-def synth_frames(agent, t0, count, width, height):
-    """Deterministic synthetic frames; returns uint8 [count, H, W]."""
+def synth_frames(agent, t0, count, width, height, dx=0):
+    """Deterministic synthetic frames; returns uint8 [count, H, W]. dx > 0 gives the
+    right image of a rectified stereo pair (the same crop shifted by dx px: disparity dx)."""
     lib = load()
     out = np.empty((count, height, width), np.uint8)
-    check(lib.orbx_synth_frames(agent, t0, count, width, height, out.ctypes.data), "orbx_synth_frames")
+    check(lib.orbx_synth_frames_shifted(agent, t0, count, width, height, dx, out.ctypes.data),
+          "orbx_synth_frames_shifted")
     return out
 
 

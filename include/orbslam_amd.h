@@ -198,12 +198,49 @@ int orbx_pack_keyframe_device(const orbx_kp* d_kps, const uint8_t* d_desc,
                               const int32_t* d_count, int cap, uint8_t* d_slot, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * Stereo -- replaces Frame::ComputeStereoMatches (ORB_SLAM2.1/src/Frame.cc:470-641, the
+ * stereo Frame constructor's step after ExtractORB(0/1), Frame.cc:80-98), reading the two
+ * extractors' pyramids (mpORBextractorLeft/Right->mvImagePyramid) where they already live.
+ * mvScaleFactors / mvInvScaleFactors come from `left`; both handles must have the same
+ * frame size and ORB parameters. bf = mbf, b = mb (Frame.cc:501-503).
+ * ---------------------------------------------------------------------------------- */
+
+/* Host form: kpsL/descL (mvKeys, mDescriptors) and kpsR/descR (mvKeysRight,
+ * mDescriptorsRight) are the outputs of the latest orbx_extract on `left` and `right`
+ * (two distinct handles, like the two ORBextractor instances). Writes mvuRight and
+ * mvDepth (nL floats, -1 = no stereo match) and the number of stereo matches kept.
+ * ORBX_EARG where the reference would throw (an 11x11 correlation window outside the level:
+ * cv::Mat::rowRange/colRange assert). */
+int orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orbx_kp* kpsL,
+                                const uint8_t* descL, int nL, const orbx_kp* kpsR,
+                                const uint8_t* descR, int nR, float bf, float b, float* uright,
+                                float* depth, int* nstereo);
+
+/* Device batch form: pair p = frame d_fl[p] of the latest orbx_extract_batch_device on
+ * `left` with frame d_fr[p] of the latest one on `right` (left == right allowed, e.g. a
+ * batch holding left and right images). Keypoints/descriptors/counts as produced by those
+ * extractions (frame f at f*kp_stride). Outputs: d_uright/d_depth[p*kp_stride + i],
+ * d_nstereo[p]. A window outside the level sets the device error flag (orbx_check_error on
+ * `left`). Enqueued on `stream` after both extractions (the caller orders the streams). */
+int orbx_stereo_matches_batch_device(orbx_handle* left, orbx_handle* right, int npairs,
+                                     const int32_t* d_fl, const int32_t* d_fr,
+                                     const orbx_kp* d_kpsL, const uint8_t* d_descL,
+                                     const int32_t* d_cntL, const orbx_kp* d_kpsR,
+                                     const uint8_t* d_descR, const int32_t* d_cntR, int kp_stride,
+                                     float bf, float b, float* d_uright, float* d_depth,
+                                     int32_t* d_nstereo, void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Synthetic input: deterministic frame t of agent a, width x height,
  * written to host out (pitch = width). Identical on every machine (integer-only).
  * ---------------------------------------------------------------------------------- */
 int orbx_synth_frame(int agent, int t, int width, int height, uint8_t* out);
 /* frames t0 .. t0+count-1 of agent a, back to back (frame stride width*height). */
 int orbx_synth_frames(int agent, int t0, int count, int width, int height, uint8_t* out);
+/* right image of a rectified stereo rig for the same frames: the crop shifted by +dx pixels
+ * in x (0 <= dx <= 26), i.e. a fronto-parallel scene at disparity dx. */
+int orbx_synth_frames_shifted(int agent, int t0, int count, int width, int height, int dx,
+                              uint8_t* out);
 
 /* Stage profiling: a pair of HIP events brackets each stage's kernel on the stream it is
  * launched on (the overlapped schedule is kept, so a stage's time includes sharing the GPU

@@ -51,6 +51,7 @@ _SIG = {
     "oc_search_for_triangulation": (_I, [C.POINTER(_View), C.POINTER(_View), _P, _F, _F, _I, _I, _P]),
     "oc_search_by_bow_kf_f": (_I, [C.POINTER(_View), C.POINTER(_View), _F, _I, _P]),
     "oc_search_by_bow_kf_kf": (_I, [C.POINTER(_View), C.POINTER(_View), _F, _I, _P]),
+    "oc_compute_stereo_matches": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _P, _P]),
 }
 
 _lib = None
@@ -222,3 +223,22 @@ def search_by_bow(kf, other, nnratio, check_ori, other_is_keyframe=False):
     out = np.empty(max(other.n, 1), np.int32)
     n = lib.oc_search_by_bow_kf_f(C.byref(a), C.byref(b), nnratio, int(check_ori), out.ctypes.data)
     return n, out[:other.n]
+
+
+def compute_stereo_matches(left, right, kpsL, descL, kpsR, descR, mbf, mb):
+    """Frame::ComputeStereoMatches (Frame.cc:470-641) on the pyramids of the last call of the two
+    OracleExtractor instances. Returns (mvuRight, mvDepth, number kept); raises where the reference throws."""
+    lib = load()
+    kpsL = np.ascontiguousarray(kpsL)
+    kpsR = np.ascontiguousarray(kpsR)
+    dL = np.ascontiguousarray(descL, np.uint8)
+    dR = np.ascontiguousarray(descR, np.uint8)
+    n = len(kpsL)
+    ur = np.empty(max(n, 1), np.float32)
+    dp = np.empty(max(n, 1), np.float32)
+    rc = lib.oc_compute_stereo_matches(left.h, right.h, kpsL.ctypes.data, dL.ctypes.data, n, kpsR.ctypes.data,
+                                       dR.ctypes.data, len(kpsR), float(mbf), float(mb), ur.ctypes.data,
+                                       dp.ctypes.data)
+    if rc < 0:
+        raise RuntimeError("oc_compute_stereo_matches rc=%d" % rc)
+    return ur[:n], dp[:n], rc

@@ -68,6 +68,11 @@ int oc_search_by_bow_kf_f(const orbm_kf_view* kf, const orbm_kf_view* f, float n
 int oc_search_by_bow_kf_kf(const orbm_kf_view* kf1, const orbm_kf_view* kf2, float nnratio,
                            int check_ori, int32_t* match12);
 
+/* Frame-level consumers (orb_oracle_frame.c) */
+int oc_compute_stereo_matches(const oc_extractor* left, const oc_extractor* right, const orbx_kp* kpsL,
+                              const uint8_t* descL, int N, const orbx_kp* kpsR, const uint8_t* descR, int Nr,
+                              float mbf, float mb, float* uright, float* depth);
+
 #ifdef __cplusplus
 }
 #endif
