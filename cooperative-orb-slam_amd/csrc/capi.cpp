@@ -1173,3 +1173,300 @@ int orbm_triangulation_bf_packed_device(orbm_ctx* ctx, const orbx_kp* d_kps1, co
 }
 
 }  // extern "C"
+
+/* ===================================================================================== */
+/* SearchByProjection x4: host prologues (per-MapPoint geometry with the reference's float  */
+/* semantics) + the device grid / windowed search / claim resolution (frame_kernels.hip)    */
+/* ===================================================================================== */
+namespace {
+
+/* cv::Mat float arithmetic as pinned in DESIGN.md (identical to the oracle's restatement):
+ * A*x + c (3x3 by 3x1, flags 0) = OpenCV's small-matrix gemm path: float products and sums,
+ * then (float)(t*alpha + c*beta) in double; A.t()*x (GEMM_1_T) = generic path, double
+ * accumulation; norm/dot accumulate in double. */
+void gemm33_fast(const float* A, int astep, const float* x, const float* c, float* d) {
+    for (int i = 0; i < 3; i++) {
+        const float* a = A + i * astep;
+        const float t0 = a[0] * x[0] + a[1] * x[1] + a[2] * x[2];
+        d[i] = (float)((double)t0 * 1.0 + (double)c[i] * 1.0);
+    }
+}
+void gemm33t_neg(const float* A, int astep, const float* x, float* d) {
+    for (int i = 0; i < 3; i++) {
+        double s = 0;
+        for (int k = 0; k < 3; k++) s += (double)A[k * astep + i] * (double)x[k];
+        d[i] = (float)(-1.0 * s);
+    }
+}
+float norm3(const float* v) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)v[k] * (double)v[k];
+    return (float)std::sqrt(s);
+}
+double dot3(const float* a, const float* b) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)a[k] * (double)b[k];
+    return s;
+}
+/* MapPoint::PredictScale (MapPoint.cc:385-417); log of a float = logf (pinned) */
+int predict_scale(float max_dist, float currentDist, const orbm_frame_view* F) {
+    const float ratio = max_dist / currentDist;
+    int nScale = (int)std::ceil(logf(ratio) / F->log_scale_factor);
+    if (nScale < 0)
+        nScale = 0;
+    else if (nScale >= F->nlevels)
+        nScale = F->nlevels - 1;
+    return nScale;
+}
+inline bool flag(const uint8_t* a, int i) { return a && a[i]; }
+
+struct ProjBatch {
+    std::vector<ProjQuery> q;
+    std::vector<uint8_t> qdesc;
+    void add(const ProjQuery& pq, const uint8_t* d) {
+        q.push_back(pq);
+        qdesc.insert(qdesc.end(), d, d + 32);
+    }
+};
+
+bool frame_view_ok(const orbm_frame_view* F) {
+    return F && F->n >= 0 && F->n < 65536 && F->nlevels >= 1 && F->nlevels <= 16 && F->scale_factors &&
+           (F->n == 0 || (F->desc && F->x && F->y && F->octave));
+}
+
+/* uploads the Frame side + queries, runs k_grid / k_proj_scan / k_proj_resolve, downloads */
+int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb, int accept_th, int ratio,
+                   float nnratio, int check_ori, int32_t* match, int* nmatches) {
+    HIPR(hipSetDevice(ctx->device));
+    const size_t n = (size_t)F->n, nq = pb.q.size();
+    Carve cv;
+    const size_t o_x = cv.take(4 * n), o_y = cv.take(4 * n), o_ang = cv.take(4 * n), o_ur = cv.take(4 * n),
+                 o_oct = cv.take(4 * n), o_occ = cv.take(n), o_desc = cv.take(32 * n),
+                 o_q = cv.take(sizeof(ProjQuery) * nq), o_qd = cv.take(32 * nq),
+                 o_gs = cv.take(4 * (kGridCols * kGridRows + 1)), o_gi = cv.take(2 * n), o_scan = cv.take(16 * nq),
+                 o_res = cv.take(8 * nq), o_match = cv.take(4 * n), o_nm = cv.take(4),
+                 o_call = cv.take(sizeof(ProjCall));
+    if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
+    uint8_t* base = ctx->scratch.as<uint8_t>();
+    hipStream_t st = ctx->stream;
+    ProjCall c;
+    memset(&c, 0, sizeof(c));
+    c.x = (const float*)(base + o_x);
+    c.y = (const float*)(base + o_y);
+    c.angle = (const float*)(base + o_ang);
+    c.uright = F->uright ? (const float*)(base + o_ur) : nullptr;
+    c.octave = (const int32_t*)(base + o_oct);
+    c.occ0 = F->occupied ? base + o_occ : nullptr;
+    c.desc = base + o_desc;
+    c.n = F->n;
+    c.min_x = F->min_x;
+    c.min_y = F->min_y;
+    c.gw_inv = F->grid_w_inv;
+    c.gh_inv = F->grid_h_inv;
+    c.q = (const ProjQuery*)(base + o_q);
+    c.qdesc = base + o_qd;
+    c.nq = (int)nq;
+    c.accept_th = accept_th;
+    c.ratio = ratio;
+    c.nnratio = nnratio;
+    c.check_ori = check_ori && F->angle;
+    c.grid_start = (int*)(base + o_gs);
+    c.grid_idx = (uint16_t*)(base + o_gi);
+    c.scan = (unsigned long long*)(base + o_scan);
+    c.res = (int*)(base + o_res);
+    c.match = (int32_t*)(base + o_match);
+    c.nmatches = (int32_t*)(base + o_nm);
+    if (n) {
+        HIPR(hipMemcpyAsync(base + o_x, F->x, 4 * n, hipMemcpyHostToDevice, st));
+        HIPR(hipMemcpyAsync(base + o_y, F->y, 4 * n, hipMemcpyHostToDevice, st));
+        if (F->angle) HIPR(hipMemcpyAsync(base + o_ang, F->angle, 4 * n, hipMemcpyHostToDevice, st));
+        if (F->uright) HIPR(hipMemcpyAsync(base + o_ur, F->uright, 4 * n, hipMemcpyHostToDevice, st));
+        HIPR(hipMemcpyAsync(base + o_oct, F->octave, 4 * n, hipMemcpyHostToDevice, st));
+        if (F->occupied) HIPR(hipMemcpyAsync(base + o_occ, F->occupied, n, hipMemcpyHostToDevice, st));
+        HIPR(hipMemcpyAsync(base + o_desc, F->desc, 32 * n, hipMemcpyHostToDevice, st));
+    }
+    if (nq) {
+        HIPR(hipMemcpyAsync(base + o_q, pb.q.data(), sizeof(ProjQuery) * nq, hipMemcpyHostToDevice, st));
+        HIPR(hipMemcpyAsync(base + o_qd, pb.qdesc.data(), 32 * nq, hipMemcpyHostToDevice, st));
+    }
+    HIPR(hipMemcpyAsync(base + o_call, &c, sizeof(c), hipMemcpyHostToDevice, st));
+    HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st));
+    int nm = 0;
+    if (n) HIPR(hipMemcpyAsync(match, c.match, 4 * n, hipMemcpyDeviceToHost, st));
+    HIPR(hipMemcpyAsync(&nm, c.nmatches, 4, hipMemcpyDeviceToHost, st));
+    HIPR(hipStreamSynchronize(st));
+    if (nmatches) *nmatches = nm;
+    return 0;
+}
+
+ProjQuery make_query(float u, float v, float radius, int minl, int maxl, float ur, float er_th, float angle, int flags,
+                     int src) {
+    ProjQuery q;
+    q.u = u;
+    q.v = v;
+    q.radius = radius;
+    q.min_level = minl;
+    q.max_level = maxl;
+    q.ur = ur;
+    q.er_th = er_th;
+    q.angle = angle;
+    q.flags = flags | kProjValid;
+    q.src = src;
+    return q;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbm_search_by_projection_local(orbm_ctx* ctx, const orbm_frame_view* F, const orbm_mappoints* mp, float th,
+                                    float nnratio, int32_t* match, int* nmatches) {
+    if (!ctx || !frame_view_ok(F) || !mp || mp->n < 0 || (mp->n && (!mp->desc || !mp->track_in_view ||
+        !mp->track_proj_x || !mp->track_proj_y || !mp->track_proj_xr || !mp->track_level || !mp->track_view_cos)) ||
+        (F->n && !match))
+        return ORBX_EARG;
+    ProjBatch pb;
+    const bool bFactor = th != 1.0;  // ORBmatcher.cc:49
+    for (int iMP = 0; iMP < mp->n; iMP++) {
+        if (!mp->track_in_view[iMP] || flag(mp->bad, iMP)) continue;
+        const int lvl = mp->track_level[iMP];
+        if (lvl < 0 || lvl >= F->nlevels) return ORBX_EARG;
+        float r = mp->track_view_cos[iMP] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:131-137)
+        if (bFactor) r *= th;
+        const float radius = r * F->scale_factors[lvl];
+        pb.add(make_query(mp->track_proj_x[iMP], mp->track_proj_y[iMP], radius, lvl - 1, lvl, mp->track_proj_xr[iMP],
+                          radius, 0.f, kProjStereo | (flag(mp->has_obs, iMP) ? kProjClaims : 0), iMP),
+               mp->desc + 32 * (size_t)iMP);
+    }
+    return run_projection(ctx, F, pb, 100 /*TH_HIGH*/, 1, nnratio, 0, match, nmatches);
+}
+
+int orbm_search_by_projection_last_frame(orbm_ctx* ctx, const orbm_frame_view* F, const float Tcw_c[16],
+                                         const orbm_mappoints* mp, const float Tcw_l[16], float th, int bMono,
+                                         int check_ori, int32_t* match, int* nmatches) {
+    if (!ctx || !frame_view_ok(F) || !Tcw_c || !Tcw_l || !mp || mp->n < 0 ||
+        (mp->n && (!mp->desc || !mp->pos || !mp->octave || (check_ori && !mp->angle))) || (F->n && !match) ||
+        (check_ori && !F->angle))
+        return ORBX_EARG;
+    const float* Rcw = Tcw_c;  // ORBmatcher.cc:1339-1351
+    const float tcw[3] = {Tcw_c[3], Tcw_c[7], Tcw_c[11]};
+    float twc[3], tlc[3];
+    gemm33t_neg(Rcw, 4, tcw, twc);
+    const float tlw[3] = {Tcw_l[3], Tcw_l[7], Tcw_l[11]};
+    gemm33_fast(Tcw_l, 4, twc, tlw, tlc);
+    const bool bForward = tlc[2] > F->b && !bMono;
+    const bool bBackward = -tlc[2] > F->b && !bMono;
+    ProjBatch pb;
+    for (int i = 0; i < mp->n; i++) {  // :1353-1405
+        if (flag(mp->skip, i)) continue;
+        float x3Dc[3];
+        gemm33_fast(Rcw, 4, mp->pos + 3 * (size_t)i, tcw, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = 1.0 / x3Dc[2];
+        if (invzc < 0) continue;
+        const float u = F->fx * xc * invzc + F->cx;
+        const float v = F->fy * yc * invzc + F->cy;
+        if (u < F->min_x || u > F->max_x) continue;
+        if (v < F->min_y || v > F->max_y) continue;
+        const int nLastOctave = mp->octave[i];
+        if (nLastOctave < 0 || nLastOctave >= F->nlevels) return ORBX_EARG;
+        const float radius = th * F->scale_factors[nLastOctave];
+        int minl, maxl;
+        if (bForward) {
+            minl = nLastOctave;
+            maxl = -1;
+        } else if (bBackward) {
+            minl = 0;
+            maxl = nLastOctave;
+        } else {
+            minl = nLastOctave - 1;
+            maxl = nLastOctave + 1;
+        }
+        const float ur = u - F->bf * invzc;
+        pb.add(make_query(u, v, radius, minl, maxl, ur, radius, mp->angle ? mp->angle[i] : 0.f,
+                          kProjStereo | (flag(mp->has_obs, i) ? kProjClaims : 0), i),
+               mp->desc + 32 * (size_t)i);
+    }
+    return run_projection(ctx, F, pb, 100 /*TH_HIGH*/, 0, 0.f, check_ori, match, nmatches);
+}
+
+int orbm_search_by_projection_keyframe(orbm_ctx* ctx, const orbm_frame_view* F, const float Tcw_c[16],
+                                       const orbm_mappoints* mp, float th, int orb_dist, int check_ori,
+                                       int32_t* match, int* nmatches) {
+    if (!ctx || !frame_view_ok(F) || !Tcw_c || !mp || mp->n < 0 ||
+        (mp->n && (!mp->desc || !mp->pos || !mp->min_dist || !mp->max_dist || (check_ori && !mp->angle))) ||
+        (F->n && !match) || (check_ori && !F->angle))
+        return ORBX_EARG;
+    const float* Rcw = Tcw_c;  // ORBmatcher.cc:1476-1478
+    const float tcw[3] = {Tcw_c[3], Tcw_c[7], Tcw_c[11]};
+    float Ow[3];
+    gemm33t_neg(Rcw, 4, tcw, Ow);
+    ProjBatch pb;
+    for (int i = 0; i < mp->n; i++) {  // :1488-1537
+        if (flag(mp->skip, i) || flag(mp->bad, i)) continue;
+        const float* x3Dw = mp->pos + 3 * (size_t)i;
+        float x3Dc[3];
+        gemm33_fast(Rcw, 4, x3Dw, tcw, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = 1.0 / x3Dc[2];
+        const float u = F->fx * xc * invzc + F->cx;
+        const float v = F->fy * yc * invzc + F->cy;
+        if (u < F->min_x || u > F->max_x) continue;
+        if (v < F->min_y || v > F->max_y) continue;
+        const float PO[3] = {x3Dw[0] - Ow[0], x3Dw[1] - Ow[1], x3Dw[2] - Ow[2]};
+        const float dist3D = norm3(PO);
+        const float maxDistance = 1.2f * mp->max_dist[i];
+        const float minDistance = 0.8f * mp->min_dist[i];
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[i], dist3D, F);
+        const float radius = th * F->scale_factors[nPredictedLevel];
+        pb.add(make_query(u, v, radius, nPredictedLevel - 1, nPredictedLevel + 1, 0.f, -1.f,
+                          mp->angle ? mp->angle[i] : 0.f, kProjClaims, i),
+               mp->desc + 32 * (size_t)i);
+    }
+    return run_projection(ctx, F, pb, orb_dist, 0, 0.f, check_ori, match, nmatches);
+}
+
+int orbm_search_by_projection_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, const float Scw[16],
+                                   const orbm_mappoints* mp, int th, int32_t* match, int* nmatches) {
+    if (!ctx || !frame_view_ok(KF) || !Scw || !mp || mp->n < 0 ||
+        (mp->n && (!mp->desc || !mp->pos || !mp->normal || !mp->min_dist || !mp->max_dist)) || (KF->n && !match))
+        return ORBX_EARG;
+    // decompose Scw (ORBmatcher.cc:298-304): sRcw/scw and t/scw are convertTo with scale (float)(1./scw)
+    const float scw = (float)std::sqrt(dot3(Scw, Scw));
+    const float inv = (float)(1. / (double)scw);
+    float Rcw[9], tcw[3], Ow[3];
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) Rcw[3 * r + c] = Scw[4 * r + c] * inv;
+        tcw[r] = Scw[4 * r + 3] * inv;
+    }
+    gemm33t_neg(Rcw, 3, tcw, Ow);
+    ProjBatch pb;
+    for (int iMP = 0; iMP < mp->n; iMP++) {  // :313-367
+        if (flag(mp->bad, iMP) || flag(mp->skip, iMP)) continue;
+        const float* p3Dw = mp->pos + 3 * (size_t)iMP;
+        float p3Dc[3];
+        gemm33_fast(Rcw, 3, p3Dw, tcw, p3Dc);
+        if (p3Dc[2] < 0.0) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz;
+        const float y = p3Dc[1] * invz;
+        const float u = KF->fx * x + KF->cx;
+        const float v = KF->fy * y + KF->cy;
+        if (!(u >= KF->min_x && u < KF->max_x && v >= KF->min_y && v < KF->max_y)) continue;  // IsInImage
+        const float maxDistance = 1.2f * mp->max_dist[iMP];
+        const float minDistance = 0.8f * mp->min_dist[iMP];
+        const float PO[3] = {p3Dw[0] - Ow[0], p3Dw[1] - Ow[1], p3Dw[2] - Ow[2]};
+        const float dist = norm3(PO);
+        if (dist < minDistance || dist > maxDistance) continue;
+        if (dot3(PO, mp->normal + 3 * (size_t)iMP) < 0.5 * dist) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[iMP], dist, KF);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        // KeyFrame::GetFeaturesInArea has no level test; the caller's kpLevel window (:385-388)
+        pb.add(make_query(u, v, radius, nPredictedLevel - 1, nPredictedLevel, 0.f, -1.f, 0.f, kProjClaims, iMP),
+               mp->desc + 32 * (size_t)iMP);
+    }
+    return run_projection(ctx, KF, pb, 50 /*TH_LOW*/, 0, 0.f, 0, match, nmatches);
+}
+
+}  // extern "C"

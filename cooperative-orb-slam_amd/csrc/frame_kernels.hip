@@ -11,6 +11,21 @@
  *              LDS (integers: exact, as cv::norm's double sum of integer-valued floats is),
  *              the parabola fit in IEEE float (no contraction), then the per-frame median
  *              rejection (Frame.cc:636-650) as an LDS radix select.
+ *   k_grid     Frame::AssignFeaturesToGrid (Frame.cc:235-250, PosInGrid 391-401): CSR cell lists
+ *              (counting sort in LDS; order inside a cell is free, see k_proj_scan).
+ *   k_proj_scan / k_proj_resolve
+ *              SearchByProjection x4 (ORBmatcher.cc:45-129, 290-403, 1328-1470, 1472-1599) with
+ *              GetFeaturesInArea (Frame.cc:332-389, KeyFrame.cc:569-608). The scan gives every
+ *              MapPoint query 16 lanes over the window's grid cells and keeps the best and
+ *              second-best candidate as 64-bit keys (dist, window cell order, feature index):
+ *              the reference's scan order is (cell, position in cell), position in a cell is
+ *              ascending feature index, so the minimum key is its first strict minimum and the
+ *              next key its `bestDist2` element. Matching assigns F.mvpMapPoints in MapPoint
+ *              order and later MapPoints skip occupied features; a claim can only change a
+ *              later result if it takes that query's best or second element, so the resolve
+ *              wave commits 64 queries at a time up to the first such conflict, re-scans that
+ *              one query against the live occupancy bitmap, and continues. Then the rotation
+ *              histogram + ComputeThreeMaxima (ORBmatcher.cc:1437-1467, 1601-1642).
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -308,6 +323,319 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
     if (kept) atomicAdd(&s_misc[4], kept);
     __syncthreads();
     if (tid == 0) nstereo[p] = s_misc[4];
+}
+
+/* ============================ SearchByProjection ============================ */
+
+constexpr unsigned long long kNoKey = ~0ull;
+
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int o) {
+    const int lo = __shfl_xor((int)(uint32_t)v, o), hi = __shfl_xor((int)(uint32_t)(v >> 32), o);
+    return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ void keep2(unsigned long long k, unsigned long long& b, unsigned long long& s) {
+    if (k < b) {
+        s = b;
+        b = k;
+    } else if (k < s) {
+        s = k;
+    }
+}
+
+/* block-wide exclusive scan of one int per thread (1024 threads); returns the exclusive prefix,
+ * *total = sum. s_tmp: 16 ints of LDS. */
+__device__ int block_scan_1024(int v, int* s_tmp, int* total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    if (lane == 63) s_tmp[wv] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int w = 0; w < 16; w++) {
+        const int t = s_tmp[w];
+        off += w < wv ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + incl - v;
+}
+
+/* Frame::AssignFeaturesToGrid (Frame.cc:235-250): cell = posX*48 + posY with PosInGrid's
+ * round((x - mnMinX) * mfGridElementWidthInv) (Frame.cc:391-401) */
+__device__ __forceinline__ int grid_cell(const ProjCall& c, int i) {
+    const int posX = (int)roundf(__fmul_rn(__fsub_rn(c.x[i], c.min_x), c.gw_inv));
+    const int posY = (int)roundf(__fmul_rn(__fsub_rn(c.y[i], c.min_y), c.gh_inv));
+    if (posX < 0 || posX >= kGridCols || posY < 0 || posY >= kGridRows) return -1;
+    return posX * kGridRows + posY;
+}
+
+__global__ __launch_bounds__(1024) void k_grid(const ProjCall* __restrict__ calls) {
+    constexpr int NC = kGridCols * kGridRows;  // 3072 = 3 per thread
+    __shared__ int s_cnt[NC];
+    __shared__ int s_tmp[16];
+    const ProjCall& c = calls[blockIdx.x];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < NC; i += 1024) s_cnt[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < c.n; i += 1024) {
+        const int cell = grid_cell(c, i);
+        if (cell >= 0) atomicAdd(&s_cnt[cell], 1);
+    }
+    __syncthreads();
+    const int a0 = s_cnt[3 * tid], a1 = s_cnt[3 * tid + 1], a2 = s_cnt[3 * tid + 2];
+    int total;
+    const int off = block_scan_1024(a0 + a1 + a2, s_tmp, &total);
+    s_cnt[3 * tid] = off;
+    s_cnt[3 * tid + 1] = off + a0;
+    s_cnt[3 * tid + 2] = off + a0 + a1;
+    c.grid_start[3 * tid] = off;
+    c.grid_start[3 * tid + 1] = off + a0;
+    c.grid_start[3 * tid + 2] = off + a0 + a1;
+    if (tid == 0) c.grid_start[NC] = total;
+    __syncthreads();
+    for (int i = tid; i < c.n; i += 1024) {
+        const int cell = grid_cell(c, i);
+        if (cell >= 0) c.grid_idx[atomicAdd(&s_cnt[cell], 1)] = (uint16_t)i;
+    }
+}
+
+/* GetFeaturesInArea (Frame.cc:332-389) + the per-candidate tests of the variants, G lanes of one
+ * query (gl = lane in group); returns the group's best / second-best keys (all lanes). */
+template <int G, class Occ>
+__device__ __forceinline__ void proj_scan(const ProjCall& c, const ProjQuery& q, const uint4 qd0, const uint4 qd1,
+                                          int gl, Occ occupied, unsigned long long& ob, unsigned long long& os) {
+    unsigned long long b = kNoKey, s = kNoKey;
+    const float r = q.radius;
+    const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(q.u, c.min_x), r), c.gw_inv)));
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(q.u, c.min_x), r), c.gw_inv)));
+    const int nMinCellY = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(q.v, c.min_y), r), c.gh_inv)));
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(q.v, c.min_y), r), c.gh_inv)));
+    if (nMinCellX < kGridCols && nMaxCellX >= 0 && nMinCellY < kGridRows && nMaxCellY >= 0) {
+        const int ny = nMaxCellY - nMinCellY + 1;
+        const int ncell = (nMaxCellX - nMinCellX + 1) * ny;
+        for (int k = gl; k < ncell; k += G) {
+            const int dx = k / ny;
+            const int cell = (nMinCellX + dx) * kGridRows + nMinCellY + (k - dx * ny);
+            const int j1 = c.grid_start[cell + 1];
+            for (int j = c.grid_start[cell]; j < j1; j++) {
+                const int idx = c.grid_idx[j];
+                const int oct = c.octave[idx];
+                if (oct < q.min_level) continue;
+                if (q.max_level >= 0 && oct > q.max_level) continue;
+                if (!(fabsf(__fsub_rn(c.x[idx], q.u)) < r && fabsf(__fsub_rn(c.y[idx], q.v)) < r)) continue;
+                if (occupied(idx)) continue;
+                if ((q.flags & kProjStereo) && c.uright) {
+                    const float urf = c.uright[idx];
+                    if (urf > 0 && fabsf(__fsub_rn(q.ur, urf)) > q.er_th) continue;
+                }
+                const uint4* fd = (const uint4*)(c.desc + (long long)idx * 32);
+                const uint4 f0 = fd[0], f1 = fd[1];
+                const int dist = __popc(qd0.x ^ f0.x) + __popc(qd0.y ^ f0.y) + __popc(qd0.z ^ f0.z) +
+                                 __popc(qd0.w ^ f0.w) + __popc(qd1.x ^ f1.x) + __popc(qd1.y ^ f1.y) +
+                                 __popc(qd1.z ^ f1.z) + __popc(qd1.w ^ f1.w);
+                if (dist < 256)  // bestDist starts at 256 (ORBmatcher.cc:78, 349, 1397, 1550)
+                    keep2(((unsigned long long)dist << 40) | ((unsigned long long)k << 16) | (unsigned)idx, b, s);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) {
+        const unsigned long long b2 = shfl_xor_u64(b, o), s2 = shfl_xor_u64(s, o);
+        const unsigned long long lo = min(b, b2), hi = max(b, b2);
+        b = lo;
+        s = min(hi, min(s, s2));
+    }
+    ob = b;
+    os = s;
+}
+
+__global__ __launch_bounds__(256) void k_proj_scan(const ProjCall* __restrict__ calls) {
+    const ProjCall& c = calls[blockIdx.y];
+    const int qi = blockIdx.x * 16 + (threadIdx.x >> 4), gl = threadIdx.x & 15;
+    if (blockIdx.x * 16 >= c.nq) return;  // block-uniform
+    const bool in = qi < c.nq;
+    ProjQuery q;
+    uint4 qd0 = make_uint4(0, 0, 0, 0), qd1 = qd0;
+    if (in) {
+        q = c.q[qi];
+        const uint4* qd = (const uint4*)(c.qdesc + (long long)qi * 32);
+        qd0 = qd[0];
+        qd1 = qd[1];
+    } else {
+        q.u = q.v = -1e30f;  // empty window
+        q.radius = 0.f;
+        q.flags = 0;
+        q.min_level = 0;
+        q.max_level = -1;
+    }
+    const uint8_t* occ0 = c.occ0;
+    unsigned long long b, s;
+    proj_scan<16>(c, q, qd0, qd1, gl, [occ0](int i) { return occ0 && occ0[i]; }, b, s);
+    if (in && gl == 0) {
+        c.scan[2 * qi] = b;
+        c.scan[2 * qi + 1] = s;
+    }
+}
+
+/* accept rule of the variant: bestDist <= threshold, and for SearchByProjection(F, vpMapPoints)
+ * the ratio test when best and second lie on one level (ORBmatcher.cc:116-125) */
+__device__ __forceinline__ bool proj_accept(const ProjCall& c, unsigned long long b, unsigned long long s) {
+    if (b == kNoKey) return false;
+    const int dist = (int)(b >> 40);
+    if (dist > c.accept_th) return false;
+    if (c.ratio) {
+        const int bi = (int)(b & 0xffff);
+        const int level = c.octave[bi];
+        const int level2 = s != kNoKey ? c.octave[(int)(s & 0xffff)] : -1;
+        const int dist2 = s != kNoKey ? (int)(s >> 40) : 256;
+        if (level == level2 && (float)dist > __fmul_rn(c.nnratio, (float)dist2)) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:1423-1430
+    float rot = __fsub_rn(a1, a2);
+    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+    int bin = (int)roundf(__fmul_rn(rot, 1.0f / 30));
+    if (bin == 30) bin = 0;
+    return min(max(bin, 0), 29);
+}
+
+constexpr int kProjMaxFeatures = 65536;
+
+__global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict__ calls) {
+    __shared__ uint32_t s_occ[kProjMaxFeatures / 32];
+    __shared__ int s_hist[32];
+    const ProjCall& c = calls[blockIdx.x];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < (c.n + 31) / 32; i += 64) {
+        uint32_t w = 0;
+        if (c.occ0)
+            for (int k = 0; k < 32; k++) {
+                const int f = 32 * i + k;
+                if (f < c.n && c.occ0[f]) w |= 1u << k;
+            }
+        s_occ[i] = w;
+    }
+    for (int i = lane; i < c.n; i += 64) c.match[i] = -1;
+    if (lane < 32) s_hist[lane] = 0;
+    __threadfence();
+    wave_lds_sync();
+    auto occ_get = [](int i) { return (s_occ[i >> 5] >> (i & 31)) & 1u; };
+    int nacc = 0;
+    int base = 0;
+    while (base < c.nq) {
+        const int qi = base + lane;
+        const bool in = qi < c.nq;
+        unsigned long long b = kNoKey, s = kNoKey;
+        int flags = 0;
+        if (in) {
+            b = c.scan[2 * qi];
+            s = c.scan[2 * qi + 1];
+            flags = c.q[qi].flags;
+        }
+        const int bi = b != kNoKey ? (int)(b & 0xffff) : -1;
+        const int si = s != kNoKey ? (int)(s & 0xffff) : -1;
+        const bool acc = in && proj_accept(c, b, s);
+        const bool cl = acc && (flags & kProjClaims);
+        bool dirty = in && ((bi >= 0 && occ_get(bi)) || (si >= 0 && occ_get(si)));
+        const int my_claim = cl ? bi : -1;
+        for (int k = 0; k < 63; k++) {
+            const int bk = __shfl(my_claim, k);
+            if (k < lane && bk >= 0 && (bk == bi || bk == si)) dirty = true;
+        }
+        const unsigned long long dm = __ballot(dirty);
+        const int d = dm ? __ffsll((long long)dm) - 1 : 64;
+        if (lane < d && acc) {
+            const ProjQuery& q = c.q[qi];
+            atomicMax(&c.match[bi], q.src);
+            if (cl) atomicOr(&s_occ[bi >> 5], 1u << (bi & 31));
+            c.res[2 * qi] = bi;
+            c.res[2 * qi + 1] = c.check_ori ? rot_bin(q.angle, c.angle[bi]) : 0;
+            nacc++;
+        } else if (lane < d && in) {
+            c.res[2 * qi] = -1;
+        }
+        __threadfence();
+        wave_lds_sync();
+        if (d < 64) {  // re-scan query base+d against the live occupancy (64 lanes)
+            const int qd = base + d;
+            const ProjQuery q = c.q[qd];
+            const uint4* qp = (const uint4*)(c.qdesc + (long long)qd * 32);
+            unsigned long long b2, s2;
+            proj_scan<64>(c, q, qp[0], qp[1], lane, occ_get, b2, s2);
+            const bool acc2 = proj_accept(c, b2, s2);
+            if (lane == 0) {
+                if (acc2) {
+                    const int bi2 = (int)(b2 & 0xffff);
+                    atomicMax(&c.match[bi2], q.src);
+                    if (q.flags & kProjClaims) atomicOr(&s_occ[bi2 >> 5], 1u << (bi2 & 31));
+                    c.res[2 * qd] = bi2;
+                    c.res[2 * qd + 1] = c.check_ori ? rot_bin(q.angle, c.angle[bi2]) : 0;
+                    nacc++;
+                } else {
+                    c.res[2 * qd] = -1;
+                }
+            }
+            __threadfence();
+            wave_lds_sync();
+            base = qd + 1;
+        } else {
+            base += 64;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nacc += __shfl_xor(nacc, o);
+    if (c.check_ori) {  // rotation consistency (ORBmatcher.cc:1437-1467)
+        for (int q = lane; q < c.nq; q += 64)
+            if (c.res[2 * q] >= 0) atomicAdd(&s_hist[c.res[2 * q + 1]], 1);
+        wave_lds_sync();
+        int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;  // ComputeThreeMaxima (:1601-1642)
+        for (int i = 0; i < 30; i++) {
+            const int sz = s_hist[i];
+            if (sz > max1) {
+                max3 = max2; max2 = max1; max1 = sz;
+                ind3 = ind2; ind2 = ind1; ind1 = i;
+            } else if (sz > max2) {
+                max3 = max2; max2 = sz;
+                ind3 = ind2; ind2 = i;
+            } else if (sz > max3) {
+                max3 = sz; ind3 = i;
+            }
+        }
+        if (max2 < __fmul_rn(0.1f, (float)max1)) {
+            ind2 = -1; ind3 = -1;
+        } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
+            ind3 = -1;
+        }
+        int removed = 0;
+        for (int q = lane; q < c.nq; q += 64) {
+            const int f = c.res[2 * q];
+            if (f < 0) continue;
+            const int bin = c.res[2 * q + 1];
+            if (bin != ind1 && bin != ind2 && bin != ind3) {
+                c.match[f] = -2;
+                removed++;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) removed += __shfl_xor(removed, o);
+        nacc -= removed;
+    }
+    if (lane == 0) *c.nmatches = nacc;
+}
+
+hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st) {
+    hipLaunchKernelGGL(k_grid, dim3(ncalls), dim3(1024), 0, st, d_calls);
+    if (max_nq > 0) hipLaunchKernelGGL(k_proj_scan, dim3((max_nq + 15) / 16, ncalls), dim3(256), 0, st, d_calls);
+    hipLaunchKernelGGL(k_proj_resolve, dim3(ncalls), dim3(64), 0, st, d_calls);
+    return hipGetLastError();
 }
 
 int stereo_lds_bytes(int cap, int nrows) { return StereoLds(cap, nrows).total; }

@@ -56,6 +56,7 @@ hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* task
 hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* angB, int swap, int32_t* nout,
                              hipStream_t st);
 
+hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st);
 int stereo_lds_bytes(int cap, int nrows);
 hipError_t stereo_setup(int lds_bytes);
 hipError_t launch_stereo(const StereoArgs& a, int npairs, const int32_t* fl, const int32_t* fr, const orbx_kp* kpsL,

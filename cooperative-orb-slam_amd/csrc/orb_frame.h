@@ -35,4 +35,42 @@ struct StereoArgs {
     long long pyr_off[kMaxLevels];
 };
 
+/* SearchByProjection (ORBmatcher.cc:45-129, 290-403, 1328-1470, 1472-1599): one MapPoint after
+ * the host prologue of its variant (projection, frustum and scale tests) */
+constexpr int kGridCols = 64;  // FRAME_GRID_COLS (Frame.h:38)
+constexpr int kGridRows = 48;  // FRAME_GRID_ROWS (Frame.h:37)
+constexpr int kProjValid = 1, kProjClaims = 2, kProjStereo = 4;
+
+struct ProjQuery {
+    float u, v, radius;        // GetFeaturesInArea(u, v, radius, min_level, max_level)
+    int min_level, max_level;
+    float ur, er_th;           // stereo check: fabs(ur - mvuRight[i]) > er_th rejects (kProjStereo)
+    float angle;               // source keypoint angle (rotation histogram)
+    int flags;                 // kProjValid | kProjClaims (a match occupies the feature) | kProjStereo
+    int src;                   // MapPoint index reported in the output
+};
+
+/* one SearchByProjection call: the Frame/KeyFrame arrays, its queries, scratch and outputs */
+struct ProjCall {
+    const float *x, *y, *angle, *uright;
+    const int32_t* octave;
+    const uint8_t* occ0;       // initial occupancy (NULL = none)
+    const uint8_t* desc;
+    int n;
+    float min_x, min_y, gw_inv, gh_inv;
+    const ProjQuery* q;
+    const uint8_t* qdesc;
+    int nq;
+    int accept_th;             // bestDist <= accept_th
+    int ratio;                 // second-best ratio test when both on one level (ORBmatcher.cc:116-121)
+    float nnratio;
+    int check_ori;
+    int* grid_start;           // [kGridCols*kGridRows + 1]
+    uint16_t* grid_idx;        // [n]
+    unsigned long long* scan;  // [2*nq] best / second keys
+    int* res;                  // [2*nq] accepted feature idx / rotation bin
+    int32_t* match;            // [n]
+    int32_t* nmatches;
+};
+
 }  // namespace orbamd

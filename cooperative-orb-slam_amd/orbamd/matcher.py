@@ -140,3 +140,37 @@ class ORBmatcher:
                                                 int(self.mbCheckOrientation), out.ctypes.data, C.byref(n)),
               "orbm_search_by_bow_kf_f")
         return n.value, out[:other.n]
+
+    # ---- SearchByProjection x4 (ORBmatcher.cc:45-129, 1328-1470, 1472-1599, 290-403). Each returns
+    # (nmatches, match[F.n]): index into the MapPoints of the assignment made to that feature
+    # (last wins), -1 untouched, -2 reset to NULL by the rotation-consistency filter.
+    def _proj(self, fn, F, *args):
+        out = np.empty(max(F.n, 1), np.int32)
+        n = C.c_int()
+        fv = F.cstruct()
+        check(getattr(self._lib, fn)(self._h, C.byref(fv), *args, out.ctypes.data, C.byref(n)), fn)
+        return n.value, out[:F.n]
+
+    def SearchByProjectionLocal(self, F, mps, th=3.0):
+        """SearchByProjection(Frame&, const vector<MapPoint*>&, th): F.occupied = mvpMapPoints[i] with
+        Observations() > 0; mps carry the isInFrustum tracking fields."""
+        m = mps.cstruct()
+        return self._proj("orbm_search_by_projection_local", F, C.byref(m), C.c_float(th), C.c_float(self.mfNNratio))
+
+    def SearchByProjectionLastFrame(self, F, Tcw, last_mps, Tcw_last, th, bMono):
+        m = last_mps.cstruct()
+        T1 = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+        T2 = np.ascontiguousarray(Tcw_last, np.float32).reshape(16)
+        return self._proj("orbm_search_by_projection_last_frame", F, T1.ctypes.data, C.byref(m), T2.ctypes.data,
+                          C.c_float(th), int(bMono), int(self.mbCheckOrientation))
+
+    def SearchByProjectionKeyFrame(self, F, Tcw, kf_mps, th, ORBdist):
+        m = kf_mps.cstruct()
+        T1 = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+        return self._proj("orbm_search_by_projection_keyframe", F, T1.ctypes.data, C.byref(m), C.c_float(th),
+                          int(ORBdist), int(self.mbCheckOrientation))
+
+    def SearchByProjectionSim3(self, KF, Scw, mps, th):
+        m = mps.cstruct()
+        S = np.ascontiguousarray(Scw, np.float32).reshape(16)
+        return self._proj("orbm_search_by_projection_sim3", KF, S.ctypes.data, C.byref(m), int(th))

@@ -189,6 +189,94 @@ void orbm_epipole(const float R2w[9], const float t2w[3], const float Cw[3], flo
                   float cx, float cy, float* ex, float* ey);
 
 /* ------------------------------------------------------------------------------------
+ * SearchByProjection x4 (ORBmatcher.cc:45-129, 1328-1470, 1472-1599, 290-403) with
+ * Frame/KeyFrame::GetFeaturesInArea over the 64x48 feature grid (Frame.cc:235-250,
+ * 332-389; KeyFrame.cc:569-613). The per-MapPoint geometry prologue of each variant
+ * (projection, frustum/scale tests, PredictScale) runs on the host with the reference's
+ * float semantics (DESIGN.md "Pinned semantics"); the grid build, windowed Hamming search
+ * (best / second best), the in-order claim resolution and the rotation histogram run on the
+ * device.
+ * ---------------------------------------------------------------------------------- */
+
+/* The Frame (or KeyFrame) side. */
+typedef struct orbm_frame_view {
+    int32_t n;                    /* N                                                    */
+    const uint8_t* desc;          /* mDescriptors, n x 32                                 */
+    const float* x;               /* mvKeysUn[i].pt.x                                     */
+    const float* y;               /* mvKeysUn[i].pt.y                                     */
+    const int32_t* octave;        /* mvKeysUn[i].octave                                   */
+    const float* angle;           /* mvKeysUn[i].angle (rotation histogram)               */
+    const float* uright;          /* mvuRight; NULL = monocular (all -1)                  */
+    const uint8_t* occupied;      /* the variant's "already matched" test on the state
+                                     before the call (see each entry point); NULL = none  */
+    float min_x, min_y, max_x, max_y;  /* mnMinX, mnMinY, mnMaxX, mnMaxY                  */
+    float grid_w_inv, grid_h_inv;      /* mfGridElementWidthInv, mfGridElementHeightInv   */
+    float fx, fy, cx, cy;              /* camera                                          */
+    float bf, b;                       /* mbf, mb                                         */
+    int32_t nlevels;                   /* mnScaleLevels                                   */
+    const float* scale_factors;        /* mvScaleFactors[nlevels]                         */
+    float log_scale_factor;            /* mfLogScaleFactor                                */
+} orbm_frame_view;
+
+/* The MapPoint side (one entry per candidate MapPoint, in the reference's loop order).
+ * Each entry point documents which arrays it reads; the rest may be NULL. */
+typedef struct orbm_mappoints {
+    int32_t n;
+    const uint8_t* desc;          /* GetDescriptor(), n x 32                              */
+    const float* pos;             /* GetWorldPos(), n x 3                                 */
+    const float* normal;          /* GetNormal(), n x 3                                   */
+    const float* min_dist;        /* mfMinDistance (GetMinDistanceInvariance = 0.8f*it)   */
+    const float* max_dist;        /* mfMaxDistance (GetMaxDistanceInvariance = 1.2f*it)   */
+    const uint8_t* bad;           /* isBad()                                              */
+    const uint8_t* has_obs;       /* Observations() > 0                                   */
+    const uint8_t* skip;          /* entry excluded before any test (see entry points)    */
+    const int32_t* octave;        /* source keypoint octave (SearchByProjection(F, LastF)) */
+    const float* angle;           /* source keypoint angle (rotation histogram)           */
+    /* Tracking fields set by Frame::isInFrustum (Frame.cc:274-330) */
+    const uint8_t* track_in_view; /* mbTrackInView                                        */
+    const float* track_proj_x;    /* mTrackProjX                                          */
+    const float* track_proj_y;    /* mTrackProjY                                          */
+    const float* track_proj_xr;   /* mTrackProjXR                                         */
+    const int32_t* track_level;   /* mnTrackScaleLevel                                    */
+    const float* track_view_cos;  /* mTrackViewCos                                        */
+} orbm_mappoints;
+
+/* Results of every variant: match[view.n] = index (into the orbm_mappoints) of the MapPoint
+ * the call assigned to that feature (the last assignment wins, as in the reference), -1 if
+ * the call left the feature untouched, -2 if the rotation-consistency filter reset it to
+ * NULL; *nmatches = the reference's return value. */
+
+/* ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, th) (ORBmatcher.cc:45-129).
+ * F.occupied[i] = F.mvpMapPoints[i] && F.mvpMapPoints[i]->Observations() > 0. Reads mp: desc,
+ * bad, has_obs, track_*. nnratio = mfNNratio. */
+int orbm_search_by_projection_local(orbm_ctx* ctx, const orbm_frame_view* F, const orbm_mappoints* mp,
+                                    float th, float nnratio, int32_t* match, int* nmatches);
+
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+ * (ORBmatcher.cc:1328-1470). mp = LastFrame's N entries: skip[i] = !LastFrame.mvpMapPoints[i]
+ * || LastFrame.mvbOutlier[i]; pos, desc, has_obs of that MapPoint; octave = LastFrame.mvKeys[i]
+ * .octave; angle = LastFrame.mvKeysUn[i].angle. F.occupied as in _local. Tcw_cur / Tcw_last =
+ * the frames' mTcw (4x4 row-major float). */
+int orbm_search_by_projection_last_frame(orbm_ctx* ctx, const orbm_frame_view* F, const float Tcw_cur[16],
+                                         const orbm_mappoints* mp, const float Tcw_last[16], float th, int mono,
+                                         int check_ori, int32_t* match, int* nmatches);
+
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&
+ * sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1472-1599). mp = pKF->GetMapPointMatches():
+ * skip[i] = NULL entry or in sAlreadyFound; pos, desc, bad, min_dist, max_dist; angle =
+ * pKF->mvKeysUn[i].angle. F.occupied[i] = CurrentFrame.mvpMapPoints[i] != NULL. */
+int orbm_search_by_projection_keyframe(orbm_ctx* ctx, const orbm_frame_view* F, const float Tcw_cur[16],
+                                       const orbm_mappoints* mp, float th, int orb_dist, int check_ori,
+                                       int32_t* match, int* nmatches);
+
+/* ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints,
+ * vector<MapPoint*>& vpMatched, th) (ORBmatcher.cc:290-403). KF.occupied[i] = vpMatched[i] !=
+ * NULL; mp = vpPoints: skip[i] = in spAlreadyFound (the non-NULL entries of vpMatched); pos,
+ * normal, desc, bad, min_dist, max_dist. Scw = 4x4 row-major float Sim3. */
+int orbm_search_by_projection_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, const float Scw[16],
+                                   const orbm_mappoints* mp, int th, int32_t* match, int* nmatches);
+
+/* ------------------------------------------------------------------------------------
  * Cross-agent exchange slot (replaces the LCM KeyFrameexample message,
  * ORB_SLAM2.1/Examples/ROS/ORB_SLAM2/src/ros_mono.cc:1907-2410).
  * slot = [u32 n | u32 pad[15] | n x orbx_kp (24 B) | n x 32 B descriptors], fixed size

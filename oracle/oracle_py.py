@@ -52,6 +52,10 @@ _SIG = {
     "oc_search_by_bow_kf_f": (_I, [C.POINTER(_View), C.POINTER(_View), _F, _I, _P]),
     "oc_search_by_bow_kf_kf": (_I, [C.POINTER(_View), C.POINTER(_View), _F, _I, _P]),
     "oc_compute_stereo_matches": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _P, _P]),
+    "oc_search_by_projection_local": (_I, [_P, _P, _F, _F, _P]),
+    "oc_search_by_projection_last_frame": (_I, [_P, _P, _P, _P, _F, _I, _I, _P]),
+    "oc_search_by_projection_keyframe": (_I, [_P, _P, _P, _F, _I, _I, _P]),
+    "oc_search_by_projection_sim3": (_I, [_P, _P, _P, _I, _P]),
 }
 
 _lib = None
@@ -242,3 +246,38 @@ def compute_stereo_matches(left, right, kpsL, descL, kpsR, descR, mbf, mb):
     if rc < 0:
         raise RuntimeError("oc_compute_stereo_matches rc=%d" % rc)
     return ur[:n], dp[:n], rc
+
+
+# ---- SearchByProjection x4 (ORBmatcher.cc:45-129, 1328-1470, 1472-1599, 290-403). F / mps: objects
+# with the orbamd.projection FrameView / MapPoints attributes (their cstruct() builds the C structs).
+def _proj(fn, F, *args):
+    out = np.empty(max(F.n, 1), np.int32)
+    fv = F.cstruct()
+    n = getattr(load(), fn)(C.byref(fv), *args, out.ctypes.data)
+    return n, out[:F.n]
+
+
+def search_by_projection_local(F, mps, th, nnratio):
+    m = mps.cstruct()
+    return _proj("oc_search_by_projection_local", F, C.byref(m), C.c_float(th), C.c_float(nnratio))
+
+
+def search_by_projection_last_frame(F, Tcw, last_mps, Tcw_last, th, bMono, check_ori):
+    m = last_mps.cstruct()
+    T1 = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+    T2 = np.ascontiguousarray(Tcw_last, np.float32).reshape(16)
+    return _proj("oc_search_by_projection_last_frame", F, T1.ctypes.data, C.byref(m), T2.ctypes.data,
+                 C.c_float(th), int(bMono), int(check_ori))
+
+
+def search_by_projection_keyframe(F, Tcw, kf_mps, th, orb_dist, check_ori):
+    m = kf_mps.cstruct()
+    T1 = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+    return _proj("oc_search_by_projection_keyframe", F, T1.ctypes.data, C.byref(m), C.c_float(th), int(orb_dist),
+                 int(check_ori))
+
+
+def search_by_projection_sim3(KF, Scw, mps, th):
+    m = mps.cstruct()
+    S = np.ascontiguousarray(Scw, np.float32).reshape(16)
+    return _proj("oc_search_by_projection_sim3", KF, S.ctypes.data, C.byref(m), int(th))

@@ -72,6 +72,14 @@ int oc_search_by_bow_kf_kf(const orbm_kf_view* kf1, const orbm_kf_view* kf2, flo
 int oc_compute_stereo_matches(const oc_extractor* left, const oc_extractor* right, const orbx_kp* kpsL,
                               const uint8_t* descL, int N, const orbx_kp* kpsR, const uint8_t* descR, int Nr,
                               float mbf, float mb, float* uright, float* depth);
+int oc_search_by_projection_local(const orbm_frame_view* F, const orbm_mappoints* mp, float th, float nnratio,
+                                  int32_t* match);
+int oc_search_by_projection_last_frame(const orbm_frame_view* F, const float* Tcw_c, const orbm_mappoints* mp,
+                                       const float* Tcw_l, float th, int bMono, int checkOri, int32_t* match);
+int oc_search_by_projection_keyframe(const orbm_frame_view* F, const float* Tcw_c, const orbm_mappoints* mp, float th,
+                                     int ORBdist, int checkOri, int32_t* match);
+int oc_search_by_projection_sim3(const orbm_frame_view* KF, const float* Scw, const orbm_mappoints* mp, int th,
+                                 int32_t* match);
 
 #ifdef __cplusplus
 }

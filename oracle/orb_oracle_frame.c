@@ -5,6 +5,9 @@
  *
  *   oc_compute_stereo_matches  Frame::ComputeStereoMatches
  *                              (ORB_SLAM2.1/src/Frame.cc:470-641)
+ *   oc_search_by_projection_*  ORBmatcher::SearchByProjection x4 (ORBmatcher.cc:45-129,
+ *                              1328-1470, 1472-1599, 290-403) with Frame/KeyFrame::
+ *                              GetFeaturesInArea and AssignFeaturesToGrid
  */
 #include <limits.h>
 #include <math.h>
@@ -12,6 +15,9 @@
 #include <string.h>
 
 #include "orb_oracle.h"
+
+static int imax(int a, int b) { return a > b ? a : b; }
+static int imin(int a, int b) { return a < b ? a : b; }
 
 #define TH_HIGH 100 /* ORBmatcher.cc:37 */
 #define TH_LOW 50   /* ORBmatcher.cc:38 */
@@ -185,4 +191,419 @@ int oc_compute_stereo_matches(const oc_extractor* left, const oc_extractor* righ
     free(vRowIndices);
     free(vDistIdx);
     return rc ? rc : nkept;
+}
+
+/* ===================================================================================== */
+/* SearchByProjection x4 + Frame/KeyFrame::GetFeaturesInArea                             */
+/* ===================================================================================== */
+#define FRAME_GRID_ROWS 48 /* Frame.h:37 */
+#define FRAME_GRID_COLS 64 /* Frame.h:38 */
+#define HISTO_LENGTH 30    /* ORBmatcher.cc:39 */
+
+typedef struct { int* v; int n, cap; } ivec2;
+static void iv_push(ivec2* s, int x) { rowvec_push((rowvec*)s, x); }
+
+/* Frame::AssignFeaturesToGrid + PosInGrid (Frame.cc:235-250, 391-401): mGrid[ix][iy] lists in
+ * feature order. round() of a float (half away from zero). */
+typedef struct { ivec2 cell[FRAME_GRID_COLS][FRAME_GRID_ROWS]; } ogrid;
+static ogrid* grid_build(const orbm_frame_view* F) {
+    ogrid* g = (ogrid*)calloc(1, sizeof(ogrid));
+    for (int i = 0; i < F->n; i++) {
+        const int posX = (int)roundf((F->x[i] - F->min_x) * F->grid_w_inv);
+        const int posY = (int)roundf((F->y[i] - F->min_y) * F->grid_h_inv);
+        if (posX < 0 || posX >= FRAME_GRID_COLS || posY < 0 || posY >= FRAME_GRID_ROWS) continue;
+        iv_push(&g->cell[posX][posY], i);
+    }
+    return g;
+}
+static void grid_free(ogrid* g) {
+    for (int i = 0; i < FRAME_GRID_COLS; i++)
+        for (int j = 0; j < FRAME_GRID_ROWS; j++) free(g->cell[i][j].v);
+    free(g);
+}
+
+/* Frame::GetFeaturesInArea (Frame.cc:332-389); KeyFrame::GetFeaturesInArea (KeyFrame.cc:569-608)
+ * is the same with minLevel = maxLevel = -1. Appends to out (cleared first). */
+static void features_in_area(const orbm_frame_view* F, const ogrid* g, float x, float y, float r, int minLevel,
+                             int maxLevel, ivec2* out) {
+    out->n = 0;
+    const int nMinCellX = imax(0, (int)floorf((x - F->min_x - r) * F->grid_w_inv));
+    if (nMinCellX >= FRAME_GRID_COLS) return;
+    const int nMaxCellX = imin(FRAME_GRID_COLS - 1, (int)ceilf((x - F->min_x + r) * F->grid_w_inv));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = imax(0, (int)floorf((y - F->min_y - r) * F->grid_h_inv));
+    if (nMinCellY >= FRAME_GRID_ROWS) return;
+    const int nMaxCellY = imin(FRAME_GRID_ROWS - 1, (int)ceilf((y - F->min_y + r) * F->grid_h_inv));
+    if (nMaxCellY < 0) return;
+    const int bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+            const ivec2* vCell = &g->cell[ix][iy];
+            for (int j = 0; j < vCell->n; j++) {
+                const int k = vCell->v[j];
+                if (bCheckLevels) {
+                    if (F->octave[k] < minLevel) continue;
+                    if (maxLevel >= 0)
+                        if (F->octave[k] > maxLevel) continue;
+                }
+                const float distx = F->x[k] - x;
+                const float disty = F->y[k] - y;
+                if (fabsf(distx) < r && fabsf(disty) < r) iv_push(out, k);
+            }
+        }
+    }
+}
+
+/* cv::Mat float arithmetic as pinned in DESIGN.md: A*x+c with A 3x3 and x 3x1 is OpenCV's
+ * small-matrix gemm path (float products and sums, then (float)(t*alpha + c*beta) in double);
+ * A.t()*x (GEMM_1_T) is the generic path (double accumulation); norm / dot accumulate in double. */
+static void gemm33_fast(const float* A, int astep, const float* x, const float* c, float* d) {
+    for (int i = 0; i < 3; i++) {
+        const float* a = A + i * astep;
+        const float t0 = a[0] * x[0] + a[1] * x[1] + a[2] * x[2];
+        d[i] = (float)((double)t0 * 1.0 + (double)c[i] * 1.0);
+    }
+}
+static void gemm33t_neg(const float* A, int astep, const float* x, float* d) {
+    for (int i = 0; i < 3; i++) {
+        double s = 0;
+        for (int k = 0; k < 3; k++) s += (double)A[k * astep + i] * (double)x[k];
+        d[i] = (float)(-1.0 * s);
+    }
+}
+static float norm3(const float* v) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)v[k] * (double)v[k];
+    return (float)sqrt(s);
+}
+static double dot3(const float* a, const float* b) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)a[k] * (double)b[k];
+    return s;
+}
+
+/* MapPoint::PredictScale (MapPoint.cc:385-417): log of a float = logf (pinned) */
+static int predict_scale(float max_dist, float currentDist, const orbm_frame_view* F) {
+    const float ratio = max_dist / currentDist;
+    int nScale = (int)ceilf(logf(ratio) / F->log_scale_factor);
+    if (nScale < 0)
+        nScale = 0;
+    else if (nScale >= F->nlevels)
+        nScale = F->nlevels - 1;
+    return nScale;
+}
+
+static void three_maxima2(const ivec2* histo, int L, int* ind1, int* ind2, int* ind3) { /* ORBmatcher.cc:1601-1642 */
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < L; i++) {
+        const int s = histo[i].n;
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            *ind3 = *ind2; *ind2 = *ind1; *ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            *ind3 = *ind2; *ind2 = i;
+        } else if (s > max3) {
+            max3 = s; *ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) {
+        *ind2 = -1; *ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+        *ind3 = -1;
+    }
+}
+
+/* the rotation-consistency block shared by ORBmatcher.cc:1437-1467 and 1578-1596 */
+static int rot_push_bin(float a1, float a2) {
+    const float factor = 1.0f / HISTO_LENGTH;
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == HISTO_LENGTH) bin = 0;
+    return bin;
+}
+static int rot_filter(ivec2* rotHist, int32_t* match, int nmatches) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima2(rotHist, HISTO_LENGTH, &ind1, &ind2, &ind3);
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        if (i != ind1 && i != ind2 && i != ind3) {
+            for (int j = 0; j < rotHist[i].n; j++) {
+                match[rotHist[i].v[j]] = -2; /* = NULL */
+                nmatches--;
+            }
+        }
+    }
+    return nmatches;
+}
+
+static int has(const uint8_t* a, int i) { return a ? a[i] != 0 : 0; }
+
+/* ORBmatcher::RadiusByViewingCos (ORBmatcher.cc:131-137) */
+static float radius_by_viewing_cos(float viewCos) { return viewCos > 0.998 ? 2.5f : 4.0f; }
+
+/* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th) (ORBmatcher.cc:45-129) */
+int oc_search_by_projection_local(const orbm_frame_view* F, const orbm_mappoints* mp, float th, float nnratio,
+                                  int32_t* match) {
+    int nmatches = 0;
+    const int bFactor = th != 1.0;
+    ogrid* g = grid_build(F);
+    uint8_t* occ = (uint8_t*)malloc((size_t)F->n + 1);
+    for (int i = 0; i < F->n; i++) {
+        occ[i] = (uint8_t)has(F->occupied, i);
+        match[i] = -1;
+    }
+    ivec2 vIndices = {0};
+    for (int iMP = 0; iMP < mp->n; iMP++) {
+        if (!mp->track_in_view[iMP]) continue;
+        if (has(mp->bad, iMP)) continue;
+        const int nPredictedLevel = mp->track_level[iMP];
+        float r = radius_by_viewing_cos(mp->track_view_cos[iMP]);
+        if (bFactor) r *= th;
+        features_in_area(F, g, mp->track_proj_x[iMP], mp->track_proj_y[iMP], r * F->scale_factors[nPredictedLevel],
+                         nPredictedLevel - 1, nPredictedLevel, &vIndices);
+        if (vIndices.n == 0) continue;
+        const uint8_t* MPdescriptor = mp->desc + 32 * (size_t)iMP;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int k = 0; k < vIndices.n; k++) {
+            const int idx = vIndices.v[k];
+            if (occ[idx]) continue; /* mvpMapPoints[idx] && Observations() > 0 */
+            if (F->uright && F->uright[idx] > 0) {
+                const float er = fabsf(mp->track_proj_xr[iMP] - F->uright[idx]);
+                if (er > r * F->scale_factors[nPredictedLevel]) continue;
+            }
+            const int dist = oc_descriptor_distance(MPdescriptor, F->desc + 32 * (size_t)idx);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = F->octave[idx];
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = F->octave[idx];
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            match[bestIdx] = iMP;
+            occ[bestIdx] = (uint8_t)has(mp->has_obs, iMP);
+            nmatches++;
+        }
+    }
+    free(vIndices.v);
+    free(occ);
+    grid_free(g);
+    return nmatches;
+}
+
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+ * (ORBmatcher.cc:1328-1470) */
+int oc_search_by_projection_last_frame(const orbm_frame_view* F, const float* Tcw_c, const orbm_mappoints* mp,
+                                       const float* Tcw_l, float th, int bMono, int checkOri, int32_t* match) {
+    int nmatches = 0;
+    ivec2 rotHist[HISTO_LENGTH];
+    memset(rotHist, 0, sizeof(rotHist));
+    const float* Rcw = Tcw_c; /* rowRange(0,3).colRange(0,3) of a 4x4: row step 4 */
+    const float tcw[3] = {Tcw_c[3], Tcw_c[7], Tcw_c[11]};
+    float twc[3];
+    gemm33t_neg(Rcw, 4, tcw, twc);
+    const float* Rlw = Tcw_l;
+    const float tlw[3] = {Tcw_l[3], Tcw_l[7], Tcw_l[11]};
+    float tlc[3];
+    gemm33_fast(Rlw, 4, twc, tlw, tlc);
+    const int bForward = tlc[2] > F->b && !bMono;
+    const int bBackward = -tlc[2] > F->b && !bMono;
+    ogrid* g = grid_build(F);
+    uint8_t* occ = (uint8_t*)malloc((size_t)F->n + 1);
+    for (int i = 0; i < F->n; i++) {
+        occ[i] = (uint8_t)has(F->occupied, i);
+        match[i] = -1;
+    }
+    ivec2 vIndices2 = {0};
+    for (int i = 0; i < mp->n; i++) {
+        if (has(mp->skip, i)) continue; /* !pMP || mvbOutlier[i] */
+        float x3Dc[3];
+        gemm33_fast(Rcw, 4, mp->pos + 3 * (size_t)i, tcw, x3Dc);
+        const float xc = x3Dc[0];
+        const float yc = x3Dc[1];
+        const float invzc = 1.0 / x3Dc[2];
+        if (invzc < 0) continue;
+        const float u = F->fx * xc * invzc + F->cx;
+        const float v = F->fy * yc * invzc + F->cy;
+        if (u < F->min_x || u > F->max_x) continue;
+        if (v < F->min_y || v > F->max_y) continue;
+        const int nLastOctave = mp->octave[i];
+        const float radius = th * F->scale_factors[nLastOctave];
+        if (bForward)
+            features_in_area(F, g, u, v, radius, nLastOctave, -1, &vIndices2);
+        else if (bBackward)
+            features_in_area(F, g, u, v, radius, 0, nLastOctave, &vIndices2);
+        else
+            features_in_area(F, g, u, v, radius, nLastOctave - 1, nLastOctave + 1, &vIndices2);
+        if (vIndices2.n == 0) continue;
+        const uint8_t* dMP = mp->desc + 32 * (size_t)i;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int k = 0; k < vIndices2.n; k++) {
+            const int i2 = vIndices2.v[k];
+            if (occ[i2]) continue;
+            if (F->uright && F->uright[i2] > 0) {
+                const float ur = u - F->bf * invzc;
+                const float er = fabsf(ur - F->uright[i2]);
+                if (er > radius) continue;
+            }
+            const int dist = oc_descriptor_distance(dMP, F->desc + 32 * (size_t)i2);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = i2;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            match[bestIdx2] = i;
+            occ[bestIdx2] = (uint8_t)has(mp->has_obs, i);
+            nmatches++;
+            if (checkOri) iv_push(&rotHist[rot_push_bin(mp->angle[i], F->angle[bestIdx2])], bestIdx2);
+        }
+    }
+    if (checkOri) nmatches = rot_filter(rotHist, match, nmatches);
+    for (int i = 0; i < HISTO_LENGTH; i++) free(rotHist[i].v);
+    free(vIndices2.v);
+    free(occ);
+    grid_free(g);
+    return nmatches;
+}
+
+/* ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
+ * (ORBmatcher.cc:1472-1599) */
+int oc_search_by_projection_keyframe(const orbm_frame_view* F, const float* Tcw_c, const orbm_mappoints* mp, float th,
+                                     int ORBdist, int checkOri, int32_t* match) {
+    int nmatches = 0;
+    const float* Rcw = Tcw_c;
+    const float tcw[3] = {Tcw_c[3], Tcw_c[7], Tcw_c[11]};
+    float Ow[3];
+    gemm33t_neg(Rcw, 4, tcw, Ow);
+    ivec2 rotHist[HISTO_LENGTH];
+    memset(rotHist, 0, sizeof(rotHist));
+    ogrid* g = grid_build(F);
+    uint8_t* occ = (uint8_t*)malloc((size_t)F->n + 1);
+    for (int i = 0; i < F->n; i++) {
+        occ[i] = (uint8_t)has(F->occupied, i);
+        match[i] = -1;
+    }
+    ivec2 vIndices2 = {0};
+    for (int i = 0; i < mp->n; i++) {
+        if (has(mp->skip, i) || has(mp->bad, i)) continue; /* !pMP, isBad, sAlreadyFound.count */
+        const float* x3Dw = mp->pos + 3 * (size_t)i;
+        float x3Dc[3];
+        gemm33_fast(Rcw, 4, x3Dw, tcw, x3Dc);
+        const float xc = x3Dc[0];
+        const float yc = x3Dc[1];
+        const float invzc = 1.0 / x3Dc[2];
+        const float u = F->fx * xc * invzc + F->cx;
+        const float v = F->fy * yc * invzc + F->cy;
+        if (u < F->min_x || u > F->max_x) continue;
+        if (v < F->min_y || v > F->max_y) continue;
+        const float PO[3] = {x3Dw[0] - Ow[0], x3Dw[1] - Ow[1], x3Dw[2] - Ow[2]};
+        const float dist3D = norm3(PO);
+        const float maxDistance = 1.2f * mp->max_dist[i];
+        const float minDistance = 0.8f * mp->min_dist[i];
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[i], dist3D, F);
+        const float radius = th * F->scale_factors[nPredictedLevel];
+        features_in_area(F, g, u, v, radius, nPredictedLevel - 1, nPredictedLevel + 1, &vIndices2);
+        if (vIndices2.n == 0) continue;
+        const uint8_t* dMP = mp->desc + 32 * (size_t)i;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int k = 0; k < vIndices2.n; k++) {
+            const int i2 = vIndices2.v[k];
+            if (occ[i2]) continue;
+            const int dist = oc_descriptor_distance(dMP, F->desc + 32 * (size_t)i2);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = i2;
+            }
+        }
+        if (bestDist <= ORBdist) {
+            match[bestIdx2] = i;
+            occ[bestIdx2] = 1;
+            nmatches++;
+            if (checkOri) iv_push(&rotHist[rot_push_bin(mp->angle[i], F->angle[bestIdx2])], bestIdx2);
+        }
+    }
+    if (checkOri) nmatches = rot_filter(rotHist, match, nmatches);
+    for (int i = 0; i < HISTO_LENGTH; i++) free(rotHist[i].v);
+    free(vIndices2.v);
+    free(occ);
+    grid_free(g);
+    return nmatches;
+}
+
+/* ORBmatcher::SearchByProjection(KeyFrame*, cv::Mat Scw, vpPoints, vpMatched, th)
+ * (ORBmatcher.cc:290-403) */
+int oc_search_by_projection_sim3(const orbm_frame_view* KF, const float* Scw, const orbm_mappoints* mp, int th,
+                                 int32_t* match) {
+    /* Decompose Scw: scw = sqrt(row0.dot(row0)); Rcw = sRcw/scw and tcw = t/scw are
+     * convertTo with scale (float)(1./scw); Ow = -Rcw.t()*tcw */
+    const double d0 = dot3(Scw, Scw);
+    const float scw = (float)sqrt(d0);
+    const float inv = (float)(1. / (double)scw);
+    float Rcw[9], tcw[3], Ow[3];
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) Rcw[3 * r + c] = Scw[4 * r + c] * inv;
+        tcw[r] = Scw[4 * r + 3] * inv;
+    }
+    gemm33t_neg(Rcw, 3, tcw, Ow);
+    int nmatches = 0;
+    ogrid* g = grid_build(KF);
+    uint8_t* occ = (uint8_t*)malloc((size_t)KF->n + 1);
+    for (int i = 0; i < KF->n; i++) {
+        occ[i] = (uint8_t)has(KF->occupied, i);
+        match[i] = -1;
+    }
+    ivec2 vIndices = {0};
+    for (int iMP = 0; iMP < mp->n; iMP++) {
+        if (has(mp->bad, iMP) || has(mp->skip, iMP)) continue;
+        const float* p3Dw = mp->pos + 3 * (size_t)iMP;
+        float p3Dc[3];
+        gemm33_fast(Rcw, 3, p3Dw, tcw, p3Dc);
+        if (p3Dc[2] < 0.0) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz;
+        const float y = p3Dc[1] * invz;
+        const float u = KF->fx * x + KF->cx;
+        const float v = KF->fy * y + KF->cy;
+        if (!(u >= KF->min_x && u < KF->max_x && v >= KF->min_y && v < KF->max_y)) continue; /* IsInImage */
+        const float maxDistance = 1.2f * mp->max_dist[iMP];
+        const float minDistance = 0.8f * mp->min_dist[iMP];
+        const float PO[3] = {p3Dw[0] - Ow[0], p3Dw[1] - Ow[1], p3Dw[2] - Ow[2]};
+        const float dist = norm3(PO);
+        if (dist < minDistance || dist > maxDistance) continue;
+        if (dot3(PO, mp->normal + 3 * (size_t)iMP) < 0.5 * dist) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[iMP], dist, KF);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        features_in_area(KF, g, u, v, radius, -1, -1, &vIndices);
+        if (vIndices.n == 0) continue;
+        const uint8_t* dMP = mp->desc + 32 * (size_t)iMP;
+        int bestDist = 256, bestIdx = -1;
+        for (int k = 0; k < vIndices.n; k++) {
+            const int idx = vIndices.v[k];
+            if (occ[idx]) continue;
+            const int kpLevel = KF->octave[idx];
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const int dist2 = oc_descriptor_distance(dMP, KF->desc + 32 * (size_t)idx);
+            if (dist2 < bestDist) {
+                bestDist = dist2;
+                bestIdx = idx;
+            }
+        }
+        if (bestDist <= TH_LOW) {
+            match[bestIdx] = iMP;
+            occ[bestIdx] = 1;
+            nmatches++;
+        }
+    }
+    free(vIndices.v);
+    free(occ);
+    grid_free(g);
+    return nmatches;
 }

@@ -1,0 +1,172 @@
+"""Deterministic SearchByProjection scenarios (ORBmatcher.cc:45-129, 290-403, 1328-1470,
+1472-1599) for the oracle/GPU parity tests.
+
+A frame's keypoints and descriptors come from the CPU oracle extractor on a synthetic image;
+MapPoints are back-projected from a subset of those keypoints at random depths (so projections
+land near real features), with perturbed descriptors, duplicates (several MapPoints competing
+for one feature: exercises the in-order claim resolution), outliers and every per-variant flag
+drawn at random."""
+import numpy as np
+
+import oracle_py
+import orbamd
+
+FX, FY, CX, CY = 715.092024, 719.025258, 334.298489, 256.326097  # ORB_SLAM2/my.yaml:8-11
+W, H = 640, 480
+
+_cache = {}
+
+
+def frame_features(agent=0, t=0, nfeatures=1000):
+    key = (agent, t, nfeatures)
+    if key not in _cache:
+        img = orbamd.synth_frames(agent, t, 1, W, H)[0]
+        orc = oracle_py.OracleExtractor(nfeatures, 1.2, 8, 20, 7)
+        k, d = orc(img)
+        _cache[key] = (k, d, orc.tables()["scale"])
+    return _cache[key]
+
+
+def rot(rng, deg):
+    a = np.deg2rad(rng.uniform(-deg, deg, 3))
+    cx, sx, cy, sy, cz, sz = np.cos(a[0]), np.sin(a[0]), np.cos(a[1]), np.sin(a[1]), np.cos(a[2]), np.sin(a[2])
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+def pose(R, t, s=1.0):
+    T = np.eye(4)
+    T[:3, :3] = s * R
+    T[:3, 3] = s * np.asarray(t)
+    return T.astype(np.float32)
+
+
+def flip_bits(rng, d, nmax):
+    d = d.copy()
+    for i in range(len(d)):
+        nb = int(rng.integers(0, nmax + 1))
+        if nb:
+            pos = rng.choice(256, nb, replace=False)
+            for p in pos:
+                d[i, p >> 3] ^= np.uint8(1 << (p & 7))
+    return d
+
+
+def make_frame(rng, agent, t, stereo, occupied_frac=0.05, nfeatures=1000):
+    k, d, scale = frame_features(agent, t, nfeatures)
+    n = len(k)
+    bf = 47.9 if stereo else 0.0
+    ur = None
+    if stereo:
+        ur = np.full(n, -1, np.float32)
+        has = rng.random(n) < 0.6
+        ur[has] = (k["x"][has] - rng.uniform(1, 40, has.sum())).astype(np.float32)
+    occ = (rng.random(n) < occupied_frac).astype(np.uint8)
+    F = orbamd.FrameView(k, d, scale, W, H, FX, FY, CX, CY, bf=bf, uright=ur, occupied=occ)
+    return F, k, d, scale
+
+
+def pick_sources(rng, n, m, dup_frac=0.15):
+    """m MapPoint source features out of n, with duplicates (competing MapPoints)."""
+    base = rng.choice(n, size=min(n, m), replace=False)
+    ndup = int(len(base) * dup_frac)
+    dups = rng.choice(base, size=ndup, replace=True)
+    src = np.concatenate([base, dups])
+    rng.shuffle(src)
+    return src
+
+
+def local_scene(seed, stereo=True, th=3.0):
+    """SearchByProjection(Frame&, vector<MapPoint*>, th): isInFrustum-style tracking fields."""
+    rng = np.random.default_rng(seed)
+    F, k, d, scale = make_frame(rng, seed % 5, 3 + seed, stereo)
+    src = pick_sources(rng, F.n, int(F.n * 0.8))
+    m = len(src)
+    px = (k["x"][src] + rng.normal(0, 2.0, m)).astype(np.float32)
+    py = (k["y"][src] + rng.normal(0, 2.0, m)).astype(np.float32)
+    lvl = np.clip(k["octave"][src] + rng.integers(-1, 2, m), 0, 7).astype(np.int32)
+    desc = flip_bits(rng, d[src], 40)
+    rnd = rng.random(m) < 0.1
+    desc[rnd] = rng.integers(0, 256, (rnd.sum(), 32), dtype=np.uint8)
+    mps = orbamd.MapPoints(
+        m, desc=desc, bad=(rng.random(m) < 0.05), has_obs=(rng.random(m) < 0.85),
+        track_in_view=(rng.random(m) < 0.9), track_proj_x=px, track_proj_y=py,
+        track_proj_xr=(px - rng.uniform(0, 40, m)).astype(np.float32), track_level=lvl,
+        track_view_cos=rng.choice([0.9995, 0.999, 0.998, 0.99], m).astype(np.float32))
+    return F, mps
+
+
+def backproject(rng, k, src, Tcw):
+    z = rng.uniform(1.0, 12.0, len(src))
+    xc = np.stack([(k["x"][src] - CX) / FX * z, (k["y"][src] - CY) / FY * z, z], 1)
+    R, t = Tcw[:3, :3].astype(np.float64), Tcw[:3, 3].astype(np.float64)
+    return ((xc - t) @ R).astype(np.float32)  # Xw = R^T (Xc - t)
+
+
+def last_frame_scene(seed, bmono=False, stereo=True, forward=0):
+    """SearchByProjection(CurrentFrame, LastFrame, th, bMono). forward: +1 / -1 moves the last
+    frame ahead / behind along the optical axis by more than mb (bForward / bBackward)."""
+    rng = np.random.default_rng(seed)
+    F, k, d, scale = make_frame(rng, seed % 5, 7 + seed, stereo)
+    Tcw = pose(rot(rng, 2.0), rng.normal(0, 0.05, 3))
+    src = pick_sources(rng, F.n, int(F.n * 0.9))
+    m = len(src)
+    Xw = backproject(rng, k, src, Tcw) + rng.normal(0, 0.003, (m, 3)).astype(np.float32)
+    dz = 0.5 * forward if forward else rng.normal(0, 0.01)
+    Tl = Tcw.copy()
+    Tl[2, 3] += np.float32(-dz)  # tlc.z = dz (camera centre of Current in Last)
+    mps = orbamd.MapPoints(
+        m, desc=flip_bits(rng, d[src], 35), pos=Xw, has_obs=(rng.random(m) < 0.85),
+        skip=(rng.random(m) < 0.1), octave=np.clip(k["octave"][src] + rng.integers(-1, 2, m), 0, 7),
+        angle=((k["angle"][src] + rng.normal(0, 4.0, m)) % 360).astype(np.float32))
+    return F, Tcw, mps, Tl
+
+
+def dist_bounds(rng, Xw, Tcw, octs):
+    Ow = -(Tcw[:3, :3].astype(np.float64).T @ Tcw[:3, 3].astype(np.float64))
+    dist = np.linalg.norm(Xw - Ow, axis=1)
+    maxd = dist * 1.2 ** (octs + rng.uniform(-0.9, 0.1, len(octs)))
+    maxd[rng.random(len(octs)) < 0.05] *= 0.5  # out of the invariance region
+    mind = maxd / 1.2 ** 7
+    return mind.astype(np.float32), maxd.astype(np.float32)
+
+
+def keyframe_scene(seed, th=10.0, orb_dist=100):
+    """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (relocalisation)."""
+    rng = np.random.default_rng(seed)
+    F, k, d, scale = make_frame(rng, seed % 5, 11 + seed, False, occupied_frac=0.1)
+    Tcw = pose(rot(rng, 3.0), rng.normal(0, 0.05, 3))
+    src = pick_sources(rng, F.n, int(F.n * 0.9))
+    m = len(src)
+    Xw = backproject(rng, k, src, Tcw) + rng.normal(0, 0.003, (m, 3)).astype(np.float32)
+    mind, maxd = dist_bounds(rng, Xw, Tcw, k["octave"][src])
+    mps = orbamd.MapPoints(
+        m, desc=flip_bits(rng, d[src], 40), pos=Xw, min_dist=mind, max_dist=maxd, bad=(rng.random(m) < 0.05),
+        skip=(rng.random(m) < 0.1), angle=((k["angle"][src] + rng.normal(0, 4.0, m)) % 360).astype(np.float32))
+    return F, Tcw, mps
+
+
+def sim3_scene(seed):
+    """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (loop closing)."""
+    rng = np.random.default_rng(seed)
+    F, k, d, scale = make_frame(rng, seed % 5, 13 + seed, False, occupied_frac=0.1)
+    s = np.float32(rng.uniform(0.7, 1.4))
+    R = rot(rng, 3.0)
+    t = rng.normal(0, 0.05, 3)
+    Scw = pose(R, t, s)
+    Tcw = pose(R, t)
+    src = pick_sources(rng, F.n, int(F.n * 0.9))
+    m = len(src)
+    Xw = backproject(rng, k, src, Tcw) + rng.normal(0, 0.003, (m, 3)).astype(np.float32)
+    Ow = -(R.T @ t)
+    nrm = (Xw - Ow)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    flip = rng.random(m) < 0.05
+    nrm[flip] *= -1
+    mind, maxd = dist_bounds(rng, Xw, Tcw, k["octave"][src])
+    mps = orbamd.MapPoints(
+        m, desc=flip_bits(rng, d[src], 25), pos=Xw, normal=nrm.astype(np.float32), min_dist=mind, max_dist=maxd,
+        bad=(rng.random(m) < 0.05), skip=(rng.random(m) < 0.1))
+    return F, Scw, mps

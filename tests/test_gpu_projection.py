@@ -1,0 +1,74 @@
+"""GPU parity: ORBmatcher::SearchByProjection x4 (ORBmatcher.cc:45-129, 1328-1470, 1472-1599,
+290-403) on the HIP path (k_grid + k_proj_scan + k_proj_resolve) vs the CPU oracle: the
+per-feature assignment (which MapPoint, last writer wins, -2 = reset by the rotation filter)
+and the returned count must be identical."""
+import numpy as np
+import pytest
+
+import oracle_py
+import orbamd
+import proj_scenes as ps
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(g, o):
+    (ng, mg), (no, mo) = g, o
+    bad = np.nonzero(mg != mo)[0]
+    assert bad.size == 0, "assignment differs at %s: gpu %s oracle %s" % (bad[:8], mg[bad[:8]], mo[bad[:8]])
+    assert ng == no, "nmatches %d vs oracle %d" % (ng, no)
+    return ng
+
+
+@pytest.mark.parametrize("seed,stereo,th,nnratio", [(1, True, 3.0, 0.8), (2, False, 1.0, 0.8),
+                                                    (3, True, 5.0, 0.6), (8, True, 10.0, 0.9)])
+def test_projection_local(seed, stereo, th, nnratio):
+    F, mps = ps.local_scene(seed, stereo)
+    g = orbamd.ORBmatcher(nnratio, False).SearchByProjectionLocal(F, mps, th)
+    o = oracle_py.search_by_projection_local(F, mps, th, nnratio)
+    assert _same(g, o) > F.n // 4
+
+
+@pytest.mark.parametrize("seed,bmono,forward,check_ori,th", [(4, False, 0, True, 7.0), (5, True, 0, True, 15.0),
+                                                             (6, False, 1, False, 7.0), (7, False, -1, True, 7.0)])
+def test_projection_last_frame(seed, bmono, forward, check_ori, th):
+    F, Tcw, mps, Tl = ps.last_frame_scene(seed, bmono, not bmono, forward)
+    g = orbamd.ORBmatcher(0.9, check_ori).SearchByProjectionLastFrame(F, Tcw, mps, Tl, th, bmono)
+    o = oracle_py.search_by_projection_last_frame(F, Tcw, mps, Tl, th, bmono, check_ori)
+    assert _same(g, o) > F.n // 4
+
+
+@pytest.mark.parametrize("seed,th,orb_dist,check_ori", [(5, 10.0, 100, True), (9, 3.0, 64, False),
+                                                        (10, 10.0, 100, False)])
+def test_projection_keyframe(seed, th, orb_dist, check_ori):
+    F, Tcw, mps = ps.keyframe_scene(seed)
+    g = orbamd.ORBmatcher(0.9, check_ori).SearchByProjectionKeyFrame(F, Tcw, mps, th, orb_dist)
+    o = oracle_py.search_by_projection_keyframe(F, Tcw, mps, th, orb_dist, check_ori)
+    assert _same(g, o) > F.n // 8
+
+
+@pytest.mark.parametrize("seed,th", [(6, 10), (11, 3)])
+def test_projection_sim3(seed, th):
+    F, Scw, mps = ps.sim3_scene(seed)
+    g = orbamd.ORBmatcher(0.75, True).SearchByProjectionSim3(F, Scw, mps, th)
+    o = oracle_py.search_by_projection_sim3(F, Scw, mps, th)
+    assert _same(g, o) > F.n // 8
+
+
+def test_projection_edge_cases():
+    """no MapPoints; every feature occupied; all MapPoints on one feature (a chain of claims)."""
+    F, mps = ps.local_scene(12, True)
+    mt = orbamd.ORBmatcher(0.8, False)
+    empty = orbamd.MapPoints(0, desc=np.zeros((0, 32), np.uint8), track_in_view=[], track_proj_x=[],
+                             track_proj_y=[], track_proj_xr=[], track_level=[], track_view_cos=[])
+    n, m = mt.SearchByProjectionLocal(F, empty, 3.0)
+    assert n == 0 and (m == -1).all()
+    F.occupied = np.ones(F.n, np.uint8)
+    assert _same(mt.SearchByProjectionLocal(F, mps, 3.0), oracle_py.search_by_projection_local(F, mps, 3.0, 0.8)) == 0
+    F.occupied = np.zeros(F.n, np.uint8)
+    k = 300
+    same = orbamd.MapPoints(k, desc=np.repeat(F.desc[7:8], k, 0), bad=np.zeros(k), has_obs=np.arange(k) % 3 != 0,
+                            track_in_view=np.ones(k), track_proj_x=np.full(k, F.x[7]), track_proj_y=np.full(k, F.y[7]),
+                            track_proj_xr=np.full(k, F.x[7]), track_level=np.full(k, F.octave[7]),
+                            track_view_cos=np.ones(k))
+    _same(mt.SearchByProjectionLocal(F, same, 4.0), oracle_py.search_by_projection_local(F, same, 4.0, 0.8))

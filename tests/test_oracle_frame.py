@@ -134,3 +134,109 @@ def test_stereo_oracle_no_right_keypoints():
     orr(np.full((H, W), 128, np.uint8))  # flat right image: no keypoints
     ur, dp, n = oracle_py.compute_stereo_matches(ol, orr, kl, dl, kl[:0], dl[:0], 40.0, 0.1)
     assert n == 0 and (ur == -1).all() and (dp == -1).all()
+
+
+# ------------------------------------------------------------------ SearchByProjection
+import proj_scenes as ps  # noqa: E402
+
+
+def grid_py(F):
+    g = {}
+    for i in range(F.n):
+        px = int(roundf_signed(f32(f32(F.x[i] - F.min_x) * F.grid_w_inv)))
+        py = int(roundf_signed(f32(f32(F.y[i] - F.min_y) * F.grid_h_inv)))
+        if 0 <= px < 64 and 0 <= py < 48:
+            g.setdefault((px, py), []).append(i)
+    return g
+
+
+def roundf_signed(v):
+    return roundf(v) if v >= 0 else -roundf(-v)
+
+
+def area_py(F, g, x, y, r, minL=-1, maxL=-1):
+    """Frame::GetFeaturesInArea (Frame.cc:332-389)."""
+    x, y, r = f32(x), f32(y), f32(r)
+    x0 = max(0, int(np.floor(f32(f32(f32(x - F.min_x) - r) * F.grid_w_inv))))
+    if x0 >= 64:
+        return []
+    x1 = min(63, int(np.ceil(f32(f32(f32(x - F.min_x) + r) * F.grid_w_inv))))
+    if x1 < 0:
+        return []
+    y0 = max(0, int(np.floor(f32(f32(f32(y - F.min_y) - r) * F.grid_h_inv))))
+    if y0 >= 48:
+        return []
+    y1 = min(47, int(np.ceil(f32(f32(f32(y - F.min_y) + r) * F.grid_h_inv))))
+    if y1 < 0:
+        return []
+    check = minL > 0 or maxL >= 0
+    out = []
+    for ix in range(x0, x1 + 1):
+        for iy in range(y0, y1 + 1):
+            for k in g.get((ix, iy), []):
+                if check:
+                    if F.octave[k] < minL:
+                        continue
+                    if maxL >= 0 and F.octave[k] > maxL:
+                        continue
+                if abs(f32(F.x[k] - x)) < r and abs(f32(F.y[k] - y)) < r:
+                    out.append(k)
+    return out
+
+
+def local_py(F, mp, th, nnratio):
+    """ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) (ORBmatcher.cc:45-129)."""
+    g = grid_py(F)
+    bits = np.unpackbits(F.desc, axis=1)
+    occ = F.occupied.astype(bool).copy()
+    match = np.full(F.n, -1, np.int32)
+    nm = 0
+    for i in range(mp.n):
+        if not mp.track_in_view[i] or mp.bad[i]:
+            continue
+        lvl = int(mp.track_level[i])
+        r = f32(2.5) if float(mp.track_view_cos[i]) > 0.998 else f32(4.0)
+        if th != 1.0:
+            r = f32(r * f32(th))
+        rad = f32(r * F.scale_factors[lvl])
+        qb = np.unpackbits(mp.desc[i])
+        best, bl, best2, bl2, bi = 256, -1, 256, -1, -1
+        for idx in area_py(F, g, mp.track_proj_x[i], mp.track_proj_y[i], rad, lvl - 1, lvl):
+            if occ[idx]:
+                continue
+            if F.uright is not None and F.uright[idx] > 0:
+                if abs(f32(mp.track_proj_xr[i] - F.uright[idx])) > rad:
+                    continue
+            dist = int(np.count_nonzero(bits[idx] != qb))
+            if dist < best:
+                best2, best, bl2, bl, bi = best, dist, bl, int(F.octave[idx]), idx
+            elif dist < best2:
+                bl2, best2 = int(F.octave[idx]), dist
+        if best <= 100:
+            if bl == bl2 and f32(best) > f32(f32(nnratio) * f32(best2)):
+                continue
+            match[bi] = i
+            occ[bi] = bool(mp.has_obs[i])
+            nm += 1
+    return nm, match
+
+
+@pytest.mark.parametrize("seed,stereo,th", [(1, True, 3.0), (2, False, 1.0), (3, True, 5.0)])
+def test_projection_local_oracle_matches_restatement(seed, stereo, th):
+    F, mps = ps.local_scene(seed, stereo)
+    n, m = oracle_py.search_by_projection_local(F, mps, th, 0.8)
+    n2, m2 = local_py(F, mps, th, 0.8)
+    assert n == n2 and n > F.n // 4
+    np.testing.assert_array_equal(m, m2)
+
+
+def test_projection_variants_oracle_sanity():
+    F, Tcw, mps, Tl = ps.last_frame_scene(4)
+    n, m = oracle_py.search_by_projection_last_frame(F, Tcw, mps, Tl, 7.0, False, True)
+    assert n > F.n // 4 and n >= (m >= 0).sum()  # has_obs == 0 claimers can be overwritten (last wins)
+    F, Tcw, mps = ps.keyframe_scene(5)
+    n, m = oracle_py.search_by_projection_keyframe(F, Tcw, mps, 10.0, 100, True)
+    assert n > F.n // 4 and n == (m >= 0).sum()  # every claim occupies
+    F, Scw, mps = ps.sim3_scene(6)
+    n, m = oracle_py.search_by_projection_sim3(F, Scw, mps, 10)
+    assert n > F.n // 8 and n == (m >= 0).sum()
