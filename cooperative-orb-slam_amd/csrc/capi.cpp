@@ -888,6 +888,17 @@ struct orbm_ctx {
     hipStream_t stream = nullptr;
     DevBuf scratch;
     std::vector<uint8_t> host;
+    void* pinned = nullptr;  // host staging of one call's inputs (one H2D copy)
+    size_t pinned_bytes = 0;
+    uint8_t* ensure_pinned(size_t need) {
+        if (need <= pinned_bytes) return (uint8_t*)pinned;
+        if (pinned) (void)hipHostFree(pinned);
+        pinned = nullptr;
+        pinned_bytes = 0;
+        if (hipHostMalloc(&pinned, need, 0) != hipSuccess) return nullptr;
+        pinned_bytes = need;
+        return (uint8_t*)pinned;
+    }
 };
 
 namespace {
@@ -1003,6 +1014,7 @@ void orbm_destroy(orbm_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->scratch.release();
+    if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1239,14 +1251,18 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
                    float nnratio, int check_ori, int32_t* match, int* nmatches) {
     HIPR(hipSetDevice(ctx->device));
     const size_t n = (size_t)F->n, nq = pb.q.size();
+    // inputs first (staged in pinned memory, one H2D copy), then outputs (one D2H copy), then scratch
     Carve cv;
-    const size_t o_x = cv.take(4 * n), o_y = cv.take(4 * n), o_ang = cv.take(4 * n), o_ur = cv.take(4 * n),
-                 o_oct = cv.take(4 * n), o_occ = cv.take(n), o_desc = cv.take(32 * n),
-                 o_q = cv.take(sizeof(ProjQuery) * nq), o_qd = cv.take(32 * nq),
-                 o_gs = cv.take(4 * (kGridCols * kGridRows + 1)), o_gi = cv.take(2 * n), o_scan = cv.take(16 * nq),
-                 o_res = cv.take(8 * nq), o_match = cv.take(4 * n), o_nm = cv.take(4),
-                 o_call = cv.take(sizeof(ProjCall));
+    const size_t o_call = cv.take(sizeof(ProjCall)), o_x = cv.take(4 * n), o_y = cv.take(4 * n),
+                 o_ang = cv.take(4 * n), o_ur = cv.take(4 * n), o_oct = cv.take(4 * n), o_occ = cv.take(n),
+                 o_desc = cv.take(32 * n), o_q = cv.take(sizeof(ProjQuery) * nq), o_qd = cv.take(32 * nq);
+    const size_t in_bytes = cv.off;
+    const size_t o_nm = cv.take(4 * n + 4);  // nmatches, then match[n]
+    const size_t o_gs = cv.take(4 * (kGridCols * kGridRows + 1)), o_gi = cv.take(2 * n), o_scan = cv.take(32 * nq),
+                 o_scnt = cv.take(4 * nq), o_res = cv.take(8 * nq);
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
+    uint8_t* hp = ctx->ensure_pinned(in_bytes + 4 * n + 4);
+    if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
     hipStream_t st = ctx->stream;
     ProjCall c;
@@ -1273,29 +1289,31 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     c.grid_start = (int*)(base + o_gs);
     c.grid_idx = (uint16_t*)(base + o_gi);
     c.scan = (unsigned long long*)(base + o_scan);
+    c.scan_cnt = (int*)(base + o_scnt);
     c.res = (int*)(base + o_res);
-    c.match = (int32_t*)(base + o_match);
     c.nmatches = (int32_t*)(base + o_nm);
+    c.match = (int32_t*)(base + o_nm + 4);
+    memcpy(hp + o_call, &c, sizeof(c));
     if (n) {
-        HIPR(hipMemcpyAsync(base + o_x, F->x, 4 * n, hipMemcpyHostToDevice, st));
-        HIPR(hipMemcpyAsync(base + o_y, F->y, 4 * n, hipMemcpyHostToDevice, st));
-        if (F->angle) HIPR(hipMemcpyAsync(base + o_ang, F->angle, 4 * n, hipMemcpyHostToDevice, st));
-        if (F->uright) HIPR(hipMemcpyAsync(base + o_ur, F->uright, 4 * n, hipMemcpyHostToDevice, st));
-        HIPR(hipMemcpyAsync(base + o_oct, F->octave, 4 * n, hipMemcpyHostToDevice, st));
-        if (F->occupied) HIPR(hipMemcpyAsync(base + o_occ, F->occupied, n, hipMemcpyHostToDevice, st));
-        HIPR(hipMemcpyAsync(base + o_desc, F->desc, 32 * n, hipMemcpyHostToDevice, st));
+        memcpy(hp + o_x, F->x, 4 * n);
+        memcpy(hp + o_y, F->y, 4 * n);
+        if (F->angle) memcpy(hp + o_ang, F->angle, 4 * n);
+        if (F->uright) memcpy(hp + o_ur, F->uright, 4 * n);
+        memcpy(hp + o_oct, F->octave, 4 * n);
+        if (F->occupied) memcpy(hp + o_occ, F->occupied, n);
+        memcpy(hp + o_desc, F->desc, 32 * n);
     }
     if (nq) {
-        HIPR(hipMemcpyAsync(base + o_q, pb.q.data(), sizeof(ProjQuery) * nq, hipMemcpyHostToDevice, st));
-        HIPR(hipMemcpyAsync(base + o_qd, pb.qdesc.data(), 32 * nq, hipMemcpyHostToDevice, st));
+        memcpy(hp + o_q, pb.q.data(), sizeof(ProjQuery) * nq);
+        memcpy(hp + o_qd, pb.qdesc.data(), 32 * nq);
     }
-    HIPR(hipMemcpyAsync(base + o_call, &c, sizeof(c), hipMemcpyHostToDevice, st));
+    HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, st));
     HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st));
-    int nm = 0;
-    if (n) HIPR(hipMemcpyAsync(match, c.match, 4 * n, hipMemcpyDeviceToHost, st));
-    HIPR(hipMemcpyAsync(&nm, c.nmatches, 4, hipMemcpyDeviceToHost, st));
+    uint8_t* ho = hp + in_bytes;
+    HIPR(hipMemcpyAsync(ho, base + o_nm, 4 * n + 4, hipMemcpyDeviceToHost, st));
     HIPR(hipStreamSynchronize(st));
-    if (nmatches) *nmatches = nm;
+    if (n) memcpy(match, ho + 4, 4 * n);
+    if (nmatches) memcpy(nmatches, ho, 4);
     return 0;
 }
 
@@ -1467,6 +1485,49 @@ int orbm_search_by_projection_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, con
                mp->desc + 32 * (size_t)iMP);
     }
     return run_projection(ctx, KF, pb, 50 /*TH_LOW*/, 0, 0.f, 0, match, nmatches);
+}
+
+}  // extern "C"
+
+/* ===================================================================================== */
+/* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307), batched                 */
+/* ===================================================================================== */
+extern "C" {
+
+int orbm_compute_distinctive_descriptors_device(orbm_ctx* ctx, int npoints, const int32_t* d_offsets,
+                                                const uint8_t* d_desc, int32_t* d_best_idx, uint8_t* d_out_desc,
+                                                void* stream) {
+    if (!ctx || npoints < 0 || (npoints && (!d_offsets || !d_desc || !d_best_idx))) return ORBX_EARG;
+    if (npoints == 0) return 0;
+    HIPR(hipSetDevice(ctx->device));
+    HIPR(launch_distinctive(npoints, d_offsets, d_desc, d_best_idx, d_out_desc, (hipStream_t)stream));
+    return 0;
+}
+
+int orbm_compute_distinctive_descriptors(orbm_ctx* ctx, int npoints, const int32_t* offsets, const uint8_t* desc,
+                                         int32_t* best_idx, uint8_t* out_desc) {
+    if (!ctx || npoints < 0 || (npoints && (!offsets || !best_idx))) return ORBX_EARG;
+    if (npoints == 0) return 0;
+    if (offsets[0] != 0) return ORBX_EARG;
+    for (int p = 0; p < npoints; p++)
+        if (offsets[p + 1] < offsets[p]) return ORBX_EARG;
+    const size_t nrows = (size_t)offsets[npoints];
+    if (nrows && !desc) return ORBX_EARG;
+    HIPR(hipSetDevice(ctx->device));
+    Carve cv;
+    const size_t o_off = cv.take(4 * ((size_t)npoints + 1)), o_desc = cv.take(32 * nrows), o_best = cv.take(4 * (size_t)npoints),
+                 o_out = cv.take(32 * (size_t)npoints);
+    if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
+    uint8_t* base = ctx->scratch.as<uint8_t>();
+    hipStream_t st = ctx->stream;
+    HIPR(hipMemcpyAsync(base + o_off, offsets, 4 * ((size_t)npoints + 1), hipMemcpyHostToDevice, st));
+    if (nrows) HIPR(hipMemcpyAsync(base + o_desc, desc, 32 * nrows, hipMemcpyHostToDevice, st));
+    HIPR(launch_distinctive(npoints, (const int32_t*)(base + o_off), base + o_desc, (int32_t*)(base + o_best),
+                            out_desc ? base + o_out : nullptr, st));
+    HIPR(hipMemcpyAsync(best_idx, base + o_best, 4 * (size_t)npoints, hipMemcpyDeviceToHost, st));
+    if (out_desc) HIPR(hipMemcpyAsync(out_desc, base + o_out, 32 * (size_t)npoints, hipMemcpyDeviceToHost, st));
+    HIPR(hipStreamSynchronize(st));
+    return 0;
 }
 
 }  // extern "C"

@@ -26,6 +26,11 @@
  *              wave commits 64 queries at a time up to the first such conflict, re-scans that
  *              one query against the live occupancy bitmap, and continues. Then the rotation
  *              histogram + ComputeThreeMaxima (ORBmatcher.cc:1437-1467, 1601-1642).
+ *   k_distinctive
+ *              MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of
+ *              MapPoints: one wave per MapPoint, row i of the Hamming distance matrix in LDS,
+ *              its median (sorted element floor(0.5*(N-1))) by a 9-bit ballot radix select,
+ *              first strict minimum of the medians.
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -406,11 +411,24 @@ __global__ __launch_bounds__(1024) void k_grid(const ProjCall* __restrict__ call
 }
 
 /* GetFeaturesInArea (Frame.cc:332-389) + the per-candidate tests of the variants, G lanes of one
- * query (gl = lane in group); returns the group's best / second-best keys (all lanes). */
-template <int G, class Occ>
-__device__ __forceinline__ void proj_scan(const ProjCall& c, const ProjQuery& q, const uint4 qd0, const uint4 qd1,
-                                          int gl, Occ occupied, unsigned long long& ob, unsigned long long& os) {
-    unsigned long long b = kNoKey, s = kNoKey;
+ * query (gl = lane in group). Returns (all lanes) the group's K smallest candidate keys, sorted,
+ * and the number of candidates (keys with dist < 256). */
+template <int K>
+__device__ __forceinline__ void topk_insert(unsigned long long k, unsigned long long (&a)[K]) {
+#pragma unroll
+    for (int t = 0; t < K; t++) {
+        const unsigned long long lo = min(k, a[t]), hi = max(k, a[t]);
+        a[t] = lo;
+        k = hi;
+    }
+}
+
+template <int G, int K, class Occ>
+__device__ __forceinline__ int proj_scan(const ProjCall& c, const ProjQuery& q, const uint4 qd0, const uint4 qd1, int gl,
+                                         Occ occupied, unsigned long long (&top)[K]) {
+#pragma unroll
+    for (int t = 0; t < K; t++) top[t] = kNoKey;
+    int ncand = 0;
     const float r = q.radius;
     const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(q.u, c.min_x), r), c.gw_inv)));
     const int nMaxCellX = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(q.u, c.min_x), r), c.gw_inv)));
@@ -439,21 +457,26 @@ __device__ __forceinline__ void proj_scan(const ProjCall& c, const ProjQuery& q,
                 const int dist = __popc(qd0.x ^ f0.x) + __popc(qd0.y ^ f0.y) + __popc(qd0.z ^ f0.z) +
                                  __popc(qd0.w ^ f0.w) + __popc(qd1.x ^ f1.x) + __popc(qd1.y ^ f1.y) +
                                  __popc(qd1.z ^ f1.z) + __popc(qd1.w ^ f1.w);
-                if (dist < 256)  // bestDist starts at 256 (ORBmatcher.cc:78, 349, 1397, 1550)
-                    keep2(((unsigned long long)dist << 40) | ((unsigned long long)k << 16) | (unsigned)idx, b, s);
+                if (dist < 256) {  // bestDist starts at 256 (ORBmatcher.cc:78, 349, 1397, 1550)
+                    topk_insert<K>(((unsigned long long)dist << 40) | ((unsigned long long)k << 16) | (unsigned)idx, top);
+                    ncand++;
+                }
             }
         }
     }
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) {
-        const unsigned long long b2 = shfl_xor_u64(b, o), s2 = shfl_xor_u64(s, o);
-        const unsigned long long lo = min(b, b2), hi = max(b, b2);
-        b = lo;
-        s = min(hi, min(s, s2));
+        unsigned long long other[K];
+#pragma unroll
+        for (int t = 0; t < K; t++) other[t] = shfl_xor_u64(top[t], o);
+#pragma unroll
+        for (int t = 0; t < K; t++) topk_insert<K>(other[t], top);
+        ncand += __shfl_xor(ncand, o);
     }
-    ob = b;
-    os = s;
+    return ncand;
 }
+
+constexpr int kProjTopK = 4;
 
 __global__ __launch_bounds__(256) void k_proj_scan(const ProjCall* __restrict__ calls) {
     const ProjCall& c = calls[blockIdx.y];
@@ -475,11 +498,15 @@ __global__ __launch_bounds__(256) void k_proj_scan(const ProjCall* __restrict__ 
         q.max_level = -1;
     }
     const uint8_t* occ0 = c.occ0;
-    unsigned long long b, s;
-    proj_scan<16>(c, q, qd0, qd1, gl, [occ0](int i) { return occ0 && occ0[i]; }, b, s);
-    if (in && gl == 0) {
-        c.scan[2 * qi] = b;
-        c.scan[2 * qi + 1] = s;
+    unsigned long long top[kProjTopK];
+    const int ncand = proj_scan<16, kProjTopK>(c, q, qd0, qd1, gl, [occ0](int i) { return occ0 && occ0[i]; }, top);
+    if (in && gl < kProjTopK) {
+        unsigned long long v = top[0];
+#pragma unroll
+        for (int t = 1; t < kProjTopK; t++)
+            if (gl == t) v = top[t];
+        c.scan[(long long)kProjTopK * qi + gl] = v;
+        if (gl == 0) c.scan_cnt[qi] = ncand;
     }
 }
 
@@ -508,9 +535,18 @@ __device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:1
 }
 
 constexpr int kProjMaxFeatures = 65536;
+constexpr int kClaimTab = 2048;  // claim table of one resolve round (power of 2)
 
+/* One wave per call. Chunks of 64 queries (lane j = query base+j) are evaluated in registers: each
+ * lane's best / second are the first two entries of its top-K list not occupied in the live bitmap
+ * (claims only remove candidates, so the remaining order is unchanged). Lanes commit in order up to
+ * the first lane whose best (or, with the ratio test, second) element is claimed by an earlier
+ * uncommitted lane of the chunk; that lane is re-filtered in the next round against the bitmap that
+ * now holds those claims. A lane whose filtered list ran out while the list was truncated (more than
+ * K candidates) is re-scanned by the whole wave against the bitmap. */
 __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict__ calls) {
     __shared__ uint32_t s_occ[kProjMaxFeatures / 32];
+    __shared__ int s_claim[kClaimTab];
     __shared__ int s_hist[32];
     const ProjCall& c = calls[blockIdx.x];
     const int lane = threadIdx.x;
@@ -528,68 +564,110 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
     __threadfence();
     wave_lds_sync();
     auto occ_get = [](int i) { return (s_occ[i >> 5] >> (i & 31)) & 1u; };
+    const int need = c.ratio ? 2 : 1;  // list entries that decide the result
+    for (int i = lane; i < kClaimTab; i += 64) s_claim[i] = 64;
+    wave_lds_sync();
     int nacc = 0;
-    int base = 0;
-    while (base < c.nq) {
+    // chunk registers; the next chunk's loads are issued before the current chunk's rounds
+    unsigned long long top[kProjTopK], ntop[kProjTopK];
+    int ncand = 0, flags = 0, src = 0, nncand = 0, nflags = 0, nsrc = 0;
+    float qang = 0.f, nqang = 0.f;
+    auto load_chunk = [&](int b0, unsigned long long (&t)[kProjTopK], int& cnt, int& fl, int& sr, float& an) {
+        const int qi = b0 + lane;
+#pragma unroll
+        for (int k = 0; k < kProjTopK; k++) t[k] = kNoKey;
+        cnt = 0;
+        fl = 0;
+        sr = 0;
+        an = 0.f;
+        if (qi < c.nq) {
+#pragma unroll
+            for (int k = 0; k < kProjTopK; k++) t[k] = c.scan[(long long)kProjTopK * qi + k];
+            cnt = c.scan_cnt[qi];
+            const ProjQuery& q = c.q[qi];
+            fl = q.flags;
+            sr = q.src;
+            an = q.angle;
+        }
+    };
+    load_chunk(0, ntop, nncand, nflags, nsrc, nqang);
+    for (int base = 0; base < c.nq; base += 64) {
         const int qi = base + lane;
         const bool in = qi < c.nq;
-        unsigned long long b = kNoKey, s = kNoKey;
-        int flags = 0;
-        if (in) {
-            b = c.scan[2 * qi];
-            s = c.scan[2 * qi + 1];
-            flags = c.q[qi].flags;
-        }
-        const int bi = b != kNoKey ? (int)(b & 0xffff) : -1;
-        const int si = s != kNoKey ? (int)(s & 0xffff) : -1;
-        const bool acc = in && proj_accept(c, b, s);
-        const bool cl = acc && (flags & kProjClaims);
-        bool dirty = in && ((bi >= 0 && occ_get(bi)) || (si >= 0 && occ_get(si)));
-        const int my_claim = cl ? bi : -1;
-        for (int k = 0; k < 63; k++) {
-            const int bk = __shfl(my_claim, k);
-            if (k < lane && bk >= 0 && (bk == bi || bk == si)) dirty = true;
-        }
-        const unsigned long long dm = __ballot(dirty);
-        const int d = dm ? __ffsll((long long)dm) - 1 : 64;
-        if (lane < d && acc) {
-            const ProjQuery& q = c.q[qi];
-            atomicMax(&c.match[bi], q.src);
-            if (cl) atomicOr(&s_occ[bi >> 5], 1u << (bi & 31));
-            c.res[2 * qi] = bi;
-            c.res[2 * qi + 1] = c.check_ori ? rot_bin(q.angle, c.angle[bi]) : 0;
-            nacc++;
-        } else if (lane < d && in) {
-            c.res[2 * qi] = -1;
-        }
-        __threadfence();
-        wave_lds_sync();
-        if (d < 64) {  // re-scan query base+d against the live occupancy (64 lanes)
-            const int qd = base + d;
-            const ProjQuery q = c.q[qd];
-            const uint4* qp = (const uint4*)(c.qdesc + (long long)qd * 32);
-            unsigned long long b2, s2;
-            proj_scan<64>(c, q, qp[0], qp[1], lane, occ_get, b2, s2);
-            const bool acc2 = proj_accept(c, b2, s2);
-            if (lane == 0) {
-                if (acc2) {
-                    const int bi2 = (int)(b2 & 0xffff);
-                    atomicMax(&c.match[bi2], q.src);
-                    if (q.flags & kProjClaims) atomicOr(&s_occ[bi2 >> 5], 1u << (bi2 & 31));
-                    c.res[2 * qd] = bi2;
-                    c.res[2 * qd + 1] = c.check_ori ? rot_bin(q.angle, c.angle[bi2]) : 0;
+#pragma unroll
+        for (int t = 0; t < kProjTopK; t++) top[t] = ntop[t];
+        ncand = nncand;
+        flags = nflags;
+        src = nsrc;
+        qang = nqang;
+        if (base + 64 < c.nq) load_chunk(base + 64, ntop, nncand, nflags, nsrc, nqang);
+        int done = 0;  // lanes < done are committed
+        while (done < 64 && base + done < c.nq) {
+            const bool act = in && lane >= done;
+            unsigned long long b = kNoKey, s = kNoKey;
+            int found = 0;
+#pragma unroll
+            for (int t = 0; t < kProjTopK; t++) {
+                const unsigned long long k = top[t];
+                if (k == kNoKey || occ_get((int)(k & 0xffff))) continue;
+                if (found == 0) b = k; else if (found == 1) s = k;
+                found++;
+            }
+            const bool rescan = act && found < need && ncand > kProjTopK;
+            const int bi = b != kNoKey ? (int)(b & 0xffff) : -1;
+            const int si = s != kNoKey ? (int)(s & 0xffff) : -1;
+            const bool acc = act && !rescan && proj_accept(c, b, s);
+            const int my_claim = acc && (flags & kProjClaims) ? bi : -1;
+            // conflicts with earlier uncommitted claims of this round: claim table (lane ids, hashed by feature;
+            // a collision only delays a lane to the next round)
+            if (my_claim >= 0) atomicMin(&s_claim[my_claim & (kClaimTab - 1)], lane);
+            wave_lds_sync();
+            bool dirty = rescan;
+            if (act && bi >= 0 && s_claim[bi & (kClaimTab - 1)] < lane) dirty = true;
+            if (act && need == 2 && si >= 0 && s_claim[si & (kClaimTab - 1)] < lane) dirty = true;
+            const unsigned long long dm = __ballot(act && dirty);
+            const int d = dm ? __ffsll((long long)dm) - 1 : 64;
+            wave_lds_sync();
+            if (my_claim >= 0) s_claim[my_claim & (kClaimTab - 1)] = 64;
+            if (act && lane < d) {
+                if (acc) {
+                    atomicMax(&c.match[bi], src);
+                    if (my_claim >= 0) atomicOr(&s_occ[bi >> 5], 1u << (bi & 31));
+                    c.res[2 * qi] = bi;
+                    c.res[2 * qi + 1] = c.check_ori ? rot_bin(qang, c.angle[bi]) : 0;
                     nacc++;
                 } else {
-                    c.res[2 * qd] = -1;
+                    c.res[2 * qi] = -1;
                 }
             }
-            __threadfence();
             wave_lds_sync();
-            base = qd + 1;
-        } else {
-            base += 64;
+            if (d < 64 && __shfl((int)rescan, d)) {  // whole-wave re-scan of query base+d
+                const int qd = base + d;
+                const ProjQuery q = c.q[qd];
+                const uint4* qp = (const uint4*)(c.qdesc + (long long)qd * 32);
+                unsigned long long t2[2];
+                proj_scan<64, 2>(c, q, qp[0], qp[1], lane, occ_get, t2);
+                const bool acc2 = proj_accept(c, t2[0], t2[1]);
+                if (lane == 0) {
+                    if (acc2) {
+                        const int bi2 = (int)(t2[0] & 0xffff);
+                        atomicMax(&c.match[bi2], q.src);
+                        if (q.flags & kProjClaims) atomicOr(&s_occ[bi2 >> 5], 1u << (bi2 & 31));
+                        c.res[2 * qd] = bi2;
+                        c.res[2 * qd + 1] = c.check_ori ? rot_bin(q.angle, c.angle[bi2]) : 0;
+                        nacc++;
+                    } else {
+                        c.res[2 * qd] = -1;
+                    }
+                }
+                wave_lds_sync();
+                done = d + 1;
+            } else {
+                done = d;
+            }
         }
     }
+    __threadfence();
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) nacc += __shfl_xor(nacc, o);
     if (c.check_ori) {  // rotation consistency (ORBmatcher.cc:1437-1467)
@@ -635,6 +713,76 @@ hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hi
     hipLaunchKernelGGL(k_grid, dim3(ncalls), dim3(1024), 0, st, d_calls);
     if (max_nq > 0) hipLaunchKernelGGL(k_proj_scan, dim3((max_nq + 15) / 16, ncalls), dim3(256), 0, st, d_calls);
     hipLaunchKernelGGL(k_proj_resolve, dim3(ncalls), dim3(64), 0, st, d_calls);
+    return hipGetLastError();
+}
+
+/* ============================ ComputeDistinctiveDescriptors ============================ */
+
+constexpr int kDistinctMaxObs = 1024;
+constexpr int kDistinctWaves = 4;
+
+__device__ __forceinline__ int desc_dist(const uint4 q0, const uint4 q1, const uint8_t* dj) {
+    const uint4 c0 = ((const uint4*)dj)[0], c1 = ((const uint4*)dj)[1];
+    return __popc(q0.x ^ c0.x) + __popc(q0.y ^ c0.y) + __popc(q0.z ^ c0.z) + __popc(q0.w ^ c0.w) +
+           __popc(q1.x ^ c1.x) + __popc(q1.y ^ c1.y) + __popc(q1.z ^ c1.z) + __popc(q1.w ^ c1.w);
+}
+
+__global__ __launch_bounds__(64 * kDistinctWaves) void k_distinctive(int npoints, const int32_t* __restrict__ off,
+                                                                      const uint8_t* __restrict__ desc,
+                                                                      int32_t* __restrict__ best_idx,
+                                                                      uint8_t* __restrict__ out_desc) {
+    __shared__ uint16_t s_d[kDistinctWaves][kDistinctMaxObs];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int p = blockIdx.x * kDistinctWaves + wv;
+    if (p >= npoints) return;
+    const int b = off[p], N = off[p + 1] - b;
+    if (N <= 0) {  // no observations / all observing KeyFrames bad: mDescriptor unchanged
+        if (lane == 0) best_idx[p] = -1;
+        return;
+    }
+    const bool in_lds = N <= kDistinctMaxObs;  // longer rows are recomputed per radix pass
+    uint16_t* d = s_d[wv];
+    const uint8_t* rows = desc + (long long)b * 32;
+    const int k = (int)(0.5 * (N - 1));  // vDists[0.5*(N-1)] (MapPoint.cc:290)
+    int bestMedian = 0x7fffffff, bestIdx = 0;
+    for (int i = 0; i < N; i++) {
+        const uint4 q0 = ((const uint4*)(rows + (long long)i * 32))[0], q1 = ((const uint4*)(rows + (long long)i * 32))[1];
+        if (in_lds) {
+            for (int j = lane; j < N; j += 64) d[j] = (uint16_t)desc_dist(q0, q1, rows + (long long)j * 32);
+            wave_lds_sync();
+        }
+        // k-th smallest of row i (Distances[i][i] = 0 is part of the row): 9-bit radix select
+        int prefix = 0, rank = k;
+        for (int bit = 8; bit >= 0; bit--) {
+            int cnt0 = 0;
+            for (int j0 = 0; j0 < N; j0 += 64) {
+                const int j = j0 + lane;
+                int v = 0x7fff;
+                if (j < N) v = in_lds ? d[j] : desc_dist(q0, q1, rows + (long long)j * 32);
+                const bool in = j < N && (v >> (bit + 1)) == (prefix >> (bit + 1)) && !((v >> bit) & 1);
+                cnt0 += __popcll(__ballot(in));
+            }
+            if (rank >= cnt0) {
+                rank -= cnt0;
+                prefix |= 1 << bit;
+            }
+        }
+        wave_lds_sync();
+        if (prefix < bestMedian) {  // first strict minimum (MapPoint.cc:292-296)
+            bestMedian = prefix;
+            bestIdx = i;
+        }
+    }
+    if (lane == 0) best_idx[p] = bestIdx;
+    if (out_desc && lane < 8)
+        ((uint32_t*)(out_desc + (long long)p * 32))[lane] = ((const uint32_t*)(rows + (long long)bestIdx * 32))[lane];
+}
+
+hipError_t launch_distinctive(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best_idx,
+                              uint8_t* out_desc, hipStream_t st) {
+    if (npoints <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_distinctive, dim3((npoints + kDistinctWaves - 1) / kDistinctWaves), dim3(64 * kDistinctWaves),
+                       0, st, npoints, off, desc, best_idx, out_desc);
     return hipGetLastError();
 }
 

@@ -57,6 +57,8 @@ hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* 
                              hipStream_t st);
 
 hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st);
+hipError_t launch_distinctive(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best_idx,
+                              uint8_t* out_desc, hipStream_t st);
 int stereo_lds_bytes(int cap, int nrows);
 hipError_t stereo_setup(int lds_bytes);
 hipError_t launch_stereo(const StereoArgs& a, int npairs, const int32_t* fl, const int32_t* fr, const orbx_kp* kpsL,

@@ -67,7 +67,8 @@ struct ProjCall {
     int check_ori;
     int* grid_start;           // [kGridCols*kGridRows + 1]
     uint16_t* grid_idx;        // [n]
-    unsigned long long* scan;  // [2*nq] best / second keys
+    unsigned long long* scan;  // [4*nq] the 4 smallest candidate keys per query, ascending
+    int* scan_cnt;             // [nq] candidates per query
     int* res;                  // [2*nq] accepted feature idx / rotation bin
     int32_t* match;            // [n]
     int32_t* nmatches;

@@ -79,6 +79,8 @@ SIGNATURES = {
     "orbm_search_by_projection_last_frame": (_I, [_P, _P, _P, _P, _P, _F, _I, _I, _P, C.POINTER(_I)]),
     "orbm_search_by_projection_keyframe": (_I, [_P, _P, _P, _P, _F, _I, _I, _P, C.POINTER(_I)]),
     "orbm_search_by_projection_sim3": (_I, [_P, _P, _P, _P, _I, _P, C.POINTER(_I)]),
+    "orbm_compute_distinctive_descriptors": (_I, [_P, _I, _P, _P, _P, _P]),
+    "orbm_compute_distinctive_descriptors_device": (_I, [_P, _I, _P, _P, _P, _P, _P]),
     "orbx_selftest_sincosf": (_I, [_P, _P, _P, _I, _P]),
     "orbx_profile_enable": (_I, [_P, _I]),
     "orbx_profile_read": (_I, [_P, C.POINTER(C.c_double), C.POINTER(_I)]),

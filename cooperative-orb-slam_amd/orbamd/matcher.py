@@ -174,3 +174,19 @@ class ORBmatcher:
         m = mps.cstruct()
         S = np.ascontiguousarray(Scw, np.float32).reshape(16)
         return self._proj("orbm_search_by_projection_sim3", KF, S.ctypes.data, C.byref(m), int(th))
+
+
+def compute_distinctive_descriptors(offsets, desc, device=0, matcher=None):
+    """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of MapPoints:
+    MapPoint p's observed descriptors are desc[offsets[p]:offsets[p+1]]. Returns (best_idx int32 [P]
+    (-1 = no descriptors), chosen descriptors uint8 [P, 32])."""
+    lib = load()
+    m = matcher or ORBmatcher(device=device)
+    off = np.ascontiguousarray(offsets, np.int32)
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    P = len(off) - 1
+    best = np.empty(max(P, 1), np.int32)
+    out = np.zeros((max(P, 1), 32), np.uint8)
+    check(lib.orbm_compute_distinctive_descriptors(m._h, P, off.ctypes.data, d.ctypes.data, best.ctypes.data,
+                                                   out.ctypes.data), "orbm_compute_distinctive_descriptors")
+    return best[:P], out[:P]

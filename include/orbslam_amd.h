@@ -277,6 +277,20 @@ int orbm_search_by_projection_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, con
                                    const orbm_mappoints* mp, int th, int32_t* match, int* nmatches);
 
 /* ------------------------------------------------------------------------------------
+ * MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of MapPoints.
+ * MapPoint p's observed descriptors (the rows pKF->mDescriptors.row(idx) of its non-bad
+ * observing KeyFrames, in mObservations order) are desc[offsets[p] .. offsets[p+1]) (32 B
+ * each). best_idx[p] = index within that list of the descriptor with the least median
+ * Hamming distance to the others (first on ties), -1 if the list is empty (mDescriptor left
+ * unchanged); out_desc[p] (optional) = that descriptor.
+ * ---------------------------------------------------------------------------------- */
+int orbm_compute_distinctive_descriptors(orbm_ctx* ctx, int npoints, const int32_t* offsets,
+                                         const uint8_t* desc, int32_t* best_idx, uint8_t* out_desc);
+int orbm_compute_distinctive_descriptors_device(orbm_ctx* ctx, int npoints, const int32_t* d_offsets,
+                                                const uint8_t* d_desc, int32_t* d_best_idx,
+                                                uint8_t* d_out_desc, void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Cross-agent exchange slot (replaces the LCM KeyFrameexample message,
  * ORB_SLAM2.1/Examples/ROS/ORB_SLAM2/src/ros_mono.cc:1907-2410).
  * slot = [u32 n | u32 pad[15] | n x orbx_kp (24 B) | n x 32 B descriptors], fixed size

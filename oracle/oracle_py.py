@@ -56,6 +56,7 @@ _SIG = {
     "oc_search_by_projection_last_frame": (_I, [_P, _P, _P, _P, _F, _I, _I, _P]),
     "oc_search_by_projection_keyframe": (_I, [_P, _P, _P, _F, _I, _I, _P]),
     "oc_search_by_projection_sim3": (_I, [_P, _P, _P, _I, _P]),
+    "oc_compute_distinctive_descriptors": (None, [_I, _P, _P, _P]),
 }
 
 _lib = None
@@ -281,3 +282,12 @@ def search_by_projection_sim3(KF, Scw, mps, th):
     m = mps.cstruct()
     S = np.ascontiguousarray(Scw, np.float32).reshape(16)
     return _proj("oc_search_by_projection_sim3", KF, S.ctypes.data, C.byref(m), int(th))
+
+
+def compute_distinctive_descriptors(offsets, desc):
+    """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) per CSR list; returns best_idx."""
+    off = np.ascontiguousarray(offsets, np.int32)
+    d = np.ascontiguousarray(desc, np.uint8)
+    out = np.empty(max(len(off) - 1, 1), np.int32)
+    load().oc_compute_distinctive_descriptors(len(off) - 1, off.ctypes.data, d.ctypes.data, out.ctypes.data)
+    return out[:len(off) - 1]

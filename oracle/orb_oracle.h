@@ -78,6 +78,8 @@ int oc_search_by_projection_last_frame(const orbm_frame_view* F, const float* Tc
                                        const float* Tcw_l, float th, int bMono, int checkOri, int32_t* match);
 int oc_search_by_projection_keyframe(const orbm_frame_view* F, const float* Tcw_c, const orbm_mappoints* mp, float th,
                                      int ORBdist, int checkOri, int32_t* match);
+void oc_compute_distinctive_descriptors(int npoints, const int32_t* offsets, const uint8_t* desc,
+                                        int32_t* best_idx);
 int oc_search_by_projection_sim3(const orbm_frame_view* KF, const float* Scw, const orbm_mappoints* mp, int th,
                                  int32_t* match);
 

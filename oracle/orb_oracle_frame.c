@@ -607,3 +607,44 @@ int oc_search_by_projection_sim3(const orbm_frame_view* KF, const float* Scw, co
     grid_free(g);
     return nmatches;
 }
+
+/* ===================================================================================== */
+/* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307)                          */
+/* ===================================================================================== */
+static int int_cmp(const void* a, const void* b) {
+    const int x = *(const int*)a, y = *(const int*)b;
+    return (x > y) - (x < y);
+}
+
+/* one MapPoint: vDescriptors = desc[0..N) (32 B rows); returns BestIdx, -1 if N == 0 */
+static int distinctive_one(const uint8_t* desc, int N) {
+    if (N <= 0) return -1;
+    float* Distances = (float*)malloc(sizeof(float) * (size_t)N * N);
+    for (int i = 0; i < N; i++) {
+        Distances[(size_t)i * N + i] = 0;
+        for (int j = i + 1; j < N; j++) {
+            const int distij = oc_descriptor_distance(desc + 32 * (size_t)i, desc + 32 * (size_t)j);
+            Distances[(size_t)i * N + j] = distij;
+            Distances[(size_t)j * N + i] = distij;
+        }
+    }
+    int BestMedian = INT_MAX, BestIdx = 0;
+    int* vDists = (int*)malloc(sizeof(int) * (size_t)N);
+    for (int i = 0; i < N; i++) {
+        for (int j = 0; j < N; j++) vDists[j] = (int)Distances[(size_t)i * N + j];
+        qsort(vDists, (size_t)N, sizeof(int), int_cmp);
+        const int median = vDists[(size_t)(0.5 * (N - 1))];
+        if (median < BestMedian) {
+            BestMedian = median;
+            BestIdx = i;
+        }
+    }
+    free(vDists);
+    free(Distances);
+    return BestIdx;
+}
+
+void oc_compute_distinctive_descriptors(int npoints, const int32_t* offsets, const uint8_t* desc, int32_t* best_idx) {
+    for (int p = 0; p < npoints; p++)
+        best_idx[p] = distinctive_one(desc + 32 * (size_t)offsets[p], offsets[p + 1] - offsets[p]);
+}

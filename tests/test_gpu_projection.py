@@ -72,3 +72,13 @@ def test_projection_edge_cases():
                             track_proj_xr=np.full(k, F.x[7]), track_level=np.full(k, F.octave[7]),
                             track_view_cos=np.ones(k))
     _same(mt.SearchByProjectionLocal(F, same, 4.0), oracle_py.search_by_projection_local(F, same, 4.0, 0.8))
+
+
+def test_distinctive_descriptors_batch():
+    from test_oracle_frame import distinctive_scene
+    off, desc = distinctive_scene(2, big=True)
+    best, chosen = orbamd.matcher.compute_distinctive_descriptors(off, desc)
+    ref = oracle_py.compute_distinctive_descriptors(off, desc)
+    np.testing.assert_array_equal(best, ref)
+    for p in np.nonzero(ref >= 0)[0]:
+        assert (chosen[p] == desc[off[p] + ref[p]]).all()

@@ -240,3 +240,42 @@ def test_projection_variants_oracle_sanity():
     F, Scw, mps = ps.sim3_scene(6)
     n, m = oracle_py.search_by_projection_sim3(F, Scw, mps, 10)
     assert n > F.n // 8 and n == (m >= 0).sum()
+
+
+# ------------------------------------------------------------------ ComputeDistinctiveDescriptors
+def distinctive_scene(seed, big=False):
+    rng = np.random.default_rng(seed)
+    sizes = list(rng.integers(0, 70, 300)) + [1, 2, 3, 0]
+    if big:
+        sizes += [1100, 1500]
+    rows = []
+    for n in sizes:
+        base = rng.integers(0, 256, 32, dtype=np.uint8)
+        obs = np.repeat(base[None], n, 0)
+        if n:
+            obs = ps.flip_bits(rng, obs, 30)
+            dup = rng.random(n) < 0.1  # exact duplicates -> median ties
+            obs[dup] = obs[0]
+        rows.append(obs)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    return off, np.concatenate(rows).astype(np.uint8)
+
+
+def distinctive_py(off, desc):
+    out = []
+    for p in range(len(off) - 1):
+        d = desc[off[p]:off[p + 1]]
+        n = len(d)
+        if n == 0:
+            out.append(-1)
+            continue
+        bits = np.unpackbits(d, axis=1).astype(np.int32)
+        D = (bits[:, None, :] != bits[None, :, :]).sum(-1)
+        med = np.sort(D, axis=1)[:, int(0.5 * (n - 1))]
+        out.append(int(np.argmin(med)))  # first minimum
+    return np.array(out, np.int32)
+
+
+def test_distinctive_oracle_matches_restatement():
+    off, desc = distinctive_scene(1)
+    np.testing.assert_array_equal(oracle_py.compute_distinctive_descriptors(off, desc), distinctive_py(off, desc))

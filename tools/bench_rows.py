@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Measurements of the SURVEY.md 8(f) rows built beside the headline path (one JSON line each).
+
+  stereo       Frame::ComputeStereoMatches on C3 (752x480 stereo, 1200 features): B pairs resident in
+               HBM, one step = extract 2B frames + k_stereo over the B pairs (device batch API);
+               reported as stereo pairs/s, k_stereo's share from HIP events, and the CPU oracle's
+               ComputeStereoMatches alone on the same pairs.
+  projection   SearchByProjection(Frame&, vector<MapPoint*>, th) host API (H2D + grid + scan + resolve
+               + D2H) per call on a 640x480 frame with ~900 candidate MapPoints vs the CPU oracle.
+  distinctive  MapPoint::ComputeDistinctiveDescriptors for 20k MapPoints x ~25 observations (device
+               batch) vs the CPU oracle.
+The CPU figures are the oracle (a plain-C restatement, 1 thread), not the reference build.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "cooperative-orb-slam_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+
+def bench_stereo(torch, steps, B=128):
+    import orbamd
+    import oracle_py
+    W, H, nf = 752, 480, 1200
+    MBF, MB = 47.90639384423901, 0.11
+    dev = torch.device("cuda", 0)
+    left = orbamd.synth_frames(0, 0, B, W, H)
+    right = orbamd.synth_frames(0, 0, B, W, H, dx=9)
+    ext = orbamd.ORBextractor(nf, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=2 * B)
+    stride = ext.max_keypoints(W, H)
+    frames = torch.from_numpy(np.concatenate([left, right])).to(dev)
+    kps = torch.empty((2 * B, stride, 6), dtype=torch.float32, device=dev)
+    desc = torch.empty((2 * B, stride, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(2 * B, dtype=torch.int32, device=dev)
+    fl = torch.arange(B, dtype=torch.int32, device=dev)
+    fr = fl + B
+    ur = torch.empty((B, stride), dtype=torch.float32, device=dev)
+    dp = torch.empty((B, stride), dtype=torch.float32, device=dev)
+    ns = torch.zeros(B, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(ev=None):
+        ext.extract_batch_device(frames, kps, desc, cnt, st)
+        if ev:
+            ev[0].record()
+        orbamd.frame.stereo_matches_batch_device(ext, ext, fl, fr, kps, desc, cnt, kps, desc, cnt, MBF, MB, ur, dp,
+                                                 ns, st)
+        if ev:
+            ev[1].record()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    # CPU oracle: ComputeStereoMatches alone (extraction excluded) on a sample of the pairs
+    ol = oracle_py.OracleExtractor(nf, 1.2, 8, 20, 7)
+    orr = oracle_py.OracleExtractor(nf, 1.2, 8, 20, 7)
+    tc, nc = 0.0, 0
+    for p in range(8):
+        ko, do_ = ol(left[p])
+        kro, dro = orr(right[p])
+        t = time.perf_counter()
+        oracle_py.compute_stereo_matches(ol, orr, ko, do_, kro, dro, MBF, MB)
+        tc += time.perf_counter() - t
+        nc += 1
+    return {"row": "stereo", "workload": "C3 752x480 stereo, 1200 feat, B=%d pairs/step" % B,
+            "pairs_per_s_extract_plus_stereo": round(B * steps / el, 1),
+            "k_stereo_ms_per_step": round(k_ms, 4), "k_stereo_us_per_pair": round(k_ms * 1e3 / B, 3),
+            "stereo_kept_per_pair": round(float(ns.float().mean().item()), 1),
+            "cpu_oracle_ms_per_pair": round(tc / nc * 1e3, 3), "cpu_threads": 1}
+
+
+def bench_projection(reps):
+    import orbamd
+    import oracle_py
+    import proj_scenes as ps
+    F, mps = ps.local_scene(1, True)
+    mt = orbamd.ORBmatcher(0.8, False)
+    for _ in range(3):
+        mt.SearchByProjectionLocal(F, mps, 3.0)
+    t = time.perf_counter()
+    for _ in range(reps):
+        n, _m = mt.SearchByProjectionLocal(F, mps, 3.0)
+    g = (time.perf_counter() - t) / reps
+    t = time.perf_counter()
+    for _ in range(reps):
+        oracle_py.search_by_projection_local(F, mps, 3.0, 0.8)
+    c = (time.perf_counter() - t) / reps
+    return {"row": "search_by_projection_local", "workload": "640x480 frame, %d features, %d MapPoints" % (F.n, mps.n),
+            "gpu_host_api_ms_per_call": round(g * 1e3, 4), "cpu_oracle_ms_per_call": round(c * 1e3, 4),
+            "nmatches": int(n), "cpu_threads": 1}
+
+
+def bench_distinctive(torch, reps):
+    import orbamd
+    import oracle_py
+    rng = np.random.default_rng(3)
+    P = 20000
+    sizes = rng.integers(2, 50, P)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    desc = rng.integers(0, 256, (int(off[-1]), 32), dtype=np.uint8)
+    dev = torch.device("cuda", 0)
+    d_off = torch.from_numpy(off).to(dev)
+    d_desc = torch.from_numpy(desc).to(dev)
+    d_best = torch.empty(P, dtype=torch.int32, device=dev)
+    d_out = torch.empty((P, 32), dtype=torch.uint8, device=dev)
+    mt = orbamd.ORBmatcher()
+    lib = orbamd.load()
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    def run():
+        lib.orbm_compute_distinctive_descriptors_device(mt._h, P, d_off.data_ptr(), d_desc.data_ptr(),
+                                                        d_best.data_ptr(), d_out.data_ptr(), st)
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    g = e0.elapsed_time(e1) / reps
+    ref = None
+    t = time.perf_counter()
+    ref = oracle_py.compute_distinctive_descriptors(off[:2001], desc)
+    c = (time.perf_counter() - t) / 2000 * P
+    assert (d_best[:2000].cpu().numpy() == ref).all()
+    return {"row": "compute_distinctive_descriptors", "workload": "%d MapPoints, %d observations" % (P, int(off[-1])),
+            "gpu_ms_per_batch": round(g, 4), "cpu_oracle_ms_per_batch": round(c * 1e3, 2), "cpu_threads": 1}
+
+
+def main():
+    import torch
+    steps = int(os.environ.get("BENCH_ROWS_STEPS", "10"))
+    for r in (bench_stereo(torch, steps), bench_projection(50), bench_distinctive(torch, 10)):
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
