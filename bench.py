@@ -7,7 +7,10 @@ FAST 20/7) + SearchForTriangulation of frame b against frame b-1 (one BoW node h
 features = the BASELINE "BF" configuration) + the cooperative exchange: each agent packs its
 latest keyframe (keypoints + descriptors) and RCCL-all-gathers it, then matches it against
 every agent's slot. One process per GPU = one agent; frames are
-agent-private, so per-GPU work is fixed as N grows ("weak" scaling).
+agent-private, so per-GPU work is fixed as N grows ("weak" scaling). The B frames of a step are
+split over P concurrent extraction+match graphs (own handle and HIP stream each; frame b of a
+graph is matched against frame b-1 of the same graph), so one graph's latency-bound tail
+(octree, describe, match) overlaps another graph's FAST.
 
 Launch (N>1): python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
               --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
@@ -98,7 +101,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=512, help="frames per step per GPU")
+    ap.add_argument("--pipes", type=int, default=2,
+                    help="concurrent extraction+match graphs per GPU (each over batch/pipes frames, own handle "
+                         "and HIP stream), so one graph's latency-bound tail overlaps the other's FAST")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -121,25 +127,41 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    W, H, B = args.width, args.height, args.batch
+    W, H, B, P = args.width, args.height, args.batch, args.pipes
+    assert B % P == 0, "--batch must be a multiple of --pipes"
+    sub = B // P
     frames_np = orbamd.synth_frames(rank, 0, B, W, H)  # agent = rank
-    frames = torch.from_numpy(frames_np).to(dev)
-    pipe = orbamd.device.BatchPipeline(torch, W, H, B, device=local)
+    frames = [torch.from_numpy(frames_np[p * sub:(p + 1) * sub]).to(dev) for p in range(P)]
+    pipes = [orbamd.device.BatchPipeline(torch, W, H, sub, device=local) for _ in range(P)]
+    streams = [torch.cuda.Stream(dev) for _ in range(P)]
+    pipe = pipes[0]
     slot_bytes = pipe.slot_bytes()
     my_slot = torch.zeros(slot_bytes, dtype=torch.uint8, device=dev)
     all_slots = torch.zeros(world * slot_bytes, dtype=torch.uint8, device=dev)
     xmatch = torch.empty((world, pipe.stride), dtype=torch.int32, device=dev)
     xn = torch.zeros(world, dtype=torch.int32, device=dev)
 
-    def step():
-        pipe.step(frames)
-        if not args.no_exchange:
-            pipe.pack(0, my_slot)  # this agent's latest keyframe
+    def exchange():
+        # this agent's latest keyframe -> RCCL all-gather -> match against every agent's slot
+        with torch.cuda.stream(streams[0]):
+            pipe.pack(0, my_slot, streams[0].cuda_stream)
             if world > 1:
                 dist.all_gather_into_tensor(all_slots, my_slot)
             else:
                 all_slots.copy_(my_slot)
-            pipe.match_packed(0, all_slots, world, xmatch, xn)
+            pipe.match_packed(0, all_slots, world, xmatch, xn, streams[0].cuda_stream)
+
+    def step(ev=None):
+        for p in range(P):
+            st = streams[p].cuda_stream
+            pipes[p].extract(frames[p], st)
+            if ev is not None:
+                ev[p][0].record(streams[p])
+            pipes[p].match_pairs(st)
+            if ev is not None:
+                ev[p][1].record(streams[p])
+        if not args.no_exchange:
+            exchange()
 
     for _ in range(args.warmup):
         step()
@@ -151,35 +173,32 @@ def main():
     def run_profiled(mask, nsteps, timed):
         """nsteps steps with HIP event pairs around the stages in `mask` (each on the stream its
         kernel runs on; the overlapped schedule is unchanged) and torch events around the matcher."""
-        lib.orbx_profile_enable(pipe.ext._h, mask)
-        e0 = [torch.cuda.Event(enable_timing=True) for _ in range(nsteps)]
-        e1 = [torch.cuda.Event(enable_timing=True) for _ in range(nsteps)]
+        for pp in pipes:
+            lib.orbx_profile_enable(pp.ext._h, mask)
+        evs = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(P)]
+               for _ in range(nsteps)]
         if timed and world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t_start = time.perf_counter()
         for i in range(nsteps):
-            pipe.extract(frames)
-            e0[i].record()
-            pipe.match_pairs()
-            e1[i].record()
-            if not args.no_exchange:
-                pipe.pack(0, my_slot)
-                if world > 1:
-                    dist.all_gather_into_tensor(all_slots, my_slot)
-                else:
-                    all_slots.copy_(my_slot)
-                pipe.match_packed(0, all_slots, world, xmatch, xn)
+            step(evs[i])
         torch.cuda.synchronize()
         if timed and world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t_start
-        ms = (C.c_double * 5)()
-        nc = C.c_int()
-        lib.orbx_profile_read(pipe.ext._h, ms, C.byref(nc))
-        lib.orbx_profile_enable(pipe.ext._h, 0)
-        st = {k: ms[i] / max(nc.value, 1) for i, k in enumerate(stages) if (mask >> i) & 1}
-        st["match"] = sum(a.elapsed_time(b) for a, b in zip(e0, e1)) / nsteps
+        acc = [0.0] * 5
+        ncalls = 0
+        for pp in pipes:
+            ms = (C.c_double * 5)()
+            nc = C.c_int()
+            lib.orbx_profile_read(pp.ext._h, ms, C.byref(nc))
+            lib.orbx_profile_enable(pp.ext._h, 0)
+            for i in range(5):
+                acc[i] += ms[i]
+            ncalls += nc.value
+        st = {k: acc[i] / max(ncalls, 1) for i, k in enumerate(stages) if (mask >> i) & 1}
+        st["match"] = sum(e[p][0].elapsed_time(e[p][1]) for e in evs for p in range(P)) / (nsteps * P)
         return elapsed, st
 
     # 1) stage split (untimed): every stage bracketed, same schedule
@@ -191,8 +210,8 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    nkp = float(pipe.counts.float().mean().item())
-    nmatch = float(pipe.nmatch.float().mean().item())
+    nkp = float(sum(pp.counts.float().mean().item() for pp in pipes) / P)
+    nmatch = float(sum(pp.nmatch.float().mean().item() for pp in pipes) / P)
 
     total_frames = world * B * args.steps
     value = total_frames / el
@@ -200,7 +219,8 @@ def main():
     if rank == 0:
         b_frame, per_stage = algorithmic_bytes(W, H, nkp)
         dom_ms = dom_live[dom]
-        achieved = per_stage[dom] * B / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and per_stage[dom] > 0 else 0.0
+        # one launch of the dominant kernel processes one graph's sub-batch (B / P frames)
+        achieved = per_stage[dom] * sub / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and per_stage[dom] > 0 else 0.0
         traffic = valu_insts = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc_path):
@@ -226,10 +246,11 @@ def main():
             "config": {"workload": "C2: synthetic %dx%d uint8, nfeatures 1000, scale 1.2, 8 levels, FAST 20/7; "
                                    "extract + BF SearchForTriangulation vs previous frame + per-step keyframe "
                                    "all-gather & cross-agent match" % (W, H),
-                       "frames_per_step_per_gpu": B, "parallelism": "agent-per-gpu x%d" % world},
+                       "frames_per_step_per_gpu": B, "graphs_per_gpu": P,
+                       "parallelism": "agent-per-gpu x%d" % world},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": per_stage[dom] * B,
+                         "algorithmic_bytes_per_launch": per_stage[dom] * sub,
                          "launch_ms": round(dom_ms, 4)},
             # what actually bounds these byte/integer kernels: vector-instruction issue
             # (wave64 VALU op = 2 cycles on a SIMD-32; 1024 SIMDs at 2.4 GHz)
@@ -253,7 +274,8 @@ def main():
         result["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(result), flush=True)
-    pipe.close()
+    for pp in pipes:
+        pp.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
