@@ -347,6 +347,77 @@ __device__ __forceinline__ int fast_strength(const uint8_t* p, int P) {
     return S < 0 ? 0 : S;
 }
 
+/* fast_strength with the dark and bright sides in the two i16 halves of one register:
+ * X_k = (v - r_k, r_k - v), so one packed min/max chain yields (A, B') with
+ * A = max_arc min(v - ring) and B' = max_arc min(ring - v) = -Bm; S = max(A, B', 0). */
+__device__ __forceinline__ int fast_strength_pk(const uint8_t* roi, int o, int P) {
+    int ow = o - 3 * P - 3;  // 7x7 window origin: every ring offset is a non-negative immediate
+    asm volatile("" : "+v"(ow));  // keep the origin as the DS base (no re-association into negative offsets)
+    const uint8_t* w = roi + ow;
+    const int v = w[3 * P + 3];
+    const short2v vp = {(short)v, (short)-v};
+    const short2v sg = {(short)-1, (short)1};
+    const int off[16] = {6 * P + 3, 6 * P + 4, 5 * P + 5, 4 * P + 6, 3 * P + 6, 2 * P + 6, P + 5, 4,
+                         3, 2, P + 1, 2 * P, 3 * P, 4 * P, 5 * P + 1, 6 * P + 2};
+    short2v x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const short r = (short)w[off[k]];
+        const short2v rr = {r, r};
+        x[k] = rr * sg + vp;
+    }
+    short2v m2[16], m4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(x[k], x[(k + 1) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+    short2v a = {(short)-1024, (short)-1024};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const short2v m9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), x[(k + 8) & 15]);
+        a = __builtin_elementwise_max(a, m9);
+    }
+    const int S = max((int)a.x, (int)a.y);
+    return S < 0 ? 0 : S;
+}
+
+/* fast_strength as packed f16 (integers in [-255, 255] are exact in f16, and min/max are exact):
+ * X_k = (v - r_k, r_k - v) from the byte r_k as f16(1024 + r_k) = bits 0x6400 | r_k (one v_perm) and one
+ * v_pk_fma_f16; every 9-arc minimum is min3(min3 of 3 consecutive) and the arc maximum a max3 tree, on
+ * gfx950's v_pk_minimum3_f16 / v_pk_maximum3_f16: about half the min/max instructions of the i16 form. */
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int fast_strength_h2(const uint8_t* roi, int o, int P) {
+    int ow = o - 3 * P - 3;  // 7x7 window origin: every ring offset is a non-negative immediate
+    asm volatile("" : "+v"(ow));
+    const uint8_t* w = roi + ow;
+    const int v = w[3 * P + 3];
+    const uint32_t vb = __builtin_amdgcn_perm(0x64646464u, (uint32_t)v, 0x04000400u);  // (1024+v, 1024+v)
+    const half2v vp = __builtin_bit_cast(half2v, vb ^ 0x80000000u);                  // (1024+v, -(1024+v))
+    const half2v sg = {(_Float16)-1.0f, (_Float16)1.0f};
+    const int off[16] = {6 * P + 3, 6 * P + 4, 5 * P + 5, 4 * P + 6, 3 * P + 6, 2 * P + 6, P + 5, 4,
+                         3, 2, P + 1, 2 * P, 3 * P, 4 * P, 5 * P + 1, 6 * P + 2};
+    half2v x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t rb = __builtin_amdgcn_perm(0x64646464u, (uint32_t)w[off[k]], 0x04000400u);
+        x[k] = __builtin_elementwise_fma(__builtin_bit_cast(half2v, rb), sg, vp);
+    }
+    half2v m3[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        m3[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(x[k], x[(k + 1) & 15]), x[(k + 2) & 15]);
+    half2v m9[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        m9[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]);
+    half2v a = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m9[0], m9[1]), m9[2]);
+#pragma unroll
+    for (int k = 3; k < 15; k += 2) a = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, m9[k]), m9[k + 1]);
+    a = __builtin_elementwise_maximum(a, m9[15]);
+    const int S = max((int)(float)a.x, (int)(float)a.y);
+    return S < 0 ? 0 : S;
+}
+
 /* NMS survivor test of cv::FAST (FAST_t, nonmax_suppression) at threshold t, on the
  * cell's S buffer (zero outside the detection band [3, rows-3) x [3, cols-3)).
  * cv::FAST keeps a corner (S > t, score S-1) iff its score is strictly greater than the score of
@@ -376,18 +447,23 @@ __device__ __forceinline__ bool fast_pretest(const uint8_t* p, int P, int t) {
 }
 
 /* LDS bytes per wave of k_fast_cells2: ROI + S map (RP x RH each) + candidate list (u16 per
- * band pixel; a band is at most (RP-6) x (RH-6)) */
+ * band pixel; a band is at most (RP-6) x (RH-6)) + 64 per-lane dummy slots of the compaction */
 __host__ __device__ inline int fast_wave_lds(int RP, int RH) {
-    return 2 * RP * RH + ((2 * (RP - 6) * (RH - 6) + 15) & ~15);
+    return 2 * RP * RH + ((2 * ((RP - 6) * (RH - 6) + 64) + 15) & ~15);
 }
 
-template <int kMaxPass>
+template <int kMaxPass, int kRP>
 __global__ __launch_bounds__(256) void k_fast_cells2(
     const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
     ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
-    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP, int RH, int cell_lo, int cell_hi) {
+    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi) {
+    // compile-time ROI pitch for the common geometries: every LDS offset of the ring/NMS reads becomes an
+    // instruction immediate
+    const int RP = kRP ? kRP : RP_;
     extern __shared__ __align__(16) uint8_t lds[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave index through readfirstlane: the cell descriptor, loop bounds and addressing are wave-uniform
+    // (scalar loads / SALU) instead of per-lane VALU
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int ci = cell_lo + blockIdx.x * 4 + wave;
     if (ci >= cell_hi) return;  // wave-uniform; no block barriers in this kernel
@@ -450,9 +526,11 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
             const int rpc = c.rpc;
             const int lr = (lane * c.magG) >> 16, j = lane - lr * G;
             const bool lane_ok = lane < rpc * G;
-            int colmask = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) colmask |= (4 * j + i >= 3 && 4 * j + i < 3 + bw) ? (1 << i) : 0;
+            // band-column masks at the keep bits: pixels 0 / 2 in keep2[0] bits 15 / 31, pixels 1 / 3 in keep2[1]
+            auto colok = [&](int i) { return 4 * j + i >= 3 && 4 * j + i < 3 + bw; };
+            const uint32_t cm0 = (colok(0) ? 0x8000u : 0u) | (colok(2) ? 0x80000000u : 0u);
+            const uint32_t cm1 = (colok(1) ? 0x8000u : 0u) | (colok(3) ? 0x80000000u : 0u);
+            const int dummy = (RP - 6) * (RH - 6);  // 64 per-lane dummy slots after the list
             const uint32_t tq = (uint32_t)(t_lo + 1) * 0x00010001u;
             for (int r0 = 0; r0 < bh; r0 += rpc) {
                 const int rr = 3 + r0 + lr;
@@ -491,28 +569,25 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
                     const uint32_t xdk = (d0 & d8) | (d4 & d12);
                     keep2[half] = ~(xb & xdk);  // bits 15 / 31 set = candidate
                 }
-                int m = (int)(((keep2[0] >> 15) & 1u) | ((keep2[1] >> 14) & 2u) | ((keep2[0] >> 29) & 4u) |
-                              ((keep2[1] >> 28) & 8u));
-                m &= (lane_ok && rr < 3 + bh) ? colmask : 0;
+                // pixel i of this lane: i = 0, 2 -> bits 15, 31 of keep2[0]; i = 1, 3 -> bits 15, 31 of keep2[1]
+                const uint32_t rowm = (lane_ok && rr < 3 + bh) ? 0xffffffffu : 0u;
+                const uint32_t k0 = keep2[0] & cm0 & rowm, k1 = keep2[1] & cm1 & rowm;
+                const bool p0 = (int)(k0 << 16) < 0, p1 = (int)(k1 << 16) < 0, p2 = (int)k0 < 0, p3 = (int)k1 < 0;
                 // ordered compaction: row-major = (lane, pixel) lexicographic
-                int pre = 0, tot = 0;
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const unsigned long long bi = __ballot((m >> i) & 1);
-                    pre = __builtin_amdgcn_mbcnt_hi((unsigned)(bi >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bi, pre));
-                    tot += __popcll(bi);
-                }
-                if (m) {
-                    int pos = ncand + pre;
-                    const int e = (rr << 8) | (4 * j);
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        if ((m >> i) & 1) {
-                            clist[pos] = (uint16_t)(e + i);
-                            pos++;
-                        }
-                    }
-                }
+                const unsigned long long B0 = __ballot(p0), B1 = __ballot(p1), B2 = __ballot(p2), B3 = __ballot(p3);
+                int pre = __builtin_amdgcn_mbcnt_hi((unsigned)(B0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)B0, 0));
+                pre = __builtin_amdgcn_mbcnt_hi((unsigned)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)B1, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((unsigned)(B2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)B2, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((unsigned)(B3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)B3, pre));
+                const int tot = __popcll(B0) + __popcll(B1) + __popcll(B2) + __popcll(B3);
+                // unconditional writes: a pixel that is not a candidate goes to this lane's dummy slot
+                const int e = (rr << 8) | (4 * j);
+                const int q0 = ncand + pre, q1 = q0 + (int)p0, q2 = q1 + (int)p1, q3 = q2 + (int)p2;
+                const int dmy = dummy + lane;
+                clist[p0 ? q0 : dmy] = (uint16_t)e;
+                clist[p1 ? q1 : dmy] = (uint16_t)(e + 1);
+                clist[p2 ? q2 : dmy] = (uint16_t)(e + 2);
+                clist[p3 ? q3 : dmy] = (uint16_t)(e + 3);
                 ncand += tot;
             }
         }
@@ -520,7 +595,7 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
         for (int i = lane; i < ncand; i += 64) {
             const int e = clist[i];
             const int o = (e >> 8) * RP + (e & 0xFF);
-            const int S = fast_strength(roi + o, RP);
+            const int S = fast_strength_h2(roi, o, RP);
             if (S > t_lo) str[o] = (uint8_t)S;
         }
         wave_sync();
@@ -1324,15 +1399,22 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
     if (cell_hi <= cell_lo) return hipSuccess;
     dim3 grid((cell_hi - cell_lo + 3) / 4, nframes);
     const size_t lds = 4 * (size_t)fast_wave_lds(RP, RH);
-    if (max_pass <= 8)
-        hipLaunchKernelGGL(k_fast_cells2<8>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
-                           cellkey, cellcnt, RP, RH, cell_lo, cell_hi);
+#define ORBX_FAST(MP, RPC)                                                                                        \
+    hipLaunchKernelGGL((k_fast_cells2<MP, RPC>), grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, \
+                       cells, cellkey, cellcnt, RP, RH, cell_lo, cell_hi)
+    if (max_pass <= 8 && RP == 40)
+        ORBX_FAST(8, 40);
+    else if (max_pass <= 8 && RP == 44)
+        ORBX_FAST(8, 44);
+    else if (max_pass <= 8 && RP == 48)
+        ORBX_FAST(8, 48);
+    else if (max_pass <= 8)
+        ORBX_FAST(8, 0);
     else if (max_pass <= 12)
-        hipLaunchKernelGGL(k_fast_cells2<12>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
-                           cellkey, cellcnt, RP, RH, cell_lo, cell_hi);
+        ORBX_FAST(12, 0);
     else
-        hipLaunchKernelGGL(k_fast_cells2<24>, grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, cells,
-                           cellkey, cellcnt, RP, RH, cell_lo, cell_hi);
+        ORBX_FAST(24, 0);
+#undef ORBX_FAST
     return hipGetLastError();
 }
 
