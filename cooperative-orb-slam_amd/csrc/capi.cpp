@@ -1034,11 +1034,13 @@ int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 
 void orbm_epipole(const float R2w[9], const float t2w[3], const float Cw[3], float fx, float fy, float cx, float cy,
                   float* ex, float* ey) {
+    // C2 = R2w*Cw + t2w: OpenCV's 3x3-by-3x1 gemm path (float products and sums, then
+    // (float)(t*alpha + c*beta) in double), as pinned in DESIGN.md
     float C2[3];
     for (int i = 0; i < 3; i++) {
-        double s = 0;
-        for (int k = 0; k < 3; k++) s += (double)R2w[3 * i + k] * (double)Cw[k];
-        C2[i] = (float)(s * 1.0 + (double)t2w[i] * 1.0);  // cv::gemm(R, C, 1, t, 1)
+        const float* a = R2w + 3 * i;
+        const float t0 = a[0] * Cw[0] + a[1] * Cw[1] + a[2] * Cw[2];
+        C2[i] = (float)((double)t0 * 1.0 + (double)t2w[i] * 1.0);
     }
     const float invz = 1.0f / C2[2];
     *ex = fx * C2[0] * invz + cx;

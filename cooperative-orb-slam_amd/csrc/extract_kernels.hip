@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
                                                      ExtractParams ep, const LevelDesc* __restrict__ levels,
                                                      const int* __restrict__ lvcnt) {
     __shared__ __align__(16) uint8_t s_rows[4][7][kBlurSeg];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     int j = blockIdx.x * 4 + wave;
     if (j >= ep.bjob_begin[ep.L]) return;

@@ -183,8 +183,9 @@ int orbm_triangulation_bf_packed_device(orbm_ctx* ctx, const orbx_kp* d_kps1,
                                         int32_t* d_match /* nref x cap1 */, int cap1,
                                         int32_t* d_nmatches /* nref */, void* stream);
 
-/* Epipole helper (ORBmatcher.cc:664-670): C2 = R2w*Cw + t2w with cv::Mat float GEMM
- * semantics (double accumulation, one rounding), ex = fx*C2.x*invz + cx, ey likewise. */
+/* Epipole helper (ORBmatcher.cc:664-670): C2 = R2w*Cw + t2w with OpenCV's small-matrix gemm
+ * semantics (float products/sums, + t in double, one rounding; DESIGN.md "Pinned semantics"),
+ * ex = fx*C2.x*invz + cx, ey likewise. */
 void orbm_epipole(const float R2w[9], const float t2w[3], const float Cw[3], float fx, float fy,
                   float cx, float cy, float* ex, float* ey);
 
