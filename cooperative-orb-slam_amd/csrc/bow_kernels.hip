@@ -1,0 +1,201 @@
+/*
+ * bow_kernels.hip -- gfx950 kernels of the DBoW2 vocabulary transform behind Frame::ComputeBoW
+ * (ORB_SLAM2/src/Frame.cc:400-407, KeyFrame::ComputeBoW): TemplatedVocabulary<FORB>::transform(
+ * features, BowVector&, FeatureVector&, levelsup) of the ORB-SLAM2 DBoW2 fork (not vendored in
+ * the reference; restated from the published algorithm, parity unpinned -- DESIGN.md).
+ *
+ *   k_voc_descend  16 lanes per descriptor: at every level the node's children (file order) are
+ *                  scored with the 256-bit Hamming distance (FORB::distance), the group minimum of
+ *                  (dist, child position) is DBoW2's first strict minimum; the descent stops at a
+ *                  node without children (Node::isLeaf) and records the word id, its weight and
+ *                  the node at level L - levelsup (the FeatureVector key).
+ *   k_voc_bow      one workgroup per frame: stable LDS bitonic sorts of (node, feature) and (word,
+ *                  feature) keys build FeatureVector::addFeature's map (ascending node id, ascending
+ *                  feature per node) and BowVector's map; a word's weights are added in feature
+ *                  order (addWeight) or the first kept (addIfNotExist), the TF division by the word
+ *                  count or BowVector::normalize (L1 / L2) sum in ascending word order -- the same
+ *                  double operations in the same order as the std::map code.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orb_bow.h"
+
+namespace orbamd {
+
+__global__ __launch_bounds__(256) void k_voc_descend(VocDev v, int levelsup, const uint8_t* __restrict__ desc,
+                                                     const int32_t* __restrict__ counts, int stride,
+                                                     int32_t* __restrict__ word, double* __restrict__ weight,
+                                                     uint32_t* __restrict__ nid_out) {
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * 16 + (threadIdx.x >> 4), gl = threadIdx.x & 15;
+    const int n = counts[f];
+    if (blockIdx.x * 16 >= n) return;  // block-uniform
+    const bool in = i < n;
+    const long long fi = (long long)f * stride + (in ? i : 0);
+    const uint4* q = (const uint4*)(desc + fi * 32);
+    const uint4 q0 = q[0], q1 = q[1];
+    const int nid_level = v.L - levelsup;
+    uint32_t nid = 0;  // root (also what a branch shallower than nid_level reports)
+    int final_id = 0, level = 0;
+    for (int step = 0; step < v.n; step++) {  // node ids strictly increase along a path
+        const int c0 = v.child_off[final_id], nc = v.child_off[final_id + 1] - c0;
+        if (nc == 0) break;  // Node::isLeaf
+        ++level;
+        uint32_t best = 0xffffffffu;
+        for (int j = gl; j < nc; j += 16) {
+            const int id = v.child[c0 + j];
+            const uint4* d = (const uint4*)(v.desc + (long long)id * 32);
+            const uint4 d0 = d[0], d1 = d[1];
+            const int dist = __popc(q0.x ^ d0.x) + __popc(q0.y ^ d0.y) + __popc(q0.z ^ d0.z) + __popc(q0.w ^ d0.w) +
+                             __popc(q1.x ^ d1.x) + __popc(q1.y ^ d1.y) + __popc(q1.z ^ d1.z) + __popc(q1.w ^ d1.w);
+            best = min(best, ((uint32_t)dist << 16) | (uint32_t)j);
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o));
+        final_id = v.child[c0 + (int)(best & 0xffff)];
+        if (level == nid_level) nid = (uint32_t)final_id;
+    }
+    if (in && gl == 0) {
+        word[fi] = v.word_id[final_id];
+        weight[fi] = v.weight[final_id];
+        nid_out[fi] = nid;
+    }
+}
+
+/* ascending bitonic sort of n2 (power of two) u64 keys in LDS by 256 threads */
+__device__ void lds_bitonic_u64(unsigned long long* a, int n2) {
+    for (int size = 2; size <= n2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (int t = threadIdx.x; t < n2 / 2; t += 256) {
+                const int lo = 2 * t - (t & (stride - 1));
+                const int hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const unsigned long long x = a[lo], y = a[hi];
+                if ((x > y) == up) {
+                    a[lo] = y;
+                    a[hi] = x;
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+/* segments of equal key-high-words in a sorted array (block scan of the segment heads): returns the
+ * segment count; s_start[s] = first element of segment s */
+__device__ int lds_segments(const unsigned long long* a, int n, int* s_start, int* s_tmp) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int carry = 0;
+    for (int base = 0; base < n; base += 256) {
+        const int i = base + tid;
+        const int head = i < n && (i == 0 || (a[i] >> 32) != (a[i - 1] >> 32));
+        int incl = head;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        if (lane == 63) s_tmp[wv] = incl;
+        __syncthreads();
+        int off = carry;
+        for (int w = 0; w < wv; w++) off += s_tmp[w];
+        const int tot = s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
+        if (i < n && head) s_start[off + incl - 1] = i;
+        carry += tot;
+        __syncthreads();
+    }
+    return carry;
+}
+
+__global__ __launch_bounds__(256) void k_voc_bow(VocDev v, const int32_t* __restrict__ counts, int stride,
+                                                 const int32_t* __restrict__ word, const double* __restrict__ weight,
+                                                 const uint32_t* __restrict__ nid, uint32_t* __restrict__ bow_word,
+                                                 double* __restrict__ bow_value, int32_t* __restrict__ nbow,
+                                                 uint32_t* __restrict__ fv_node, int32_t* __restrict__ fv_off,
+                                                 int32_t* __restrict__ fv_feat, int32_t* __restrict__ nfv) {
+    __shared__ unsigned long long s_key[kVocMaxFeatures];
+    __shared__ int s_start[kVocMaxFeatures + 1];
+    __shared__ int s_tmp[8];
+    __shared__ double s_norm;
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = counts[f];
+    const long long fb = (long long)f * stride;
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    // ---- FeatureVector: stable by (node id, feature index); stopped features (weight <= 0) sort last
+    for (int i = tid; i < n2; i += 256)
+        s_key[i] = i < n && weight[fb + i] > 0 ? ((unsigned long long)nid[fb + i] << 32) | (unsigned)i : ~0ull;
+    lds_bitonic_u64(s_key, n2);
+    int kept = 0;
+    for (int i = tid; i < n; i += 256) kept += s_key[i] != ~0ull;
+    for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
+    if ((tid & 63) == 0) s_tmp[4 + (tid >> 6)] = kept;
+    __syncthreads();
+    const int m = s_tmp[4] + s_tmp[5] + s_tmp[6] + s_tmp[7];
+    __syncthreads();
+    const int nseg = lds_segments(s_key, m, s_start, s_tmp);
+    for (int i = tid; i < m; i += 256) fv_feat[fb + i] = (int32_t)(s_key[i] & 0xffffffffu);
+    for (int s = tid; s < nseg; s += 256) {
+        fv_node[fb + s] = (uint32_t)(s_key[s_start[s]] >> 32);
+        fv_off[(long long)f * (stride + 1) + s] = s_start[s];
+    }
+    if (tid == 0) {
+        fv_off[(long long)f * (stride + 1) + nseg] = m;
+        nfv[f] = nseg;
+    }
+    __syncthreads();
+    // ---- BowVector: stable by (word id, feature index)
+    for (int i = tid; i < n2; i += 256)
+        s_key[i] = i < n && weight[fb + i] > 0 ? ((unsigned long long)(uint32_t)word[fb + i] << 32) | (unsigned)i : ~0ull;
+    lds_bitonic_u64(s_key, n2);
+    const int nw = lds_segments(s_key, m, s_start, s_tmp);
+    if (tid == 0) s_start[nw] = m;
+    __syncthreads();
+    const bool add = v.weighting == 0 || v.weighting == 1;  // TF_IDF / TF: addWeight; IDF / BINARY: addIfNotExist
+    const bool must = v.scoring != 5;                       // every scoring but DOT_PRODUCT normalises
+    for (int s = tid; s < nw; s += 256) {
+        const int b = s_start[s], e = s_start[s + 1];
+        double val = weight[fb + (int)(s_key[b] & 0xffffffffu)];
+        if (add)
+            for (int i = b + 1; i < e; i++) val += weight[fb + (int)(s_key[i] & 0xffffffffu)];
+        if (add && !must) val /= (double)nw;
+        bow_word[fb + s] = (uint32_t)(s_key[b] >> 32);
+        bow_value[fb + s] = val;
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (must) {
+        if (tid == 0) {  // BowVector::normalize: sum in ascending word order, as the map iteration
+            double norm = 0.0;
+            if (v.scoring == 1) {
+                for (int s = 0; s < nw; s++) norm += bow_value[fb + s] * bow_value[fb + s];
+                norm = sqrt(norm);
+            } else {
+                for (int s = 0; s < nw; s++) norm += fabs(bow_value[fb + s]);
+            }
+            s_norm = norm;
+        }
+        __syncthreads();
+        const double norm = s_norm;
+        if (norm > 0.0)
+            for (int s = tid; s < nw; s += 256) bow_value[fb + s] = bow_value[fb + s] / norm;
+    }
+    if (tid == 0) nbow[f] = nw;
+}
+
+hipError_t launch_voc_transform(const VocDev& v, int levelsup, int nframes, const uint8_t* desc, const int32_t* counts,
+                                int stride, int max_n, int32_t* word, double* weight, uint32_t* nid, uint32_t* bow_word,
+                                double* bow_value, int32_t* nbow, uint32_t* fv_node, int32_t* fv_off, int32_t* fv_feat,
+                                int32_t* nfv, hipStream_t st) {
+    if (nframes <= 0) return hipSuccess;
+    if (max_n > 0)
+        hipLaunchKernelGGL(k_voc_descend, dim3((max_n + 15) / 16, nframes), dim3(256), 0, st, v, levelsup, desc, counts,
+                           stride, word, weight, nid);
+    hipLaunchKernelGGL(k_voc_bow, dim3(nframes), dim3(256), 0, st, v, counts, stride, word, weight, nid, bow_word,
+                       bow_value, nbow, fv_node, fv_off, fv_feat, nfv);
+    return hipGetLastError();
+}
+
+}  // namespace orbamd

@@ -1533,3 +1533,196 @@ int orbm_compute_distinctive_descriptors(orbm_ctx* ctx, int npoints, const int32
 }
 
 }  // extern "C"
+
+/* ===================================================================================== */
+/* DBoW2 vocabulary transform (Frame::ComputeBoW, Frame.cc:400-407)                       */
+/* ===================================================================================== */
+#include <fstream>
+#include <sstream>
+#include <string>
+
+#include "orb_bow.h"
+
+struct orbv_handle {
+    int device = 0;
+    int k = 0, L = 0, scoring = 0, weighting = 0, nnodes = 0, nwords = 0;
+    hipStream_t stream = nullptr;
+    DevBuf nodes;    // desc | weight | word_id | child_off | child
+    DevBuf scratch;  // per-call staging
+    VocDev v{};
+};
+
+extern "C" {
+
+int orbv_create(int k, int L, int scoring, int weighting, int nlines, const int32_t* parent, const uint8_t* is_leaf,
+                const uint8_t* desc, const double* weight, int device, orbv_handle** out) {
+    if (!out || k < 0 || k > 20 || L < 1 || L > 10 || scoring < 0 || scoring > 5 || weighting < 0 || weighting > 3 ||
+        nlines < 0 || (nlines && (!parent || !is_leaf || !desc || !weight)))
+        return ORBX_EARG;
+    *out = nullptr;
+    if (device < 0 || device >= orbx_device_count()) return ORBX_EDEVICE;
+    const int n = nlines + 1;
+    std::vector<int32_t> word(n, 0), child_off(n + 1, 0), child(std::max(n, 1), 0), fill(n, 0);
+    std::vector<double> w(n, 0.0);
+    std::vector<uint8_t> d(32 * (size_t)n, 0);
+    int nwords = 0;
+    for (int i = 1; i < n; i++) {  // loadFromTextFile's node loop: ids in file order
+        const int pid = parent[i - 1];
+        if (pid < 0 || pid >= i) return ORBX_EARG;
+        memcpy(&d[32 * (size_t)i], desc + 32 * (size_t)(i - 1), 32);
+        w[i] = weight[i - 1];
+        if (is_leaf[i - 1] > 0) word[i] = nwords++;
+        child_off[pid + 1]++;
+    }
+    for (int i = 0; i < n; i++) child_off[i + 1] += child_off[i];
+    for (int i = 1; i < n; i++) child[child_off[parent[i - 1]] + fill[parent[i - 1]]++] = i;  // push_back order
+    HIPR(hipSetDevice(device));
+    orbv_handle* h = new orbv_handle();
+    h->device = device;
+    h->k = k, h->L = L, h->scoring = scoring, h->weighting = weighting, h->nnodes = n, h->nwords = nwords;
+    Carve cv;
+    const size_t o_d = cv.take(32 * (size_t)n), o_w = cv.take(8 * (size_t)n), o_word = cv.take(4 * (size_t)n),
+                 o_co = cv.take(4 * ((size_t)n + 1)), o_c = cv.take(4 * (size_t)n);
+    if (h->nodes.ensure(cv.off) || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        orbv_destroy(h);
+        return ORBX_EDEVICE;
+    }
+    uint8_t* b = h->nodes.as<uint8_t>();
+    if (hipMemcpy(b + o_d, d.data(), 32 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(b + o_w, w.data(), 8 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(b + o_word, word.data(), 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(b + o_co, child_off.data(), 4 * ((size_t)n + 1), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(b + o_c, child.data(), 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) {
+        orbv_destroy(h);
+        return ORBX_EDEVICE;
+    }
+    h->v.desc = b + o_d;
+    h->v.weight = (const double*)(b + o_w);
+    h->v.word_id = (const int32_t*)(b + o_word);
+    h->v.child_off = (const int32_t*)(b + o_co);
+    h->v.child = (const int32_t*)(b + o_c);
+    h->v.n = n, h->v.L = L, h->v.scoring = scoring, h->v.weighting = weighting;
+    *out = h;
+    return 0;
+}
+
+/* TemplatedVocabulary::loadFromTextFile of the ORB-SLAM2 DBoW2 fork (System.cc:64-65 loads
+ * ORBvoc.txt with it): "k L scoring weighting", then one line per node "parent isLeaf d0 .. d31
+ * weight". Blank lines are skipped (the reference turns a trailing one into a node with an
+ * indeterminate descriptor). */
+int orbv_load_text(const char* path, int device, orbv_handle** out) {
+    if (!path || !out) return ORBX_EARG;
+    std::ifstream f(path);
+    if (!f) return ORBX_EARG;
+    std::string s;
+    if (!std::getline(f, s)) return ORBX_EARG;
+    std::stringstream ss(s);
+    int k = -1, L = -1, n1 = -1, n2 = -1;
+    ss >> k >> L >> n1 >> n2;
+    if (k < 0 || k > 20 || L < 1 || L > 10 || n1 < 0 || n1 > 5 || n2 < 0 || n2 > 3) return ORBX_EARG;
+    std::vector<int32_t> parent;
+    std::vector<uint8_t> leaf, desc;
+    std::vector<double> weight;
+    while (std::getline(f, s)) {
+        if (s.find_first_not_of(" \t\r") == std::string::npos) continue;
+        std::stringstream sn(s);
+        int pid = 0, isleaf = 0;
+        sn >> pid >> isleaf;
+        uint8_t d[32];
+        for (int i = 0; i < 32; i++) {  // FORB::fromString: ints, one per byte
+            int v = 0;
+            sn >> v;
+            d[i] = (uint8_t)v;
+        }
+        double w = 0;
+        sn >> w;
+        if (sn.fail()) return ORBX_EARG;
+        parent.push_back(pid);
+        leaf.push_back((uint8_t)(isleaf > 0));
+        desc.insert(desc.end(), d, d + 32);
+        weight.push_back(w);
+    }
+    return orbv_create(k, L, n1, n2, (int)parent.size(), parent.data(), leaf.data(), desc.data(), weight.data(),
+                       device, out);
+}
+
+void orbv_destroy(orbv_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    h->nodes.release();
+    h->scratch.release();
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int orbv_info(const orbv_handle* h, int* k, int* L, int* nnodes, int* nwords) {
+    if (!h) return ORBX_EARG;
+    if (k) *k = h->k;
+    if (L) *L = h->L;
+    if (nnodes) *nnodes = h->nnodes;
+    if (nwords) *nwords = h->nwords;
+    return 0;
+}
+
+int orbv_transform_batch_device(orbv_handle* h, int nframes, const uint8_t* d_desc, const int32_t* d_counts,
+                                int kp_stride, int levelsup, int32_t* d_word, double* d_weight, uint32_t* d_nid,
+                                uint32_t* d_bow_word, double* d_bow_value, int32_t* d_nbow, uint32_t* d_fv_node,
+                                int32_t* d_fv_off, int32_t* d_fv_feat, int32_t* d_nfv, void* stream) {
+    if (!h || nframes < 0 || kp_stride < 1 || kp_stride > kVocMaxFeatures || !d_desc || !d_counts || !d_word ||
+        !d_weight || !d_nid || !d_bow_word || !d_bow_value || !d_nbow || !d_fv_node || !d_fv_off || !d_fv_feat ||
+        !d_nfv)
+        return ORBX_EARG;
+    if (nframes == 0) return 0;
+    HIPR(hipSetDevice(h->device));
+    HIPR(launch_voc_transform(h->v, levelsup, nframes, d_desc, d_counts, kp_stride, kp_stride, d_word, d_weight, d_nid,
+                              d_bow_word, d_bow_value, d_nbow, d_fv_node, d_fv_off, d_fv_feat, d_nfv,
+                              (hipStream_t)stream));
+    return 0;
+}
+
+int orbv_transform(orbv_handle* h, const uint8_t* desc, int n, int levelsup, uint32_t* bow_word, double* bow_value,
+                   int* nbow, uint32_t* fv_node, int32_t* fv_off, int32_t* fv_feat, int* nfv) {
+    if (!h || n < 0 || n > kVocMaxFeatures || (n && !desc) || !bow_word || !bow_value || !nbow || !fv_node ||
+        !fv_off || !fv_feat || !nfv)
+        return ORBX_EARG;
+    *nbow = 0;
+    *nfv = 0;
+    fv_off[0] = 0;
+    // TemplatedVocabulary::empty(): no nodes under the root
+    if (n == 0 || h->nnodes <= 1) return 0;
+    HIPR(hipSetDevice(h->device));
+    const size_t N = (size_t)n;
+    Carve cv;
+    const size_t o_desc = cv.take(32 * N), o_cnt = cv.take(4), o_word = cv.take(4 * N), o_w = cv.take(8 * N),
+                 o_nid = cv.take(4 * N), o_bw = cv.take(4 * N), o_bv = cv.take(8 * N), o_nb = cv.take(4),
+                 o_fn = cv.take(4 * N), o_fo = cv.take(4 * (N + 1)), o_ff = cv.take(4 * N), o_nf = cv.take(4);
+    if (h->scratch.ensure(cv.off)) return ORBX_EDEVICE;
+    uint8_t* b = h->scratch.as<uint8_t>();
+    hipStream_t st = h->stream;
+    const int32_t cnt = n;
+    HIPR(hipMemcpyAsync(b + o_desc, desc, 32 * N, hipMemcpyHostToDevice, st));
+    HIPR(hipMemcpyAsync(b + o_cnt, &cnt, 4, hipMemcpyHostToDevice, st));
+    HIPR(launch_voc_transform(h->v, levelsup, 1, b + o_desc, (const int32_t*)(b + o_cnt), n, n, (int32_t*)(b + o_word),
+                              (double*)(b + o_w), (uint32_t*)(b + o_nid), (uint32_t*)(b + o_bw), (double*)(b + o_bv),
+                              (int32_t*)(b + o_nb), (uint32_t*)(b + o_fn), (int32_t*)(b + o_fo), (int32_t*)(b + o_ff),
+                              (int32_t*)(b + o_nf), st));
+    int nb = 0, nf = 0;
+    HIPR(hipMemcpyAsync(&nb, b + o_nb, 4, hipMemcpyDeviceToHost, st));
+    HIPR(hipMemcpyAsync(&nf, b + o_nf, 4, hipMemcpyDeviceToHost, st));
+    HIPR(hipStreamSynchronize(st));
+    if (nb) {
+        HIPR(hipMemcpyAsync(bow_word, b + o_bw, 4 * (size_t)nb, hipMemcpyDeviceToHost, st));
+        HIPR(hipMemcpyAsync(bow_value, b + o_bv, 8 * (size_t)nb, hipMemcpyDeviceToHost, st));
+    }
+    HIPR(hipMemcpyAsync(fv_off, b + o_fo, 4 * ((size_t)nf + 1), hipMemcpyDeviceToHost, st));
+    if (nf) HIPR(hipMemcpyAsync(fv_node, b + o_fn, 4 * (size_t)nf, hipMemcpyDeviceToHost, st));
+    HIPR(hipStreamSynchronize(st));
+    const int nfeat = fv_off[nf];
+    if (nfeat) HIPR(hipMemcpy(fv_feat, b + o_ff, 4 * (size_t)nfeat, hipMemcpyDeviceToHost));
+    *nbow = nb;
+    *nfv = nf;
+    return 0;
+}
+
+}  // extern "C"

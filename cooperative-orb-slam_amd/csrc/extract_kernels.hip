@@ -88,9 +88,9 @@ __device__ __forceinline__ int resize_px(const uint8_t* S0, const uint8_t* S1, i
     }
     int v;
     if (x < simd_end)  // SSE2 VResizeLinearVec_32s8u: mulhi_epi16 on (h >> 4)
-        v = ((((h0 >> 4) * b.x) >> 16) + (((h1 >> 4) * b.y) >> 16) + 2) >> 2;
+        v = (((__mul24(h0 >> 4, (int)b.x)) >> 16) + ((__mul24(h1 >> 4, (int)b.y)) >> 16) + 2) >> 2;
     else  // scalar FixedPtCast<int, uchar, 22>
-        v = (h0 * b.x + h1 * b.y + (1 << 21)) >> 22;
+        v = (__mul24(h0, (int)b.x) + __mul24(h1, (int)b.y) + (1 << 21)) >> 22;
     return iclamp(v, 0, 255);
 }
 
@@ -197,9 +197,9 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
         const short2 b = bv[k];
         int v;
         if (c < simd_end)
-            v = ((((h0 >> 4) * b.x) >> 16) + (((h1 >> 4) * b.y) >> 16) + 2) >> 2;
+            v = (((__mul24(h0 >> 4, (int)b.x)) >> 16) + ((__mul24(h1 >> 4, (int)b.y)) >> 16) + 2) >> 2;
         else
-            v = (h0 * b.x + h1 * b.y + (1 << 21)) >> 22;
+            v = (__mul24(h0, (int)b.x) + __mul24(h1, (int)b.y) + (1 << 21)) >> 22;
         D[(long long)y * dst_pitch + c] = (uint8_t)iclamp(v, 0, 255);
     }
 }
@@ -288,8 +288,9 @@ __global__ __launch_bounds__(1024) void k_pyramid_frames(const uint8_t* __restri
                     uint32_t packed = 0;
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
-                        int v = ((((h[0][i] >> 4) * b.x) >> 16) + (((h[1][i] >> 4) * b.y) >> 16) + 2) >> 2;
-                        if (tail && x0 + i >= lv.simd_end) v = (h[0][i] * b.x + h[1][i] * b.y + (1 << 21)) >> 22;
+                        // taps < 2^20, weights <= 2048: 24-bit multiplies (full rate) are exact
+                        int v = ((__mul24(h[0][i] >> 4, (int)b.x) >> 16) + (__mul24(h[1][i] >> 4, (int)b.y) >> 16) + 2) >> 2;
+                        if (tail && x0 + i >= lv.simd_end) v = (__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
                         packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
                     }
                     if (xg < gw) *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
@@ -1207,7 +1208,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     int cl[kMaxLevels];
 #pragma unroll
     for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;
-    s_pat[tid] = my_pat;
+    s_pat[(tid & 15) * 16 + (tid >> 4)] = my_pat;  // pair p at (p % 16) * 16 + p / 16
     s_ic[tid] = my_ic;
     if (blockIdx.x == 0 && tid == 0) {
         int tot = 0;
@@ -1298,19 +1299,17 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     const float a = ca, b = sa;
     wave_sync();  // patch stores of the other lanes of this group
     const uint8_t* pc0 = patch + kDescPatchR * kDescPatchPitch + kDescPatchR + pmis;  // keypoint
-    uint32_t myword = 0;  // descriptor bytes 2ln, 2ln+1 of this lane's keypoint
+    uint32_t myword = 0;  // descriptor bytes 2ln, 2ln+1 of this lane's keypoint = pairs 16ln .. 16ln+15
 #pragma unroll
-    for (int kq = 0; kq < 16; kq++) {
-        const PatPt pp = s_pat[16 * kq + ln];
+    for (int j = 0; j < 16; j++) {
+        const PatPt pp = s_pat[16 * j + ln];  // pair 16ln + j (transposed table: conflict-free reads)
         const int r0 = cv_round(__fadd_rn(__fmul_rn(pp.x0, b), __fmul_rn(pp.y0, a)));
         const int c0 = cv_round(__fsub_rn(__fmul_rn(pp.x0, a), __fmul_rn(pp.y0, b)));
         const int r1 = cv_round(__fadd_rn(__fmul_rn(pp.x1, b), __fmul_rn(pp.y1, a)));
         const int c1 = cv_round(__fsub_rn(__fmul_rn(pp.x1, a), __fmul_rn(pp.y1, b)));
-        const int t0 = pc0[r0 * kDescPatchPitch + c0];
-        const int t1 = pc0[r1 * kDescPatchPitch + c1];
-        const unsigned long long bal = __ballot(t0 < t1);
-        const uint32_t w16 = (uint32_t)(bal >> (16 * sub)) & 0xFFFFu;
-        myword = ln == kq ? w16 : myword;
+        const int t0 = pc0[__mul24(r0, kDescPatchPitch) + c0];  // |r| <= 18: 24-bit multiply
+        const int t1 = pc0[__mul24(r1, kDescPatchPitch) + c1];
+        myword |= (uint32_t)(t0 < t1) << j;
     }
     if (valid) {
         const long long o = (long long)f * kp_stride + outidx;

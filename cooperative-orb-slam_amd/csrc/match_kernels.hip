@@ -327,6 +327,10 @@ __global__ __launch_bounds__(256) void k_tri_bf(const int32_t* __restrict__ q1, 
 }
 
 /* cross-agent: the query frame against nref packed slots (orbx_pack_keyframe_device) */
+/* one query frame against a few slots is a small problem: 16 candidate slices per query (16 queries
+ * per workgroup) so ~1000 queries spread over ~64 workgroups instead of 16 */
+constexpr int kPackedSplit = 16;
+
 __global__ __launch_bounds__(256) void k_tri_bf_packed(const orbx_kp* __restrict__ kps1, const uint8_t* __restrict__ desc1,
                                                        const int32_t* __restrict__ count1, const uint8_t* __restrict__ slots,
                                                        long long slot_bytes, int slot_cap, MatchGeom g,
@@ -340,7 +344,7 @@ __global__ __launch_bounds__(256) void k_tri_bf_packed(const orbx_kp* __restrict
     (void)slot_cap;
     s.kps2 = (const orbx_kp*)(slot + 64);
     s.desc2 = slot + 64 + (long long)cap2 * sizeof(orbx_kp);
-    tri_bf_body<4>(s, g, match + (long long)r * cap1, nmatches + r);
+    tri_bf_body<kPackedSplit>(s, g, match + (long long)r * cap1, nmatches + r);
 }
 
 /* pack one frame's (n, kps, desc) into an exchange slot */
@@ -605,7 +609,7 @@ hipError_t launch_rot_filter_pairs(int npairs, const int32_t* q1, const int32_t*
 hipError_t launch_tri_bf_packed(const orbx_kp* kps1, const uint8_t* desc1, const int32_t* count1, int nref,
                                 const uint8_t* slots, long long slot_bytes, int slot_cap, const MatchGeom& g,
                                 int32_t* match, int cap1, int32_t* nmatches, hipStream_t st) {
-    dim3 grid((cap1 + 63) / 64, nref);
+    dim3 grid((cap1 + 256 / kPackedSplit - 1) / (256 / kPackedSplit), nref);
     hipLaunchKernelGGL(k_tri_bf_packed, grid, dim3(256), 0, st, kps1, desc1, count1, slots, slot_bytes, slot_cap, g,
                        match, cap1, nmatches);
     return hipGetLastError();

@@ -14,4 +14,5 @@ from .extractor import ORBextractor, synth_frames, kp_dtype  # noqa: F401
 from .matcher import ORBmatcher, KeyFrameView, epipole, compute_f12  # noqa: F401
 from . import device, frame, projection  # noqa: F401
 from .projection import FrameView, MapPoints  # noqa: F401
+from .vocabulary import ORBVocabulary  # noqa: F401
 from .frame import compute_stereo_matches  # noqa: F401

@@ -80,6 +80,12 @@ SIGNATURES = {
     "orbm_search_by_projection_keyframe": (_I, [_P, _P, _P, _P, _F, _I, _I, _P, C.POINTER(_I)]),
     "orbm_search_by_projection_sim3": (_I, [_P, _P, _P, _P, _I, _P, C.POINTER(_I)]),
     "orbm_compute_distinctive_descriptors": (_I, [_P, _I, _P, _P, _P, _P]),
+    "orbv_load_text": (_I, [C.c_char_p, _I, C.POINTER(_P)]),
+    "orbv_create": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _I, C.POINTER(_P)]),
+    "orbv_destroy": (None, [_P]),
+    "orbv_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
+    "orbv_transform": (_I, [_P, _P, _I, _I, _P, _P, C.POINTER(_I), _P, _P, _P, C.POINTER(_I)]),
+    "orbv_transform_batch_device": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "orbm_compute_distinctive_descriptors_device": (_I, [_P, _I, _P, _P, _P, _P, _P]),
     "orbx_selftest_sincosf": (_I, [_P, _P, _P, _I, _P]),
     "orbx_profile_enable": (_I, [_P, _I]),

@@ -292,6 +292,42 @@ int orbm_compute_distinctive_descriptors_device(orbm_ctx* ctx, int npoints, cons
                                                 uint8_t* d_out_desc, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * DBoW2 vocabulary transform -- replaces ORBVocabulary::transform(features, BowVector&,
+ * FeatureVector&, levelsup) as called by Frame::ComputeBoW (Frame.cc:400-407) and
+ * KeyFrame::ComputeBoW (levelsup 4), with the vocabulary loaded by loadFromTextFile
+ * (System.cc:64-65). DBoW2 is not vendored in the reference: the ORB-SLAM2 fork's published
+ * algorithm is restated (parity unpinned).
+ * ---------------------------------------------------------------------------------- */
+typedef struct orbv_handle orbv_handle;
+
+/* ORBvoc.txt text format: "k L scoring weighting", then "parent isLeaf d0..d31 weight" per node
+ * (node ids = line order, root = 0). */
+int orbv_load_text(const char* path, int device, orbv_handle** out);
+/* the same from arrays of the node lines (nlines nodes after the root, in file order) */
+int orbv_create(int k, int L, int scoring, int weighting, int nlines, const int32_t* parent,
+                const uint8_t* is_leaf, const uint8_t* desc, const double* weight, int device,
+                orbv_handle** out);
+void orbv_destroy(orbv_handle* h);
+int orbv_info(const orbv_handle* h, int* k, int* L, int* nnodes, int* nwords);
+
+/* n descriptors (32 B rows, n <= 4096) -> BowVector (bow_word ascending, bow_value; *nbow
+ * entries) and FeatureVector as CSR (fv_node ascending, fv_off[*nfv+1], fv_feat ascending within
+ * a node). Capacities: n entries each, fv_off n+1. */
+int orbv_transform(orbv_handle* h, const uint8_t* desc, int n, int levelsup, uint32_t* bow_word,
+                   double* bow_value, int* nbow, uint32_t* fv_node, int32_t* fv_off,
+                   int32_t* fv_feat, int* nfv);
+/* device batch over the frames of an orbx_extract_batch_device output (descriptors at f*kp_stride,
+ * d_counts[f]; kp_stride <= 4096): per-feature word id / weight / node id at L-levelsup and per
+ * frame the BowVector / FeatureVector (frame f's arrays at f*kp_stride, fv_off at
+ * f*(kp_stride+1), counts d_nbow[f], d_nfv[f]). */
+int orbv_transform_batch_device(orbv_handle* h, int nframes, const uint8_t* d_desc,
+                                const int32_t* d_counts, int kp_stride, int levelsup,
+                                int32_t* d_word, double* d_weight, uint32_t* d_nid,
+                                uint32_t* d_bow_word, double* d_bow_value, int32_t* d_nbow,
+                                uint32_t* d_fv_node, int32_t* d_fv_off, int32_t* d_fv_feat,
+                                int32_t* d_nfv, void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Cross-agent exchange slot (replaces the LCM KeyFrameexample message,
  * ORB_SLAM2.1/Examples/ROS/ORB_SLAM2/src/ros_mono.cc:1907-2410).
  * slot = [u32 n | u32 pad[15] | n x orbx_kp (24 B) | n x 32 B descriptors], fixed size

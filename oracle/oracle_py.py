@@ -57,6 +57,10 @@ _SIG = {
     "oc_search_by_projection_keyframe": (_I, [_P, _P, _P, _F, _I, _I, _P]),
     "oc_search_by_projection_sim3": (_I, [_P, _P, _P, _I, _P]),
     "oc_compute_distinctive_descriptors": (None, [_I, _P, _P, _P]),
+    "oc_vocab_create": (_P, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "oc_vocab_destroy": (None, [_P]),
+    "oc_vocab_transform": (_I, [_P, _P, _I, _I, _P, _P, C.POINTER(_I), _P, _P, _P, C.POINTER(_I)]),
+    "oc_vocab_descend": (None, [_P, _P, _I, _I, _P, _P, _P]),
 }
 
 _lib = None
@@ -291,3 +295,47 @@ def compute_distinctive_descriptors(offsets, desc):
     out = np.empty(max(len(off) - 1, 1), np.int32)
     load().oc_compute_distinctive_descriptors(len(off) - 1, off.ctypes.data, d.ctypes.data, out.ctypes.data)
     return out[:len(off) - 1]
+
+
+class OracleVocabulary:
+    """DBoW2 TemplatedVocabulary<FORB> restated in C (orb_oracle_voc.c; parity unpinned)."""
+
+    def __init__(self, k, L, scoring, weighting, parent, is_leaf, desc, weight):
+        self.lib = load()
+        self._keep = [np.ascontiguousarray(parent, np.int32), np.ascontiguousarray(is_leaf, np.uint8),
+                      np.ascontiguousarray(desc, np.uint8), np.ascontiguousarray(weight, np.float64)]
+        p, lf, d, w = self._keep
+        self.h = self.lib.oc_vocab_create(k, L, scoring, weighting, len(p), p.ctypes.data, lf.ctypes.data,
+                                          d.ctypes.data, w.ctypes.data)
+        if not self.h:
+            raise ValueError("bad vocabulary")
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.oc_vocab_destroy(self.h)
+        except Exception:
+            pass
+
+    def transform(self, descriptors, levelsup=4):
+        d = np.ascontiguousarray(descriptors, np.uint8)
+        n = len(d)
+        bw = np.empty(max(n, 1), np.uint32)
+        bv = np.empty(max(n, 1), np.float64)
+        fn = np.empty(max(n, 1), np.uint32)
+        fo = np.empty(n + 1, np.int32)
+        ff = np.empty(max(n, 1), np.int32)
+        nb, nf = C.c_int(), C.c_int()
+        self.lib.oc_vocab_transform(self.h, d.ctypes.data, n, levelsup, bw.ctypes.data, bv.ctypes.data, C.byref(nb),
+                                    fn.ctypes.data, fo.ctypes.data, ff.ctypes.data, C.byref(nf))
+        fv = {int(fn[i]): ff[fo[i]:fo[i + 1]].tolist() for i in range(nf.value)}
+        return (bw[:nb.value].copy(), bv[:nb.value].copy()), fv
+
+    def descend(self, descriptors, levelsup=4):
+        d = np.ascontiguousarray(descriptors, np.uint8)
+        n = len(d)
+        w = np.empty(max(n, 1), np.int32)
+        wt = np.empty(max(n, 1), np.float64)
+        nid = np.empty(max(n, 1), np.int32)
+        self.lib.oc_vocab_descend(self.h, d.ctypes.data, n, levelsup, w.ctypes.data, wt.ctypes.data, nid.ctypes.data)
+        return w[:n], wt[:n], nid[:n]

@@ -83,6 +83,16 @@ void oc_compute_distinctive_descriptors(int npoints, const int32_t* offsets, con
 int oc_search_by_projection_sim3(const orbm_frame_view* KF, const float* Scw, const orbm_mappoints* mp, int th,
                                  int32_t* match);
 
+/* DBoW2 vocabulary transform (orb_oracle_voc.c; parity unpinned: DBoW2 is not vendored) */
+typedef struct oc_vocab oc_vocab;
+oc_vocab* oc_vocab_create(int k, int L, int scoring, int weighting, int nlines, const int32_t* parent,
+                          const uint8_t* is_leaf, const uint8_t* desc, const double* weight);
+void oc_vocab_destroy(oc_vocab* v);
+int oc_vocab_transform(const oc_vocab* v, const uint8_t* desc, int n, int levelsup, uint32_t* bow_word,
+                       double* bow_value, int* nbow, uint32_t* fv_node, int32_t* fv_off, int32_t* fv_feat, int* nfv);
+void oc_vocab_descend(const oc_vocab* v, const uint8_t* desc, int n, int levelsup, int32_t* word, double* weight,
+                      int32_t* nid);
+
 #ifdef __cplusplus
 }
 #endif
