@@ -109,6 +109,35 @@ def synth_vocabulary(k=10, L=4, seed=0, flip_bits=40, zero_weight_frac=0.02, rag
         np.array(weight, np.float64)
 
 
+def synth_vocabulary_full(k=10, L=6, seed=0):
+    """A full k-ary synthetic vocabulary of depth L (ORBvoc.txt's shape is k=10, L=6: 1,111,110 nodes),
+    vectorised: children = parent descriptor XOR (r1 & r2 & r3) (about 32 flipped bits), breadth-first
+    node order, idf-like weights on every node. For benchmarks; same return layout as synth_vocabulary."""
+    rng = np.random.default_rng(seed)
+    parents, leaves, descs, weights = [], [], [], []
+    level_desc = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+    level_ids = np.arange(1, k + 1)
+    parents.append(np.zeros(k, np.int32))
+    next_id = k + 1
+    for depth in range(1, L + 1):
+        n = len(level_ids)
+        leaves.append(np.full(n, 1 if depth == L else 0, np.uint8))
+        descs.append(level_desc)
+        weights.append(rng.uniform(0.1, 8.0, n))
+        if depth == L:
+            break
+        child_desc = np.repeat(level_desc, k, axis=0)
+        m = rng.integers(0, 256, child_desc.shape, dtype=np.uint8)
+        m &= rng.integers(0, 256, child_desc.shape, dtype=np.uint8)
+        m &= rng.integers(0, 256, child_desc.shape, dtype=np.uint8)
+        child_desc ^= m
+        child_ids = np.arange(next_id, next_id + n * k)
+        parents.append(np.repeat(level_ids, k).astype(np.int32))
+        next_id += n * k
+        level_desc, level_ids = child_desc, child_ids
+    return k, L, np.concatenate(parents), np.concatenate(leaves), np.concatenate(descs), np.concatenate(weights)
+
+
 def to_text(path, k, L, parent, is_leaf, desc, weight, scoring=L1_NORM, weighting=TF_IDF):
     """Writes the ORBvoc.txt text format (saveToTextFile of the ORB-SLAM2 DBoW2 fork)."""
     with open(path, "w") as f:

@@ -9,6 +9,8 @@
                + D2H) per call on a 640x480 frame with ~900 candidate MapPoints vs the CPU oracle.
   distinctive  MapPoint::ComputeDistinctiveDescriptors for 20k MapPoints x ~25 observations (device
                batch) vs the CPU oracle.
+  bow          Frame::ComputeBoW (DBoW2 transform, levelsup 4) of 256 extracted 640x480 frames with a synthetic
+               vocabulary of ORBvoc.txt's shape (k=10, L=6, 1.1M nodes) resident in HBM, vs the CPU oracle.
 The CPU figures are the oracle (a plain-C restatement, 1 thread), not the reference build.
 """
 import json
@@ -140,10 +142,56 @@ def bench_distinctive(torch, reps):
             "gpu_ms_per_batch": round(g, 4), "cpu_oracle_ms_per_batch": round(c * 1e3, 2), "cpu_threads": 1}
 
 
+def bench_bow(torch, reps):
+    import orbamd
+    import oracle_py
+    from orbamd.vocabulary import synth_vocabulary_full, L1_NORM, TF_IDF
+    k, L, parent, leaf, desc, weight = synth_vocabulary_full(10, 6, 7)
+    gv = orbamd.ORBVocabulary.from_arrays(k, L, L1_NORM, TF_IDF, parent, leaf, desc, weight)
+    B = 256
+    pipe = orbamd.device.BatchPipeline(torch, 640, 480, B)
+    dev = torch.device("cuda", 0)
+    frames = torch.from_numpy(orbamd.synth_frames(0, 0, B, 640, 480)).to(dev)
+    pipe.extract(frames)
+    S = pipe.stride
+    z = lambda *s, dt=torch.int32: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
+    word, wt, nid = z(B, S), z(B, S, dt=torch.float64), z(B, S)
+    bw, bv, nb = z(B, S), z(B, S, dt=torch.float64), z(B)
+    fn, fo, ff, nf = z(B, S), z(B, S + 1), z(B, S), z(B)
+    lib = orbamd.load()
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    def run():
+        lib.orbv_transform_batch_device(gv._h, B, pipe.desc.data_ptr(), pipe.counts.data_ptr(), S, 4, word.data_ptr(),
+                                        wt.data_ptr(), nid.data_ptr(), bw.data_ptr(), bv.data_ptr(), nb.data_ptr(),
+                                        fn.data_ptr(), fo.data_ptr(), ff.data_ptr(), nf.data_ptr(), st)
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    g = e0.elapsed_time(e1) / reps
+    ov = oracle_py.OracleVocabulary(k, L, L1_NORM, TF_IDF, parent, leaf, desc, weight)
+    k0, d0, _m = pipe.host_results(0)
+    t = time.perf_counter()
+    (ow, oval), ofv = ov.transform(d0, 4)
+    c = time.perf_counter() - t
+    assert int(nb[0]) == len(ow) and np.array_equal(bw[0, :len(ow)].cpu().numpy().astype(np.uint32), ow)
+    mean_n = float(pipe.counts.float().mean().item())
+    return {"row": "dbow2_transform", "workload": "256 frames x %.0f descriptors, vocabulary k=10 L=6 (%d nodes)" % (
+            mean_n, len(parent) + 1),
+            "gpu_ms_per_256_frames": round(g, 4), "gpu_us_per_frame": round(g * 1e3 / B, 3),
+            "cpu_oracle_ms_per_frame": round(c * 1e3, 3), "cpu_threads": 1}
+    # (pipe's buffers are torch tensors; its handles close with the process)
+
+
 def main():
     import torch
     steps = int(os.environ.get("BENCH_ROWS_STEPS", "10"))
-    for r in (bench_stereo(torch, steps), bench_projection(50), bench_distinctive(torch, 10)):
+    for r in (bench_stereo(torch, steps), bench_projection(50), bench_distinctive(torch, 10), bench_bow(torch, 10)):
         print(json.dumps(r), flush=True)
 
 
