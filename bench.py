@@ -9,8 +9,9 @@ latest keyframe (keypoints + descriptors) and RCCL-all-gathers it, then matches 
 every agent's slot. One process per GPU = one agent; frames are
 agent-private, so per-GPU work is fixed as N grows ("weak" scaling). The B frames of a step are
 split over P concurrent extraction+match graphs (own handle and HIP stream each; frame b of a
-graph is matched against frame b-1 of the same graph), so one graph's latency-bound tail
-(octree, describe, match) overlaps another graph's FAST.
+graph is matched against frame b-1 of the same graph), staggered so that one graph's FAST
+overlaps another graph's latency-bound tail (octree, describe, match) -- default 1024 frames as
+4 graphs of 256.
 
 Launch (N>1): python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
               --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
@@ -101,10 +102,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512, help="frames per step per GPU")
-    ap.add_argument("--pipes", type=int, default=2,
+    ap.add_argument("--batch", type=int, default=1024, help="frames per step per GPU")
+    ap.add_argument("--pipes", type=int, default=4,
                     help="concurrent extraction+match graphs per GPU (each over batch/pipes frames, own handle "
-                         "and HIP stream), so one graph's latency-bound tail overlaps the other's FAST")
+                         "and HIP stream), staggered: graph p starts a step when graph p-1 finished extracting it")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -151,10 +152,17 @@ def main():
                 all_slots.copy_(my_slot)
             pipe.match_packed(0, all_slots, world, xmatch, xn, streams[0].cuda_stream)
 
+    done = [torch.cuda.Event() for _ in range(P)]
+
     def step(ev=None):
         for p in range(P):
             st = streams[p].cuda_stream
+            if p > 0:
+                # staggered graphs: graph p's extraction (FAST-heavy) overlaps graph p-1's matcher and the
+                # latency-bound tail stages instead of running in lockstep with them
+                streams[p].wait_event(done[p - 1])
             pipes[p].extract(frames[p], st)
+            done[p].record(streams[p])
             if ev is not None:
                 ev[p][0].record(streams[p])
             pipes[p].match_pairs(st)

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cooperative-orb-slam_amd"))
 
 
-def run(torch, orbamd, frames_np, P, steps=20, warm=3):
+def run(torch, orbamd, frames_np, P, steps=20, warm=3, offset=False):
     B = frames_np.shape[0]
     dev = torch.device("cuda", 0)
     sub = B // P
@@ -19,9 +19,17 @@ def run(torch, orbamd, frames_np, P, steps=20, warm=3):
     fr = [torch.from_numpy(frames_np[p * sub:(p + 1) * sub]).to(dev) for p in range(P)]
     torch.cuda.synchronize()
 
+    evs = [torch.cuda.Event() for _ in range(P)]
+
     def step():
         for p in range(P):
-            pipes[p].step(fr[p], streams[p].cuda_stream)
+            if offset and p > 0:
+                # graph p starts its step once graph p-1's extraction of this step is done: its FAST then
+                # overlaps graph p-1's matcher / next pyramid instead of running in lockstep with it
+                streams[p].wait_event(evs[p - 1])
+            pipes[p].extract(fr[p], streams[p].cuda_stream)
+            evs[p].record(streams[p])
+            pipes[p].match_pairs(streams[p].cuda_stream)
 
     for _ in range(warm):
         step()
@@ -39,10 +47,14 @@ def run(torch, orbamd, frames_np, P, steps=20, warm=3):
 def main():
     import torch
     import orbamd
-    for B in (256, 512):
+    for B in (512, 1024):
         frames = orbamd.synth_frames(0, 0, B, 640, 480)
         for P in (1, 2, 4):
-            print("B=%d P=%d frames/s=%.0f" % (B, P, run(torch, orbamd, frames, P)), flush=True)
+            for off in (False, True):
+                if P == 1 and off:
+                    continue
+                print("B=%d P=%d offset=%d frames/s=%.0f" % (B, P, off, run(torch, orbamd, frames, P, offset=off)),
+                      flush=True)
 
 
 if __name__ == "__main__":
