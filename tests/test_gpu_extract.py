@@ -117,3 +117,26 @@ def test_large_batch_whole_frame_pyramid(W, H, nf):
             np.testing.assert_array_equal(pipe.ext.pyramid_level(l, frame=b), orc.pyramid(l),
                                           err_msg="frame %d pyramid level %d" % (b, l))
     pipe.close()
+
+
+PARAMS = [
+    # (W, H, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST): other my.yaml settings / odd sizes
+    (641, 479, 1000, 1.2, 8, 20, 7),
+    (320, 240, 500, 1.2, 5, 20, 7),
+    (800, 600, 1500, 1.3, 6, 12, 5),
+    (512, 384, 800, 1.15, 10, 25, 9),
+    (1024, 768, 3000, 1.2, 8, 20, 7),
+]
+
+
+@pytest.mark.parametrize("W,H,nf,sf,nl,ini,mini", PARAMS)
+def test_extract_other_parameters(W, H, nf, sf, nl, ini, mini):
+    """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) beyond the default config:
+    odd frame sizes, other scale factors / level counts / thresholds (ORBextractor.cc:410-470)."""
+    frames = orbamd.synth_frames(1, 2, 2, W, H)
+    ext = orbamd.ORBextractor(nf, sf, nl, ini, mini, max_width=W, max_height=H)
+    orc = oracle_py.OracleExtractor(nf, sf, nl, ini, mini)
+    for f in range(frames.shape[0]):
+        kg, dg = ext(frames[f])
+        ko, do = orc(frames[f])
+        _compare(kg, dg, ko, do)
