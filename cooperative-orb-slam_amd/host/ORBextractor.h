@@ -44,6 +44,10 @@ public:
 
     std::vector<cv::Mat> mvImagePyramid;
 
+    // the device handle holding this extractor's last pyramid (used by the drop-in
+    // Frame::ComputeStereoMatches, host/Frame_stereo_amd.cc); addition to the reference surface
+    orbx_handle* DeviceHandle() const { return mpHandle; }
+
 protected:
     void ensureHandle(int width, int height);
 

@@ -1,0 +1,259 @@
+/*
+ * ORBmatcher_projection_amd.cc -- MI355X definitions of the four ORBmatcher::SearchByProjection
+ * overloads (replace the same definitions in ORB_SLAM2/src/ORBmatcher.cc):
+ *   SearchByProjection(Frame&, const vector<MapPoint*>&, th)                 ORBmatcher.cc:45-129
+ *   SearchByProjection(Frame&, const Frame&, th, bMono)                      ORBmatcher.cc:1328-1470
+ *   SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist) ORBmatcher.cc:1472-1599
+ *   SearchByProjection(KeyFrame*, cv::Mat Scw, vpPoints, vpMatched, th)      ORBmatcher.cc:290-403
+ * Each call gathers what the reference reads (keypoints, descriptors, mvuRight, grid bounds, the
+ * MapPoint state through the same accessors), runs orbm_search_by_projection_* (geometry prologue
+ * on the host with the reference's float semantics; grid, windowed Hamming search, in-order claims
+ * and the rotation histogram on the device) and writes the assignments back. MapPoint's private
+ * mfMinDistance / mfMaxDistance are read through GetMinDistance() / GetMaxDistance(), two getters
+ * the maintainer adds to MapPoint.h. Device failures throw std::runtime_error.
+ */
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ORBmatcher.h"
+#include "orbslam_amd.h"
+
+namespace ORB_SLAM2 {
+
+namespace {
+
+void proj_ok(int rc, const char* what) {
+    if (rc != ORBX_OK) throw std::runtime_error(std::string("orbslam_amd: ") + what + " failed rc=" + std::to_string(rc));
+}
+
+orbm_ctx* proj_ctx() {
+    struct Holder {
+        orbm_ctx* c = nullptr;
+        ~Holder() { if (c) orbm_destroy(c); }
+    };
+    static thread_local Holder h;
+    if (!h.c) {
+        const char* dev = getenv("ORBAMD_DEVICE");
+        proj_ok(orbm_create(dev ? atoi(dev) : 0, &h.c), "orbm_create");
+    }
+    return h.c;
+}
+
+/* the Frame / KeyFrame side of a call */
+struct FrameSide {
+    std::vector<float> x, y, angle;
+    std::vector<int32_t> octave;
+    std::vector<uint8_t> occ;
+    cv::Mat desc;
+    orbm_frame_view v;
+    template <class FK>
+    void gather(FK& F, const std::vector<float>* uright, float bf, float b) {
+        const size_t n = F.mvKeysUn.size();
+        x.resize(n); y.resize(n); angle.resize(n); octave.resize(n);
+        for (size_t i = 0; i < n; i++) {
+            x[i] = F.mvKeysUn[i].pt.x;
+            y[i] = F.mvKeysUn[i].pt.y;
+            angle[i] = F.mvKeysUn[i].angle;
+            octave[i] = F.mvKeysUn[i].octave;
+        }
+        desc = F.mDescriptors.isContinuous() ? F.mDescriptors : F.mDescriptors.clone();
+        memset(&v, 0, sizeof(v));
+        v.n = (int32_t)n;
+        v.desc = n ? desc.data : nullptr;
+        v.x = x.data(); v.y = y.data(); v.octave = octave.data(); v.angle = angle.data();
+        v.uright = uright && !uright->empty() ? uright->data() : nullptr;
+        v.min_x = F.mnMinX; v.min_y = F.mnMinY; v.max_x = F.mnMaxX; v.max_y = F.mnMaxY;
+        v.grid_w_inv = F.mfGridElementWidthInv; v.grid_h_inv = F.mfGridElementHeightInv;
+        v.fx = F.fx; v.fy = F.fy; v.cx = F.cx; v.cy = F.cy;
+        v.bf = bf; v.b = b;
+        v.nlevels = (int32_t)F.mvScaleFactors.size();
+        v.scale_factors = F.mvScaleFactors.data();
+        v.log_scale_factor = F.mfLogScaleFactor;
+    }
+    void occupied(const std::vector<uint8_t>& o) {
+        occ = o;
+        v.occupied = occ.data();
+    }
+};
+
+/* the MapPoint side */
+struct PointSide {
+    std::vector<uint8_t> desc, bad, has_obs, skip, in_view;
+    std::vector<float> pos, normal, mind, maxd, angle, px, py, pxr, vcos;
+    std::vector<int32_t> octave, level;
+    orbm_mappoints m;
+    void reserve(size_t n) {
+        desc.assign(32 * n, 0); bad.assign(n, 0); has_obs.assign(n, 0); skip.assign(n, 0);
+        pos.assign(3 * n, 0.f); normal.assign(3 * n, 0.f); mind.assign(n, 0.f); maxd.assign(n, 0.f);
+        angle.assign(n, 0.f); octave.assign(n, 0);
+    }
+    void point(size_t i, MapPoint* p, bool geometry) {
+        bad[i] = p->isBad();
+        has_obs[i] = p->Observations() > 0;
+        cv::Mat d = p->GetDescriptor();
+        memcpy(&desc[32 * i], d.ptr<unsigned char>(), 32);
+        if (geometry) {
+            cv::Mat w = p->GetWorldPos();
+            for (int k = 0; k < 3; k++) pos[3 * i + k] = w.at<float>(k, 0);
+            mind[i] = p->GetMinDistance();
+            maxd[i] = p->GetMaxDistance();
+        }
+    }
+    void finish(size_t n) {
+        memset(&m, 0, sizeof(m));
+        m.n = (int32_t)n;
+        m.desc = desc.data(); m.pos = pos.data(); m.normal = normal.data(); m.min_dist = mind.data();
+        m.max_dist = maxd.data(); m.bad = bad.data(); m.has_obs = has_obs.data(); m.skip = skip.data();
+        m.octave = octave.data(); m.angle = angle.data();
+        if (!in_view.empty()) {
+            m.track_in_view = in_view.data(); m.track_proj_x = px.data(); m.track_proj_y = py.data();
+            m.track_proj_xr = pxr.data(); m.track_level = level.data(); m.track_view_cos = vcos.data();
+        }
+    }
+};
+
+std::vector<uint8_t> occupied_obs(const std::vector<MapPoint*>& mps) {
+    std::vector<uint8_t> o(mps.size());
+    for (size_t i = 0; i < mps.size(); i++) o[i] = mps[i] && mps[i]->Observations() > 0;
+    return o;
+}
+
+std::vector<uint8_t> occupied_any(const std::vector<MapPoint*>& mps) {
+    std::vector<uint8_t> o(mps.size());
+    for (size_t i = 0; i < mps.size(); i++) o[i] = mps[i] != NULL;
+    return o;
+}
+
+const float* mat44(const cv::Mat& T, cv::Mat& keep) {
+    keep = T.isContinuous() ? T : T.clone();
+    return keep.ptr<float>();
+}
+
+/* match[i] >= 0: assign src[match[i]]; -2: the rotation filter reset it to NULL */
+void apply(std::vector<MapPoint*>& dst, const std::vector<int32_t>& m, const std::vector<MapPoint*>& src) {
+    for (size_t i = 0; i < dst.size(); i++) {
+        if (m[i] >= 0) dst[i] = src[m[i]];
+        else if (m[i] == -2) dst[i] = static_cast<MapPoint*>(NULL);
+    }
+}
+
+}  // namespace
+
+// ORBmatcher.cc:45-129
+int ORBmatcher::SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th) {
+    FrameSide fs;
+    fs.gather(F, &F.mvuRight, F.mbf, F.mb);
+    fs.occupied(occupied_obs(F.mvpMapPoints));
+    const size_t n = vpMapPoints.size();
+    PointSide ps;
+    ps.reserve(n);
+    ps.in_view.assign(n, 0); ps.px.assign(n, 0.f); ps.py.assign(n, 0.f); ps.pxr.assign(n, 0.f);
+    ps.level.assign(n, 0); ps.vcos.assign(n, 0.f);
+    for (size_t i = 0; i < n; i++) {
+        MapPoint* p = vpMapPoints[i];
+        ps.in_view[i] = p->mbTrackInView;
+        if (!p->mbTrackInView) continue;
+        ps.point(i, p, false);
+        ps.px[i] = p->mTrackProjX; ps.py[i] = p->mTrackProjY; ps.pxr[i] = p->mTrackProjXR;
+        ps.level[i] = p->mnTrackScaleLevel; ps.vcos[i] = p->mTrackViewCos;
+    }
+    ps.finish(n);
+    std::vector<int32_t> m((size_t)std::max(F.N, 1));
+    int nm = 0;
+    proj_ok(orbm_search_by_projection_local(proj_ctx(), &fs.v, &ps.m, th, mfNNratio, m.data(), &nm),
+            "orbm_search_by_projection_local");
+    apply(F.mvpMapPoints, m, vpMapPoints);
+    return nm;
+}
+
+// ORBmatcher.cc:1328-1470
+int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono) {
+    FrameSide fs;
+    fs.gather(CurrentFrame, &CurrentFrame.mvuRight, CurrentFrame.mbf, CurrentFrame.mb);
+    fs.occupied(occupied_obs(CurrentFrame.mvpMapPoints));
+    const size_t n = (size_t)LastFrame.N;
+    PointSide ps;
+    ps.reserve(n);
+    for (size_t i = 0; i < n; i++) {
+        MapPoint* p = LastFrame.mvpMapPoints[i];
+        ps.skip[i] = !p || LastFrame.mvbOutlier[i];
+        if (ps.skip[i]) continue;
+        ps.point(i, p, true);
+        ps.octave[i] = LastFrame.mvKeys[i].octave;
+        ps.angle[i] = LastFrame.mvKeysUn[i].angle;
+    }
+    ps.finish(n);
+    cv::Mat kc, kl;
+    std::vector<int32_t> m((size_t)std::max(CurrentFrame.N, 1));
+    int nm = 0;
+    proj_ok(orbm_search_by_projection_last_frame(proj_ctx(), &fs.v, mat44(CurrentFrame.mTcw, kc), &ps.m,
+                                                 mat44(LastFrame.mTcw, kl), th, bMono ? 1 : 0,
+                                                 mbCheckOrientation ? 1 : 0, m.data(), &nm),
+            "orbm_search_by_projection_last_frame");
+    apply(CurrentFrame.mvpMapPoints, m, LastFrame.mvpMapPoints);
+    return nm;
+}
+
+// ORBmatcher.cc:1472-1599
+int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
+                                   const float th, const int ORBdist) {
+    FrameSide fs;
+    fs.gather(CurrentFrame, &CurrentFrame.mvuRight, CurrentFrame.mbf, CurrentFrame.mb);
+    fs.occupied(occupied_any(CurrentFrame.mvpMapPoints));
+    const std::vector<MapPoint*> vpMPs = pKF->GetMapPointMatches();
+    const size_t n = vpMPs.size();
+    PointSide ps;
+    ps.reserve(n);
+    for (size_t i = 0; i < n; i++) {
+        MapPoint* p = vpMPs[i];
+        ps.skip[i] = !p || sAlreadyFound.count(p);
+        if (ps.skip[i]) continue;
+        ps.point(i, p, true);
+        ps.angle[i] = pKF->mvKeysUn[i].angle;
+    }
+    ps.finish(n);
+    cv::Mat kc;
+    std::vector<int32_t> m((size_t)std::max(CurrentFrame.N, 1));
+    int nm = 0;
+    proj_ok(orbm_search_by_projection_keyframe(proj_ctx(), &fs.v, mat44(CurrentFrame.mTcw, kc), &ps.m, th, ORBdist,
+                                               mbCheckOrientation ? 1 : 0, m.data(), &nm),
+            "orbm_search_by_projection_keyframe");
+    apply(CurrentFrame.mvpMapPoints, m, vpMPs);
+    return nm;
+}
+
+// ORBmatcher.cc:290-403
+int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints,
+                                   std::vector<MapPoint*>& vpMatched, int th) {
+    FrameSide fs;
+    fs.gather(*pKF, nullptr, 0.f, 0.f);
+    fs.occupied(occupied_any(vpMatched));
+    std::set<MapPoint*> spAlreadyFound(vpMatched.begin(), vpMatched.end());
+    spAlreadyFound.erase(static_cast<MapPoint*>(NULL));
+    const size_t n = vpPoints.size();
+    PointSide ps;
+    ps.reserve(n);
+    for (size_t i = 0; i < n; i++) {
+        MapPoint* p = vpPoints[i];
+        ps.skip[i] = spAlreadyFound.count(p) > 0;
+        if (ps.skip[i]) continue;
+        ps.point(i, p, true);
+        cv::Mat nv = p->GetNormal();
+        for (int k = 0; k < 3; k++) ps.normal[3 * i + k] = nv.at<float>(k, 0);
+    }
+    ps.finish(n);
+    cv::Mat ks;
+    std::vector<int32_t> m(vpMatched.size() ? vpMatched.size() : 1);
+    int nm = 0;
+    proj_ok(orbm_search_by_projection_sim3(proj_ctx(), &fs.v, mat44(Scw, ks), &ps.m, th, m.data(), &nm),
+            "orbm_search_by_projection_sim3");
+    apply(vpMatched, m, vpPoints);
+    return nm;
+}
+
+}  // namespace ORB_SLAM2

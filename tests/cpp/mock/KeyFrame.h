@@ -14,6 +14,10 @@ class KeyFrame {
 public:
     int N = 0;
     float fx = 0, fy = 0, cx = 0, cy = 0;
+    float mnMinX = 0, mnMaxX = 0, mnMinY = 0, mnMaxY = 0;
+    float mfGridElementWidthInv = 0, mfGridElementHeightInv = 0;
+    int mnScaleLevels = 0;
+    float mfLogScaleFactor = 0;
     std::vector<cv::KeyPoint> mvKeys, mvKeysUn;
     std::vector<float> mvuRight;
     cv::Mat mDescriptors;

@@ -1,11 +1,26 @@
-/* TEST-ONLY mock of the MapPoint accessors ORBmatcher reads (isBad). */
+/* TEST-ONLY mock of the MapPoint members ORBmatcher reads (names as in ORB_SLAM2/include/MapPoint.h).
+ * GetMinDistance/GetMaxDistance are the two getters INTEGRATION.md asks a maintainer to add
+ * (mfMinDistance / mfMaxDistance are private in the reference). */
 #ifndef MAPPOINT_H
 #define MAPPOINT_H
+#include <opencv2/core/core.hpp>
 namespace ORB_SLAM2 {
 class MapPoint {
 public:
     bool bad = false;
+    int nObs = 1;
+    cv::Mat mWorldPos, mNormalVector, mDescriptor;
+    float mfMinDistance = 0, mfMaxDistance = 0;
+    bool mbTrackInView = false;
+    float mTrackProjX = 0, mTrackProjY = 0, mTrackProjXR = 0, mTrackViewCos = 0;
+    int mnTrackScaleLevel = 0;
     bool isBad() { return bad; }
+    int Observations() { return nObs; }
+    cv::Mat GetWorldPos() { return mWorldPos.clone(); }
+    cv::Mat GetNormal() { return mNormalVector.clone(); }
+    cv::Mat GetDescriptor() { return mDescriptor.clone(); }
+    float GetMinDistance() { return mfMinDistance; }
+    float GetMaxDistance() { return mfMaxDistance; }
 };
 }  // namespace ORB_SLAM2
 #endif

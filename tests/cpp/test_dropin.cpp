@@ -1,6 +1,7 @@
 /* test_dropin.cpp -- the C++ drop-in classes (cooperative-orb-slam_amd/host/) used the way
- * ORB-SLAM2's callers use them (Frame::ExtractORB, LocalMapping/LoopClosing/Tracking matcher
- * calls), checked bit-exactly against the CPU oracle. Needs a GPU to run; prints
+ * ORB-SLAM2's callers use them (Frame::ExtractORB, the stereo Frame's ComputeStereoMatches,
+ * LocalMapping/LoopClosing/Tracking matcher calls incl. SearchByProjection), checked bit-exactly
+ * against the CPU oracle. Needs a GPU to run; prints
  * "ALL PASS" on success. Build: tests/cpp/build.sh */
 #include <cmath>
 #include <cstdint>
@@ -216,6 +217,171 @@ int main() {
             for (int i = 0; i < F.N; i++) diff += vf[i] != (omf[i] >= 0 ? kf1.mvpMapPoints[omf[i]] : nullptr);
             CHECK(n == on && diff == 0, "SearchByBoW(KF,F) ratio=%.2f ori=%d: %d vs %d, %d diffs", ratio, ori, n, on, diff);
         }
+    }
+    // ---- SearchByProjection(Frame&, vector<MapPoint*>, th) and (Frame&, const Frame&, th, bMono)
+    {
+        Frame F;
+        F.N = (int)K[0].size(); F.mvKeys = K[0]; F.mvKeysUn = K[0]; F.mDescriptors = D[0];
+        F.mvScaleFactors = ext.GetScaleFactors(); F.mvLevelSigma2 = ext.GetScaleSigmaSquares();
+        F.mnScaleLevels = 8; F.mfLogScaleFactor = logf(1.2f);
+        F.fx = 715.092024f; F.fy = 719.025258f; F.cx = 334.298489f; F.cy = 256.326097f; F.mbf = 47.9f; F.mb = F.mbf / F.fx;
+        F.mnMinX = 0.f; F.mnMaxX = (float)W; F.mnMinY = 0.f; F.mnMaxY = (float)H;
+        F.mfGridElementWidthInv = 64.f / (F.mnMaxX - F.mnMinX);
+        F.mfGridElementHeightInv = 48.f / (F.mnMaxY - F.mnMinY);
+        uint32_t s = 77;
+        F.mvuRight.assign(F.N, -1.f);
+        for (int i = 0; i < F.N; i++) if (lcg(s) % 2) F.mvuRight[i] = F.mvKeys[i].pt.x - (float)(lcg(s) % 30);
+        std::vector<MapPoint> pre(F.N);
+        F.mvpMapPoints.assign(F.N, nullptr);
+        for (int i = 0; i < F.N; i++)
+            if (lcg(s) % 20 == 0) { pre[i].nObs = (int)(lcg(s) % 2); F.mvpMapPoints[i] = &pre[i]; }
+        const std::vector<MapPoint*> F0 = F.mvpMapPoints;
+        // local-map points near the frame's features (isInFrustum fields), with duplicates
+        const int M = 900;
+        std::vector<MapPoint> mp(M);
+        std::vector<MapPoint*> vp(M);
+        for (int j = 0; j < M; j++) {
+            const int src = (int)(lcg(s) % F.N);
+            MapPoint& p = mp[j];
+            vp[j] = &p;
+            p.mDescriptor = cv::Mat(1, 32, CV_8U);
+            memcpy(p.mDescriptor.data, F.mDescriptors.ptr<unsigned char>(src), 32);
+            for (int b = 0; b < 8; b++) { const uint32_t r = lcg(s) % 256; p.mDescriptor.data[r >> 3] ^= (uint8_t)(1u << (r & 7)); }
+            p.bad = lcg(s) % 25 == 0;
+            p.nObs = lcg(s) % 6 ? 2 : 0;
+            p.mbTrackInView = lcg(s) % 10 != 0;
+            p.mTrackProjX = F.mvKeys[src].pt.x + (float)((int)(lcg(s) % 7) - 3) * 0.5f;
+            p.mTrackProjY = F.mvKeys[src].pt.y + (float)((int)(lcg(s) % 7) - 3) * 0.5f;
+            p.mTrackProjXR = p.mTrackProjX - (float)(lcg(s) % 30);
+            p.mnTrackScaleLevel = F.mvKeys[src].octave;
+            p.mTrackViewCos = lcg(s) % 2 ? 0.9995f : 0.99f;
+        }
+        // oracle inputs built independently of the drop-in's gathering
+        std::vector<float> fx_(F.N), fy_(F.N), fa_(F.N);
+        std::vector<int32_t> fo_(F.N);
+        std::vector<uint8_t> occ(F.N);
+        for (int i = 0; i < F.N; i++) {
+            fx_[i] = F.mvKeysUn[i].pt.x; fy_[i] = F.mvKeysUn[i].pt.y; fa_[i] = F.mvKeysUn[i].angle;
+            fo_[i] = F.mvKeysUn[i].octave; occ[i] = F0[i] && F0[i]->nObs > 0;
+        }
+        orbm_frame_view fv;
+        memset(&fv, 0, sizeof(fv));
+        fv.n = F.N; fv.desc = F.mDescriptors.data; fv.x = fx_.data(); fv.y = fy_.data(); fv.octave = fo_.data();
+        fv.angle = fa_.data(); fv.uright = F.mvuRight.data(); fv.occupied = occ.data();
+        fv.min_x = F.mnMinX; fv.min_y = F.mnMinY; fv.max_x = F.mnMaxX; fv.max_y = F.mnMaxY;
+        fv.grid_w_inv = F.mfGridElementWidthInv; fv.grid_h_inv = F.mfGridElementHeightInv;
+        fv.fx = F.fx; fv.fy = F.fy; fv.cx = F.cx; fv.cy = F.cy; fv.bf = F.mbf; fv.b = F.mb;
+        fv.nlevels = 8; fv.scale_factors = F.mvScaleFactors.data(); fv.log_scale_factor = F.mfLogScaleFactor;
+        std::vector<uint8_t> md(32 * M), mbad(M), mobs(M), miv(M);
+        std::vector<float> mpx(M), mpy(M), mpxr(M), mcos(M);
+        std::vector<int32_t> mlv(M);
+        for (int j = 0; j < M; j++) {
+            memcpy(&md[32 * j], mp[j].mDescriptor.data, 32);
+            mbad[j] = mp[j].bad; mobs[j] = mp[j].nObs > 0; miv[j] = mp[j].mbTrackInView;
+            mpx[j] = mp[j].mTrackProjX; mpy[j] = mp[j].mTrackProjY; mpxr[j] = mp[j].mTrackProjXR;
+            mlv[j] = mp[j].mnTrackScaleLevel; mcos[j] = mp[j].mTrackViewCos;
+        }
+        orbm_mappoints om;
+        memset(&om, 0, sizeof(om));
+        om.n = M; om.desc = md.data(); om.bad = mbad.data(); om.has_obs = mobs.data(); om.track_in_view = miv.data();
+        om.track_proj_x = mpx.data(); om.track_proj_y = mpy.data(); om.track_proj_xr = mpxr.data();
+        om.track_level = mlv.data(); om.track_view_cos = mcos.data();
+        for (float th : {1.0f, 3.0f}) {
+            F.mvpMapPoints = F0;
+            ORBmatcher m(0.8f, false);
+            const int n = m.SearchByProjection(F, vp, th);
+            std::vector<int32_t> ref(F.N);
+            const int on = oc_search_by_projection_local(&fv, &om, th, 0.8f, ref.data());
+            int diff = 0;
+            for (int i = 0; i < F.N; i++) diff += F.mvpMapPoints[i] != (ref[i] >= 0 ? vp[ref[i]] : F0[i]);
+            CHECK(n == on && diff == 0, "SearchByProjection(F, local) th=%.0f: %d vs oracle %d, %d diffs", th, n, on, diff);
+        }
+        // motion model: LastFrame's MapPoints back-projected from the current keypoints (identity current pose)
+        Frame L;
+        L.N = F.N; L.mvKeys = F.mvKeys; L.mvKeysUn = F.mvKeysUn;
+        L.mvpMapPoints.assign(L.N, nullptr);
+        L.mvbOutlier.assign(L.N, false);
+        std::vector<MapPoint> lp(L.N);
+        for (int i = 0; i < L.N; i++) {
+            if (lcg(s) % 8 == 0) continue;
+            MapPoint& p = lp[i];
+            const float z = 1.f + (float)(lcg(s) % 1000) * 0.01f;
+            p.mWorldPos = cv::Mat(3, 1, CV_32F);
+            p.mWorldPos.at<float>(0, 0) = (F.mvKeys[i].pt.x - F.cx) / F.fx * z;
+            p.mWorldPos.at<float>(1, 0) = (F.mvKeys[i].pt.y - F.cy) / F.fy * z;
+            p.mWorldPos.at<float>(2, 0) = z;
+            p.mDescriptor = cv::Mat(1, 32, CV_8U);
+            memcpy(p.mDescriptor.data, F.mDescriptors.ptr<unsigned char>(i), 32);
+            p.mDescriptor.data[lcg(s) % 32] ^= 0x11;
+            p.nObs = lcg(s) % 5 ? 1 : 0;
+            L.mvpMapPoints[i] = &p;
+            L.mvbOutlier[i] = lcg(s) % 15 == 0;
+        }
+        F.mTcw = cv::Mat(4, 4, CV_32F);
+        L.mTcw = cv::Mat(4, 4, CV_32F);
+        for (int i = 0; i < 16; i++) F.mTcw.at<float>(i / 4, i % 4) = L.mTcw.at<float>(i / 4, i % 4) = (i % 5 == 0) ? 1.f : 0.f;
+        L.mTcw.at<float>(2, 3) = -0.02f;
+        std::vector<uint8_t> lsk(L.N), lobs(L.N), lmd(32 * L.N);
+        std::vector<float> lpos(3 * L.N), lang(L.N);
+        std::vector<int32_t> loct(L.N);
+        for (int i = 0; i < L.N; i++) {
+            lsk[i] = !L.mvpMapPoints[i] || L.mvbOutlier[i];
+            loct[i] = L.mvKeys[i].octave; lang[i] = L.mvKeysUn[i].angle;
+            if (!L.mvpMapPoints[i]) continue;
+            lobs[i] = L.mvpMapPoints[i]->nObs > 0;
+            memcpy(&lmd[32 * i], L.mvpMapPoints[i]->mDescriptor.data, 32);
+            for (int k = 0; k < 3; k++) lpos[3 * i + k] = L.mvpMapPoints[i]->mWorldPos.at<float>(k, 0);
+        }
+        orbm_mappoints ol;
+        memset(&ol, 0, sizeof(ol));
+        ol.n = L.N; ol.desc = lmd.data(); ol.pos = lpos.data(); ol.has_obs = lobs.data(); ol.skip = lsk.data();
+        ol.octave = loct.data(); ol.angle = lang.data();
+        for (int mono = 0; mono < 2; mono++) {
+            F.mvpMapPoints = F0;
+            ORBmatcher m(0.9f, true);
+            const int n = m.SearchByProjection(F, L, 7.0f, mono != 0);
+            std::vector<int32_t> ref(F.N);
+            const int on = oc_search_by_projection_last_frame(&fv, F.mTcw.ptr<float>(), &ol, L.mTcw.ptr<float>(), 7.0f,
+                                                              mono, 1, ref.data());
+            int diff = 0;
+            for (int i = 0; i < F.N; i++)
+                diff += F.mvpMapPoints[i] != (ref[i] >= 0 ? L.mvpMapPoints[ref[i]] : (ref[i] == -2 ? nullptr : F0[i]));
+            CHECK(n == on && n > F.N / 4 && diff == 0, "SearchByProjection(F, LastFrame) mono=%d: %d vs oracle %d, %d diffs",
+                  mono, n, on, diff);
+        }
+    }
+    // ---- Frame::ComputeStereoMatches with two extractors (the stereo Frame ctor, Frame.cc:80-98)
+    {
+        std::vector<uint8_t> right((size_t)W * H);
+        orbx_synth_frames_shifted(0, 0, 1, W, H, 9, right.data());
+        ORBextractor el(1000, 1.2f, 8, 20, 7), er(1000, 1.2f, 8, 20, 7);
+        Frame F;
+        cv::Mat iml(H, W, CV_8U, frames.data(), W), imr(H, W, CV_8U, right.data(), W);
+        el(iml, cv::Mat(), F.mvKeys, F.mDescriptors);
+        er(imr, cv::Mat(), F.mvKeysRight, F.mDescriptorsRight);
+        F.N = (int)F.mvKeys.size();
+        F.mpORBextractorLeft = &el; F.mpORBextractorRight = &er;
+        F.mbf = 47.90639384423901f; F.mb = 0.11f;
+        F.ComputeStereoMatches();
+        oc_extractor* ol = oc_create(&p);
+        oc_extractor* orr = oc_create(&p);
+        std::vector<orbx_kp> kl(64 * 1024), kr(64 * 1024);
+        std::vector<uint8_t> dl(32 * 64 * 1024), dr(32 * 64 * 1024);
+        int nl = 0, nr = 0;
+        oc_extract(ol, frames.data(), W, H, W, kl.data(), dl.data(), 64 * 1024, &nl);
+        oc_extract(orr, right.data(), W, H, W, kr.data(), dr.data(), 64 * 1024, &nr);
+        std::vector<float> ur(nl), dp(nl);
+        const int ok = oc_compute_stereo_matches(ol, orr, kl.data(), dl.data(), nl, kr.data(), dr.data(), nr, F.mbf, F.mb,
+                                                 ur.data(), dp.data());
+        int diff = 0, kept = 0;
+        for (int i = 0; i < nl && nl == F.N; i++) {
+            diff += !same_bits(F.mvuRight[i], ur[i]) || !same_bits(F.mvDepth[i], dp[i]);
+            kept += F.mvuRight[i] >= 0;
+        }
+        CHECK(nl == F.N && diff == 0 && ok == kept && kept > F.N / 4, "ComputeStereoMatches: %d diffs, kept %d vs %d", diff,
+              kept, ok);
+        oc_destroy(ol);
+        oc_destroy(orr);
     }
     // DescriptorDistance (ORBmatcher.cc:1647-1663)
     int dd = 0;
