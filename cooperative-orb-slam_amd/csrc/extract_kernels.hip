@@ -1196,11 +1196,27 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     __shared__ __align__(8) uint8_t s_patch[16][kDescPatchRows * kDescPatchPitch];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int sub = lane >> 4, ln = lane & 15;
-    const int f = blockIdx.y;
+    // XCD-aware block mapping (1-D grid of G groups x F frames): workgroups are dispatched to the 8
+    // XCDs round-robin, so with F % 8 == 0 block b runs on XCD b % 8 and serves frame
+    // (b % 8) + 8 * ((b / 8) / G): every workgroup of a frame shares one XCD's L2, where the
+    // overlapping 37x37 patches and IC rows of neighbouring keypoints hit
+    const int G = (ep.kp_per_frame + 15) / 16;
+    int f, blk;
+    {
+        const int b = blockIdx.x;
+        if ((gridDim.x / G) % 8 == 0) {
+            const int k = b >> 3;
+            f = (b & 7) + 8 * (k / G);
+            blk = k % G;
+        } else {
+            f = b / G;
+            blk = b % G;
+        }
+    }
     // everything that depends only on the slot is issued before the table barrier
     const PatPt my_pat = kPatternF.t[tid];
     const int2 my_ic = ((const int2*)(ptab + ep.ic_off))[tid];
-    const int g = (blockIdx.x * 4 + wave) * 4 + sub;  // octree output slot of this lane group
+    const int g = (blk * 4 + wave) * 4 + sub;  // octree output slot of this lane group
     const int gc = min(g, ep.kp_per_frame - 1);
     const uint32_t kk_raw = lvkey[(long long)f * ep.kp_per_frame + gc];
     // per-level counts of this frame (lvcnt is padded by kMaxLevels ints; entries >= L masked)
@@ -1210,7 +1226,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;
     s_pat[(tid & 15) * 16 + (tid >> 4)] = my_pat;  // pair p at (p % 16) * 16 + p / 16
     s_ic[tid] = my_ic;
-    if (blockIdx.x == 0 && tid == 0) {
+    if (blk == 0 && tid == 0) {
         int tot = 0;
 #pragma unroll
         for (int q = 0; q < kMaxLevels; q++) tot += cl[q];
@@ -1454,7 +1470,7 @@ hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0,
                            const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
                            const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,
                            int* out_counts, int kp_stride, const int* ptab, int nframes, hipStream_t st) {
-    dim3 grid((ep.kp_per_frame + 15) / 16, nframes);
+    dim3 grid(((ep.kp_per_frame + 15) / 16) * nframes);
     hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, lvkey,
                        lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
     return hipGetLastError();

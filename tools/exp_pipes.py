@@ -47,12 +47,11 @@ def run(torch, orbamd, frames_np, P, steps=20, warm=3, offset=False):
 def main():
     import torch
     import orbamd
-    for B in (512, 1024):
+    cfgs = [(1024, 4, True), (2048, 4, True), (1024, 3, True), (1536, 3, True)]
+    for B, P, off in cfgs:
         frames = orbamd.synth_frames(0, 0, B, 640, 480)
-        for P in (1, 2, 4):
-            for off in (False, True):
-                if P == 1 and off:
-                    continue
+        if True:
+            if True:
                 print("B=%d P=%d offset=%d frames/s=%.0f" % (B, P, off, run(torch, orbamd, frames, P, offset=off)),
                       flush=True)
 
