@@ -154,22 +154,28 @@ def main():
 
     done = [torch.cuda.Event() for _ in range(P)]
 
-    def step(ev=None):
+    def step(ev=None, xev=None, extract=True, match=True, xchg=True):
         for p in range(P):
             st = streams[p].cuda_stream
-            if p > 0:
-                # staggered graphs: graph p's extraction (FAST-heavy) overlaps graph p-1's matcher and the
-                # latency-bound tail stages instead of running in lockstep with them
-                streams[p].wait_event(done[p - 1])
-            pipes[p].extract(frames[p], st)
-            done[p].record(streams[p])
-            if ev is not None:
-                ev[p][0].record(streams[p])
-            pipes[p].match_pairs(st)
-            if ev is not None:
-                ev[p][1].record(streams[p])
-        if not args.no_exchange:
+            if extract:
+                if p > 0:
+                    # staggered graphs: graph p's extraction (FAST-heavy) overlaps graph p-1's matcher and the
+                    # latency-bound tail stages instead of running in lockstep with them
+                    streams[p].wait_event(done[p - 1])
+                pipes[p].extract(frames[p], st)
+                done[p].record(streams[p])
+            if match:
+                if ev is not None:
+                    ev[p][0].record(streams[p])
+                pipes[p].match_pairs(st)
+                if ev is not None:
+                    ev[p][1].record(streams[p])
+        if xchg and not args.no_exchange:
+            if xev is not None:
+                xev[0].record(streams[0])
             exchange()
+            if xev is not None:
+                xev[1].record(streams[0])
 
     for _ in range(args.warmup):
         step()
@@ -185,12 +191,13 @@ def main():
             lib.orbx_profile_enable(pp.ext._h, mask)
         evs = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(P)]
                for _ in range(nsteps)]
+        xevs = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(nsteps)]
         if timed and world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t_start = time.perf_counter()
         for i in range(nsteps):
-            step(evs[i])
+            step(evs[i], xevs[i])
         torch.cuda.synchronize()
         if timed and world > 1:
             dist.barrier()
@@ -207,7 +214,18 @@ def main():
             ncalls += nc.value
         st = {k: acc[i] / max(ncalls, 1) for i, k in enumerate(stages) if (mask >> i) & 1}
         st["match"] = sum(e[p][0].elapsed_time(e[p][1]) for e in evs for p in range(P)) / (nsteps * P)
+        if not args.no_exchange:
+            st["exchange"] = sum(x[0].elapsed_time(x[1]) for x in xevs) / nsteps
         return elapsed, st
+
+    def run_part(nsteps, **kw):
+        """untimed breakdown pass: wall time of nsteps steps doing only part of the work"""
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(nsteps):
+            step(**kw)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
 
     # 1) stage split (untimed): every stage bracketed, same schedule
     _, stage_ms = run_profiled(0x1F, args.steps, False)
@@ -218,6 +236,9 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    # 3) extract-only and match-only rates, untimed breakdown passes
+    extract_fps = B * args.steps / run_part(args.steps, match=False, xchg=False)
+    match_pps = B * args.steps / run_part(args.steps, extract=False, xchg=False)
     nkp = float(sum(pp.counts.float().mean().item() for pp in pipes) / P)
     nmatch = float(sum(pp.nmatch.float().mean().item() for pp in pipes) / P)
 
@@ -268,6 +289,8 @@ def main():
             "pipeline_hbm": {"bytes_per_frame": b_frame, "achieved_GBs": round(b_frame * value / world / 1e9, 2),
                              "frac": round(b_frame * value / world / 1e9 / HBM_PEAK_GBS, 5)},
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
+            "extract_only_frames_per_s_per_gpu": round(extract_fps, 1),
+            "match_only_pairs_per_s_per_gpu": round(match_pps, 1),
             "kp_per_frame": round(nkp, 1),
             "matches_per_pair": round(nmatch, 1),
         }
