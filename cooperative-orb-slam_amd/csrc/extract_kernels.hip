@@ -37,6 +37,7 @@ __device__ __forceinline__ int iclamp(int v, int lo, int hi) { return v < lo ? l
 
 typedef short short2v __attribute__((ext_vector_type(2)));
 typedef float float2v __attribute__((ext_vector_type(2)));
+typedef unsigned int uint2v __attribute__((ext_vector_type(2)));
 static inline int iclamp_host(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 /* n consecutive little-endian dwords starting at an arbitrary byte address, from n+1 aligned
@@ -522,17 +523,24 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
         int ncand = 0;
         {
             // SWAR pretest: each lane tests the 4 pixels of one aligned ROI dword (band columns
-            // [3, 3+bw)), as two u16 pairs (pixels 0,2 and 1,3) with packed 16-bit arithmetic.
+            // [3, 3+bw)) as 4 bytes with v_lerp_u8 (per byte (a + b + r) >> 1, exact in 9 bits):
+            // m = lerp(c, 255 - v, r) = floor((c - v + 255 + r) / 2), and m >= M <=> bit 7 of lerp(m, 255 - M, 1).
+            // With r of the right parity, c - v > t <=> m_b >= (t + 256 + r_b) / 2 (r_b = t & 1) and
+            // c - v < -t <=> NOT m_d >= (255 - t + r_d) / 2 (r_d = 1 - r_b); for t = 255 the bright bound is
+            // clamped to 255 (looser: the pretest stays a necessary condition). Exhaustive check over
+            // (c, v, t): tests/test_oracle_primitives.py::test_fast_pretest_lerp_exact.
             const int G = c.G;  // dword groups covering columns [0, bw+3): (bw + 6) / 4
             const int rpc = c.rpc;
             const int lr = (lane * c.magG) >> 16, j = lane - lr * G;
             const bool lane_ok = lane < rpc * G;
-            // band-column masks at the keep bits: pixels 0 / 2 in keep2[0] bits 15 / 31, pixels 1 / 3 in keep2[1]
+            // band-column mask at the candidate bits: pixel i of this lane's dword -> bit 8 i + 7
             auto colok = [&](int i) { return 4 * j + i >= 3 && 4 * j + i < 3 + bw; };
-            const uint32_t cm0 = (colok(0) ? 0x8000u : 0u) | (colok(2) ? 0x80000000u : 0u);
-            const uint32_t cm1 = (colok(1) ? 0x8000u : 0u) | (colok(3) ? 0x80000000u : 0u);
+            const uint32_t colm = (colok(0) ? 0x80u : 0u) | (colok(1) ? 0x8000u : 0u) | (colok(2) ? 0x800000u : 0u) |
+                                  (colok(3) ? 0x80000000u : 0u);
             const int dummy = (RP - 6) * (RH - 6);  // 64 per-lane dummy slots after the list
-            const uint32_t tq = (uint32_t)(t_lo + 1) * 0x00010001u;
+            const uint32_t RB = (t_lo & 1) ? 0x01010101u : 0u, RD = RB ^ 0x01010101u;
+            const uint32_t CB = (uint32_t)(255 - min((t_lo + 256 + (t_lo & 1)) >> 1, 255)) * 0x01010101u;
+            const uint32_t CD = (uint32_t)(255 - ((256 - t_lo - (t_lo & 1)) >> 1)) * 0x01010101u;
             for (int r0 = 0; r0 < bh; r0 += rpc) {
                 const int rr = 3 + r0 + lr;
                 const int rrc = min(rr, bh + 2);
@@ -544,36 +552,22 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
                 const uint32_t xu = *(const uint32_t*)(q - 3 * RP);  // ring 8 (row - 3)
                 const uint32_t xr = __builtin_amdgcn_alignbyte(xn, xv, 3);  // ring 4 (col + 3)
                 const uint32_t xl = __builtin_amdgcn_alignbyte(xv, xp, 1);  // ring 12 (col - 3)
-                uint32_t keep2[2];
-#pragma unroll
-                for (int half = 0; half < 2; half++) {
-                    const uint32_t sel = half ? 0x0c030c01u : 0x0c020c00u;
-                    const short2v pv = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xv, sel));
-                    const short2v c0 = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xd, sel));
-                    const short2v c4 = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xr, sel));
-                    const short2v c8 = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xu, sel));
-                    const short2v c12 = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, xl, sel));
-                    const short2v tv = __builtin_bit_cast(short2v, tq);
-                    const short2v hv = pv + tv, lv2 = pv - tv;
-                    // sign bit set = NOT brighter (c < v+t+1) / NOT darker (c > v-t-1)
-                    const uint32_t b0 = __builtin_bit_cast(uint32_t, (short2v)(c0 - hv));
-                    const uint32_t b4 = __builtin_bit_cast(uint32_t, (short2v)(c4 - hv));
-                    const uint32_t b8 = __builtin_bit_cast(uint32_t, (short2v)(c8 - hv));
-                    const uint32_t b12 = __builtin_bit_cast(uint32_t, (short2v)(c12 - hv));
-                    const uint32_t d0 = __builtin_bit_cast(uint32_t, (short2v)(lv2 - c0));
-                    const uint32_t d4 = __builtin_bit_cast(uint32_t, (short2v)(lv2 - c4));
-                    const uint32_t d8 = __builtin_bit_cast(uint32_t, (short2v)(lv2 - c8));
-                    const uint32_t d12 = __builtin_bit_cast(uint32_t, (short2v)(lv2 - c12));
-                    // candidate iff two cyclically adjacent cardinals agree: (b0|b8)&(b4|b12) in
-                    // "is brighter" terms = NOT((nb0&nb8)|(nb4&nb12)) in sign terms
-                    const uint32_t xb = (b0 & b8) | (b4 & b12);
-                    const uint32_t xdk = (d0 & d8) | (d4 & d12);
-                    keep2[half] = ~(xb & xdk);  // bits 15 / 31 set = candidate
-                }
-                // pixel i of this lane: i = 0, 2 -> bits 15, 31 of keep2[0]; i = 1, 3 -> bits 15, 31 of keep2[1]
-                const uint32_t rowm = (lane_ok && rr < 3 + bh) ? 0xffffffffu : 0u;
-                const uint32_t k0 = keep2[0] & cm0 & rowm, k1 = keep2[1] & cm1 & rowm;
-                const bool p0 = (int)(k0 << 16) < 0, p1 = (int)(k1 << 16) < 0, p2 = (int)k0 < 0, p3 = (int)k1 < 0;
+                const uint32_t nv = ~xv;  // 255 - v per byte
+                auto bright = [&](uint32_t cb) {
+                    return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(cb, nv, RB), CB, 0x01010101u);
+                };
+                auto notdark = [&](uint32_t cb) {
+                    return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(cb, nv, RD), CD, 0x01010101u);
+                };
+                const uint32_t b0 = bright(xd), b4 = bright(xr), b8 = bright(xu), b12 = bright(xl);
+                const uint32_t n0 = notdark(xd), n4 = notdark(xr), n8 = notdark(xu), n12 = notdark(xl);
+                // candidate iff two cyclically adjacent cardinals are both brighter ((b0|b8)&(b4|b12)) or
+                // both darker (NOT((n0&n8)|(n4&n12)))
+                const uint32_t cand = ((b0 | b8) & (b4 | b12)) | ~((n0 & n8) | (n4 & n12));
+                const uint32_t rowm = (lane_ok && rr < 3 + bh) ? colm : 0u;
+                const uint32_t k = cand & rowm;  // bit 8 i + 7 = pixel i is a candidate
+                const bool p0 = (k & 0x80u) != 0u, p1 = (k & 0x8000u) != 0u, p2 = (k & 0x800000u) != 0u,
+                           p3 = (int)k < 0;
                 // ordered compaction: row-major = (lane, pixel) lexicographic
                 const unsigned long long B0 = __ballot(p0), B1 = __ballot(p1), B2 = __ballot(p2), B3 = __ballot(p3);
                 int pre = __builtin_amdgcn_mbcnt_hi((unsigned)(B0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)B0, 0));
@@ -1151,9 +1145,10 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     }
 }
 
-/* rBRIEF test pairs as floats (x0, y0, x1, y1), one 16-byte load per test */
+/* rBRIEF test pairs as floats, one 16-byte load per test; stored (x0, x1, y0, y1) so the two points'
+ * x and y coordinates are float pairs for the packed-f32 rotation */
 struct PatPt {
-    float x0, y0, x1, y1;
+    float x0, x1, y0, y1;
 };
 struct PatTable {
     PatPt t[256];
@@ -1161,9 +1156,12 @@ struct PatTable {
 constexpr float pat_s8(unsigned char c) { return (float)(c < 128 ? (int)c : (int)c - 256); }
 constexpr PatTable make_pattern_table() {
     PatTable p{};
-    for (int t = 0; t < 256; t++)
-        p.t[t] = PatPt{pat_s8(orbx_pattern_soa_u8[t]), pat_s8(orbx_pattern_soa_u8[256 + t]),
-                       pat_s8(orbx_pattern_soa_u8[512 + t]), pat_s8(orbx_pattern_soa_u8[768 + t])};
+    for (int t = 0; t < 256; t++) {
+        p.t[t].x0 = pat_s8(orbx_pattern_soa_u8[t]);
+        p.t[t].y0 = pat_s8(orbx_pattern_soa_u8[256 + t]);
+        p.t[t].x1 = pat_s8(orbx_pattern_soa_u8[512 + t]);
+        p.t[t].y1 = pat_s8(orbx_pattern_soa_u8[768 + t]);
+    }
     return p;
 }
 __device__ constexpr PatTable kPatternF = make_pattern_table();
@@ -1287,17 +1285,21 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     }
     int m10, m01;
     {
-        int A = 0, M = 0;
+        // per row ri = r + 2p: A' += sum (u+15) I, S += sum I, M' += 2p * sum I (24-bit multiply by a
+        // constant); then m10 = A' - 15 S and m01 = M' + (r - 15) S
+        uint32_t Ap = 0, S = 0, Mp = 0;
 #pragma unroll
         for (int p = 0; p < 16; p++) {
             const int ri = r + 2 * p;
             const uint32_t al = (mis + (uint32_t)p * dmis) & 3u;
             const uint32_t I4 = __builtin_amdgcn_alignbyte(wv[p].y, wv[p].x, al);
             const int2 msk = s_ic[ri * 8 + g4];
-            const int sI = (int)__builtin_amdgcn_udot4(I4, (uint32_t)msk.y, 0u, false);
-            A += (int)__builtin_amdgcn_udot4(I4, (uint32_t)msk.x, 0u, false) - 15 * sI;
-            M += (ri - 15) * sI;
+            const uint32_t sI = __builtin_amdgcn_udot4(I4, (uint32_t)msk.y, 0u, false);
+            Ap = __builtin_amdgcn_udot4(I4, (uint32_t)msk.x, Ap, false);
+            S += sI;
+            Mp += __umul24(sI, 2u * (uint32_t)p);
         }
+        int A = (int)Ap - 15 * (int)S, M = (int)Mp + (r - 15) * (int)S;
 #pragma unroll
         for (int o = 8; o > 0; o >>= 1) {
             A += __shfl_xor(A, o, 16);
@@ -1316,16 +1318,33 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     wave_sync();  // patch stores of the other lanes of this group
     const uint8_t* pc0 = patch + kDescPatchR * kDescPatchPitch + kDescPatchR + pmis;  // keypoint
     uint32_t myword = 0;  // descriptor bytes 2ln, 2ln+1 of this lane's keypoint = pairs 16ln .. 16ln+15
+    {
+        // Both points of a pair at once in packed f32 (v_pk_mul_f32 / v_pk_add_f32: per component the
+        // same IEEE products and sums as the reference's x*b + y*a, no contraction). cvRound (RNE) by
+        // adding 1.5*2^23: the sum's bits are 0x4B400000 + round(v) for |v| < 2^22, so the rounded
+        // row/column feed v_mad_u32_u24 (low 24 bits 0x400000 + r) and the constant bias
+        // K = 0x400000 * pitch + 0x4B400000 is removed once per address.
+#pragma clang fp contract(off)
+        const float2v A2 = {a, a}, B2 = {b, b};
+        const float2v MAG = {12582912.f, 12582912.f};
+        constexpr uint32_t K = 0x400000u * (uint32_t)kDescPatchPitch + 0x4B400000u;
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const PatPt pp = s_pat[16 * j + ln];  // pair 16ln + j (transposed table: conflict-free reads)
-        const int r0 = cv_round(__fadd_rn(__fmul_rn(pp.x0, b), __fmul_rn(pp.y0, a)));
-        const int c0 = cv_round(__fsub_rn(__fmul_rn(pp.x0, a), __fmul_rn(pp.y0, b)));
-        const int r1 = cv_round(__fadd_rn(__fmul_rn(pp.x1, b), __fmul_rn(pp.y1, a)));
-        const int c1 = cv_round(__fsub_rn(__fmul_rn(pp.x1, a), __fmul_rn(pp.y1, b)));
-        const int t0 = pc0[__mul24(r0, kDescPatchPitch) + c0];  // |r| <= 18: 24-bit multiply
-        const int t1 = pc0[__mul24(r1, kDescPatchPitch) + c1];
-        myword |= (uint32_t)(t0 < t1) << j;
+        for (int j = 0; j < 16; j++) {
+            const PatPt pp = s_pat[16 * j + ln];  // pair 16ln + j (transposed table: conflict-free reads)
+            const float2v X = {pp.x0, pp.x1}, Y = {pp.y0, pp.y1};
+            float2v R = (X * B2 + Y * A2) + MAG;  // rows    round(x*b + y*a) of points 0, 1
+            float2v C = (X * A2 - Y * B2) + MAG;  // columns round(x*a - y*b)
+            // opaque to the optimizer: keeps the pairs packed (v_pk_*_f32) and the bit patterns unfolded
+            asm("" : "+v"(R), "+v"(C));
+            // (bit_cast of the whole pair: clang folds a bit_cast of a single vector element to undef here)
+            const uint2v RB = __builtin_bit_cast(uint2v, R), CB = __builtin_bit_cast(uint2v, C);
+            const uint32_t rb0 = RB.x, rb1 = RB.y, cb0 = CB.x, cb1 = CB.y;
+            const uint32_t o0 = (rb0 & 0xFFFFFFu) * (uint32_t)kDescPatchPitch + cb0 - K;
+            const uint32_t o1 = (rb1 & 0xFFFFFFu) * (uint32_t)kDescPatchPitch + cb1 - K;
+            const int t0 = pc0[(int)o0];
+            const int t1 = pc0[(int)o1];
+            myword |= (uint32_t)(t0 < t1) << j;
+        }
     }
     if (valid) {
         const long long o = (long long)f * kp_stride + outidx;

@@ -52,6 +52,31 @@ def test_fast_matches_definition(seed, t):
     assert np.array_equal(got, exp)
 
 
+def test_fast_pretest_lerp_exact():
+    """k_fast_cells2's byte-SWAR pretest compares with v_lerp_u8 (per byte (a + b + r) >> 1):
+    bright = bit 7 of lerp(lerp(c, 255 - v, r_b), 255 - M_b, 1) must equal c > v + t, and
+    notdark = bit 7 of lerp(lerp(c, 255 - v, r_d), 255 - M_d, 1) must equal NOT c < v - t, for every
+    (c, v, t) in [0, 255]^3 (t = 255: the bright bound is clamped, so only c > v + t => bright)."""
+    c = np.arange(256, dtype=np.int32)[:, None]
+    v = np.arange(256, dtype=np.int32)[None, :]
+
+    def lerp(a, b, r):
+        return (a + b + r) >> 1
+
+    for t in range(256):
+        rb, rd = t & 1, 1 - (t & 1)
+        mb_c = min((t + 256 + rb) >> 1, 255)
+        md_c = (256 - t - (t & 1)) >> 1
+        bright = (lerp(lerp(c, 255 - v, rb), 255 - mb_c, 1) & 0x80) != 0
+        notdark = (lerp(lerp(c, 255 - v, rd), 255 - md_c, 1) & 0x80) != 0
+        assert lerp(lerp(c, 255 - v, rb), 255 - mb_c, 1).max() <= 255
+        if t < 255:
+            assert np.array_equal(bright, c > v + t), t
+        else:
+            assert not (c > v + t).any() or bright[c > v + t].all()
+        assert np.array_equal(notdark, ~(c < v - t)), t
+
+
 def test_fast_on_synthetic_cell_roi():
     frame = orbamd.synth_frames(0, 0, 1, 640, 480)[0]
     roi = frame[100:138, 200:237]
