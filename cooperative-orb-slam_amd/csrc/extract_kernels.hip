@@ -537,7 +537,8 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
             auto colok = [&](int i) { return 4 * j + i >= 3 && 4 * j + i < 3 + bw; };
             const uint32_t colm = (colok(0) ? 0x80u : 0u) | (colok(1) ? 0x8000u : 0u) | (colok(2) ? 0x800000u : 0u) |
                                   (colok(3) ? 0x80000000u : 0u);
-            const int dummy = (RP - 6) * (RH - 6);  // 64 per-lane dummy slots after the list
+            uint32_t* rec = (uint32_t*)str;  // <= bh x G records, zeroed again by the expansion
+            int nrec = 0;
             const uint32_t RB = (t_lo & 1) ? 0x01010101u : 0u, RD = RB ^ 0x01010101u;
             const uint32_t CB = (uint32_t)(255 - min((t_lo + 256 + (t_lo & 1)) >> 1, 255)) * 0x01010101u;
             const uint32_t CD = (uint32_t)(255 - ((256 - t_lo - (t_lo & 1)) >> 1)) * 0x01010101u;
@@ -564,26 +565,44 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
                 // candidate iff two cyclically adjacent cardinals are both brighter ((b0|b8)&(b4|b12)) or
                 // both darker (NOT((n0&n8)|(n4&n12)))
                 const uint32_t cand = ((b0 | b8) & (b4 | b12)) | ~((n0 & n8) | (n4 & n12));
-                const uint32_t rowm = (lane_ok && rr < 3 + bh) ? colm : 0u;
-                const uint32_t k = cand & rowm;  // bit 8 i + 7 = pixel i is a candidate
-                const bool p0 = (k & 0x80u) != 0u, p1 = (k & 0x8000u) != 0u, p2 = (k & 0x800000u) != 0u,
-                           p3 = (int)k < 0;
-                // ordered compaction: row-major = (lane, pixel) lexicographic
-                const unsigned long long B0 = __ballot(p0), B1 = __ballot(p1), B2 = __ballot(p2), B3 = __ballot(p3);
-                int pre = __builtin_amdgcn_mbcnt_hi((unsigned)(B0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)B0, 0));
-                pre = __builtin_amdgcn_mbcnt_hi((unsigned)(B1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)B1, pre));
-                pre = __builtin_amdgcn_mbcnt_hi((unsigned)(B2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)B2, pre));
-                pre = __builtin_amdgcn_mbcnt_hi((unsigned)(B3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)B3, pre));
-                const int tot = __popcll(B0) + __popcll(B1) + __popcll(B2) + __popcll(B3);
-                // unconditional writes: a pixel that is not a candidate goes to this lane's dummy slot
-                const int e = (rr << 8) | (4 * j);
-                const int q0 = ncand + pre, q1 = q0 + (int)p0, q2 = q1 + (int)p1, q3 = q2 + (int)p2;
-                const int dmy = dummy + lane;
-                clist[p0 ? q0 : dmy] = (uint16_t)e;
-                clist[p1 ? q1 : dmy] = (uint16_t)(e + 1);
-                clist[p2 ? q2 : dmy] = (uint16_t)(e + 2);
-                clist[p3 ? q3 : dmy] = (uint16_t)(e + 3);
-                ncand += tot;
+                const uint32_t k = (lane_ok && rr < 3 + bh) ? (cand & colm) : 0u;  // bit 8 i + 7: pixel i
+                // sparse ordered record of this dword (lanes with a candidate, ~1 in 5): row-major =
+                // lane order within a row pass; record = candidate bits | group j | ROI row << 8
+                // (j, rr < 128 fit the 7 free bits of bytes 0 / 1)
+                const unsigned long long Bk = __ballot(k != 0u);
+                if (k != 0u) {
+                    const int at = nrec + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(Bk >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((unsigned)Bk, 0));
+                    rec[at] = k | (uint32_t)j | ((uint32_t)rr << 8);
+                }
+                nrec += __popcll(Bk);
+            }
+            wave_sync();
+            // expand the records into the candidate list (order kept: records in order, pixels of a
+            // record ascending); the record area is zeroed behind, so str is the zero S map again
+            for (int c0 = 0; c0 < nrec; c0 += 64) {
+                const int i = c0 + lane;
+                uint32_t r = 0u;
+                if (i < nrec) {
+                    r = rec[i];
+                    rec[i] = 0u;
+                }
+                const uint32_t km = r & 0x80808080u;
+                const int cntl = __popc(km);
+                int pos = ncand;
+#pragma unroll
+                for (int bit = 0; bit < 3; bit++) {  // cntl <= 4
+                    const unsigned long long B = __ballot((cntl >> bit) & 1);
+                    pos += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(B >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((unsigned)B, 0))
+                           << bit;
+                    ncand += __popcll(B) << bit;
+                }
+                const int e = (int)(((r >> 8) & 127u) << 8) | (int)(4u * (r & 127u));
+                if (km & 0x80u) clist[pos++] = (uint16_t)e;
+                if (km & 0x8000u) clist[pos++] = (uint16_t)(e + 1);
+                if (km & 0x800000u) clist[pos++] = (uint16_t)(e + 2);
+                if (km & 0x80000000u) clist[pos++] = (uint16_t)(e + 3);
             }
         }
         wave_sync();
