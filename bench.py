@@ -63,13 +63,16 @@ def algorithmic_bytes(W, H, nkp):
 
 def cpu_baseline(frames, seconds, threads):
     """Oracle ("port") timed on host cores: extract + BF SearchForTriangulation vs the previous
-    frame, one independent frame stream per thread (ctypes releases the GIL)."""
+    frame, one independent frame stream per thread (ctypes releases the GIL). Returns frames/s,
+    frames, seconds, and the per-stage seconds per frame summed over the threads' extractors
+    (oracle stage timers + the matcher timed around its call)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
     import oracle_py
     import orbamd
     F12, ex, ey = orbamd.device.default_geometry()
     count = [0] * threads
+    stage = [None] * threads
+    match_s = [0.0] * threads
     stop = time.perf_counter() + seconds
 
     def work(tid):
@@ -82,10 +85,13 @@ def cpu_baseline(frames, seconds, threads):
             k, d = orc(img)
             cur = orbamd.KeyFrameView(k, d, tabs["scale"], tabs["sigma2"])
             if prev is not None:
+                tm = time.perf_counter()
                 oracle_py.search_for_triangulation(cur, prev, F12, ex, ey, False, False)
+                match_s[tid] += time.perf_counter() - tm
             prev = cur
             count[tid] += 1
             i += threads
+        stage[tid] = orc.stage_times()[0]
 
     t0 = time.perf_counter()
     ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
@@ -94,7 +100,10 @@ def cpu_baseline(frames, seconds, threads):
     for t in ths:
         t.join()
     el = time.perf_counter() - t0
-    return sum(count) / el, sum(count), el
+    n = max(sum(count), 1)
+    per = {k: sum(st[k] for st in stage) / n for k in stage[0]}
+    per["match"] = sum(match_s) / max(n - threads, 1)
+    return sum(count) / el, sum(count), el, per
 
 
 def main():
@@ -296,10 +305,15 @@ def main():
         }
     if rank == 0 and not args.no_cpu:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        fps, nfr, sec = cpu_baseline(frames_np, args.cpu_seconds, threads)
+        fps, nfr, sec, _ = cpu_baseline(frames_np, args.cpu_seconds, threads)
+        # the reference's own architecture: one Tracking thread, with its stage split
+        fps1, nfr1, sec1, per1 = cpu_baseline(frames_np, max(args.cpu_seconds / 2, 1.0), 1)
         result["cpu_baseline"] = {"value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
                                   "sample": "%d synthetic 640x480 frames (extract + BF triangulation vs previous) "
-                                            "in %.1f s on %d threads, oracle/orb_oracle.c -O2" % (nfr, sec, threads)}
+                                            "in %.1f s on %d threads, oracle/orb_oracle.c -O2; 1-thread leg: %d "
+                                            "frames in %.1f s" % (nfr, sec, threads, nfr1, sec1),
+                                  "value_1thread": round(fps1, 2),
+                                  "stage_ms_per_frame_1thread": {k: round(v * 1e3, 3) for k, v in per1.items()}}
         result["speedup_vs_cpu"] = round(value / fps, 1)
     elif rank == 0:
         result["cpu_baseline"] = None

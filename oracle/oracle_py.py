@@ -41,6 +41,7 @@ _SIG = {
     "oc_level_candidates": (_I, [_P, _I, _P, _I]),
     "oc_level_octree": (_I, [_P, _I, _P, _I]),
     "oc_get_tables": (None, [_P, _P, _P, _P, _P, _P, _P]),
+    "oc_stage_times": (None, [_P, _P, _P]),
     "oc_fast_atan2": (_F, [_F, _F]),
     "oc_gauss_kernel_q8": (_I, [_P]),
     "oc_resize_linear": (None, [_P, _I, _I, _SZ, _P, _I, _I, _SZ]),
@@ -144,6 +145,15 @@ class OracleExtractor:
 
     def octree(self, l):
         return self._xyr(self.lib.oc_level_octree, l)
+
+    STAGES = ("pyramid", "fast", "octree", "orientation", "blur", "descriptor")
+
+    def stage_times(self):
+        """accumulated seconds per stage over all calls, and the number of frames"""
+        sec = (C.c_double * 6)()
+        nf = C.c_int()
+        self.lib.oc_stage_times(self.h, sec, C.byref(nf))
+        return dict(zip(self.STAGES, list(sec))), nf.value
 
     def tables(self):
         L = self.nlevels

@@ -10,11 +10,13 @@
  * Citations are to files under /root/reference/ORB_SLAM2/src (identical to ORB_SLAM2.1).
  * Build: -O2 -ffp-contract=off (no FMA contraction: the pinned float semantics).
  */
+#define _POSIX_C_SOURCE 199309L /* clock_gettime for the stage timers */
 #include "orb_oracle.h"
 
 #include <float.h>
 #include <math.h>
 #include <stdlib.h>
+#include <time.h>
 #include <string.h>
 
 #include "orb_pattern_data.h"
@@ -581,7 +583,16 @@ struct oc_extractor {
     int ncand[MAXL], capcand[MAXL];
     okey* oct[MAXL];
     int noct[MAXL];
+    /* per-stage wall time (bench.py's CPU breakdown): pyramid, FAST, octree, orientation, blur, descriptor */
+    double stage_s[6];
+    int stage_frames;
 };
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 /* ORBextractor::ORBextractor (ORBextractor.cc:410-470) */
 oc_extractor* oc_create(const orbx_params* p) {
@@ -665,6 +676,7 @@ static void compute_keypoints_octtree(oc_extractor* e) {
         const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
         const uint8_t* img = e->pyr[level];
         const size_t step = (size_t)e->lw[level];
+        const double t_fast = now_s();
         for (int i = 0; i < nRows; i++) {
             const float iniY = (float)(minBorderY + i * hCell);
             float maxY = iniY + hCell + 6;
@@ -689,6 +701,8 @@ static void compute_keypoints_octtree(oc_extractor* e) {
                              cell[3 * k + 2]);
             }
         }
+        const double t_oct = now_s();
+        e->stage_s[1] += t_oct - t_fast;
         e->oct[level] = (okey*)malloc(sizeof(okey) * (size_t)(e->ncand[level] + 1));
         e->noct[level] = e->ncand[level] == 0
                              ? 0
@@ -699,6 +713,7 @@ static void compute_keypoints_octtree(oc_extractor* e) {
             e->oct[level][k].x += minBorderX;
             e->oct[level][k].y += minBorderY;
         }
+        e->stage_s[2] += now_s() - t_oct;
     }
     free(cell);
 }
@@ -709,6 +724,7 @@ int oc_extract(oc_extractor* e, const uint8_t* img, int w, int h, size_t pitch, 
     *n = 0;
     if (w <= 0 || h <= 0 || !img) return 0;
     free_frame(e);
+    double t0 = now_s();
     /* ComputePyramid (ORBextractor.cc:1107-1132); padded borders are never read. */
     for (int level = 0; level < e->nlevels; ++level) {
         float scale = e->inv_scale[level];
@@ -723,6 +739,7 @@ int oc_extract(oc_extractor* e, const uint8_t* img, int w, int h, size_t pitch, 
                              (size_t)e->lw[level - 1], e->pyr[level], sw, sh, (size_t)sw);
         }
     }
+    e->stage_s[0] += now_s() - t0;
     compute_keypoints_octtree(e);
     int total = 0;
     for (int level = 0; level < e->nlevels; ++level) total += e->noct[level];
@@ -732,12 +749,24 @@ int oc_extract(oc_extractor* e, const uint8_t* img, int w, int h, size_t pitch, 
         const int nl = e->noct[level];
         if (nl == 0) continue;
         const int lw = e->lw[level], lh = e->lh[level];
+        /* computeOrientation (ORBextractor.cc:851-852) runs before the per-level blur + describe
+         * loop in the reference; the two per-keypoint loops are independent, so timing them
+         * separately does not change any output */
+        t0 = now_s();
+        for (int k = 0; k < nl; k++) {
+            const okey* kp = &e->oct[level][k];
+            kps[offset + k].angle = ic_angle(e->pyr[level], (size_t)lw, kp->x, kp->y, e->umax);
+        }
+        double t1 = now_s();
+        e->stage_s[3] += t1 - t0;
         e->blur[level] = (uint8_t*)malloc((size_t)lw * lh);
         oc_gauss7(e->pyr[level], lw, lh, (size_t)lw, e->blur[level], (size_t)lw);
+        t0 = now_s();
+        e->stage_s[4] += t0 - t1;
         const float scaledPatchSize = (float)(int)(PATCH_SIZE * e->scale[level]);
         for (int k = 0; k < nl; k++) {
             const okey* kp = &e->oct[level][k];
-            float ang = ic_angle(e->pyr[level], (size_t)lw, kp->x, kp->y, e->umax);
+            const float ang = kps[offset + k].angle;
             orb_descriptor(kp->x, kp->y, ang, e->blur[level], (size_t)lw, desc + 32 * (offset + k));
             orbx_kp* o = &kps[offset + k];
             o->x = kp->x;
@@ -751,10 +780,17 @@ int oc_extract(oc_extractor* e, const uint8_t* img, int w, int h, size_t pitch, 
             o->response = kp->r;
             o->octave = level;
         }
+        e->stage_s[5] += now_s() - t0;
         offset += nl;
     }
+    e->stage_frames++;
     *n = total;
     return 0;
+}
+
+void oc_stage_times(const oc_extractor* e, double* sec6, int* nframes) {
+    for (int i = 0; i < 6; i++) sec6[i] = e->stage_s[i];
+    *nframes = e->stage_frames;
 }
 
 int oc_level_size(const oc_extractor* e, int level, int* w, int* h) {

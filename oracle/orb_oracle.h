@@ -32,6 +32,10 @@ void oc_destroy(oc_extractor* e);
 int oc_extract(oc_extractor* e, const uint8_t* img, int w, int h, size_t pitch, orbx_kp* kps,
                uint8_t* desc, int cap, int* n);
 
+/* accumulated per-stage wall time over all oc_extract calls of this extractor (seconds):
+ * pyramid, FAST, octree, orientation, blur, descriptor; for bench.py's CPU breakdown */
+void oc_stage_times(const oc_extractor* e, double* sec6, int* nframes);
+
 /* stage access for stage-isolated parity tests (valid after oc_extract) */
 int oc_level_size(const oc_extractor* e, int level, int* w, int* h);
 const uint8_t* oc_pyramid(const oc_extractor* e, int level);
