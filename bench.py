@@ -245,7 +245,21 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    # 3) extract-only and match-only rates, untimed breakdown passes
+    # 3) extract-only and match-only rates, untimed breakdown passes; and the box's
+    # measured device-to-device copy bandwidth (read + write bytes of a 1 GiB copy) beside the nominal peak
+    copy_gbs = None
+    if rank == 0:
+        a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        b2 = torch.empty_like(a)
+        b2.copy_(a)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record()
+        for _ in range(5):
+            b2.copy_(a)
+        c1.record()
+        torch.cuda.synchronize()
+        copy_gbs = 2.0 * 5 * (1 << 30) / (c0.elapsed_time(c1) * 1e-3) / 1e9
+        del a, b2
     extract_fps = B * args.steps / run_part(args.steps, match=False, xchg=False)
     match_pps = B * args.steps / run_part(args.steps, extract=False, xchg=False)
     nkp = float(sum(pp.counts.float().mean().item() for pp in pipes) / P)
@@ -289,7 +303,9 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "algorithmic_bytes_per_launch": per_stage[dom] * sub,
-                         "launch_ms": round(dom_ms, 4)},
+                         "launch_ms": round(dom_ms, 4),
+                         "measured_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
+                         "frac_vs_copy": round(achieved / copy_gbs, 5) if copy_gbs else None},
             # what actually bounds these byte/integer kernels: vector-instruction issue
             # (wave64 VALU op = 2 cycles on a SIMD-32; 1024 SIMDs at 2.4 GHz)
             "valu_issue": None if not valu_insts else {
