@@ -8,6 +8,7 @@ g++ -std=c++14 -O1 -Wall -Wno-unused-function \
   "$R/tests/cpp/test_dropin.cpp" "$R/cooperative-orb-slam_amd/host/ORBextractor.cc" \
   "$R/cooperative-orb-slam_amd/host/ORBmatcher_amd.cc" "$R/cooperative-orb-slam_amd/host/ORBmatcher_base_amd.cc" \
   "$R/cooperative-orb-slam_amd/host/ORBmatcher_projection_amd.cc" "$R/cooperative-orb-slam_amd/host/Frame_stereo_amd.cc" \
+  "$R/cooperative-orb-slam_amd/host/MapPoint_distinctive_amd.cc" "$R/cooperative-orb-slam_amd/host/Frame_bow_amd.cc" \
   -L "$R/cooperative-orb-slam_amd/lib" -lorbamd -L "$R/oracle/build" -lorb_oracle \
   -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,"$R/oracle/build" -Wl,-rpath,/opt/rocm/lib \
   -o "$R/tests/cpp/build/test_dropin"

@@ -10,6 +10,9 @@ public:
     std::vector<cv::KeyPoint> mvKeys, mvKeysUn, mvKeysRight;
     cv::Mat mDescriptors, mDescriptorsRight;
     DBoW2::FeatureVector mFeatVec;
+    DBoW2::BowVector mBowVec;
+    ORBVocabulary* mpORBvocabulary = nullptr;
+    void ComputeBoW();
     std::vector<float> mvScaleFactors, mvInvScaleFactors, mvLevelSigma2;
     std::vector<float> mvuRight, mvDepth;
     std::vector<MapPoint*> mvpMapPoints;

@@ -6,8 +6,10 @@
 #include <opencv2/features2d/features2d.hpp>
 #include <vector>
 #include "MapPoint.h"
+#include "ORBVocabulary.h"
 namespace DBoW2 {
 typedef std::map<unsigned int, std::vector<unsigned int> > FeatureVector;
+typedef std::map<unsigned int, double> BowVector;
 }
 namespace ORB_SLAM2 {
 class KeyFrame {
@@ -22,6 +24,11 @@ public:
     std::vector<float> mvuRight;
     cv::Mat mDescriptors;
     DBoW2::FeatureVector mFeatVec;
+    DBoW2::BowVector mBowVec;
+    ORBVocabulary* mpORBvocabulary = nullptr;
+    bool mbBad = false;
+    bool isBad() { return mbBad; }
+    void ComputeBoW();
     std::vector<float> mvScaleFactors, mvLevelSigma2;
     std::vector<MapPoint*> mvpMapPoints;
     cv::Mat Rcw, tcw, Ow;

@@ -3,11 +3,27 @@
  * (mfMinDistance / mfMaxDistance are private in the reference). */
 #ifndef MAPPOINT_H
 #define MAPPOINT_H
+#include <map>
+#include <mutex>
+#include <vector>
 #include <opencv2/core/core.hpp>
 namespace ORB_SLAM2 {
+class KeyFrame;
 class MapPoint {
 public:
     bool bad = false;
+    bool& mbBad = bad;  // the reference's flag behind isBad()
+    std::map<KeyFrame*, size_t> mObservations;
+    std::mutex mMutexFeatures;
+    MapPoint() = default;
+    MapPoint(const MapPoint& o)
+        : bad(o.bad), mObservations(o.mObservations), nObs(o.nObs), mWorldPos(o.mWorldPos),
+          mNormalVector(o.mNormalVector), mDescriptor(o.mDescriptor), mfMinDistance(o.mfMinDistance),
+          mfMaxDistance(o.mfMaxDistance), mbTrackInView(o.mbTrackInView), mTrackProjX(o.mTrackProjX),
+          mTrackProjY(o.mTrackProjY), mTrackProjXR(o.mTrackProjXR), mTrackViewCos(o.mTrackViewCos),
+          mnTrackScaleLevel(o.mnTrackScaleLevel) {}
+    void ComputeDistinctiveDescriptors();
+    static void ComputeDistinctiveDescriptorsBatch(const std::vector<MapPoint*>& vpMPs);
     int nObs = 1;
     cv::Mat mWorldPos, mNormalVector, mDescriptor;
     float mfMinDistance = 0, mfMaxDistance = 0;

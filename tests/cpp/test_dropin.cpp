@@ -13,6 +13,7 @@
 #include "ORBmatcher.h"
 #include "orb_oracle.h"
 #include "orbslam_amd.h"
+#include "ORBVocabulary_amd.h"
 
 using namespace ORB_SLAM2;
 
@@ -382,6 +383,137 @@ int main() {
               kept, ok);
         oc_destroy(ol);
         oc_destroy(orr);
+    }
+    // ---- MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307): single and batched
+    {
+        const int NKF = 12, NP = 300;
+        std::vector<KeyFrame> kfs(NKF);
+        uint32_t s = 4242;
+        for (int k = 0; k < NKF; k++) {
+            kfs[k].mDescriptors = cv::Mat(64, 32, CV_8U);
+            for (int i = 0; i < 64 * 32; i++) kfs[k].mDescriptors.data[i] = (uint8_t)(lcg(s) & 0xFF);
+            kfs[k].mbBad = k == 5;  // its rows are skipped
+        }
+        std::vector<MapPoint> mps(NP);
+        std::vector<MapPoint*> vp(NP);
+        std::vector<int32_t> off(1, 0);
+        std::vector<uint8_t> od;
+        std::vector<int> has(NP, 0);
+        for (int p = 0; p < NP; p++) {
+            MapPoint& m = mps[p];
+            vp[p] = &m;
+            m.mDescriptor = cv::Mat(1, 32, CV_8U);
+            memset(m.mDescriptor.data, 0xEE, 32);
+            m.bad = p % 37 == 0;
+            const int nobs = (int)(lcg(s) % 14);  // 0 .. 13 observations
+            for (int o = 0; o < nobs; o++) m.mObservations[&kfs[lcg(s) % NKF]] = lcg(s) % 64;
+            // oracle input: the same gathering, done independently
+            const size_t before = od.size();
+            if (!m.bad)
+                for (auto& ob : m.mObservations)
+                    if (!ob.first->mbBad) {
+                        const unsigned char* r = ob.first->mDescriptors.ptr<unsigned char>((int)ob.second);
+                        od.insert(od.end(), r, r + 32);
+                    }
+            if (od.size() > before) { has[p] = (int)off.size(); off.push_back((int32_t)(od.size() / 32)); }
+        }
+        std::vector<int32_t> ob(off.size() - 1);
+        oc_compute_distinctive_descriptors((int)ob.size(), off.data(), od.data(), ob.data());
+        mps[1].ComputeDistinctiveDescriptors();
+        MapPoint::ComputeDistinctiveDescriptorsBatch(vp);
+        int diff = 0, untouched = 0;
+        for (int p = 0; p < NP; p++) {
+            if (!has[p]) {
+                for (int b = 0; b < 32; b++) diff += mps[p].mDescriptor.data[b] != 0xEE;
+                untouched++;
+                continue;
+            }
+            const int q = has[p] - 1;
+            diff += memcmp(mps[p].mDescriptor.data, od.data() + 32 * (off[q] + ob[q]), 32) != 0;
+        }
+        CHECK(diff == 0 && untouched > 0 && untouched < NP, "ComputeDistinctiveDescriptors: %d diffs (%d untouched)", diff,
+              untouched);
+    }
+    // ---- Frame::ComputeBoW / KeyFrame::ComputeBoW (Frame.cc:396-403, KeyFrame.cc:60-69) on a synthetic
+    // vocabulary (k = 6, L = 4, breadth-first node lines) registered for a stand-in ORBVocabulary
+    {
+        const int k = 6, L = 4;
+        std::vector<int32_t> parent;
+        std::vector<uint8_t> leaf, vdesc;
+        std::vector<double> weight;
+        uint32_t s = 99;
+        std::vector<std::pair<int, int> > frontier(1, std::make_pair(0, 0));  // (node id, depth)
+        std::vector<std::vector<uint8_t> > nd(1, std::vector<uint8_t>(32));
+        for (auto& b : nd[0]) b = (uint8_t)(lcg(s) & 0xFF);
+        int nid = 0;
+        while (!frontier.empty()) {
+            std::vector<std::pair<int, int> > nxt;
+            for (auto& fr : frontier) {
+                if (fr.second >= L) continue;
+                for (int c = 0; c < k; c++) {
+                    std::vector<uint8_t> d = nd[fr.first];
+                    for (int b = 0; b < (fr.second ? 40 : 256); b++) {
+                        const uint32_t r = lcg(s) % 256;
+                        d[r >> 3] ^= (uint8_t)(1u << (r & 7));
+                    }
+                    nd.push_back(d);
+                    nid++;
+                    parent.push_back(fr.first);
+                    leaf.push_back(fr.second + 1 == L ? 1 : 0);
+                    vdesc.insert(vdesc.end(), d.begin(), d.end());
+                    weight.push_back(0.1 + (double)(lcg(s) % 1000) / 125.0);
+                    nxt.push_back(std::make_pair(nid, fr.second + 1));
+                }
+            }
+            frontier = nxt;
+        }
+        const int nlines = (int)parent.size();
+        for (int scoring = 0; scoring < 2; scoring++) {  // L1_NORM (ORB-SLAM2's) and L2_NORM
+            orbv_handle* h = nullptr;
+            CHECK(orbv_create(k, L, scoring, 0, nlines, parent.data(), leaf.data(), vdesc.data(), weight.data(), 0, &h) ==
+                      ORBX_OK, "orbv_create");
+            oc_vocab* ov = oc_vocab_create(k, L, scoring, 0, nlines, parent.data(), leaf.data(), vdesc.data(), weight.data());
+            ORBVocabulary voc;
+            amd::RegisterVocabulary(&voc, h);
+            Frame F;
+            F.mDescriptors = D[2];
+            F.mpORBvocabulary = &voc;
+            F.ComputeBoW();
+            KeyFrame KF;
+            KF.mDescriptors = D[1];
+            KF.mpORBvocabulary = &voc;
+            KF.ComputeBoW();
+            int bad = 0;
+            for (int which = 0; which < 2; which++) {
+                const cv::Mat& Dm = which ? D[1] : D[2];
+                const DBoW2::BowVector& bv = which ? KF.mBowVec : F.mBowVec;
+                const DBoW2::FeatureVector& fv = which ? KF.mFeatVec : F.mFeatVec;
+                const int n = Dm.rows;
+                std::vector<uint32_t> w(n), nodes(n);
+                std::vector<double> val(n);
+                std::vector<int32_t> fo(n + 1), ff(n);
+                int nb = 0, nf = 0;
+                oc_vocab_transform(ov, Dm.ptr<unsigned char>(0), n, 4, w.data(), val.data(), &nb, nodes.data(), fo.data(),
+                                   ff.data(), &nf);
+                bad += (int)bv.size() != nb || (int)fv.size() != nf;
+                int i = 0;
+                for (auto& e : bv) { bad += i >= nb || e.first != w[i] || memcmp(&e.second, &val[i], 8) != 0; i++; }
+                int j = 0;
+                for (auto& e : fv) {
+                    bad += j >= nf || e.first != nodes[j] ||
+                           e.second != std::vector<unsigned int>(ff.begin() + fo[j], ff.begin() + fo[j + 1]);
+                    j++;
+                }
+                bad += nb == 0 || nf == 0;
+            }
+            // guards: a Frame with a BowVector is not recomputed
+            F.mDescriptors = D[0];
+            const DBoW2::BowVector keep = F.mBowVec;
+            F.ComputeBoW();
+            bad += F.mBowVec != keep;
+            CHECK(bad == 0, "ComputeBoW scoring=%d: %d mismatches", scoring, bad);
+            oc_vocab_destroy(ov);
+        }
     }
     // DescriptorDistance (ORBmatcher.cc:1647-1663)
     int dd = 0;
