@@ -131,9 +131,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal hooks (defaults = the product setting): ORBAMD_DIST_BACKEND=gloo and
+    # ORBAMD_BENCH_DEVICE=0 run a multi-rank bench on a one-GPU box (tools/rehearse_ranks.sh)
+    backend = os.environ.get("ORBAMD_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("ORBAMD_BENCH_DEVICE", local))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
