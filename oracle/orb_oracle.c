@@ -8,7 +8,7 @@
  * independent statement. PARITY UNPINNED at the OpenCV boundary (see header).
  *
  * Citations are to files under /root/reference/ORB_SLAM2/src (identical to ORB_SLAM2.1).
- * Build: -O2 -ffp-contract=off (no FMA contraction: the pinned float semantics).
+ * Build: -O3 -ffp-contract=off (no FMA contraction: the pinned float semantics).
  */
 #define _POSIX_C_SOURCE 199309L /* clock_gettime for the stage timers */
 #include "orb_oracle.h"
