@@ -121,6 +121,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-exchange", action="store_true")
+    ap.add_argument("--stagger", choices=("each", "once", "none"), default="each",
+                    help="graph p starts extracting after graph p-1's extraction: every step / only in the "
+                         "first step of a run (the phase offset then persists) / never")
     args = ap.parse_args()
 
     import numpy as np
@@ -170,11 +173,11 @@ def main():
 
     done = [torch.cuda.Event() for _ in range(P)]
 
-    def step(ev=None, xev=None, extract=True, match=True, xchg=True):
+    def step(ev=None, xev=None, extract=True, match=True, xchg=True, first=True):
         for p in range(P):
             st = streams[p].cuda_stream
             if extract:
-                if p > 0:
+                if p > 0 and (args.stagger == "each" or (args.stagger == "once" and first)):
                     # staggered graphs: graph p's extraction (FAST-heavy) overlaps graph p-1's matcher and the
                     # latency-bound tail stages instead of running in lockstep with them
                     streams[p].wait_event(done[p - 1])
@@ -213,7 +216,7 @@ def main():
         torch.cuda.synchronize()
         t_start = time.perf_counter()
         for i in range(nsteps):
-            step(evs[i], xevs[i])
+            step(evs[i], xevs[i], first=i == 0)
         torch.cuda.synchronize()
         if timed and world > 1:
             dist.barrier()
@@ -238,8 +241,8 @@ def main():
         """untimed breakdown pass: wall time of nsteps steps doing only part of the work"""
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(nsteps):
-            step(**kw)
+        for i in range(nsteps):
+            step(first=i == 0, **kw)
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
