@@ -11,6 +11,8 @@
                batch) vs the CPU oracle.
   bow          Frame::ComputeBoW (DBoW2 transform, levelsup 4) of 256 extracted 640x480 frames with a synthetic
                vocabulary of ORBvoc.txt's shape (k=10, L=6, 1.1M nodes) resident in HBM, vs the CPU oracle.
+  extract_host ORBextractor::operator() through the host-buffer C ABI on one 640x480 frame per call
+               (H2D + whole pipeline + D2H): the Tracking thread's per-frame latency, vs the oracle.
 The CPU figures are the oracle (a plain-C restatement, 1 thread), not the reference build.
 """
 import json
@@ -81,6 +83,27 @@ def bench_stereo(torch, steps, B=128):
             "k_stereo_ms_per_step": round(k_ms, 4), "k_stereo_us_per_pair": round(k_ms * 1e3 / B, 3),
             "stereo_kept_per_pair": round(float(ns.float().mean().item()), 1),
             "cpu_oracle_ms_per_pair": round(tc / nc * 1e3, 3), "cpu_threads": 1}
+
+
+def bench_extract_host(reps):
+    import orbamd
+    import oracle_py
+    img = orbamd.synth_frames(0, 5, 1, 640, 480)[0]
+    ext = orbamd.ORBextractor(1000, 1.2, 8, 20, 7)
+    for _ in range(5):
+        ext(img)
+    t = time.perf_counter()
+    for _ in range(reps):
+        k, d = ext(img)
+    g = (time.perf_counter() - t) / reps
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    t = time.perf_counter()
+    for _ in range(5):
+        ko, do = orc(img)
+    c = (time.perf_counter() - t) / 5
+    assert len(k) == len(ko) and np.array_equal(d, do)
+    return {"row": "extract_single_frame_host_api", "workload": "640x480, 1000 features, one frame per call",
+            "gpu_ms_per_call": round(g * 1e3, 4), "cpu_oracle_ms_per_call": round(c * 1e3, 3), "cpu_threads": 1}
 
 
 def bench_projection(reps):
@@ -191,7 +214,8 @@ def bench_bow(torch, reps):
 def main():
     import torch
     steps = int(os.environ.get("BENCH_ROWS_STEPS", "10"))
-    for r in (bench_stereo(torch, steps), bench_projection(50), bench_distinctive(torch, 10), bench_bow(torch, 10)):
+    for r in (bench_extract_host(100), bench_stereo(torch, steps), bench_projection(50), bench_distinctive(torch, 10),
+              bench_bow(torch, 10)):
         print(json.dumps(r), flush=True)
 
 
