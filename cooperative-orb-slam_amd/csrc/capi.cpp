@@ -388,6 +388,16 @@ struct orbx_handle {
     long long last_fstride = 0;
     int last_pitch = 0, last_nframes = 0;
     bool lds_attr_set = false;
+    // host path as one captured hipGraph (orbx_extract): pinned staging in / out, replayed per frame
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    int graph_w = 0, graph_h = 0;
+    unsigned graph_epoch = 0;   // geometry / buffer epoch the graph was captured at
+    unsigned epoch = 1;         // bumped whenever ensure_geometry rebuilds or reallocates
+    int graph_warm = 0;         // eager runs at the current epoch (the first one runs uncaptured)
+    uint8_t* pin_in = nullptr;  // W*H frame
+    uint8_t* pin_out = nullptr; // {cnt, err} + K orbx_kp + K x 32 descriptors
+    size_t pin_in_bytes = 0, pin_out_bytes = 0;
     // stage profiling (orbx_profile_*)
     bool prof_on = false;
     int prof_mask = 0;  // stages with event pairs (bit k = stage k)
@@ -416,16 +426,20 @@ static int prof_mark(orbx_handle* h, int k, int e, hipStream_t st) {
 static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
     if (nframes < 1 || nframes > h->max_batch) return ORBX_EARG;
     if (h->geo.W != W || h->geo.H != H) {
+        h->epoch++;
         int rc = h->geo.build(h->T, W, H);
         if (rc) { h->geo.W = h->geo.H = 0; return rc; }
     }
     const ExtractParams& ep = h->geo.ep;
     const size_t B = (size_t)h->max_batch;
+    const void* before[7] = {h->pyr.p, h->blur.p, h->cellkey.p, h->cellcnt.p, h->lvkey.p, h->lvcnt.p, h->gscratch.p};
     if (h->pyr.ensure(B * ep.pyr_frame_bytes) || h->blur.ensure(B * ep.blur_frame_bytes) ||
         h->cellkey.ensure(B * ep.keys_per_frame * 4) || h->cellcnt.ensure(B * ep.ncells * 4) ||
         h->lvkey.ensure(B * ep.kp_per_frame * 4) || h->lvcnt.ensure((B * ep.L + kMaxLevels) * 4) ||
         h->gscratch.ensure(B * (size_t)ep.keys_per_frame * 8) || h->err.ensure(256))
         return ORBX_EDEVICE;
+    const void* after[7] = {h->pyr.p, h->blur.p, h->cellkey.p, h->cellcnt.p, h->lvkey.p, h->lvcnt.p, h->gscratch.p};
+    if (memcmp(before, after, sizeof(before))) h->epoch++;
     if (h->geo.lds_bytes > 64 * 1024 && !h->lds_attr_set) {
         HIPR(octree_setup(h->geo.lds_bytes));
         h->lds_attr_set = true;
@@ -598,6 +612,10 @@ void orbx_destroy(orbx_handle* h) {
     for (hipEvent_t e : {h->ev_fork, h->ev_pyr, h->ev_blur})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
+    if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+    if (h->graph) (void)hipGraphDestroy(h->graph);
+    if (h->pin_in) (void)hipHostFree(h->pin_in);
+    if (h->pin_out) (void)hipHostFree(h->pin_out);
     delete h;
 }
 
@@ -672,6 +690,95 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
                        (hipStream_t)stream);
 }
 
+/* The captured host path: pinned H2D -> run_extract -> one pinned D2H of {count, error flag, K
+ * keypoints, K descriptors}, as one hipGraph per geometry (replayed: no per-kernel launch cost on
+ * the calling thread, one synchronisation per frame). The first call at a new geometry/buffer epoch
+ * runs eagerly (it also performs one-time setup such as LDS attributes), the next one captures. */
+static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int height, size_t pitch, orbx_kp* kps,
+                         uint8_t* desc, int cap, int* n) {
+    const int K = h->geo.ep.kp_per_frame;
+    const size_t in_bytes = (size_t)width * height;
+    const size_t out_bytes = 64 + (sizeof(orbx_kp) + 32) * (size_t)K;
+    if (h->pin_in_bytes < in_bytes) {
+        if (h->pin_in) (void)hipHostFree(h->pin_in);
+        h->pin_in = nullptr;
+        h->pin_in_bytes = 0;
+        HIPR(hipHostMalloc((void**)&h->pin_in, in_bytes, hipHostMallocDefault));
+        h->pin_in_bytes = in_bytes;
+        h->epoch++;
+    }
+    if (h->pin_out_bytes < out_bytes) {
+        if (h->pin_out) (void)hipHostFree(h->pin_out);
+        h->pin_out = nullptr;
+        h->pin_out_bytes = 0;
+        HIPR(hipHostMalloc((void**)&h->pin_out, out_bytes, hipHostMallocDefault));
+        h->pin_out_bytes = out_bytes;
+        h->epoch++;
+    }
+    for (int y = 0; y < height; y++) memcpy(h->pin_in + (size_t)y * width, img + (size_t)y * pitch, width);
+    uint8_t* o_kps = h->pin_out + 64;
+    uint8_t* o_desc = o_kps + sizeof(orbx_kp) * (size_t)K;
+    auto enqueue = [&]() -> int {
+        HIPR(hipMemcpyAsync(h->in_frame.p, h->pin_in, in_bytes, hipMemcpyHostToDevice, h->stream));
+        int rc = run_extract(h, 1, h->in_frame.as<uint8_t>(), (long long)in_bytes, width, h->out_kps.as<orbx_kp>(),
+                             h->out_desc.as<uint8_t>(), h->out_cnt.as<int32_t>(), K, h->stream);
+        if (rc) return rc;
+        HIPR(hipMemcpyAsync(h->pin_out, h->out_cnt.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+        HIPR(hipMemcpyAsync(h->pin_out + 4, h->err.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+        HIPR(hipMemcpyAsync(o_kps, h->out_kps.p, sizeof(orbx_kp) * (size_t)K, hipMemcpyDeviceToHost, h->stream));
+        HIPR(hipMemcpyAsync(o_desc, h->out_desc.p, 32 * (size_t)K, hipMemcpyDeviceToHost, h->stream));
+        return 0;
+    };
+    const bool valid = h->gexec && h->graph_w == width && h->graph_h == height && h->graph_epoch == h->epoch;
+    if (!valid) {
+        if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+        if (h->graph) (void)hipGraphDestroy(h->graph);
+        h->gexec = nullptr;
+        h->graph = nullptr;
+        if (h->graph_epoch != h->epoch || h->graph_w != width || h->graph_h != height) h->graph_warm = 0;
+        h->graph_w = width;
+        h->graph_h = height;
+        h->graph_epoch = h->epoch;
+    }
+    if (!h->gexec && h->graph_warm == 0) {
+        // first frame at this epoch: eager
+        int rc = enqueue();
+        if (rc) return rc;
+        h->graph_warm = 1;
+    } else {
+        if (!h->gexec) {
+            HIPR(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+            int rc = enqueue();
+            hipGraph_t g = nullptr;
+            const hipError_t ce = hipStreamEndCapture(h->stream, &g);
+            if (rc) {
+                if (g) (void)hipGraphDestroy(g);
+                return rc;
+            }
+            HIPR(ce);
+            h->graph = g;
+            HIPR(hipGraphInstantiate(&h->gexec, h->graph, nullptr, nullptr, 0));
+        }
+        HIPR(hipGraphLaunch(h->gexec, h->stream));
+    }
+    HIPR(hipStreamSynchronize(h->stream));
+    h->last_frames = h->in_frame.as<uint8_t>();
+    h->last_fstride = (long long)in_bytes;
+    h->last_pitch = width;
+    h->last_nframes = 1;
+    int cnt = 0, errflag = 0;
+    memcpy(&cnt, h->pin_out, sizeof(int));
+    memcpy(&errflag, h->pin_out + 4, sizeof(int));
+    if (errflag) return ORBX_EDEVICE;
+    if (cnt > cap) return ORBX_ECAPACITY;
+    if (cnt > 0) {
+        if (kps) memcpy(kps, o_kps, sizeof(orbx_kp) * (size_t)cnt);
+        if (desc) memcpy(desc, o_desc, 32 * (size_t)cnt);
+    }
+    *n = cnt;
+    return 0;
+}
+
 int orbx_extract(orbx_handle* h, const uint8_t* img, int width, int height, size_t pitch, orbx_kp* kps,
                  uint8_t* desc, int cap, int* n) {
     if (!h || !n) return ORBX_EARG;
@@ -682,9 +789,14 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int width, int height, size
     int rc = ensure_geometry(h, width, height, 1);
     if (rc) return rc;
     const int K = h->geo.ep.kp_per_frame;
+    const void* before[4] = {h->in_frame.p, h->out_kps.p, h->out_desc.p, h->out_cnt.p};
     if (h->in_frame.ensure((size_t)width * height) || h->out_kps.ensure(sizeof(orbx_kp) * K) ||
         h->out_desc.ensure(32 * (size_t)K) || h->out_cnt.ensure(64))
         return ORBX_EDEVICE;
+    const void* after[4] = {h->in_frame.p, h->out_kps.p, h->out_desc.p, h->out_cnt.p};
+    if (memcmp(before, after, sizeof(before))) h->epoch++;
+    static const bool no_graph = getenv("ORBX_NO_GRAPH") != nullptr;
+    if (!no_graph && !h->prof_on) return extract_graph(h, img, width, height, pitch, kps, desc, cap, n);
     HIPR(hipMemcpy2DAsync(h->in_frame.p, width, img, pitch, width, height, hipMemcpyHostToDevice, h->stream));
     rc = run_extract(h, 1, h->in_frame.as<uint8_t>(), (long long)width * height, width, h->out_kps.as<orbx_kp>(),
                      h->out_desc.as<uint8_t>(), h->out_cnt.as<int32_t>(), K, h->stream);
