@@ -161,14 +161,20 @@ def main():
     xmatch = torch.empty((world, pipe.stride), dtype=torch.int32, device=dev)
     xn = torch.zeros(world, dtype=torch.int32, device=dev)
 
-    def exchange():
+    ag_events = []  # (start, end) around the all-gather alone, timed steps only
+
+    def exchange(ag=None):
         # this agent's latest keyframe -> RCCL all-gather -> match against every agent's slot
         with torch.cuda.stream(streams[0]):
             pipe.pack(0, my_slot, streams[0].cuda_stream)
+            if ag is not None:
+                ag[0].record(streams[0])
             if world > 1:
                 dist.all_gather_into_tensor(all_slots, my_slot)
             else:
                 all_slots.copy_(my_slot)
+            if ag is not None:
+                ag[1].record(streams[0])
             pipe.match_packed(0, all_slots, world, xmatch, xn, streams[0].cuda_stream)
 
     done = [torch.cuda.Event() for _ in range(P)]
@@ -192,7 +198,11 @@ def main():
         if xchg and not args.no_exchange:
             if xev is not None:
                 xev[0].record(streams[0])
-            exchange()
+            ag = None
+            if xev is not None:
+                ag = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ag_events.append(ag)
+            exchange(ag)
             if xev is not None:
                 xev[1].record(streams[0])
 
@@ -235,6 +245,8 @@ def main():
         st["match"] = sum(e[p][0].elapsed_time(e[p][1]) for e in evs for p in range(P)) / (nsteps * P)
         if not args.no_exchange:
             st["exchange"] = sum(x[0].elapsed_time(x[1]) for x in xevs) / nsteps
+            st["allgather"] = sum(a.elapsed_time(b) for a, b in ag_events) / max(len(ag_events), 1)
+            ag_events.clear()
         return elapsed, st
 
     def run_part(nsteps, **kw):
@@ -324,6 +336,7 @@ def main():
             "pipeline_hbm": {"bytes_per_frame": b_frame, "achieved_GBs": round(b_frame * value / world / 1e9, 2),
                              "frac": round(b_frame * value / world / 1e9 / HBM_PEAK_GBS, 5)},
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
+            "per_gpu_frames_per_s": round(value / world, 2),
             "extract_only_frames_per_s_per_gpu": round(extract_fps, 1),
             "match_only_pairs_per_s_per_gpu": round(match_pps, 1),
             "kp_per_frame": round(nkp, 1),
