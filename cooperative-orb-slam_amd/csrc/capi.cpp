@@ -1279,6 +1279,30 @@ int orbm_triangulation_bf_batch_device(orbm_ctx* ctx, int npairs, const int32_t*
     return 0;
 }
 
+int orbm_triangulation_nodes_batch_device(orbm_ctx* ctx, int npairs, const int32_t* d_q1, const int32_t* d_q2,
+                                          const orbx_kp* d_kps, const uint8_t* d_desc, const int32_t* d_counts,
+                                          int kp_stride, const uint32_t* d_fv_node, const int32_t* d_fv_off,
+                                          const int32_t* d_fv_feat, const int32_t* d_nfv, int max_nodes,
+                                          const float F12[9], float ex, float ey, int nlevels,
+                                          const float* scale_factors, const float* level_sigma2, int check_ori,
+                                          int32_t* d_match12, int32_t* d_nmatches, void* stream) {
+    if (!ctx || npairs < 0 || !F12 || nlevels < 1 || nlevels > 16 || !scale_factors || !level_sigma2 ||
+        kp_stride < 1 || max_nodes < 0 || max_nodes > kp_stride)
+        return ORBX_EARG;
+    if (npairs == 0) return 0;
+    HIPR(hipSetDevice(ctx->device));
+    MatchGeom g;
+    make_geom(g, F12, ex, ey, nlevels, scale_factors, level_sigma2);
+    hipStream_t st = (hipStream_t)stream;
+    HIPR(hipMemsetAsync(d_match12, 0xFF, sizeof(int32_t) * (size_t)npairs * kp_stride, st));
+    HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * npairs, st));
+    HIPR(launch_tri_nodes_pairs(npairs, max_nodes, d_q1, d_q2, d_kps, d_desc, kp_stride, d_fv_node, d_fv_off,
+                                d_fv_feat, d_nfv, g, d_match12, d_nmatches, st));
+    if (check_ori)
+        HIPR(launch_rot_filter_pairs(npairs, d_q1, d_q2, d_kps, d_counts, kp_stride, d_match12, d_nmatches, st));
+    return 0;
+}
+
 int orbm_triangulation_bf_packed_device(orbm_ctx* ctx, const orbx_kp* d_kps1, const uint8_t* d_desc1,
                                         const int32_t* d_count1, int nref, const uint8_t* d_slots,
                                         size_t slot_bytes, const float F12[9], float ex, float ey, int nlevels,

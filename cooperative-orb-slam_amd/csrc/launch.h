@@ -41,6 +41,10 @@ hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0,
 hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
                          int32_t* nmatches, hipStream_t st);
+hipError_t launch_tri_nodes_pairs(int npairs, int max_nodes, const int32_t* q1, const int32_t* q2, const orbx_kp* kps,
+                                  const uint8_t* desc, int kp_stride, const uint32_t* fv_node, const int32_t* fv_off,
+                                  const int32_t* fv_feat, const int32_t* nfv, const MatchGeom& g, int32_t* match12,
+                                  int32_t* nmatches, hipStream_t st);
 hipError_t launch_rot_filter_pairs(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps,
                                    const int32_t* counts, int kp_stride, int32_t* match12, int32_t* nmatches,
                                    hipStream_t st);

@@ -6,6 +6,7 @@
  *                     KF2 tile staged in LDS, descriptors compared as 8 x u32 XOR+popcount
  *                     (v_bcnt_u32_b32) -- ORBmatcher.cc:657-823, 1647-1663.
  *   k_tri_nodes       SearchForTriangulation over common BoW nodes (general form).
+ *   k_tri_nodes_pairs the same for a batch of frame pairs, FeatureVectors on the device.
  *   k_bow             SearchByBoW(KF,F) / SearchByBoW(KF,KF): per common node, greedy over the
  *                     node's queries in order, wave-parallel best/second-best over candidates
  *                     (ORBmatcher.cc:159-288, 522-655).
@@ -403,6 +404,70 @@ __global__ __launch_bounds__(64) void k_tri_nodes(const DevView v1, const DevVie
 }
 
 /* ----------------------------------------------------------------------------------- */
+/* SearchForTriangulation over common BoW nodes for a batch of frame pairs, with the       */
+/* FeatureVectors of orbv_transform_batch_device (levelsup nodes) left on the device:       */
+/* block (i, p) takes node i of KF1 = frame q1[p]; its partner in KF2 = frame q2[p] is      */
+/* found by binary search over KF2's ascending node ids (the reference's merge walk,        */
+/* ORBmatcher.cc:691-789, visits exactly the common ids). One lane per query of the node,   */
+/* candidates scanned in node order with the reference's rule (dist > TH_LOW or > best:     */
+/* skip; epipole radius and CheckDistEpipolarLine; accept = new best, ties to the later).   */
+/* All keypoints mono, no MapPoints (the batch configuration of k_tri_mfma).               */
+/* ----------------------------------------------------------------------------------- */
+__global__ __launch_bounds__(64) void k_tri_nodes_pairs(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
+                                                        const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
+                                                        int kp_stride, const uint32_t* __restrict__ fv_node,
+                                                        const int32_t* __restrict__ fv_off,
+                                                        const int32_t* __restrict__ fv_feat,
+                                                        const int32_t* __restrict__ nfv, MatchGeom g,
+                                                        int32_t* __restrict__ match12, int32_t* __restrict__ nmatches) {
+    const int p = blockIdx.y, i = blockIdx.x;
+    const int f1 = q1[p], f2 = q2[p];
+    if (i >= nfv[f1]) return;
+    const uint32_t* nodes2 = fv_node + (long long)f2 * kp_stride;
+    const uint32_t node = fv_node[(long long)f1 * kp_stride + i];
+    int lo = 0, hi = nfv[f2];
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (nodes2[mid] < node) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo >= nfv[f2] || nodes2[lo] != node) return;  // not a common node: its queries stay -1
+    const int32_t* off1 = fv_off + (long long)f1 * (kp_stride + 1);
+    const int32_t* off2 = fv_off + (long long)f2 * (kp_stride + 1);
+    const int32_t* feat1 = fv_feat + (long long)f1 * kp_stride;
+    const int32_t* feat2 = fv_feat + (long long)f2 * kp_stride;
+    const orbx_kp* k1 = kps + (long long)f1 * kp_stride;
+    const orbx_kp* k2 = kps + (long long)f2 * kp_stride;
+    const uint8_t* d1 = desc + (long long)f1 * kp_stride * 32;
+    const uint8_t* d2 = desc + (long long)f2 * kp_stride * 32;
+    const int cb = off2[lo], ce = off2[lo + 1];
+    for (int qi = off1[i] + (int)threadIdx.x; qi < off1[i + 1]; qi += 64) {
+        const int idx1 = feat1[qi];
+        uint32_t q[8];
+        const uint4* qd = (const uint4*)(d1 + (long long)idx1 * 32);
+        const uint4 qa = qd[0], qb = qd[1];
+        q[0] = qa.x; q[1] = qa.y; q[2] = qa.z; q[3] = qa.w; q[4] = qb.x; q[5] = qb.y; q[6] = qb.z; q[7] = qb.w;
+        const orbx_kp kp1 = k1[idx1];
+        float a, b, c;
+        epi_line(g, kp1.x, kp1.y, &a, &b, &c);
+        int bestDist = 50, bestIdx2 = -1;  // TH_LOW (ORBmatcher.cc:704)
+        for (int ci = cb; ci < ce; ci++) {
+            const int idx2 = feat2[ci];
+            const int dist = hamming8(q, (const uint32_t*)(d2 + (long long)idx2 * 32));
+            if (dist > 50 || dist > bestDist) continue;
+            const orbx_kp kp2 = k2[idx2];
+            if (near_epipole(g, kp2.x, kp2.y, kp2.octave)) continue;  // mono-mono (:743-749)
+            if (epi_ok(a, b, c, kp2.x, kp2.y, g.th384[kp2.octave])) {
+                bestIdx2 = idx2;
+                bestDist = dist;
+            }
+        }
+        match12[(long long)p * kp_stride + idx1] = bestIdx2;
+        if (bestIdx2 >= 0) atomicAdd(&nmatches[p], 1);
+    }
+}
+
+/* ----------------------------------------------------------------------------------- */
 /* SearchByBoW: one wave per common node. Queries of node1 in order (greedy exclusion of */
 /* already-matched candidates is node-local); per query the wave computes best/second   */
 /* best over node2 with the sequential scan's semantics: best1 = first strict minimum,   */
@@ -595,6 +660,16 @@ hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const
         hipLaunchKernelGGL(k_tri_bf<1>, grid, dim3(256), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
                            nmatches);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_tri_nodes_pairs(int npairs, int max_nodes, const int32_t* q1, const int32_t* q2, const orbx_kp* kps,
+                                  const uint8_t* desc, int kp_stride, const uint32_t* fv_node, const int32_t* fv_off,
+                                  const int32_t* fv_feat, const int32_t* nfv, const MatchGeom& g, int32_t* match12,
+                                  int32_t* nmatches, hipStream_t st) {
+    if (npairs == 0 || max_nodes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tri_nodes_pairs, dim3(max_nodes, npairs), dim3(64), 0, st, q1, q2, kps, desc, kp_stride,
+                       fv_node, fv_off, fv_feat, nfv, g, match12, nmatches);
     return hipGetLastError();
 }
 

@@ -79,6 +79,36 @@ class BatchPipeline:
             self.scale.ctypes.data, self.sigma2.ctypes.data, self.check_ori, self.match.data_ptr(),
             self.nmatch.data_ptr(), st), "orbm_triangulation_bf_batch_device")
 
+    def bow(self, vocabulary, levelsup=4, stream=None):
+        """Frame::ComputeBoW of every extracted frame on the device (orbv_transform_batch_device); the
+        FeatureVectors stay in self.fv_node / fv_off / fv_feat / nfv for match_pairs_nodes."""
+        torch, dev, B, S = self.torch, self.dev, self.B, self.stride
+        if getattr(self, "_bow_bufs", None) is None:
+            z = lambda *sh, dt=torch.int32: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
+            self.word, self.word_w, self.word_nid = z(B, S), z(B, S, dt=torch.float64), z(B, S)
+            self.bow_word, self.bow_val, self.nbow = z(B, S), z(B, S, dt=torch.float64), z(B)
+            self.fv_node, self.fv_off, self.fv_feat, self.nfv = z(B, S), z(B, S + 1), z(B, S), z(B)
+            self._bow_bufs = True
+        st = self.stream_ptr() if stream is None else stream
+        check(self.lib.orbv_transform_batch_device(
+            vocabulary._h, B, self.desc.data_ptr(), self.counts.data_ptr(), S, levelsup, self.word.data_ptr(),
+            self.word_w.data_ptr(), self.word_nid.data_ptr(), self.bow_word.data_ptr(), self.bow_val.data_ptr(),
+            self.nbow.data_ptr(), self.fv_node.data_ptr(), self.fv_off.data_ptr(), self.fv_feat.data_ptr(),
+            self.nfv.data_ptr(), st), "orbv_transform_batch_device")
+        info = vocabulary.info()
+        self.max_nodes = int(min(S, info["k"] ** max(info["L"] - levelsup, 0)))
+
+    def match_pairs_nodes(self, stream=None):
+        """SearchForTriangulation over the common BoW nodes of each pair (after bow())."""
+        st = self.stream_ptr() if stream is None else stream
+        F = np.ascontiguousarray(self.F12.reshape(9))
+        check(self.lib.orbm_triangulation_nodes_batch_device(
+            self.mh, self.B, self.q1.data_ptr(), self.q2.data_ptr(), self.kps.data_ptr(), self.desc.data_ptr(),
+            self.counts.data_ptr(), self.stride, self.fv_node.data_ptr(), self.fv_off.data_ptr(),
+            self.fv_feat.data_ptr(), self.nfv.data_ptr(), self.max_nodes, F.ctypes.data, self.ex, self.ey,
+            len(self.scale), self.scale.ctypes.data, self.sigma2.ctypes.data, self.check_ori, self.match.data_ptr(),
+            self.nmatch.data_ptr(), st), "orbm_triangulation_nodes_batch_device")
+
     def step(self, frames, stream=None):
         self.extract(frames, stream)
         self.match_pairs(stream)

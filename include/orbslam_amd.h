@@ -171,6 +171,21 @@ int orbm_triangulation_bf_batch_device(orbm_ctx* ctx, int npairs, const int32_t*
                                        int nlevels, const float* scale_factors,
                                        const float* level_sigma2, int check_ori,
                                        int32_t* d_match12, int32_t* d_nmatches, void* stream);
+/* The same batch over common BoW nodes (SearchForTriangulation's own merge walk,
+ * ORBmatcher.cc:691-789, as LocalMapping::CreateNewMapPoints calls it with a real vocabulary):
+ * the FeatureVectors are orbv_transform_batch_device's device output for the same frames
+ * (fv_node / fv_feat at f*kp_stride, fv_off at f*(kp_stride+1), nfv[f]); max_nodes bounds nfv
+ * (e.g. min(kp_stride, k^(L-levelsup))). Mono, no MapPoints, as above. */
+int orbm_triangulation_nodes_batch_device(orbm_ctx* ctx, int npairs, const int32_t* d_q1,
+                                          const int32_t* d_q2, const orbx_kp* d_kps,
+                                          const uint8_t* d_desc, const int32_t* d_counts,
+                                          int kp_stride, const uint32_t* d_fv_node,
+                                          const int32_t* d_fv_off, const int32_t* d_fv_feat,
+                                          const int32_t* d_nfv, int max_nodes, const float F12[9],
+                                          float ex, float ey, int nlevels,
+                                          const float* scale_factors, const float* level_sigma2,
+                                          int check_ori, int32_t* d_match12, int32_t* d_nmatches,
+                                          void* stream);
 
 /* Cross-agent variant: one query frame (kps/desc/count on device, e.g. this rank's latest
  * keyframe) against nref reference slots packed by orbx_pack_keyframe (e.g. the RCCL

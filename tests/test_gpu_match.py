@@ -118,3 +118,40 @@ def test_batch_pairs_match_oracle():
         np.testing.assert_array_equal(mg, mo)
         assert int(pipe.nmatch[b].item()) == no
     pipe.close()
+
+
+@pytest.mark.parametrize("levelsup,check_ori", [(2, False), (1, True)])
+def test_batch_pairs_over_bow_nodes(levelsup, check_ori):
+    """Device chain extract -> ComputeBoW (orbv_transform_batch_device) -> SearchForTriangulation over
+    the common FeatureVector nodes (orbm_triangulation_nodes_batch_device) vs the oracle's
+    SearchForTriangulation with the oracle vocabulary's FeatureVectors."""
+    torch = pytest.importorskip("torch")
+    from orbamd.vocabulary import synth_vocabulary, L1_NORM, TF_IDF
+    k, L = 10, 3
+    v = synth_vocabulary(k, L, 5, flip_bits=24)
+    gv = orbamd.ORBVocabulary.from_arrays(k, L, L1_NORM, TF_IDF, *v[2:])
+    ov = oracle_py.OracleVocabulary(k, L, L1_NORM, TF_IDF, *v[2:])
+    W, H, B = 640, 480, 4
+    frames = orbamd.synth_frames(1, 7, B, W, H)
+    pipe = orbamd.device.BatchPipeline(torch, W, H, B, check_ori=check_ori)
+    pipe.extract(torch.from_numpy(frames).cuda())
+    pipe.bow(gv, levelsup)
+    pipe.match_pairs_nodes()
+    torch.cuda.synchronize()
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    tabs = orc.tables()
+    res = [orc(frames[b]) for b in range(B)]
+    fvs = [ov.transform(res[b][1], levelsup)[1] for b in range(B)]
+    total = 0
+    for b in range(B):
+        pb = (b + B - 1) % B
+        v1 = _view(res[b][0], res[b][1], tabs, feat_vec=fvs[b])
+        v2 = _view(res[pb][0], res[pb][1], tabs, feat_vec=fvs[pb])
+        no, mo = oracle_py.search_for_triangulation(v1, v2, pipe.F12, pipe.ex, pipe.ey, False, check_ori)
+        n = len(res[b][0])
+        mg = pipe.match[b, :n].cpu().numpy()
+        np.testing.assert_array_equal(mg, mo)
+        assert int(pipe.nmatch[b].item()) == no
+        total += no
+    assert total > 0
+    pipe.close()

@@ -11,6 +11,9 @@
                batch) vs the CPU oracle.
   bow          Frame::ComputeBoW (DBoW2 transform, levelsup 4) of 256 extracted 640x480 frames with a synthetic
                vocabulary of ORBvoc.txt's shape (k=10, L=6, 1.1M nodes) resident in HBM, vs the CPU oracle.
+  tri_nodes    SearchForTriangulation over common BoW nodes (levelsup 4, ORBvoc.txt-shaped synthetic
+               vocabulary) for 256 frame pairs, FeatureVectors from the device BoW transform, vs the
+               BF batch (one node) on the same pairs and vs the oracle per pair.
   extract_host ORBextractor::operator() through the host-buffer C ABI on one 640x480 frame per call
                (H2D + whole pipeline + D2H): the Tracking thread's per-frame latency, vs the oracle.
 The CPU figures are the oracle (a plain-C restatement, 1 thread), not the reference build.
@@ -83,6 +86,53 @@ def bench_stereo(torch, steps, B=128):
             "k_stereo_ms_per_step": round(k_ms, 4), "k_stereo_us_per_pair": round(k_ms * 1e3 / B, 3),
             "stereo_kept_per_pair": round(float(ns.float().mean().item()), 1),
             "cpu_oracle_ms_per_pair": round(tc / nc * 1e3, 3), "cpu_threads": 1}
+
+
+def bench_tri_nodes(torch, reps):
+    import orbamd
+    import oracle_py
+    from orbamd.matcher import KeyFrameView
+    from orbamd.vocabulary import synth_vocabulary_full, L1_NORM, TF_IDF
+    k, L, parent, leaf, desc, weight = synth_vocabulary_full(10, 6, 7)
+    gv = orbamd.ORBVocabulary.from_arrays(k, L, L1_NORM, TF_IDF, parent, leaf, desc, weight)
+    B = 256
+    pipe = orbamd.device.BatchPipeline(torch, 640, 480, B)
+    frames = orbamd.synth_frames(0, 0, B, 640, 480)
+    pipe.extract(torch.from_numpy(frames).cuda())
+    pipe.bow(gv, 4)
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+    t_nodes = timed(pipe.match_pairs_nodes)
+    n_nodes = float(pipe.nmatch.float().mean().item())
+    t_bow = timed(lambda: pipe.bow(gv, 4))
+    t_bf = timed(pipe.match_pairs)
+    n_bf = float(pipe.nmatch.float().mean().item())
+    ov = oracle_py.OracleVocabulary(k, L, L1_NORM, TF_IDF, parent, leaf, desc, weight)
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    tabs = orc.tables()
+    r0, r1 = orc(frames[1]), orc(frames[0])
+    v1 = KeyFrameView(r0[0], r0[1], tabs["scale"], tabs["sigma2"], feat_vec=ov.transform(r0[1], 4)[1])
+    v2 = KeyFrameView(r1[0], r1[1], tabs["scale"], tabs["sigma2"], feat_vec=ov.transform(r1[1], 4)[1])
+    t = time.perf_counter()
+    for _ in range(5):
+        oracle_py.search_for_triangulation(v1, v2, pipe.F12, pipe.ex, pipe.ey, False, False)
+    c = (time.perf_counter() - t) / 5
+    pipe.close()
+    return {"row": "search_for_triangulation_bow_nodes", "workload": "256 pairs of 640x480 frames, levelsup 4, "
+            "vocabulary k=10 L=6", "gpu_ms_per_256_pairs_nodes": round(t_nodes, 4),
+            "gpu_ms_per_256_frames_bow": round(t_bow, 4), "gpu_ms_per_256_pairs_bf": round(t_bf, 4),
+            "matches_per_pair_nodes": round(n_nodes, 1), "matches_per_pair_bf": round(n_bf, 1),
+            "cpu_oracle_ms_per_pair_nodes": round(c * 1e3, 3), "cpu_threads": 1}
 
 
 def bench_extract_host(reps):
@@ -215,7 +265,7 @@ def main():
     import torch
     steps = int(os.environ.get("BENCH_ROWS_STEPS", "10"))
     for r in (bench_extract_host(100), bench_stereo(torch, steps), bench_projection(50), bench_distinctive(torch, 10),
-              bench_bow(torch, 10)):
+              bench_bow(torch, 10), bench_tri_nodes(torch, 10)):
         print(json.dumps(r), flush=True)
 
 
