@@ -1303,6 +1303,35 @@ int orbm_triangulation_nodes_batch_device(orbm_ctx* ctx, int npairs, const int32
     return 0;
 }
 
+int orbm_search_by_bow_batch_device(orbm_ctx* ctx, int npairs, int mode, const int32_t* d_qf, const int32_t* d_cf,
+                                    const orbx_kp* d_kps, const uint8_t* d_desc, const int32_t* d_counts,
+                                    int kp_stride, const uint8_t* d_mp_flags, const uint32_t* d_fv_node,
+                                    const int32_t* d_fv_off, const int32_t* d_fv_feat, const int32_t* d_nfv,
+                                    int max_nodes, float nnratio, int check_ori, int32_t* d_out,
+                                    int32_t* d_nmatches, void* stream) {
+    if (!ctx || npairs < 0 || (mode != 0 && mode != 1) || kp_stride < 1 || max_nodes < 0 || max_nodes > kp_stride ||
+        kp_stride > 64 * 1024)
+        return ORBX_EARG;
+    if (npairs == 0) return 0;
+    HIPR(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    HIPR(hipMemsetAsync(d_out, 0xFF, sizeof(int32_t) * (size_t)npairs * kp_stride, st));
+    HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * npairs, st));
+    HIPR(launch_bow_pairs(npairs, max_nodes, d_qf, d_cf, d_desc, kp_stride, d_mp_flags, d_fv_node, d_fv_off, d_fv_feat,
+                          d_nfv, nnratio, mode, d_out, st));
+    if (check_ori) {
+        // rows of out: (KF,KF) the query frame's features, rot = angle1 - angle2; (KF,F) the Frame's,
+        // rot = angleKF - angleF (ORBmatcher.cc:236-246, 616-627)
+        if (mode == 1)
+            HIPR(launch_rot_filter_pairs(npairs, d_qf, d_cf, d_kps, d_counts, kp_stride, d_out, d_nmatches, st, 0));
+        else
+            HIPR(launch_rot_filter_pairs(npairs, d_cf, d_qf, d_kps, d_counts, kp_stride, d_out, d_nmatches, st, 1));
+    } else {
+        HIPR(launch_count_pairs(npairs, d_out, kp_stride, d_nmatches, st));
+    }
+    return 0;
+}
+
 int orbm_triangulation_bf_packed_device(orbm_ctx* ctx, const orbx_kp* d_kps1, const uint8_t* d_desc1,
                                         const int32_t* d_count1, int nref, const uint8_t* d_slots,
                                         size_t slot_bytes, const float F12[9], float ex, float ey, int nlevels,

@@ -47,7 +47,12 @@ hipError_t launch_tri_nodes_pairs(int npairs, int max_nodes, const int32_t* q1, 
                                   int32_t* nmatches, hipStream_t st);
 hipError_t launch_rot_filter_pairs(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps,
                                    const int32_t* counts, int kp_stride, int32_t* match12, int32_t* nmatches,
-                                   hipStream_t st);
+                                   hipStream_t st, int swap = 0);
+hipError_t launch_bow_pairs(int npairs, int max_nodes, const int32_t* qf, const int32_t* cf, const uint8_t* desc,
+                            int kp_stride, const uint8_t* mp_flags, const uint32_t* fv_node, const int32_t* fv_off,
+                            const int32_t* fv_feat, const int32_t* nfv, float nnratio, int mode, int32_t* out,
+                            hipStream_t st);
+hipError_t launch_count_pairs(int npairs, const int32_t* out, int kp_stride, int32_t* nmatches, hipStream_t st);
 hipError_t launch_tri_bf_packed(const orbx_kp* kps1, const uint8_t* desc1, const int32_t* count1, int nref,
                                 const uint8_t* slots, long long slot_bytes, int slot_cap, const MatchGeom& g,
                                 int32_t* match, int cap1, int32_t* nmatches, hipStream_t st);

@@ -7,6 +7,7 @@
  *                     (v_bcnt_u32_b32) -- ORBmatcher.cc:657-823, 1647-1663.
  *   k_tri_nodes       SearchForTriangulation over common BoW nodes (general form).
  *   k_tri_nodes_pairs the same for a batch of frame pairs, FeatureVectors on the device.
+ *   k_bow_pairs       SearchByBoW (KF,F) / (KF,KF) for a batch of frame pairs, FeatureVectors on the device.
  *   k_bow             SearchByBoW(KF,F) / SearchByBoW(KF,KF): per common node, greedy over the
  *                     node's queries in order, wave-parallel best/second-best over candidates
  *                     (ORBmatcher.cc:159-288, 522-655).
@@ -536,6 +537,91 @@ __global__ __launch_bounds__(64) void k_bow(const DevView vq, const DevView vc, 
     }
 }
 
+/* SearchByBoW for a batch of frame pairs with the FeatureVectors of orbv_transform_batch_device on
+ * the device: block (i, p) takes node i of the query frame qf[p] and, if the candidate frame cf[p]
+ * has the same node (binary search), runs k_bow's node-local greedy (queries in order; best / second
+ * over the not yet matched candidates). mp_flags[f * kp_stride + idx]: bit 0 = a MapPoint, bit 1 = it
+ * is bad. mode 0 = (KF,F) (ORBmatcher.cc:159-288): qf = KF, out[cf index] = KF index;
+ * mode 1 = (KF,KF) (:522-655): out[qf index] = cf index. */
+__global__ __launch_bounds__(64) void k_bow_pairs(const int32_t* __restrict__ qf, const int32_t* __restrict__ cf,
+                                                  const uint8_t* __restrict__ desc, int kp_stride,
+                                                  const uint8_t* __restrict__ mp_flags,
+                                                  const uint32_t* __restrict__ fv_node, const int32_t* __restrict__ fv_off,
+                                                  const int32_t* __restrict__ fv_feat, const int32_t* __restrict__ nfv,
+                                                  float nnratio, int mode, int32_t* __restrict__ out) {
+    extern __shared__ uint8_t matched[];  // per candidate position in the node (<= kp_stride)
+    const int p = blockIdx.y, i = blockIdx.x;
+    const int fq = qf[p], fc = cf[p];
+    if (i >= nfv[fq]) return;
+    const uint32_t* nodes_c = fv_node + (long long)fc * kp_stride;
+    const uint32_t node = fv_node[(long long)fq * kp_stride + i];
+    int lo = 0, hi = nfv[fc];
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (nodes_c[mid] < node) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo >= nfv[fc] || nodes_c[lo] != node) return;
+    const int32_t* offq = fv_off + (long long)fq * (kp_stride + 1);
+    const int32_t* offc = fv_off + (long long)fc * (kp_stride + 1);
+    const int32_t* featq = fv_feat + (long long)fq * kp_stride;
+    const int32_t* featc = fv_feat + (long long)fc * kp_stride + offc[lo];
+    const uint8_t* fq_flags = mp_flags + (long long)fq * kp_stride;
+    const uint8_t* fc_flags = mp_flags + (long long)fc * kp_stride;
+    const uint8_t* dq = desc + (long long)fq * kp_stride * 32;
+    const uint8_t* dc = desc + (long long)fc * kp_stride * 32;
+    int32_t* o = out + (long long)p * kp_stride;
+    const int lane = threadIdx.x;
+    const int nc = offc[lo + 1] - offc[lo];
+    for (int j = lane; j < nc; j += 64) matched[j] = 0;
+    __syncthreads();
+    for (int i1 = offq[i]; i1 < offq[i + 1]; i1++) {
+        const int idxq = featq[i1];
+        if ((fq_flags[idxq] & 3) != 1) continue;  // a good MapPoint
+        const uint32_t* qd = (const uint32_t*)(dq + (long long)idxq * 32);
+        uint32_t q[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) q[k] = qd[k];
+        Top2 r = {256, -1, 256};
+        for (int j = lane; j < nc; j += 64) {
+            if (matched[j]) continue;
+            const int idxc = featc[j];
+            if (mode == 1 && (fc_flags[idxc] & 3) != 1) continue;
+            const int dist = hamming8(q, (const uint32_t*)(dc + (long long)idxc * 32));
+            if (dist < r.b1) { r.b2 = r.b1; r.b1 = dist; r.i1 = j; }
+            else if (dist < r.b2) { r.b2 = dist; }
+        }
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            Top2 o2;
+            o2.b1 = __shfl_xor(r.b1, sh, 64);
+            o2.i1 = __shfl_xor(r.i1, sh, 64);
+            o2.b2 = __shfl_xor(r.b2, sh, 64);
+            r = top2_merge(r, o2);
+        }
+        const bool ok_th = mode == 0 ? (r.b1 <= 50) : (r.b1 < 50);
+        if (ok_th && r.i1 >= 0 && __fmul_rn(1.0f, (float)r.b1) < __fmul_rn(nnratio, (float)r.b2)) {
+            const int idxc = featc[r.i1];
+            __syncthreads();
+            if (lane == 0) {
+                matched[r.i1] = 1;
+                if (mode == 0) o[idxc] = idxq;
+                else o[idxq] = idxc;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+/* per-pair count of out >= 0 (after the optional rotation filter) */
+__global__ __launch_bounds__(256) void k_count_pairs(const int32_t* __restrict__ out, int kp_stride,
+                                                     int32_t* __restrict__ nmatches) {
+    const int p = blockIdx.x;
+    int local = 0;
+    for (int i = threadIdx.x; i < kp_stride; i += 256) local += out[(long long)p * kp_stride + i] >= 0;
+    atomicAdd(&nmatches[p], local);
+}
+
 /* Rotation consistency (ORBmatcher.cc:236-246 + 267-285): entries i with m[i] >= 0; rot =
  * angA[a] - angB[b] where (a,b) = (i, m[i]) or, with swap, (m[i], i). One workgroup. */
 __global__ __launch_bounds__(256) void k_rot_filter(int n, int32_t* __restrict__ m, const float* __restrict__ angA,
@@ -586,7 +672,7 @@ __global__ __launch_bounds__(256) void k_rot_filter(int n, int32_t* __restrict__
 __global__ __launch_bounds__(256) void k_rot_filter_pairs(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
                                                           const orbx_kp* __restrict__ kps, const int32_t* __restrict__ counts,
                                                           int kp_stride, int32_t* __restrict__ match12,
-                                                          int32_t* __restrict__ nmatches) {
+                                                          int32_t* __restrict__ nmatches, int swap) {
     __shared__ int hist[30];
     __shared__ int keep[3];
     const int p = blockIdx.x;
@@ -600,7 +686,7 @@ __global__ __launch_bounds__(256) void k_rot_filter_pairs(const int32_t* __restr
     for (int i = threadIdx.x; i < n; i += 256) {
         const int j = m[i];
         if (j < 0) continue;
-        float rot = __fsub_rn(k1[i].angle, k2[j].angle);
+        float rot = swap ? __fsub_rn(k2[j].angle, k1[i].angle) : __fsub_rn(k1[i].angle, k2[j].angle);
         if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
         int bin = (int)roundf(__fmul_rn(rot, factor));
         if (bin == 30) bin = 0;
@@ -625,7 +711,7 @@ __global__ __launch_bounds__(256) void k_rot_filter_pairs(const int32_t* __restr
     for (int i = threadIdx.x; i < n; i += 256) {
         const int j = m[i];
         if (j < 0) continue;
-        float rot = __fsub_rn(k1[i].angle, k2[j].angle);
+        float rot = swap ? __fsub_rn(k2[j].angle, k1[i].angle) : __fsub_rn(k1[i].angle, k2[j].angle);
         if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
         int bin = (int)roundf(__fmul_rn(rot, factor));
         if (bin == 30) bin = 0;
@@ -675,9 +761,25 @@ hipError_t launch_tri_nodes_pairs(int npairs, int max_nodes, const int32_t* q1, 
 
 hipError_t launch_rot_filter_pairs(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps,
                                    const int32_t* counts, int kp_stride, int32_t* match12, int32_t* nmatches,
-                                   hipStream_t st) {
+                                   hipStream_t st, int swap) {
     hipLaunchKernelGGL(k_rot_filter_pairs, dim3(npairs), dim3(256), 0, st, q1, q2, kps, counts, kp_stride, match12,
-                       nmatches);
+                       nmatches, swap);
+    return hipGetLastError();
+}
+
+hipError_t launch_bow_pairs(int npairs, int max_nodes, const int32_t* qf, const int32_t* cf, const uint8_t* desc,
+                            int kp_stride, const uint8_t* mp_flags, const uint32_t* fv_node, const int32_t* fv_off,
+                            const int32_t* fv_feat, const int32_t* nfv, float nnratio, int mode, int32_t* out,
+                            hipStream_t st) {
+    if (npairs == 0 || max_nodes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bow_pairs, dim3(max_nodes, npairs), dim3(64), (size_t)kp_stride, st, qf, cf, desc, kp_stride,
+                       mp_flags, fv_node, fv_off, fv_feat, nfv, nnratio, mode, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_pairs(int npairs, const int32_t* out, int kp_stride, int32_t* nmatches, hipStream_t st) {
+    if (npairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_count_pairs, dim3(npairs), dim3(256), 0, st, out, kp_stride, nmatches);
     return hipGetLastError();
 }
 

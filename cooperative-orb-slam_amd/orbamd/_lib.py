@@ -67,6 +67,8 @@ SIGNATURES = {
                                                  _P]),
     "orbm_triangulation_nodes_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P, _F, _F,
                                                    _I, _P, _P, _I, _P, _P, _P]),
+    "orbm_search_by_bow_batch_device": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _F, _I, _P,
+                                             _P, _P]),
     "orbm_epipole": (None, [_P, _P, _P, _F, _F, _F, _F, C.POINTER(_F), C.POINTER(_F)]),
     "orbx_slot_bytes": (_SZ, [_I]),
     "orbx_pack_keyframe_device": (_I, [_P, _P, _P, _I, _P, _P]),

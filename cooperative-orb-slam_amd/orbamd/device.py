@@ -109,6 +109,16 @@ class BatchPipeline:
             len(self.scale), self.scale.ctypes.data, self.sigma2.ctypes.data, self.check_ori, self.match.data_ptr(),
             self.nmatch.data_ptr(), st), "orbm_triangulation_nodes_batch_device")
 
+    def search_by_bow_pairs(self, mode, qf, cf, mp_flags, nnratio, check_ori, out, nmatches, stream=None):
+        """SearchByBoW over the device FeatureVectors of bow(): mode 1 = (KF,KF), 0 = (KF,F); qf / cf int32
+        cuda [npairs]; mp_flags uint8 cuda [B, stride] (bit 0 MapPoint, bit 1 bad); out int32 [npairs, stride]."""
+        st = self.stream_ptr() if stream is None else stream
+        check(self.lib.orbm_search_by_bow_batch_device(
+            self.mh, int(qf.numel()), int(mode), qf.data_ptr(), cf.data_ptr(), self.kps.data_ptr(), self.desc.data_ptr(),
+            self.counts.data_ptr(), self.stride, mp_flags.data_ptr(), self.fv_node.data_ptr(), self.fv_off.data_ptr(),
+            self.fv_feat.data_ptr(), self.nfv.data_ptr(), self.max_nodes, float(nnratio), int(check_ori),
+            out.data_ptr(), nmatches.data_ptr(), st), "orbm_search_by_bow_batch_device")
+
     def step(self, frames, stream=None):
         self.extract(frames, stream)
         self.match_pairs(stream)

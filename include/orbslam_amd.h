@@ -186,6 +186,20 @@ int orbm_triangulation_nodes_batch_device(orbm_ctx* ctx, int npairs, const int32
                                           const float* scale_factors, const float* level_sigma2,
                                           int check_ori, int32_t* d_match12, int32_t* d_nmatches,
                                           void* stream);
+/* SearchByBoW for a batch of frame pairs over the same device FeatureVectors: mode 1 =
+ * SearchByBoW(KF1, KF2, vpMatches12) (ORBmatcher.cc:522-655; out[p*kp_stride + idx1] = idx2),
+ * mode 0 = SearchByBoW(KF, F, vpMapPointMatches) (:159-288; qf = KF, cf = F,
+ * out[p*kp_stride + idxF] = idxKF). mp_flags[f*kp_stride + idx]: bit 0 = the feature has a
+ * MapPoint, bit 1 = that MapPoint is bad (the KF side, and in mode 1 both sides, need bit 0
+ * without bit 1). Rotation histogram with check_ori. nmatches[p] = entries >= 0. */
+int orbm_search_by_bow_batch_device(orbm_ctx* ctx, int npairs, int mode, const int32_t* d_qf,
+                                    const int32_t* d_cf, const orbx_kp* d_kps,
+                                    const uint8_t* d_desc, const int32_t* d_counts, int kp_stride,
+                                    const uint8_t* d_mp_flags, const uint32_t* d_fv_node,
+                                    const int32_t* d_fv_off, const int32_t* d_fv_feat,
+                                    const int32_t* d_nfv, int max_nodes, float nnratio,
+                                    int check_ori, int32_t* d_out, int32_t* d_nmatches,
+                                    void* stream);
 
 /* Cross-agent variant: one query frame (kps/desc/count on device, e.g. this rank's latest
  * keyframe) against nref reference slots packed by orbx_pack_keyframe (e.g. the RCCL

@@ -155,3 +155,49 @@ def test_batch_pairs_over_bow_nodes(levelsup, check_ori):
         total += no
     assert total > 0
     pipe.close()
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_search_by_bow_pairs_device(mode):
+    """SearchByBoW (KF,KF) / (KF,F) for frame pairs over the device FeatureVectors
+    (orbm_search_by_bow_batch_device) vs the oracle with the oracle vocabulary's FeatureVectors."""
+    torch = pytest.importorskip("torch")
+    from orbamd.vocabulary import synth_vocabulary, L1_NORM, TF_IDF
+    k, L, levelsup = 10, 3, 1
+    v = synth_vocabulary(k, L, 9, flip_bits=24)
+    gv = orbamd.ORBVocabulary.from_arrays(k, L, L1_NORM, TF_IDF, *v[2:])
+    ov = oracle_py.OracleVocabulary(k, L, L1_NORM, TF_IDF, *v[2:])
+    W, H, B = 640, 480, 4
+    frames = orbamd.synth_frames(2, 4, B, W, H)
+    pipe = orbamd.device.BatchPipeline(torch, W, H, B)
+    pipe.extract(torch.from_numpy(frames).cuda())
+    pipe.bow(gv, levelsup)
+    rng = np.random.default_rng(5 + mode)
+    S = pipe.stride
+    has_mp = rng.random((B, S)) < 0.8
+    bad = rng.random((B, S)) < 0.1
+    flags = torch.from_numpy((has_mp.astype(np.uint8) | (bad.astype(np.uint8) << 1))).cuda()
+    qf = torch.arange(B, dtype=torch.int32).cuda()
+    cf = ((qf + 1) % B).to(torch.int32)
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    tabs = orc.tables()
+    res = [orc(frames[b]) for b in range(B)]
+    fvs = [ov.transform(res[b][1], levelsup)[1] for b in range(B)]
+    total = 0
+    for ratio, ori in ((0.75, True), (0.6, False)):
+        out = torch.empty((B, S), dtype=torch.int32).cuda()
+        nm = torch.zeros(B, dtype=torch.int32).cuda()
+        pipe.search_by_bow_pairs(mode, qf, cf, flags, ratio, ori, out, nm)
+        torch.cuda.synchronize()
+        for p in range(B):
+            a, b = p, (p + 1) % B
+            na, nb = len(res[a][0]), len(res[b][0])
+            va = _view(res[a][0], res[a][1], tabs, feat_vec=fvs[a], has_mp=has_mp[a, :na], mp_bad=bad[a, :na])
+            vb = _view(res[b][0], res[b][1], tabs, feat_vec=fvs[b], has_mp=has_mp[b, :nb], mp_bad=bad[b, :nb])
+            no, mo = oracle_py.search_by_bow(va, vb, ratio, ori, other_is_keyframe=mode == 1)
+            rows = na if mode == 1 else nb
+            np.testing.assert_array_equal(out[p, :rows].cpu().numpy(), mo)
+            assert int(nm[p].item()) == no
+            total += no
+    assert total > 0
+    pipe.close()
