@@ -1286,20 +1286,33 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     const int bp = lv.pitch;  // blurred rows are 64-aligned: one misalignment for every row
     const int pmis = (int)((uint32_t)(x - kDescPatchR) & 3u);
     const int pbase = (y - kDescPatchR) * bp + x - kDescPatchR - pmis;
-    uint2 pw[12];
-#pragma unroll
-    for (int q = 0; q < 12; q++) {
-        const int it = min(ln + 16 * q, kDescPatchRows * 5 - 1);
-        const int pr = it / 5, pc = it - pr * 5;
-        pw[q] = *(const uint2*)(bl + (pbase + pr * bp + 8 * pc));
-    }
+    // patch by LDS-DMA (global_load_lds_dword, no VGPR staging): per keypoint of the wave 37 rows x
+    // 10 dwords = 370 dwords, linear in LDS (pitch 40), as 6 wave-instructions of lanes
+    // d = 64q + lane < 370; the keypoint's patch origin and level pitch are wave-uniform (readlane)
     uint8_t* patch = s_patch[wave * 4 + sub];
+    {
+        const uint64_t pg = (uint64_t)(uintptr_t)(bl + pbase);
+        int rq[6], cq[6];
 #pragma unroll
-    for (int q = 0; q < 12; q++) {
-        const int it = ln + 16 * q;
-        if (it < kDescPatchRows * 5) {
-            const int pr = it / 5, pc = it - pr * 5;
-            *(uint2*)(patch + pr * kDescPatchPitch + 8 * pc) = pw[q];
+        for (int q = 0; q < 6; q++) {
+            const int d = 64 * q + lane;
+            rq[q] = d / 10;
+            cq[q] = 4 * (d - 10 * rq[q]);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pg, 16 * s);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pg >> 32), 16 * s);
+            const uint8_t* sb = (const uint8_t*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+            const int sbp = __builtin_amdgcn_readlane(bp, 16 * s);
+            uint8_t* dst = s_patch[wave * 4 + s];
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                if (64 * q + lane < kDescPatchRows * kDescPatchPitch / 4)
+                    __builtin_amdgcn_global_load_lds(
+                        (__attribute__((address_space(1))) void*)(sb + (unsigned)(rq[q] * sbp + cq[q])),
+                        (__attribute__((address_space(3))) void*)(dst + 256 * q), 4, 0, 0);
+            }
         }
     }
     int m10, m01;
@@ -1334,6 +1347,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     float sa, ca;
     glibc_sincosf(theta, &sa, &ca);
     const float a = ca, b = sa;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA patch writes have landed
     wave_sync();  // patch stores of the other lanes of this group
     const uint8_t* pc0 = patch + kDescPatchR * kDescPatchPitch + kDescPatchR + pmis;  // keypoint
     uint32_t myword = 0;  // descriptor bytes 2ln, 2ln+1 of this lane's keypoint = pairs 16ln .. 16ln+15

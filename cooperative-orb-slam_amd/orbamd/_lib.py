@@ -8,7 +8,10 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "liborbamd.so")
+# ORBAMD_LIB_VARIANT=<tag> loads lib/liborbamd_<tag>.so instead: A/B builds of one source tree for the
+# tools/ab_*.sh experiments (same ABI, different kernel variants)
+_VARIANT = os.environ.get("ORBAMD_LIB_VARIANT", "")
+LIB_PATH = os.path.join(PKG_DIR, "lib", "liborbamd%s.so" % ("_" + _VARIANT if _VARIANT else ""))
 
 ORBX_OK = 0
 ORBX_EARG = -1
