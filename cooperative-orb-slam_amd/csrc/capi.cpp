@@ -116,7 +116,7 @@ struct Geometry {
      * (r0, r1, beta). Returns false if some group's taps do not fit an 8-byte window. */
     bool build_pyr_tables(LevelDesc& d, const int* xofs, const short* alpha, const int* yofs, const short* beta,
                           int xmax, int sw, int sh, int dw, int dh) {
-        bool ok = dh <= kPyrMaxRows && (dw + 3) / 4 <= 1024 && sw >= 12;
+        bool ok = dh <= kPyrMaxRows && (dw + 3) / 4 <= kPyrThreads && sw >= 12;
         const int AU = (int)align_up(sw, 4);
         const int gw = (dw + 3) / 4;
         d.cg_off = (int)ptab.size();

@@ -225,8 +225,8 @@ struct PyrColGroup {
 };
 static_assert(sizeof(PyrColGroup) == 48, "PyrColGroup layout");
 
-template <int U>
-__global__ __launch_bounds__(1024) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
+template <int U, int NT>
+__global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
                                                          int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
                                                          const LevelDesc* __restrict__ levels,
                                                          const int* __restrict__ ptab) {
@@ -241,9 +241,9 @@ __global__ __launch_bounds__(1024) void k_pyramid_frames(const uint8_t* __restri
         uint8_t* dst = P + lv.pyr_off;
         const int dh = lv.h;
         const int4* rt = (const int4*)(ptab + lv.rt_off);
-        for (int i = tid; i < dh; i += 1024) s_rt[i] = rt[i];
+        for (int i = tid; i < dh; i += NT) s_rt[i] = rt[i];
         const int gw = (lv.w + 3) >> 2;
-        const int R = 1024 / gw;  // rows per pass
+        const int R = NT / gw;  // rows per pass
         const int ry = tid / gw, xg = tid - ry * gw;
         const PyrColGroup cg = ((const PyrColGroup*)(ptab + lv.cg_off))[min(xg, gw - 1)];
         const int A = cg.W & ~3, k = cg.W & 3;
@@ -1427,7 +1427,7 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
                                  const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int nframes,
                                  hipStream_t st) {
-    hipLaunchKernelGGL(k_pyramid_frames<kPyrU>, dim3(nframes), dim3(1024), 0, st, frames, fstride, pitch0, pyr, ep,
+    hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), dim3(nframes), dim3(kPyrThreads), 0, st, frames, fstride, pitch0, pyr, ep,
                        levels, ptab);
     return hipGetLastError();
 }

@@ -272,14 +272,14 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
             if (pb - amax > lim) continue;
             // key = D << 16 | (65535 - idx2) = kbase - (acc << 16 | row)
             const uint32_t kbase = ((uint32_t)pb << 16) + 65535u - (uint32_t)(cb + 32 * tile + 4 * h);
-            uint32_t key[16];
+            // keys are recomputed from the accumulators where needed (not kept: 16 fewer live VGPRs)
+            auto key = [&](int rg) {
+                const uint32_t row = (uint32_t)((rg & 3) + 8 * (rg >> 2));
+                return kbase - (((uint32_t)acc[rg] << 16) + row);
+            };
             uint32_t kmin = 0xFFFFFFFFu;
 #pragma unroll
-            for (int rg = 0; rg < 16; rg++) {
-                const uint32_t row = (uint32_t)((rg & 3) + 8 * (rg >> 2));
-                key[rg] = kbase - (((uint32_t)acc[rg] << 16) + row);
-                kmin = min(kmin, key[rg]);
-            }
+            for (int rg = 0; rg < 16; rg++) kmin = min(kmin, key(rg));
             uint32_t km = kmin;
             while (km < best && (km >> 16) <= 50u) {
                 const int jl = (int)(65535u - (km & 0xFFFFu)) - cb;
@@ -289,7 +289,7 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
                 }
                 uint32_t nx = 0xFFFFFFFFu;
 #pragma unroll
-                for (int rg = 0; rg < 16; rg++) nx = key[rg] > km ? min(nx, key[rg]) : nx;
+                for (int rg = 0; rg < 16; rg++) nx = key(rg) > km ? min(nx, key(rg)) : nx;
                 km = nx;
             }
         }

@@ -28,7 +28,14 @@ constexpr int kRoiMax = 72;         // max FAST cell ROI side (cells are < 60+6 
 constexpr int kRoiPitch = 72;
 constexpr int kBlurRows = 63;      // blur strip chunk height: 9 x 7 (the 7-row window loop has no partial step)
 constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity (levels >= 1)
-constexpr int kPyrU = 4;            // k_pyramid_frames: rows in flight per thread
+#ifndef ORBX_PYR_U
+#define ORBX_PYR_U 4
+#endif
+constexpr int kPyrU = ORBX_PYR_U;   // k_pyramid_frames: rows in flight per thread
+#ifndef ORBX_PYR_NT
+#define ORBX_PYR_NT 1024
+#endif
+constexpr int kPyrThreads = ORBX_PYR_NT;  // k_pyramid_frames: threads per frame's workgroup (>= column groups)
 constexpr int kPyrFramesMinBatch = 64;  // batches below this use the per-level pyramid kernels
 
 struct LevelDesc {
