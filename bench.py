@@ -120,6 +120,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--prio", choices=("none", "lead", "lead1"), default="none",
+                    help="HIP stream priorities of the graphs: lead = the first half of the staggered graphs (the ones "
+                         "in their latency-bound tail stages) high, lead1 = graph 0 only")
     ap.add_argument("--no-exchange", action="store_true")
     ap.add_argument("--stagger", choices=("each", "once", "none"), default="each",
                     help="graph p starts extracting after graph p-1's extraction: every step / only in the "
@@ -153,7 +156,9 @@ def main():
     frames_np = orbamd.synth_frames(rank, 0, B, W, H)  # agent = rank
     frames = [torch.from_numpy(frames_np[p * sub:(p + 1) * sub]).to(dev) for p in range(P)]
     pipes = [orbamd.device.BatchPipeline(torch, W, H, sub, device=local) for _ in range(P)]
-    streams = [torch.cuda.Stream(dev) for _ in range(P)]
+    lo_prio, hi_prio = torch.cuda.Stream.priority_range()
+    n_hi = {"none": 0, "lead": P // 2, "lead1": 1}[args.prio]
+    streams = [torch.cuda.Stream(dev, priority=hi_prio if p < n_hi else lo_prio) for p in range(P)]
     pipe = pipes[0]
     slot_bytes = pipe.slot_bytes()
     my_slot = torch.zeros(slot_bytes, dtype=torch.uint8, device=dev)
@@ -342,7 +347,8 @@ def main():
             "kp_per_frame": round(nkp, 1),
             "matches_per_pair": round(nmatch, 1),
         }
-    if rank == 0 and not args.no_cpu:
+    # the CPU baseline is measured at N=1 only (rank 0); multi-GPU lines report null
+    if rank == 0 and world == 1 and not args.no_cpu:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         # median of 5 short runs on all host cores, then the reference's own
         # architecture: one Tracking thread ((i), median of 3), with the oracle's stage split
