@@ -613,35 +613,29 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
             if (S > t_lo) str[o] = (uint8_t)S;
         }
         wave_sync();
-        int t = ep.ini_th;
-        int cnt = 0;
-        for (int i0 = 0; i0 < ncand; i0 += 64) {
-            const int i = i0 + lane;
-            bool keep = false;
-            if (i < ncand) {
-                const int e = clist[i];
-                keep = fast_survivor(str + (e >> 8) * RP + (e & 0xFF), RP, t);
-            }
-            cnt += __popcll(__ballot(keep));
-        }
-        if (cnt == 0) t = ep.min_th;
+        // one emission pass at iniThFAST; only a cell with no corner there (nothing was written) is
+        // scanned again at minThFAST (ORBextractor.cc:811-826): the same keys as a count pass at
+        // iniThFAST followed by an emission pass at the chosen threshold, with one NMS pass fewer
         uint32_t* out = cellkey + (long long)f * ep.keys_per_frame + c.slot;
-        for (int i0 = 0; i0 < ncand; i0 += 64) {
-            const int i = i0 + lane;
-            bool keep = false;
-            int e = 0;
-            if (i < ncand) {
-                e = clist[i];
-                keep = fast_survivor(str + (e >> 8) * RP + (e & 0xFF), RP, t);
+        for (int t = ep.ini_th;; t = ep.min_th) {
+            for (int i0 = 0; i0 < ncand; i0 += 64) {
+                const int i = i0 + lane;
+                bool keep = false;
+                int e = 0;
+                if (i < ncand) {
+                    e = clist[i];
+                    keep = fast_survivor(str + (e >> 8) * RP + (e & 0xFF), RP, t);
+                }
+                const unsigned long long m = __ballot(keep);
+                if (keep) {
+                    const int pos = total + lane_prefix(m);
+                    const int sc = str[(e >> 8) * RP + (e & 0xFF)] - 1;
+                    const uint32_t xr = (uint32_t)((e & 0xFF) + c.xoff), yr = (uint32_t)((e >> 8) + c.yoff);
+                    if (pos < c.cap) out[pos] = xr | (yr << 12) | ((uint32_t)sc << 24);
+                }
+                total += __popcll(m);
             }
-            const unsigned long long m = __ballot(keep);
-            if (keep) {
-                const int pos = total + lane_prefix(m);
-                const int sc = str[(e >> 8) * RP + (e & 0xFF)] - 1;
-                const uint32_t xr = (uint32_t)((e & 0xFF) + c.xoff), yr = (uint32_t)((e >> 8) + c.yoff);
-                if (pos < c.cap) out[pos] = xr | (yr << 12) | ((uint32_t)sc << 24);
-            }
-            total += __popcll(m);
+            if (total != 0 || t == ep.min_th) break;  // wave-uniform
         }
         if (total > c.cap) total = c.cap;
     }
