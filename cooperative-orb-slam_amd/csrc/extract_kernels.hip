@@ -425,8 +425,8 @@ __device__ __forceinline__ int fast_strength_h2(const uint8_t* roi, int o, int P
  * cv::FAST keeps a corner (S > t, score S-1) iff its score is strictly greater than the score of
  * every neighbouring corner. A neighbour with S_n >= S_c > t is a corner, and one with
  * S_n < S_c never suppresses, so the test is S_c > t && S_c > 1 && max8(S_n) < S_c. */
-__device__ __forceinline__ bool fast_survivor(const uint8_t* s, int P, int t) {
-    const int c = s[0];
+/* (the centre's S c is passed in: the caller holds it in a register or has read s[0]) */
+__device__ __forceinline__ bool fast_survivor_c(const uint8_t* s, int P, int t, int c) {
     const int n0 = s[-P - 1], n1 = s[-P], n2 = s[-P + 1], n3 = s[-1], n4 = s[1], n5 = s[P - 1], n6 = s[P],
               n7 = s[P + 1];
     const int mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
@@ -606,11 +606,19 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
             }
         }
         wave_sync();
-        for (int i = lane; i < ncand; i += 64) {
-            const int e = clist[i];
-            const int o = (e >> 8) * RP + (e & 0xFF);
-            const int S = fast_strength_h2(roi, o, RP);
-            if (S > t_lo) str[o] = (uint8_t)S;
+        // the first 64 candidates (all of them in most cells) keep their list entry and strength in
+        // registers for the NMS passes: one dependent LDS read fewer per pass
+        const int e0 = lane < ncand ? (int)clist[lane] : 0;
+        int s0 = 0;
+        for (int i0 = 0; i0 < ncand; i0 += 64) {
+            const int i = i0 + lane;
+            if (i < ncand) {
+                const int e = i0 == 0 ? e0 : (int)clist[i];
+                const int o = (e >> 8) * RP + (e & 0xFF);
+                const int S = fast_strength_h2(roi, o, RP);
+                if (S > t_lo) str[o] = (uint8_t)S;
+                if (i0 == 0) s0 = S > t_lo ? S : 0;
+            }
         }
         wave_sync();
         // one emission pass at iniThFAST; only a cell with no corner there (nothing was written) is
@@ -622,14 +630,24 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
                 const int i = i0 + lane;
                 bool keep = false;
                 int e = 0;
+                int cS = 0;
                 if (i < ncand) {
-                    e = clist[i];
-                    keep = fast_survivor(str + (e >> 8) * RP + (e & 0xFF), RP, t);
+                    const uint8_t* sp;
+                    if (i0 == 0) {
+                        e = e0;
+                        sp = str + (e >> 8) * RP + (e & 0xFF);
+                        cS = s0;
+                    } else {
+                        e = clist[i];
+                        sp = str + (e >> 8) * RP + (e & 0xFF);
+                        cS = sp[0];
+                    }
+                    keep = fast_survivor_c(sp, RP, t, cS);
                 }
                 const unsigned long long m = __ballot(keep);
                 if (keep) {
                     const int pos = total + lane_prefix(m);
-                    const int sc = str[(e >> 8) * RP + (e & 0xFF)] - 1;
+                    const int sc = cS - 1;
                     const uint32_t xr = (uint32_t)((e & 0xFF) + c.xoff), yr = (uint32_t)((e >> 8) + c.yoff);
                     if (pos < c.cap) out[pos] = xr | (yr << 12) | ((uint32_t)sc << 24);
                 }
