@@ -26,7 +26,11 @@ constexpr int kPatchSize = 31;      // ORBextractor.cc:72
 constexpr int kHalfPatch = 15;      // ORBextractor.cc:73
 constexpr int kRoiMax = 72;         // max FAST cell ROI side (cells are < 60+6 px)
 constexpr int kRoiPitch = 72;
-constexpr int kBlurRows = 63;      // blur strip chunk height: 9 x 7 (the 7-row window loop has no partial step)
+#ifndef ORBX_BLUR_ROWS
+#define ORBX_BLUR_ROWS 63
+#endif
+constexpr int kBlurRows = ORBX_BLUR_ROWS;  // blur strip chunk height: 9 x 7 (the 7-row window loop has no partial step)
+static_assert(kBlurRows % 7 == 0, "blur chunk height must be a multiple of 7");
 constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity (levels >= 1)
 #ifndef ORBX_PYR_U
 #define ORBX_PYR_U 4
