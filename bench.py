@@ -1,17 +1,22 @@
 #!/usr/bin/env python3
 """bench.py -- frames/s of ORB extract + match (BASELINE.json metric) on 1..N MI355X.
 
-One step = one pass of the hot path over one batch of B synthetic 640x480 frames already
-resident in HBM:  ORBextractor::operator() on every frame (nfeatures 1000, 1.2, 8 levels,
-FAST 20/7) + SearchForTriangulation of frame b against frame b-1 (one BoW node holding all
-features = the BASELINE "BF" configuration) + the cooperative exchange: each agent packs its
-latest keyframe (keypoints + descriptors) and RCCL-all-gathers it, then matches it against
-every agent's slot. One process per GPU = one agent; frames are
-agent-private, so per-GPU work is fixed as N grows ("weak" scaling). The B frames of a step are
-split over P concurrent extraction+match graphs (own handle and HIP stream each; frame b of a
-graph is matched against frame b-1 of the same graph), staggered so that one graph's FAST
-overlaps another graph's latency-bound tail (octree, describe, match) -- default 1024 frames as
-4 graphs of 256.
+One step = one pass of the hot path over one batch of B synthetic frames already resident in HBM
+(orbamd.agent.AgentSchedule): ORBextractor::operator() on every frame (C2: nfeatures 1000, 1.2,
+8 levels, FAST 20/7) + SearchForTriangulation of frame b against frame b-1 (one BoW node holding
+all features = the BASELINE "BF" configuration) + the cooperative exchange: each agent packs its
+latest keyframe into a keyframe slot, RCCL-all-gathers it, then matches it against every agent's
+slot. One process per GPU = one agent; frames are agent-private, so
+per-GPU work is fixed as N grows ("weak" scaling). The B frames are split over P concurrent,
+staggered extraction+match graphs (default 1024 frames as 4 graphs of 256).
+
+After the timed region the run checks itself: every graph's device error flags, then sampled
+frames (first / middle / last of every graph) with their match rows and the cross-agent matches,
+bit-compared against the CPU oracle (oracle/check_schedule.py, the checker); "bit_exact" in the
+JSON line, exit status 3 on a mismatch.
+
+--config c2 (default, the BASELINE metric) | c3 (752x480, 1200 features) | c4 (1241x376, 2000
+features): the BASELINE configs 3 and 4 at their geometries (left images, same step).
 
 Launch (N>1): python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
               --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
@@ -29,6 +34,15 @@ sys.path.insert(0, os.path.join(ROOT, "cooperative-orb-slam_amd"))
 
 VALU_PEAK_GINST = 1228.8  # 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU op (G wave-instr/s)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA, 2x the 2.5 PF dense bf16 rate (MI355X_MICROARCH.md "Matrix cores")
+
+CONFIGS = {
+    "c2": dict(W=640, H=480, nfeatures=1000, name="C2: synthetic 640x480 uint8, nfeatures 1000"),
+    "c3": dict(W=752, H=480, nfeatures=1200, name="C3: synthetic 752x480 uint8 (EuRoC geometry, left images), "
+                                                  "nfeatures 1200"),
+    "c4": dict(W=1241, H=376, nfeatures=2000, name="C4: synthetic 1241x376 uint8 (KITTI geometry, left images), "
+                                                   "nfeatures 2000"),
+}
 
 
 def level_sizes(W, H, nlevels=8, scale=1.2):
@@ -61,11 +75,31 @@ def algorithmic_bytes(W, H, nkp):
     return total, per_stage
 
 
-def cpu_baseline(frames, seconds, threads):
+def host_cpu_info():
+    """nproc / affinity / cgroup quota / CPU model of the host this process runs on."""
+    info = {"cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": None,
+            "model": None}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return info
+
+
+def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000):
     """Oracle ("port") timed on host cores: extract + BF SearchForTriangulation vs the previous
-    frame, one independent frame stream per thread (ctypes releases the GIL). Returns frames/s,
-    frames, seconds, and the per-stage seconds per frame summed over the threads' extractors
-    (oracle stage timers + the matcher timed around its call)."""
+    frame, one independent frame stream per thread (ctypes releases the GIL). Stops after `seconds`
+    or once `nframes` frames are done in total. Returns frames/s, frames, seconds, per-stage seconds
+    per frame (oracle stage timers + the matcher timed around its call)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
     import orbamd
@@ -73,14 +107,21 @@ def cpu_baseline(frames, seconds, threads):
     count = [0] * threads
     stage = [None] * threads
     match_s = [0.0] * threads
-    stop = time.perf_counter() + seconds
+    stop = time.perf_counter() + (seconds if seconds else 1e9)
+    total = [0]
+    lock = threading.Lock()
 
     def work(tid):
-        orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+        orc = oracle_py.OracleExtractor(nfeatures, 1.2, 8, 20, 7)
         tabs = orc.tables()
         prev = None
         i = tid
         while time.perf_counter() < stop:
+            if nframes is not None:
+                with lock:
+                    if total[0] >= nframes:
+                        break
+                    total[0] += 1
             img = frames[i % len(frames)]
             k, d = orc(img)
             cur = orbamd.KeyFrameView(k, d, tabs["scale"], tabs["sigma2"])
@@ -111,15 +152,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
     ap.add_argument("--batch", type=int, default=1024, help="frames per step per GPU")
     ap.add_argument("--pipes", type=int, default=4,
                     help="concurrent extraction+match graphs per GPU (each over batch/pipes frames, own handle "
                          "and HIP stream), staggered: graph p starts a step when graph p-1 finished extracting it")
-    ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="all-cores CPU leg: total seconds (5 runs)")
+    ap.add_argument("--cpu-frames-1t", type=int, default=0,
+                    help="1-thread CPU leg: frames (0 = 2000 at c2, 1000 at c3/c4)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this process may use (affinity set capped by the cgroup quota)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip the post-run bit-exact check")
     ap.add_argument("--prio", choices=("none", "lead", "lead1"), default="none",
                     help="HIP stream priorities of the graphs: lead = the first half of the staggered graphs (the ones "
                          "in their latency-bound tail stages) high, lead1 = graph 0 only")
@@ -128,11 +172,13 @@ def main():
                     help="graph p starts extracting after graph p-1's extraction: every step / only in the "
                          "first step of a run (the phase offset then persists) / never")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
 
     import numpy as np
     import torch
     import torch.distributed as dist
     import orbamd
+    from orbamd.agent import AgentSchedule
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -150,69 +196,20 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    W, H, B, P = args.width, args.height, args.batch, args.pipes
+    W, H, B, P = cfg["W"], cfg["H"], args.batch, args.pipes
     assert B % P == 0, "--batch must be a multiple of --pipes"
     sub = B // P
     frames_np = orbamd.synth_frames(rank, 0, B, W, H)  # agent = rank
-    frames = [torch.from_numpy(frames_np[p * sub:(p + 1) * sub]).to(dev) for p in range(P)]
-    pipes = [orbamd.device.BatchPipeline(torch, W, H, sub, device=local) for _ in range(P)]
     lo_prio, hi_prio = torch.cuda.Stream.priority_range()
     n_hi = {"none": 0, "lead": P // 2, "lead1": 1}[args.prio]
-    streams = [torch.cuda.Stream(dev, priority=hi_prio if p < n_hi else lo_prio) for p in range(P)]
-    pipe = pipes[0]
-    slot_bytes = pipe.slot_bytes()
-    my_slot = torch.zeros(slot_bytes, dtype=torch.uint8, device=dev)
-    all_slots = torch.zeros(world * slot_bytes, dtype=torch.uint8, device=dev)
-    xmatch = torch.empty((world, pipe.stride), dtype=torch.int32, device=dev)
-    xn = torch.zeros(world, dtype=torch.int32, device=dev)
-
-    ag_events = []  # (start, end) around the all-gather alone, timed steps only
-
-    def exchange(ag=None):
-        # this agent's latest keyframe -> RCCL all-gather -> match against every agent's slot
-        with torch.cuda.stream(streams[0]):
-            pipe.pack(0, my_slot, streams[0].cuda_stream)
-            if ag is not None:
-                ag[0].record(streams[0])
-            if world > 1:
-                dist.all_gather_into_tensor(all_slots, my_slot)
-            else:
-                all_slots.copy_(my_slot)
-            if ag is not None:
-                ag[1].record(streams[0])
-            pipe.match_packed(0, all_slots, world, xmatch, xn, streams[0].cuda_stream)
-
-    done = [torch.cuda.Event() for _ in range(P)]
-
-    def step(ev=None, xev=None, extract=True, match=True, xchg=True, first=True):
-        for p in range(P):
-            st = streams[p].cuda_stream
-            if extract:
-                if p > 0 and (args.stagger == "each" or (args.stagger == "once" and first)):
-                    # staggered graphs: graph p's extraction (FAST-heavy) overlaps graph p-1's matcher and the
-                    # latency-bound tail stages instead of running in lockstep with them
-                    streams[p].wait_event(done[p - 1])
-                pipes[p].extract(frames[p], st)
-                done[p].record(streams[p])
-            if match:
-                if ev is not None:
-                    ev[p][0].record(streams[p])
-                pipes[p].match_pairs(st)
-                if ev is not None:
-                    ev[p][1].record(streams[p])
-        if xchg and not args.no_exchange:
-            if xev is not None:
-                xev[0].record(streams[0])
-            ag = None
-            if xev is not None:
-                ag = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                ag_events.append(ag)
-            exchange(ag)
-            if xev is not None:
-                xev[1].record(streams[0])
+    sched = AgentSchedule(torch, frames_np, W, H, P, device=local, rank=rank, world=world,
+                          allgather=(lambda o, i: dist.all_gather_into_tensor(o, i)) if world > 1 else None,
+                          stagger=args.stagger, exchange=not args.no_exchange,
+                          priorities=[hi_prio if p < n_hi else lo_prio for p in range(P)], nfeatures=cfg["nfeatures"])
+    pipes = sched.pipes
 
     for _ in range(args.warmup):
-        step()
+        sched.step()
     torch.cuda.synchronize()
     lib = orbamd.load()
     import ctypes as C
@@ -231,7 +228,7 @@ def main():
         torch.cuda.synchronize()
         t_start = time.perf_counter()
         for i in range(nsteps):
-            step(evs[i], xevs[i], first=i == 0)
+            sched.step(evs[i], xevs[i], first=i == 0)
         torch.cuda.synchronize()
         if timed and world > 1:
             dist.barrier()
@@ -250,8 +247,8 @@ def main():
         st["match"] = sum(e[p][0].elapsed_time(e[p][1]) for e in evs for p in range(P)) / (nsteps * P)
         if not args.no_exchange:
             st["exchange"] = sum(x[0].elapsed_time(x[1]) for x in xevs) / nsteps
-            st["allgather"] = sum(a.elapsed_time(b) for a, b in ag_events) / max(len(ag_events), 1)
-            ag_events.clear()
+            st["allgather"] = sum(a.elapsed_time(b) for a, b in sched.ag_events) / max(len(sched.ag_events), 1)
+            sched.ag_events.clear()
         return elapsed, st
 
     def run_part(nsteps, **kw):
@@ -259,7 +256,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(nsteps):
-            step(first=i == 0, **kw)
+            sched.step(first=i == 0, **kw)
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
@@ -272,7 +269,26 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    # 3) extract-only and match-only rates, untimed breakdown passes; and the box's
+    # 3) self-check of the last timed step (error flags on every rank; oracle bit-compare of sampled frames,
+    # their match rows and the cross-agent matches)
+    err_msg = None
+    try:
+        sched.check_errors()
+    except RuntimeError as e:
+        err_msg = str(e)
+    check = None
+    if not args.no_check:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from check_schedule import check_schedule
+        check = check_schedule(sched, frames_np, nfeatures=cfg["nfeatures"],
+                               agent_frames=lambda r: orbamd.synth_frames(r, 0, 1, W, H)[0])
+    ok_local = err_msg is None and (check is None or check["bit_exact"])
+    ok_all = ok_local
+    if world > 1:
+        t = torch.tensor([0 if ok_local else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ok_all = int(t.item()) == 0
+    # 4) extract-only and match-only rates, untimed breakdown passes; and the box's
     # measured device-to-device copy bandwidth (read + write bytes of a 1 GiB copy) beside the nominal peak
     copy_gbs = None
     if rank == 0:
@@ -299,18 +315,36 @@ def main():
         b_frame, per_stage = algorithmic_bytes(W, H, nkp)
         dom_ms = dom_live[dom]
         # one launch of the dominant kernel processes one graph's sub-batch (B / P frames)
-        achieved = per_stage[dom] * sub / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and per_stage[dom] > 0 else 0.0
+        hbm_gbs = per_stage[dom] * sub / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and per_stage[dom] > 0 else 0.0
         traffic = valu_insts = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path):
+        if os.path.exists(pmc_path) and args.config == "c2" and sub == 256:
             try:
                 rec = json.load(open(pmc_path)).get(dom, {})
                 traffic = rec.get("hbm_bytes_per_launch")
                 valu_insts = rec.get("valu_insts_per_launch")
             except Exception:
                 traffic = valu_insts = None
+        valu_gs = valu_insts / (dom_ms * 1e-3) / 1e9 if valu_insts and dom_ms > 0 else None
+        hbm = {"achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(hbm_gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": per_stage[dom] * sub,
+               "measured_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
+               "frac_vs_copy": round(hbm_gbs / copy_gbs, 5) if copy_gbs else None}
+        if valu_gs is not None and valu_gs / VALU_PEAK_GINST > hbm_gbs / HBM_PEAK_GBS:
+            # the byte/integer kernels are bound by vector-instruction issue, not HBM
+            roof = {"bound": "valu", "kernel": dom, "achieved": round(valu_gs, 1), "peak": VALU_PEAK_GINST,
+                    "unit": "G wave64 VALU instr/s", "frac": round(valu_gs / VALU_PEAK_GINST, 4),
+                    "traffic": traffic, "valu_insts_per_launch": valu_insts, "launch_ms": round(dom_ms, 4),
+                    "hbm": hbm}
+        else:
+            roof = {"bound": "hbm", "kernel": dom, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm["frac"], "traffic": traffic, "launch_ms": round(dom_ms, 4), "hbm": hbm}
+        # the matcher on the int8 matrix cores: algorithmic ops = n1*n2 distances x 256 bits x 2 per pair
+        m_ms = stage_ms.get("match", 0.0)
+        m_tops = nkp * nkp * 512 * sub / (m_ms * 1e-3) / 1e12 if m_ms > 0 else 0.0
         result = {
-            "metric": "frames/sec ORB extract+match, 640x480 mono, 1000 feat/frame",
+            "metric": "frames/sec ORB extract+match, 640x480 mono, 1000 feat/frame" if args.config == "c2" else
+                      "frames/sec ORB extract+match, %dx%d, %d feat/frame" % (W, H, cfg["nfeatures"]),
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -322,22 +356,20 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic textured pan, SURVEY.md 8(d)); resident in HBM",
-            "config": {"workload": "C2: synthetic %dx%d uint8, nfeatures 1000, scale 1.2, 8 levels, FAST 20/7; "
-                                   "extract + BF SearchForTriangulation vs previous frame + per-step keyframe "
-                                   "all-gather & cross-agent match" % (W, H),
-                       "frames_per_step_per_gpu": B, "graphs_per_gpu": P,
+            "config": {"workload": cfg["name"] + ", scale 1.2, 8 levels, FAST 20/7; extract + BF "
+                                                 "SearchForTriangulation vs previous frame + per-step keyframe-slot "
+                                                 "all-gather & cross-agent SearchForTriangulation",
+                       "config": args.config, "frames_per_step_per_gpu": B, "graphs_per_gpu": P,
                        "parallelism": "agent-per-gpu x%d" % world},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": per_stage[dom] * sub,
-                         "launch_ms": round(dom_ms, 4),
-                         "measured_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
-                         "frac_vs_copy": round(achieved / copy_gbs, 5) if copy_gbs else None},
-            # what actually bounds these byte/integer kernels: vector-instruction issue
-            # (wave64 VALU op = 2 cycles on a SIMD-32; 1024 SIMDs at 2.4 GHz)
-            "valu_issue": None if not valu_insts else {
-                "insts_per_launch": valu_insts, "achieved_Ginst_s": round(valu_insts / (dom_ms * 1e-3) / 1e9, 1),
-                "peak_Ginst_s": VALU_PEAK_GINST, "frac": round(valu_insts / (dom_ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4)},
+            "bit_exact": bool(ok_all) if check is not None else None,
+            "checked_frames": check["checked_frames"] if check else 0,
+            "checked_pairs": check["checked_pairs"] if check else 0,
+            "checked_slots": check["checked_slots"] if check else 0,
+            "device_errors": err_msg,
+            "roofline": roof,
+            "match_roofline": {"bound": "mfma", "kernel": "k_tri_mfma", "achieved": round(m_tops, 2),
+                               "peak": I8_MFMA_PEAK_TOPS, "unit": "int8 TOPS", "frac": round(m_tops / I8_MFMA_PEAK_TOPS, 4),
+                               "launch_ms": round(m_ms, 4)},
             "pipeline_hbm": {"bytes_per_frame": b_frame, "achieved_GBs": round(b_frame * value / world / 1e9, 2),
                              "frac": round(b_frame * value / world / 1e9 / HBM_PEAK_GBS, 5)},
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
@@ -347,33 +379,44 @@ def main():
             "kp_per_frame": round(nkp, 1),
             "matches_per_pair": round(nmatch, 1),
         }
+        if check is not None and check["mismatches"]:
+            result["mismatches"] = check["mismatches"]
     # the CPU baseline is measured at N=1 only (rank 0); multi-GPU lines report null
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        # median of 5 short runs on all host cores, then the reference's own
-        # architecture: one Tracking thread ((i), median of 3), with the oracle's stage split
-        runs = [cpu_baseline(frames_np, args.cpu_seconds / 5, threads) for _ in range(5)]
+        info = host_cpu_info()
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from check_schedule import host_threads
+        threads = args.cpu_threads or host_threads()
+        nf1 = args.cpu_frames_1t or (2000 if args.config == "c2" else 1000)
+        # median of 5 short runs on every usable host core (the headline ratio), then the
+        # reference's own architecture: one Tracking thread ((i), >= 2000 frames at C2) with the oracle's stage split
+        runs = [cpu_baseline(frames_np, threads, seconds=args.cpu_seconds / 5, nfeatures=cfg["nfeatures"])
+                for _ in range(5)]
         fps = sorted(r[0] for r in runs)[2]
         nfr, sec = sum(r[1] for r in runs), sum(r[2] for r in runs)
-        runs1 = [cpu_baseline(frames_np, max(args.cpu_seconds / 6, 1.0), 1) for _ in range(3)]
-        fps1, nfr1, sec1, per1 = sorted(runs1, key=lambda r: r[0])[1]
-        result["cpu_baseline"] = {"value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
-                                  "sample": "median of 5 runs, %d synthetic 640x480 frames in %.1f s in total (extract + "
-                                            "BF triangulation vs previous) on %d threads, oracle/orb_oracle.c -O3 "
-                                            "-ffp-contract=off; 1-thread leg: median of 3 runs (%d frames in %.1f s)"
-                                            % (nfr, sec, threads, nfr1, sec1),
-                                  "value_1thread": round(fps1, 2),
-                                  "stage_ms_per_frame_1thread": {k: round(v * 1e3, 3) for k, v in per1.items()}}
+        fps1, nfr1, sec1, per1 = cpu_baseline(frames_np, 1, nframes=nf1, nfeatures=cfg["nfeatures"])
+        result["cpu_baseline"] = {
+            "value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": "median of 5 runs, %d synthetic %dx%d frames in %.1f s in total (extract + BF triangulation vs "
+                      "previous) on %d threads (every CPU of the affinity set, capped by the cgroup quota), "
+                      "oracle/orb_oracle.c -O3 -ffp-contract=off (a scalar restatement: no OpenCV SIMD/IPP); "
+                      "1-thread leg: %d frames in %.1f s" % (nfr, W, H, sec, threads, nfr1, sec1),
+            "host": info,
+            "value_1thread": round(fps1, 2),
+            "frames_1thread": nfr1,
+            "stage_ms_per_frame_1thread": {k: round(v * 1e3, 3) for k, v in per1.items()}}
         result["speedup_vs_cpu"] = round(value / fps, 1)
+        result["speedup_vs_cpu_1thread"] = round(value / fps1, 1)
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(result), flush=True)
-    for pp in pipes:
-        pp.close()
+    sched.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if not ok_all:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

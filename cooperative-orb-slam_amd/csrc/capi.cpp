@@ -387,6 +387,7 @@ struct orbx_handle {
     const uint8_t* last_frames = nullptr;
     long long last_fstride = 0;
     int last_pitch = 0, last_nframes = 0;
+    hipStream_t last_stream = nullptr;  // stream of the last run_extract
     bool lds_attr_set = false;
     // host path as one captured hipGraph (orbx_extract): pinned staging in / out, replayed per frame
     hipGraph_t graph = nullptr;
@@ -552,6 +553,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     h->last_fstride = fstride;
     h->last_pitch = pitch;
     h->last_nframes = nframes;
+    h->last_stream = st;
     return 0;
 }
 
@@ -671,6 +673,7 @@ int orbx_max_keypoints(const orbx_handle* h, int width, int height) {
     for (int l = 0; l < h->T.nlevels; l++) {
         const int w = cv_round_f((float)width * h->T.inv_scale[l]);
         const int hh = cv_round_f((float)height * h->T.inv_scale[l]);
+        if (w - 32 <= 0 || hh - 32 <= 0) return ORBX_EARG;  // as Geometry::build rejects the level
         const int nIni = (int)roundf((float)(w - 32) / (hh - 32));
         total += std::max(h->T.nfeat[l] + 3, 4 * std::max(nIni, 1));
     }
@@ -824,7 +827,10 @@ int orbx_pyramid_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_
     if (!dst) return 0;
     if (!h->last_frames || frame < 0 || frame >= h->last_nframes || pitch < (size_t)d.w) return ORBX_EARG;
     HIPR(hipSetDevice(h->device));
-    HIPR(hipDeviceSynchronize());
+    // wait for this handle's own last extraction only (the stream it was enqueued on and the handle's side
+    // stream), not for every stream on the device (other extractor / matcher threads)
+    HIPR(hipStreamSynchronize(h->last_stream));
+    HIPR(hipStreamSynchronize(h->side));
     const uint8_t* src = level == 0 ? h->last_frames + frame * h->last_fstride
                                     : h->pyr.as<uint8_t>() + frame * h->geo.ep.pyr_frame_bytes + d.pyr_off;
     const size_t sp = level == 0 ? (size_t)h->last_pitch : (size_t)d.pitch;
@@ -852,18 +858,6 @@ int orbx_get_feature_split(const orbx_handle* h, int32_t* per_level, int32_t* um
         if (per_level) per_level[l] = h->T.nfeat[l];
     for (int v = 0; v < 16; v++)
         if (umax16) umax16[v] = h->T.umax[v];
-    return 0;
-}
-
-size_t orbx_slot_bytes(int cap) {
-    const long long c = (cap + 1) & ~1;
-    return (size_t)align_up(64 + c * (long long)sizeof(orbx_kp) + c * 32, 256);
-}
-
-int orbx_pack_keyframe_device(const orbx_kp* d_kps, const uint8_t* d_desc, const int32_t* d_count, int cap,
-                              uint8_t* d_slot, void* stream) {
-    if (!d_kps || !d_desc || !d_count || !d_slot || cap < 1) return ORBX_EARG;
-    HIPR(launch_pack_slot(d_kps, d_desc, d_count, (cap + 1) & ~1, d_slot, (hipStream_t)stream));
     return 0;
 }
 
@@ -999,6 +993,7 @@ struct orbm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf scratch;
+    DevBuf err;  // device error flag of the *_device calls that validate their input (orbm_check_error)
     std::vector<uint8_t> host;
     void* pinned = nullptr;  // host staging of one call's inputs (one H2D copy)
     size_t pinned_bytes = 0;
@@ -1117,6 +1112,10 @@ int orbm_create(int device, orbm_ctx** out) {
         delete c;
         return ORBX_EDEVICE;
     }
+    if (c->err.ensure(64) || hipMemset(c->err.p, 0, 64) != hipSuccess) {
+        orbm_destroy(c);
+        return ORBX_EDEVICE;
+    }
     *out = c;
     return 0;
 }
@@ -1126,6 +1125,7 @@ void orbm_destroy(orbm_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->scratch.release();
+    c->err.release();
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1332,22 +1332,198 @@ int orbm_search_by_bow_batch_device(orbm_ctx* ctx, int npairs, int mode, const i
     return 0;
 }
 
-int orbm_triangulation_bf_packed_device(orbm_ctx* ctx, const orbx_kp* d_kps1, const uint8_t* d_desc1,
-                                        const int32_t* d_count1, int nref, const uint8_t* d_slots,
-                                        size_t slot_bytes, const float F12[9], float ex, float ey, int nlevels,
-                                        const float* scale_factors, const float* level_sigma2, int32_t* d_match,
-                                        int cap1, int32_t* d_nmatches, void* stream) {
-    if (!ctx || nref < 0 || !F12 || nlevels < 1 || nlevels > 16 || cap1 < 1) return ORBX_EARG;
+}  // extern "C"
+
+/* ===================================================================================== */
+/* Cross-agent keyframe slot (include/orbslam_amd.h; replaces lcmKeyFrameInfo,              */
+/* lcmKeyFrameInfo.hpp:24-150) and the cross-agent SearchForTriangulation over slots        */
+/* ===================================================================================== */
+namespace {
+
+SlotLayout slot_layout_of(int cap) {
+    SlotLayout L;
+    L.cap = cap;
+    if (!slot_offsets(cap, L.off, &L.bytes)) L.bytes = 0;
+    return L;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t orbx_slot_bytes(int cap) {
+    uint32_t off[ORBX_SLOT_NSECTIONS], total = 0;
+    if (!slot_offsets(cap, off, &total)) return 0;
+    return total;
+}
+
+int orbx_slot_layout(int cap, orbx_slot_header* hdr) {
+    const SlotLayout L = slot_layout_of(cap);
+    if (!L.bytes) return ORBX_EARG;
+    if (hdr) {
+        memset(hdr, 0, sizeof(*hdr));
+        hdr->magic = ORBX_SLOT_MAGIC;
+        hdr->version = ORBX_SLOT_VERSION;
+        hdr->cap = cap;
+        hdr->bytes = L.bytes;
+        for (int k = 0; k < ORBX_SLOT_NSECTIONS; k++) hdr->off[k] = L.off[k];
+    }
+    return 0;
+}
+
+int orbx_pack_keyframe_device(const orbx_kf_source* src, const orbx_kf_meta* meta, int cap, uint8_t* d_slot,
+                              int32_t* d_err, void* stream) {
+    if (!src || !meta || !src->kps || !src->desc || !src->count || !d_slot || cap < 1) return ORBX_EARG;
+    const SlotLayout L = slot_layout_of(cap);
+    if (!L.bytes) return ORBX_EARG;
+    HIPR(launch_pack_slot(*src, L, *meta, d_slot, d_err, (hipStream_t)stream));
+    return 0;
+}
+
+/* host restatement of k_pack_slot, byte for byte */
+int orbx_pack_keyframe_host(const orbx_kf_source* s, const orbx_kf_meta* meta, int cap, uint8_t* slot,
+                            size_t slot_bytes) {
+    if (!s || !meta || !s->count || !slot || cap < 1) return ORBX_EARG;
+    const SlotLayout L = slot_layout_of(cap);
+    if (!L.bytes || slot_bytes < L.bytes) return ORBX_EARG;
+    const int n = *s->count;
+    if (n < 0) return ORBX_EARG;
+    if (n > 0 && (!s->kps || !s->desc)) return ORBX_EARG;
+    const bool has_bow = s->bow_word && s->bow_value;
+    const int nbow = has_bow && s->nbow ? *s->nbow : 0;
+    const bool has_fv = s->fv_node && s->fv_off && s->fv_feat;
+    const int nfv = has_fv && s->nfv ? *s->nfv : 0;
+    const int nfeat = has_fv && nfv > 0 ? s->fv_off[nfv] : 0;
+    if (n > cap || nbow < 0 || nbow > cap || nfv < 0 || nfv > cap || nfeat < 0 || nfeat > cap) return ORBX_ECAPACITY;
+    memset(slot, 0, L.bytes);
+    orbx_slot_header* h = (orbx_slot_header*)slot;
+    h->magic = ORBX_SLOT_MAGIC;
+    h->version = ORBX_SLOT_VERSION;
+    h->n = n;
+    h->cap = cap;
+    h->nbow = has_bow ? nbow : 0;
+    h->nfv = nfv;
+    h->flags = (s->kun ? ORBX_SLOT_F_KUN : 0u) | ((s->uright && s->depth) ? ORBX_SLOT_F_STEREO : 0u) |
+               (s->mp_flags ? ORBX_SLOT_F_MP : 0u) | (has_bow ? ORBX_SLOT_F_BOW : 0u) | (has_fv ? ORBX_SLOT_F_FV : 0u);
+    h->bytes = L.bytes;
+    for (int k = 0; k < ORBX_SLOT_NSECTIONS; k++) h->off[k] = L.off[k];
+    memcpy(slot + kSlotMetaOff, meta, sizeof(*meta));
+    orbx_kp* kps = (orbx_kp*)(slot + L.off[ORBX_SLOT_KPS]);
+    float* kun = (float*)(slot + L.off[ORBX_SLOT_KUN]);
+    float* ur = (float*)(slot + L.off[ORBX_SLOT_URIGHT]);
+    float* dp = (float*)(slot + L.off[ORBX_SLOT_DEPTH]);
+    for (int i = 0; i < n; i++) {
+        kps[i] = s->kps[i];
+        kun[2 * i] = s->kun ? s->kun[2 * i] : s->kps[i].x;
+        kun[2 * i + 1] = s->kun ? s->kun[2 * i + 1] : s->kps[i].y;
+        const bool st = s->uright && s->depth;
+        ur[i] = st ? s->uright[i] : -1.f;
+        dp[i] = st ? s->depth[i] : -1.f;
+    }
+    if (n) memcpy(slot + L.off[ORBX_SLOT_DESC], s->desc, 32 * (size_t)n);
+    if (s->mp_flags && n) {
+        memcpy(slot + L.off[ORBX_SLOT_MPFLAGS], s->mp_flags, (size_t)n);
+        if (s->mp_pos) memcpy(slot + L.off[ORBX_SLOT_MPPOS], s->mp_pos, 12 * (size_t)n);
+    }
+    if (has_bow && nbow) {
+        memcpy(slot + L.off[ORBX_SLOT_BOWWORD], s->bow_word, 4 * (size_t)nbow);
+        memcpy(slot + L.off[ORBX_SLOT_BOWVALUE], s->bow_value, 8 * (size_t)nbow);
+    }
+    if (has_fv && nfv) {
+        memcpy(slot + L.off[ORBX_SLOT_FVNODE], s->fv_node, 4 * (size_t)nfv);
+        int32_t* fo = (int32_t*)(slot + L.off[ORBX_SLOT_FVOFF]);
+        for (int k = 0; k <= nfv; k++) fo[k] = std::min(std::max(s->fv_off[k], 0), cap);
+        if (nfeat) memcpy(slot + L.off[ORBX_SLOT_FVFEAT], s->fv_feat, 4 * (size_t)nfeat);
+    }
+    return 0;
+}
+
+int orbx_slot_parse(const uint8_t* slot, size_t slot_bytes, orbx_slot_view* v) {
+    if (!slot || !v || slot_bytes < kSlotBodyOff) return ORBX_EARG;
+    const orbx_slot_header* h = (const orbx_slot_header*)slot;
+    if (h->magic != ORBX_SLOT_MAGIC || h->version != ORBX_SLOT_VERSION) return ORBX_EARG;
+    const SlotLayout L = slot_layout_of(h->cap);
+    if (!L.bytes || h->bytes != L.bytes || (size_t)L.bytes > slot_bytes) return ORBX_EARG;
+    for (int k = 0; k < ORBX_SLOT_NSECTIONS; k++)
+        if (h->off[k] != L.off[k]) return ORBX_EARG;
+    const int n = h->n, cap = h->cap;
+    if (n < 0 || n > cap || h->nbow < 0 || h->nbow > cap || h->nfv < 0 || h->nfv > cap) return ORBX_EARG;
+    const orbx_kf_meta* m = (const orbx_kf_meta*)(slot + kSlotMetaOff);
+    if (m->mnScaleLevels < 1 || m->mnScaleLevels > 16) return ORBX_EARG;
+    const orbx_kp* kps = (const orbx_kp*)(slot + L.off[ORBX_SLOT_KPS]);
+    for (int i = 0; i < n; i++)
+        if (kps[i].octave < 0 || kps[i].octave >= m->mnScaleLevels) return ORBX_EARG;
+    const uint32_t* bw = (const uint32_t*)(slot + L.off[ORBX_SLOT_BOWWORD]);
+    for (int k = 1; k < h->nbow; k++)
+        if (bw[k] <= bw[k - 1]) return ORBX_EARG;
+    const uint32_t* fn = (const uint32_t*)(slot + L.off[ORBX_SLOT_FVNODE]);
+    const int32_t* fo = (const int32_t*)(slot + L.off[ORBX_SLOT_FVOFF]);
+    const int32_t* ff = (const int32_t*)(slot + L.off[ORBX_SLOT_FVFEAT]);
+    if (h->nfv > 0) {
+        if (fo[0] != 0 || fo[h->nfv] > n) return ORBX_EARG;
+        for (int k = 0; k < h->nfv; k++) {
+            if (k && fn[k] <= fn[k - 1]) return ORBX_EARG;
+            if (fo[k + 1] < fo[k]) return ORBX_EARG;
+            for (int j = fo[k]; j < fo[k + 1]; j++)
+                if (ff[j] < 0 || ff[j] >= n || (j > fo[k] && ff[j] <= ff[j - 1])) return ORBX_EARG;
+        }
+    }
+    v->hdr = h;
+    v->meta = m;
+    v->kps = kps;
+    v->kun = (const float*)(slot + L.off[ORBX_SLOT_KUN]);
+    v->uright = (const float*)(slot + L.off[ORBX_SLOT_URIGHT]);
+    v->depth = (const float*)(slot + L.off[ORBX_SLOT_DEPTH]);
+    v->desc = slot + L.off[ORBX_SLOT_DESC];
+    v->mp_flags = slot + L.off[ORBX_SLOT_MPFLAGS];
+    v->mp_pos = (const float*)(slot + L.off[ORBX_SLOT_MPPOS]);
+    v->bow_word = bw;
+    v->bow_value = (const double*)(slot + L.off[ORBX_SLOT_BOWVALUE]);
+    v->fv_node = fn;
+    v->fv_off = fo;
+    v->fv_feat = ff;
+    return 0;
+}
+
+int orbm_check_error(orbm_ctx* ctx, void* stream) {
+    if (!ctx) return ORBX_EARG;
+    HIPR(hipSetDevice(ctx->device));
+    int flag = 0;
+    HIPR(hipMemcpyAsync(&flag, ctx->err.p, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIPR(hipStreamSynchronize((hipStream_t)stream));
+    if (flag) HIPR(hipMemsetAsync(ctx->err.p, 0, sizeof(int), (hipStream_t)stream));
+    return flag ? ORBX_EDEVICE : 0;
+}
+
+int orbm_search_for_triangulation_slots_device(orbm_ctx* ctx, const orbx_kf_source* query, int cap1, int nref,
+                                               const uint8_t* d_slots, size_t slot_bytes, const orbm_slot_geom* geom,
+                                               int use_bow, int max_nodes, int32_t* d_match, int32_t* d_nmatches,
+                                               void* stream) {
+    if (!ctx || !query || !query->kps || !query->desc || !query->count || cap1 < 1 || nref < 0 ||
+        (nref > 0 && (!d_slots || !geom || !d_match || !d_nmatches)) || slot_bytes < kSlotBodyOff)
+        return ORBX_EARG;
+    if (use_bow && (!query->fv_node || !query->fv_off || !query->fv_feat || !query->nfv || max_nodes < 0 ||
+                    max_nodes > cap1))
+        return ORBX_EARG;
     if (nref == 0) return 0;
     HIPR(hipSetDevice(ctx->device));
-    // slot capacity implied by slot_bytes: 64 + cap*24 + cap*32 <= slot_bytes
-    const int slot_cap = (int)(((long long)slot_bytes - 64) / (long long)(sizeof(orbx_kp) + 32)) & ~1;
-    MatchGeom g;
-    make_geom(g, F12, ex, ey, nlevels, scale_factors, level_sigma2);
+    QueryKF q;
+    q.kps = query->kps;
+    q.kun = (const float2*)query->kun;
+    q.uright = query->uright;
+    q.mpf = query->mp_flags;
+    q.desc = query->desc;
+    q.count = query->count;
+    q.fv_node = query->fv_node;
+    q.fv_off = query->fv_off;
+    q.fv_feat = query->fv_feat;
+    q.nfv = query->nfv;
+    q.cap = cap1;
     hipStream_t st = (hipStream_t)stream;
-    HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * nref, st));
-    HIPR(launch_tri_bf_packed(d_kps1, d_desc1, d_count1, nref, d_slots, (long long)slot_bytes, slot_cap, g, d_match,
-                              cap1, d_nmatches, st));
+    HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * (size_t)nref, st));
+    if (use_bow) HIPR(hipMemsetAsync(d_match, 0xFF, sizeof(int32_t) * (size_t)nref * cap1, st));
+    HIPR(launch_tri_slots(q, d_slots, (long long)slot_bytes, nref, geom, use_bow, max_nodes, d_match, d_nmatches,
+                          ctx->err.as<int32_t>(), st));
     return 0;
 }
 

@@ -813,7 +813,10 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         }
         __syncthreads();
         for (int i = tid; i < n; i += 256) K.label[i] = (uint16_t)spos[K.label[i]];
-        if (size > NC) { if (tid == 0) atomicOr(err, 2); return; }
+        if (size > NC) {  // capacity overflow: flag it and leave this level empty (never a stale count)
+            if (tid == 0) { atomicOr(err, 2); lvcnt[f * ep.L + l] = 0; }
+            return;
+        }
         __syncthreads();
         uint32_t next_seq = (uint32_t)nIni;
         int phase = 1;
@@ -950,7 +953,10 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
             }
             __syncthreads();
             const int newSize = TC + nsurv;
-            if (newSize > NC) { if (tid == 0) atomicOr(err, 4); return; }
+            if (newSize > NC) {
+                if (tid == 0) { atomicOr(err, 4); lvcnt[f * ep.L + l] = 0; }
+                return;
+            }
             // write new table: survivors copy, children created
             for (int s = tid; s < size; s += 256) {
                 const int np = spos[s];

@@ -7,6 +7,7 @@
 #include "orb_device.h"
 #include "orb_frame.h"
 #include "orb_match.h"
+#include "orb_slot.h"
 
 namespace orbamd {
 
@@ -53,17 +54,18 @@ hipError_t launch_bow_pairs(int npairs, int max_nodes, const int32_t* qf, const 
                             const int32_t* fv_feat, const int32_t* nfv, float nnratio, int mode, int32_t* out,
                             hipStream_t st);
 hipError_t launch_count_pairs(int npairs, const int32_t* out, int kp_stride, int32_t* nmatches, hipStream_t st);
-hipError_t launch_tri_bf_packed(const orbx_kp* kps1, const uint8_t* desc1, const int32_t* count1, int nref,
-                                const uint8_t* slots, long long slot_bytes, int slot_cap, const MatchGeom& g,
-                                int32_t* match, int cap1, int32_t* nmatches, hipStream_t st);
-hipError_t launch_pack_slot(const orbx_kp* kps, const uint8_t* desc, const int32_t* count, int cap, uint8_t* slot,
-                            hipStream_t st);
 hipError_t launch_tri_nodes(const DevView& v1, const DevView& v2, const NodeTask* tasks, int ntasks,
                             const MatchGeom& g, int only_stereo, int32_t* match12, hipStream_t st);
 hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* tasks, int ntasks, int max_nc,
                       float nnratio, int mode, int32_t* out, hipStream_t st);
 hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* angB, int swap, int32_t* nout,
                              hipStream_t st);
+
+hipError_t launch_pack_slot(const orbx_kf_source& src, const SlotLayout& L, const orbx_kf_meta& meta, uint8_t* slot,
+                            int32_t* err, hipStream_t st);
+hipError_t launch_tri_slots(const QueryKF& q, const uint8_t* slots, long long slot_bytes, int nref,
+                            const orbm_slot_geom* geom, int use_bow, int max_nodes, int32_t* match,
+                            int32_t* nmatches, int32_t* err, hipStream_t st);
 
 hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st);
 hipError_t launch_distinctive(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best_idx,

@@ -328,45 +328,6 @@ __global__ __launch_bounds__(256) void k_tri_bf(const int32_t* __restrict__ q1, 
     tri_bf_body<SPLIT>(s, g, match12 + (long long)p * kp_stride, nmatches + p);
 }
 
-/* cross-agent: the query frame against nref packed slots (orbx_pack_keyframe_device) */
-/* one query frame against a few slots is a small problem: 16 candidate slices per query (16 queries
- * per workgroup) so ~1000 queries spread over ~64 workgroups instead of 16 */
-constexpr int kPackedSplit = 16;
-
-__global__ __launch_bounds__(256) void k_tri_bf_packed(const orbx_kp* __restrict__ kps1, const uint8_t* __restrict__ desc1,
-                                                       const int32_t* __restrict__ count1, const uint8_t* __restrict__ slots,
-                                                       long long slot_bytes, int slot_cap, MatchGeom g,
-                                                       int32_t* __restrict__ match, int cap1, int32_t* __restrict__ nmatches) {
-    const int r = blockIdx.y;
-    const uint8_t* slot = slots + (long long)r * slot_bytes;
-    PairSrc s;
-    s.kps1 = kps1; s.desc1 = desc1; s.n1 = *count1;
-    s.n2 = ((const int32_t*)slot)[0];
-    const int cap2 = ((const int32_t*)slot)[1];  // written by k_pack_slot (even)
-    (void)slot_cap;
-    s.kps2 = (const orbx_kp*)(slot + 64);
-    s.desc2 = slot + 64 + (long long)cap2 * sizeof(orbx_kp);
-    tri_bf_body<kPackedSplit>(s, g, match + (long long)r * cap1, nmatches + r);
-}
-
-/* pack one frame's (n, kps, desc) into an exchange slot */
-__global__ __launch_bounds__(256) void k_pack_slot(const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
-                                                   const int32_t* __restrict__ count, int cap, uint8_t* __restrict__ slot) {
-    const int n = *count;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ((int32_t*)slot)[0] = n;
-        ((int32_t*)slot)[1] = cap;
-    }
-    orbx_kp* ok = (orbx_kp*)(slot + 64);
-    uint4* od = (uint4*)(slot + 64 + (long long)cap * sizeof(orbx_kp));
-    const uint4* id = (const uint4*)desc;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        ok[i] = kps[i];
-        od[2 * i] = id[2 * i];
-        od[2 * i + 1] = id[2 * i + 1];
-    }
-}
-
 /* ----------------------------------------------------------------------------------- */
 /* General node-based SearchForTriangulation: one wave per (common node, 64 queries).   */
 /* ----------------------------------------------------------------------------------- */
@@ -780,21 +741,6 @@ hipError_t launch_bow_pairs(int npairs, int max_nodes, const int32_t* qf, const 
 hipError_t launch_count_pairs(int npairs, const int32_t* out, int kp_stride, int32_t* nmatches, hipStream_t st) {
     if (npairs == 0) return hipSuccess;
     hipLaunchKernelGGL(k_count_pairs, dim3(npairs), dim3(256), 0, st, out, kp_stride, nmatches);
-    return hipGetLastError();
-}
-
-hipError_t launch_tri_bf_packed(const orbx_kp* kps1, const uint8_t* desc1, const int32_t* count1, int nref,
-                                const uint8_t* slots, long long slot_bytes, int slot_cap, const MatchGeom& g,
-                                int32_t* match, int cap1, int32_t* nmatches, hipStream_t st) {
-    dim3 grid((cap1 + 256 / kPackedSplit - 1) / (256 / kPackedSplit), nref);
-    hipLaunchKernelGGL(k_tri_bf_packed, grid, dim3(256), 0, st, kps1, desc1, count1, slots, slot_bytes, slot_cap, g,
-                       match, cap1, nmatches);
-    return hipGetLastError();
-}
-
-hipError_t launch_pack_slot(const orbx_kp* kps, const uint8_t* desc, const int32_t* count, int cap, uint8_t* slot,
-                            hipStream_t st) {
-    hipLaunchKernelGGL(k_pack_slot, dim3((cap + 255) / 256), dim3(256), 0, st, kps, desc, count, cap, slot);
     return hipGetLastError();
 }
 

@@ -37,6 +37,51 @@ class OrbmKfView(C.Structure):
                 ("nlevels", C.c_int32), ("scale_factors", C.c_void_p), ("level_sigma2", C.c_void_p)]
 
 
+SLOT_NSECTIONS = 12
+SLOT_SECTIONS = ("KPS", "KUN", "URIGHT", "DEPTH", "DESC", "MPFLAGS", "MPPOS", "BOWWORD", "BOWVALUE", "FVNODE", "FVOFF",
+                 "FVFEAT")
+SLOT_MAGIC = 0x4B42524F
+SLOT_VERSION = 2
+SLOT_F_KUN, SLOT_F_STEREO, SLOT_F_MP, SLOT_F_BOW, SLOT_F_FV = 1, 2, 4, 8, 16
+
+
+class OrbxSlotHeader(C.Structure):
+    _fields_ = [("magic", C.c_uint32), ("version", C.c_uint32), ("n", C.c_int32), ("cap", C.c_int32),
+                ("nbow", C.c_int32), ("nfv", C.c_int32), ("flags", C.c_uint32), ("bytes", C.c_uint32),
+                ("off", C.c_uint32 * SLOT_NSECTIONS), ("reserved", C.c_uint32 * 12)]
+
+
+_META_I64 = ["nNextId", "mnId", "mnFrameId", "mnGridCols", "mnGridRows", "mnTrackReferenceForFrame",
+             "mnFuseTargetForKF", "mnBALocalForKF", "mnBAFixedForKF", "mnLoopQuery", "mnLoopWords", "mnRelocQuery",
+             "mnRelocWords", "mnBAGlobalForKF", "mnMinX", "mnMinY", "mnMaxX", "mnMaxY"]
+_META_F32 = ["mfGridElementWidthInv", "mfGridElementHeightInv", "mLoopScore", "mRelocScore", "fx", "fy", "cx", "cy",
+             "invfx", "invfy", "mbf", "mb", "mThDepth", "mfScaleFactor", "mfLogScaleFactor"]
+
+
+class OrbxKfMeta(C.Structure):
+    """orbx_kf_meta: the scalar / matrix fields of lcmKeyFrameInfo (lcmKeyFrameInfo.hpp:24-100)."""
+    _fields_ = ([(k, C.c_int64) for k in _META_I64] + [("mTimeStamp", C.c_double), ("agent", C.c_int32),
+                                                       ("mnScaleLevels", C.c_int32)] +
+                [(k, C.c_float) for k in _META_F32] +
+                [("mvScaleFactors", C.c_float * 16), ("mvLevelSigma2", C.c_float * 16),
+                 ("mvInvLevelSigma2", C.c_float * 16), ("mK", C.c_float * 9), ("mTcw", C.c_float * 16),
+                 ("mTcwGBA", C.c_float * 16), ("mTcwBefGBA", C.c_float * 16), ("mTcp", C.c_float * 16)])
+
+
+class OrbxKfSource(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("kps", "desc", "count", "kun", "uright", "depth", "mp_flags", "mp_pos",
+                                          "bow_word", "bow_value", "nbow", "fv_node", "fv_off", "fv_feat", "nfv")]
+
+
+class OrbxSlotView(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("hdr", "meta", "kps", "kun", "uright", "depth", "desc", "mp_flags",
+                                          "mp_pos", "bow_word", "bow_value", "fv_node", "fv_off", "fv_feat")]
+
+
+class OrbmSlotGeom(C.Structure):
+    _fields_ = [("F12", C.c_float * 9), ("ex", C.c_float), ("ey", C.c_float)]
+
+
 # numpy dtype matching orbx_kp (24 bytes)
 KP_FIELDS = [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
              ("octave", "<i4")]
@@ -66,15 +111,19 @@ SIGNATURES = {
     "orbm_search_by_bow_kf_kf": (_I, [_P, C.POINTER(OrbmKfView), C.POINTER(OrbmKfView), _F, _I, _P, C.POINTER(_I)]),
     "orbm_triangulation_bf_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _F, _F, _I, _P, _P, _I, _P, _P,
                                                 _P]),
-    "orbm_triangulation_bf_packed_device": (_I, [_P, _P, _P, _P, _I, _P, _SZ, _P, _F, _F, _I, _P, _P, _P, _I, _P,
-                                                 _P]),
+    "orbm_search_for_triangulation_slots_device": (_I, [_P, C.POINTER(OrbxKfSource), _I, _I, _P, _SZ,
+                                                        C.POINTER(OrbmSlotGeom), _I, _I, _P, _P, _P]),
+    "orbm_check_error": (_I, [_P, _P]),
     "orbm_triangulation_nodes_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P, _F, _F,
                                                    _I, _P, _P, _I, _P, _P, _P]),
     "orbm_search_by_bow_batch_device": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _F, _I, _P,
                                              _P, _P]),
     "orbm_epipole": (None, [_P, _P, _P, _F, _F, _F, _F, C.POINTER(_F), C.POINTER(_F)]),
     "orbx_slot_bytes": (_SZ, [_I]),
-    "orbx_pack_keyframe_device": (_I, [_P, _P, _P, _I, _P, _P]),
+    "orbx_slot_layout": (_I, [_I, C.POINTER(OrbxSlotHeader)]),
+    "orbx_pack_keyframe_device": (_I, [C.POINTER(OrbxKfSource), C.POINTER(OrbxKfMeta), _I, _P, _P, _P]),
+    "orbx_pack_keyframe_host": (_I, [C.POINTER(OrbxKfSource), C.POINTER(OrbxKfMeta), _I, _P, _SZ]),
+    "orbx_slot_parse": (_I, [_P, _SZ, C.POINTER(OrbxSlotView)]),
     "orbx_synth_frame": (_I, [_I, _I, _I, _I, _P]),
     "orbx_synth_frames": (_I, [_I, _I, _I, _I, _I, _P]),
     "orbx_synth_frames_shifted": (_I, [_I, _I, _I, _I, _I, _I, _P]),

@@ -1,0 +1,119 @@
+"""One agent's per-step work on one GPU: the schedule bench.py times and tests/test_gpu_schedule.py
+checks.
+
+A step = B frames already resident in HBM, split over P concurrent extraction+match graphs (own
+orbx handle, matcher ctx and HIP stream each):
+  * ORBextractor::operator() on every frame (orbx_extract_batch_device);
+  * SearchForTriangulation of frame b against frame b-1 of the same graph (one node holding every
+    feature, mono, no MapPoints: the BASELINE "BF" configuration);
+  * the cooperative exchange: graph 0's frame 0 is this agent's keyframe; it is packed into a
+    keyframe slot (orbx_pack_keyframe_device), all-gathered across the agents (RCCL over xGMI at
+    N > 1, a local copy at N = 1), and matched against every agent's slot straight from the receive
+    buffer (orbm_search_for_triangulation_slots_device).
+Graphs are staggered: graph p starts extracting a step once graph p-1 has finished extracting it,
+so one graph's FAST overlaps another's latency-bound tail (octree, describe, matcher).
+torch is plumbing only (HBM buffers, streams, torch.distributed); every kernel is liborbamd.so's.
+"""
+from .device import BatchPipeline
+
+
+class AgentSchedule:
+    def __init__(self, torch, frames_np, width, height, pipes, device=0, rank=0, world=1, allgather=None,
+                 stagger="each", exchange=True, priorities=None, nfeatures=1000):
+        """frames_np: uint8 [B, H, W] host frames of this agent (copied to HBM once); allgather(out, inp):
+        all-gather of equal-sized device byte tensors across agents (None at world 1)."""
+        B = len(frames_np)
+        assert B % pipes == 0, "frames per step must be a multiple of the graph count"
+        self.torch, self.W, self.H, self.B, self.P = torch, width, height, B, pipes
+        self.sub = B // pipes
+        self.rank, self.world, self.allgather = rank, world, allgather
+        self.stagger, self.exchange_on = stagger, exchange
+        dev = torch.device("cuda", device)
+        self.dev = dev
+        sub = self.sub
+        self.frames = [torch.from_numpy(frames_np[p * sub:(p + 1) * sub]).to(dev) for p in range(pipes)]
+        self.nfeatures = nfeatures
+        self.pipes = [BatchPipeline(torch, width, height, sub, nfeatures=nfeatures, device=device)
+                      for _ in range(pipes)]
+        prio = priorities or [0] * pipes
+        self.streams = [torch.cuda.Stream(dev, priority=prio[p]) for p in range(pipes)]
+        self.done = [torch.cuda.Event() for _ in range(pipes)]
+        p0 = self.pipes[0]
+        self.slot_bytes = p0.slot_bytes()
+        self.my_slot = torch.zeros(self.slot_bytes, dtype=torch.uint8, device=dev)
+        self.all_slots = torch.zeros(world * self.slot_bytes, dtype=torch.uint8, device=dev)
+        self.xmatch = torch.empty((world, p0.stride), dtype=torch.int32, device=dev)
+        self.xn = torch.zeros(world, dtype=torch.int32, device=dev)
+        self.pack_err = torch.zeros(16, dtype=torch.int32, device=dev)
+        self.meta = p0.meta(0, agent=rank)
+        self.src0 = p0.kf_source(0)
+        self.ag_events = []
+
+    # ------------------------------------------------------------------------------------------
+    def exchange(self, ag=None):
+        """this agent's keyframe -> slot -> all-gather -> cross-agent SearchForTriangulation"""
+        torch, st = self.torch, self.streams[0]
+        p0 = self.pipes[0]
+        with torch.cuda.stream(st):
+            p0.pack(0, self.my_slot, self.meta, st.cuda_stream, err=self.pack_err, src=self.src0)
+            if ag is not None:
+                ag[0].record(st)
+            if self.world > 1:
+                self.allgather(self.all_slots, self.my_slot)
+            else:
+                self.all_slots.copy_(self.my_slot)
+            if ag is not None:
+                ag[1].record(st)
+            p0.match_slots(0, self.all_slots, self.world, self.xmatch, self.xn, st.cuda_stream, query=self.src0)
+
+    def step(self, ev=None, xev=None, extract=True, match=True, xchg=True, first=True):
+        """enqueue one step; ev[p] = (start, end) events around graph p's matcher, xev around the exchange"""
+        torch = self.torch
+        for p in range(self.P):
+            st = self.streams[p].cuda_stream
+            if extract:
+                if p > 0 and (self.stagger == "each" or (self.stagger == "once" and first)):
+                    self.streams[p].wait_event(self.done[p - 1])
+                self.pipes[p].extract(self.frames[p], st)
+                self.done[p].record(self.streams[p])
+            if match:
+                if ev is not None:
+                    ev[p][0].record(self.streams[p])
+                self.pipes[p].match_pairs(st)
+                if ev is not None:
+                    ev[p][1].record(self.streams[p])
+        if xchg and self.exchange_on:
+            if xev is not None:
+                xev[0].record(self.streams[0])
+            ag = None
+            if xev is not None:
+                ag = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                self.ag_events.append(ag)
+            self.exchange(ag)
+            if xev is not None:
+                xev[1].record(self.streams[0])
+
+    # ------------------------------------------------------------------------------------------
+    def check_errors(self):
+        """Device-side consistency flags of every graph (extraction: octree capacity / root index;
+        matcher: slot validation) and of the keyframe pack; raises RuntimeError on any."""
+        for p, pp in enumerate(self.pipes):
+            st = self.streams[p].cuda_stream
+            pp.check_error(st)
+            pp.check_match_error(st)
+        self.torch.cuda.synchronize(self.dev)
+        if int(self.pack_err.max().item()) != 0:
+            raise RuntimeError("keyframe pack clamped a count (slot capacity)")
+
+    def frame_results(self, p, b):
+        """(keypoints, descriptors, match12 vs frame b-1 of the same graph) of frame b of graph p"""
+        return self.pipes[p].host_results(b)
+
+    def exchange_results(self):
+        """match rows [world, n] of this agent's keyframe against every agent's slot"""
+        n = int(self.pipes[0].counts[0].item())
+        return self.xmatch[:, :n].cpu().numpy(), self.xn.cpu().numpy()
+
+    def close(self):
+        for pp in self.pipes:
+            pp.close()

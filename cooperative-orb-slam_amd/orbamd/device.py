@@ -123,23 +123,56 @@ class BatchPipeline:
         self.extract(frames, stream)
         self.match_pairs(stream)
 
+    # ---- cross-agent exchange (include/orbslam_amd.h "Cross-agent keyframe slot") ----
     def slot_bytes(self):
         return int(self.lib.orbx_slot_bytes(self.stride))
 
-    def pack(self, frame_idx, slot, stream=None):
-        st = self.stream_ptr() if stream is None else stream
-        check(self.lib.orbx_pack_keyframe_device(
-            self.kps[frame_idx].data_ptr(), self.desc[frame_idx].data_ptr(), self.counts[frame_idx:].data_ptr(),
-            self.stride, slot.data_ptr(), st), "orbx_pack_keyframe_device")
+    def meta(self, frame_idx=0, agent=0):
+        """orbx_kf_meta of frame frame_idx as a keyframe of agent `agent` (camera of my.yaml, the
+        extractor's scale tables, identity pose)."""
+        from .exchange import make_meta
+        inv = self.ext.GetInverseScaleSigmaSquares()
+        K = np.array([[FX, 0, CX], [0, FY, CY], [0, 0, 1]], np.float32)
+        return make_meta(agent=agent, mnId=frame_idx, nlevels=len(self.scale), scale=self.scale, sigma2=self.sigma2,
+                         inv_sigma2=inv, scale_factor=self.ext.GetScaleFactor(), K=K, width=self.W, height=self.H)
 
-    def match_packed(self, frame_idx, slots, nref, out_match, out_n, stream=None):
+    def kf_source(self, frame_idx, with_bow=False, uright=None, depth=None, mp_flags=None, mp_pos=None):
+        """orbx_kf_source of frame frame_idx's device arrays (its BoW / FeatureVector from bow() with
+        with_bow; optional per-keypoint uright/depth/MapPoint device tensors)."""
+        from .exchange import kf_source
+        f, S = frame_idx, self.stride
+        kw = {}
+        if with_bow:
+            kw = dict(bow_word=self.bow_word[f], bow_value=self.bow_val[f], nbow=self.nbow[f:f + 1],
+                      fv_node=self.fv_node[f], fv_off=self.fv_off[f], fv_feat=self.fv_feat[f], nfv=self.nfv[f:f + 1])
+        return kf_source(self.kps[f], self.desc[f], self.counts[f:f + 1], uright=uright, depth=depth,
+                         mp_flags=mp_flags, mp_pos=mp_pos, **kw)
+
+    def pack(self, frame_idx, slot, meta, stream=None, with_bow=False, err=None, src=None):
+        """orbx_pack_keyframe_device of frame frame_idx into the device slot."""
+        from .exchange import pack_device
         st = self.stream_ptr() if stream is None else stream
-        F = np.ascontiguousarray(self.F12.reshape(9))
-        check(self.lib.orbm_triangulation_bf_packed_device(
-            self.mh, self.kps[frame_idx].data_ptr(), self.desc[frame_idx].data_ptr(),
-            self.counts[frame_idx:].data_ptr(), nref, slots.data_ptr(), self.slot_bytes(), F.ctypes.data, self.ex,
-            self.ey, len(self.scale), self.scale.ctypes.data, self.sigma2.ctypes.data, out_match.data_ptr(),
-            self.stride, out_n.data_ptr(), st), "orbm_triangulation_bf_packed_device")
+        src = self.kf_source(frame_idx, with_bow) if src is None else src
+        pack_device(src, meta, self.stride, slot, err, st)
+
+    def match_slots(self, frame_idx, slots, nref, out_match, out_n, stream=None, use_bow=False, geoms=None,
+                    query=None):
+        """Cross-agent SearchForTriangulation of frame frame_idx against nref received slots
+        (orbm_search_for_triangulation_slots_device); geoms = per-slot (F12, ex, ey), default the bench
+        geometry for every slot."""
+        from .exchange import match_slots_device, slot_geoms
+        st = self.stream_ptr() if stream is None else stream
+        if geoms is None:
+            if getattr(self, "_geo_cache", (None, None))[0] != nref:
+                self._geo_cache = (nref, slot_geoms([(self.F12, self.ex, self.ey)] * nref))
+            geoms = self._geo_cache[1]
+        q = self.kf_source(frame_idx, use_bow) if query is None else query
+        match_slots_device(self.mh, q, self.stride, nref, slots, self.slot_bytes(), geoms, out_match, out_n,
+                           use_bow=use_bow, max_nodes=getattr(self, "max_nodes", 0) if use_bow else 0, stream=st)
+
+    def check_match_error(self, stream=None):
+        st = self.stream_ptr() if stream is None else stream
+        check(self.lib.orbm_check_error(self.mh, st), "orbm_check_error")
 
     def host_results(self, b):
         """(keypoints structured array, descriptors uint8 [n,32], match12 int32 [n]) of frame b."""

@@ -201,16 +201,10 @@ int orbm_search_by_bow_batch_device(orbm_ctx* ctx, int npairs, int mode, const i
                                     int check_ori, int32_t* d_out, int32_t* d_nmatches,
                                     void* stream);
 
-/* Cross-agent variant: one query frame (kps/desc/count on device, e.g. this rank's latest
- * keyframe) against nref reference slots packed by orbx_pack_keyframe (e.g. the RCCL
- * all-gather receive buffer). Same BF SearchForTriangulation semantics per slot. */
-int orbm_triangulation_bf_packed_device(orbm_ctx* ctx, const orbx_kp* d_kps1,
-                                        const uint8_t* d_desc1, const int32_t* d_count1,
-                                        int nref, const uint8_t* d_slots, size_t slot_bytes,
-                                        const float F12[9], float ex, float ey, int nlevels,
-                                        const float* scale_factors, const float* level_sigma2,
-                                        int32_t* d_match /* nref x cap1 */, int cap1,
-                                        int32_t* d_nmatches /* nref */, void* stream);
+/* Waits for `stream` and reports (then clears) the ctx's device error flag, raised by the
+ * *_device calls that validate device-resident input (orbm_search_for_triangulation_slots_device:
+ * a malformed or foreign slot, a query count above its capacity): 0 = OK, ORBX_EDEVICE. */
+int orbm_check_error(orbm_ctx* ctx, void* stream);
 
 /* Epipole helper (ORBmatcher.cc:664-670): C2 = R2w*Cw + t2w with OpenCV's small-matrix gemm
  * semantics (float products/sums, + t in double, one rounding; DESIGN.md "Pinned semantics"),
@@ -357,13 +351,153 @@ int orbv_transform_batch_device(orbv_handle* h, int nframes, const uint8_t* d_de
                                 int32_t* d_nfv, void* stream);
 
 /* ------------------------------------------------------------------------------------
- * Cross-agent exchange slot (replaces the LCM KeyFrameexample message,
- * ORB_SLAM2.1/Examples/ROS/ORB_SLAM2/src/ros_mono.cc:1907-2410).
- * slot = [u32 n | u32 pad[15] | n x orbx_kp (24 B) | n x 32 B descriptors], fixed size
- * orbx_slot_bytes(cap). */
+ * Cross-agent keyframe slot -- replaces the LCM message lcmKeyFrame::lcmKeyFrameInfo
+ * (ORB_SLAM2.1/include/lcmKeyFrame/lcmKeyFrameInfo.hpp:24-150), published by the sending
+ * agent (ORB_SLAM2.1/Examples/ROS/ORB_SLAM2/src/ros_mono.cc:1907-2410) and decoded into
+ * receiveKeyframeInfo by the receiving one (ORB_SLAM2/Examples/ROS/ORB_SLAM2/src/
+ * ros_mono.cc:88-166, 230-544) for Tracking::CreateNewKeyFrame (:2108-2192). One slot is a
+ * fixed-size, self-describing byte block (so an RCCL all-gather of equal-sized slots is the
+ * whole transport):
+ *   [0, 128)      orbx_slot_header (magic, version, counts, section offsets)
+ *   [128, 832)    orbx_kf_meta     (every scalar / matrix field of lcmKeyFrameInfo)
+ *   [1024, ...)   sections, each 256-byte aligned, sized by the capacity `cap`:
+ *     KPS      cap x orbx_kp        mvKeys (float coordinates; LCM truncated them to int16,
+ *                                   lcmKeyPoint.hpp:19-24)
+ *     KUN      cap x float[2]       mvKeysUn[i].pt (size/angle/octave equal mvKeys')
+ *     URIGHT   cap x float          mvuRight (-1 = monocular)
+ *     DEPTH    cap x float          mvDepth
+ *     DESC     cap x 32 B           mDescriptors (bytes; LCM sent them as float rows)
+ *     MPFLAGS  cap x u8             bit 0: mvpMapPoints[i] != NULL  (lcmKeyFrameMapPoints
+ *                                   .ifMapPoints), bit 1: that MapPoint isBad()
+ *     MPPOS    cap x float[3]       its world position (poseX/Y/Z)
+ *     BOWWORD  cap x u32, BOWVALUE cap x f64   mBowVec (ascending word id), nbow entries
+ *     FVNODE   cap x u32, FVOFF (cap+1) x i32, FVFEAT cap x i32   mFeatVec as CSR, nfv nodes
+ * Entries past n (nbow, nfv) are zero. All-little-endian, no pointers.
+ * ---------------------------------------------------------------------------------- */
+#define ORBX_SLOT_MAGIC 0x4B42524Fu /* "ORBK" */
+#define ORBX_SLOT_VERSION 2
+enum {
+    ORBX_SLOT_KPS = 0, ORBX_SLOT_KUN, ORBX_SLOT_URIGHT, ORBX_SLOT_DEPTH, ORBX_SLOT_DESC,
+    ORBX_SLOT_MPFLAGS, ORBX_SLOT_MPPOS, ORBX_SLOT_BOWWORD, ORBX_SLOT_BOWVALUE, ORBX_SLOT_FVNODE,
+    ORBX_SLOT_FVOFF, ORBX_SLOT_FVFEAT, ORBX_SLOT_NSECTIONS
+};
+/* header.flags: which optional fields the sender filled (the rest hold their defaults) */
+#define ORBX_SLOT_F_KUN 1u     /* mvKeysUn differs from mvKeys (else KUN = mvKeys' pt)   */
+#define ORBX_SLOT_F_STEREO 2u  /* mvuRight / mvDepth present (else -1)                   */
+#define ORBX_SLOT_F_MP 4u      /* MapPoint records present (else none)                   */
+#define ORBX_SLOT_F_BOW 8u     /* BowVector present                                      */
+#define ORBX_SLOT_F_FV 16u     /* FeatureVector present                                  */
+
+typedef struct orbx_slot_header {
+    uint32_t magic, version;
+    int32_t n;        /* N (keypoints)                                                    */
+    int32_t cap;      /* capacity the section sizes were computed for                     */
+    int32_t nbow;     /* BowVector entries                                                */
+    int32_t nfv;      /* FeatureVector nodes                                              */
+    uint32_t flags;   /* ORBX_SLOT_F_*                                                    */
+    uint32_t bytes;   /* orbx_slot_bytes(cap)                                             */
+    uint32_t off[ORBX_SLOT_NSECTIONS]; /* byte offset of each section                    */
+    uint32_t reserved[12];
+} orbx_slot_header; /* 128 bytes */
+
+/* The scalar and matrix fields of lcmKeyFrameInfo (lcmKeyFrameInfo.hpp:24-100), grouped by
+ * type; 4x4 / 3x3 matrices row-major (cv::Mat::at<float>(r,c)). 704 bytes. */
+typedef struct orbx_kf_meta {
+    int64_t nNextId, mnId, mnFrameId, mnGridCols, mnGridRows, mnTrackReferenceForFrame,
+        mnFuseTargetForKF, mnBALocalForKF, mnBAFixedForKF, mnLoopQuery, mnLoopWords, mnRelocQuery,
+        mnRelocWords, mnBAGlobalForKF, mnMinX, mnMinY, mnMaxX, mnMaxY;
+    double mTimeStamp;
+    int32_t agent;          /* sending agent (rank); not in the LCM message              */
+    int32_t mnScaleLevels;
+    float mfGridElementWidthInv, mfGridElementHeightInv, mLoopScore, mRelocScore;
+    float fx, fy, cx, cy, invfx, invfy, mbf, mb, mThDepth;
+    float mfScaleFactor, mfLogScaleFactor;
+    float mvScaleFactors[16], mvLevelSigma2[16], mvInvLevelSigma2[16];
+    float mK[9];
+    float mTcw[16], mTcwGBA[16], mTcwBefGBA[16], mTcp[16];
+} orbx_kf_meta;
+
+/* One keyframe's per-feature arrays (device memory for the *_device calls, host memory for
+ * orbx_pack_keyframe_host). count -> N. Optional arrays may be NULL (see ORBX_SLOT_F_*):
+ * kun (n x 2 floats), uright + depth, mp_flags (+ mp_pos n x 3), bow_word + bow_value + nbow,
+ * fv_node + fv_off + fv_feat + nfv. */
+typedef struct orbx_kf_source {
+    const orbx_kp* kps;
+    const uint8_t* desc;
+    const int32_t* count;
+    const float* kun;
+    const float* uright;
+    const float* depth;
+    const uint8_t* mp_flags;
+    const float* mp_pos;
+    const uint32_t* bow_word;
+    const double* bow_value;
+    const int32_t* nbow;
+    const uint32_t* fv_node;
+    const int32_t* fv_off;
+    const int32_t* fv_feat;
+    const int32_t* nfv;
+} orbx_kf_source;
+
+/* Fixed slot size for capacity cap (and the header with the section offsets, hdr optional). */
 size_t orbx_slot_bytes(int cap);
-int orbx_pack_keyframe_device(const orbx_kp* d_kps, const uint8_t* d_desc,
-                              const int32_t* d_count, int cap, uint8_t* d_slot, void* stream);
+int orbx_slot_layout(int cap, orbx_slot_header* hdr);
+
+/* Pack one keyframe (device arrays, e.g. an orbx_extract_batch_device frame + its
+ * orbv_transform_batch_device BoW) into d_slot (orbx_slot_bytes(cap) bytes), enqueued on
+ * `stream`. Counts above cap are clamped to cap and raise bit 0 of *d_err (optional device int). */
+int orbx_pack_keyframe_device(const orbx_kf_source* src, const orbx_kf_meta* meta, int cap,
+                              uint8_t* d_slot, int32_t* d_err, void* stream);
+/* The same from host arrays into a host slot (byte-identical to the device pack). ORBX_ECAPACITY
+ * if a count exceeds cap. */
+int orbx_pack_keyframe_host(const orbx_kf_source* src, const orbx_kf_meta* meta, int cap,
+                            uint8_t* slot, size_t slot_bytes);
+
+/* A validated view of a received slot in host memory: magic/version, cap vs slot_bytes, every
+ * section offset, n/nbow/nfv <= cap, the FeatureVector CSR (offsets monotone, node ids and word
+ * ids strictly ascending, feature indices < n and ascending within a node). ORBX_EARG if any
+ * check fails. Pointers alias `slot`. */
+typedef struct orbx_slot_view {
+    const orbx_slot_header* hdr;
+    const orbx_kf_meta* meta;
+    const orbx_kp* kps;
+    const float* kun;
+    const float* uright;
+    const float* depth;
+    const uint8_t* desc;
+    const uint8_t* mp_flags;
+    const float* mp_pos;
+    const uint32_t* bow_word;
+    const double* bow_value;
+    const uint32_t* fv_node;
+    const int32_t* fv_off;
+    const int32_t* fv_feat;
+} orbx_slot_view;
+int orbx_slot_parse(const uint8_t* slot, size_t slot_bytes, orbx_slot_view* out);
+
+/* Geometry of one (query keyframe, slot keyframe) pair: F12 (LocalMapping::ComputeF12,
+ * LocalMapping.cc:536-553) and the epipole (ex, ey) of the query's centre in the slot's
+ * keyframe (ORBmatcher.cc:664-670). */
+typedef struct orbm_slot_geom {
+    float F12[9];
+    float ex, ey;
+} orbm_slot_geom;
+
+/* Cross-agent ORBmatcher::SearchForTriangulation(query KF, slot KF, F12, vMatchedPairs,
+ * bOnlyStereo = false) (ORBmatcher.cc:657-823) of this agent's keyframe (`query`, device
+ * arrays: kps/desc/count, optional kun, uright, mp_flags and, with use_bow, its FeatureVector)
+ * against nref received slots at d_slots + r*slot_bytes (e.g. the all-gather receive buffer),
+ * straight from device memory. Per slot: geom[r] (host array), the slot keyframe's
+ * mvScaleFactors / mvLevelSigma2 from its meta, its mvKeysUn / mvuRight / MapPoint flags.
+ * use_bow = 0: one node holding every feature (brute force, the BASELINE configuration);
+ * use_bow = 1: the common nodes of the two FeatureVectors (query nodes <= max_nodes).
+ * Outputs d_match[r*cap1 + idx1] (idx2 or -1), d_nmatches[r]. A slot that fails validation
+ * (magic, version, size, counts, CSR bounds) contributes no matches and raises the ctx's
+ * device error flag (orbm_check_error). */
+int orbm_search_for_triangulation_slots_device(orbm_ctx* ctx, const orbx_kf_source* query, int cap1,
+                                               int nref, const uint8_t* d_slots, size_t slot_bytes,
+                                               const orbm_slot_geom* geom, int use_bow, int max_nodes,
+                                               int32_t* d_match, int32_t* d_nmatches, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Stereo -- replaces Frame::ComputeStereoMatches (ORB_SLAM2.1/src/Frame.cc:470-641, the

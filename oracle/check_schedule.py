@@ -1,0 +1,91 @@
+"""Checker of the bench schedule's outputs against the CPU oracle (test infrastructure).
+
+Used by tests/test_gpu_schedule.py and by bench.py after its timed region (the oracle is the
+checker here, never the measured path): recomputes, for sampled frames of an
+orbamd.agent.AgentSchedule step, ORBextractor::operator() (oracle/orb_oracle.c) and the BF
+SearchForTriangulation against the previous frame of the same graph, and the cross-agent
+SearchForTriangulation of this agent's keyframe against every agent's keyframe, and compares
+every keypoint field (raw float bits), descriptor byte and match index with the device results.
+"""
+import os
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+import oracle_py  # noqa: E402
+
+
+def host_threads():
+    """CPU threads this process may use: the affinity set, capped by the cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except Exception:
+        pass
+    return max(1, n)
+
+
+def check_schedule(sched, frames_np, samples=None, agent_frames=None, threads=None, nfeatures=None):
+    """samples: list of (graph p, frame b) to check (default: first, middle and last frame of each
+    graph, plus each one's predecessor so the match row can be recomputed); agent_frames(r) -> the
+    keyframe image of agent r (default: frames_np[0] for every agent, i.e. world 1).
+    Returns dict(bit_exact, checked_frames, checked_pairs, checked_slots, mismatches[...])."""
+    import orbamd
+    sub = sched.sub
+    nfeat = nfeatures or getattr(sched, "nfeatures", 1000)
+    if samples is None:
+        samples = sorted({(p, b) for p in range(sched.P) for b in (0, sub // 2, sub - 1)})
+    F12, ex, ey = orbamd.device.default_geometry()
+    tabs = oracle_py.OracleExtractor(nfeat, 1.2, 8, 20, 7).tables()
+    need = set()
+    for p, b in samples:
+        need.add((p, b))
+        need.add((p, (b - 1) % sub))
+    need = sorted(need)
+    local = {}
+
+    def extract(img):
+        orc = oracle_py.OracleExtractor(nfeat, 1.2, 8, 20, 7)
+        return orc(img)
+
+    threads = threads or host_threads()
+    with ThreadPoolExecutor(max_workers=threads) as ex_pool:
+        outs = list(ex_pool.map(lambda pb: extract(frames_np[pb[0] * sub + pb[1]]), need))
+    for pb, o in zip(need, outs):
+        local[pb] = o
+    mism = []
+    for p, b in samples:
+        kg, dg, mg = sched.frame_results(p, b)
+        ko, do = local[(p, b)]
+        if len(kg) != len(ko) or kg.tobytes() != ko.tobytes() or not np.array_equal(dg, do):
+            mism.append("frame p=%d b=%d: %d vs %d keypoints or differing fields" % (p, b, len(kg), len(ko)))
+            continue
+        kp, dp = local[(p, (b - 1) % sub)]
+        v1 = orbamd.KeyFrameView(ko, do, tabs["scale"], tabs["sigma2"])
+        v2 = orbamd.KeyFrameView(kp, dp, tabs["scale"], tabs["sigma2"])
+        _, mo = oracle_py.search_for_triangulation(v1, v2, F12, ex, ey, False, False)
+        if not np.array_equal(mg, mo):
+            mism.append("match p=%d b=%d vs b-1: %d entries differ" % (p, b, int((mg != mo).sum())))
+    nslots = 0
+    if sched.exchange_on:
+        xm, xn = sched.exchange_results()
+        kq, dq = local.get((0, 0)) or extract(frames_np[0])
+        vq = orbamd.KeyFrameView(kq, dq, tabs["scale"], tabs["sigma2"])
+        for r in range(sched.world):
+            img = frames_np[0] if agent_frames is None else agent_frames(r)
+            kr, dr = extract(img) if agent_frames is not None else (kq, dq)
+            vr = orbamd.KeyFrameView(kr, dr, tabs["scale"], tabs["sigma2"])
+            n_o, mo = oracle_py.search_for_triangulation(vq, vr, F12, ex, ey, False, False)
+            if not np.array_equal(xm[r], mo) or int(xn[r]) != int(n_o):
+                mism.append("cross-agent match vs agent %d: %d entries differ, count %d vs %d"
+                            % (r, int((xm[r] != mo).sum()), int(xn[r]), int(n_o)))
+            nslots += 1
+    return {"bit_exact": not mism, "checked_frames": len(samples), "checked_pairs": len(samples),
+            "checked_slots": nslots, "mismatches": mism[:8]}

@@ -12,3 +12,10 @@ g++ -std=c++14 -O1 -Wall -Wno-unused-function \
   -L "$R/cooperative-orb-slam_amd/lib" -lorbamd -L "$R/oracle/build" -lorb_oracle \
   -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,"$R/oracle/build" -Wl,-rpath,/opt/rocm/lib \
   -o "$R/tests/cpp/build/test_dropin"
+# the slot codec (host only, no GPU needed to run)
+g++ -std=c++14 -O1 -Wall -Wno-unused-function \
+  -I "$R/tests/cpp/cvmin" -I "$R/tests/cpp/mock" -I "$R/cooperative-orb-slam_amd/host" -I "$R/include" \
+  "$R/tests/cpp/test_slot.cpp" "$R/cooperative-orb-slam_amd/host/KeyFrameSlot_amd.cc" \
+  -L "$R/cooperative-orb-slam_amd/lib" -lorbamd \
+  -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,/opt/rocm/lib \
+  -o "$R/tests/cpp/build/test_slot"

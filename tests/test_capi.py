@@ -9,7 +9,6 @@ import numpy as np
 import pytest
 
 import orbamd
-from orbamd import exchange
 from orbamd._lib import SIGNATURES, OrbxParams
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -77,17 +76,3 @@ def test_bad_arguments():
     assert lib.orbx_create(None, 0, 640, 480, 1, C.byref(h)) == -1
     p = OrbxParams(1000, 1.2, 99, 20, 7)
     assert lib.orbx_create(C.byref(p), 0, 640, 480, 1, C.byref(h)) == -1
-
-
-def test_slot_layout_roundtrip():
-    assert orbamd.load().orbx_slot_bytes(1031) == exchange.slot_bytes(1031)
-    rng = np.random.default_rng(1)
-    n = 700
-    k = np.zeros(n, exchange.KP_DTYPE)
-    for f in ("x", "y", "size", "angle", "response"):
-        k[f] = rng.random(n, dtype=np.float32) * 500
-    k["octave"] = rng.integers(0, 8, n)
-    d = rng.integers(0, 256, (n, 32), dtype=np.uint8)
-    buf = exchange.pack_slot_host(k, d, 1031)
-    k2, d2 = exchange.unpack_slot_host(buf)
-    assert k2.tobytes() == k.tobytes() and np.array_equal(d2, d)

@@ -25,3 +25,13 @@ def test_dropin_bit_exact_on_gpu():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout[-4000:], r.stderr[-2000:])
     assert r.returncode == 0 and "ALL PASS" in r.stdout
+
+
+def test_slot_codec_roundtrip_cpp():
+    """host/KeyFrameSlot_amd.*: receiveKeyframeInfo -> slot -> receiveKeyframeInfo, field for field (CPU)"""
+    _build()
+    env = dict(os.environ, ORBAMD_NO_TORCH="1")
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "build", "test_slot")], capture_output=True, text=True,
+                       timeout=120, env=env)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0 and "ALL PASS" in r.stdout

@@ -1,5 +1,6 @@
-"""Multi-agent exchange on CPU: world_size-2 gloo all-gather of packed keyframe slots and the
-cross-agent SearchForTriangulation (oracle as the matcher) equal a single-process run that
+"""Multi-agent exchange on CPU: world_size-2 gloo all-gather of keyframe slots (packed by the
+library's host packer, orbx_pack_keyframe_host; decoded by its validating parser, orbx_slot_parse)
+and the cross-agent SearchForTriangulation (oracle as the matcher) equal a single-process run that
 matches the concatenated buffers."""
 import os
 import socket
@@ -27,6 +28,12 @@ def _agent_keyframe(agent):
     return k, d, orc.tables()
 
 
+def _pack(agent, k, d, tabs, cap):
+    from orbamd import exchange
+    meta = exchange.make_meta(agent=agent, mnId=agent, scale=tabs["scale"], sigma2=tabs["sigma2"])
+    return exchange.pack_host(meta, k, d, cap)
+
+
 def _cross_match(kq, dq, tabs, slots):
     import oracle_py
     import orbamd
@@ -35,8 +42,9 @@ def _cross_match(kq, dq, tabs, slots):
     out = []
     vq = orbamd.KeyFrameView(kq, dq, tabs["scale"], tabs["sigma2"])
     for buf in slots:
-        k2, d2 = exchange.unpack_slot_host(buf)
-        v2 = orbamd.KeyFrameView(k2, d2, tabs["scale"], tabs["sigma2"])
+        got = exchange.parse(buf)
+        k2, d2 = got["kps"], got["desc"]
+        v2 = orbamd.KeyFrameView(k2, d2, got["meta"].mvScaleFactors[:8], got["meta"].mvLevelSigma2[:8])
         out.append(oracle_py.search_for_triangulation(vq, v2, F12, ex, ey, False, False)[1])
     return out
 
@@ -52,7 +60,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     k, d, tabs = _agent_keyframe(rank)
     cap = 1031
-    mine = torch.from_numpy(exchange.pack_slot_host(k, d, cap))
+    mine = torch.from_numpy(_pack(rank, k, d, tabs, cap))
     allb = torch.empty(world * mine.numel(), dtype=torch.uint8)
     dist.all_gather_into_tensor(allb, mine)
     slots = allb.numpy().reshape(world, -1)
@@ -77,7 +85,7 @@ def test_gloo_allgather_cross_agent_match():
         p.join(timeout=60)
         assert p.exitcode == 0
     kfs = [_agent_keyframe(a) for a in range(world)]
-    slots = [exchange.pack_slot_host(k, d, 1031) for k, d, _ in kfs]
+    slots = [_pack(a, k, d, t, 1031) for a, (k, d, t) in enumerate(kfs)]
     for r in range(world):
         exp = _cross_match(kfs[r][0], kfs[r][1], kfs[r][2], slots)
         assert [e.tolist() for e in exp] == got[r]

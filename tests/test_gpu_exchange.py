@@ -1,0 +1,236 @@
+"""GPU: the cross-agent keyframe exchange on the product path.
+
+* orbx_pack_keyframe_device writes the same bytes as the host packer (every field the receiving
+  agent consumes: mvKeys/mvKeysUn/mvuRight/mvDepth/descriptors/MapPoints/BowVector/FeatureVector +
+  the lcmKeyFrameInfo scalars), clamps an over-capacity count and flags it;
+* orbm_search_for_triangulation_slots_device (brute force and over common BoW nodes, stereo and
+  MapPoint flags on both sides, a different geometry per slot) equals the oracle's
+  SearchForTriangulation (ORBmatcher.cc:657-823) on the decoded slots; a corrupt slot yields no
+  matches and raises the matcher's error flag while the others stay exact;
+* two agents in two processes on cuda:0: device extract -> device pack -> all-gather -> slot match,
+  against the oracle (the agents exchange over gloo here; the product run uses RCCL over xGMI).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_py
+import orbamd
+from orbamd import exchange
+from orbamd.matcher import KeyFrameView
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _cuda(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _extract(agent, t, n=1, W=640, H=480, nf=1000):
+    orc = oracle_py.OracleExtractor(nf, 1.2, 8, 20, 7)
+    return [orc(img) for img in orbamd.synth_frames(agent, t, n, W, H)], orc.tables()
+
+
+def _extras(rng, k, with_fv=True):
+    n = len(k)
+    ur = np.where(rng.random(n) < 0.4, k["x"] - rng.random(n, dtype=np.float32) * 40, -1).astype(np.float32)
+    kun = (np.stack([k["x"], k["y"]], 1) + (rng.random((n, 2), dtype=np.float32) - 0.5)).astype(np.float32)
+    e = dict(kun=kun, uright=ur, depth=np.where(ur >= 0, np.float32(3.5), np.float32(-1)).astype(np.float32),
+             mp_flags=((rng.random(n) < 0.25).astype(np.uint8) | ((rng.random(n) < 0.1).astype(np.uint8) << 1)),
+             mp_pos=rng.standard_normal((n, 3)).astype(np.float32))
+    if with_fv:
+        nodes = np.sort(rng.choice(3000, 48, replace=False)).astype(np.uint32)
+        assign = rng.integers(0, len(nodes), n)
+        feats = [np.nonzero(assign == i)[0] for i in range(len(nodes))]
+        keep = [i for i in range(len(nodes)) if len(feats[i])]
+        nodes = nodes[keep]
+        feats = [feats[i] for i in keep]
+        off = np.concatenate([[0], np.cumsum([len(f) for f in feats])]).astype(np.int32)
+        e["fv"] = (nodes, off, np.concatenate(feats).astype(np.int32))
+        words = np.sort(rng.choice(10 ** 6, 200, replace=False)).astype(np.uint32)
+        e["bow"] = (words, rng.random(200))
+    return e
+
+
+def _device_source(torch, k, d, e):
+    n = len(k)
+    t = {"kps": _cuda(torch, np.ascontiguousarray(k, exchange.KP_DTYPE).view(np.uint8)), "desc": _cuda(torch, d),
+         "count": _cuda(torch, np.array([n], np.int32))}
+    for key in ("kun", "uright", "depth", "mp_flags", "mp_pos"):
+        if key in e:
+            t[key] = _cuda(torch, e[key])
+    if "bow" in e:
+        t.update(bow_word=_cuda(torch, e["bow"][0]), bow_value=_cuda(torch, e["bow"][1]),
+                 nbow=_cuda(torch, np.array([len(e["bow"][0])], np.int32)))
+    if "fv" in e:
+        t.update(fv_node=_cuda(torch, e["fv"][0]), fv_off=_cuda(torch, e["fv"][1]), fv_feat=_cuda(torch, e["fv"][2]),
+                 nfv=_cuda(torch, np.array([len(e["fv"][0])], np.int32)))
+    return exchange.kf_source(**t), t
+
+
+def _meta(agent, tabs):
+    return exchange.make_meta(agent=agent, mnId=7 + agent, scale=tabs["scale"], sigma2=tabs["sigma2"],
+                              inv_sigma2=tabs["inv_sigma2"], bf=40.0, b=0.11, th_depth=35.0)
+
+
+@pytest.mark.parametrize("full", [True, False])
+def test_device_pack_equals_host_pack(full):
+    torch = pytest.importorskip("torch")
+    (res,), tabs = _extract(0, 3)
+    k, d = res
+    rng = np.random.default_rng(1)
+    e = _extras(rng, k) if full else {}
+    meta = _meta(0, tabs)
+    cap = 1100
+    src, keep = _device_source(torch, k, d, e)
+    slot = torch.full((exchange.slot_bytes(cap),), 0xAB, dtype=torch.uint8, device="cuda")  # dirty buffer
+    err = torch.zeros(4, dtype=torch.int32, device="cuda")
+    exchange.pack_device(src, meta, cap, slot, err)
+    torch.cuda.synchronize()
+    host = exchange.pack_host(meta, k, d, cap, **e)
+    got = slot.cpu().numpy()
+    assert got.tobytes() == host.tobytes()
+    assert int(err[0].item()) == 0
+    dec = exchange.parse(got)
+    assert dec["kps"].tobytes() == k.tobytes() and np.array_equal(dec["desc"], d)
+    if full:
+        for key in ("kun", "uright", "depth", "mp_flags", "mp_pos"):
+            assert np.array_equal(dec[key], e[key]), key
+        assert np.array_equal(dec["fv_feat"], e["fv"][2]) and np.array_equal(dec["bow_value"], e["bow"][1])
+
+
+def test_device_pack_clamps_and_flags_overflow():
+    torch = pytest.importorskip("torch")
+    (res,), tabs = _extract(0, 5)
+    k, d = res
+    cap = 600
+    assert len(k) > cap
+    src, keep = _device_source(torch, k, d, {})
+    slot = torch.zeros(exchange.slot_bytes(cap), dtype=torch.uint8, device="cuda")
+    err = torch.zeros(4, dtype=torch.int32, device="cuda")
+    exchange.pack_device(src, _meta(0, tabs), cap, slot, err)
+    torch.cuda.synchronize()
+    assert int(err[0].item()) & 1
+    dec = exchange.parse(slot.cpu().numpy())
+    assert dec["n"] == cap and dec["kps"].tobytes() == k[:cap].tobytes()
+
+
+def _oracle_slot_match(kq, dq, eq, dec, geo, use_bow):
+    """oracle SearchForTriangulation(query KF, slot KF) with mvKeysUn / mvuRight / MapPoints from both sides"""
+    F12, ex, ey = geo
+    m = dec["meta"]
+    nl = m.mnScaleLevels
+    scale = np.array(m.mvScaleFactors[:nl], np.float32)
+    sig = np.array(m.mvLevelSigma2[:nl], np.float32)
+
+    def view(k, d, e, fvd, sc, sg):
+        kk = k.copy()
+        if e.get("kun") is not None:
+            kk["x"], kk["y"] = e["kun"][:, 0], e["kun"][:, 1]
+        fv = None
+        if use_bow:
+            node, off, feat = fvd
+            fv = {int(node[i]): list(feat[off[i]:off[i + 1]]) for i in range(len(node))}
+        has_mp = None if e.get("mp_flags") is None else (e["mp_flags"] & 1).astype(bool)
+        return KeyFrameView(kk, d, sc, sg, feat_vec=fv, uright=e.get("uright"), has_mp=has_mp)
+
+    vq = view(kq, dq, eq, eq.get("fv"), scale, sig)
+    ds = {"kun": dec["kun"], "uright": dec["uright"], "mp_flags": dec["mp_flags"]}
+    vs = view(dec["kps"], dec["desc"], ds, (dec["fv_node"], dec["fv_off"], dec["fv_feat"]), scale, sig)
+    return oracle_py.search_for_triangulation(vq, vs, F12, ex, ey, False, False)
+
+
+@pytest.mark.parametrize("use_bow", [False, True])
+def test_slot_match_equals_oracle(use_bow):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(17)
+    frames, tabs = _extract(1, 0, n=4)
+    cap = 1100
+    nref = 3
+    # query = frame 0 (stereo + MapPoints + FeatureVector); slots = frames 1..3 of agents 0..2
+    kq, dq = frames[0]
+    eq = _extras(rng, kq)
+    srcq, keepq = _device_source(torch, kq, dq, eq)
+    slots = torch.zeros(nref * exchange.slot_bytes(cap), dtype=torch.uint8, device="cuda")
+    decs = []
+    for r in range(nref):
+        k, d = frames[1 + r]
+        e = _extras(rng, k) if r != 1 else ({"fv": _extras(rng, k)["fv"]} if use_bow else {})  # slot 1 mono
+        host = exchange.pack_host(_meta(r, tabs), k, d, cap, **e)
+        slots[r * host.size:(r + 1) * host.size].copy_(torch.from_numpy(host))
+        decs.append(exchange.parse(host))
+    R = [np.eye(3, dtype=np.float32), np.array([[0.9998, -0.02, 0], [0.02, 0.9998, 0], [0, 0, 1]], np.float32),
+         np.eye(3, dtype=np.float32)]
+    t = [np.array([0.05, 0, 0.01], np.float32), np.array([-0.1, 0.02, 0.0], np.float32),
+         np.array([0.0, 0.08, -0.02], np.float32)]
+    K = np.array([[orbamd.device.FX, 0, orbamd.device.CX], [0, orbamd.device.FY, orbamd.device.CY], [0, 0, 1]],
+                 np.float32)
+    geos = []
+    for r in range(nref):
+        F12 = orbamd.matcher.compute_f12(np.eye(3), np.zeros(3), R[r], t[r], K, K)
+        ex, ey = orbamd.epipole(R[r], t[r], np.zeros(3, np.float32), orbamd.device.FX, orbamd.device.FY,
+                                orbamd.device.CX, orbamd.device.CY)
+        geos.append((F12, ex, ey))
+    mh = orbamd.ORBmatcher(0.6, False)
+    out = torch.empty((nref, cap), dtype=torch.int32, device="cuda")
+    nm = torch.zeros(nref, dtype=torch.int32, device="cuda")
+    exchange.match_slots_device(mh._h, srcq, cap, nref, slots, exchange.slot_bytes(cap), geos, out, nm,
+                                use_bow=use_bow, max_nodes=len(eq["fv"][0]))
+    torch.cuda.synchronize()
+    assert orbamd.load().orbm_check_error(mh._h, None) == 0
+    total = 0
+    for r in range(nref):
+        no, mo = _oracle_slot_match(kq, dq, eq, decs[r], geos[r], use_bow)
+        np.testing.assert_array_equal(out[r, :len(kq)].cpu().numpy(), mo)
+        assert int(nm[r].item()) == no
+        assert np.all(out[r, len(kq):].cpu().numpy() == -1)
+        total += no
+    assert total > 0
+    # a corrupt slot (foreign version) in the middle: no matches, error flag, the others unchanged
+    bad = slots.clone()
+    sb = exchange.slot_bytes(cap)
+    bad[sb + 4:sb + 8] = torch.tensor([1, 0, 0, 0], dtype=torch.uint8)
+    out2 = torch.empty_like(out)
+    exchange.match_slots_device(mh._h, srcq, cap, nref, bad, sb, geos, out2, nm, use_bow=use_bow,
+                                max_nodes=len(eq["fv"][0]))
+    torch.cuda.synchronize()
+    assert orbamd.load().orbm_check_error(mh._h, None) == -2
+    assert orbamd.load().orbm_check_error(mh._h, None) == 0  # cleared by the read
+    assert np.all(out2[1].cpu().numpy() == -1) and int(nm[1].item()) == 0
+    assert torch.equal(out2[0], out[0]) and torch.equal(out2[2], out[2])
+    mh.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_agents_exchange_on_device():
+    """two agent processes (fresh children, both on cuda:0): AgentSchedule step with the device pack ->
+    all-gather -> slot match, every rank checked against the oracle by oracle/check_schedule.py"""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    script = os.path.join(ROOT, "tests", "agent_child.py")
+    procs = [subprocess.Popen([sys.executable, script], env=dict(env, RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            o, _ = p.communicate()
+        outs.append(o)
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        print(o[-3000:])
+        assert p.returncode == 0, "rank %d failed" % r
+        assert "AGENT OK" in o

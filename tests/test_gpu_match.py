@@ -30,10 +30,18 @@ def _random_featvec(rng, n, nodes):
                                                     for a in range(nodes)}
 
 
+# the BASELINE geometries: C2 640x480/1000, C3 752x480/1200, C4 1241x376/2000, and the monocular
+# initialisation extractor (2000 features at 640x480, Tracking.cc:119-125); every n2 spans many
+# 64-candidate MFMA chunks and 512-candidate SIMT tiles
+CONFIGS = [(640, 480, 1000), (752, 480, 1200), (1241, 376, 2000), (640, 480, 2000)]
+
+
+@pytest.mark.parametrize("W,H,nf", CONFIGS)
 @pytest.mark.parametrize("check_ori", [False, True])
-def test_triangulation_bf(check_ori):
-    (k1, d1), (k2, d2) = _frames_kf(0, 0)[0]
-    tabs = _frames_kf(0, 0, 1)[1]
+def test_triangulation_bf(check_ori, W, H, nf):
+    (k1, d1), (k2, d2) = _frames_kf(0, 0, W=W, H=H, nf=nf)[0]
+    tabs = _frames_kf(0, 0, 1, W=W, H=H, nf=nf)[1]
+    assert len(k1) > 0.9 * nf and len(k2) > 0.9 * nf
     F12, ex, ey = orbamd.device.default_geometry()
     v1, v2 = _view(k1, d1, tabs), _view(k2, d2, tabs)
     m = orbamd.ORBmatcher(0.6, check_ori)
@@ -99,14 +107,18 @@ def test_search_by_bow(kfkf, nodes):
         np.testing.assert_array_equal(mg, mo)
 
 
-def test_batch_pairs_match_oracle():
+@pytest.mark.parametrize("W,H,nf", CONFIGS)
+@pytest.mark.parametrize("check_ori", [False, True])
+def test_batch_pairs_match_oracle(W, H, nf, check_ori):
+    """the MFMA batch kernel (k_tri_mfma) at every BASELINE geometry, rotation filter on and off"""
     torch = pytest.importorskip("torch")
-    W, H, B = 640, 480, 4
+    B = 4
     frames = orbamd.synth_frames(0, 0, B, W, H)
-    pipe = orbamd.device.BatchPipeline(torch, W, H, B)
+    pipe = orbamd.device.BatchPipeline(torch, W, H, B, nfeatures=nf, check_ori=check_ori)
     pipe.step(torch.from_numpy(frames).cuda())
     torch.cuda.synchronize()
-    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    pipe.check_error()
+    orc = oracle_py.OracleExtractor(nf, 1.2, 8, 20, 7)
     tabs = orc.tables()
     res = [orc(frames[b]) for b in range(B)]
     for b in range(B):
@@ -114,9 +126,10 @@ def test_batch_pairs_match_oracle():
         pb = (b + B - 1) % B
         v1 = _view(res[b][0], res[b][1], tabs)
         v2 = _view(res[pb][0], res[pb][1], tabs)
-        no, mo = oracle_py.search_for_triangulation(v1, v2, pipe.F12, pipe.ex, pipe.ey, False, False)
+        assert kg.tobytes() == res[b][0].tobytes() and np.array_equal(dg, res[b][1])
+        no, mo = oracle_py.search_for_triangulation(v1, v2, pipe.F12, pipe.ex, pipe.ey, False, check_ori)
         np.testing.assert_array_equal(mg, mo)
-        assert int(pipe.nmatch[b].item()) == no
+        assert int(pipe.nmatch[b].item()) == no and no > 0
     pipe.close()
 
 
