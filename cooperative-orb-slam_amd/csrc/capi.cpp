@@ -1051,7 +1051,6 @@ bool view_ok(const orbm_kf_view* v) {
            v->scale_factors && v->level_sigma2;
 }
 
-/* upload one view into the scratch at offsets computed by plan_view */
 struct ViewPlan {
     size_t desc, x, y, angle, octave, uright, has_mp, mp_bad, feat;
     int nfeat;
@@ -1069,32 +1068,34 @@ void plan_view(Carve& c, const orbm_kf_view* v, ViewPlan& p) {
     p.mp_bad = v->mp_bad ? c.take(n) : (size_t)-1;
     p.feat = c.take(4 * (size_t)std::max(p.nfeat, 1));
 }
-int upload_view(orbm_ctx* ctx, const orbm_kf_view* v, const ViewPlan& p, DevView& d) {
-    uint8_t* base = ctx->scratch.as<uint8_t>();
-    hipStream_t st = ctx->stream;
+
+/* stage one view into the pinned host image of the scratch (offsets from plan_view) and return
+ * the device view of the same offsets: a call then uploads all its inputs with ONE H2D copy */
+DevView stage_view(uint8_t* hbase, uint8_t* dbase, const orbm_kf_view* v, const ViewPlan& p) {
+    DevView d;
     const size_t n = (size_t)v->n;
     d.n = v->n;
-    d.desc = base + p.desc;
-    d.x = (const float*)(base + p.x);
-    d.y = (const float*)(base + p.y);
-    d.angle = (const float*)(base + p.angle);
-    d.octave = (const int32_t*)(base + p.octave);
-    d.uright = v->uright ? (const float*)(base + p.uright) : nullptr;
-    d.has_mp = v->has_mp ? base + p.has_mp : nullptr;
-    d.mp_bad = v->mp_bad ? base + p.mp_bad : nullptr;
-    d.node_feat = (const int32_t*)(base + p.feat);
+    d.desc = dbase + p.desc;
+    d.x = (const float*)(dbase + p.x);
+    d.y = (const float*)(dbase + p.y);
+    d.angle = (const float*)(dbase + p.angle);
+    d.octave = (const int32_t*)(dbase + p.octave);
+    d.uright = v->uright ? (const float*)(dbase + p.uright) : nullptr;
+    d.has_mp = v->has_mp ? dbase + p.has_mp : nullptr;
+    d.mp_bad = v->mp_bad ? dbase + p.mp_bad : nullptr;
+    d.node_feat = (const int32_t*)(dbase + p.feat);
     if (n) {
-        HIPR(hipMemcpyAsync(base + p.desc, v->desc, 32 * n, hipMemcpyHostToDevice, st));
-        HIPR(hipMemcpyAsync(base + p.x, v->x, 4 * n, hipMemcpyHostToDevice, st));
-        HIPR(hipMemcpyAsync(base + p.y, v->y, 4 * n, hipMemcpyHostToDevice, st));
-        HIPR(hipMemcpyAsync(base + p.angle, v->angle, 4 * n, hipMemcpyHostToDevice, st));
-        HIPR(hipMemcpyAsync(base + p.octave, v->octave, 4 * n, hipMemcpyHostToDevice, st));
-        if (v->uright) HIPR(hipMemcpyAsync(base + p.uright, v->uright, 4 * n, hipMemcpyHostToDevice, st));
-        if (v->has_mp) HIPR(hipMemcpyAsync(base + p.has_mp, v->has_mp, n, hipMemcpyHostToDevice, st));
-        if (v->mp_bad) HIPR(hipMemcpyAsync(base + p.mp_bad, v->mp_bad, n, hipMemcpyHostToDevice, st));
+        memcpy(hbase + p.desc, v->desc, 32 * n);
+        memcpy(hbase + p.x, v->x, 4 * n);
+        memcpy(hbase + p.y, v->y, 4 * n);
+        memcpy(hbase + p.angle, v->angle, 4 * n);
+        memcpy(hbase + p.octave, v->octave, 4 * n);
+        if (v->uright) memcpy(hbase + p.uright, v->uright, 4 * n);
+        if (v->has_mp) memcpy(hbase + p.has_mp, v->has_mp, n);
+        if (v->mp_bad) memcpy(hbase + p.mp_bad, v->mp_bad, n);
     }
-    if (p.nfeat) HIPR(hipMemcpyAsync(base + p.feat, v->node_feat, 4 * (size_t)p.nfeat, hipMemcpyHostToDevice, st));
-    return 0;
+    if (p.nfeat) memcpy(hbase + p.feat, v->node_feat, 4 * (size_t)p.nfeat);
+    return d;
 }
 
 }  // namespace
@@ -1183,14 +1184,15 @@ int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const 
     plan_view(cv, kf1, p1);
     plan_view(cv, kf2, p2);
     const size_t o_tasks = cv.take(sizeof(NodeTask) * std::max<size_t>(tasks.size(), 1));
+    const size_t in_bytes = cv.off;
     const size_t o_out = cv.take(4 * (size_t)std::max(kf1->n, 1));
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
-    DevView d1, d2;
-    if (upload_view(ctx, kf1, p1, d1) || upload_view(ctx, kf2, p2, d2)) return ORBX_EDEVICE;
+    uint8_t* hp = ctx->ensure_pinned(cv.off);
+    if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
-    if (!tasks.empty())
-        HIPR(hipMemcpyAsync(base + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size(), hipMemcpyHostToDevice,
-                            ctx->stream));
+    DevView d1 = stage_view(hp, base, kf1, p1), d2 = stage_view(hp, base, kf2, p2);
+    if (!tasks.empty()) memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
+    HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     int32_t* dout = (int32_t*)(base + o_out);
     HIPR(hipMemsetAsync(dout, 0xFF, 4 * (size_t)std::max(kf1->n, 1), ctx->stream));
     MatchGeom g;
@@ -1198,8 +1200,9 @@ int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const 
     HIPR(launch_tri_nodes(d1, d2, (const NodeTask*)(base + o_tasks), (int)tasks.size(), g, only_stereo, dout,
                           ctx->stream));
     if (check_ori) HIPR(launch_rot_filter(kf1->n, dout, d1.angle, d2.angle, 0, nullptr, ctx->stream));
-    if (kf1->n) HIPR(hipMemcpyAsync(match12, dout, 4 * (size_t)kf1->n, hipMemcpyDeviceToHost, ctx->stream));
+    if (kf1->n) HIPR(hipMemcpyAsync(hp + o_out, dout, 4 * (size_t)kf1->n, hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipStreamSynchronize(ctx->stream));
+    if (kf1->n) memcpy(match12, hp + o_out, 4 * (size_t)kf1->n);
     if (nmatches) *nmatches = count_matches(match12, kf1->n);
     return 0;
 }
@@ -1223,14 +1226,15 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
     plan_view(cv, vq, pq);
     plan_view(cv, vc, pc);
     const size_t o_tasks = cv.take(sizeof(NodeTask) * std::max<size_t>(tasks.size(), 1));
+    const size_t in_bytes = cv.off;
     const size_t o_out = cv.take(4 * (size_t)std::max(nout, 1));
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
-    DevView dq, dc;
-    if (upload_view(ctx, vq, pq, dq) || upload_view(ctx, vc, pc, dc)) return ORBX_EDEVICE;
+    uint8_t* hp = ctx->ensure_pinned(cv.off);
+    if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
-    if (!tasks.empty())
-        HIPR(hipMemcpyAsync(base + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size(), hipMemcpyHostToDevice,
-                            ctx->stream));
+    DevView dq = stage_view(hp, base, vq, pq), dc = stage_view(hp, base, vc, pc);
+    if (!tasks.empty()) memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
+    HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     int32_t* dout = (int32_t*)(base + o_out);
     HIPR(hipMemsetAsync(dout, 0xFF, 4 * (size_t)std::max(nout, 1), ctx->stream));
     HIPR(launch_bow(dq, dc, (const NodeTask*)(base + o_tasks), (int)tasks.size(), max_nc, nnratio, mode, dout,
@@ -1241,8 +1245,9 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
         else
             HIPR(launch_rot_filter(nout, dout, dq.angle, dc.angle, 0, nullptr, ctx->stream));
     }
-    if (nout) HIPR(hipMemcpyAsync(out, dout, 4 * (size_t)nout, hipMemcpyDeviceToHost, ctx->stream));
+    if (nout) HIPR(hipMemcpyAsync(hp + o_out, dout, 4 * (size_t)nout, hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipStreamSynchronize(ctx->stream));
+    if (nout) memcpy(out, hp + o_out, 4 * (size_t)nout);
     if (nmatches) *nmatches = count_matches(out, nout);
     return 0;
 }

@@ -21,10 +21,12 @@ static void orbx_ok(int rc, const char* what) {
 
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
     : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
-      minThFAST(_minThFAST), mpHandle(nullptr), mHandleW(0), mHandleH(0), mDevice(0), mbHostPyramid(true) {
+      minThFAST(_minThFAST), mpHandle(nullptr), mHandleW(0), mHandleH(0), mDevice(0), mbHostPyramid(false),
+      mbPyramidStale(false) {
     const char* dev = getenv("ORBAMD_DEVICE");
     if (dev) mDevice = atoi(dev);
-    if (getenv("ORBAMD_NO_HOST_PYRAMID")) mbHostPyramid = false;
+    const char* hp = getenv("ORBAMD_HOST_PYRAMID");
+    if (hp && atoi(hp) != 0) mbHostPyramid = true;
     // the tables are computed by the library with the reference's float semantics
     // (ORBextractor.cc:415-431); a probe handle at 640x480 answers the getters.
     ensureHandle(640, 480);
@@ -83,15 +85,21 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask, std::
     const orbx_kp* k = (const orbx_kp*)mKpBuf.data();
     for (int i = 0; i < n; i++)
         _keypoints.push_back(cv::KeyPoint(k[i].x, k[i].y, k[i].size, k[i].angle, k[i].response, k[i].octave, -1));
-    if (mbHostPyramid) {
-        for (int l = 0; l < nlevels; l++) {
-            int w = 0, h = 0;
-            orbx_ok(orbx_pyramid_level(mpHandle, 0, l, nullptr, 0, &w, &h), "orbx_pyramid_level");
-            mvImagePyramid[l].create(h, w, CV_8U);
-            orbx_ok(orbx_pyramid_level(mpHandle, 0, l, mvImagePyramid[l].data, mvImagePyramid[l].step, &w, &h),
-                    "orbx_pyramid_level");
-        }
+    mbPyramidStale = true;
+    if (mbHostPyramid) SyncImagePyramid();
+}
+
+const std::vector<cv::Mat>& ORBextractor::SyncImagePyramid() {
+    if (!mbPyramidStale) return mvImagePyramid;
+    for (int l = 0; l < nlevels; l++) {
+        int w = 0, h = 0;
+        orbx_ok(orbx_pyramid_level(mpHandle, 0, l, nullptr, 0, &w, &h), "orbx_pyramid_level");
+        mvImagePyramid[l].create(h, w, CV_8U);
+        orbx_ok(orbx_pyramid_level(mpHandle, 0, l, mvImagePyramid[l].data, mvImagePyramid[l].step, &w, &h),
+                "orbx_pyramid_level");
     }
+    mbPyramidStale = false;
+    return mvImagePyramid;
 }
 
 }  // namespace ORB_SLAM2

@@ -9,9 +9,11 @@
  * non-8UC1 image asserts (ORBextractor.cc:1046-1050); a device failure throws
  * std::runtime_error (the reference has no failure mode there; there is no CPU fallback).
  *
- * mvImagePyramid is materialised from the device after every call (needed by
- * Frame::ComputeStereoMatches, A1 Frame.cc:474-581); set ORBAMD_NO_HOST_PYRAMID=1 in
- * monocular deployments to skip that PCIe copy.
+ * mvImagePyramid: the pyramid stays on the device. Its one reader in the reference,
+ * Frame::ComputeStereoMatches (A1 Frame.cc:474-581), is replaced by host/Frame_stereo_amd.cc, which
+ * reads the device copy, so no PCIe copy is made by default. A caller that does read the public
+ * member calls SyncImagePyramid() first (a lazy copy of the last call's levels, done once per call),
+ * or sets ORBAMD_HOST_PYRAMID=1 to have every call materialise it as the reference does.
  */
 #ifndef ORBEXTRACTOR_H
 #define ORBEXTRACTOR_H
@@ -44,6 +46,9 @@ public:
 
     std::vector<cv::Mat> mvImagePyramid;
 
+    // materialise mvImagePyramid from the device for the last call (no-op if already done); returns it
+    const std::vector<cv::Mat>& SyncImagePyramid();
+
     // the device handle holding this extractor's last pyramid (used by the drop-in
     // Frame::ComputeStereoMatches, host/Frame_stereo_amd.cc); addition to the reference surface
     orbx_handle* DeviceHandle() const { return mpHandle; }
@@ -64,7 +69,8 @@ protected:
     orbx_handle* mpHandle;
     int mHandleW, mHandleH;
     int mDevice;
-    bool mbHostPyramid;
+    bool mbHostPyramid;   // ORBAMD_HOST_PYRAMID=1: materialise after every call
+    bool mbPyramidStale;  // mvImagePyramid does not hold the last call's levels yet
     std::vector<unsigned char> mKpBuf, mDescBuf;
 };
 

@@ -3,7 +3,7 @@
 set -e
 R=$(cd "$(dirname "$0")/../.." && pwd)
 mkdir -p "$R/tests/cpp/build"
-g++ -std=c++14 -O1 -Wall -Wno-unused-function \
+g++ -std=c++14 -O1 -pthread -Wall -Wno-unused-function \
   -I "$R/tests/cpp/cvmin" -I "$R/tests/cpp/mock" -I "$R/cooperative-orb-slam_amd/host" -I "$R/include" -I "$R/oracle" \
   "$R/tests/cpp/test_dropin.cpp" "$R/cooperative-orb-slam_amd/host/ORBextractor.cc" \
   "$R/cooperative-orb-slam_amd/host/ORBmatcher_amd.cc" "$R/cooperative-orb-slam_amd/host/ORBmatcher_base_amd.cc" \

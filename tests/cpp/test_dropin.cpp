@@ -7,6 +7,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
+#include <thread>
 #include <vector>
 
 #include "ORBextractor.h"
@@ -59,6 +61,8 @@ static void check_extract(ORBextractor& ext, oc_extractor* orc, const uint8_t* i
         bad += memcmp(desc.ptr<unsigned char>(i), of.desc.data() + 32 * (size_t)i, 32) != 0;
     }
     CHECK(bad == 0, "%d keypoint/descriptor rows differ", bad);
+    // the host pyramid is lazy (no PCIe copy unless a caller asks for it)
+    ext.SyncImagePyramid();
     for (int l = 0; l < ext.GetLevels(); l++) {
         int w, h;
         oc_level_size(orc, l, &w, &h);
@@ -514,6 +518,74 @@ int main() {
             CHECK(bad == 0, "ComputeBoW scoring=%d: %d mismatches", scoring, bad);
             oc_vocab_destroy(ov);
         }
+    }
+    // ---- concurrency (SURVEY.md 8(b) "Threading"): two extractors on two std::threads, as the stereo Frame
+    // constructor runs them (Frame.cc:80-81), while matchers run on a Tracking-like (SearchByBoW(KF,F),
+    // Tracking.cc:767), a LocalMapping-like (SearchForTriangulation, LocalMapping.cc:268) and a
+    // LoopClosing-like thread (SearchByBoW(KF,KF), LoopClosing.cc:267); every call must equal the
+    // single-threaded result
+    {
+        Frame F2;
+        F2.N = kf2.N; F2.mvKeys = kf2.mvKeys; F2.mvKeysUn = kf2.mvKeysUn; F2.mDescriptors = kf2.mDescriptors;
+        F2.mFeatVec = kf2.mFeatVec; F2.mvScaleFactors = kf2.mvScaleFactors; F2.mvLevelSigma2 = kf2.mvLevelSigma2;
+        std::vector<std::pair<size_t, size_t> > e_tri;
+        std::vector<MapPoint*> e_kk, e_kf;
+        int e_ntri, e_nkk, e_nkf;
+        {
+            ORBmatcher a(0.6f, false), b(0.75f, true), c(0.7f, true);
+            e_ntri = a.SearchForTriangulation(&kf1, &kf2, F12, e_tri, false);
+            e_nkk = b.SearchByBoW(&kf1, &kf2, e_kk);
+            e_nkf = c.SearchByBoW(&kf1, F2, e_kf);
+        }
+        std::atomic<int> bad(0), calls(0);
+        const int iters = 30;
+        auto extractor = [&](int f) {
+            ORBextractor e(1000, 1.2f, 8, 20, 7);
+            for (int it = 0; it < iters; it++) {
+                std::vector<cv::KeyPoint> k;
+                cv::Mat d;
+                e(cv::Mat(H, W, CV_8U, frames.data() + (size_t)f * W * H, W), cv::Mat(), k, d);
+                bool ok = k.size() == K[f].size() && d.rows == D[f].rows;
+                for (size_t i = 0; ok && i < k.size(); i++)
+                    ok = same_bits(k[i].pt.x, K[f][i].pt.x) && same_bits(k[i].pt.y, K[f][i].pt.y) &&
+                         same_bits(k[i].angle, K[f][i].angle) && k[i].octave == K[f][i].octave &&
+                         memcmp(d.ptr<unsigned char>((int)i), D[f].ptr<unsigned char>((int)i), 32) == 0;
+                bad += !ok;
+                calls++;
+            }
+        };
+        auto tri = [&]() {
+            ORBmatcher m(0.6f, false);
+            for (int it = 0; it < iters; it++) {
+                std::vector<std::pair<size_t, size_t> > pr;
+                bad += m.SearchForTriangulation(&kf1, &kf2, F12, pr, false) != e_ntri || pr != e_tri;
+                calls++;
+            }
+        };
+        auto kk = [&]() {
+            ORBmatcher m(0.75f, true);
+            for (int it = 0; it < iters; it++) {
+                std::vector<MapPoint*> v;
+                bad += m.SearchByBoW(&kf1, &kf2, v) != e_nkk || v != e_kk;
+                calls++;
+            }
+        };
+        auto kf = [&]() {
+            ORBmatcher m(0.7f, true);
+            for (int it = 0; it < iters; it++) {
+                std::vector<MapPoint*> v;
+                bad += m.SearchByBoW(&kf1, F2, v) != e_nkf || v != e_kf;
+                calls++;
+            }
+        };
+        std::vector<std::thread> th;
+        th.emplace_back(extractor, 0);
+        th.emplace_back(extractor, 1);
+        th.emplace_back(tri);
+        th.emplace_back(kk);
+        th.emplace_back(kf);
+        for (std::thread& t : th) t.join();
+        CHECK(bad == 0 && calls == 5 * iters, "concurrent drop-ins: %d of %d calls differ", (int)bad, (int)calls);
     }
     // DescriptorDistance (ORBmatcher.cc:1647-1663)
     int dd = 0;

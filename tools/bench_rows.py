@@ -16,6 +16,8 @@
                BF batch (one node) on the same pairs and vs the oracle per pair.
   extract_host ORBextractor::operator() through the host-buffer C ABI on one 640x480 frame per call
                (H2D + whole pipeline + D2H): the Tracking thread's per-frame latency, vs the oracle.
+  matcher_host SearchForTriangulation (BF and over BoW nodes), SearchByBoW(KF,F), SearchByBoW(KF,KF)
+               through the host C ABI, one keyframe pair per call (how the C++ drop-ins call them).
 The CPU figures are the oracle (a plain-C restatement, 1 thread), not the reference build.
 """
 import json
@@ -156,6 +158,67 @@ def bench_extract_host(reps):
             "gpu_ms_per_call": round(g * 1e3, 4), "cpu_oracle_ms_per_call": round(c * 1e3, 3), "cpu_threads": 1}
 
 
+def bench_matcher_host(reps):
+    """per-call latency of the drop-in matcher entry points through the host C ABI (one keyframe pair
+    per call, as LocalMapping.cc:268 / Tracking.cc:767 / LoopClosing.cc:267 call them) vs the oracle"""
+    import orbamd
+    import oracle_py
+    from orbamd.matcher import KeyFrameView
+    rng = np.random.default_rng(7)
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    tabs = orc.tables()
+    (k1, d1), (k2, d2) = [orc(img) for img in orbamd.synth_frames(0, 10, 2, 640, 480)]
+    F12, ex, ey = orbamd.device.default_geometry()
+    ids = np.sort(rng.choice(100000, 90, replace=False))  # ~ the node count at levelsup 4 of ORBvoc.txt
+
+    def fv(n):
+        a = rng.integers(0, len(ids), n)
+        return {int(ids[i]): list(np.nonzero(a == i)[0]) for i in range(len(ids)) if (a == i).any()}
+    fv1, fv2 = fv(len(k1)), fv(len(k2))
+    mp1, mp2 = rng.random(len(k1)) < 0.8, rng.random(len(k2)) < 0.8
+    rows = []
+    cases = [
+        ("search_for_triangulation_bf", "SearchForTriangulation, one node (BF), mono, no MapPoints",
+         lambda m, a, b: m.SearchForTriangulation(a, b, F12, ex, ey),
+         lambda a, b: oracle_py.search_for_triangulation(a, b, F12, ex, ey, False, False),
+         KeyFrameView(k1, d1, tabs["scale"], tabs["sigma2"]), KeyFrameView(k2, d2, tabs["scale"], tabs["sigma2"]),
+         (0.6, False)),
+        ("search_for_triangulation_nodes", "SearchForTriangulation over ~90 common BoW nodes (LocalMapping.cc:268)",
+         lambda m, a, b: m.SearchForTriangulation(a, b, F12, ex, ey),
+         lambda a, b: oracle_py.search_for_triangulation(a, b, F12, ex, ey, False, False),
+         KeyFrameView(k1, d1, tabs["scale"], tabs["sigma2"], feat_vec=fv1),
+         KeyFrameView(k2, d2, tabs["scale"], tabs["sigma2"], feat_vec=fv2), (0.6, False)),
+        ("search_by_bow_kf_f", "SearchByBoW(KF, F), ~90 nodes, 80% MapPoints, ratio 0.7, rotation check (Tracking.cc:767)",
+         lambda m, a, b: m.SearchByBoW(a, b, other_is_keyframe=False),
+         lambda a, b: oracle_py.search_by_bow(a, b, 0.7, True, other_is_keyframe=False),
+         KeyFrameView(k1, d1, tabs["scale"], tabs["sigma2"], feat_vec=fv1, has_mp=mp1),
+         KeyFrameView(k2, d2, tabs["scale"], tabs["sigma2"], feat_vec=fv2), (0.7, True)),
+        ("search_by_bow_kf_kf", "SearchByBoW(KF, KF), ~90 nodes, 80% MapPoints, ratio 0.75 (LoopClosing.cc:267)",
+         lambda m, a, b: m.SearchByBoW(a, b, other_is_keyframe=True),
+         lambda a, b: oracle_py.search_by_bow(a, b, 0.75, True, other_is_keyframe=True),
+         KeyFrameView(k1, d1, tabs["scale"], tabs["sigma2"], feat_vec=fv1, has_mp=mp1),
+         KeyFrameView(k2, d2, tabs["scale"], tabs["sigma2"], feat_vec=fv2, has_mp=mp2), (0.75, True)),
+    ]
+    for name, what, g_call, o_call, a, b, (ratio, ori) in cases:
+        m = orbamd.ORBmatcher(ratio, ori)
+        for _ in range(5):
+            ng, mg = g_call(m, a, b)
+        t = time.perf_counter()
+        for _ in range(reps):
+            g_call(m, a, b)
+        g = (time.perf_counter() - t) / reps
+        t = time.perf_counter()
+        for _ in range(max(reps // 5, 3)):
+            no, mo = o_call(a, b)
+        c = (time.perf_counter() - t) / max(reps // 5, 3)
+        assert ng == no and np.array_equal(mg, mo), name
+        rows.append({"row": name, "workload": what + "; 640x480 frames, %d / %d features" % (len(k1), len(k2)),
+                     "gpu_host_api_ms_per_call": round(g * 1e3, 4), "cpu_oracle_ms_per_call": round(c * 1e3, 4),
+                     "nmatches": int(ng), "cpu_threads": 1})
+        m.close()
+    return rows
+
+
 def bench_projection(reps):
     import orbamd
     import oracle_py
@@ -264,9 +327,17 @@ def bench_bow(torch, reps):
 def main():
     import torch
     steps = int(os.environ.get("BENCH_ROWS_STEPS", "10"))
-    for r in (bench_extract_host(100), bench_stereo(torch, steps), bench_projection(50), bench_distinctive(torch, 10),
-              bench_bow(torch, 10), bench_tri_nodes(torch, 10)):
-        print(json.dumps(r), flush=True)
+    only = os.environ.get("BENCH_ROWS_ONLY")
+    rows = {"extract_host": lambda: bench_extract_host(100), "matcher_host": lambda: bench_matcher_host(100),
+            "stereo": lambda: bench_stereo(torch, steps), "projection": lambda: bench_projection(50),
+            "distinctive": lambda: bench_distinctive(torch, 10), "bow": lambda: bench_bow(torch, 10),
+            "tri_nodes": lambda: bench_tri_nodes(torch, 10)}
+    for name, fn in rows.items():
+        if only and name not in only.split(","):
+            continue
+        r = fn()
+        for line in (r if isinstance(r, list) else [r]):
+            print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
