@@ -21,6 +21,10 @@
 #include "orb_math.h"
 #include "orb_pattern.h"
 
+#ifndef ORBX_FAST_STOP
+#define ORBX_FAST_STOP 0  // phase-cost experiment only (tools/exp_fast_phases.sh): >0 cuts k_fast_cells2 short
+#endif
+
 namespace orbamd {
 
 __device__ __forceinline__ void wave_sync() {
@@ -516,116 +520,125 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
         }
     }
     wave_sync();
+#if ORBX_FAST_STOP == 1
+    if (lane == 0) cellcnt[(long long)f * ep.ncells + ci] = 0;
+    return;
+#endif
     const int bw = c.w - 6, bh = c.h - 6;
     int total = 0;
     if (bw > 0 && bh > 0) {
-        const int t_lo = min(ep.ini_th, ep.min_th);
-        int ncand = 0;
-        {
-            // SWAR pretest: each lane tests the 4 pixels of one aligned ROI dword (band columns
-            // [3, 3+bw)) as 4 bytes with v_lerp_u8 (per byte (a + b + r) >> 1, exact in 9 bits):
-            // m = lerp(c, 255 - v, r) = floor((c - v + 255 + r) / 2), and m >= M <=> bit 7 of lerp(m, 255 - M, 1).
-            // With r of the right parity, c - v > t <=> m_b >= (t + 256 + r_b) / 2 (r_b = t & 1) and
-            // c - v < -t <=> NOT m_d >= (255 - t + r_d) / 2 (r_d = 1 - r_b); for t = 255 the bright bound is
-            // clamped to 255 (looser: the pretest stays a necessary condition). Exhaustive check over
-            // (c, v, t): tests/test_oracle_primitives.py::test_fast_pretest_lerp_exact.
-            const int G = c.G;  // dword groups covering columns [0, bw+3): (bw + 6) / 4
-            const int rpc = c.rpc;
-            const int lr = (lane * c.magG) >> 16, j = lane - lr * G;
-            const bool lane_ok = lane < rpc * G;
-            // band-column mask at the candidate bits: pixel i of this lane's dword -> bit 8 i + 7
-            auto colok = [&](int i) { return 4 * j + i >= 3 && 4 * j + i < 3 + bw; };
-            const uint32_t colm = (colok(0) ? 0x80u : 0u) | (colok(1) ? 0x8000u : 0u) | (colok(2) ? 0x800000u : 0u) |
-                                  (colok(3) ? 0x80000000u : 0u);
-            uint32_t* rec = (uint32_t*)str;  // <= bh x G records, zeroed again by the expansion
-            int nrec = 0;
-            const uint32_t RB = (t_lo & 1) ? 0x01010101u : 0u, RD = RB ^ 0x01010101u;
-            const uint32_t CB = (uint32_t)(255 - min((t_lo + 256 + (t_lo & 1)) >> 1, 255)) * 0x01010101u;
-            const uint32_t CD = (uint32_t)(255 - ((256 - t_lo - (t_lo & 1)) >> 1)) * 0x01010101u;
-            for (int r0 = 0; r0 < bh; r0 += rpc) {
-                const int rr = 3 + r0 + lr;
-                const int rrc = min(rr, bh + 2);
-                const uint8_t* q = roi + rrc * RP + 4 * j;
-                const uint32_t xv = *(const uint32_t*)q;
-                const uint32_t xn = *(const uint32_t*)(q + 4);
-                const uint32_t xp = *(const uint32_t*)(q - 4);
-                const uint32_t xd = *(const uint32_t*)(q + 3 * RP);  // ring 0 (row + 3)
-                const uint32_t xu = *(const uint32_t*)(q - 3 * RP);  // ring 8 (row - 3)
-                const uint32_t xr = __builtin_amdgcn_alignbyte(xn, xv, 3);  // ring 4 (col + 3)
-                const uint32_t xl = __builtin_amdgcn_alignbyte(xv, xp, 1);  // ring 12 (col - 3)
-                const uint32_t nv = ~xv;  // 255 - v per byte
-                auto bright = [&](uint32_t cb) {
-                    return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(cb, nv, RB), CB, 0x01010101u);
-                };
-                auto notdark = [&](uint32_t cb) {
-                    return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(cb, nv, RD), CD, 0x01010101u);
-                };
-                const uint32_t b0 = bright(xd), b4 = bright(xr), b8 = bright(xu), b12 = bright(xl);
-                const uint32_t n0 = notdark(xd), n4 = notdark(xr), n8 = notdark(xu), n12 = notdark(xl);
-                // candidate iff two cyclically adjacent cardinals are both brighter ((b0|b8)&(b4|b12)) or
-                // both darker (NOT((n0&n8)|(n4&n12)))
-                const uint32_t cand = ((b0 | b8) & (b4 | b12)) | ~((n0 & n8) | (n4 & n12));
-                const uint32_t k = (lane_ok && rr < 3 + bh) ? (cand & colm) : 0u;  // bit 8 i + 7: pixel i
-                // sparse ordered record of this dword (lanes with a candidate, ~1 in 5): row-major =
-                // lane order within a row pass; record = candidate bits | group j | ROI row << 8
-                // (j, rr < 128 fit the 7 free bits of bytes 0 / 1)
-                const unsigned long long Bk = __ballot(k != 0u);
-                if (k != 0u) {
-                    const int at = nrec + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(Bk >> 32),
-                                                                          __builtin_amdgcn_mbcnt_lo((unsigned)Bk, 0));
-                    rec[at] = k | (uint32_t)j | ((uint32_t)rr << 8);
-                }
-                nrec += __popcll(Bk);
-            }
-            wave_sync();
-            // expand the records into the candidate list (order kept: records in order, pixels of a
-            // record ascending); the record area is zeroed behind, so str is the zero S map again
-            for (int c0 = 0; c0 < nrec; c0 += 64) {
-                const int i = c0 + lane;
-                uint32_t r = 0u;
-                if (i < nrec) {
-                    r = rec[i];
-                    rec[i] = 0u;
-                }
-                const uint32_t km = r & 0x80808080u;
-                const int cntl = __popc(km);
-                int pos = ncand;
-#pragma unroll
-                for (int bit = 0; bit < 3; bit++) {  // cntl <= 4
-                    const unsigned long long B = __ballot((cntl >> bit) & 1);
-                    pos += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(B >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((unsigned)B, 0))
-                           << bit;
-                    ncand += __popcll(B) << bit;
-                }
-                const int e = (int)(((r >> 8) & 127u) << 8) | (int)(4u * (r & 127u));
-                if (km & 0x80u) clist[pos++] = (uint16_t)e;
-                if (km & 0x8000u) clist[pos++] = (uint16_t)(e + 1);
-                if (km & 0x800000u) clist[pos++] = (uint16_t)(e + 2);
-                if (km & 0x80000000u) clist[pos++] = (uint16_t)(e + 3);
-            }
-        }
-        wave_sync();
-        // the first 64 candidates (all of them in most cells) keep their list entry and strength in
-        // registers for the NMS passes: one dependent LDS read fewer per pass
-        const int e0 = lane < ncand ? (int)clist[lane] : 0;
-        int s0 = 0;
-        for (int i0 = 0; i0 < ncand; i0 += 64) {
-            const int i = i0 + lane;
-            if (i < ncand) {
-                const int e = i0 == 0 ? e0 : (int)clist[i];
-                const int o = (e >> 8) * RP + (e & 0xFF);
-                const int S = fast_strength_h2(roi, o, RP);
-                if (S > t_lo) str[o] = (uint8_t)S;
-                if (i0 == 0) s0 = S > t_lo ? S : 0;
-            }
-        }
-        wave_sync();
-        // one emission pass at iniThFAST; only a cell with no corner there (nothing was written) is
-        // scanned again at minThFAST (ORBextractor.cc:811-826): the same keys as a count pass at
-        // iniThFAST followed by an emission pass at the chosen threshold, with one NMS pass fewer
+        // One pass per threshold: iniThFAST first; only a cell with no corner there is scanned again at
+        // minThFAST (ORBextractor.cc:811-826). Each pass pretests, computes S and stores it in the S map
+        // only at its own threshold t: the NMS at t is exact with the S of the pretest(t) candidates alone
+        // (a neighbour can suppress a corner with S_c > t only if S_n >= S_c > t, and then it passed the
+        // pretest at t), so the common first pass computes S for the ~9% of band pixels passing the
+        // pretest at 20 instead of the ~15% passing it at 7. The fallback pass sees a superset of the
+        // first pass's candidates and stores the same S for them (S does not depend on t).
+        const int G = c.G;  // dword groups covering columns [0, bw+3): (bw + 6) / 4
+        const int rpc = c.rpc;
+        const int lr = (lane * c.magG) >> 16, j = lane - lr * G;
+        const bool lane_ok = lane < rpc * G;
+        // band-column mask at the candidate bits: pixel i of this lane's dword -> bit 8 i + 7
+        auto colok = [&](int i) { return 4 * j + i >= 3 && 4 * j + i < 3 + bw; };
+        const uint32_t colm = (colok(0) ? 0x80u : 0u) | (colok(1) ? 0x8000u : 0u) | (colok(2) ? 0x800000u : 0u) |
+                              (colok(3) ? 0x80000000u : 0u);
         uint32_t* out = cellkey + (long long)f * ep.keys_per_frame + c.slot;
         for (int t = ep.ini_th;; t = ep.min_th) {
+            int ncand = 0;
+            {
+                // SWAR pretest: each lane tests the 4 pixels of one aligned ROI dword (band columns
+                // [3, 3+bw)) as 4 bytes with v_lerp_u8 (per byte (a + b + r) >> 1, exact in 9 bits):
+                // m = lerp(c, 255 - v, r) = floor((c - v + 255 + r) / 2), and m >= M <=> bit 7 of lerp(m, 255 - M, 1).
+                // With r of the right parity, c - v > t <=> m_b >= (t + 256 + r_b) / 2 (r_b = t & 1) and
+                // c - v < -t <=> NOT m_d >= (255 - t + r_d) / 2 (r_d = 1 - r_b); for t = 255 the bright bound is
+                // clamped to 255 (looser: the pretest stays a necessary condition). Exhaustive check over
+                // (c, v, t): tests/test_oracle_primitives.py::test_fast_pretest_lerp_exact.
+                uint32_t* rec = (uint32_t*)str;  // <= bh x G records, zeroed again by the expansion
+                int nrec = 0;
+                const uint32_t RB = (t & 1) ? 0x01010101u : 0u, RD = RB ^ 0x01010101u;
+                const uint32_t CB = (uint32_t)(255 - min((t + 256 + (t & 1)) >> 1, 255)) * 0x01010101u;
+                const uint32_t CD = (uint32_t)(255 - ((256 - t - (t & 1)) >> 1)) * 0x01010101u;
+                for (int r0 = 0; r0 < bh; r0 += rpc) {
+                    const int rr = 3 + r0 + lr;
+                    const int rrc = min(rr, bh + 2);
+                    const uint8_t* q = roi + rrc * RP + 4 * j;
+                    const uint32_t xv = *(const uint32_t*)q;
+                    const uint32_t xn = *(const uint32_t*)(q + 4);
+                    const uint32_t xp = *(const uint32_t*)(q - 4);
+                    const uint32_t xd = *(const uint32_t*)(q + 3 * RP);  // ring 0 (row + 3)
+                    const uint32_t xu = *(const uint32_t*)(q - 3 * RP);  // ring 8 (row - 3)
+                    const uint32_t xr = __builtin_amdgcn_alignbyte(xn, xv, 3);  // ring 4 (col + 3)
+                    const uint32_t xl = __builtin_amdgcn_alignbyte(xv, xp, 1);  // ring 12 (col - 3)
+                    const uint32_t nv = ~xv;  // 255 - v per byte
+                    auto bright = [&](uint32_t cb) {
+                        return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(cb, nv, RB), CB, 0x01010101u);
+                    };
+                    auto notdark = [&](uint32_t cb) {
+                        return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(cb, nv, RD), CD, 0x01010101u);
+                    };
+                    const uint32_t b0 = bright(xd), b4 = bright(xr), b8 = bright(xu), b12 = bright(xl);
+                    const uint32_t n0 = notdark(xd), n4 = notdark(xr), n8 = notdark(xu), n12 = notdark(xl);
+                    // candidate iff two cyclically adjacent cardinals are both brighter ((b0|b8)&(b4|b12)) or
+                    // both darker (NOT((n0&n8)|(n4&n12)))
+                    const uint32_t cand = ((b0 | b8) & (b4 | b12)) | ~((n0 & n8) | (n4 & n12));
+                    const uint32_t k = (lane_ok && rr < 3 + bh) ? (cand & colm) : 0u;  // bit 8 i + 7: pixel i
+                    // sparse ordered record of this dword (lanes with a candidate, ~1 in 5): row-major =
+                    // lane order within a row pass; record = candidate bits | group j | ROI row << 8
+                    // (j, rr < 128 fit the 7 free bits of bytes 0 / 1)
+                    const unsigned long long Bk = __ballot(k != 0u);
+                    if (k != 0u) {
+                        const int at = nrec + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(Bk >> 32),
+                                                                              __builtin_amdgcn_mbcnt_lo((unsigned)Bk, 0));
+                        rec[at] = k | (uint32_t)j | ((uint32_t)rr << 8);
+                    }
+                    nrec += __popcll(Bk);
+                }
+                wave_sync();
+                // expand the records into the candidate list (order kept: records in order, pixels of a
+                // record ascending); the record area is zeroed behind, so str is the S map again (zero
+                // except S values of an earlier pass, which this pass rewrites unchanged)
+                for (int c0 = 0; c0 < nrec; c0 += 64) {
+                    const int i = c0 + lane;
+                    uint32_t r = 0u;
+                    if (i < nrec) {
+                        r = rec[i];
+                        rec[i] = 0u;
+                    }
+                    const uint32_t km = r & 0x80808080u;
+                    const int cntl = __popc(km);
+                    int pos = ncand;
+#pragma unroll
+                    for (int bit = 0; bit < 3; bit++) {  // cntl <= 4
+                        const unsigned long long B = __ballot((cntl >> bit) & 1);
+                        pos += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(B >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)B, 0))
+                               << bit;
+                        ncand += __popcll(B) << bit;
+                    }
+                    const int e = (int)(((r >> 8) & 127u) << 8) | (int)(4u * (r & 127u));
+                    if (km & 0x80u) clist[pos++] = (uint16_t)e;
+                    if (km & 0x8000u) clist[pos++] = (uint16_t)(e + 1);
+                    if (km & 0x800000u) clist[pos++] = (uint16_t)(e + 2);
+                    if (km & 0x80000000u) clist[pos++] = (uint16_t)(e + 3);
+                }
+            }
+            wave_sync();
+            // the first 64 candidates (all of them in most cells) keep their list entry and strength in
+            // registers for the NMS pass: one dependent LDS read fewer
+            const int e0 = lane < ncand ? (int)clist[lane] : 0;
+            int s0 = 0;
+            for (int i0 = 0; i0 < ncand; i0 += 64) {
+                const int i = i0 + lane;
+                if (i < ncand) {
+                    const int e = i0 == 0 ? e0 : (int)clist[i];
+                    const int o = (e >> 8) * RP + (e & 0xFF);
+                    const int S = fast_strength_h2(roi, o, RP);
+                    if (S > t) str[o] = (uint8_t)S;
+                    if (i0 == 0) s0 = S > t ? S : 0;
+                }
+            }
+            wave_sync();
+            // NMS + row-major emission at t
             for (int i0 = 0; i0 < ncand; i0 += 64) {
                 const int i = i0 + lane;
                 bool keep = false;
@@ -654,6 +667,7 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
                 total += __popcll(m);
             }
             if (total != 0 || t == ep.min_th) break;  // wave-uniform
+            wave_sync();  // the fallback pass rewrites the record area / candidate list
         }
         if (total > c.cap) total = c.cap;
     }
@@ -706,6 +720,14 @@ __device__ __forceinline__ int block_sum(int v, int* red) {
  *   sortkey   : NC x u64                                   =  8 NC
  *   keys      : KL x (4 + 2 + 1) (if n <= KL, else global scratch)
  */
+#ifndef ORBX_OCT_STOP
+#define ORBX_OCT_STOP 0  // phase-cost experiment only: >0 cuts k_octree short (results invalid)
+#endif
+#ifndef ORBX_OCT_FLAT
+#define ORBX_OCT_FLAT 1
+#endif
+constexpr bool kOctFlatGather = ORBX_OCT_FLAT != 0;  // A/B switch (tools/build_variant.sh -DORBX_OCT_FLAT=0)
+
 struct NodeT {
     int* x0; int* y0; int* x1; int* y1; int* nk; uint32_t* seq;
 };
@@ -761,19 +783,71 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
     struct KeysGlobal { uint32_t* key; uint16_t* label; uint8_t* quad; };
     auto tail = [&](auto K) {
         carry = 0;
-        for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
-            const int c = c0 + tid;
-            const int v = c < lv.ncells ? ccnt[c] : 0;
-            int tot;
-            const int off = block_scan_excl(v, &tot, red) + carry;
-            if (c < lv.ncells) {
-                const uint32_t* src = ckey + cells[lv.cell_begin + c].slot;
-                for (int k = 0; k < v; k++) K.key[off + k] = src[k];
+        if (kOctFlatGather && 2 * lv.ncells + 2 <= 4 * NC) {
+            // flat gather: the cells' key offsets and slots go to LDS (cnt4's space, unused until the roots),
+            // then thread t copies keys t, t+256, ... finding each key's cell by a fixed-trip binary search, four
+            // keys in flight per thread. (A thread per cell copying its keys one by one waited on one global
+            // load per key of the level's fullest cell: the level-0 workgroup's long pole.)
+            int* coff = cnt4;                   // [ncells + 1]
+            int* cslot = cnt4 + lv.ncells + 1;  // [ncells]
+            for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
+                const int c = c0 + tid;
+                const int v = c < lv.ncells ? ccnt[c] : 0;
+                const int sl = c < lv.ncells ? cells[lv.cell_begin + c].slot : 0;
+                int tot;
+                const int off = block_scan_excl(v, &tot, red) + carry;
+                if (c < lv.ncells) {
+                    coff[c] = off;
+                    cslot[c] = sl;
+                }
+                carry += tot;
             }
-            carry += tot;
+            if (tid == 0) coff[lv.ncells] = carry;
+            __syncthreads();
+            int top = 1;
+            while (top < lv.ncells) top <<= 1;
+            constexpr int kG = 4;
+            for (int i0 = tid; i0 < n; i0 += 256 * kG) {
+                int pos[kG];
+#pragma unroll
+                for (int g = 0; g < kG; g++) pos[g] = 0;
+                for (int step = top >> 1; step > 0; step >>= 1) {  // largest c with coff[c] <= i
+#pragma unroll
+                    for (int g = 0; g < kG; g++) {
+                        const int i = min(i0 + 256 * g, n - 1);
+                        const int q = pos[g] + step;
+                        if (q < lv.ncells && coff[q] <= i) pos[g] = q;
+                    }
+                }
+                uint32_t kv[kG];
+#pragma unroll
+                for (int g = 0; g < kG; g++) {
+                    const int i = min(i0 + 256 * g, n - 1);
+                    kv[g] = ckey[cslot[pos[g]] + (i - coff[pos[g]])];
+                }
+#pragma unroll
+                for (int g = 0; g < kG; g++)
+                    if (i0 + 256 * g < n) K.key[i0 + 256 * g] = kv[g];
+            }
+        } else {
+            for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
+                const int c = c0 + tid;
+                const int v = c < lv.ncells ? ccnt[c] : 0;
+                int tot;
+                const int off = block_scan_excl(v, &tot, red) + carry;
+                if (c < lv.ncells) {
+                    const uint32_t* src = ckey + cells[lv.cell_begin + c].slot;
+                    for (int k = 0; k < v; k++) K.key[off + k] = src[k];
+                }
+                carry += tot;
+            }
         }
         __syncthreads();
         uint32_t* outk = lvkey + (long long)f * ep.kp_per_frame + lv.kp_off;
+#if ORBX_OCT_STOP == 1
+        if (tid == 0) lvcnt[f * ep.L + l] = 0;
+        return;
+#endif
         if (n == 0) {
             if (tid == 0) lvcnt[f * ep.L + l] = 0;
             return;
@@ -813,6 +887,10 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         }
         __syncthreads();
         for (int i = tid; i < n; i += 256) K.label[i] = (uint16_t)spos[K.label[i]];
+#if ORBX_OCT_STOP == 2
+        if (tid == 0) lvcnt[f * ep.L + l] = 0;
+        return;
+#endif
         if (size > NC) {  // capacity overflow: flag it and leave this level empty (never a stale count)
             if (tid == 0) { atomicOr(err, 2); lvcnt[f * ep.L + l] = 0; }
             return;
@@ -859,6 +937,12 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
             }
             __syncthreads();
             if (nD == 0) break;  // cannot happen while size changes, kept for safety
+#if ORBX_OCT_STOP == 3
+            if (phase == 2) {
+                if (tid == 0) lvcnt[f * ep.L + l] = 0;
+                return;
+            }
+#endif
             if (phase == 2) {
                 // bitonic sort of skey[0..P) descending; pad with 0
                 int P2 = 1;
