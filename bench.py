@@ -200,10 +200,19 @@ def main():
     assert B % P == 0, "--batch must be a multiple of --pipes"
     sub = B // P
     frames_np = orbamd.synth_frames(rank, 0, B, W, H)  # agent = rank
+    def allgather(out, inp):
+        # RCCL: in place (inp is out's slice of this rank). gloo (the one-GPU rehearsal): through host memory
+        if backend == "nccl":
+            dist.all_gather_into_tensor(out, inp)
+        else:
+            o = torch.empty(out.numel(), dtype=torch.uint8)
+            dist.all_gather_into_tensor(o, inp.cpu().clone())
+            out.copy_(o.to(out.device))
+
     lo_prio, hi_prio = torch.cuda.Stream.priority_range()
     n_hi = {"none": 0, "lead": P // 2, "lead1": 1}[args.prio]
     sched = AgentSchedule(torch, frames_np, W, H, P, device=local, rank=rank, world=world,
-                          allgather=(lambda o, i: dist.all_gather_into_tensor(o, i)) if world > 1 else None,
+                          allgather=allgather if world > 1 else None,
                           stagger=args.stagger, exchange=not args.no_exchange,
                           priorities=[hi_prio if p < n_hi else lo_prio for p in range(P)], nfeatures=cfg["nfeatures"])
     pipes = sched.pipes

@@ -727,6 +727,10 @@ __device__ __forceinline__ int block_sum(int v, int* red) {
 #define ORBX_OCT_FLAT 1
 #endif
 constexpr bool kOctFlatGather = ORBX_OCT_FLAT != 0;  // A/B switch (tools/build_variant.sh -DORBX_OCT_FLAT=0)
+#ifndef ORBX_OCT_FAST1
+#define ORBX_OCT_FAST1 1
+#endif
+constexpr bool kOctFastPhase1 = ORBX_OCT_FAST1 != 0;  // A/B switch (-DORBX_OCT_FAST1=0: general rounds only)
 
 struct NodeT {
     int* x0; int* y0; int* x1; int* y1; int* nk; uint32_t* seq;
@@ -900,12 +904,95 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         int phase = 1;
         const int N = lv.N;
         // --- 3. division rounds (ORBextractor.cc:594-739)
+        bool cnt_clean = false;  // cnt4[0, 4 size) already zero (cleared by the previous fast round)
         for (int iter = 0; iter < 100000; iter++) {
             const int prevSize = size;
-            for (int s = tid; s < size; s += 256) {
-                cnt4[4 * s] = 0; cnt4[4 * s + 1] = 0; cnt4[4 * s + 2] = 0; cnt4[4 * s + 3] = 0;
+            if (!cnt_clean) {
+                for (int s = tid; s < size; s += 256) {
+                    cnt4[4 * s] = 0; cnt4[4 * s + 1] = 0; cnt4[4 * s + 2] = 0; cnt4[4 * s + 3] = 0;
+                }
+                __syncthreads();
             }
-            __syncthreads();
+            cnt_clean = false;
+            if (kOctFastPhase1 && phase == 1 && size <= 256) {
+                // Phase-1 round with every node in one thread (slot s = tid): every node with > 1 key divides,
+                // in list order, so one packed scan gives the children's creation indices, the survivors'
+                // positions and the number of children with > 1 key at once (4 barriers per round instead of
+                // ~20 for the general path below, which phase 2 and tables of > 256 nodes take).
+                for (int i = tid; i < n; i += 256) {
+                    const int s = K.label[i];
+                    if (A.nk[s] >= 2) {
+                        const uint32_t kk = K.key[i];
+                        const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF);
+                        const int hx = (A.x1[s] - A.x0[s] + 1) >> 1, hy = (A.y1[s] - A.y0[s] + 1) >> 1;
+                        const int q = (x >= A.x0[s] + hx ? 1 : 0) + (y >= A.y0[s] + hy ? 2 : 0);
+                        K.quad[i] = (uint8_t)q;
+                        atomicAdd(&cnt4[4 * s + q], 1);
+                    }
+                }
+                __syncthreads();
+                const int s = tid;
+                const bool live = s < size;
+                const bool isD = live && A.nk[s] >= 2;
+                int c4[4] = {0, 0, 0, 0};
+                if (isD) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) c4[q] = cnt4[4 * s + q];
+                }
+                const int nc = (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0);
+                const int ne = (c4[0] > 1) + (c4[1] > 1) + (c4[2] > 1) + (c4[3] > 1);
+                const int sv = (live && !isD) ? 1 : 0;
+                // fields: children (<= 1024, bits 0-10), survivors (<= 256, bits 11-19), children with
+                // > 1 key (<= 1024, bits 20-30)
+                int tot;
+                const int ex = block_scan_excl(nc | (sv << 11) | (ne << 20), &tot, red);
+                const int TC = tot & 0x7FF, nsurv = (tot >> 11) & 0x1FF, nToExpand = tot >> 20;
+                const int newSize = TC + nsurv;
+                if (newSize > NC) {
+                    if (tid == 0) { atomicOr(err, 4); lvcnt[f * ep.L + l] = 0; }
+                    return;
+                }
+                if (isD) {
+                    const int x0 = A.x0[s], y0 = A.y0[s], x1 = A.x1[s], y1 = A.y1[s];
+                    const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;
+                    int ci = ex & 0x7FF;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (c4[q] > 0) {
+                            const int np = TC - 1 - ci;  // children pushed to the front, reverse creation order
+                            Bt.x0[np] = (q & 1) ? x0 + hx : x0;
+                            Bt.x1[np] = (q & 1) ? x1 : x0 + hx;
+                            Bt.y0[np] = (q & 2) ? y0 + hy : y0;
+                            Bt.y1[np] = (q & 2) ? y1 : y0 + hy;
+                            Bt.nk[np] = c4[q];
+                            Bt.seq[np] = next_seq + (uint32_t)ci;
+                            cpos[4 * s + q] = (uint16_t)np;
+                            ci++;
+                        }
+                    }
+                    spos[s] = -1;
+                } else if (live) {
+                    const int np = TC + ((ex >> 11) & 0x1FF);
+                    Bt.x0[np] = A.x0[s]; Bt.y0[np] = A.y0[s]; Bt.x1[np] = A.x1[s]; Bt.y1[np] = A.y1[s];
+                    Bt.nk[np] = A.nk[s]; Bt.seq[np] = A.seq[s];
+                    spos[s] = np;
+                }
+                __syncthreads();
+                for (int i = tid; i < n; i += 256) {
+                    const int s2 = K.label[i];
+                    const int np = spos[s2];
+                    K.label[i] = (uint16_t)(np >= 0 ? np : cpos[4 * s2 + K.quad[i]]);
+                }
+                for (int i = tid; i < 4 * newSize; i += 256) cnt4[i] = 0;  // for the next round's count pass
+                __syncthreads();
+                cnt_clean = true;
+                { NodeT t = A; A = Bt; Bt = t; }
+                next_seq += (uint32_t)TC;
+                size = newSize;
+                if (size >= N || size == prevSize) break;
+                if (size + nToExpand * 3 > N) phase = 2;
+                continue;
+            }
             for (int i = tid; i < n; i += 256) {
                 const int s = K.label[i];
                 if (A.nk[s] >= 2) {

@@ -21,7 +21,8 @@ class AgentSchedule:
     def __init__(self, torch, frames_np, width, height, pipes, device=0, rank=0, world=1, allgather=None,
                  stagger="each", exchange=True, priorities=None, nfeatures=1000):
         """frames_np: uint8 [B, H, W] host frames of this agent (copied to HBM once); allgather(out, inp):
-        all-gather of equal-sized device byte tensors across agents (None at world 1)."""
+        all-gather of equal-sized device byte tensors across agents (None at world 1); inp is out's slice of
+        this rank (in place)."""
         B = len(frames_np)
         assert B % pipes == 0, "frames per step must be a multiple of the graph count"
         self.torch, self.W, self.H, self.B, self.P = torch, width, height, B, pipes
@@ -40,8 +41,10 @@ class AgentSchedule:
         self.done = [torch.cuda.Event() for _ in range(pipes)]
         p0 = self.pipes[0]
         self.slot_bytes = p0.slot_bytes()
-        self.my_slot = torch.zeros(self.slot_bytes, dtype=torch.uint8, device=dev)
+        # the keyframe is packed straight into this agent's slot of the receive buffer: an in-place
+        # all-gather (RCCL's sendbuff == recvbuff + rank * count) and no copy at all at N = 1
         self.all_slots = torch.zeros(world * self.slot_bytes, dtype=torch.uint8, device=dev)
+        self.my_slot = self.all_slots[rank * self.slot_bytes:(rank + 1) * self.slot_bytes]
         self.xmatch = torch.empty((world, p0.stride), dtype=torch.int32, device=dev)
         self.xn = torch.zeros(world, dtype=torch.int32, device=dev)
         self.pack_err = torch.zeros(16, dtype=torch.int32, device=dev)
@@ -60,8 +63,6 @@ class AgentSchedule:
                 ag[0].record(st)
             if self.world > 1:
                 self.allgather(self.all_slots, self.my_slot)
-            else:
-                self.all_slots.copy_(self.my_slot)
             if ag is not None:
                 ag[1].record(st)
             p0.match_slots(0, self.all_slots, self.world, self.xmatch, self.xn, st.cuda_stream, query=self.src0)
