@@ -731,6 +731,10 @@ constexpr bool kOctFlatGather = ORBX_OCT_FLAT != 0;  // A/B switch (tools/build_
 #define ORBX_OCT_FAST1 1
 #endif
 constexpr bool kOctFastPhase1 = ORBX_OCT_FAST1 != 0;  // A/B switch (-DORBX_OCT_FAST1=0: general rounds only)
+#ifndef ORBX_OCT_RANK
+#define ORBX_OCT_RANK 1
+#endif
+constexpr bool kOctRankSort = ORBX_OCT_RANK != 0;  // A/B switch (-DORBX_OCT_RANK=0: bitonic phase-2 sort)
 
 struct NodeT {
     int* x0; int* y0; int* x1; int* y1; int* nk; uint32_t* seq;
@@ -1030,7 +1034,20 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 return;
             }
 #endif
-            if (phase == 2) {
+            if (phase == 2 && kOctRankSort) {
+                // processing order = descending (size, creation) key; keys are unique (seq), so a node's
+                // rank is the number of larger keys: nD broadcast LDS reads per node and two barriers
+                // instead of a bitonic network's log2(P)(log2(P)+1)/2 barriers
+                for (int j = tid; j < nD; j += 256) {
+                    const unsigned long long key = skey[j];
+                    int rank = 0;
+                    for (int i = 0; i < nD; i++) rank += skey[i] > key ? 1 : 0;
+                    dbase[rank] = dflag[j];
+                }
+                __syncthreads();
+                for (int j = tid; j < nD; j += 256) dflag[j] = dbase[j];
+                __syncthreads();
+            } else if (phase == 2) {
                 // bitonic sort of skey[0..P) descending; pad with 0
                 int P2 = 1;
                 while (P2 < nD) P2 <<= 1;
