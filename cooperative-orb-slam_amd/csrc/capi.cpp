@@ -456,8 +456,10 @@ static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fst
     // 4-byte-aligned frames, per-level kernels otherwise
     const bool aligned = ((uintptr_t)d_frames & 3) == 0 && (fstride & 3) == 0 && (pitch & 3) == 0;
     if (g.frames_ok && aligned && nframes >= kPyrFramesMinBatch && ep.L > 1) {
+        int max_rows = 1;
+        for (int l = 1; l < ep.L; l++) max_rows = std::max(max_rows, g.lv[l].h);
         HIPR(launch_pyramid_frames(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, g.d_lv.as<LevelDesc>(),
-                                   g.d_ptab.as<int>(), nframes, st));
+                                   g.d_ptab.as<int>(), max_rows, nframes, st));
         return 0;
     }
     for (int l = 1; l < ep.L; l++) {

@@ -234,7 +234,10 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
                                                          int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
                                                          const LevelDesc* __restrict__ levels,
                                                          const int* __restrict__ ptab) {
-    __shared__ int4 s_rt[kPyrMaxRows];
+    // the current level's row table; sized at launch for the tallest level >= 1 (rows x 16 B: 6.4 KB at
+    // 640x480) instead of kPyrMaxRows, so the LDS the long-lived pyramid workgroup holds (one per CU)
+    // stays free for the other graphs' FAST / describe workgroups beside it
+    extern __shared__ int4 s_rt[];
     const int f = blockIdx.x, tid = threadIdx.x;
     uint8_t* P = pyr + (long long)f * ep.pyr_frame_bytes;
     for (int l = 1; l < ep.L; l++) {
@@ -1631,10 +1634,11 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 }
 
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
-                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int nframes,
-                                 hipStream_t st) {
-    hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), dim3(nframes), dim3(kPyrThreads), 0, st, frames, fstride, pitch0, pyr, ep,
-                       levels, ptab);
+                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int max_rows,
+                                 int nframes, hipStream_t st) {
+    if (max_rows < 1 || max_rows > kPyrMaxRows) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), dim3(nframes), dim3(kPyrThreads),
+                       (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab);
     return hipGetLastError();
 }
 
