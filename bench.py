@@ -201,7 +201,7 @@ def main():
     sub = B // P
     frames_np = orbamd.synth_frames(rank, 0, B, W, H)  # agent = rank
     def allgather(out, inp):
-        # RCCL: in place (inp is out's slice of this rank). gloo (the one-GPU rehearsal): through host memory
+        # RCCL over xGMI; gloo (the one-GPU rehearsal): through host memory
         if backend == "nccl":
             dist.all_gather_into_tensor(out, inp)
         else:

@@ -21,8 +21,7 @@ class AgentSchedule:
     def __init__(self, torch, frames_np, width, height, pipes, device=0, rank=0, world=1, allgather=None,
                  stagger="each", exchange=True, priorities=None, nfeatures=1000):
         """frames_np: uint8 [B, H, W] host frames of this agent (copied to HBM once); allgather(out, inp):
-        all-gather of equal-sized device byte tensors across agents (None at world 1); inp is out's slice of
-        this rank (in place)."""
+        all-gather of equal-sized device byte tensors across agents (None at world 1)."""
         B = len(frames_np)
         assert B % pipes == 0, "frames per step must be a multiple of the graph count"
         self.torch, self.W, self.H, self.B, self.P = torch, width, height, B, pipes
@@ -41,10 +40,11 @@ class AgentSchedule:
         self.done = [torch.cuda.Event() for _ in range(pipes)]
         p0 = self.pipes[0]
         self.slot_bytes = p0.slot_bytes()
-        # the keyframe is packed straight into this agent's slot of the receive buffer: an in-place
-        # all-gather (RCCL's sendbuff == recvbuff + rank * count) and no copy at all at N = 1
+        # N = 1: the keyframe is packed straight into the receive buffer (no copy); N > 1: into its own
+        # send buffer for an out-of-place all-gather
         self.all_slots = torch.zeros(world * self.slot_bytes, dtype=torch.uint8, device=dev)
-        self.my_slot = self.all_slots[rank * self.slot_bytes:(rank + 1) * self.slot_bytes]
+        self.my_slot = (self.all_slots if world == 1 else
+                        torch.zeros(self.slot_bytes, dtype=torch.uint8, device=dev))
         self.xmatch = torch.empty((world, p0.stride), dtype=torch.int32, device=dev)
         self.xn = torch.zeros(world, dtype=torch.int32, device=dev)
         self.pack_err = torch.zeros(16, dtype=torch.int32, device=dev)

@@ -23,7 +23,7 @@ def main():
     torch.cuda.set_device(0)
     W, H, B, P = 640, 480, 64, 2
 
-    def allgather(out, inp):  # inp is out's slice of this rank
+    def allgather(out, inp):
         o = torch.empty(out.numel(), dtype=torch.uint8)
         dist.all_gather_into_tensor(o, inp.cpu().clone())
         out.copy_(o.to(out.device))
