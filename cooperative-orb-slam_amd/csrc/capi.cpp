@@ -346,11 +346,13 @@ struct Geometry {
         // octree LDS: node arrays (92 B/node, NC pow2) + keys (7 B/key)
         NC = 1;
         while (NC < maxnode) NC <<= 1;
-        const int node_bytes = 92 * NC;
-        // keys of a level stay in LDS up to KL (2048 covers a 640x480 / 1000-feature level 0);
-        // larger levels use global scratch. ~38 KB per workgroup -> 4 workgroups per CU.
+        const int node_bytes = 76 * NC;
+        // keys of a level stay in LDS up to KL, larger levels use global scratch. KL is sized so a workgroup
+        // fits 32 KB when that still leaves >= 1024 keys (five octree workgroups per CU beside the other
+        // graphs' kernels; 1888 keys at NC = 256 cover a 640x480 / 1000-feature level 0), else up to 2048.
         if (node_bytes + 7 * 256 > 160 * 1024) return ORBX_EARG;
-        KL = std::min(2048, ((160 * 1024 - node_bytes) / 7) & ~15);
+        const int kl32 = ((32 * 1024 - node_bytes - 64) / 7) & ~15;
+        KL = kl32 >= 1024 ? std::min(2048, kl32) : std::min(2048, ((160 * 1024 - node_bytes) / 7) & ~15);
         lds_bytes = node_bytes + 7 * KL;
         // upload
         if (d_lv.ensure(sizeof(LevelDesc) * L) || d_cells.ensure(sizeof(CellDesc) * cells.size()) ||

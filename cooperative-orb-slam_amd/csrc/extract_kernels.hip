@@ -716,7 +716,7 @@ __device__ __forceinline__ int block_sum(int v, int* red) {
 }
 
 /* LDS layout (bytes), NC = node capacity (pow2-rounded for the sort):
- *   nodes A/B : 2 x NC x {int x0,y0,x1,y1,nk; uint seq}   = 48 NC
+ *   nodes A/B : 2 x NC x {u16 x0,y0,x1,y1; int nk; uint seq} = 32 NC
  *   cnt4      : NC x 4 int                                 = 16 NC
  *   cpos      : NC x 4 u16                                 =  8 NC
  *   spos, dflag, dbase : 3 x NC int                        = 12 NC
@@ -739,8 +739,11 @@ constexpr bool kOctFastPhase1 = ORBX_OCT_FAST1 != 0;  // A/B switch (-DORBX_OCT_
 #endif
 constexpr bool kOctRankSort = ORBX_OCT_RANK != 0;  // A/B switch (-DORBX_OCT_RANK=0: bitonic phase-2 sort)
 
+/* node rectangles as u16 (level coordinates < 4096, the 12-bit key fields): 76 B of LDS per node
+ * instead of 92, so a 256-node table plus 1888 keys fits 32 KB and five workgroups share a CU with
+ * the other graphs' kernels */
 struct NodeT {
-    int* x0; int* y0; int* x1; int* y1; int* nk; uint32_t* seq;
+    uint16_t* x0; uint16_t* y0; uint16_t* x1; uint16_t* y1; int* nk; uint32_t* seq;
 };
 
 __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDesc* __restrict__ levels,
@@ -759,10 +762,10 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
     // --- carve LDS
     uint8_t* p = lds;
     NodeT A, Bt;
-    A.x0 = (int*)p; p += 4 * NC; A.y0 = (int*)p; p += 4 * NC; A.x1 = (int*)p; p += 4 * NC;
-    A.y1 = (int*)p; p += 4 * NC; A.nk = (int*)p; p += 4 * NC; A.seq = (uint32_t*)p; p += 4 * NC;
-    Bt.x0 = (int*)p; p += 4 * NC; Bt.y0 = (int*)p; p += 4 * NC; Bt.x1 = (int*)p; p += 4 * NC;
-    Bt.y1 = (int*)p; p += 4 * NC; Bt.nk = (int*)p; p += 4 * NC; Bt.seq = (uint32_t*)p; p += 4 * NC;
+    A.x0 = (uint16_t*)p; p += 2 * NC; A.y0 = (uint16_t*)p; p += 2 * NC; A.x1 = (uint16_t*)p; p += 2 * NC;
+    A.y1 = (uint16_t*)p; p += 2 * NC; A.nk = (int*)p; p += 4 * NC; A.seq = (uint32_t*)p; p += 4 * NC;
+    Bt.x0 = (uint16_t*)p; p += 2 * NC; Bt.y0 = (uint16_t*)p; p += 2 * NC; Bt.x1 = (uint16_t*)p; p += 2 * NC;
+    Bt.y1 = (uint16_t*)p; p += 2 * NC; Bt.nk = (int*)p; p += 4 * NC; Bt.seq = (uint32_t*)p; p += 4 * NC;
     int* cnt4 = (int*)p; p += 16 * NC;
     int* spos = (int*)p; p += 4 * NC;
     int* dflag = (int*)p; p += 4 * NC;
