@@ -723,6 +723,9 @@ __device__ __forceinline__ int block_sum(int v, int* red) {
  *   sortkey   : NC x u64                                   =  8 NC
  *   keys      : KL x (4 + 2 + 1) (if n <= KL, else global scratch)
  */
+#ifndef ORBX_DESC_STOP
+#define ORBX_DESC_STOP 0  // phase-cost experiment only: >0 cuts k_describe short (results invalid)
+#endif
 #ifndef ORBX_OCT_STOP
 #define ORBX_OCT_STOP 0  // phase-cost experiment only: >0 cuts k_octree short (results invalid)
 #endif
@@ -1527,6 +1530,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
             }
         }
     }
+#if ORBX_DESC_STOP == 1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase-cost experiment: staging only
+    if (wv[0].x == 0x12345678u && wv[15].y == 0x9abcdef0u) out_counts[f] = -1;  // keep the loads alive
+    return;
+#endif
     int m10, m01;
     {
         // per row ri = r + 2p: A' += sum (u+15) I, S += sum I, M' += 2p * sum I (24-bit multiply by a
@@ -1559,6 +1567,10 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     float sa, ca;
     glibc_sincosf(theta, &sa, &ca);
     const float a = ca, b = sa;
+#if ORBX_DESC_STOP == 2
+    if (a == 12345.f && b == 54321.f) out_counts[f] = -1;  // phase-cost experiment: up to the angle / sincos
+    return;
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA patch writes have landed
     wave_sync();  // patch stores of the other lanes of this group
     const uint8_t* pc0 = patch + kDescPatchR * kDescPatchPitch + kDescPatchR + pmis;  // keypoint
