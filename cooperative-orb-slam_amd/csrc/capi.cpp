@@ -525,8 +525,10 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     if (prof_mark(h, 0, 1, st)) return ORBX_EDEVICE;
     auto blur = [&](hipStream_t bs) -> int {
         if (prof_mark(h, 3, 0, bs)) return ORBX_EDEVICE;
+#ifndef ORBX_SKIP_BLUR  // upper-bound experiment only (results invalid): the step without the blur kernel
         HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                                 nullptr, g.nbjobs, nullptr, nframes, bs));
+#endif
         return prof_mark(h, 3, 1, bs);
     };
     if (!serial) {
@@ -999,17 +1001,28 @@ struct orbm_ctx {
     DevBuf scratch;
     DevBuf err;  // device error flag of the *_device calls that validate their input (orbm_check_error)
     std::vector<uint8_t> host;
-    void* pinned = nullptr;  // host staging of one call's inputs (one H2D copy)
+    void* pinned = nullptr;  // host staging of one call's inputs (one H2D copy) and its results
+    void* pinned_dev = nullptr;
     size_t pinned_bytes = 0;
     uint8_t* ensure_pinned(size_t need) {
         if (need <= pinned_bytes) return (uint8_t*)pinned;
         if (pinned) (void)hipHostFree(pinned);
         pinned = nullptr;
+        pinned_dev = nullptr;
         pinned_bytes = 0;
         if (hipHostMalloc(&pinned, need, 0) != hipSuccess) return nullptr;
+        if (hipHostGetDevicePointer(&pinned_dev, pinned, 0) != hipSuccess) {
+            (void)hipHostFree(pinned);
+            pinned = nullptr;
+            return nullptr;
+        }
         pinned_bytes = need;
         return (uint8_t*)pinned;
     }
+    /* device address of byte `off` of the pinned buffer (kernels write results there directly) */
+    int32_t* pinned_on_device(size_t off) const { return (int32_t*)((uint8_t*)pinned_dev + off); }
+    /* the per-call state words (match_kernels.hip call_tail): ints 16..47 of the zeroed err buffer */
+    int32_t* call_state() { return err.as<int32_t>() + 16; }
 };
 
 namespace {
@@ -1117,7 +1130,7 @@ int orbm_create(int device, orbm_ctx** out) {
         delete c;
         return ORBX_EDEVICE;
     }
-    if (c->err.ensure(64) || hipMemset(c->err.p, 0, 64) != hipSuccess) {
+    if (c->err.ensure(256) || hipMemset(c->err.p, 0, 256) != hipSuccess) {
         orbm_destroy(c);
         return ORBX_EDEVICE;
     }
@@ -1164,12 +1177,6 @@ void orbm_epipole(const float R2w[9], const float t2w[3], const float Cw[3], flo
     *ey = fy * C2[1] * invz + cy;
 }
 
-static int count_matches(const int32_t* m, int n) {
-    int c = 0;
-    for (int i = 0; i < n; i++) c += m[i] >= 0;
-    return c;
-}
-
 int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2,
                                   const float F12[9], float ex, float ey, int only_stereo, int check_ori,
                                   int32_t* match12, int* nmatches) {
@@ -1183,31 +1190,40 @@ int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const 
         for (int q = qb; q < qe; q += 64)
             tasks.push_back({q, std::min(q + 64, qe), kf2->node_off[c.second], kf2->node_off[c.second + 1]});
     }
+    const int n1 = kf1->n;
+    if (tasks.empty()) {  // no common node: nothing to match
+        std::fill(match12, match12 + n1, -1);
+        if (nmatches) *nmatches = 0;
+        return 0;
+    }
+    // one H2D copy (views, tasks), one launch whose last workgroup writes the (rotation-filtered)
+    // matches into pinned host memory pre-filled with -1, one synchronize
     Carve cv;
     ViewPlan p1, p2;
     plan_view(cv, kf1, p1);
     plan_view(cv, kf2, p2);
-    const size_t o_tasks = cv.take(sizeof(NodeTask) * std::max<size_t>(tasks.size(), 1));
+    const size_t o_tasks = cv.take(sizeof(NodeTask) * tasks.size());
     const size_t in_bytes = cv.off;
-    const size_t o_out = cv.take(4 * (size_t)std::max(kf1->n, 1));
+    const size_t o_list = cv.take(16 * (size_t)std::max(n1, 1));
+    const size_t o_res = cv.take(4 * ((size_t)n1 + 1));
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
     uint8_t* hp = ctx->ensure_pinned(cv.off);
     if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
     DevView d1 = stage_view(hp, base, kf1, p1), d2 = stage_view(hp, base, kf2, p2);
-    if (!tasks.empty()) memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
+    memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
+    int32_t* res = (int32_t*)(hp + o_res);
+    std::fill(res, res + n1 + 1, -1);
     HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
-    int32_t* dout = (int32_t*)(base + o_out);
-    HIPR(hipMemsetAsync(dout, 0xFF, 4 * (size_t)std::max(kf1->n, 1), ctx->stream));
     MatchGeom g;
     make_geom(g, F12, ex, ey, kf2->nlevels, kf2->scale_factors, kf2->level_sigma2);
-    HIPR(launch_tri_nodes(d1, d2, (const NodeTask*)(base + o_tasks), (int)tasks.size(), g, only_stereo, dout,
+    const CallTail tail{ctx->call_state(), (int32_t*)(base + o_list), ctx->pinned_on_device(o_res), d1.angle, d2.angle,
+                        n1, check_ori ? 1 : 0, 0};
+    HIPR(launch_tri_nodes(d1, d2, (const NodeTask*)(base + o_tasks), (int)tasks.size(), g, only_stereo, tail,
                           ctx->stream));
-    if (check_ori) HIPR(launch_rot_filter(kf1->n, dout, d1.angle, d2.angle, 0, nullptr, ctx->stream));
-    if (kf1->n) HIPR(hipMemcpyAsync(hp + o_out, dout, 4 * (size_t)kf1->n, hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipStreamSynchronize(ctx->stream));
-    if (kf1->n) memcpy(match12, hp + o_out, 4 * (size_t)kf1->n);
-    if (nmatches) *nmatches = count_matches(match12, kf1->n);
+    memcpy(match12, res + 1, 4 * (size_t)n1);
+    if (nmatches) *nmatches = res[0];
     return 0;
 }
 
@@ -1225,34 +1241,38 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
         tasks.push_back(t);
     }
     if (max_nc > 64 * 1024) return ORBX_EARG;
+    if (tasks.empty()) {  // no common node: nothing to match
+        std::fill(out, out + nout, -1);
+        if (nmatches) *nmatches = 0;
+        return 0;
+    }
+    // one H2D copy, one launch (greedy per node; the last workgroup's rotation filter writes the
+    // matches into pinned host memory pre-filled with -1), one synchronize
     Carve cv;
     ViewPlan pq, pc;
     plan_view(cv, vq, pq);
     plan_view(cv, vc, pc);
-    const size_t o_tasks = cv.take(sizeof(NodeTask) * std::max<size_t>(tasks.size(), 1));
+    const size_t o_tasks = cv.take(sizeof(NodeTask) * tasks.size());
     const size_t in_bytes = cv.off;
-    const size_t o_out = cv.take(4 * (size_t)std::max(nout, 1));
+    const size_t o_list = cv.take(16 * (size_t)std::max(nout, 1));
+    const size_t o_res = cv.take(4 * ((size_t)nout + 1));
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
     uint8_t* hp = ctx->ensure_pinned(cv.off);
     if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
     DevView dq = stage_view(hp, base, vq, pq), dc = stage_view(hp, base, vc, pc);
-    if (!tasks.empty()) memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
+    memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
+    int32_t* res = (int32_t*)(hp + o_res);
+    std::fill(res, res + nout + 1, -1);
     HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
-    int32_t* dout = (int32_t*)(base + o_out);
-    HIPR(hipMemsetAsync(dout, 0xFF, 4 * (size_t)std::max(nout, 1), ctx->stream));
-    HIPR(launch_bow(dq, dc, (const NodeTask*)(base + o_tasks), (int)tasks.size(), max_nc, nnratio, mode, dout,
+    // mode 0: out indexed by the F idx, partner = KF idx -> rot = angKF[m] - angF[i] (swap)
+    const CallTail tail{ctx->call_state(), (int32_t*)(base + o_list), ctx->pinned_on_device(o_res), dq.angle,
+                        dc.angle, nout, check_ori ? 1 : 0, mode == 0 ? 1 : 0};
+    HIPR(launch_bow(dq, dc, (const NodeTask*)(base + o_tasks), (int)tasks.size(), max_nc, nnratio, mode, tail,
                     ctx->stream));
-    if (check_ori) {
-        if (mode == 0)  // out indexed by F idx, partner = KF idx: rot = angKF[m] - angF[i]
-            HIPR(launch_rot_filter(nout, dout, dq.angle, dc.angle, 1, nullptr, ctx->stream));
-        else
-            HIPR(launch_rot_filter(nout, dout, dq.angle, dc.angle, 0, nullptr, ctx->stream));
-    }
-    if (nout) HIPR(hipMemcpyAsync(hp + o_out, dout, 4 * (size_t)nout, hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipStreamSynchronize(ctx->stream));
-    if (nout) memcpy(out, hp + o_out, 4 * (size_t)nout);
-    if (nmatches) *nmatches = count_matches(out, nout);
+    memcpy(out, res + 1, 4 * (size_t)nout);
+    if (nmatches) *nmatches = res[0];
     return 0;
 }
 

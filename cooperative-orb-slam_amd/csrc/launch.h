@@ -55,9 +55,9 @@ hipError_t launch_bow_pairs(int npairs, int max_nodes, const int32_t* qf, const 
                             hipStream_t st);
 hipError_t launch_count_pairs(int npairs, const int32_t* out, int kp_stride, int32_t* nmatches, hipStream_t st);
 hipError_t launch_tri_nodes(const DevView& v1, const DevView& v2, const NodeTask* tasks, int ntasks,
-                            const MatchGeom& g, int only_stereo, int32_t* match12, hipStream_t st);
+                            const MatchGeom& g, int only_stereo, const CallTail& tail, hipStream_t st);
 hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* tasks, int ntasks, int max_nc,
-                      float nnratio, int mode, int32_t* out, hipStream_t st);
+                      float nnratio, int mode, const CallTail& tail, hipStream_t st);
 hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* angB, int swap, int32_t* nout,
                              hipStream_t st);
 

@@ -328,41 +328,164 @@ __global__ __launch_bounds__(256) void k_tri_bf(const int32_t* __restrict__ q1, 
     tri_bf_body<SPLIT>(s, g, match12 + (long long)p * kp_stride, nmatches + p);
 }
 
-/* ----------------------------------------------------------------------------------- */
-/* General node-based SearchForTriangulation: one wave per (common node, 64 queries).   */
-/* ----------------------------------------------------------------------------------- */
-__global__ __launch_bounds__(64) void k_tri_nodes(const DevView v1, const DevView v2, const NodeTask* __restrict__ tasks,
-                                                  MatchGeom g, int only_stereo, int32_t* __restrict__ match12) {
-    const NodeTask t = tasks[blockIdx.x];
-    const int i1 = t.q_begin + threadIdx.x;
-    if (i1 >= t.q_end) return;
-    const int idx1 = v1.node_feat[i1];
-    if (v1.has_mp && v1.has_mp[idx1]) return;
-    const bool st1 = v1.uright ? v1.uright[idx1] >= 0.f : false;
-    if (only_stereo && !st1) return;
-    uint32_t q[8];
-    const uint32_t* qd = (const uint32_t*)(v1.desc + (long long)idx1 * 32);
-#pragma unroll
-    for (int k = 0; k < 8; k++) q[k] = qd[k];
-    float a, b, c;
-    epi_line(g, v1.x[idx1], v1.y[idx1], &a, &b, &c);
-    int bestDist = 50, bestIdx2 = -1;
-    for (int i2 = t.c_begin; i2 < t.c_end; i2++) {
-        const int idx2 = v2.node_feat[i2];
-        if (v2.has_mp && v2.has_mp[idx2]) continue;
-        const bool st2 = v2.uright ? v2.uright[idx2] >= 0.f : false;
-        if (only_stereo && !st2) continue;
-        const int dist = hamming8(q, (const uint32_t*)(v2.desc + (long long)idx2 * 32));
-        if (dist > 50 || dist > bestDist) continue;
-        const float x2 = v2.x[idx2], y2 = v2.y[idx2];
-        const int oct2 = v2.octave[idx2];
-        if (!st1 && !st2 && near_epipole(g, x2, y2, oct2)) continue;
-        if (epi_ok(a, b, c, x2, y2, g.th384[oct2])) {
-            bestIdx2 = idx2;
-            bestDist = dist;
+/* rotation bin of a match (ORBmatcher.cc:236-246): rot = angA[a] - angB[b], (a,b) = (i, j) or,
+ * with swap, (j, i) */
+__device__ __forceinline__ int rot_bin(const float* angA, const float* angB, int i, int j, int swap) {
+    float rot = swap ? __fsub_rn(angA[j], angB[i]) : __fsub_rn(angA[i], angB[j]);
+    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+    int bin = (int)roundf(__fmul_rn(rot, 1.0f / 30));
+    return bin == 30 ? 0 : bin;
+}
+
+/* ComputeThreeMaxima (ORBmatcher.cc:1601-1642) over a 30-bin histogram, by one thread */
+__device__ __forceinline__ void three_maxima(const int* hist, int* keep) {
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < 30; i++) {
+        const int s = hist[i];
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+        else if (s > max3) { max3 = s; ind3 = i; }
+    }
+    if (max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
+    else if (max3 < __fmul_rn(0.1f, (float)max1)) { ind3 = -1; }
+    keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
+}
+
+/* Single host-API call (k_tri_nodes / k_bow), one launch: every accepted match is appended to a
+ * compact device list with its rotation bin (ORBmatcher.cc:236-246), and the bin counted in a device
+ * histogram, as it is made. The last workgroup of the launch to finish (a ticket; agent-scope fences
+ * order every workgroup's list writes before it) takes ComputeThreeMaxima of the histogram
+ * (ORBmatcher.cc:1601-1642) and writes the surviving matches and their count straight into the
+ * caller's pinned host buffer, which the host filled with -1 (host_out[0] = count, host_out[1 + i]).
+ * Its work is proportional to the matches, not to N. The state words are zero between calls. */
+__device__ __forceinline__ void call_emit(const CallTail& t, int i, int j) {
+    const int bin = t.check_ori ? rot_bin(t.angA, t.angB, i, j, t.swap) : 0;
+    if (t.check_ori) atomicAdd(t.state + 2 + bin, 1);
+    const int k = atomicAdd(t.state + 1, 1);
+    ((int4*)t.list)[k] = make_int4(i, j, bin, 0);
+}
+
+__device__ void call_tail(const CallTail& t) {
+    __shared__ int s_last, s_cnt, s_nl;
+    __shared__ int hist[30], keep[3];
+    __syncthreads();
+    __threadfence();
+    if (threadIdx.x == 0) s_last = atomicAdd(t.state, 1) == (int)(gridDim.x - 1);
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (threadIdx.x < 30) hist[threadIdx.x] = t.check_ori ? t.state[2 + threadIdx.x] : 0;
+    if (threadIdx.x == 0) {
+        s_cnt = 0;
+        s_nl = t.state[1];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (t.check_ori) three_maxima(hist, keep);
+        else keep[0] = keep[1] = keep[2] = -2;
+    }
+    __syncthreads();
+    const int nl = s_nl;
+    int local = 0;
+    for (int k = threadIdx.x; k < nl; k += blockDim.x) {
+        const int4 e = ((const int4*)t.list)[k];
+        if (!t.check_ori || e.z == keep[0] || e.z == keep[1] || e.z == keep[2]) {
+            t.host_out[1 + e.x] = e.y;
+            local++;
         }
     }
-    match12[idx1] = bestIdx2;
+    atomicAdd(&s_cnt, local);
+    __syncthreads();
+    if (threadIdx.x < 30) t.state[2 + threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        t.host_out[0] = s_cnt;
+        t.state[1] = 0;
+        t.state[0] = 0;
+    }
+}
+
+/* ----------------------------------------------------------------------------------- */
+/* General node-based SearchForTriangulation (host API, one keyframe pair per call):     */
+/* one 256-thread workgroup per (common node, 64 queries). The node's candidates are      */
+/* staged through LDS kNodeStage at a time (descriptor, position, octave, eligibility:    */
+/* one round of global-load latency per round instead of a dependent chain per candidate)  */
+/* and the 4 waves scan interleaved quarters of each round for the same 64 queries. The    */
+/* reference's scan (ORBmatcher.cc:704-776: skip dist > TH_LOW or > best, geometric checks, */
+/* accept ties) returns the valid candidate of minimum distance, the later one on ties, so */
+/* the quarters merge by (distance, node position).                                        */
+/* ----------------------------------------------------------------------------------- */
+constexpr int kNodeStage = 256;
+
+__global__ __launch_bounds__(256) void k_tri_nodes(const DevView v1, const DevView v2, const NodeTask* __restrict__ tasks,
+                                                   MatchGeom g, int only_stereo, CallTail tail) {
+    __shared__ uint4 s_d[kNodeStage * 2];
+    __shared__ float s_x[kNodeStage], s_y[kNodeStage];
+    __shared__ int s_oct[kNodeStage];  // octave | 0x100 stereo; -1 = not a candidate (MapPoint / mono in stereo mode)
+    __shared__ int s_idx[kNodeStage];
+    __shared__ int s_bd[4][64], s_bp[4][64];
+    const NodeTask t = tasks[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
+    const int i1 = t.q_begin + lane;
+    const int idx1 = i1 < t.q_end ? v1.node_feat[i1] : -1;
+    const bool st1 = idx1 >= 0 && v1.uright ? v1.uright[idx1] >= 0.f : false;
+    const bool active = idx1 >= 0 && !(v1.has_mp && v1.has_mp[idx1]) && (!only_stereo || st1);
+    uint32_t q[8];
+    float a = 0.f, b = 0.f, c = 0.f;
+    if (active) {
+        const uint4* qd = (const uint4*)(v1.desc + (long long)idx1 * 32);
+        const uint4 qa = qd[0], qb = qd[1];
+        q[0] = qa.x; q[1] = qa.y; q[2] = qa.z; q[3] = qa.w; q[4] = qb.x; q[5] = qb.y; q[6] = qb.z; q[7] = qb.w;
+        epi_line(g, v1.x[idx1], v1.y[idx1], &a, &b, &c);
+    }
+    int bestDist = 50, bestPos = -1, bestIdx2 = -1;  // TH_LOW (ORBmatcher.cc:704)
+    for (int cb = t.c_begin; cb < t.c_end; cb += kNodeStage) {
+        const int nt = min(kNodeStage, t.c_end - cb);
+        __syncthreads();
+        if (tid < nt) {
+            const int idx2 = v2.node_feat[cb + tid];
+            const bool st2 = v2.uright ? v2.uright[idx2] >= 0.f : false;
+            const bool ok = !(v2.has_mp && v2.has_mp[idx2]) && (!only_stereo || st2);
+            const uint4* cd = (const uint4*)(v2.desc + (long long)idx2 * 32);
+            s_d[2 * tid] = cd[0];
+            s_d[2 * tid + 1] = cd[1];
+            s_x[tid] = v2.x[idx2];
+            s_y[tid] = v2.y[idx2];
+            s_oct[tid] = ok ? (v2.octave[idx2] | (st2 ? 0x100 : 0)) : -1;
+            s_idx[tid] = idx2;
+        }
+        __syncthreads();
+        if (!active) continue;
+        for (int j = part; j < nt; j += 4) {
+            const int oc = s_oct[j];
+            if (oc < 0) continue;
+            const uint4 c0 = s_d[2 * j], c1 = s_d[2 * j + 1];
+            const int dist = __popc(q[0] ^ c0.x) + __popc(q[1] ^ c0.y) + __popc(q[2] ^ c0.z) + __popc(q[3] ^ c0.w) +
+                             __popc(q[4] ^ c1.x) + __popc(q[5] ^ c1.y) + __popc(q[6] ^ c1.z) + __popc(q[7] ^ c1.w);
+            if (dist > 50 || dist > bestDist) continue;
+            const float x2 = s_x[j], y2 = s_y[j];
+            const int oct2 = oc & 0xFF;
+            if (!st1 && !(oc & 0x100) && near_epipole(g, x2, y2, oct2)) continue;  // ORBmatcher.cc:743-749
+            if (epi_ok(a, b, c, x2, y2, g.th384[oct2])) {
+                bestDist = dist;
+                bestPos = cb + j;
+                bestIdx2 = s_idx[j];
+            }
+        }
+    }
+    s_bd[part][lane] = bestDist;
+    s_bp[part][lane] = bestPos;
+    __syncthreads();
+    if (part == 0 && active) {
+        for (int k = 1; k < 4; k++) {
+            const int d = s_bd[k][lane], pos = s_bp[k][lane];
+            if (pos >= 0 && (bestPos < 0 || d < bestDist || (d == bestDist && pos > bestPos))) {
+                bestDist = d;
+                bestPos = pos;
+            }
+        }
+        if (bestPos >= 0) call_emit(tail, idx1, bestPos == s_bp[0][lane] ? bestIdx2 : v2.node_feat[bestPos]);
+    }
+    call_tail(tail);
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -448,54 +571,107 @@ __device__ __forceinline__ Top2 top2_merge(Top2 A, Top2 B) {
     return r;
 }
 
+/* STAGED (node of <= kBowStage candidates, the common case: ~10 per node at levelsup 4): the node's
+ * candidate descriptors and eligibility and, 64 at a time, its queries' descriptors are staged in LDS
+ * first, so the greedy loop over queries runs without a global-load round trip per query */
+constexpr int kBowStage = 512;
+
+template <bool STAGED>
 __global__ __launch_bounds__(64) void k_bow(const DevView vq, const DevView vc, const NodeTask* __restrict__ tasks,
-                                            float nnratio, int mode, int32_t* __restrict__ out) {
-    extern __shared__ uint8_t matched[];  // per candidate position in the node
+                                            float nnratio, int mode, CallTail tail) {
+    extern __shared__ uint8_t matched[];  // per candidate position in the node (unstaged form)
+    __shared__ uint4 s_cd[STAGED ? kBowStage * 2 : 1];
+    __shared__ uint8_t s_cok[STAGED ? kBowStage : 1], s_cm[STAGED ? kBowStage : 1];
+    __shared__ uint4 s_qd[STAGED ? 128 : 1];
+    __shared__ int s_qi[STAGED ? 64 : 1];
     const NodeTask t = tasks[blockIdx.x];
     const int lane = threadIdx.x;
     const int nc = t.c_end - t.c_begin;
-    for (int j = lane; j < nc; j += 64) matched[j] = 0;
-    __syncthreads();
-    for (int i1 = t.q_begin; i1 < t.q_end; i1++) {
-        const int idxq = vq.node_feat[i1];
-        if (!(vq.has_mp && vq.has_mp[idxq])) continue;
-        if (vq.mp_bad && vq.mp_bad[idxq]) continue;
-        const uint32_t* qd = (const uint32_t*)(vq.desc + (long long)idxq * 32);
-        uint32_t q[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) q[k] = qd[k];
-        Top2 r = {256, -1, 256};
-        for (int j = lane; j < nc; j += 64) {
-            if (matched[j]) continue;
+    uint8_t* mflag = STAGED ? s_cm : matched;
+    for (int j = lane; j < nc; j += 64) {
+        mflag[j] = 0;
+        if (STAGED) {
             const int idxc = vc.node_feat[t.c_begin + j];
-            if (mode == 1) {
-                if (!(vc.has_mp && vc.has_mp[idxc])) continue;
-                if (vc.mp_bad && vc.mp_bad[idxc]) continue;
-            }
-            const int dist = hamming8(q, (const uint32_t*)(vc.desc + (long long)idxc * 32));
-            if (dist < r.b1) { r.b2 = r.b1; r.b1 = dist; r.i1 = j; }
-            else if (dist < r.b2) { r.b2 = dist; }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            Top2 o2;
-            o2.b1 = __shfl_xor(r.b1, o, 64);
-            o2.i1 = __shfl_xor(r.i1, o, 64);
-            o2.b2 = __shfl_xor(r.b2, o, 64);
-            r = top2_merge(r, o2);
-        }
-        const bool ok_th = mode == 0 ? (r.b1 <= 50) : (r.b1 < 50);
-        if (ok_th && r.i1 >= 0 && __fmul_rn(1.0f, (float)r.b1) < __fmul_rn(nnratio, (float)r.b2)) {
-            const int idxc = vc.node_feat[t.c_begin + r.i1];
-            __syncthreads();
-            if (lane == 0) {
-                matched[r.i1] = 1;
-                if (mode == 0) out[idxc] = idxq;  // vpMapPointMatches[bestIdxF] = pMP(KF idx)
-                else out[idxq] = idxc;            // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
-            }
-            __syncthreads();
+            const uint4* cd = (const uint4*)(vc.desc + (long long)idxc * 32);
+            s_cd[2 * j] = cd[0];
+            s_cd[2 * j + 1] = cd[1];
+            s_cok[j] = mode == 0 || ((vc.has_mp && vc.has_mp[idxc]) && !(vc.mp_bad && vc.mp_bad[idxc]));
         }
     }
+    __syncthreads();
+    for (int qb = t.q_begin; qb < t.q_end; qb += 64) {
+        const int nq = min(64, t.q_end - qb);
+        if (STAGED) {
+            // this chunk's queries: index (-1 = no good MapPoint) and descriptor
+            if (lane < nq) {
+                const int idxq = vq.node_feat[qb + lane];
+                const bool ok = (vq.has_mp && vq.has_mp[idxq]) && !(vq.mp_bad && vq.mp_bad[idxq]);
+                s_qi[lane] = ok ? idxq : -1;
+                const uint4* qd = (const uint4*)(vq.desc + (long long)idxq * 32);
+                s_qd[2 * lane] = qd[0];
+                s_qd[2 * lane + 1] = qd[1];
+            }
+            __syncthreads();
+        }
+        for (int k = 0; k < nq; k++) {
+            int idxq;
+            uint32_t q[8];
+            if (STAGED) {
+                idxq = s_qi[k];
+                if (idxq < 0) continue;
+                const uint4 a0 = s_qd[2 * k], a1 = s_qd[2 * k + 1];
+                q[0] = a0.x; q[1] = a0.y; q[2] = a0.z; q[3] = a0.w; q[4] = a1.x; q[5] = a1.y; q[6] = a1.z; q[7] = a1.w;
+            } else {
+                idxq = vq.node_feat[qb + k];
+                if (!(vq.has_mp && vq.has_mp[idxq])) continue;
+                if (vq.mp_bad && vq.mp_bad[idxq]) continue;
+                const uint32_t* qd = (const uint32_t*)(vq.desc + (long long)idxq * 32);
+#pragma unroll
+                for (int u = 0; u < 8; u++) q[u] = qd[u];
+            }
+            Top2 r = {256, -1, 256};
+            for (int j = lane; j < nc; j += 64) {
+                if (mflag[j]) continue;
+                int dist;
+                if (STAGED) {
+                    if (!s_cok[j]) continue;
+                    const uint4 c0 = s_cd[2 * j], c1 = s_cd[2 * j + 1];
+                    dist = __popc(q[0] ^ c0.x) + __popc(q[1] ^ c0.y) + __popc(q[2] ^ c0.z) + __popc(q[3] ^ c0.w) +
+                           __popc(q[4] ^ c1.x) + __popc(q[5] ^ c1.y) + __popc(q[6] ^ c1.z) + __popc(q[7] ^ c1.w);
+                } else {
+                    const int idxc = vc.node_feat[t.c_begin + j];
+                    if (mode == 1) {
+                        if (!(vc.has_mp && vc.has_mp[idxc])) continue;
+                        if (vc.mp_bad && vc.mp_bad[idxc]) continue;
+                    }
+                    dist = hamming8(q, (const uint32_t*)(vc.desc + (long long)idxc * 32));
+                }
+                if (dist < r.b1) { r.b2 = r.b1; r.b1 = dist; r.i1 = j; }
+                else if (dist < r.b2) { r.b2 = dist; }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                Top2 o2;
+                o2.b1 = __shfl_xor(r.b1, o, 64);
+                o2.i1 = __shfl_xor(r.i1, o, 64);
+                o2.b2 = __shfl_xor(r.b2, o, 64);
+                r = top2_merge(r, o2);
+            }
+            const bool ok_th = mode == 0 ? (r.b1 <= 50) : (r.b1 < 50);
+            if (ok_th && r.i1 >= 0 && __fmul_rn(1.0f, (float)r.b1) < __fmul_rn(nnratio, (float)r.b2)) {
+                const int idxc = vc.node_feat[t.c_begin + r.i1];
+                __syncthreads();
+                if (lane == 0) {
+                    mflag[r.i1] = 1;
+                    if (mode == 0) call_emit(tail, idxc, idxq);  // vpMapPointMatches[bestIdxF] = pMP(KF idx)
+                    else call_emit(tail, idxq, idxc);            // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
+                }
+                __syncthreads();
+            }
+        }
+        if (STAGED) __syncthreads();  // s_qi / s_qd are rewritten by the next chunk
+    }
+    call_tail(tail);
 }
 
 /* SearchByBoW for a batch of frame pairs with the FeatureVectors of orbv_transform_batch_device on
@@ -591,38 +767,18 @@ __global__ __launch_bounds__(256) void k_rot_filter(int n, int32_t* __restrict__
     __shared__ int keep[3];
     if (threadIdx.x < 30) hist[threadIdx.x] = 0;
     __syncthreads();
-    const float factor = 1.0f / 30;
     for (int i = threadIdx.x; i < n; i += 256) {
         const int j = m[i];
-        if (j < 0) continue;
-        float rot = swap ? __fsub_rn(angA[j], angB[i]) : __fsub_rn(angA[i], angB[j]);
-        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-        int bin = (int)roundf(__fmul_rn(rot, factor));
-        if (bin == 30) bin = 0;
-        atomicAdd(&hist[bin], 1);
+        if (j >= 0) atomicAdd(&hist[rot_bin(angA, angB, i, j, swap)], 1);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-        for (int i = 0; i < 30; i++) {
-            const int s = hist[i];
-            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-            else if (s > max3) { max3 = s; ind3 = i; }
-        }
-        if (max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
-        else if (max3 < __fmul_rn(0.1f, (float)max1)) { ind3 = -1; }
-        keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
-    }
+    if (threadIdx.x == 0) three_maxima(hist, keep);
     __syncthreads();
     int local = 0;
     for (int i = threadIdx.x; i < n; i += 256) {
         const int j = m[i];
         if (j < 0) continue;
-        float rot = swap ? __fsub_rn(angA[j], angB[i]) : __fsub_rn(angA[i], angB[j]);
-        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-        int bin = (int)roundf(__fmul_rn(rot, factor));
-        if (bin == 30) bin = 0;
+        const int bin = rot_bin(angA, angB, i, j, swap);
         if (bin != keep[0] && bin != keep[1] && bin != keep[2]) m[i] = -1;
         else local++;
     }
@@ -643,28 +799,19 @@ __global__ __launch_bounds__(256) void k_rot_filter_pairs(const int32_t* __restr
     const int n = counts[q1[p]];
     if (threadIdx.x < 30) hist[threadIdx.x] = 0;
     __syncthreads();
-    const float factor = 1.0f / 30;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        const int j = m[i];
-        if (j < 0) continue;
+    auto bin_of = [&](int i, int j) {
         float rot = swap ? __fsub_rn(k2[j].angle, k1[i].angle) : __fsub_rn(k1[i].angle, k2[j].angle);
         if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-        int bin = (int)roundf(__fmul_rn(rot, factor));
-        if (bin == 30) bin = 0;
-        atomicAdd(&hist[bin], 1);
+        const int bin = (int)roundf(__fmul_rn(rot, 1.0f / 30));
+        return bin == 30 ? 0 : bin;
+    };
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int j = m[i];
+        if (j >= 0) atomicAdd(&hist[bin_of(i, j)], 1);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-        for (int i = 0; i < 30; i++) {
-            const int s = hist[i];
-            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-            else if (s > max3) { max3 = s; ind3 = i; }
-        }
-        if (max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
-        else if (max3 < __fmul_rn(0.1f, (float)max1)) { ind3 = -1; }
-        keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
+        three_maxima(hist, keep);
         nmatches[p] = 0;
     }
     __syncthreads();
@@ -672,10 +819,7 @@ __global__ __launch_bounds__(256) void k_rot_filter_pairs(const int32_t* __restr
     for (int i = threadIdx.x; i < n; i += 256) {
         const int j = m[i];
         if (j < 0) continue;
-        float rot = swap ? __fsub_rn(k2[j].angle, k1[i].angle) : __fsub_rn(k1[i].angle, k2[j].angle);
-        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-        int bin = (int)roundf(__fmul_rn(rot, factor));
-        if (bin == 30) bin = 0;
+        const int bin = bin_of(i, j);
         if (bin != keep[0] && bin != keep[1] && bin != keep[2]) m[i] = -1;
         else local++;
     }
@@ -745,17 +889,20 @@ hipError_t launch_count_pairs(int npairs, const int32_t* out, int kp_stride, int
 }
 
 hipError_t launch_tri_nodes(const DevView& v1, const DevView& v2, const NodeTask* tasks, int ntasks,
-                            const MatchGeom& g, int only_stereo, int32_t* match12, hipStream_t st) {
+                            const MatchGeom& g, int only_stereo, const CallTail& tail, hipStream_t st) {
     if (ntasks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_tri_nodes, dim3(ntasks), dim3(64), 0, st, v1, v2, tasks, g, only_stereo, match12);
+    hipLaunchKernelGGL(k_tri_nodes, dim3(ntasks), dim3(256), 0, st, v1, v2, tasks, g, only_stereo, tail);
     return hipGetLastError();
 }
 
 hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* tasks, int ntasks, int max_nc,
-                      float nnratio, int mode, int32_t* out, hipStream_t st) {
+                      float nnratio, int mode, const CallTail& tail, hipStream_t st) {
     if (ntasks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_bow, dim3(ntasks), dim3(64), (size_t)(max_nc > 0 ? max_nc : 1), st, vq, vc, tasks,
-                       nnratio, mode, out);
+    if (max_nc <= kBowStage)
+        hipLaunchKernelGGL(k_bow<true>, dim3(ntasks), dim3(64), 0, st, vq, vc, tasks, nnratio, mode, tail);
+    else
+        hipLaunchKernelGGL(k_bow<false>, dim3(ntasks), dim3(64), (size_t)max_nc, st, vq, vc, tasks, nnratio, mode,
+                           tail);
     return hipGetLastError();
 }
 

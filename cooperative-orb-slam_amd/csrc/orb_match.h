@@ -35,4 +35,16 @@ struct NodeTask {
     int q_begin, q_end, c_begin, c_end;
 };
 
+/* one host-API match call (match_kernels.hip call_emit / call_tail): state = 32 zeroed device
+ * words (ticket, list length, 30 rotation bins), list = device scratch for up to n matches,
+ * host_out = the caller's pinned buffer (count, then n entries pre-filled with -1) */
+struct CallTail {
+    int32_t* state;
+    int32_t* list;  // 4 words per match: index, partner, rotation bin, 0
+    int32_t* host_out;
+    const float* angA;
+    const float* angB;
+    int n, check_ori, swap;
+};
+
 }  // namespace orbamd

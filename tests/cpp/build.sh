@@ -19,3 +19,8 @@ g++ -std=c++14 -O1 -Wall -Wno-unused-function \
   -L "$R/cooperative-orb-slam_amd/lib" -lorbamd \
   -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,/opt/rocm/lib \
   -o "$R/tests/cpp/build/test_slot"
+# per-call latency of the host C ABI vs the oracle, from C++ (tools/run_latency.sh, profiles/)
+g++ -std=c++14 -O2 -Wall -I "$R/include" -I "$R/oracle" "$R/tests/cpp/bench_latency.cpp" \
+  -L "$R/cooperative-orb-slam_amd/lib" -lorbamd -L "$R/oracle/build" -lorb_oracle \
+  -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,"$R/oracle/build" -Wl,-rpath,/opt/rocm/lib \
+  -o "$R/tests/cpp/build/bench_latency"

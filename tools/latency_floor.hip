@@ -1,0 +1,92 @@
+// latency_floor.hip -- per-call latency floor of a host-API matcher call on one stream: what an
+// H2D upload, N dependent kernel launches, an async memset, a D2H download and the final
+// hipStreamSynchronize cost with no work in the kernels. Sizes are those of one SearchByBoW call
+// (two 1000-keypoint views, ~100 KB in, 4 KB out). Build: hipcc --offload-arch=gfx950 -O2.
+#include <hip/hip_runtime.h>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+
+__global__ void k_empty(int* p) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && p[0] == 12345) p[1] = 1;
+}
+__global__ void k_write_host(int* __restrict__ out, const int* __restrict__ in, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = in[i];
+}
+
+#define CK(x)                                                   \
+    do {                                                        \
+        hipError_t e = (x);                                     \
+        if (e != hipSuccess) {                                  \
+            printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); \
+            return 1;                                           \
+        }                                                       \
+    } while (0)
+
+int main() {
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const size_t in_b = 100 << 10, out_b = 4 << 10;
+    char *hp, *dp;
+    CK(hipHostMalloc((void**)&hp, in_b + out_b, 0));
+    CK(hipMalloc((void**)&dp, in_b + out_b));
+    memset(hp, 0, in_b + out_b);
+    const int iters = 2000;
+    auto run = [&](const char* name, auto&& body) -> int {
+        for (int i = 0; i < 200; i++) {
+            if (body()) return 1;
+            if (hipStreamSynchronize(st) != hipSuccess) return 1;
+        }
+        auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < iters; i++) {
+            if (body()) return 1;
+            if (hipStreamSynchronize(st) != hipSuccess) return 1;
+        }
+        const double us =
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
+        printf("{\"case\": \"%s\", \"us_per_call\": %.2f}\n", name, us);
+        return 0;
+    };
+    int* di = (int*)dp;
+    int rc = 0;
+    rc |= run("sync_only", [&] { return 0; });
+    rc |= run("1_kernel", [&] { hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st, di); return (int)hipGetLastError(); });
+    rc |= run("2_kernels", [&] {
+        hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st, di);
+        hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st, di);
+        return (int)hipGetLastError();
+    });
+    rc |= run("h2d_100k", [&] { return (int)hipMemcpyAsync(dp, hp, in_b, hipMemcpyHostToDevice, st); });
+    rc |= run("d2h_4k", [&] { return (int)hipMemcpyAsync(hp + in_b, dp + in_b, out_b, hipMemcpyDeviceToHost, st); });
+    rc |= run("memset_4k", [&] { return (int)hipMemsetAsync(dp + in_b, 0xFF, out_b, st); });
+    rc |= run("h2d+kernel+d2h", [&] {
+        if (hipMemcpyAsync(dp, hp, in_b, hipMemcpyHostToDevice, st)) return 1;
+        hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st, di);
+        return (int)hipMemcpyAsync(hp + in_b, dp + in_b, out_b, hipMemcpyDeviceToHost, st);
+    });
+    rc |= run("h2d+memset+2kernels+d2h", [&] {
+        if (hipMemcpyAsync(dp, hp, in_b, hipMemcpyHostToDevice, st)) return 1;
+        if (hipMemsetAsync(dp + in_b, 0xFF, out_b, st)) return 1;
+        hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st, di);
+        hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st, di);
+        return (int)hipMemcpyAsync(hp + in_b, dp + in_b, out_b, hipMemcpyDeviceToHost, st);
+    });
+    rc |= run("h2d+kernel_writes_host", [&] {
+        if (hipMemcpyAsync(dp, hp, in_b, hipMemcpyHostToDevice, st)) return 1;
+        hipLaunchKernelGGL(k_write_host, dim3(1), dim3(256), 0, st, (int*)(hp + in_b), di, (int)(out_b / 4));
+        return (int)hipGetLastError();
+    });
+    rc |= run("h2d+kernel+d2h_small_h2d_4k", [&] {
+        if (hipMemcpyAsync(dp, hp, 4096, hipMemcpyHostToDevice, st)) return 1;
+        hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st, di);
+        return (int)hipMemcpyAsync(hp + in_b, dp + in_b, out_b, hipMemcpyDeviceToHost, st);
+    });
+    rc |= run("kernel_reads_host_writes_host", [&] {
+        hipLaunchKernelGGL(k_write_host, dim3(1), dim3(256), 0, st, (int*)(hp + in_b), (const int*)hp, (int)(out_b / 4));
+        return (int)hipGetLastError();
+    });
+    (void)hipFree(dp);
+    (void)hipHostFree(hp);
+    (void)hipStreamDestroy(st);
+    return rc;
+}
