@@ -413,6 +413,20 @@ static const int kProfMaxCalls = 4096;
 
 /* stage k = {pyramid, fast_cells, octree, blur, describe}; e = 0 start / 1 end, recorded on the
  * stream the stage's kernel is launched on (the overlapped schedule is kept) */
+/* Marginal-cost experiment only (results of a changing input invalid): with -DORBX_SKIP_WARM=<mask>
+ * the stages in the mask (1 pyramid, 2 FAST, 4 octree, 8 blur, 16 describe, 32 batch matcher) are
+ * launched only during the first 64 calls. bench.py repeats the same frames every step, so the
+ * skipped stages' buffers still hold this step's results and the step times what the others cost. */
+#ifndef ORBX_SKIP_WARM
+#define ORBX_SKIP_WARM 0
+#endif
+static bool skip_warm(int bit) {
+    if (!(ORBX_SKIP_WARM & bit)) return false;
+    static int calls[8] = {0};
+    int& c = calls[__builtin_ctz((unsigned)bit)];
+    return c++ >= 64;
+}
+
 static int prof_mark(orbx_handle* h, int k, int e, hipStream_t st) {
     if (!h->prof_on || !((h->prof_mask >> k) & 1)) return 0;
     if (h->prof_calls >= kProfMaxCalls) return 0;
@@ -521,19 +535,13 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         if (launch_fast(h, d_frames, fstride, pitch, 0, ncell0, nframes, sd)) return ORBX_EDEVICE;
     }
     if (prof_mark(h, 0, 0, st)) return ORBX_EDEVICE;
-    if (launch_pyramid(h, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
+    if (!skip_warm(1) && launch_pyramid(h, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 0, 1, st)) return ORBX_EDEVICE;
     auto blur = [&](hipStream_t bs) -> int {
         if (prof_mark(h, 3, 0, bs)) return ORBX_EDEVICE;
-#ifndef ORBX_BLUR_FRAMES  // upper-bound experiment only (results invalid): blur only this many frames
-        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                                nullptr, g.nbjobs, nullptr, nframes, bs));
-#else  // after 40 full calls (the blur buffers then hold the bench's repeated frames' blur)
-        static int calls = 0;
-        const int bf = calls++ < 40 ? nframes : std::min(nframes, ORBX_BLUR_FRAMES);
-        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                                nullptr, g.nbjobs, nullptr, bf, bs));
-#endif
+        if (!skip_warm(8))
+            HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                                    nullptr, g.nbjobs, nullptr, nframes, bs));
         return prof_mark(h, 3, 1, bs);
     };
     if (!serial) {
@@ -543,9 +551,9 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         HIPR(hipEventRecord(h->ev_blur, sd));
     }
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
-    if (launch_fast(h, d_frames, fstride, pitch, ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
+    if (!skip_warm(2) && launch_fast(h, d_frames, fstride, pitch, ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 1, 1, st) || prof_mark(h, 2, 0, st)) return ORBX_EDEVICE;
-    HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
+    if (!skip_warm(4)) HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                        h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
                        (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, h->err.as<int>(), nframes, st));
     if (prof_mark(h, 2, 1, st)) return ORBX_EDEVICE;
@@ -555,7 +563,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     }
     if (prof_mark(h, 4, 0, st)) return ORBX_EDEVICE;
-    HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+    if (!skip_warm(16)) HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                          h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
                          g.d_ptab.as<int>(), nframes, st));
     if (prof_mark(h, 4, 1, st)) return ORBX_EDEVICE;
@@ -1306,6 +1314,7 @@ int orbm_triangulation_bf_batch_device(orbm_ctx* ctx, int npairs, const int32_t*
     MatchGeom g;
     make_geom(g, F12, ex, ey, nlevels, scale_factors, level_sigma2);
     hipStream_t st = (hipStream_t)stream;
+    if (skip_warm(32)) return 0;
     HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * npairs, st));
     HIPR(launch_tri_bf(npairs, d_q1, d_q2, d_kps, d_desc, d_counts, kp_stride, g, d_match12, d_nmatches, st));
     if (check_ori)

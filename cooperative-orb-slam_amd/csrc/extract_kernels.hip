@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
     }
 }
 
-/* Whole-pyramid form: one 1024-thread workgroup per frame builds levels 1..L-1 in order
+/* Whole-pyramid form: one 512-thread workgroup per frame builds levels 1..L-1 in order
  * (level l+1 is read back from L2 right after this CU wrote level l; a workgroup barrier
  * separates the levels). A batch of >= 256 frames fills every CU with equal work, and the
  * seven dependent per-level launches (each too small to hide its own latency) become one.

@@ -37,10 +37,13 @@ constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity 
 #endif
 constexpr int kPyrU = ORBX_PYR_U;   // k_pyramid_frames: rows in flight per thread
 #ifndef ORBX_PYR_NT
-#define ORBX_PYR_NT 1024
+#define ORBX_PYR_NT 512
 #endif
 constexpr int kPyrThreads = ORBX_PYR_NT;  // k_pyramid_frames: threads per frame's workgroup (>= column groups)
-constexpr int kPyrFramesMinBatch = 64;  // batches below this use the per-level pyramid kernels
+#ifndef ORBX_PYR_MIN_BATCH
+#define ORBX_PYR_MIN_BATCH 64
+#endif
+constexpr int kPyrFramesMinBatch = ORBX_PYR_MIN_BATCH;  // batches below this use the per-level pyramid kernels
 
 struct LevelDesc {
     int w, h, pitch;
