@@ -186,6 +186,9 @@ __device__ __forceinline__ uint32_t spread_pm1(uint32_t nib) {  // 4 bits -> 4 b
 }
 
 constexpr int kMfChunk = 64;  // candidates staged per step (two 32-row tiles)
+#ifndef ORBX_MATCH_STOP
+#define ORBX_MATCH_STOP 0  // phase-cost experiment only (tools/exp_phases.sh): >0 cuts k_tri_mfma short (results invalid)
+#endif
 
 __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
                                               int32_t* __restrict__ nmatch) {
@@ -255,12 +258,22 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
         }
         __syncthreads();
         if (cb + kMfChunk < s.n2) load_chunk(cb + kMfChunk, pd, pk);
+#if ORBX_MATCH_STOP == 1
+        best ^= (uint32_t)s_frag[lane & 1][lane & 7][lane].x;  // staging + expansion only
+        __syncthreads();
+        continue;
+#endif
         v16i acc0 = (v16i)0, acc1 = (v16i)0;
 #pragma unroll
         for (int st = 0; st < 8; st++) {
             acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(s_frag[0][st][lane], bq[st], acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(s_frag[1][st][lane], bq[st], acc1, 0, 0, 0);
         }
+#if ORBX_MATCH_STOP == 2
+        best ^= (uint32_t)(acc0[lane & 15] + acc1[(lane + 3) & 15]);  // + MFMA, no selection
+        __syncthreads();
+        continue;
+#endif
 #pragma unroll
         for (int tile = 0; tile < 2; tile++) {
             const v16i acc = tile ? acc1 : acc0;
