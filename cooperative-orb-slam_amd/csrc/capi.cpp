@@ -116,7 +116,7 @@ struct Geometry {
      * (r0, r1, beta). Returns false if some group's taps do not fit an 8-byte window. */
     bool build_pyr_tables(LevelDesc& d, const int* xofs, const short* alpha, const int* yofs, const short* beta,
                           int xmax, int sw, int sh, int dw, int dh) {
-        bool ok = dh <= kPyrMaxRows && (dw + 3) / 4 <= kPyrThreads && sw >= 12;
+        bool ok = dh <= kPyrMaxRows && (dw + 3) / 4 <= kPyrThreadsMax && sw >= 12;
         const int AU = (int)align_up(sw, 4);
         const int gw = (dw + 3) / 4;
         d.cg_off = (int)ptab.size();
@@ -472,10 +472,13 @@ static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fst
     // 4-byte-aligned frames, per-level kernels otherwise
     const bool aligned = ((uintptr_t)d_frames & 3) == 0 && (fstride & 3) == 0 && (pitch & 3) == 0;
     if (g.frames_ok && aligned && nframes >= kPyrFramesMinBatch && ep.L > 1) {
-        int max_rows = 1;
-        for (int l = 1; l < ep.L; l++) max_rows = std::max(max_rows, g.lv[l].h);
+        int max_rows = 1, max_groups = 1;
+        for (int l = 1; l < ep.L; l++) {
+            max_rows = std::max(max_rows, g.lv[l].h);
+            max_groups = std::max(max_groups, (g.lv[l].w + 3) / 4);
+        }
         HIPR(launch_pyramid_frames(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, g.d_lv.as<LevelDesc>(),
-                                   g.d_ptab.as<int>(), max_rows, nframes, st));
+                                   g.d_ptab.as<int>(), max_rows, max_groups, nframes, st));
         return 0;
     }
     for (int l = 1; l < ep.L; l++) {

@@ -1650,10 +1650,17 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
                                  const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int max_rows,
-                                 int nframes, hipStream_t st) {
+                                 int max_groups, int nframes, hipStream_t st) {
     if (max_rows < 1 || max_rows > kPyrMaxRows) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), dim3(nframes), dim3(kPyrThreads),
-                       (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab);
+    // 512-thread workgroups pack beside the other graphs' kernels while every level
+    // keeps >= 2 rows per pass; a level 1 wider than 4 x 256 columns (C4's 1034) would leave half the
+    // threads idle, so such geometries take 1024 threads
+    if (max_groups <= kPyrThreads / 2)
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), dim3(nframes), dim3(kPyrThreads),
+                           (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab);
+    else
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), dim3(nframes), dim3(kPyrThreadsMax),
+                           (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab);
     return hipGetLastError();
 }
 

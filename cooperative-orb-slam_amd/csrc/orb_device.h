@@ -39,7 +39,11 @@ constexpr int kPyrU = ORBX_PYR_U;   // k_pyramid_frames: rows in flight per thre
 #ifndef ORBX_PYR_NT
 #define ORBX_PYR_NT 512
 #endif
-constexpr int kPyrThreads = ORBX_PYR_NT;  // k_pyramid_frames: threads per frame's workgroup (>= column groups)
+// k_pyramid_frames: threads per frame's workgroup. kPyrThreads is used when every level's 4-column
+// group count fits half of it (>= 2 rows per pass); wider levels take kPyrThreadsMax, the limit the
+// whole-frame kernel accepts (>= column groups of every level)
+constexpr int kPyrThreads = ORBX_PYR_NT;
+constexpr int kPyrThreadsMax = 1024;
 #ifndef ORBX_PYR_MIN_BATCH
 #define ORBX_PYR_MIN_BATCH 64
 #endif

@@ -31,7 +31,15 @@ class AgentSchedule:
         dev = torch.device("cuda", device)
         self.dev = dev
         sub = self.sub
-        self.frames = [torch.from_numpy(frames_np[p * sub:(p + 1) * sub]).to(dev) for p in range(pipes)]
+        # frames live in a pitched HBM buffer: rows padded to 64 bytes when the width is not a multiple of 4
+        # (C4's 1241), so every row starts 4-aligned and the whole-frame pyramid kernel applies
+        pitch = width if width % 4 == 0 else (width + 63) // 64 * 64
+        self.frames = []
+        for p in range(pipes):
+            buf = torch.zeros((sub, height, pitch), dtype=torch.uint8, device=dev)
+            view = buf[:, :, :width]
+            view.copy_(torch.from_numpy(frames_np[p * sub:(p + 1) * sub]).to(dev))
+            self.frames.append(view)
         self.nfeatures = nfeatures
         self.pipes = [BatchPipeline(torch, width, height, sub, nfeatures=nfeatures, device=device)
                       for _ in range(pipes)]
