@@ -1415,8 +1415,13 @@ __device__ constexpr PatTable kPatternF = make_pattern_table();
 constexpr int kDescPatchR = 18;                   // |round(rotated pattern coordinate)| <= 13*sqrt(2)
 constexpr int kDescPatchRows = 2 * kDescPatchR + 1;  // 37
 constexpr int kDescPatchPitch = 40;                 // 10 dwords: 37 columns + up to 3 bytes misalignment
+#ifndef ORBX_DESC_WAVES
+#define ORBX_DESC_WAVES 4
+#endif
+constexpr int kDescWaves = ORBX_DESC_WAVES;         // waves (x 4 keypoints) per k_describe workgroup
+constexpr int kDescKps = 4 * kDescWaves;            // keypoints per workgroup
 
-__global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
+__global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                   const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   ExtractParams ep, const LevelDesc* __restrict__ levels,
                                                   const uint32_t* __restrict__ lvkey, const int* __restrict__ lvcnt,
@@ -1425,14 +1430,14 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
                                                   const int* __restrict__ ptab) {
     __shared__ PatPt s_pat[256];
     __shared__ int2 s_ic[256];
-    __shared__ __align__(8) uint8_t s_patch[16][kDescPatchRows * kDescPatchPitch];
+    __shared__ __align__(8) uint8_t s_patch[kDescKps][kDescPatchRows * kDescPatchPitch];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int sub = lane >> 4, ln = lane & 15;
     // XCD-aware block mapping (1-D grid of G groups x F frames): workgroups are dispatched to the 8
     // XCDs round-robin, so with F % 8 == 0 block b runs on XCD b % 8 and serves frame
     // (b % 8) + 8 * ((b / 8) / G): every workgroup of a frame shares one XCD's L2, where the
     // overlapping 37x37 patches and IC rows of neighbouring keypoints hit
-    const int G = (ep.kp_per_frame + 15) / 16;
+    const int G = (ep.kp_per_frame + kDescKps - 1) / kDescKps;
     int f, blk;
     {
         const int b = blockIdx.x;
@@ -1446,9 +1451,15 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
         }
     }
     // everything that depends only on the slot is issued before the table barrier
-    const PatPt my_pat = kPatternF.t[tid];
-    const int2 my_ic = ((const int2*)(ptab + ep.ic_off))[tid];
-    const int g = (blk * 4 + wave) * 4 + sub;  // octree output slot of this lane group
+    constexpr int NT = 64 * kDescWaves;
+    PatPt my_pat[256 / NT];
+    int2 my_ic[256 / NT];
+#pragma unroll
+    for (int q = 0; q < 256 / NT; q++) {
+        my_pat[q] = kPatternF.t[tid + q * NT];
+        my_ic[q] = ((const int2*)(ptab + ep.ic_off))[tid + q * NT];
+    }
+    const int g = (blk * kDescWaves + wave) * 4 + sub;  // octree output slot of this lane group
     const int gc = min(g, ep.kp_per_frame - 1);
     const uint32_t kk_raw = lvkey[(long long)f * ep.kp_per_frame + gc];
     // per-level counts of this frame (lvcnt is padded by kMaxLevels ints; entries >= L masked)
@@ -1456,8 +1467,12 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ fr
     int cl[kMaxLevels];
 #pragma unroll
     for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;
-    s_pat[(tid & 15) * 16 + (tid >> 4)] = my_pat;  // pair p at (p % 16) * 16 + p / 16
-    s_ic[tid] = my_ic;
+#pragma unroll
+    for (int q = 0; q < 256 / NT; q++) {
+        const int t = tid + q * NT;
+        s_pat[(t & 15) * 16 + (t >> 4)] = my_pat[q];  // pair p at (p % 16) * 16 + p / 16
+        s_ic[t] = my_ic[q];
+    }
     if (blk == 0 && tid == 0) {
         int tot = 0;
 #pragma unroll
@@ -1754,8 +1769,8 @@ hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0,
                            const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
                            const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,
                            int* out_counts, int kp_stride, const int* ptab, int nframes, hipStream_t st) {
-    dim3 grid(((ep.kp_per_frame + 15) / 16) * nframes);
-    hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, lvkey,
+    dim3 grid(((ep.kp_per_frame + kDescKps - 1) / kDescKps) * nframes);
+    hipLaunchKernelGGL(k_describe, grid, dim3(64 * kDescWaves), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, lvkey,
                        lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
     return hipGetLastError();
 }
