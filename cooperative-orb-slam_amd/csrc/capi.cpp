@@ -516,7 +516,8 @@ static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstrid
  * barrier/latency-bound); describe joins both. (The reference blurs only levels that kept
  * keypoints (ORBextractor.cc:1081); blurring every level changes no output, since describe
  * reads only levels with keypoints.) ORBX_SCHED=split also starts FAST on level 0 (which needs
- * only the input) beside the pyramid; ORBX_SCHED=serial runs everything on `st` (A/B only).
+ * only the input) beside the pyramid; ORBX_SCHED=serial runs everything on `st` (A/B only), and
+ * ORBX_SCHED=serial_blur_first does so with the blur right after the pyramid.
  * With stage profiling on, everything runs in order on `st` between timing events. */
 static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
                        orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st) {
@@ -525,9 +526,10 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
     static const int sched = [] {
         const char* e = getenv("ORBX_SCHED");
-        return !e ? 0 : (!strcmp(e, "split") ? 1 : (!strcmp(e, "serial") ? 2 : 0));
+        return !e ? 0 : (!strcmp(e, "split") ? 1 : (!strcmp(e, "serial") ? 2 : (!strcmp(e, "serial_blur_first") ? 3 : 0)));
     }();
-    const bool serial = sched == 2;
+    const bool serial = sched == 2 || sched == 3;
+    const bool blur_first = sched == 3;
     const bool split = !serial && sched == 1;
     const int ncell0 = split ? g.lv[0].ncells : 0;
     hipStream_t sd = serial ? st : h->side;
@@ -552,6 +554,8 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         HIPR(hipStreamWaitEvent(sd, h->ev_pyr, 0));
         if (blur(sd)) return ORBX_EDEVICE;
         HIPR(hipEventRecord(h->ev_blur, sd));
+    } else if (blur_first) {
+        if (blur(st)) return ORBX_EDEVICE;
     }
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
     if (!skip_warm(2) && launch_fast(h, d_frames, fstride, pitch, ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
@@ -561,7 +565,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
                        (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, h->err.as<int>(), nframes, st));
     if (prof_mark(h, 2, 1, st)) return ORBX_EDEVICE;
     if (serial) {
-        if (blur(st)) return ORBX_EDEVICE;
+        if (!blur_first && blur(st)) return ORBX_EDEVICE;
     } else {
         HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     }
