@@ -24,6 +24,7 @@ Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
+import math
 import os
 import sys
 import threading
@@ -168,6 +169,8 @@ def main():
                     help="HIP stream priorities of the graphs: lead = the first half of the staggered graphs (the ones "
                          "in their latency-bound tail stages) high, lead1 = graph 0 only")
     ap.add_argument("--no-exchange", action="store_true")
+    ap.add_argument("--sustain", type=float, default=6.0,
+                    help="seconds of the untimed sustained pass after the timed region (0: skip)")
     ap.add_argument("--stagger", choices=("each", "once", "none"), default="each",
                     help="graph p starts extracting after graph p-1's extraction: every step / only in the "
                          "first step of a run (the phase offset then persists) / never")
@@ -314,6 +317,21 @@ def main():
         del a, b2
     extract_fps = B * args.steps / run_part(args.steps, match=False, xchg=False)
     match_pps = B * args.steps / run_part(args.steps, extract=False, xchg=False)
+    # 5) sustained pass (untimed for `value`): the full schedule for ~--sustain seconds, which reports the
+    # steady-state rate over thousands of steps and keeps the GPU busy long enough for a utilisation sampler
+    # to see it. The step count comes from the max-over-ranks timing, so every rank runs the same number of
+    # exchange all-gathers.
+    sustained = None
+    if args.sustain > 0:
+        n_sus = max(1, int(math.ceil(args.sustain / (el / args.steps))))
+        if world > 1:
+            dist.barrier()
+        sus_s = run_part(n_sus)
+        if world > 1:
+            t = torch.tensor([sus_s], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            sus_s = float(t.item())
+        sustained = {"seconds": round(sus_s, 3), "steps": n_sus, "frames_per_s": round(world * B * n_sus / sus_s, 1)}
     nkp = float(sum(pp.counts.float().mean().item() for pp in pipes) / P)
     nmatch = float(sum(pp.nmatch.float().mean().item() for pp in pipes) / P)
 
@@ -387,6 +405,7 @@ def main():
             "match_only_pairs_per_s_per_gpu": round(match_pps, 1),
             "kp_per_frame": round(nkp, 1),
             "matches_per_pair": round(nmatch, 1),
+            "sustained": sustained,
         }
         if check is not None and check["mismatches"]:
             result["mismatches"] = check["mismatches"]
