@@ -13,11 +13,11 @@ done
 summ='import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); s=d["stage_ms_per_step"]; print("%.0f" % d["value"], " ".join("%s=%.3f" % (k, s[k]) for k in ("pyramid","fast_cells","octree","blur","describe","match")))'
 for r in 1 2 3; do
   for v in "$@"; do
-    out=$(ORBAMD_LIB_VARIANT=$v timeout -k 10 120 python bench.py --no-cpu --steps 30 | python -c "$summ") || exit $?
+    out=$(ORBAMD_LIB_VARIANT=$v timeout -k 10 120 python bench.py --sustain 0 --no-cpu --steps 30 | python -c "$summ") || exit $?
     echo "r$r $v overlapped: $out"
   done
 done
 for v in "$@"; do
-  out=$(ORBAMD_LIB_VARIANT=$v ORBX_SCHED=serial timeout -k 10 120 python bench.py --no-cpu --steps 30 --pipes 1 --batch 256 | python -c "$summ") || exit $?
+  out=$(ORBAMD_LIB_VARIANT=$v ORBX_SCHED=serial timeout -k 10 120 python bench.py --sustain 0 --no-cpu --steps 30 --pipes 1 --batch 256 | python -c "$summ") || exit $?
   echo "$v serial-1graph: $out"
 done

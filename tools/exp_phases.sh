@@ -4,7 +4,7 @@
 # bench runs with --no-check. usage: tools/exp_phases.sh <stage key> v1 v2 ... (e.g. octree os1 os2 os3 head)
 st=$1; shift
 for v in "$@"; do
-  out=$(ORBAMD_LIB_VARIANT=$v ORBX_SCHED=serial timeout -k 10 120 python bench.py --no-cpu --no-check --steps 30 --pipes 1 --batch 256 | \
+  out=$(ORBAMD_LIB_VARIANT=$v ORBX_SCHED=serial timeout -k 10 120 python bench.py --sustain 0 --no-cpu --no-check --steps 30 --pipes 1 --batch 256 | \
     python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$st=%.4f' % d['stage_ms_per_step']['$st'])") || exit $?
   echo "$v $out"
 done

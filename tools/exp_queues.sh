@@ -4,7 +4,7 @@
 # HIP init). Prints one line per configuration.
 for q in 4 8 16; do
   for p in 4 6 8; do
-    v=$(GPU_MAX_HW_QUEUES=$q timeout -k 10 120 python bench.py --no-cpu --pipes $p --batch $((256 * p)) --steps 20 \
+    v=$(GPU_MAX_HW_QUEUES=$q timeout -k 10 120 python bench.py --sustain 0 --no-cpu --pipes $p --batch $((256 * p)) --steps 20 \
         | python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])")
     echo "queues=$q pipes=$p frames/s,ms = $v"
   done
