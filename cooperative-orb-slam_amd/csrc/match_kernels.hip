@@ -190,13 +190,31 @@ constexpr int kMfChunk = 64;  // candidates staged per step (two 32-row tiles)
 #define ORBX_MATCH_STOP 0  // phase-cost experiment only (tools/exp_phases.sh): >0 cuts k_tri_mfma short (results invalid)
 #endif
 
+#ifndef ORBX_MATCH_WAVES
+#define ORBX_MATCH_WAVES 4  // query waves per workgroup (32 queries each); they share each chunk's expansion
+#endif
+constexpr int kMfWaves = ORBX_MATCH_WAVES;
+constexpr int kMfThreads = 64 * kMfWaves;
+static_assert(kMfWaves == 4 || kMfWaves == 8 || kMfWaves == 16, "ORBX_MATCH_WAVES: 4, 8 or 16");
+// expansion units: 16 descriptor bits of one candidate (one half h of one 32-bit step); a chunk has
+// 64 x 16 of them, each thread expands kMfUnits consecutive units of one candidate
+constexpr int kMfUnits = 64 * 16 / kMfThreads;
+
+template <int U> struct ChunkBits;
+template <> struct ChunkBits<4> { uint2 v; };
+template <> struct ChunkBits<2> { uint32_t v; };
+template <> struct ChunkBits<1> { uint16_t v; };
+__device__ __forceinline__ uint32_t unit_bits(const ChunkBits<4>& b, int u) { return ((u >> 1) ? b.v.y : b.v.x) >> (16 * (u & 1)); }
+__device__ __forceinline__ uint32_t unit_bits(const ChunkBits<2>& b, int u) { return b.v >> (16 * u); }
+__device__ __forceinline__ uint32_t unit_bits(const ChunkBits<1>& b, int) { return b.v; }
+
 __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
                                               int32_t* __restrict__ nmatch) {
     __shared__ v4i s_frag[2][8][64];  // [tile][step][lane] candidate fragments (0/1 bytes)
     __shared__ float s_x[kMfChunk], s_y[kMfChunk];
     __shared__ int s_oct[kMfChunk], s_ok[kMfChunk];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int qblk = blockIdx.x * 128;
+    const int qblk = blockIdx.x * (32 * kMfWaves);
     if (qblk >= s.n1) return;  // block-uniform
     const int h = lane >> 5;
     const int qi = qblk + wave * 32 + (lane & 31);
@@ -221,16 +239,17 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
         epi_line(g, k1.x, k1.y, &la, &lb, &lc);
     }
     uint32_t best = 0xFFFFFFFFu;
-    // expansion role of this thread: candidate c = tid >> 2 of the chunk, descriptor bytes 8q..8q+7;
-    // the next chunk's bytes (and, for tid < 64, keypoint) are prefetched into registers while
-    // the current chunk is multiplied
-    const int ec = tid >> 2, eq = tid & 3;
-    auto load_chunk = [&](int cb, uint2& d, orbx_kp& k2) {
+    // expansion role of this thread: candidate c = ec of the chunk, units eu..eu+kMfUnits-1 (unit
+    // u = descriptor bits 16u..16u+15); the next chunk's bits (and, for tid < 64, keypoint) are
+    // prefetched into registers while the current chunk is multiplied
+    constexpr int kTPC = 16 / kMfUnits;  // threads per candidate
+    const int ec = tid / kTPC, eu = (tid % kTPC) * kMfUnits;
+    auto load_chunk = [&](int cb, ChunkBits<kMfUnits>& d, orbx_kp& k2) {
         const int c = min(cb + ec, s.n2 - 1);
-        d = *(const uint2*)(s.desc2 + (long long)c * 32 + 8 * eq);
+        d = *(const ChunkBits<kMfUnits>*)(s.desc2 + (long long)c * 32 + 2 * eu);
         k2 = s.kps2[min(cb + (tid & (kMfChunk - 1)), s.n2 - 1)];
     };
-    uint2 pd;
+    ChunkBits<kMfUnits> pd;
     orbx_kp pk;
     load_chunk(0, pd, pk);
     for (int cb = 0; cb < s.n2; cb += kMfChunk) {
@@ -238,15 +257,12 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
             const bool on = cb + ec < s.n2;
             const int tile = ec >> 5, r = ec & 31;
 #pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const uint32_t w = on ? (k ? pd.y : pd.x) : 0u;
-#pragma unroll
-                for (int hh = 0; hh < 2; hh++) {
-                    const uint32_t b16 = w >> (16 * hh);
-                    s_frag[tile][2 * eq + k][32 * hh + r] =
-                        (v4i){(int)spread01(b16 & 15), (int)spread01((b16 >> 4) & 15), (int)spread01((b16 >> 8) & 15),
-                              (int)spread01((b16 >> 12) & 15)};
-                }
+            for (int k = 0; k < kMfUnits; k++) {
+                const int u = eu + k, st = u >> 1, hh = u & 1;
+                const uint32_t b16 = on ? unit_bits(pd, k) : 0u;
+                s_frag[tile][st][32 * hh + r] =
+                    (v4i){(int)spread01(b16 & 15), (int)spread01((b16 >> 4) & 15), (int)spread01((b16 >> 8) & 15),
+                          (int)spread01((b16 >> 12) & 15)};
             }
             if (tid < kMfChunk) {
                 const bool on2 = cb + tid < s.n2;
@@ -316,7 +332,7 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
     }
 }
 
-__global__ __launch_bounds__(256) void k_tri_mfma(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
+__global__ __launch_bounds__(kMfThreads) void k_tri_mfma(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
                                                   const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
                                                   const int32_t* __restrict__ counts, int kp_stride, MatchGeom g,
                                                   int32_t* __restrict__ match12, int32_t* __restrict__ nmatches) {
@@ -849,8 +865,8 @@ hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
                          int32_t* nmatches, hipStream_t st) {
     if (!getenv("ORBX_TRI_SIMT")) {
-        dim3 grid((kp_stride + 127) / 128, npairs);
-        hipLaunchKernelGGL(k_tri_mfma, grid, dim3(256), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
+        dim3 grid((kp_stride + 32 * kMfWaves - 1) / (32 * kMfWaves), npairs);
+        hipLaunchKernelGGL(k_tri_mfma, grid, dim3(kMfThreads), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
                            nmatches);
         return hipGetLastError();
     }
