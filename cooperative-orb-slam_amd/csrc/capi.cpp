@@ -160,6 +160,8 @@ struct Geometry {
     int tiled_ok[kMaxLevels] = {0};   // level's resize fits the LDS-tiled kernel
     std::vector<int> ptab;            // k_pyramid_frames column-group / row tables
     bool frames_ok = true;            // every level fits k_pyramid_frames
+    int pyr_band_off = 0;             // k_pyramid_frames band ranges: int2 [band][kMaxLevels] in ptab
+    int pyr_band_rows = 1;            // longest band range of any level >= 1 (LDS row table rows)
     DevBuf d_lv, d_cells, d_coef, d_ptab;
 
     int build(const Tables& T, int W_, int H_) {
@@ -343,6 +345,32 @@ struct Geometry {
             ep.kp_off[l] = l < L ? lv[l].kp_off : kp_off;
             ep.bjob_begin[l] = l <= L ? bjob_begin[l] : nbjobs;
         }
+        // k_pyramid_frames bands (top level down): a band's rows of level l are its own share
+        // [b*h/K, (b+1)*h/K) plus every row its range of level l+1 reads (row table r0 / r1)
+        pyr_band_off = (int)ptab.size();
+        pyr_band_rows = 1;
+        ptab.resize(ptab.size() + 2 * (size_t)kPyrBands * kMaxLevels, 0);
+        if (frames_ok) {
+            for (int b = 0; b < kPyrBands; b++) {
+                int* bt = ptab.data() + pyr_band_off + 2 * b * kMaxLevels;
+                for (int l = L - 1; l >= 1; l--) {
+                    const int h = lv[l].h;
+                    int lo = (int)((long long)b * h / kPyrBands), hi = (int)((long long)(b + 1) * h / kPyrBands);
+                    if (l + 1 < L && bt[2 * (l + 1)] < bt[2 * (l + 1) + 1]) {
+                        const int* rt = ptab.data() + lv[l + 1].rt_off;
+                        for (int y = bt[2 * (l + 1)]; y < bt[2 * (l + 1) + 1]; y++) {
+                            lo = std::min(lo, rt[4 * y]);
+                            hi = std::max(hi, rt[4 * y + 1] + 1);
+                        }
+                    }
+                    lo = std::max(lo, 0);
+                    hi = std::min(hi, h);
+                    bt[2 * l] = lo;
+                    bt[2 * l + 1] = std::max(hi, lo);
+                    pyr_band_rows = std::max(pyr_band_rows, hi - lo);
+                }
+            }
+        }
         // octree LDS: node arrays (92 B/node, NC pow2) + keys (7 B/key)
         NC = 1;
         while (NC < maxnode) NC <<= 1;
@@ -472,13 +500,11 @@ static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fst
     // 4-byte-aligned frames, per-level kernels otherwise
     const bool aligned = ((uintptr_t)d_frames & 3) == 0 && (fstride & 3) == 0 && (pitch & 3) == 0;
     if (g.frames_ok && aligned && nframes >= kPyrFramesMinBatch && ep.L > 1) {
-        int max_rows = 1, max_groups = 1;
-        for (int l = 1; l < ep.L; l++) {
-            max_rows = std::max(max_rows, g.lv[l].h);
-            max_groups = std::max(max_groups, (g.lv[l].w + 3) / 4);
-        }
+        int max_groups = 1;
+        for (int l = 1; l < ep.L; l++) max_groups = std::max(max_groups, (g.lv[l].w + 3) / 4);
         HIPR(launch_pyramid_frames(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, g.d_lv.as<LevelDesc>(),
-                                   g.d_ptab.as<int>(), max_rows, max_groups, nframes, st));
+                                   g.d_ptab.as<int>(), (const int2*)(g.d_ptab.as<int>() + g.pyr_band_off),
+                                   g.pyr_band_rows, max_groups, nframes, st));
         return 0;
     }
     for (int l = 1; l < ep.L; l++) {

@@ -233,12 +233,12 @@ template <int U, int NT>
 __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
                                                          int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
                                                          const LevelDesc* __restrict__ levels,
-                                                         const int* __restrict__ ptab) {
-    // the current level's row table; sized at launch for the tallest level >= 1 (rows x 16 B: 6.4 KB at
-    // 640x480) instead of kPyrMaxRows, so the LDS the long-lived pyramid workgroup holds (one per CU)
-    // stays free for the other graphs' FAST / describe workgroups beside it
+                                                         const int* __restrict__ ptab, const int2* __restrict__ bands) {
+    // the current level's row table (this band's rows); sized at launch for the longest band range
+    // (rows x 16 B: 6.4 KB at 640x480 with one band) instead of kPyrMaxRows, so the LDS the long-lived
+    // pyramid workgroup holds stays free for the other graphs' FAST / describe workgroups beside it
     extern __shared__ int4 s_rt[];
-    const int f = blockIdx.x, tid = threadIdx.x;
+    const int f = blockIdx.x / kPyrBands, band = blockIdx.x - f * kPyrBands, tid = threadIdx.x;
     uint8_t* P = pyr + (long long)f * ep.pyr_frame_bytes;
     for (int l = 1; l < ep.L; l++) {
         const LevelDesc sv = levels[l - 1];
@@ -246,9 +246,13 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
         const uint8_t* src = l == 1 ? frames + (long long)f * fstride : P + sv.pyr_off;
         const int sp = l == 1 ? pitch0 : sv.pitch;
         uint8_t* dst = P + lv.pyr_off;
-        const int dh = lv.h;
+        // rows [lo, hi) of this level: the band's own rows plus the rows the band's range of level l+1
+        // reads (recomputed here, so bands never wait on each other; overlapping rows are written by
+        // two workgroups with identical bytes)
+        const int2 rg = bands[band * kMaxLevels + l];
+        const int lo = rg.x, hi = rg.y;
         const int4* rt = (const int4*)(ptab + lv.rt_off);
-        for (int i = tid; i < dh; i += NT) s_rt[i] = rt[i];
+        for (int i = tid; i < hi - lo; i += NT) s_rt[i] = rt[lo + i];
         const int gw = (lv.w + 3) >> 2;
         const int R = NT / gw;  // rows per pass
         const int ry = tid / gw, xg = tid - ry * gw;
@@ -258,37 +262,37 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
         const bool tail = x0 + 3 >= lv.simd_end;
         __syncthreads();
         if (ry < R) {
-            for (int y0 = ry; y0 < dh; y0 += U * R) {
+            for (int y0 = lo + ry; y0 < hi; y0 += U * R) {
                 uint32_t w[U][2][3];
                 int4 rr[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    rr[u] = s_rt[min(y0 + u * R, dh - 1)];
+                    rr[u] = s_rt[min(y0 + u * R, hi - 1) - lo];
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
 #pragma unroll
                     for (int q = 0; q < 2; q++) {
                         const unsigned off = (unsigned)((q ? rr[u].y : rr[u].x) * sp + A);
-                        const uint2 lo = *(const uint2*)(src + off);
-                        w[u][q][0] = lo.x;
-                        w[u][q][1] = lo.y;
+                        const uint2 lo2 = *(const uint2*)(src + off);
+                        w[u][q][0] = lo2.x;
+                        w[u][q][1] = lo2.y;
                         w[u][q][2] = *(const uint32_t*)(src + min(off + 8u, (unsigned)((q ? rr[u].y : rr[u].x) * sp + cg.pad[0])));
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const int y = y0 + u * R;
-                    if (y >= dh) break;
+                    if (y >= hi) break;
                     const short2 b = __builtin_bit_cast(short2, rr[u].z);
                     int h[2][4];
 #pragma unroll
                     for (int q = 0; q < 2; q++) {
-                        const uint32_t lo = __builtin_amdgcn_alignbyte(w[u][q][1], w[u][q][0], k);
-                        const uint32_t hi = __builtin_amdgcn_alignbyte(w[u][q][2], w[u][q][1], k);
+                        const uint32_t lw = __builtin_amdgcn_alignbyte(w[u][q][1], w[u][q][0], k);
+                        const uint32_t hw = __builtin_amdgcn_alignbyte(w[u][q][2], w[u][q][1], k);
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
-                            const uint32_t pr = __builtin_amdgcn_perm(hi, lo, cg.sel[i]);
+                            const uint32_t pr = __builtin_amdgcn_perm(hw, lw, cg.sel[i]);
                             h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
                                                              __builtin_bit_cast(short2v, cg.alpha[i]), 0, false);
                         }
@@ -1664,18 +1668,19 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 }
 
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
-                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int max_rows,
-                                 int max_groups, int nframes, hipStream_t st) {
+                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, const int2* bands,
+                                 int max_rows, int max_groups, int nframes, hipStream_t st) {
     if (max_rows < 1 || max_rows > kPyrMaxRows) return hipErrorInvalidValue;
     // 512-thread workgroups pack beside the other graphs' kernels while every level
     // keeps >= 2 rows per pass; a level 1 wider than 4 x 256 columns (C4's 1034) would leave half the
     // threads idle, so such geometries take 1024 threads
+    const dim3 grid(nframes * kPyrBands);
     if (max_groups <= kPyrThreads / 2)
-        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), dim3(nframes), dim3(kPyrThreads),
-                           (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab);
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), grid, dim3(kPyrThreads),
+                           (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab, bands);
     else
-        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), dim3(nframes), dim3(kPyrThreadsMax),
-                           (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab);
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), grid, dim3(kPyrThreadsMax),
+                           (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab, bands);
     return hipGetLastError();
 }
 

@@ -44,6 +44,12 @@ constexpr int kPyrU = ORBX_PYR_U;   // k_pyramid_frames: rows in flight per thre
 // whole-frame kernel accepts (>= column groups of every level)
 constexpr int kPyrThreads = ORBX_PYR_NT;
 constexpr int kPyrThreadsMax = 1024;
+#ifndef ORBX_PYR_BANDS
+#define ORBX_PYR_BANDS 1
+#endif
+// k_pyramid_frames: workgroups per frame; each builds every level for one horizontal band of rows,
+// recomputing the few rows its next level reads across the band edge
+constexpr int kPyrBands = ORBX_PYR_BANDS;
 #ifndef ORBX_PYR_MIN_BATCH
 #define ORBX_PYR_MIN_BATCH 64
 #endif
