@@ -17,6 +17,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <limits.h>
 
 #include "../../include/orbslam_amd.h"
 #include "orb_match.h"
@@ -194,6 +195,9 @@ constexpr int kMfChunk = 64;  // candidates staged per step (two 32-row tiles)
 #define ORBX_MATCH_WAVES 4  // query waves per workgroup (32 queries each); they share each chunk's expansion
 #endif
 constexpr int kMfWaves = ORBX_MATCH_WAVES;
+#ifndef ORBX_MATCH_PACKED_MAX
+#define ORBX_MATCH_PACKED_MAX 1  // selection by one packed (dot, row) maximum per tile (0: threshold pass + key pass)
+#endif
 constexpr int kMfThreads = 64 * kMfWaves;
 static_assert(kMfWaves == 4 || kMfWaves == 8 || kMfWaves == 16, "ORBX_MATCH_WAVES: 4, 8 or 16");
 // expansion units: 16 descriptor bits of one candidate (one half h of one 32-bit step); a chunk has
@@ -293,14 +297,36 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
 #pragma unroll
         for (int tile = 0; tile < 2; tile++) {
             const v16i acc = tile ? acc1 : acc0;
+            // key = D << 16 | (65535 - idx2) = kbase - P with P = acc << 16 | row (signed; rows are
+            // distinct per lane), so the lane's minimum key is kbase - max P: one v_lshl_add per
+            // accumulator and a v_max3 chain, no separate threshold pass
+            const uint32_t kbase = ((uint32_t)pb << 16) + 65535u - (uint32_t)(cb + 32 * tile + 4 * h);
+#if ORBX_MATCH_PACKED_MAX
+            auto pk = [&](int rg) { return (int)(((uint32_t)acc[rg] << 16) + (uint32_t)((rg & 3) + 8 * (rg >> 2))); };
+            int pmax = pk(0);
+#pragma unroll
+            for (int rg = 1; rg < 16; rg++) pmax = max(pmax, pk(rg));
+            uint32_t km = kbase - (uint32_t)pmax;
+            while (km < best && (km >> 16) <= 50u) {  // TH_LOW (ORBmatcher.cc:715)
+                const int jl = (int)(65535u - (km & 0xFFFFu)) - cb;
+                if (s_ok[jl] && epi_ok(la, lb, lc, s_x[jl], s_y[jl], g.th384[s_oct[jl]])) {
+                    best = km;
+                    break;
+                }
+                // next key of the lane = largest P below the rejected one
+                const int cur = (int)(kbase - km);
+                int nx = INT_MIN;
+#pragma unroll
+                for (int rg = 0; rg < 16; rg++) nx = pk(rg) < cur ? max(nx, pk(rg)) : nx;
+                km = nx == INT_MIN ? 0xFFFFFFFFu : kbase - (uint32_t)nx;
+            }
+#else
             // cheap filter: the lane's best dot in this tile (D = pb - dot)
             int amax = acc[0];
 #pragma unroll
             for (int rg = 1; rg < 16; rg++) amax = max(amax, acc[rg]);
             const int lim = min(50, (int)(best >> 16));  // TH_LOW (ORBmatcher.cc:715)
             if (pb - amax > lim) continue;
-            // key = D << 16 | (65535 - idx2) = kbase - (acc << 16 | row)
-            const uint32_t kbase = ((uint32_t)pb << 16) + 65535u - (uint32_t)(cb + 32 * tile + 4 * h);
             // keys are recomputed from the accumulators where needed (not kept: 16 fewer live VGPRs)
             auto key = [&](int rg) {
                 const uint32_t row = (uint32_t)((rg & 3) + 8 * (rg >> 2));
@@ -321,6 +347,7 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
                 for (int rg = 0; rg < 16; rg++) nx = key(rg) > km ? min(nx, key(rg)) : nx;
                 km = nx;
             }
+#endif
         }
         __syncthreads();
     }
