@@ -1403,6 +1403,15 @@ constexpr PatTable make_pattern_table() {
     return p;
 }
 __device__ constexpr PatTable kPatternF = make_pattern_table();
+/* the same pairs transposed (pair p at (p % 16) * 16 + p / 16): the 16 lanes of a keypoint read 256
+ * contiguous bytes per step */
+constexpr PatTable make_pattern_table_t() {
+    PatTable p{};
+    const PatTable a = make_pattern_table();
+    for (int t = 0; t < 256; t++) p.t[(t & 15) * 16 + (t >> 4)] = a.t[t];
+    return p;
+}
+__device__ constexpr PatTable kPatternT = make_pattern_table_t();
 
 /* ----------------------------------------------------------------------------------- */
 /* IC_Angle + rBRIEF + output: 16 lanes per keypoint, 4 keypoints per wave.               */
@@ -1424,15 +1433,22 @@ constexpr int kDescPatchPitch = 40;                 // 10 dwords: 37 columns + u
 #endif
 constexpr int kDescWaves = ORBX_DESC_WAVES;         // waves (x 4 keypoints) per k_describe workgroup
 constexpr int kDescKps = 4 * kDescWaves;            // keypoints per workgroup
+#ifndef ORBX_DESC_PAT_GLOBAL
+#define ORBX_DESC_PAT_GLOBAL 0  // 1: rBRIEF pairs read from global (L1/L2) instead of an LDS copy (4 KB less LDS)
+#endif
+#ifndef ORBX_DESC_MINW
+#define ORBX_DESC_MINW 1        // __launch_bounds__ min waves per SIMD (6: VGPR budget 80)
+#endif
+constexpr bool kDescPatGlobal = ORBX_DESC_PAT_GLOBAL != 0;
 
-__global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
+__global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                   const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   ExtractParams ep, const LevelDesc* __restrict__ levels,
                                                   const uint32_t* __restrict__ lvkey, const int* __restrict__ lvcnt,
                                                   orbx_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
                                                   int* __restrict__ out_counts, int kp_stride,
                                                   const int* __restrict__ ptab) {
-    __shared__ PatPt s_pat[256];
+    __shared__ PatPt s_pat[kDescPatGlobal ? 1 : 256];
     __shared__ int2 s_ic[256];
     __shared__ __align__(8) uint8_t s_patch[kDescKps][kDescPatchRows * kDescPatchPitch];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1460,7 +1476,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
     int2 my_ic[256 / NT];
 #pragma unroll
     for (int q = 0; q < 256 / NT; q++) {
-        my_pat[q] = kPatternF.t[tid + q * NT];
+        if (!kDescPatGlobal) my_pat[q] = kPatternF.t[tid + q * NT];
         my_ic[q] = ((const int2*)(ptab + ep.ic_off))[tid + q * NT];
     }
     const int g = (blk * kDescWaves + wave) * 4 + sub;  // octree output slot of this lane group
@@ -1474,7 +1490,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
 #pragma unroll
     for (int q = 0; q < 256 / NT; q++) {
         const int t = tid + q * NT;
-        s_pat[(t & 15) * 16 + (t >> 4)] = my_pat[q];  // pair p at (p % 16) * 16 + p / 16
+        if (!kDescPatGlobal) s_pat[(t & 15) * 16 + (t >> 4)] = my_pat[q];  // pair p at (p % 16) * 16 + p / 16
         s_ic[t] = my_ic[q];
     }
     if (blk == 0 && tid == 0) {
@@ -1606,7 +1622,10 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
         constexpr uint32_t K = 0x400000u * (uint32_t)kDescPatchPitch + 0x4B400000u;
 #pragma unroll
         for (int j = 0; j < 16; j++) {
-            const PatPt pp = s_pat[16 * j + ln];  // pair 16ln + j (transposed table: conflict-free reads)
+            // global table: pairs fetched 4 steps at a time (a scheduling fence per group keeps the compiler
+            // from hoisting all 16 loads, i.e. 64 live VGPRs)
+            if (kDescPatGlobal && (j & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+            const PatPt pp = kDescPatGlobal ? kPatternT.t[16 * j + ln] : s_pat[16 * j + ln];  // pair 16ln + j (transposed)
             const float2v X = {pp.x0, pp.x1}, Y = {pp.y0, pp.y1};
             float2v R = (X * B2 + Y * A2) + MAG;  // rows    round(x*b + y*a) of points 0, 1
             float2v C = (X * A2 - Y * B2) + MAG;  // columns round(x*a - y*b)
