@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of liborbamd variants (tools/build_variant.sh) on the GPU box: parity tests of the extraction
 # per variant, then interleaved bench runs (4 graphs x 256 frames) and a serial one-graph run whose
-# stage timings are the kernels alone. usage: tools/ab.sh "<test selector>" v1 v2 ...
+# stage timings are the kernels alone. usage: [AB_ARGS="--config c4"] tools/ab.sh "<test selector>" v1 v2 ...
 sel=$1; shift
 mkdir -p gpurun_out
 for v in "$@"; do
@@ -13,11 +13,11 @@ done
 summ='import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); s=d["stage_ms_per_step"]; print("%.0f" % d["value"], " ".join("%s=%.3f" % (k, s[k]) for k in ("pyramid","fast_cells","octree","blur","describe","match")))'
 for r in 1 2 3; do
   for v in "$@"; do
-    out=$(ORBAMD_LIB_VARIANT=$v timeout -k 10 120 python bench.py --sustain 0 --no-cpu --steps 30 | python -c "$summ") || exit $?
+    out=$(ORBAMD_LIB_VARIANT=$v timeout -k 10 120 python bench.py --sustain 0 --no-cpu --steps 30 ${AB_ARGS} | python -c "$summ") || exit $?
     echo "r$r $v overlapped: $out"
   done
 done
 for v in "$@"; do
-  out=$(ORBAMD_LIB_VARIANT=$v ORBX_SCHED=serial timeout -k 10 120 python bench.py --sustain 0 --no-cpu --steps 30 --pipes 1 --batch 256 | python -c "$summ") || exit $?
+  out=$(ORBAMD_LIB_VARIANT=$v ORBX_SCHED=serial timeout -k 10 120 python bench.py --sustain 0 --no-cpu --steps 30 ${AB_ARGS} --pipes 1 --batch 256 | python -c "$summ") || exit $?
   echo "$v serial-1graph: $out"
 done
