@@ -1118,15 +1118,18 @@ struct ViewPlan {
     size_t desc, x, y, angle, octave, uright, has_mp, mp_bad, feat;
     int nfeat;
 };
-void plan_view(Carve& c, const orbm_kf_view* v, ViewPlan& p) {
+/* geom = false (SearchByBoW): positions, octaves and mvuRight are not uploaded (the BoW matchers read
+ * descriptors, MapPoint flags, angles and the node lists only) */
+void plan_view(Carve& c, const orbm_kf_view* v, ViewPlan& p, bool geom = true) {
     const size_t n = (size_t)std::max(v->n, 1);
+    const size_t none = (size_t)-1;
     p.nfeat = v->n_nodes ? v->node_off[v->n_nodes] : 0;
     p.desc = c.take(32 * n);
-    p.x = c.take(4 * n);
-    p.y = c.take(4 * n);
+    p.x = geom ? c.take(4 * n) : none;
+    p.y = geom ? c.take(4 * n) : none;
     p.angle = c.take(4 * n);
-    p.octave = c.take(4 * n);
-    p.uright = v->uright ? c.take(4 * n) : (size_t)-1;
+    p.octave = geom ? c.take(4 * n) : none;
+    p.uright = geom && v->uright ? c.take(4 * n) : none;
     p.has_mp = v->has_mp ? c.take(n) : (size_t)-1;
     p.mp_bad = v->mp_bad ? c.take(n) : (size_t)-1;
     p.feat = c.take(4 * (size_t)std::max(p.nfeat, 1));
@@ -1139,21 +1142,22 @@ DevView stage_view(uint8_t* hbase, uint8_t* dbase, const orbm_kf_view* v, const 
     const size_t n = (size_t)v->n;
     d.n = v->n;
     d.desc = dbase + p.desc;
-    d.x = (const float*)(dbase + p.x);
-    d.y = (const float*)(dbase + p.y);
+    const size_t none = (size_t)-1;
+    d.x = p.x != none ? (const float*)(dbase + p.x) : nullptr;
+    d.y = p.y != none ? (const float*)(dbase + p.y) : nullptr;
     d.angle = (const float*)(dbase + p.angle);
-    d.octave = (const int32_t*)(dbase + p.octave);
-    d.uright = v->uright ? (const float*)(dbase + p.uright) : nullptr;
+    d.octave = p.octave != none ? (const int32_t*)(dbase + p.octave) : nullptr;
+    d.uright = p.uright != none ? (const float*)(dbase + p.uright) : nullptr;
     d.has_mp = v->has_mp ? dbase + p.has_mp : nullptr;
     d.mp_bad = v->mp_bad ? dbase + p.mp_bad : nullptr;
     d.node_feat = (const int32_t*)(dbase + p.feat);
     if (n) {
         memcpy(hbase + p.desc, v->desc, 32 * n);
-        memcpy(hbase + p.x, v->x, 4 * n);
-        memcpy(hbase + p.y, v->y, 4 * n);
+        if (p.x != none) memcpy(hbase + p.x, v->x, 4 * n);
+        if (p.y != none) memcpy(hbase + p.y, v->y, 4 * n);
         memcpy(hbase + p.angle, v->angle, 4 * n);
-        memcpy(hbase + p.octave, v->octave, 4 * n);
-        if (v->uright) memcpy(hbase + p.uright, v->uright, 4 * n);
+        if (p.octave != none) memcpy(hbase + p.octave, v->octave, 4 * n);
+        if (p.uright != none) memcpy(hbase + p.uright, v->uright, 4 * n);
         if (v->has_mp) memcpy(hbase + p.has_mp, v->has_mp, n);
         if (v->mp_bad) memcpy(hbase + p.mp_bad, v->mp_bad, n);
     }
@@ -1296,8 +1300,8 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
     // matches into pinned host memory pre-filled with -1), one synchronize
     Carve cv;
     ViewPlan pq, pc;
-    plan_view(cv, vq, pq);
-    plan_view(cv, vc, pc);
+    plan_view(cv, vq, pq, false);
+    plan_view(cv, vc, pc, false);
     const size_t o_tasks = cv.take(sizeof(NodeTask) * tasks.size());
     const size_t in_bytes = cv.off;
     const size_t o_list = cv.take(16 * (size_t)std::max(nout, 1));

@@ -37,6 +37,7 @@
 
 #include "../../include/orbslam_amd.h"
 #include "orb_frame.h"
+#include "orb_wave.h"
 
 namespace orbamd {
 
@@ -68,11 +69,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
-}
 
 __device__ __forceinline__ const uint8_t* level_base(const PyrSide& s, const StereoArgs& a, int f, int l,
                                                      int* pitch) {

@@ -21,6 +21,7 @@
 
 #include "../../include/orbslam_amd.h"
 #include "orb_match.h"
+#include "orb_wave.h"
 
 namespace orbamd {
 
@@ -627,6 +628,10 @@ __device__ __forceinline__ Top2 top2_merge(Top2 A, Top2 B) {
     return r;
 }
 
+#ifndef ORBX_BOW_LANE
+#define ORBX_BOW_LANE 1  // nodes of <= 64 candidates: candidate per lane, DPP reductions (0: LDS + shuffles)
+#endif
+
 /* STAGED (node of <= kBowStage candidates, the common case: ~10 per node at levelsup 4): the node's
  * candidate descriptors and eligibility and, 64 at a time, its queries' descriptors are staged in LDS
  * first, so the greedy loop over queries runs without a global-load round trip per query */
@@ -640,10 +645,82 @@ __global__ __launch_bounds__(64) void k_bow(const DevView vq, const DevView vc, 
     __shared__ uint8_t s_cok[STAGED ? kBowStage : 1], s_cm[STAGED ? kBowStage : 1];
     __shared__ uint4 s_qd[STAGED ? 128 : 1];
     __shared__ int s_qi[STAGED ? 64 : 1];
+    __shared__ int s_cidx[STAGED ? kBowStage : 1];  // candidates' feature indices (node order)
+    __shared__ int2 s_acc[STAGED ? 64 : 1];         // this query chunk's accepted (query idx, candidate idx)
     const NodeTask t = tasks[blockIdx.x];
     const int lane = threadIdx.x;
     const int nc = t.c_end - t.c_begin;
     uint8_t* mflag = STAGED ? s_cm : matched;
+    if (STAGED && ORBX_BOW_LANE && nc <= 64) {
+        // candidate j = lane, its descriptor in registers; query k's descriptor broadcast by readlane. Per
+        // query: best1 = the first strict minimum = min over eligible lanes of dist << 6 | j; best2 = min dist
+        // of the other eligible lanes (ORBmatcher.cc:205-225); a claimed candidate drops out of its lane
+        // (vpMapPointMatches / vbMatched2 within the node). The greedy chain never leaves registers.
+        uint32_t cdw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        bool elig = false;
+        int idxc = -1;
+        if (lane < nc) {
+            idxc = vc.node_feat[t.c_begin + lane];
+            const uint4* cd = (const uint4*)(vc.desc + (long long)idxc * 32);
+            const uint4 a = cd[0], b = cd[1];
+            cdw[0] = a.x; cdw[1] = a.y; cdw[2] = a.z; cdw[3] = a.w; cdw[4] = b.x; cdw[5] = b.y; cdw[6] = b.z; cdw[7] = b.w;
+            elig = mode == 0 || ((vc.has_mp && vc.has_mp[idxc]) && !(vc.mp_bad && vc.mp_bad[idxc]));
+        }
+        for (int qb = t.q_begin; qb < t.q_end; qb += 64) {
+            const int nq = min(64, t.q_end - qb);
+            int myq = -1;
+            uint32_t qdw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (lane < nq) {
+                const int iq = vq.node_feat[qb + lane];
+                const bool ok = (vq.has_mp && vq.has_mp[iq]) && !(vq.mp_bad && vq.mp_bad[iq]);
+                myq = ok ? iq : -1;
+                const uint4* qd = (const uint4*)(vq.desc + (long long)iq * 32);
+                const uint4 a = qd[0], b = qd[1];
+                qdw[0] = a.x; qdw[1] = a.y; qdw[2] = a.z; qdw[3] = a.w; qdw[4] = b.x; qdw[5] = b.y; qdw[6] = b.z; qdw[7] = b.w;
+            }
+            int na = 0;
+            for (int k = 0; k < nq; k++) {
+                const int idxq = __builtin_amdgcn_readlane(myq, k);
+                if (idxq < 0) continue;  // no good MapPoint (uniform)
+                int dist = 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) dist += __popc(cdw[u] ^ (uint32_t)__builtin_amdgcn_readlane((int)qdw[u], k));
+                const uint32_t m1 = wave_min_u32(elig ? ((uint32_t)dist << 6 | (uint32_t)lane) : 0xFFFFFFFFu);
+                if (m1 == 0xFFFFFFFFu) continue;  // no eligible candidate left
+                const int i1 = (int)(m1 & 63u), b1 = (int)(m1 >> 6);
+                const int b2 = (int)wave_min_u32((elig && lane != i1) ? (uint32_t)dist : 256u);
+                const bool ok_th = mode == 0 ? (b1 <= 50) : (b1 < 50);  // TH_LOW (ORBmatcher.cc:228 / :598)
+                if (ok_th && __fmul_rn(1.0f, (float)b1) < __fmul_rn(nnratio, (float)b2)) {
+                    const int idxc_w = __builtin_amdgcn_readlane(idxc, i1);
+                    if (lane == i1) elig = false;
+                    if (lane == 0) s_acc[na] = make_int2(idxq, idxc_w);
+                    na++;
+                }
+            }
+            __syncthreads();
+            if (lane < na) {
+                const int2 a = s_acc[lane];
+                if (mode == 0) call_emit(tail, a.y, a.x);  // vpMapPointMatches[bestIdxF] = pMP(KF idx)
+                else call_emit(tail, a.x, a.y);            // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
+            }
+            __syncthreads();
+        }
+        call_tail(tail);
+        return;
+    }
+    // STAGED: a chunk's queries: index (-1 = no good MapPoint) and descriptor; the first chunk is loaded
+    // together with the candidates (one dependent load pair instead of two before the greedy loop)
+    auto load_queries = [&](int qb) {
+        if (lane < min(64, t.q_end - qb)) {
+            const int idxq = vq.node_feat[qb + lane];
+            const bool ok = (vq.has_mp && vq.has_mp[idxq]) && !(vq.mp_bad && vq.mp_bad[idxq]);
+            s_qi[lane] = ok ? idxq : -1;
+            const uint4* qd = (const uint4*)(vq.desc + (long long)idxq * 32);
+            s_qd[2 * lane] = qd[0];
+            s_qd[2 * lane + 1] = qd[1];
+        }
+    };
+    if (STAGED) load_queries(t.q_begin);
     for (int j = lane; j < nc; j += 64) {
         mflag[j] = 0;
         if (STAGED) {
@@ -652,21 +729,15 @@ __global__ __launch_bounds__(64) void k_bow(const DevView vq, const DevView vc, 
             s_cd[2 * j] = cd[0];
             s_cd[2 * j + 1] = cd[1];
             s_cok[j] = mode == 0 || ((vc.has_mp && vc.has_mp[idxc]) && !(vc.mp_bad && vc.mp_bad[idxc]));
+            s_cidx[j] = idxc;
         }
     }
     __syncthreads();
     for (int qb = t.q_begin; qb < t.q_end; qb += 64) {
         const int nq = min(64, t.q_end - qb);
-        if (STAGED) {
-            // this chunk's queries: index (-1 = no good MapPoint) and descriptor
-            if (lane < nq) {
-                const int idxq = vq.node_feat[qb + lane];
-                const bool ok = (vq.has_mp && vq.has_mp[idxq]) && !(vq.mp_bad && vq.mp_bad[idxq]);
-                s_qi[lane] = ok ? idxq : -1;
-                const uint4* qd = (const uint4*)(vq.desc + (long long)idxq * 32);
-                s_qd[2 * lane] = qd[0];
-                s_qd[2 * lane + 1] = qd[1];
-            }
+        int na = 0;  // STAGED: accepts of this chunk, emitted together after it
+        if (STAGED && qb != t.q_begin) {
+            load_queries(qb);
             __syncthreads();
         }
         for (int k = 0; k < nq; k++) {
@@ -715,17 +786,35 @@ __global__ __launch_bounds__(64) void k_bow(const DevView vq, const DevView vc, 
             }
             const bool ok_th = mode == 0 ? (r.b1 <= 50) : (r.b1 < 50);
             if (ok_th && r.i1 >= 0 && __fmul_rn(1.0f, (float)r.b1) < __fmul_rn(nnratio, (float)r.b2)) {
-                const int idxc = vc.node_feat[t.c_begin + r.i1];
-                __syncthreads();
-                if (lane == 0) {
-                    mflag[r.i1] = 1;
-                    if (mode == 0) call_emit(tail, idxc, idxq);  // vpMapPointMatches[bestIdxF] = pMP(KF idx)
-                    else call_emit(tail, idxq, idxc);            // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
+                if (STAGED) {
+                    // the greedy chain touches LDS only: the match is recorded here and emitted (global
+                    // atomics) after the chunk, so no accept waits for a global round trip
+                    if (lane == 0) {
+                        mflag[r.i1] = 1;
+                        s_acc[na] = make_int2(idxq, s_cidx[r.i1]);
+                    }
+                    na++;
+                    __syncthreads();
+                } else {
+                    const int idxc = vc.node_feat[t.c_begin + r.i1];
+                    __syncthreads();
+                    if (lane == 0) {
+                        mflag[r.i1] = 1;
+                        if (mode == 0) call_emit(tail, idxc, idxq);  // vpMapPointMatches[bestIdxF] = pMP(KF idx)
+                        else call_emit(tail, idxq, idxc);            // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
+                    }
+                    __syncthreads();
                 }
-                __syncthreads();
             }
         }
-        if (STAGED) __syncthreads();  // s_qi / s_qd are rewritten by the next chunk
+        if (STAGED) {
+            if (lane < na) {
+                const int2 a = s_acc[lane];
+                if (mode == 0) call_emit(tail, a.y, a.x);  // vpMapPointMatches[bestIdxF] = pMP(KF idx)
+                else call_emit(tail, a.x, a.y);            // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
+            }
+            __syncthreads();  // s_qi / s_qd / s_acc are rewritten by the next chunk
+        }
     }
     call_tail(tail);
 }
