@@ -1671,7 +1671,8 @@ bool frame_view_ok(const orbm_frame_view* F) {
 
 /* uploads the Frame side + queries, runs k_grid / k_proj_scan / k_proj_resolve, downloads */
 int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb, int accept_th, int ratio,
-                   float nnratio, int check_ori, int32_t* match, int* nmatches) {
+                   float nnratio, int check_ori, int32_t* match, int* nmatches, const float* inv_sigma2 = nullptr,
+                   int32_t* qres = nullptr) {
     HIPR(hipSetDevice(ctx->device));
     const size_t n = (size_t)F->n, nq = pb.q.size();
     // inputs first (staged in pinned memory, one H2D copy), then outputs (one D2H copy), then scratch
@@ -1684,7 +1685,7 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     const size_t o_gs = cv.take(4 * (kGridCols * kGridRows + 1)), o_gi = cv.take(2 * n), o_scan = cv.take(32 * nq),
                  o_scnt = cv.take(4 * nq), o_res = cv.take(8 * nq);
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
-    uint8_t* hp = ctx->ensure_pinned(in_bytes + 4 * n + 4);
+    uint8_t* hp = ctx->ensure_pinned(in_bytes + std::max(4 * n + 4, 8 * nq));
     if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
     hipStream_t st = ctx->stream;
@@ -1716,6 +1717,8 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     c.res = (int*)(base + o_res);
     c.nmatches = (int32_t*)(base + o_nm);
     c.match = (int32_t*)(base + o_nm + 4);
+    if (inv_sigma2)
+        for (int l = 0; l < F->nlevels; l++) c.inv_sigma2[l] = inv_sigma2[l];
     memcpy(hp + o_call, &c, sizeof(c));
     if (n) {
         memcpy(hp + o_x, F->x, 4 * n);
@@ -1733,6 +1736,13 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, st));
     HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st));
     uint8_t* ho = hp + in_bytes;
+    if (qres) {
+        // per-query results (Fuse): res[2 qi] = the accepted feature or -1, reported at the query's src
+        HIPR(hipMemcpyAsync(ho, base + o_res, 8 * nq, hipMemcpyDeviceToHost, st));
+        HIPR(hipStreamSynchronize(st));
+        for (size_t qi = 0; qi < nq; qi++) qres[pb.q[qi].src] = ((const int32_t*)ho)[2 * qi];
+        return 0;
+    }
     HIPR(hipMemcpyAsync(ho, base + o_nm, 4 * n + 4, hipMemcpyDeviceToHost, st));
     HIPR(hipStreamSynchronize(st));
     if (n) memcpy(match, ho + 4, 4 * n);
@@ -1908,6 +1918,112 @@ int orbm_search_by_projection_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, con
                mp->desc + 32 * (size_t)iMP);
     }
     return run_projection(ctx, KF, pb, 50 /*TH_LOW*/, 0, 0.f, 0, match, nmatches);
+}
+
+}  // extern "C"
+
+/* ===================================================================================== */
+/* ORBmatcher::Fuse x2: the per-MapPoint projection + windowed search on the device (the    */
+/* k_grid / k_proj_scan / k_proj_resolve pipeline without claims); the map updates that     */
+/* follow each match stay with the caller, in the reference's loop order                    */
+/* ===================================================================================== */
+extern "C" {
+
+int orbm_fuse(orbm_ctx* ctx, const orbm_frame_view* KF, const float Tcw[16], const float Ow[3],
+              const orbm_mappoints* mp, float th, const float* inv_level_sigma2, int32_t* best_idx, int* nfused) {
+    if (!ctx || !frame_view_ok(KF) || !Tcw || !Ow || !inv_level_sigma2 || !mp || mp->n < 0 ||
+        (mp->n && (!mp->desc || !mp->pos || !mp->normal || !mp->min_dist || !mp->max_dist || !best_idx)))
+        return ORBX_EARG;
+    const float* Rcw = Tcw;  // ORBmatcher.cc:827-837
+    const float tcw[3] = {Tcw[3], Tcw[7], Tcw[11]};
+    ProjBatch pb;
+    for (int i = 0; i < mp->n; i++) {  // :843-892
+        best_idx[i] = -1;
+        if (flag(mp->skip, i) || flag(mp->bad, i)) continue;
+        const float* p3Dw = mp->pos + 3 * (size_t)i;
+        float p3Dc[3];
+        gemm33_fast(Rcw, 4, p3Dw, tcw, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz;
+        const float y = p3Dc[1] * invz;
+        const float u = KF->fx * x + KF->cx;
+        const float v = KF->fy * y + KF->cy;
+        if (!(u >= KF->min_x && u < KF->max_x && v >= KF->min_y && v < KF->max_y)) continue;  // IsInImage
+        const float ur = u - KF->bf * invz;
+        const float maxDistance = 1.2f * mp->max_dist[i];
+        const float minDistance = 0.8f * mp->min_dist[i];
+        const float PO[3] = {p3Dw[0] - Ow[0], p3Dw[1] - Ow[1], p3Dw[2] - Ow[2]};
+        const float dist3D = norm3(PO);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        if (dot3(PO, mp->normal + 3 * (size_t)i) < 0.5 * dist3D) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[i], dist3D, KF);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        // KeyFrame::GetFeaturesInArea has no level test; the caller's kpLevel window (:901-902)
+        pb.add(make_query(u, v, radius, nPredictedLevel - 1, nPredictedLevel, ur, -1.f, 0.f, kProjChi2, i),
+               mp->desc + 32 * (size_t)i);
+    }
+    orbm_frame_view K = *KF;
+    K.occupied = nullptr;  // Fuse searches every feature
+    const int rc = run_projection(ctx, &K, pb, 50 /*TH_LOW*/, 0, 0.f, 0, nullptr, nullptr, inv_level_sigma2, best_idx);
+    if (rc) return rc;
+    if (nfused) {
+        int nf = 0;
+        for (int i = 0; i < mp->n; i++) nf += best_idx[i] >= 0;
+        *nfused = nf;
+    }
+    return 0;
+}
+
+int orbm_fuse_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, const float Scw[16], const orbm_mappoints* mp, float th,
+                   int32_t* best_idx, int* nfused) {
+    if (!ctx || !frame_view_ok(KF) || !Scw || !mp || mp->n < 0 ||
+        (mp->n && (!mp->desc || !mp->pos || !mp->normal || !mp->min_dist || !mp->max_dist || !best_idx)))
+        return ORBX_EARG;
+    // decompose Scw (ORBmatcher.cc:985-990) as in orbm_search_by_projection_sim3
+    const float scw = (float)std::sqrt(dot3(Scw, Scw));
+    const float inv = (float)(1. / (double)scw);
+    float Rcw[9], tcw[3], Ow[3];
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) Rcw[3 * r + c] = Scw[4 * r + c] * inv;
+        tcw[r] = Scw[4 * r + 3] * inv;
+    }
+    gemm33t_neg(Rcw, 3, tcw, Ow);
+    ProjBatch pb;
+    for (int iMP = 0; iMP < mp->n; iMP++) {  // :1000-1052
+        best_idx[iMP] = -1;
+        if (flag(mp->bad, iMP) || flag(mp->skip, iMP)) continue;
+        const float* p3Dw = mp->pos + 3 * (size_t)iMP;
+        float p3Dc[3];
+        gemm33_fast(Rcw, 3, p3Dw, tcw, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = (float)(1.0 / (double)p3Dc[2]);  // 1.0/ here (:1019)
+        const float x = p3Dc[0] * invz;
+        const float y = p3Dc[1] * invz;
+        const float u = KF->fx * x + KF->cx;
+        const float v = KF->fy * y + KF->cy;
+        if (!(u >= KF->min_x && u < KF->max_x && v >= KF->min_y && v < KF->max_y)) continue;  // IsInImage
+        const float maxDistance = 1.2f * mp->max_dist[iMP];
+        const float minDistance = 0.8f * mp->min_dist[iMP];
+        const float PO[3] = {p3Dw[0] - Ow[0], p3Dw[1] - Ow[1], p3Dw[2] - Ow[2]};
+        const float dist3D = norm3(PO);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        if (dot3(PO, mp->normal + 3 * (size_t)iMP) < 0.5 * dist3D) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[iMP], dist3D, KF);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        pb.add(make_query(u, v, radius, nPredictedLevel - 1, nPredictedLevel, 0.f, -1.f, 0.f, 0, iMP),
+               mp->desc + 32 * (size_t)iMP);
+    }
+    orbm_frame_view K = *KF;
+    K.occupied = nullptr;
+    const int rc = run_projection(ctx, &K, pb, 50 /*TH_LOW*/, 0, 0.f, 0, nullptr, nullptr, nullptr, best_idx);
+    if (rc) return rc;
+    if (nfused) {
+        int nf = 0;
+        for (int i = 0; i < mp->n; i++) nf += best_idx[i] >= 0;
+        *nfused = nf;
+    }
+    return 0;
 }
 
 }  // extern "C"

@@ -448,6 +448,16 @@ __device__ __forceinline__ int proj_scan(const ProjCall& c, const ProjQuery& q, 
                     const float urf = c.uright[idx];
                     if (urf > 0 && fabsf(__fsub_rn(q.ur, urf)) > q.er_th) continue;
                 }
+                if (q.flags & kProjChi2) {  // ORBmatcher.cc:904-929 (float residual, double threshold)
+                    const float ex = __fsub_rn(q.u, c.x[idx]), ey = __fsub_rn(q.v, c.y[idx]);
+                    float e2 = __fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
+                    const float urf = c.uright ? c.uright[idx] : -1.0f;
+                    if (urf >= 0) {
+                        const float er = __fsub_rn(q.ur, urf);
+                        e2 = __fadd_rn(e2, __fmul_rn(er, er));
+                    }
+                    if ((double)__fmul_rn(e2, c.inv_sigma2[oct]) > (urf >= 0 ? 7.8 : 5.99)) continue;
+                }
                 const uint4* fd = (const uint4*)(c.desc + (long long)idx * 32);
                 const uint4 f0 = fd[0], f1 = fd[1];
                 const int dist = __popc(qd0.x ^ f0.x) + __popc(qd0.y ^ f0.y) + __popc(qd0.z ^ f0.z) +

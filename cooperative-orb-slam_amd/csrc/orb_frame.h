@@ -40,11 +40,15 @@ struct StereoArgs {
 constexpr int kGridCols = 64;  // FRAME_GRID_COLS (Frame.h:38)
 constexpr int kGridRows = 48;  // FRAME_GRID_ROWS (Frame.h:37)
 constexpr int kProjValid = 1, kProjClaims = 2, kProjStereo = 4;
+// Fuse(pKF, vpMapPoints, th) (ORBmatcher.cc:904-929): reprojection-error test of each candidate,
+// e2 * mvInvLevelSigma2[level] > 7.8 (stereo: u, v, ur) or > 5.99 (mono: u, v) rejects
+constexpr int kProjChi2 = 8;
 
 struct ProjQuery {
     float u, v, radius;        // GetFeaturesInArea(u, v, radius, min_level, max_level)
     int min_level, max_level;
-    float ur, er_th;           // stereo check: fabs(ur - mvuRight[i]) > er_th rejects (kProjStereo)
+    float ur, er_th;           // stereo check: fabs(ur - mvuRight[i]) > er_th rejects (kProjStereo); ur also
+                               // feeds the kProjChi2 residual
     float angle;               // source keypoint angle (rotation histogram)
     int flags;                 // kProjValid | kProjClaims (a match occupies the feature) | kProjStereo
     int src;                   // MapPoint index reported in the output
@@ -70,6 +74,7 @@ struct ProjCall {
     unsigned long long* scan;  // [4*nq] the 4 smallest candidate keys per query, ascending
     int* scan_cnt;             // [nq] candidates per query
     int* res;                  // [2*nq] accepted feature idx / rotation bin
+    float inv_sigma2[kMaxLevels];  // mvInvLevelSigma2 (kProjChi2 queries)
     int32_t* match;            // [n]
     int32_t* nmatches;
 };

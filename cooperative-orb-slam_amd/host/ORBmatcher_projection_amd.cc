@@ -5,12 +5,19 @@
  *   SearchByProjection(Frame&, const Frame&, th, bMono)                      ORBmatcher.cc:1328-1470
  *   SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist) ORBmatcher.cc:1472-1599
  *   SearchByProjection(KeyFrame*, cv::Mat Scw, vpPoints, vpMatched, th)      ORBmatcher.cc:290-403
+ * and the two Fuse overloads:
+ *   Fuse(KeyFrame*, const vector<MapPoint*>&, th)                            ORBmatcher.cc:825-975
+ *   Fuse(KeyFrame*, cv::Mat Scw, vpPoints, th, vpReplacePoint)               ORBmatcher.cc:977-1100
  * Each call gathers what the reference reads (keypoints, descriptors, mvuRight, grid bounds, the
  * MapPoint state through the same accessors), runs orbm_search_by_projection_* (geometry prologue
  * on the host with the reference's float semantics; grid, windowed Hamming search, in-order claims
  * and the rotation histogram on the device) and writes the assignments back. MapPoint's private
  * mfMinDistance / mfMaxDistance are read through GetMinDistance() / GetMaxDistance(), two getters
  * the maintainer adds to MapPoint.h. Device failures throw std::runtime_error.
+ * Fuse: the device returns each MapPoint's fused keypoint (orbm_fuse*); the map updates (Replace,
+ * AddObservation, AddMapPoint / vpReplacePoint) then run here in the reference's loop order, with the
+ * reference's per-iteration isBad() / IsInKeyFrame() test, so an entry changed by an earlier update is
+ * skipped exactly as in ORBmatcher.cc.
  */
 #include <algorithm>
 #include <cstdlib>
@@ -254,6 +261,98 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector
             "orbm_search_by_projection_sim3");
     apply(vpMatched, m, vpPoints);
     return nm;
+}
+
+// ORBmatcher.cc:825-975
+int ORBmatcher::Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, const float th) {
+    FrameSide fs;
+    fs.gather(*pKF, &pKF->mvuRight, pKF->mbf, 0.f);
+    const size_t n = vpMapPoints.size();
+    PointSide ps;
+    ps.reserve(n);
+    for (size_t i = 0; i < n; i++) {  // :843-850
+        MapPoint* p = vpMapPoints[i];
+        ps.skip[i] = !p || p->isBad() || p->IsInKeyFrame(pKF);
+        if (ps.skip[i]) continue;
+        ps.point(i, p, true);
+        cv::Mat nv = p->GetNormal();
+        for (int k = 0; k < 3; k++) ps.normal[3 * i + k] = nv.at<float>(k, 0);
+    }
+    ps.finish(n);
+    cv::Mat R = pKF->GetRotation(), t = pKF->GetTranslation(), Ow = pKF->GetCameraCenter();
+    float T[16] = {0}, O[3];
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) T[4 * r + c] = R.at<float>(r, c);
+        T[4 * r + 3] = t.at<float>(r, 0);
+        O[r] = Ow.at<float>(r, 0);
+    }
+    T[15] = 1.f;
+    std::vector<int32_t> best(n ? n : 1);
+    int nf = 0;
+    proj_ok(orbm_fuse(proj_ctx(), &fs.v, T, O, &ps.m, th, pKF->mvInvLevelSigma2.data(), best.data(), &nf),
+            "orbm_fuse");
+    // the reference's updates, in order (:947-971)
+    int nFused = 0;
+    for (size_t i = 0; i < n; i++) {
+        MapPoint* pMP = vpMapPoints[i];
+        if (!pMP || best[i] < 0) continue;
+        if (pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;  // changed by an earlier update
+        const size_t bestIdx = (size_t)best[i];
+        MapPoint* pMPinKF = pKF->GetMapPoint(bestIdx);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) {
+                if (pMPinKF->Observations() > pMP->Observations())
+                    pMP->Replace(pMPinKF);
+                else
+                    pMPinKF->Replace(pMP);
+            }
+        } else {
+            pMP->AddObservation(pKF, bestIdx);
+            pKF->AddMapPoint(pMP, bestIdx);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+
+// ORBmatcher.cc:977-1100
+int ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints, float th,
+                     std::vector<MapPoint*>& vpReplacePoint) {
+    FrameSide fs;
+    fs.gather(*pKF, nullptr, 0.f, 0.f);
+    const std::set<MapPoint*> spAlreadyFound = pKF->GetMapPoints();  // :993
+    const size_t n = vpPoints.size();
+    PointSide ps;
+    ps.reserve(n);
+    for (size_t i = 0; i < n; i++) {
+        MapPoint* p = vpPoints[i];
+        ps.skip[i] = p->isBad() || spAlreadyFound.count(p) > 0;  // :1005-1006
+        if (ps.skip[i]) continue;
+        ps.point(i, p, true);
+        cv::Mat nv = p->GetNormal();
+        for (int k = 0; k < 3; k++) ps.normal[3 * i + k] = nv.at<float>(k, 0);
+    }
+    ps.finish(n);
+    cv::Mat ks;
+    std::vector<int32_t> best(n ? n : 1);
+    int nf = 0;
+    proj_ok(orbm_fuse_sim3(proj_ctx(), &fs.v, mat44(Scw, ks), &ps.m, th, best.data(), &nf), "orbm_fuse_sim3");
+    int nFused = 0;
+    for (size_t i = 0; i < n; i++) {  // :1082-1097, in order
+        if (best[i] < 0) continue;
+        MapPoint* pMP = vpPoints[i];
+        if (pMP->isBad()) continue;
+        const size_t bestIdx = (size_t)best[i];
+        MapPoint* pMPinKF = pKF->GetMapPoint(bestIdx);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) vpReplacePoint[i] = pMPinKF;
+        } else {
+            pMP->AddObservation(pKF, bestIdx);
+            pKF->AddMapPoint(pMP, bestIdx);
+        }
+        nFused++;
+    }
+    return nFused;
 }
 
 }  // namespace ORB_SLAM2

@@ -175,6 +175,30 @@ class ORBmatcher:
         S = np.ascontiguousarray(Scw, np.float32).reshape(16)
         return self._proj("orbm_search_by_projection_sim3", KF, S.ctypes.data, C.byref(m), int(th))
 
+    # ---- Fuse x2 (ORBmatcher.cc:825-975, 977-1100): (nFused, best_idx[mps.n]) = the keypoint of KF each
+    # MapPoint fuses with (-1: none); the map updates that follow stay with the caller, in order.
+    def Fuse(self, KF, Tcw, Ow, mps, th, inv_level_sigma2):
+        m = mps.cstruct()
+        fv = KF.cstruct()
+        T = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+        O = np.ascontiguousarray(Ow, np.float32).reshape(3)
+        inv = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        out = np.empty(max(mps.n, 1), np.int32)
+        n = C.c_int()
+        check(self._lib.orbm_fuse(self._h, C.byref(fv), T.ctypes.data, O.ctypes.data, C.byref(m), C.c_float(th),
+                                  inv.ctypes.data, out.ctypes.data, C.byref(n)), "orbm_fuse")
+        return n.value, out[:mps.n]
+
+    def FuseSim3(self, KF, Scw, mps, th):
+        m = mps.cstruct()
+        fv = KF.cstruct()
+        S = np.ascontiguousarray(Scw, np.float32).reshape(16)
+        out = np.empty(max(mps.n, 1), np.int32)
+        n = C.c_int()
+        check(self._lib.orbm_fuse_sim3(self._h, C.byref(fv), S.ctypes.data, C.byref(m), C.c_float(th),
+                                       out.ctypes.data, C.byref(n)), "orbm_fuse_sim3")
+        return n.value, out[:mps.n]
+
 
 def compute_distinctive_descriptors(offsets, desc, device=0, matcher=None):
     """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of MapPoints:

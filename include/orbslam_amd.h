@@ -300,6 +300,28 @@ int orbm_search_by_projection_keyframe(orbm_ctx* ctx, const orbm_frame_view* F, 
 int orbm_search_by_projection_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, const float Scw[16],
                                    const orbm_mappoints* mp, int th, int32_t* match, int* nmatches);
 
+/* ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, th) (ORBmatcher.cc:825-975,
+ * called by LocalMapping::SearchInNeighbors, LocalMapping.cc:489,514): the per-MapPoint projection,
+ * frustum / scale / viewing-angle tests, windowed search with the reprojection-error (chi2) test on
+ * the device; best_idx[i] = the keypoint of pKF that MapPoint i fuses with (bestDist <= TH_LOW),
+ * -1 otherwise, *nfused = the reference's return value. The caller then applies, for i in order,
+ * the reference's update (:947-971: Replace by Observations() or AddObservation + AddMapPoint),
+ * re-checking isBad() / IsInKeyFrame(pKF) at that point exactly as the reference loop does (an
+ * entry that turns true there was changed by an earlier update and is skipped). mp: skip = NULL
+ * entry or IsInKeyFrame(pKF), bad, pos, normal, desc, min_dist, max_dist. KF.occupied is ignored.
+ * Tcw = pKF->GetPose() (4x4 row-major), Ow = pKF->GetCameraCenter(), inv_level_sigma2 =
+ * pKF->mvInvLevelSigma2[nlevels]. */
+int orbm_fuse(orbm_ctx* ctx, const orbm_frame_view* KF, const float Tcw[16], const float Ow[3],
+              const orbm_mappoints* mp, float th, const float* inv_level_sigma2, int32_t* best_idx, int* nfused);
+
+/* ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints, th, vpReplacePoint)
+ * (ORBmatcher.cc:977-1100, LoopClosing::SearchAndFuse): best_idx as in orbm_fuse (no reprojection
+ * test); the caller sets vpReplacePoint[i] = pKF->GetMapPoint(best) when that is a good MapPoint,
+ * else adds the observation (:1084-1096), in order. mp: skip = in pKF->GetMapPoints() at the call,
+ * bad, pos, normal, desc, min_dist, max_dist. Scw = 4x4 row-major float Sim3. */
+int orbm_fuse_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, const float Scw[16], const orbm_mappoints* mp,
+                   float th, int32_t* best_idx, int* nfused);
+
 /* ------------------------------------------------------------------------------------
  * MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of MapPoints.
  * MapPoint p's observed descriptors (the rows pKF->mDescriptors.row(idx) of its non-bad

@@ -57,6 +57,8 @@ _SIG = {
     "oc_search_by_projection_last_frame": (_I, [_P, _P, _P, _P, _F, _I, _I, _P]),
     "oc_search_by_projection_keyframe": (_I, [_P, _P, _P, _F, _I, _I, _P]),
     "oc_search_by_projection_sim3": (_I, [_P, _P, _P, _I, _P]),
+    "oc_fuse": (_I, [_P, _P, _P, _P, _F, _P, _P]),
+    "oc_fuse_sim3": (_I, [_P, _P, _P, _F, _P]),
     "oc_compute_distinctive_descriptors": (None, [_I, _P, _P, _P]),
     "oc_vocab_create": (_P, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "oc_vocab_destroy": (None, [_P]),
@@ -296,6 +298,28 @@ def search_by_projection_sim3(KF, Scw, mps, th):
     m = mps.cstruct()
     S = np.ascontiguousarray(Scw, np.float32).reshape(16)
     return _proj("oc_search_by_projection_sim3", KF, S.ctypes.data, C.byref(m), int(th))
+
+
+# ---- Fuse x2 (ORBmatcher.cc:825-975, 977-1100): (nFused, best_idx[mps.n]), -1 = no fuse.
+def fuse(KF, Tcw, Ow, mps, th, inv_sigma2):
+    m = mps.cstruct()
+    fv = KF.cstruct()
+    T = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+    O = np.ascontiguousarray(Ow, np.float32).reshape(3)
+    inv = np.ascontiguousarray(inv_sigma2, np.float32)
+    out = np.empty(max(mps.n, 1), np.int32)
+    n = load().oc_fuse(C.byref(fv), T.ctypes.data, O.ctypes.data, C.byref(m), C.c_float(th), inv.ctypes.data,
+                       out.ctypes.data)
+    return n, out[:mps.n]
+
+
+def fuse_sim3(KF, Scw, mps, th):
+    m = mps.cstruct()
+    fv = KF.cstruct()
+    S = np.ascontiguousarray(Scw, np.float32).reshape(16)
+    out = np.empty(max(mps.n, 1), np.int32)
+    n = load().oc_fuse_sim3(C.byref(fv), S.ctypes.data, C.byref(m), C.c_float(th), out.ctypes.data)
+    return n, out[:mps.n]
 
 
 def compute_distinctive_descriptors(offsets, desc):

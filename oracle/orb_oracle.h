@@ -86,6 +86,10 @@ void oc_compute_distinctive_descriptors(int npoints, const int32_t* offsets, con
                                         int32_t* best_idx);
 int oc_search_by_projection_sim3(const orbm_frame_view* KF, const float* Scw, const orbm_mappoints* mp, int th,
                                  int32_t* match);
+/* ORBmatcher::Fuse x2 (ORBmatcher.cc:825-975, 977-1100): per-MapPoint best_idx (-1 = no fuse) */
+int oc_fuse(const orbm_frame_view* KF, const float* Tcw, const float* Ow, const orbm_mappoints* mp, float th,
+            const float* inv_sigma2, int32_t* best_idx);
+int oc_fuse_sim3(const orbm_frame_view* KF, const float* Scw, const orbm_mappoints* mp, float th, int32_t* best_idx);
 
 /* DBoW2 vocabulary transform (orb_oracle_voc.c; parity unpinned: DBoW2 is not vendored) */
 typedef struct oc_vocab oc_vocab;

@@ -608,6 +608,135 @@ int oc_search_by_projection_sim3(const orbm_frame_view* KF, const float* Scw, co
     return nmatches;
 }
 
+/* ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, th) (ORBmatcher.cc:825-975),
+ * the per-MapPoint search: best_idx[i] = bestIdx when bestDist <= TH_LOW (the reference then fuses or
+ * adds the observation, :947-971, on the caller's side), else -1. mp: skip = NULL entry or
+ * IsInKeyFrame(pKF), bad, pos, normal, desc, min_dist, max_dist. Tcw = pKF's pose (4x4 row-major),
+ * Ow = pKF->GetCameraCenter(), inv_sigma2 = mvInvLevelSigma2. Returns nFused. */
+int oc_fuse(const orbm_frame_view* KF, const float* Tcw, const float* Ow, const orbm_mappoints* mp, float th,
+            const float* inv_sigma2, int32_t* best_idx) {
+    const float tcw[3] = {Tcw[3], Tcw[7], Tcw[11]};
+    int nFused = 0;
+    ogrid* g = grid_build(KF);
+    ivec2 vIndices = {0};
+    for (int i = 0; i < mp->n; i++) {
+        best_idx[i] = -1;
+        if (has(mp->skip, i) || has(mp->bad, i)) continue; /* :844-850 */
+        const float* p3Dw = mp->pos + 3 * (size_t)i;
+        float p3Dc[3];
+        gemm33_fast(Tcw, 4, p3Dw, tcw, p3Dc); /* Rcw*p3Dw + tcw */
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz;
+        const float y = p3Dc[1] * invz;
+        const float u = KF->fx * x + KF->cx;
+        const float v = KF->fy * y + KF->cy;
+        if (!(u >= KF->min_x && u < KF->max_x && v >= KF->min_y && v < KF->max_y)) continue; /* IsInImage */
+        const float ur = u - KF->bf * invz;
+        const float maxDistance = 1.2f * mp->max_dist[i];
+        const float minDistance = 0.8f * mp->min_dist[i];
+        const float PO[3] = {p3Dw[0] - Ow[0], p3Dw[1] - Ow[1], p3Dw[2] - Ow[2]};
+        const float dist3D = norm3(PO);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        if (dot3(PO, mp->normal + 3 * (size_t)i) < 0.5 * dist3D) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[i], dist3D, KF);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        features_in_area(KF, g, u, v, radius, -1, -1, &vIndices);
+        if (vIndices.n == 0) continue;
+        const uint8_t* dMP = mp->desc + 32 * (size_t)i;
+        int bestDist = 256, bestIdx = -1;
+        for (int k = 0; k < vIndices.n; k++) {
+            const int idx = vIndices.v[k];
+            const int kpLevel = KF->octave[idx];
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const float kpx = KF->x[idx], kpy = KF->y[idx];
+            const float ex = u - kpx, ey = v - kpy;
+            if (KF->uright && KF->uright[idx] >= 0) { /* reprojection error, stereo (:907-918) */
+                const float er = ur - KF->uright[idx];
+                const float e2 = ex * ex + ey * ey + er * er;
+                if (e2 * inv_sigma2[kpLevel] > 7.8) continue;
+            } else { /* mono (:920-929) */
+                const float e2 = ex * ex + ey * ey;
+                if (e2 * inv_sigma2[kpLevel] > 5.99) continue;
+            }
+            const int dist = oc_descriptor_distance(dMP, KF->desc + 32 * (size_t)idx);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx = idx;
+            }
+        }
+        if (bestDist <= TH_LOW) {
+            best_idx[i] = bestIdx;
+            nFused++;
+        }
+    }
+    free(vIndices.v);
+    grid_free(g);
+    return nFused;
+}
+
+/* ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints, th, vpReplacePoint)
+ * (ORBmatcher.cc:977-1100), the per-MapPoint search: best_idx[i] as in oc_fuse (the caller then sets
+ * vpReplacePoint[i] or adds the observation, :1084-1096). mp: skip = in spAlreadyFound
+ * (pKF->GetMapPoints() at the call), bad, pos, normal, desc, min_dist, max_dist. Returns nFused. */
+int oc_fuse_sim3(const orbm_frame_view* KF, const float* Scw, const orbm_mappoints* mp, float th, int32_t* best_idx) {
+    const double d0 = dot3(Scw, Scw); /* :987-991, decomposition as in oc_search_by_projection_sim3 */
+    const float scw = (float)sqrt(d0);
+    const float inv = (float)(1. / (double)scw);
+    float Rcw[9], tcw[3], Ow[3];
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) Rcw[3 * r + c] = Scw[4 * r + c] * inv;
+        tcw[r] = Scw[4 * r + 3] * inv;
+    }
+    gemm33t_neg(Rcw, 3, tcw, Ow);
+    int nFused = 0;
+    ogrid* g = grid_build(KF);
+    ivec2 vIndices = {0};
+    for (int iMP = 0; iMP < mp->n; iMP++) {
+        best_idx[iMP] = -1;
+        if (has(mp->bad, iMP) || has(mp->skip, iMP)) continue; /* :1005-1006 */
+        const float* p3Dw = mp->pos + 3 * (size_t)iMP;
+        float p3Dc[3];
+        gemm33_fast(Rcw, 3, p3Dw, tcw, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = (float)(1.0 / (double)p3Dc[2]); /* 1.0/ (double) here, 1/ (float) in :322 */
+        const float x = p3Dc[0] * invz;
+        const float y = p3Dc[1] * invz;
+        const float u = KF->fx * x + KF->cx;
+        const float v = KF->fy * y + KF->cy;
+        if (!(u >= KF->min_x && u < KF->max_x && v >= KF->min_y && v < KF->max_y)) continue; /* IsInImage */
+        const float maxDistance = 1.2f * mp->max_dist[iMP];
+        const float minDistance = 0.8f * mp->min_dist[iMP];
+        const float PO[3] = {p3Dw[0] - Ow[0], p3Dw[1] - Ow[1], p3Dw[2] - Ow[2]};
+        const float dist3D = norm3(PO);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        if (dot3(PO, mp->normal + 3 * (size_t)iMP) < 0.5 * dist3D) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[iMP], dist3D, KF);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        features_in_area(KF, g, u, v, radius, -1, -1, &vIndices);
+        if (vIndices.n == 0) continue;
+        const uint8_t* dMP = mp->desc + 32 * (size_t)iMP;
+        int bestDist = INT_MAX, bestIdx = -1;
+        for (int k = 0; k < vIndices.n; k++) {
+            const int idx = vIndices.v[k];
+            const int kpLevel = KF->octave[idx];
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const int dist = oc_descriptor_distance(dMP, KF->desc + 32 * (size_t)idx);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx = idx;
+            }
+        }
+        if (bestDist <= TH_LOW) {
+            best_idx[iMP] = bestIdx;
+            nFused++;
+        }
+    }
+    free(vIndices.v);
+    grid_free(g);
+    return nFused;
+}
+
 /* ===================================================================================== */
 /* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307)                          */
 /* ===================================================================================== */

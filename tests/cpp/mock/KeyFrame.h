@@ -2,6 +2,7 @@
 #ifndef KEYFRAME_H
 #define KEYFRAME_H
 #include <map>
+#include <set>
 #include <opencv2/core/core.hpp>
 #include <opencv2/features2d/features2d.hpp>
 #include <vector>
@@ -37,6 +38,34 @@ public:
     cv::Mat GetRotation() { return Rcw.clone(); }
     cv::Mat GetTranslation() { return tcw.clone(); }
     cv::Mat GetCameraCenter() { return Ow.clone(); }
+    float mbf = 0;
+    std::vector<float> mvInvLevelSigma2;
+    void AddMapPoint(MapPoint* pMP, const size_t& idx) { mvpMapPoints[idx] = pMP; }
+    std::set<MapPoint*> GetMapPoints() {  // KeyFrame.cc:173-186
+        std::set<MapPoint*> s;
+        for (MapPoint* p : mvpMapPoints)
+            if (p && !p->isBad()) s.insert(p);
+        return s;
+    }
 };
+inline void MapPoint::AddObservation(KeyFrame* pKF, size_t idx) {  // MapPoint.cc:63-74
+    if (mObservations.count(pKF)) return;
+    mObservations[pKF] = idx;
+    nObs += pKF->mvuRight[idx] >= 0 ? 2 : 1;
+}
+inline void MapPoint::Replace(MapPoint* pMP) {  // MapPoint.cc:130-170 (map bookkeeping only)
+    if (pMP == this) return;
+    std::map<KeyFrame*, size_t> obs = mObservations;
+    mObservations.clear();
+    bad = true;
+    for (auto& o : obs) {
+        if (!pMP->IsInKeyFrame(o.first)) {
+            o.first->mvpMapPoints[o.second] = pMP;  // ReplaceMapPointMatch
+            pMP->AddObservation(o.first, o.second);
+        } else {
+            o.first->mvpMapPoints[o.second] = nullptr;  // EraseMapPointMatch
+        }
+    }
+}
 }  // namespace ORB_SLAM2
 #endif

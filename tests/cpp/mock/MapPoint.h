@@ -31,6 +31,10 @@ public:
     float mTrackProjX = 0, mTrackProjY = 0, mTrackProjXR = 0, mTrackViewCos = 0;
     int mnTrackScaleLevel = 0;
     bool isBad() { return bad; }
+    /* MapPoint.cc:63-120, 130-170 (Fuse's updates): observations, replacement */
+    bool IsInKeyFrame(KeyFrame* pKF) { return mObservations.count(pKF) > 0; }
+    void AddObservation(KeyFrame* pKF, size_t idx);
+    void Replace(MapPoint* pMP);
     int Observations() { return nObs; }
     cv::Mat GetWorldPos() { return mWorldPos.clone(); }
     cv::Mat GetNormal() { return mNormalVector.clone(); }

@@ -9,6 +9,8 @@
 #include <cstring>
 #include <atomic>
 #include <thread>
+#include <string>
+#include <set>
 #include <vector>
 
 #include "ORBextractor.h"
@@ -131,6 +133,208 @@ static void oview(KeyFrame& kf, OView& w, bool with_mp, bool with_ur) {
     w.v.n_nodes = (int32_t)w.id.size(); w.v.node_id = w.id.data(); w.v.node_off = w.off.data();
     w.v.node_feat = w.feat.data(); w.v.nlevels = (int32_t)kf.mvScaleFactors.size();
     w.v.scale_factors = kf.mvScaleFactors.data(); w.v.level_sigma2 = kf.mvLevelSigma2.data();
+}
+
+/* ---- Fuse x2 (ORBmatcher.cc:825-975, 977-1100): the drop-in (device search + in-order updates) vs a
+ * literal restatement of the reference loop that searches each MapPoint from the map state of its own
+ * iteration (oracle oc_fuse* on that one MapPoint), compared on the final map state. */
+struct FuseWorld {
+    KeyFrame kf;
+    std::vector<MapPoint> pre, mps;
+    std::vector<MapPoint*> vp;
+};
+static void build_fuse_world(FuseWorld& w, const std::vector<cv::KeyPoint>& kps, const cv::Mat& desc,
+                             ORBextractor& ext, int W, int H, uint32_t seed) {
+    KeyFrame& kf = w.kf;
+    uint32_t s = seed;
+    auto urand = [&](float a, float b) { return a + (b - a) * (float)(lcg(s) % 100000) / 100000.f; };
+    kf.N = (int)kps.size(); kf.mvKeys = kps; kf.mvKeysUn = kps; kf.mDescriptors = desc;
+    kf.mvScaleFactors = ext.GetScaleFactors(); kf.mvLevelSigma2 = ext.GetScaleSigmaSquares();
+    kf.mvInvLevelSigma2 = ext.GetInverseScaleSigmaSquares();
+    kf.mnScaleLevels = 8; kf.mfLogScaleFactor = logf(1.2f);
+    kf.fx = 715.092024f; kf.fy = 719.025258f; kf.cx = 334.298489f; kf.cy = 256.326097f; kf.mbf = 47.9f;
+    kf.mnMinX = 0.f; kf.mnMaxX = (float)W; kf.mnMinY = 0.f; kf.mnMaxY = (float)H;
+    kf.mfGridElementWidthInv = 64.f / (kf.mnMaxX - kf.mnMinX);
+    kf.mfGridElementHeightInv = 48.f / (kf.mnMaxY - kf.mnMinY);
+    kf.mvuRight.assign(kf.N, -1.f);
+    for (int i = 0; i < kf.N; i++) if (lcg(s) % 2) kf.mvuRight[i] = kps[i].pt.x - urand(1.f, 30.f);
+    kf.Rcw = cv::Mat(3, 3, CV_32F);
+    for (int i = 0; i < 9; i++) kf.Rcw.at<float>(i / 3, i % 3) = (i % 4 == 0) ? 1.f : 0.f;
+    kf.tcw = cv::Mat(3, 1, CV_32F);
+    kf.tcw.at<float>(0) = 0.02f; kf.tcw.at<float>(1) = -0.01f; kf.tcw.at<float>(2) = 0.03f;
+    kf.Ow = cv::Mat(3, 1, CV_32F);
+    for (int k = 0; k < 3; k++) kf.Ow.at<float>(k) = -kf.tcw.at<float>(k);  // -R^T t, R = I
+    w.pre.resize(kf.N);
+    kf.mvpMapPoints.assign(kf.N, nullptr);
+    for (int i = 0; i < kf.N; i++) {
+        if (lcg(s) % 5) continue;
+        MapPoint& p = w.pre[i];
+        p.bad = lcg(s) % 10 == 0;
+        p.nObs = 0;
+        p.mObservations[&kf] = i;
+        p.nObs = (int)(lcg(s) % 6) + 1;
+        kf.mvpMapPoints[i] = &p;
+    }
+    const int M = 700;
+    w.mps.resize(M);
+    w.vp.resize(M);
+    for (int j = 0; j < M; j++) {
+        MapPoint& p = w.mps[j];
+        w.vp[j] = &p;
+        const int src = (int)(lcg(s) % (uint32_t)(j < 100 ? 40 : kf.N));  // the first 100 crowd 40 features
+        const float z = urand(1.f, 10.f), nz = lcg(s) % 3 ? 0.002f : 0.02f;
+        const float Xc[3] = {(kps[src].pt.x - kf.cx) / kf.fx * z + urand(-nz, nz),
+                             (kps[src].pt.y - kf.cy) / kf.fy * z + urand(-nz, nz), z + urand(-nz, nz)};
+        p.mWorldPos = cv::Mat(3, 1, CV_32F);
+        float d2 = 0;
+        for (int k = 0; k < 3; k++) {
+            p.mWorldPos.at<float>(k) = Xc[k] - kf.tcw.at<float>(k);  // R = I
+            const float o = p.mWorldPos.at<float>(k) - kf.Ow.at<float>(k);
+            d2 += o * o;
+        }
+        const float dist = sqrtf(d2);
+        p.mNormalVector = cv::Mat(3, 1, CV_32F);
+        const float sg = lcg(s) % 20 == 0 ? -1.f : 1.f;
+        for (int k = 0; k < 3; k++)
+            p.mNormalVector.at<float>(k) = sg * (p.mWorldPos.at<float>(k) - kf.Ow.at<float>(k)) / dist;
+        p.mfMaxDistance = dist * powf(1.2f, (float)kps[src].octave + urand(-0.9f, 0.1f));
+        p.mfMinDistance = p.mfMaxDistance / powf(1.2f, 7.f);
+        p.mDescriptor = cv::Mat(1, 32, CV_8U);
+        memcpy(p.mDescriptor.data, desc.ptr<unsigned char>(src), 32);
+        const int nb = (int)(lcg(s) % 31);
+        for (int b = 0; b < nb; b++) { const uint32_t r = lcg(s) % 256; p.mDescriptor.data[r >> 3] ^= (uint8_t)(1u << (r & 7)); }
+        p.bad = lcg(s) % 20 == 0;
+        p.nObs = (int)(lcg(s) % 6) + 1;
+        if (lcg(s) % 20 == 0) p.mObservations[&kf] = (size_t)(lcg(s) % kf.N);  // already in the keyframe
+    }
+}
+static orbm_frame_view fuse_kf_view(KeyFrame& kf, std::vector<float>& x, std::vector<float>& y, std::vector<int32_t>& o) {
+    x.clear(); y.clear(); o.clear();
+    for (const cv::KeyPoint& k : kf.mvKeysUn) { x.push_back(k.pt.x); y.push_back(k.pt.y); o.push_back(k.octave); }
+    orbm_frame_view v;
+    memset(&v, 0, sizeof(v));
+    v.n = kf.N; v.desc = kf.mDescriptors.data; v.x = x.data(); v.y = y.data(); v.octave = o.data();
+    v.uright = kf.mvuRight.data();
+    v.min_x = kf.mnMinX; v.min_y = kf.mnMinY; v.max_x = kf.mnMaxX; v.max_y = kf.mnMaxY;
+    v.grid_w_inv = kf.mfGridElementWidthInv; v.grid_h_inv = kf.mfGridElementHeightInv;
+    v.fx = kf.fx; v.fy = kf.fy; v.cx = kf.cx; v.cy = kf.cy; v.bf = kf.mbf;
+    v.nlevels = 8; v.scale_factors = kf.mvScaleFactors.data(); v.log_scale_factor = kf.mfLogScaleFactor;
+    return v;
+}
+/* one MapPoint's current state as a 1-entry orbm_mappoints */
+struct OneMP {
+    float pos[3], nrm[3], mind, maxd;
+    orbm_mappoints m;
+    explicit OneMP(MapPoint* p) {
+        for (int k = 0; k < 3; k++) { pos[k] = p->mWorldPos.at<float>(k); nrm[k] = p->mNormalVector.at<float>(k); }
+        mind = p->mfMinDistance; maxd = p->mfMaxDistance;
+        memset(&m, 0, sizeof(m));
+        m.n = 1; m.desc = p->mDescriptor.data; m.pos = pos; m.normal = nrm; m.min_dist = &mind; m.max_dist = &maxd;
+    }
+};
+/* the reference loops, literally (ORBmatcher.cc:843-972 / 1000-1097) */
+static int ref_fuse(FuseWorld& w, float th) {
+    KeyFrame* pKF = &w.kf;
+    std::vector<float> x, y;
+    std::vector<int32_t> o;
+    const orbm_frame_view v = fuse_kf_view(*pKF, x, y, o);
+    float T[16] = {0};
+    for (int r = 0; r < 3; r++) { for (int c = 0; c < 3; c++) T[4 * r + c] = pKF->Rcw.at<float>(r, c); T[4 * r + 3] = pKF->tcw.at<float>(r); }
+    int nFused = 0;
+    for (MapPoint* pMP : w.vp) {
+        if (!pMP || pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;
+        OneMP one(pMP);
+        int32_t best = -1;
+        oc_fuse(&v, T, pKF->Ow.ptr<float>(), &one.m, th, pKF->mvInvLevelSigma2.data(), &best);
+        if (best < 0) continue;
+        MapPoint* pMPinKF = pKF->GetMapPoint((size_t)best);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) {
+                if (pMPinKF->Observations() > pMP->Observations()) pMP->Replace(pMPinKF);
+                else pMPinKF->Replace(pMP);
+            }
+        } else {
+            pMP->AddObservation(pKF, (size_t)best);
+            pKF->AddMapPoint(pMP, (size_t)best);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+static int ref_fuse_sim3(FuseWorld& w, const cv::Mat& Scw, float th, std::vector<MapPoint*>& repl) {
+    KeyFrame* pKF = &w.kf;
+    std::vector<float> x, y;
+    std::vector<int32_t> o;
+    const orbm_frame_view v = fuse_kf_view(*pKF, x, y, o);
+    const std::set<MapPoint*> already = pKF->GetMapPoints();
+    int nFused = 0;
+    for (size_t i = 0; i < w.vp.size(); i++) {
+        MapPoint* pMP = w.vp[i];
+        if (pMP->isBad() || already.count(pMP)) continue;
+        OneMP one(pMP);
+        int32_t best = -1;
+        oc_fuse_sim3(&v, Scw.ptr<float>(), &one.m, th, &best);
+        if (best < 0) continue;
+        MapPoint* pMPinKF = pKF->GetMapPoint((size_t)best);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) repl[i] = pMPinKF;
+        } else {
+            pMP->AddObservation(pKF, (size_t)best);
+            pKF->AddMapPoint(pMP, (size_t)best);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+/* map state as labels: keyframe slot -> "p<k>" / "m<j>"; per MapPoint: bad, index observed in kf */
+static std::string label(FuseWorld& w, const MapPoint* p) {
+    if (!p) return "-";
+    if (p >= w.pre.data() && p < w.pre.data() + w.pre.size()) return "p" + std::to_string(p - w.pre.data());
+    return "m" + std::to_string(p - w.mps.data());
+}
+static int fuse_state_diff(FuseWorld& a, FuseWorld& b) {
+    int d = 0;
+    for (int i = 0; i < a.kf.N; i++) d += label(a, a.kf.mvpMapPoints[i]) != label(b, b.kf.mvpMapPoints[i]);
+    for (size_t j = 0; j < a.mps.size(); j++) {
+        MapPoint &p = a.mps[j], &q = b.mps[j];
+        const long ia = p.mObservations.count(&a.kf) ? (long)p.mObservations[&a.kf] : -1;
+        const long ib = q.mObservations.count(&b.kf) ? (long)q.mObservations[&b.kf] : -1;
+        d += p.bad != q.bad || ia != ib || p.nObs != q.nObs;
+    }
+    for (size_t k = 0; k < a.pre.size(); k++) d += a.pre[k].bad != b.pre[k].bad || a.pre[k].nObs != b.pre[k].nObs;
+    return d;
+}
+static void test_fuse(const std::vector<cv::KeyPoint>& kps, const cv::Mat& desc, ORBextractor& ext, int W, int H) {
+    for (float th : {3.0f, 5.0f}) {
+        FuseWorld a, b;
+        build_fuse_world(a, kps, desc, ext, W, H, 91);
+        build_fuse_world(b, kps, desc, ext, W, H, 91);
+        const int na = ref_fuse(a, th);
+        ORBmatcher m(0.6f, true);
+        const int nb = m.Fuse(&b.kf, b.vp, th);
+        const int d = fuse_state_diff(a, b);
+        CHECK(na == nb && na > 100 && d == 0, "Fuse(pKF, vpMapPoints) th=%.0f: %d vs reference loop %d, %d state diffs",
+              th, nb, na, d);
+    }
+    {
+        FuseWorld a, b;
+        build_fuse_world(a, kps, desc, ext, W, H, 92);
+        build_fuse_world(b, kps, desc, ext, W, H, 92);
+        cv::Mat Scw(4, 4, CV_32F);
+        for (int i = 0; i < 16; i++) Scw.at<float>(i / 4, i % 4) = (i % 5 == 0) ? 1.f : 0.f;
+        const float sc = 1.1f;
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) Scw.at<float>(r, c) = sc * a.kf.Rcw.at<float>(r, c);
+            Scw.at<float>(r, 3) = sc * a.kf.tcw.at<float>(r);
+        }
+        std::vector<MapPoint*> ra(a.vp.size(), nullptr), rb(b.vp.size(), nullptr);
+        const int na = ref_fuse_sim3(a, Scw, 4.0f, ra);
+        ORBmatcher m(0.75f, true);
+        const int nb = m.Fuse(&b.kf, Scw, b.vp, 4.0f, rb);
+        int d = fuse_state_diff(a, b);
+        for (size_t i = 0; i < ra.size(); i++) d += label(a, ra[i]) != label(b, rb[i]);
+        CHECK(na == nb && na > 100 && d == 0, "Fuse(pKF, Scw, vpPoints) : %d vs reference loop %d, %d state diffs", nb, na, d);
+    }
 }
 
 int main() {
@@ -587,6 +791,7 @@ int main() {
         for (std::thread& t : th) t.join();
         CHECK(bad == 0 && calls == 5 * iters, "concurrent drop-ins: %d of %d calls differ", (int)bad, (int)calls);
     }
+    test_fuse(K[2], D[2], ext, W, H);
     // DescriptorDistance (ORBmatcher.cc:1647-1663)
     int dd = 0;
     for (int i = 0; i + 1 < kf1.N; i += 17)

@@ -170,3 +170,37 @@ def sim3_scene(seed):
         m, desc=flip_bits(rng, d[src], 25), pos=Xw, normal=nrm.astype(np.float32), min_dist=mind, max_dist=maxd,
         bad=(rng.random(m) < 0.05), skip=(rng.random(m) < 0.1))
     return F, Scw, mps
+
+
+def inv_level_sigma2(scale):
+    """mvInvLevelSigma2 = 1.0f / (mvScaleFactor^2) in float (ORBextractor.cc:416-424, Frame.cc)."""
+    s = np.asarray(scale, np.float32)
+    return (np.float32(1.0) / (s * s)).astype(np.float32)
+
+
+def fuse_scene(seed, stereo=True):
+    """Fuse(pKF, vpMapPoints, th) (LocalMapping::SearchInNeighbors): MapPoints of a neighbour keyframe
+    projected into pKF, 3-D noise so that part of them fail the reprojection-error (chi2) test."""
+    rng = np.random.default_rng(seed)
+    F, k, d, scale = make_frame(rng, seed % 5, 17 + seed, stereo, occupied_frac=0.0)
+    R, t = rot(rng, 3.0), rng.normal(0, 0.05, 3)
+    Tcw = pose(R, t)
+    Ow = (-(R.T @ t)).astype(np.float32)
+    src = pick_sources(rng, F.n, int(F.n * 0.9))
+    m = len(src)
+    noise = np.where(rng.random(m)[:, None] < 0.3, 0.02, 0.002)
+    Xw = (backproject(rng, k, src, Tcw) + rng.normal(0, 1, (m, 3)) * noise).astype(np.float32)
+    nrm = Xw - Ow
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    nrm[rng.random(m) < 0.05] *= -1
+    mind, maxd = dist_bounds(rng, Xw, Tcw, k["octave"][src])
+    mps = orbamd.MapPoints(
+        m, desc=flip_bits(rng, d[src], 30), pos=Xw, normal=nrm.astype(np.float32), min_dist=mind, max_dist=maxd,
+        bad=(rng.random(m) < 0.05), skip=(rng.random(m) < 0.1))
+    return F, Tcw, Ow, mps, inv_level_sigma2(scale)
+
+
+def fuse_sim3_scene(seed):
+    """Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (LoopClosing::SearchAndFuse)."""
+    F, Scw, mps = sim3_scene(seed)
+    return F, Scw, mps

@@ -82,3 +82,48 @@ def test_distinctive_descriptors_batch():
     np.testing.assert_array_equal(best, ref)
     for p in np.nonzero(ref >= 0)[0]:
         assert (chosen[p] == desc[off[p] + ref[p]]).all()
+
+
+def _same_fuse(g, o):
+    (ng, bg), (no, bo) = g, o
+    bad = np.nonzero(bg != bo)[0]
+    assert bad.size == 0, "best_idx differs at %s: gpu %s oracle %s" % (bad[:8], bg[bad[:8]], bo[bad[:8]])
+    assert ng == no, "nfused %d vs oracle %d" % (ng, no)
+    return ng
+
+
+@pytest.mark.parametrize("seed,stereo,th", [(3, True, 3.0), (4, False, 3.0), (5, True, 5.0), (13, False, 1.5)])
+def test_fuse(seed, stereo, th):
+    """ORBmatcher::Fuse(pKF, vpMapPoints, th) (ORBmatcher.cc:825-975): per-MapPoint fused keypoint."""
+    F, Tcw, Ow, mps, inv = ps.fuse_scene(seed, stereo)
+    g = orbamd.ORBmatcher(0.6, True).Fuse(F, Tcw, Ow, mps, th, inv)
+    o = oracle_py.fuse(F, Tcw, Ow, mps, th, inv)
+    assert _same_fuse(g, o) > mps.n // 4
+
+
+@pytest.mark.parametrize("seed,th", [(6, 4.0), (11, 10.0)])
+def test_fuse_sim3(seed, th):
+    """ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (ORBmatcher.cc:977-1100)."""
+    F, Scw, mps = ps.fuse_sim3_scene(seed)
+    g = orbamd.ORBmatcher(0.75, True).FuseSim3(F, Scw, mps, th)
+    o = oracle_py.fuse_sim3(F, Scw, mps, th)
+    assert _same_fuse(g, o) > mps.n // 4
+
+
+def test_fuse_edge_cases():
+    """no MapPoints; every MapPoint skipped; many MapPoints on one feature (no claims: all may fuse to it)."""
+    F, Tcw, Ow, mps, inv = ps.fuse_scene(7, True)
+    mt = orbamd.ORBmatcher(0.6, True)
+    empty = orbamd.MapPoints(0, desc=np.zeros((0, 32), np.uint8), pos=np.zeros((0, 3), np.float32),
+                             normal=np.zeros((0, 3), np.float32), min_dist=[], max_dist=[])
+    n, b = mt.Fuse(F, Tcw, Ow, empty, 3.0, inv)
+    assert n == 0 and b.size == 0
+    mps.skip = np.ones(mps.n, np.uint8)
+    n, b = mt.Fuse(F, Tcw, Ow, mps, 3.0, inv)
+    assert n == 0 and (b == -1).all()
+    mps.skip = np.zeros(mps.n, np.uint8)
+    k = 200
+    rep = orbamd.MapPoints(k, desc=np.repeat(mps.desc[:1], k, 0), pos=np.repeat(mps.pos[:1], k, 0),
+                           normal=np.repeat(mps.normal[:1], k, 0), min_dist=np.repeat(mps.min_dist[:1], k),
+                           max_dist=np.repeat(mps.max_dist[:1], k))
+    _same_fuse(mt.Fuse(F, Tcw, Ow, rep, 3.0, inv), oracle_py.fuse(F, Tcw, Ow, rep, 3.0, inv))

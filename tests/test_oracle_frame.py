@@ -242,6 +242,114 @@ def test_projection_variants_oracle_sanity():
     assert n > F.n // 8 and n == (m >= 0).sum()
 
 
+# ------------------------------------------------------------------ Fuse x2 (ORBmatcher.cc:825-1100)
+import ctypes as _C  # noqa: E402
+
+_libm = _C.CDLL("libm.so.6")
+_libm.logf.restype = _C.c_float
+_libm.logf.argtypes = [_C.c_float]
+
+
+def _gemm33_fast(A, x, c):
+    """cv::Mat A*x + c, 3x3 by 3x1 (OpenCV's small-matrix gemm: float products and sums, + c in double)."""
+    out = []
+    for i in range(3):
+        t0 = f32(f32(f32(A[i][0] * x[0]) + f32(A[i][1] * x[1])) + f32(A[i][2] * x[2]))
+        out.append(f32(float(t0) + float(c[i])))
+    return out
+
+
+def _norm3(v):
+    return f32(np.sqrt(sum(float(a) * float(a) for a in v)))
+
+
+def _dot3(a, b):
+    return sum(float(x) * float(y) for x, y in zip(a, b))
+
+
+def _predict_scale(max_dist, d, F):
+    """MapPoint::PredictScale (MapPoint.cc:385-417), logf of the float ratio."""
+    ratio = f32(f32(max_dist) / f32(d))
+    n = int(np.ceil(f32(f32(_libm.logf(float(ratio))) / f32(F.log_scale_factor))))
+    return min(max(n, 0), len(F.scale_factors) - 1)
+
+
+def fuse_py(F, mp, th, R, t, Ow, inv=None, sim3=False):
+    """ORBmatcher::Fuse(pKF, vpMapPoints, th) (ORBmatcher.cc:825-975) or, with sim3, Fuse(pKF, Scw,
+    vpPoints, th, vpReplacePoint) (:977-1100): per MapPoint the bestIdx that the reference fuses."""
+    g = grid_py(F)
+    bits = np.unpackbits(F.desc, axis=1)
+    best = np.full(mp.n, -1, np.int32)
+    for i in range(mp.n):
+        if mp.skip[i] or mp.bad[i]:
+            continue
+        p = [f32(v) for v in mp.pos[i]]
+        pc = _gemm33_fast(R, p, t)
+        if pc[2] < f32(0):
+            continue
+        invz = f32(1.0 / float(pc[2])) if sim3 else f32(f32(1) / pc[2])
+        u = f32(f32(f32(F.fx) * f32(pc[0] * invz)) + f32(F.cx))
+        v = f32(f32(f32(F.fy) * f32(pc[1] * invz)) + f32(F.cy))
+        if not (u >= F.min_x and u < F.max_x and v >= F.min_y and v < F.max_y):
+            continue
+        ur = f32(u - f32(f32(F.bf) * invz))
+        PO = [f32(p[k] - f32(Ow[k])) for k in range(3)]
+        d3 = _norm3(PO)
+        if d3 < f32(f32(0.8) * f32(mp.min_dist[i])) or d3 > f32(f32(1.2) * f32(mp.max_dist[i])):
+            continue
+        if _dot3(PO, mp.normal[i]) < 0.5 * float(d3):
+            continue
+        lvl = _predict_scale(mp.max_dist[i], d3, F)
+        rad = f32(f32(th) * f32(F.scale_factors[lvl]))
+        qb = np.unpackbits(mp.desc[i])
+        bd, bi = 1 << 30, -1
+        for idx in area_py(F, g, u, v, rad):
+            kl = int(F.octave[idx])
+            if kl < lvl - 1 or kl > lvl:
+                continue
+            if not sim3:
+                ex, ey = f32(u - F.x[idx]), f32(v - F.y[idx])
+                if F.uright is not None and F.uright[idx] >= 0:
+                    er = f32(ur - F.uright[idx])
+                    e2 = f32(f32(f32(ex * ex) + f32(ey * ey)) + f32(er * er))
+                    if float(f32(e2 * inv[kl])) > 7.8:
+                        continue
+                else:
+                    e2 = f32(f32(ex * ex) + f32(ey * ey))
+                    if float(f32(e2 * inv[kl])) > 5.99:
+                        continue
+            dist = int(np.count_nonzero(bits[idx] != qb))
+            if dist < bd:
+                bd, bi = dist, idx
+        if bd <= 50:
+            best[i] = bi
+    return int((best >= 0).sum()), best
+
+
+@pytest.mark.parametrize("seed,stereo,th", [(3, True, 3.0), (4, False, 3.0), (5, True, 5.0)])
+def test_fuse_oracle_matches_restatement(seed, stereo, th):
+    F, Tcw, Ow, mps, inv = ps.fuse_scene(seed, stereo)
+    n, b = oracle_py.fuse(F, Tcw, Ow, mps, th, inv)
+    R = [[f32(Tcw[r][c]) for c in range(3)] for r in range(3)]
+    t = [f32(Tcw[r][3]) for r in range(3)]
+    n2, b2 = fuse_py(F, mps, th, R, t, Ow, inv)
+    assert n == n2 and n > mps.n // 4
+    np.testing.assert_array_equal(b, b2)
+
+
+def test_fuse_sim3_oracle_matches_restatement():
+    F, Scw, mps = ps.fuse_sim3_scene(6)
+    n, b = oracle_py.fuse_sim3(F, Scw, mps, 4.0)
+    scw = f32(np.sqrt(sum(float(Scw[0][c]) * float(Scw[0][c]) for c in range(3))))
+    inv = f32(1.0 / float(scw))
+    R = [[f32(Scw[r][c] * inv) for c in range(3)] for r in range(3)]
+    t = [f32(Scw[r][3] * inv) for r in range(3)]
+    Ow = [f32(-sum(float(R[k][i]) * float(t[k]) for k in range(3))) for i in range(3)]
+    n2, b2 = fuse_py(F, mps, 4.0, R, t, Ow, sim3=True)
+    assert n == n2 and n > mps.n // 4
+    np.testing.assert_array_equal(b, b2)
+
+
 # ------------------------------------------------------------------ ComputeDistinctiveDescriptors
 def distinctive_scene(seed, big=False):
     rng = np.random.default_rng(seed)
