@@ -240,6 +240,31 @@ def bench_projection(reps):
             "nmatches": int(n), "cpu_threads": 1}
 
 
+def bench_fuse(reps):
+    """ORBmatcher::Fuse(pKF, vpMapPoints, th) (ORBmatcher.cc:825-975) per call: the device search
+    (host prologue + one H2D, three kernels, one D2H) vs the oracle's search loop (the map updates that
+    follow are host bookkeeping in both)."""
+    import orbamd
+    import oracle_py
+    import proj_scenes as ps
+    F, Tcw, Ow, mps, inv = ps.fuse_scene(3, True)
+    mt = orbamd.ORBmatcher(0.6, True)
+    for _ in range(3):
+        mt.Fuse(F, Tcw, Ow, mps, 3.0, inv)
+    t = time.perf_counter()
+    for _ in range(reps):
+        n, _b = mt.Fuse(F, Tcw, Ow, mps, 3.0, inv)
+    g = (time.perf_counter() - t) / reps
+    t = time.perf_counter()
+    for _ in range(reps):
+        oracle_py.fuse(F, Tcw, Ow, mps, 3.0, inv)
+    c = (time.perf_counter() - t) / reps
+    return {"row": "fuse", "workload": "Fuse(pKF, vpMapPoints, 3) (LocalMapping::SearchInNeighbors), 640x480 keyframe, "
+            "%d features, %d MapPoints" % (F.n, mps.n),
+            "gpu_host_api_ms_per_call": round(g * 1e3, 4), "cpu_oracle_ms_per_call": round(c * 1e3, 4),
+            "nfused": int(n), "cpu_threads": 1}
+
+
 def bench_distinctive(torch, reps):
     import orbamd
     import oracle_py
@@ -329,7 +354,7 @@ def main():
     steps = int(os.environ.get("BENCH_ROWS_STEPS", "10"))
     only = os.environ.get("BENCH_ROWS_ONLY")
     rows = {"extract_host": lambda: bench_extract_host(100), "matcher_host": lambda: bench_matcher_host(100),
-            "stereo": lambda: bench_stereo(torch, steps), "projection": lambda: bench_projection(50),
+            "stereo": lambda: bench_stereo(torch, steps), "projection": lambda: bench_projection(50), "fuse": lambda: bench_fuse(50),
             "distinctive": lambda: bench_distinctive(torch, 10), "bow": lambda: bench_bow(torch, 10),
             "tri_nodes": lambda: bench_tri_nodes(torch, 10)}
     for name, fn in rows.items():
