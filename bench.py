@@ -35,7 +35,7 @@ sys.path.insert(0, os.path.join(ROOT, "cooperative-orb-slam_amd"))
 
 VALU_PEAK_GINST = 1228.8  # 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU op (G wave-instr/s)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA, 2x the 2.5 PF dense bf16 rate (MI355X_MICROARCH.md "Matrix cores")
+FP4_MFMA_PEAK_TOPS = 10000.0  # dense fp4 (MX-scaled f8f6f4) MFMA, 4x the 2.5 PF dense bf16 rate (MI355X_MICROARCH.md "Matrix cores")
 
 CONFIGS = {
     "c2": dict(W=640, H=480, nfeatures=1000, name="C2: synthetic 640x480 uint8, nfeatures 1000"),
@@ -151,8 +151,8 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
     ap.add_argument("--batch", type=int, default=1024, help="frames per step per GPU")
     ap.add_argument("--pipes", type=int, default=4,
@@ -240,7 +240,12 @@ def main():
         torch.cuda.synchronize()
         t_start = time.perf_counter()
         for i in range(nsteps):
-            sched.step(evs[i], xevs[i], first=i == 0)
+            # the timed pass records only the dominant kernel's event pairs (inside the graphs); the matcher /
+            # exchange split comes from the untimed stage pass
+            if timed:
+                sched.step(first=i == 0)
+            else:
+                sched.step(evs[i], xevs[i], first=i == 0)
         torch.cuda.synchronize()
         if timed and world > 1:
             dist.barrier()
@@ -256,6 +261,8 @@ def main():
                 acc[i] += ms[i]
             ncalls += nc.value
         st = {k: acc[i] / max(ncalls, 1) for i, k in enumerate(stages) if (mask >> i) & 1}
+        if timed:
+            return elapsed, st
         st["match"] = sum(e[p][0].elapsed_time(e[p][1]) for e in evs for p in range(P)) / (nsteps * P)
         if not args.no_exchange:
             st["exchange"] = sum(x[0].elapsed_time(x[1]) for x in xevs) / nsteps
@@ -366,7 +373,8 @@ def main():
         else:
             roof = {"bound": "hbm", "kernel": dom, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": hbm["frac"], "traffic": traffic, "launch_ms": round(dom_ms, 4), "hbm": hbm}
-        # the matcher on the int8 matrix cores: algorithmic ops = n1*n2 distances x 256 bits x 2 per pair
+        # the matcher on the matrix cores (fp4 +-1 operands, v_mfma_scale_f32_32x32x64_f8f6f4): algorithmic ops =
+        # n1*n2 distances x 256 bits x 2 per pair
         m_ms = stage_ms.get("match", 0.0)
         m_tops = nkp * nkp * 512 * sub / (m_ms * 1e-3) / 1e12 if m_ms > 0 else 0.0
         result = {
@@ -395,7 +403,7 @@ def main():
             "device_errors": err_msg,
             "roofline": roof,
             "match_roofline": {"bound": "mfma", "kernel": "k_tri_mfma", "achieved": round(m_tops, 2),
-                               "peak": I8_MFMA_PEAK_TOPS, "unit": "int8 TOPS", "frac": round(m_tops / I8_MFMA_PEAK_TOPS, 4),
+                               "peak": FP4_MFMA_PEAK_TOPS, "unit": "fp4 TOPS", "frac": round(m_tops / FP4_MFMA_PEAK_TOPS, 4),
                                "launch_ms": round(m_ms, 4)},
             "pipeline_hbm": {"bytes_per_frame": b_frame, "achieved_GBs": round(b_frame * value / world / 1e9, 2),
                              "frac": round(b_frame * value / world / 1e9 / HBM_PEAK_GBS, 5)},

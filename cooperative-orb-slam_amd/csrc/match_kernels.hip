@@ -160,7 +160,9 @@ __device__ __forceinline__ void tri_bf_body(const PairSrc& s, const MatchGeom& g
 }
 
 /* ----------------------------------------------------------------------------------- */
-/* MFMA form of the BF SearchForTriangulation scan.                                       */
+/* MFMA form of the BF SearchForTriangulation scan (this i8 form with ORBX_MATCH_FP4=0;    */
+/* the default fp4 form, tri_mfma_body_fp4 below, takes both operands as +-1 on the        */
+/* MX-scaled f8f6f4 instruction at K = 64 and the same selection).                        */
 /*                                                                                       */
 /* Hamming distance as an int8 GEMM: with candidate bits a in {0,1} and query bits mapped  */
 /* to b' = 2b-1 in {-1,+1},  sum_k a_k b'_k = 2|a&b| - |a|, so                             */
@@ -187,6 +189,26 @@ __device__ __forceinline__ uint32_t spread_pm1(uint32_t nib) {  // 4 bits -> 4 b
     return ~(spread01(nib) * 0xFEu);
 }
 
+/* fp4 form: both operands as +-1 (e2m1 nibbles: +1.0 = 0x2, -1.0 = 0xA, block scale 2^0), so the  */
+/* 32x32x64 product gives dot' = sum (2a-1)(2b-1) = 256 - 2 D over 256 bits in 4 instructions    */
+/* (the i8 form needs 8), exact in the f32 accumulator. 8 descriptor bits -> one dword of 8       */
+/* nibbles: nibble 2i = bit i, nibble 2i+1 = bit 4+i (any fixed order serves: both operands use */
+/* it, so the k order inside an instruction is irrelevant). The sign bit (nibble bit 3) is set   */
+/* for a clear descriptor bit: spread of the inverted nibbles by one multiply each.             */
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ uint32_t fp4_pm1_byte(uint32_t nb) {  // nb = the INVERTED byte in bits 0..7
+    const uint32_t lo = nb & 15u, hi = (nb >> 4) & 15u;
+    return ((hi * 0x10204080u) & 0x80808080u) | (((lo * 0x01020408u) & 0x08080808u) | 0x22222222u);
+}
+__device__ __forceinline__ v4i fp4_pm1_dword(uint32_t w) {  // 32 descriptor bits -> 128 bits of fp4
+    const uint32_t n = ~w;
+    return (v4i){(int)fp4_pm1_byte(n), (int)fp4_pm1_byte(n >> 8), (int)fp4_pm1_byte(n >> 16), (int)fp4_pm1_byte(n >> 24)};
+}
+__device__ __forceinline__ v8i fp4_operand(v4i a) {  // fp4 reads only the low 4 registers of an operand
+    return __builtin_shufflevector(a, a, 0, 1, 2, 3, -1, -1, -1, -1);
+}
+
 constexpr int kMfChunk = 64;  // candidates staged per step (two 32-row tiles)
 #ifndef ORBX_MATCH_STOP
 #define ORBX_MATCH_STOP 0  // phase-cost experiment only (tools/exp_phases.sh): >0 cuts k_tri_mfma short (results invalid)
@@ -199,6 +221,10 @@ constexpr int kMfWaves = ORBX_MATCH_WAVES;
 #ifndef ORBX_MATCH_PACKED_MAX
 #define ORBX_MATCH_PACKED_MAX 1  // selection by one packed (dot, row) maximum per tile (0: threshold pass + key pass)
 #endif
+#ifndef ORBX_MATCH_FP4
+#define ORBX_MATCH_FP4 1  // 1: fp4 (e2m1) +-1 operands on v_mfma_scale_f32_32x32x64_f8f6f4 (K = 64); 0: the i8 form
+#endif
+constexpr bool kMfFp4 = ORBX_MATCH_FP4 != 0;
 constexpr int kMfThreads = 64 * kMfWaves;
 static_assert(kMfWaves == 4 || kMfWaves == 8 || kMfWaves == 16, "ORBX_MATCH_WAVES: 4, 8 or 16");
 // expansion units: 16 descriptor bits of one candidate (one half h of one 32-bit step); a chunk has
@@ -360,6 +386,123 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
     }
 }
 
+/* fp4 form of tri_mfma_body (same roles and selection): per 64-candidate chunk each */
+/* thread expands 2 descriptor dwords of one candidate (8 KB of fragments in LDS instead of 16),  */
+/* each wave runs 4 MFMAs per 32-candidate tile instead of 8, and the packed selection key is the */
+/* f32 accumulator's bit pattern (dot' is an even integer <= 256: its low 14 mantissa bits are     */
+/* zero) OR the tile row, whose signed maximum is the first candidate of maximum dot' = minimum D  */
+/* with ties to the later row, as the i8 form's (dot << 16 | row).                                */
+__device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
+                                                  int32_t* __restrict__ nmatch) {
+    static_assert(kMfThreads == 256, "fp4 expansion roles assume 4 waves (2 dwords per thread)");
+    __shared__ v4i s_frag[2][4][64];  // [tile][step][lane] candidate fragments (fp4 +-1)
+    __shared__ float s_x[kMfChunk], s_y[kMfChunk];
+    __shared__ int s_oct[kMfChunk], s_ok[kMfChunk];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int qblk = blockIdx.x * (32 * kMfWaves);
+    if (qblk >= s.n1) return;  // block-uniform
+    const int h = lane >> 5;
+    const int qi = qblk + wave * 32 + (lane & 31);
+    const bool qon = qi < s.n1;
+    // query fragments: step st covers descriptor bits 64 st .. 64 st + 63, lane half h dword 2 st + h
+    v4i bq[4];
+    float la = 0.f, lb = 0.f, lc = 0.f;
+    {
+        const int qc = qon ? qi : 0;
+        const uint4* qd = (const uint4*)(s.desc1 + (long long)qc * 32);
+        const uint4 d0 = qd[0], d1 = qd[1];
+        const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int st = 0; st < 4; st++) bq[st] = fp4_pm1_dword(h ? dw[2 * st + 1] : dw[2 * st]);
+        const orbx_kp k1 = s.kps1[qc];
+        epi_line(g, k1.x, k1.y, &la, &lb, &lc);
+    }
+    uint32_t best = 0xFFFFFFFFu;
+    // expansion role: candidate ec of the chunk, descriptor dwords ed, ed + 1 (= step ed / 2, halves 0, 1)
+    const int ec = tid >> 2, ed = (tid & 3) * 2;
+    auto load_chunk = [&](int cb, uint2& d, orbx_kp& k2) {
+        const int c = min(cb + ec, s.n2 - 1);
+        d = *(const uint2*)(s.desc2 + (long long)c * 32 + 4 * ed);
+        k2 = s.kps2[min(cb + (tid & (kMfChunk - 1)), s.n2 - 1)];
+    };
+    uint2 pd;
+    orbx_kp pk;
+    load_chunk(0, pd, pk);
+    for (int cb = 0; cb < s.n2; cb += kMfChunk) {
+        {
+            const bool on = cb + ec < s.n2;
+            const int tile = ec >> 5, r = ec & 31;
+            s_frag[tile][ed >> 1][r] = fp4_pm1_dword(on ? pd.x : 0u);
+            s_frag[tile][ed >> 1][32 + r] = fp4_pm1_dword(on ? pd.y : 0u);
+            if (tid < kMfChunk) {
+                const bool on2 = cb + tid < s.n2;
+                s_x[tid] = pk.x;
+                s_y[tid] = pk.y;
+                s_oct[tid] = pk.octave;
+                s_ok[tid] = on2 && !near_epipole(g, pk.x, pk.y, pk.octave);
+            }
+        }
+        __syncthreads();
+        if (cb + kMfChunk < s.n2) load_chunk(cb + kMfChunk, pd, pk);
+#if ORBX_MATCH_STOP == 1
+        best ^= (uint32_t)s_frag[lane & 1][lane & 3][lane].x;  // staging + expansion only
+        __syncthreads();
+        continue;
+#endif
+        v16f acc0 = (v16f)0.f, acc1 = (v16f)0.f;
+#pragma unroll
+        for (int st = 0; st < 4; st++) {
+            // cbsz = blgp = 4: fp4 (e2m1) A and B; E8M0 scales 127 = 2^0
+            acc0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_operand(s_frag[0][st][lane]), fp4_operand(bq[st]),
+                                                                   acc0, 4, 4, 0, 127, 0, 127);
+            acc1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_operand(s_frag[1][st][lane]), fp4_operand(bq[st]),
+                                                                   acc1, 4, 4, 0, 127, 0, 127);
+        }
+#if ORBX_MATCH_STOP == 2
+        best ^= (uint32_t)__float_as_int(acc0[lane & 15] + acc1[(lane + 3) & 15]);  // + MFMA, no selection
+        __syncthreads();
+        continue;
+#endif
+#pragma unroll
+        for (int tile = 0; tile < 2; tile++) {
+            const v16f acc = tile ? acc1 : acc0;
+            // key = D << 16 | (65535 - idx2) with D = (256 - dot') / 2 and idx2 = cb + 32 tile + 4 h + row
+            const uint32_t kb = 65535u - (uint32_t)(cb + 32 * tile + 4 * h);
+            auto pk = [&](int rg) { return __float_as_int(acc[rg]) | ((rg & 3) + 8 * (rg >> 2)); };
+            auto key = [&](int p) {
+                const float dp = __int_as_float(p & ~31);
+                return ((uint32_t)(int)(256.f - dp) >> 1 << 16) + kb - (uint32_t)(p & 31);
+            };
+            int pmax = pk(0);
+#pragma unroll
+            for (int rg = 1; rg < 16; rg++) pmax = max(pmax, pk(rg));
+            uint32_t km = key(pmax);
+            while (km < best && (km >> 16) <= 50u) {  // TH_LOW (ORBmatcher.cc:715)
+                const int jl = (int)(65535u - (km & 0xFFFFu)) - cb;
+                if (s_ok[jl] && epi_ok(la, lb, lc, s_x[jl], s_y[jl], g.th384[s_oct[jl]])) {
+                    best = km;
+                    break;
+                }
+                // next key of the lane = largest packed value below the rejected one (rows are distinct);
+                // a negative dot' (D > 128) ends the walk through the threshold test
+                const int cur = pmax;
+                int nx = INT_MIN;
+#pragma unroll
+                for (int rg = 0; rg < 16; rg++) nx = pk(rg) < cur ? max(nx, pk(rg)) : nx;
+                pmax = nx;
+                km = nx == INT_MIN ? 0xFFFFFFFFu : key(nx);
+            }
+        }
+        __syncthreads();
+    }
+    best = min(best, (uint32_t)__shfl_xor((int)best, 32, 64));
+    if (qon && h == 0) {
+        const int idx2 = (best >> 16) <= 50u ? (int)(65535u - (best & 0xFFFFu)) : -1;
+        out[qi] = idx2;
+        if (idx2 >= 0) atomicAdd(nmatch, 1);
+    }
+}
+
 __global__ __launch_bounds__(kMfThreads) void k_tri_mfma(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
                                                   const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
                                                   const int32_t* __restrict__ counts, int kp_stride, MatchGeom g,
@@ -369,7 +512,11 @@ __global__ __launch_bounds__(kMfThreads) void k_tri_mfma(const int32_t* __restri
     PairSrc s;
     s.kps1 = kps + (long long)f1 * kp_stride; s.desc1 = desc + (long long)f1 * kp_stride * 32; s.n1 = counts[f1];
     s.kps2 = kps + (long long)f2 * kp_stride; s.desc2 = desc + (long long)f2 * kp_stride * 32; s.n2 = counts[f2];
+#if ORBX_MATCH_FP4
+    tri_mfma_body_fp4(s, g, match12 + (long long)p * kp_stride, nmatches + p);
+#else
     tri_mfma_body(s, g, match12 + (long long)p * kp_stride, nmatches + p);
+#endif
 }
 
 template <int SPLIT>
