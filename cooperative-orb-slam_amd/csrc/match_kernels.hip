@@ -215,7 +215,7 @@ constexpr int kMfChunk = 64;  // candidates staged per step (two 32-row tiles)
 #endif
 
 #ifndef ORBX_MATCH_WAVES
-#define ORBX_MATCH_WAVES 4  // query waves per workgroup (32 queries each); they share each chunk's expansion
+#define ORBX_MATCH_WAVES 8  // query waves per workgroup (32 queries each); they share each chunk's expansion
 #endif
 constexpr int kMfWaves = ORBX_MATCH_WAVES;
 #ifndef ORBX_MATCH_PACKED_MAX
@@ -394,7 +394,8 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
 /* with ties to the later row, as the i8 form's (dot << 16 | row).                                */
 __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
                                                   int32_t* __restrict__ nmatch) {
-    static_assert(kMfThreads == 256, "fp4 expansion roles assume 4 waves (2 dwords per thread)");
+    static_assert(kMfWaves == 4 || kMfWaves == 8, "fp4 expansion roles: 4 waves (2 dwords per thread) or 8 (1)");
+    constexpr int kDw = 512 / kMfThreads;  // descriptor dwords expanded per thread and chunk
     __shared__ v4i s_frag[2][4][64];  // [tile][step][lane] candidate fragments (fp4 +-1)
     __shared__ float s_x[kMfChunk], s_y[kMfChunk];
     __shared__ int s_oct[kMfChunk], s_ok[kMfChunk];
@@ -418,22 +419,25 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
         epi_line(g, k1.x, k1.y, &la, &lb, &lc);
     }
     uint32_t best = 0xFFFFFFFFu;
-    // expansion role: candidate ec of the chunk, descriptor dwords ed, ed + 1 (= step ed / 2, halves 0, 1)
-    const int ec = tid >> 2, ed = (tid & 3) * 2;
-    auto load_chunk = [&](int cb, uint2& d, orbx_kp& k2) {
+    // expansion role: candidate ec of the chunk, descriptor dwords ed .. ed + kDw - 1 (dword d = step d / 2,
+    // half d % 2)
+    const int ec = tid / (8 / kDw), ed = (tid % (8 / kDw)) * kDw;
+    struct DwT { uint32_t w[kDw]; };
+    auto load_chunk = [&](int cb, DwT& d, orbx_kp& k2) {
         const int c = min(cb + ec, s.n2 - 1);
-        d = *(const uint2*)(s.desc2 + (long long)c * 32 + 4 * ed);
+        d = *(const DwT*)(s.desc2 + (long long)c * 32 + 4 * ed);
         k2 = s.kps2[min(cb + (tid & (kMfChunk - 1)), s.n2 - 1)];
     };
-    uint2 pd;
+    DwT pd;
     orbx_kp pk;
     load_chunk(0, pd, pk);
     for (int cb = 0; cb < s.n2; cb += kMfChunk) {
         {
             const bool on = cb + ec < s.n2;
             const int tile = ec >> 5, r = ec & 31;
-            s_frag[tile][ed >> 1][r] = fp4_pm1_dword(on ? pd.x : 0u);
-            s_frag[tile][ed >> 1][32 + r] = fp4_pm1_dword(on ? pd.y : 0u);
+#pragma unroll
+            for (int k = 0; k < kDw; k++)
+                s_frag[tile][(ed + k) >> 1][32 * ((ed + k) & 1) + r] = fp4_pm1_dword(on ? pd.w[k] : 0u);
             if (tid < kMfChunk) {
                 const bool on2 = cb + tid < s.n2;
                 s_x[tid] = pk.x;
