@@ -229,11 +229,17 @@ struct PyrColGroup {
 };
 static_assert(sizeof(PyrColGroup) == 48, "PyrColGroup layout");
 
-template <int U, int NT>
+/* FLAT (ORBX_PYR_FLAT): items = (row, column group) pairs of the level numbered row-major and dealt
+ * to the threads round-robin, so every thread has an item in every pass but the last (the fixed
+ * column per thread leaves NT - (NT / gw) * gw threads idle: 22 % of a 512-thread workgroup at
+ * 640x480's level 1); the level's column-group table is staged in LDS beside the row table and read
+ * per item. Every output byte is computed by the same operations either way. */
+template <int U, int NT, bool FLAT>
 __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
                                                          int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
                                                          const LevelDesc* __restrict__ levels,
-                                                         const int* __restrict__ ptab, const int2* __restrict__ bands) {
+                                                         const int* __restrict__ ptab, const int2* __restrict__ bands,
+                                                         int rt_cap) {
     // the current level's row table (this band's rows); sized at launch for the longest band range
     // (rows x 16 B: 6.4 KB at 640x480 with one band) instead of kPyrMaxRows, so the LDS the long-lived
     // pyramid workgroup holds stays free for the other graphs' FAST / describe workgroups beside it
@@ -254,6 +260,82 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
         const int4* rt = (const int4*)(ptab + lv.rt_off);
         for (int i = tid; i < hi - lo; i += NT) s_rt[i] = rt[lo + i];
         const int gw = (lv.w + 3) >> 2;
+        if constexpr (FLAT) {
+            // gw x 3 int4: sel[4], alpha[4], (W, clamp dword, -, -); staged in LDS (ORBX_PYR_FLAT=1) or read
+            // through the L1 (2: the workgroup's LDS stays the row table alone)
+            const int4* cgt = (const int4*)(ptab + lv.cg_off);
+            const int4* s_cg = cgt;
+            if (kPyrFlatLds) {
+                int4* c = s_rt + rt_cap;
+                for (int i = tid; i < 3 * gw; i += NT) c[i] = cgt[i];
+                s_cg = c;
+            }
+            __syncthreads();
+            const int n = (hi - lo) * gw;
+            // row = item / gw by a multiply-high: exact for item * (M * gw - 2^32) < 2^32 (items < 2^21, gw < 2^10)
+            const uint32_t M = (uint32_t)((0x100000000ull + gw - 1) / gw);
+            for (int i0 = tid; i0 < n; i0 += U * NT) {
+                uint32_t w[U][2][3];
+                int4 rr[U];
+                int4 cs[U], ca[U];
+                int xg[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int it = min(i0 + u * NT, n - 1);
+                    const int ry = (int)__umulhi((uint32_t)it, M);
+                    xg[u] = it - ry * gw;
+                    rr[u] = s_rt[ry];
+                    cs[u] = s_cg[3 * xg[u]];
+                    ca[u] = s_cg[3 * xg[u] + 1];
+                    const int2 wc = *(const int2*)&s_cg[3 * xg[u] + 2];
+                    const int A = wc.x & ~3;
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const int r = q ? rr[u].y : rr[u].x;
+                        const unsigned off = (unsigned)(r * sp + A);
+                        const uint2 lo2 = *(const uint2*)(src + off);
+                        w[u][q][0] = lo2.x;
+                        w[u][q][1] = lo2.y;
+                        w[u][q][2] = *(const uint32_t*)(src + min(off + 8u, (unsigned)(r * sp + wc.y)));
+                    }
+                    cs[u].w = (cs[u].w & 0x0F0F0F0F) | ((wc.x & 3) << 4);  // keep k = W & 3 beside sel[3]
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int it = i0 + u * NT;
+                    if (it >= n) break;
+                    const int y = lo + (int)__umulhi((uint32_t)it, M);
+                    const int x0 = 4 * xg[u];
+                    const int k = (cs[u].w >> 4) & 3;
+                    const int sel[4] = {cs[u].x, cs[u].y, cs[u].z, cs[u].w & 0x0F0F0F0F};
+                    const int alpha[4] = {ca[u].x, ca[u].y, ca[u].z, ca[u].w};
+                    const short2 b = __builtin_bit_cast(short2, rr[u].z);
+                    int h[2][4];
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const uint32_t lw = __builtin_amdgcn_alignbyte(w[u][q][1], w[u][q][0], k);
+                        const uint32_t hw = __builtin_amdgcn_alignbyte(w[u][q][2], w[u][q][1], k);
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const uint32_t pr = __builtin_amdgcn_perm(hw, lw, sel[i]);
+                            h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
+                                                             __builtin_bit_cast(short2v, alpha[i]), 0, false);
+                        }
+                    }
+                    const bool tail = x0 + 3 >= lv.simd_end;
+                    uint32_t packed = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        int v = ((__mul24(h[0][i] >> 4, (int)b.x) >> 16) + (__mul24(h[1][i] >> 4, (int)b.y) >> 16) + 2) >> 2;
+                        if (tail && x0 + i >= lv.simd_end) v = (__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
+                        packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
+                    }
+                    *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         const int R = NT / gw;  // rows per pass
         const int ry = tid / gw, xg = tid - ry * gw;
         const PyrColGroup cg = ((const PyrColGroup*)(ptab + lv.cg_off))[min(xg, gw - 1)];
@@ -1694,12 +1776,14 @@ hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int p
     // keeps >= 2 rows per pass; a level 1 wider than 4 x 256 columns (C4's 1034) would leave half the
     // threads idle, so such geometries take 1024 threads
     const dim3 grid(nframes * kPyrBands);
+    // flat items: the row table and the widest level's column-group table (3 int4 per group) in LDS
+    const size_t lds = (size_t)max_rows * sizeof(int4) + (kPyrFlatLds ? (size_t)max_groups * 3 * sizeof(int4) : 0);
     if (max_groups <= kPyrThreads / 2)
-        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), grid, dim3(kPyrThreads),
-                           (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab, bands);
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads, kPyrFlat>), grid, dim3(kPyrThreads), lds, st, frames,
+                           fstride, pitch0, pyr, ep, levels, ptab, bands, max_rows);
     else
-        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), grid, dim3(kPyrThreadsMax),
-                           (size_t)max_rows * sizeof(int4), st, frames, fstride, pitch0, pyr, ep, levels, ptab, bands);
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax, kPyrFlat>), grid, dim3(kPyrThreadsMax), lds, st,
+                           frames, fstride, pitch0, pyr, ep, levels, ptab, bands, max_rows);
     return hipGetLastError();
 }
 

@@ -44,6 +44,11 @@ constexpr int kPyrU = ORBX_PYR_U;   // k_pyramid_frames: rows in flight per thre
 // whole-frame kernel accepts (>= column groups of every level)
 constexpr int kPyrThreads = ORBX_PYR_NT;
 constexpr int kPyrThreadsMax = 1024;
+#ifndef ORBX_PYR_FLAT
+#define ORBX_PYR_FLAT 0  // A/B knob: 1 = table in LDS, 2 = via L1 (both slower overlapped)
+#endif
+constexpr bool kPyrFlat = ORBX_PYR_FLAT != 0;  // k_pyramid_frames: (row, column group) items dealt round-robin
+constexpr bool kPyrFlatLds = ORBX_PYR_FLAT == 1;  // ... with the column-group table staged in LDS (2: read via L1)
 #ifndef ORBX_PYR_BANDS
 #define ORBX_PYR_BANDS 1
 #endif
