@@ -214,3 +214,60 @@ def test_search_by_bow_pairs_device(mode):
             total += no
     assert total > 0
     pipe.close()
+
+
+def _crafted_descriptors(rng, n1, n2):
+    """KF1 / KF2 descriptor rows that stress the MFMA selection: exact duplicates among the candidates
+    (distance ties: the later candidate wins, ORBmatcher.cc:719 `dist > bestDist` skips only larger
+    ones), candidates at Hamming distance exactly TH_LOW = 50 and 51 from a query (ORBmatcher.cc:715),
+    all-zero / all-one rows (D = 0 and 256: the extremes of the fp4 dot product), random rows."""
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+    d2 = rng.integers(0, 256, (n2, 32), dtype=np.uint8)
+    pat = rng.integers(0, 256, 32, dtype=np.uint8)
+    d2[::7] = pat                     # ties at D = 0 for the queries equal to pat, every 7th candidate
+    d1[::5] = pat
+    d1[1::11] = 0
+    d1[2::11] = 255
+    d2[3::13] = 0
+    d2[4::13] = 255
+    bits = np.unpackbits(pat)
+    for i, flips in ((3, 50), (8, 51)):   # a query pat^50 bits and one pat^51 bits, next to pat rows
+        b = bits.copy()
+        b[rng.choice(256, flips, replace=False)] ^= 1
+        d1[i] = np.packbits(b)
+    for j, flips in ((10, 50), (17, 49), (24, 51)):
+        b = bits.copy()
+        b[rng.choice(256, flips, replace=False)] ^= 1
+        d2[j] = np.packbits(b)
+    return d1, d2
+
+
+@pytest.mark.parametrize("W,H,nf", [(640, 480, 1000), (1241, 376, 2000)])
+@pytest.mark.parametrize("check_ori", [False, True])
+def test_batch_pairs_crafted_descriptors(W, H, nf, check_ori):
+    """k_tri_mfma on real keypoint geometry with crafted descriptors (ties, the TH_LOW boundary,
+    D = 0 / 256 extremes) vs the oracle's SearchForTriangulation, both pair directions."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(nf + check_ori)
+    (k1, _), (k2, _) = _frames_kf(3, 2, W=W, H=H, nf=nf)[0]
+    tabs = _frames_kf(3, 2, 1, W=W, H=H, nf=nf)[1]
+    d1, d2 = _crafted_descriptors(rng, len(k1), len(k2))
+    pipe = orbamd.device.BatchPipeline(torch, W, H, 2, nfeatures=nf, check_ori=check_ori)
+    assert k1.dtype.itemsize == 24 and max(len(k1), len(k2)) <= pipe.stride
+    kps = np.zeros((2, pipe.stride, 24), np.uint8)
+    desc = np.zeros((2, pipe.stride, 32), np.uint8)
+    for b, (k, d) in enumerate(((k1, d1), (k2, d2))):
+        kps[b, :len(k)] = np.frombuffer(k.tobytes(), np.uint8).reshape(len(k), 24)
+        desc[b, :len(k)] = d
+    pipe.kps.copy_(torch.from_numpy(kps.view(np.float32).reshape(2, pipe.stride, 6)))
+    pipe.desc.copy_(torch.from_numpy(desc))
+    pipe.counts.copy_(torch.tensor([len(k1), len(k2)], dtype=torch.int32))
+    pipe.match_pairs()
+    torch.cuda.synchronize()
+    mg = pipe.match.cpu().numpy()
+    v = (_view(k1, d1, tabs), _view(k2, d2, tabs))
+    for p, (a, b) in enumerate(((0, 1), (1, 0))):   # pair p = (frame p, frame p - 1 mod 2)
+        no, mo = oracle_py.search_for_triangulation(v[a], v[b], pipe.F12, pipe.ex, pipe.ey, False, check_ori)
+        np.testing.assert_array_equal(mg[p, :v[a].n], mo)
+        assert int(pipe.nmatch[p].item()) == no
+    pipe.close()
