@@ -356,8 +356,11 @@ def main():
         # one launch of the dominant kernel processes one graph's sub-batch (B / P frames)
         hbm_gbs = per_stage[dom] * sub / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and per_stage[dom] > 0 else 0.0
         traffic = valu_insts = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path) and args.config == "c2" and sub == 256:
+        # counter passes of this configuration (tools/prof_round.sh for c2, tools/pmc_config.sh for c3 / c4), taken
+        # at 256 frames per launch
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if args.config == "c2" else
+                                "pmc_traffic_%s.json" % args.config)
+        if os.path.exists(pmc_path) and sub == 256:
             try:
                 rec = json.load(open(pmc_path)).get(dom, {})
                 traffic = rec.get("hbm_bytes_per_launch")
