@@ -164,28 +164,41 @@ void oc_gauss7(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst, siz
     int32_t k[7];
     oc_gauss_kernel_q8(k);
     int* rows = (int*)malloc(sizeof(int) * (size_t)w * h);
+    /* the same sums as written per pixel with reflect101 on every tap, arranged so the compiler can
+     * vectorise them: reflected taps only for the 3 border columns on each side, contiguous inner loops */
+    const int xi0 = w < 3 ? w : 3, xi1 = w - 3 > xi0 ? w - 3 : xi0;  /* interior columns [xi0, xi1) */
     for (int y = 0; y < h; y++) {
         const uint8_t* S = src + (size_t)y * sstep;
+        int* R = rows + (size_t)y * w;
         for (int x = 0; x < w; x++) {
-            int s = 0;
-            for (int i = -3; i <= 3; i++) s += k[i + 3] * S[reflect101(x + i, w)];
-            rows[(size_t)y * w + x] = s;
+            if (x == xi0) x = xi1;  /* skip the interior (below) */
+            if (x >= w) break;
+            int sum = 0;
+            for (int i = -3; i <= 3; i++) sum += k[i + 3] * S[reflect101(x + i, w)];
+            R[x] = sum;
         }
+        for (int x = xi0; x < xi1; x++)
+            R[x] = k[0] * S[x - 3] + k[1] * S[x - 2] + k[2] * S[x - 1] + k[3] * S[x] + k[4] * S[x + 1] +
+                   k[5] * S[x + 2] + k[6] * S[x + 3];
     }
-    int vec_end = w & ~3;
+    const int vec_end = w & ~3;
     for (int y = 0; y < h; y++) {
         uint8_t* D = dst + (size_t)y * dstep;
+        const int* r0 = rows + (size_t)y * w;
+        const int* rp[3];
+        const int* rm[3];
+        for (int i = 1; i <= 3; i++) {
+            rp[i - 1] = rows + (size_t)reflect101(y + i, h) * w;
+            rm[i - 1] = rows + (size_t)reflect101(y - i, h) * w;
+        }
         for (int x = 0; x < w; x++) {
-            int s = k[3] * rows[(size_t)y * w + x];
-            for (int i = 1; i <= 3; i++)
-                s += k[3 + i] * (rows[(size_t)reflect101(y + i, h) * w + x] +
-                                 rows[(size_t)reflect101(y - i, h) * w + x]);
-            int v;
-            if (x < vec_end)
-                v = (int)lrintf((float)s * (1.0f / 65536.0f)); /* exact: s < 2^24 or saturates */
-            else
-                v = (s + (1 << 15)) >> 16;
-            D[x] = sat_u8(v);
+            const int sum = k[3] * r0[x] + k[4] * (rp[0][x] + rm[0][x]) + k[5] * (rp[1][x] + rm[1][x]) +
+                            k[6] * (rp[2][x] + rm[2][x]);
+            /* x < vec_end: the SSE2 path's float sum scaled by 2^-16 and rounded half to even
+             * (_mm_cvtps_epi32), exact for sum < 2^24 and saturating above, = the integer round half even
+             * below; the scalar tail (sum + 2^15) >> 16. sum >= 0 (non-negative taps and pixels). */
+            const int v = x < vec_end ? (sum + 0x7FFF + ((sum >> 16) & 1)) >> 16 : (sum + (1 << 15)) >> 16;
+            D[x] = (uint8_t)(v > 255 ? 255 : v);
         }
     }
     free(rows);
