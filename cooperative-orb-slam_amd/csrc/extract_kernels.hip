@@ -1554,12 +1554,14 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
     }
     // everything that depends only on the slot is issued before the table barrier
     constexpr int NT = 64 * kDescWaves;
-    PatPt my_pat[256 / NT];
-    int2 my_ic[256 / NT];
+    constexpr int kTab = (256 + NT - 1) / NT;  // table entries per thread (workgroups of more than 256 threads: 1)
+    PatPt my_pat[kTab];
+    int2 my_ic[kTab];
 #pragma unroll
-    for (int q = 0; q < 256 / NT; q++) {
-        if (!kDescPatGlobal) my_pat[q] = kPatternF.t[tid + q * NT];
-        my_ic[q] = ((const int2*)(ptab + ep.ic_off))[tid + q * NT];
+    for (int q = 0; q < kTab; q++) {
+        const int t = min(tid + q * NT, 255);
+        if (!kDescPatGlobal) my_pat[q] = kPatternF.t[t];
+        my_ic[q] = ((const int2*)(ptab + ep.ic_off))[t];
     }
     const int g = (blk * kDescWaves + wave) * 4 + sub;  // octree output slot of this lane group
     const int gc = min(g, ep.kp_per_frame - 1);
@@ -1570,8 +1572,9 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
 #pragma unroll
     for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;
 #pragma unroll
-    for (int q = 0; q < 256 / NT; q++) {
+    for (int q = 0; q < kTab; q++) {
         const int t = tid + q * NT;
+        if (t >= 256) break;
         if (!kDescPatGlobal) s_pat[(t & 15) * 16 + (t >> 4)] = my_pat[q];  // pair p at (p % 16) * 16 + p / 16
         s_ic[t] = my_ic[q];
     }
