@@ -478,11 +478,13 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
     const ExtractParams& ep = h->geo.ep;
     const size_t B = (size_t)h->max_batch;
     const void* before[7] = {h->pyr.p, h->blur.p, h->cellkey.p, h->cellcnt.p, h->lvkey.p, h->lvcnt.p, h->gscratch.p};
+    const void* err_before = h->err.p;
     if (h->pyr.ensure(B * ep.pyr_frame_bytes) || h->blur.ensure(B * ep.blur_frame_bytes) ||
         h->cellkey.ensure(B * ep.keys_per_frame * 4) || h->cellcnt.ensure(B * ep.ncells * 4) ||
         h->lvkey.ensure(B * ep.kp_per_frame * 4) || h->lvcnt.ensure((B * ep.L + kMaxLevels) * 4) ||
         h->gscratch.ensure(B * (size_t)ep.keys_per_frame * 8) || h->err.ensure(256))
         return ORBX_EDEVICE;
+    if (h->err.p != err_before && hipMemset(h->err.p, 0, 256) != hipSuccess) return ORBX_EDEVICE;  // sticky flag starts clear
     const void* after[7] = {h->pyr.p, h->blur.p, h->cellkey.p, h->cellcnt.p, h->lvkey.p, h->lvcnt.p, h->gscratch.p};
     if (memcmp(before, after, sizeof(before))) h->epoch++;
     if (h->geo.lds_bytes > 64 * 1024 && !h->lds_attr_set) {
@@ -545,8 +547,13 @@ static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstrid
  * only the input) beside the pyramid; ORBX_SCHED=serial runs everything on `st` (A/B only), and
  * ORBX_SCHED=serial_blur_first does so with the blur right after the pyramid.
  * With stage profiling on, everything runs in order on `st` between timing events. */
+#ifndef ORBX_ERR_STICKY
+#define ORBX_ERR_STICKY 1  // device batch path: error flag sticky until orbx_check_error (0: reset every call)
+#endif
+constexpr bool kErrSticky = ORBX_ERR_STICKY != 0;
 static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
-                       orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st) {
+                       orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st,
+                       bool reset_err = true) {
     Geometry& g = h->geo;
     const ExtractParams& ep = g.ep;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
@@ -559,7 +566,9 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     const bool split = !serial && sched == 1;
     const int ncell0 = split ? g.lv[0].ncells : 0;
     hipStream_t sd = serial ? st : h->side;
-    HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), st));
+    // the host-buffer paths report the flag per call; the device batch path leaves it sticky until
+    // orbx_check_error reads (and clears) it, so no fill kernel sits on the batch stream every call
+    if (reset_err || !kErrSticky) HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), st));
     if (split) {
         HIPR(hipEventRecord(h->ev_fork, st));
         HIPR(hipStreamWaitEvent(sd, h->ev_fork, 0));
@@ -679,6 +688,7 @@ int orbx_check_error(orbx_handle* h, void* stream) {
     int flag = 0;
     HIPR(hipMemcpyAsync(&flag, h->err.p, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
     HIPR(hipStreamSynchronize((hipStream_t)stream));
+    if (flag) HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), (hipStream_t)stream));  // read and clear
     return flag ? ORBX_EDEVICE : 0;
 }
 
@@ -742,7 +752,7 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
     if (rc) return rc;
     if (kp_stride < h->geo.ep.kp_per_frame) return ORBX_ECAPACITY;
     return run_extract(h, nframes, d_frames, (long long)frame_stride, (int)pitch, d_kps, d_desc, d_counts, kp_stride,
-                       (hipStream_t)stream);
+                       (hipStream_t)stream, false);
 }
 
 /* The captured host path: pinned H2D -> run_extract -> one pinned D2H of {count, error flag, K

@@ -84,8 +84,9 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
                               orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
                               int kp_stride, void* stream);
 
-/* Waits for `stream` and reports a device-side consistency failure of the last batched
- * extraction (octree capacity or root-index overflow): 0 = OK, ORBX_EDEVICE otherwise. */
+/* Waits for `stream` and reports a device-side consistency failure (octree capacity or
+ * root-index overflow) of any batched extraction since the previous check: 0 = OK,
+ * ORBX_EDEVICE otherwise (the flag is then cleared). */
 int orbx_check_error(orbx_handle* h, void* stream);
 
 /* public ORBextractor::mvImagePyramid (ORBextractor.h:85), materialised lazily: copies
