@@ -1680,6 +1680,10 @@ bool frame_view_ok(const orbm_frame_view* F) {
 }
 
 /* uploads the Frame side + queries, runs k_grid / k_proj_scan / k_proj_resolve, downloads */
+#ifndef ORBX_PROJ_DIRECT
+#define ORBX_PROJ_DIRECT 1  // Fuse: results written by the scan kernel (0: through k_proj_resolve)
+#endif
+constexpr bool kProjDirect = ORBX_PROJ_DIRECT != 0;
 int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb, int accept_th, int ratio,
                    float nnratio, int check_ori, int32_t* match, int* nmatches, const float* inv_sigma2 = nullptr,
                    int32_t* qres = nullptr) {
@@ -1720,6 +1724,10 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     c.ratio = ratio;
     c.nnratio = nnratio;
     c.check_ori = check_ori && F->angle;
+    // per-query results with nothing to arbitrate (Fuse): the scan writes them, no resolve wave
+    bool claims = false;
+    for (const ProjQuery& q : pb.q) claims |= (q.flags & kProjClaims) != 0;
+    c.direct = kProjDirect && qres && !ratio && !c.check_ori && !claims;
     c.grid_start = (int*)(base + o_gs);
     c.grid_idx = (uint16_t*)(base + o_gi);
     c.scan = (unsigned long long*)(base + o_scan);
@@ -1744,7 +1752,7 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
         memcpy(hp + o_qd, pb.qdesc.data(), 32 * nq);
     }
     HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, st));
-    HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st));
+    HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st, !c.direct));
     uint8_t* ho = hp + in_bytes;
     if (qres) {
         // per-query results (Fuse): res[2 qi] = the accepted feature or -1, reported at the query's src

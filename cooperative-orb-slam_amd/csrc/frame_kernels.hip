@@ -513,6 +513,13 @@ __global__ __launch_bounds__(256) void k_proj_scan(const ProjCall* __restrict__ 
             if (gl == t) v = top[t];
         c.scan[(long long)kProjTopK * qi + gl] = v;
         if (gl == 0) c.scan_cnt[qi] = ncand;
+        // Fuse: nothing claims, so the query's answer is its best key (occupied features are already
+        // excluded by the scan), accepted when bestDist <= the threshold -- what k_proj_resolve would write
+        if (c.direct && gl == 0) {
+            const bool acc = top[0] != kNoKey && (int)(top[0] >> 40) <= c.accept_th;
+            c.res[2 * qi] = acc ? (int)(top[0] & 0xffff) : -1;
+            c.res[2 * qi + 1] = 0;
+        }
     }
 }
 
@@ -715,10 +722,10 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
     if (lane == 0) *c.nmatches = nacc;
 }
 
-hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st) {
+hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st, bool resolve) {
     hipLaunchKernelGGL(k_grid, dim3(ncalls), dim3(1024), 0, st, d_calls);
     if (max_nq > 0) hipLaunchKernelGGL(k_proj_scan, dim3((max_nq + 15) / 16, ncalls), dim3(256), 0, st, d_calls);
-    hipLaunchKernelGGL(k_proj_resolve, dim3(ncalls), dim3(64), 0, st, d_calls);
+    if (resolve) hipLaunchKernelGGL(k_proj_resolve, dim3(ncalls), dim3(64), 0, st, d_calls);
     return hipGetLastError();
 }
 

@@ -77,6 +77,8 @@ struct ProjCall {
     float inv_sigma2[kMaxLevels];  // mvInvLevelSigma2 (kProjChi2 queries)
     int32_t* match;            // [n]
     int32_t* nmatches;
+    int direct;                // per-query results only, no claims / ratio / rotation (Fuse): k_proj_scan writes
+                               // res[] from its best key and k_proj_resolve is not launched
 };
 
 }  // namespace orbamd
