@@ -1823,7 +1823,10 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
                               int cell_hi, int nframes, hipStream_t st) {
     if (cell_hi <= cell_lo) return hipSuccess;
     dim3 grid((cell_hi - cell_lo + 3) / 4, nframes);
-    const size_t lds = 4 * (size_t)fast_wave_lds(RP, RH);
+#ifndef ORBX_FAST_LDS_MIN
+#define ORBX_FAST_LDS_MIN 0  // A/B knob: minimum LDS bytes per FAST workgroup (caps FAST's workgroups per CU)
+#endif
+    const size_t lds = std::max<size_t>(4 * (size_t)fast_wave_lds(RP, RH), ORBX_FAST_LDS_MIN);
 #define ORBX_FAST(MP, RPC)                                                                                        \
     hipLaunchKernelGGL((k_fast_cells2<MP, RPC>), grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, \
                        cells, cellkey, cellcnt, RP, RH, cell_lo, cell_hi)
