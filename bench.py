@@ -13,13 +13,21 @@ staggered extraction+match graphs (default 1024 frames as 4 graphs of 256).
 After the timed region the run checks itself: every graph's device error flags, then sampled
 frames (first / middle / last of every graph) with their match rows and the cross-agent matches,
 bit-compared against the CPU oracle (oracle/check_schedule.py, the checker); "bit_exact" in the
-JSON line, exit status 3 on a mismatch.
+JSON line, exit status 3 on a mismatch. The frames form a pool of --pool resident batches and
+consecutive steps process consecutive batches, so the last step's correct outputs differ from the
+step before: a stage that stopped launching fails the check ("stale_guard").
+
+Beside `value` (frames already in HBM) the "ingest" leg reports the rate with every step's frames
+uploaded from pinned host memory on a copy stream, overlapped with the previous step's compute
+(ORBextractor::operator() takes a host image, ORBextractor.cc:1043-1050).
 
 --config c2 (default, the BASELINE metric) | c3 (752x480, 1200 features) | c4 (1241x376, 2000
 features): the BASELINE configs 3 and 4 at their geometries (left images, same step).
 
 Launch (N>1): python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
               --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+(--dist at N=1 under torch.distributed.run: the same RCCL process group and out-of-place all-gather
+as N>1, with one rank.)
 Rank 0 prints ONE JSON line.
 """
 import argparse
@@ -148,6 +156,54 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000):
     return sum(count) / el, sum(count), el, per
 
 
+def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, dist):
+    """The schedule with every step's B frames uploaded from pinned host memory (the frame pool, batch
+    i mod pool at step i) on a copy stream into the device batch the step processes. Upload i waits for
+    step i-pool (the previous user of that device batch) and step i waits for upload i, so an upload
+    overlaps the previous step's compute. Returns frames/s over nsteps after `pool` warm-up steps and the
+    H2D rate achieved (W*H bytes per frame, max over ranks)."""
+    P, sub, dev = sched.P, sched.sub, sched.dev
+    host = [torch.from_numpy(frames_np[r * B:(r + 1) * B]).pin_memory() for r in range(pool)]
+    copy_st = torch.cuda.Stream(dev)
+    up = [torch.cuda.Event() for _ in range(pool)]
+    done = [[torch.cuda.Event() for _ in range(P)] for _ in range(pool)]
+    used = [False] * pool
+
+    def one(i):
+        r = i % pool
+        with torch.cuda.stream(copy_st):
+            if used[r]:
+                for e in done[r]:
+                    copy_st.wait_event(e)
+            for p in range(P):
+                sched.frames[r][p].copy_(host[r][p * sub:(p + 1) * sub], non_blocking=True)
+            up[r].record(copy_st)
+        sched.step(batch=r, wait=up[r], first=i == 0)
+        for p in range(P):
+            done[r][p].record(sched.streams[p])
+        used[r] = True
+
+    for i in range(pool):
+        one(i)
+    torch.cuda.synchronize()
+    if use_dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(nsteps):
+        one(pool + i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if use_dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    fps = world * B * nsteps / el
+    return {"frames_per_s": round(fps, 1), "per_gpu_frames_per_s": round(fps / world, 1),
+            "h2d_GBs_per_gpu": round(B * W * H * nsteps / el / 1e9, 2), "steps": nsteps, "seconds": round(el, 3),
+            "source": "pinned host memory, %d batches of %d frames uploaded round-robin (one batch per step), "
+                      "copy stream overlapped with the previous step's compute" % (pool, B)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -173,6 +229,12 @@ def main():
                     default="fast_cells", help="extraction kernel priced in `roofline` (timed live in the timed region)")
     ap.add_argument("--sustain", type=float, default=6.0,
                     help="seconds of the untimed sustained pass after the timed region (0: skip)")
+    ap.add_argument("--pool", type=int, default=2,
+                    help="resident batches of distinct frames; step k processes batch k mod pool (stale-output guard)")
+    ap.add_argument("--dist", action="store_true",
+                    help="use torch.distributed (RCCL) and the out-of-place all-gather even at world 1")
+    ap.add_argument("--ingest-steps", type=int, default=100,
+                    help="steps of the ingest leg (frames uploaded from pinned host memory each step; 0: skip)")
     ap.add_argument("--stagger", choices=("each", "once", "none"), default="each",
                     help="graph p starts extracting after graph p-1's extraction: every step / only in the "
                          "first step of a run (the phase offset then persists) / never")
@@ -192,19 +254,22 @@ def main():
     # ORBAMD_BENCH_DEVICE=0 run a multi-rank bench on a one-GPU box (tools/rehearse_ranks.sh)
     backend = os.environ.get("ORBAMD_DIST_BACKEND", "nccl")
     local = int(os.environ.get("ORBAMD_BENCH_DEVICE", local))
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == world
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     W, H, B, P = cfg["W"], cfg["H"], args.batch, args.pipes
     assert B % P == 0, "--batch must be a multiple of --pipes"
+    assert args.pool >= 1
     sub = B // P
-    frames_np = orbamd.synth_frames(rank, 0, B, W, H)  # agent = rank
+    frames_np = orbamd.synth_frames(rank, 0, args.pool * B, W, H)  # agent = rank; pool batches back to back
     def allgather(out, inp):
         # RCCL over xGMI; gloo (the one-GPU rehearsal): through host memory
         if backend == "nccl":
@@ -217,9 +282,10 @@ def main():
     lo_prio, hi_prio = torch.cuda.Stream.priority_range()
     n_hi = {"none": 0, "lead": P // 2, "lead1": 1}[args.prio]
     sched = AgentSchedule(torch, frames_np, W, H, P, device=local, rank=rank, world=world,
-                          allgather=allgather if world > 1 else None,
+                          allgather=allgather if use_dist else None,
                           stagger=args.stagger, exchange=not args.no_exchange,
-                          priorities=[hi_prio if p < n_hi else lo_prio for p in range(P)], nfeatures=cfg["nfeatures"])
+                          priorities=[hi_prio if p < n_hi else lo_prio for p in range(P)], nfeatures=cfg["nfeatures"],
+                          pool=args.pool)
     pipes = sched.pipes
 
     for _ in range(args.warmup):
@@ -237,7 +303,7 @@ def main():
         evs = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(P)]
                for _ in range(nsteps)]
         xevs = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(nsteps)]
-        if timed and world > 1:
+        if timed and use_dist:
             dist.barrier()
         torch.cuda.synchronize()
         t_start = time.perf_counter()
@@ -249,7 +315,7 @@ def main():
             else:
                 sched.step(evs[i], xevs[i], first=i == 0)
         torch.cuda.synchronize()
-        if timed and world > 1:
+        if timed and use_dist:
             dist.barrier()
         elapsed = time.perf_counter() - t_start
         acc = [0.0] * 5
@@ -289,7 +355,8 @@ def main():
     dom = args.roof_kernel
     # 2) timed region: only the dominant kernel bracketed (its live launch duration for the roofline)
     el, dom_live = run_profiled(1 << stages.index(dom), args.steps, True)
-    if world > 1:
+    last_batch, prev_batch = sched.last_batch, (sched.last_batch - 1) % args.pool
+    if use_dist:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -301,14 +368,14 @@ def main():
     except RuntimeError as e:
         err_msg = str(e)
     check = None
+    agent_kf = lambda r, t: orbamd.synth_frames(r, t, 1, W, H)[0]  # noqa: E731 (agent r's keyframe image)
     if not args.no_check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from check_schedule import check_schedule
-        check = check_schedule(sched, frames_np, nfeatures=cfg["nfeatures"],
-                               agent_frames=lambda r: orbamd.synth_frames(r, 0, 1, W, H)[0])
+        check = check_schedule(sched, frames_np, nfeatures=cfg["nfeatures"], agent_frames=agent_kf)
     ok_local = err_msg is None and (check is None or check["bit_exact"])
     ok_all = ok_local
-    if world > 1:
+    if use_dist:
         t = torch.tensor([0 if ok_local else 1], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ok_all = int(t.item()) == 0
@@ -329,6 +396,18 @@ def main():
         del a, b2
     extract_fps = B * args.steps / run_part(args.steps, match=False, xchg=False)
     match_pps = B * args.steps / run_part(args.steps, extract=False, xchg=False)
+    # 4b) ingest leg (untimed for `value`): every step's frames are uploaded from pinned host memory on a
+    # copy stream into the device batch that step processes, overlapped with the previous step's compute;
+    # checked against the oracle like the timed region
+    ingest = None
+    if args.ingest_steps > 0:
+        if use_dist:
+            dist.barrier()
+        ingest = run_ingest(torch, sched, frames_np, args.pool, args.ingest_steps, B, W, H, world, use_dist, dist)
+        if not args.no_check:
+            chk = check_schedule(sched, frames_np, nfeatures=cfg["nfeatures"], agent_frames=agent_kf)
+            ingest["bit_exact"] = bool(chk["bit_exact"])
+            ok_all = ok_all and chk["bit_exact"]
     # 5) sustained pass (untimed for `value`): the full schedule for ~--sustain seconds, which reports the
     # steady-state rate over thousands of steps and keeps the GPU busy long enough for a utilisation sampler
     # to see it. The step count comes from the max-over-ranks timing, so every rank runs the same number of
@@ -336,10 +415,10 @@ def main():
     sustained = None
     if args.sustain > 0:
         n_sus = max(1, int(math.ceil(args.sustain / (el / args.steps))))
-        if world > 1:
+        if use_dist:
             dist.barrier()
         sus_s = run_part(n_sus)
-        if world > 1:
+        if use_dist:
             t = torch.tensor([sus_s], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             sus_s = float(t.item())
@@ -422,6 +501,16 @@ def main():
             "kp_per_frame": round(nkp, 1),
             "matches_per_pair": round(nmatch, 1),
             "sustained": sustained,
+            "ingest": ingest,
+            "stale_guard": {"frame_pool_batches": args.pool, "checked_step_batch": last_batch,
+                            "previous_step_batch": prev_batch,
+                            "note": "consecutive steps process different resident batches, so a stage that did not "
+                                    "launch in the checked (last timed) step leaves the previous batch's outputs and "
+                                    "fails the oracle check" if args.pool > 1 else
+                                    "pool of 1: repeated frames, a skipped launch would not be detected"},
+            "collective": ("rccl all_gather_into_tensor (out-of-place slot buffer)" if use_dist and backend == "nccl"
+                           else "gloo all_gather through host memory (rehearsal)" if use_dist
+                           else "none (N=1: the keyframe slot is packed in place)"),
         }
         if check is not None and check["mismatches"]:
             result["mismatches"] = check["mismatches"]
@@ -456,7 +545,7 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     sched.close()
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
     if not ok_all:

@@ -435,6 +435,7 @@ struct orbx_handle {
     std::vector<hipEvent_t> prof_ev;  // per profiled call: 5 stages x {start, end}
     int prof_calls = 0;
     double prof_ms[5] = {0, 0, 0, 0, 0};
+    int skip_mask = 0;  // orbx_debug_skip_stages (test hook)
 };
 
 static const int kProfMaxCalls = 4096;
@@ -551,9 +552,13 @@ static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstrid
 #define ORBX_ERR_STICKY 1  // device batch path: error flag sticky until orbx_check_error (0: reset every call)
 #endif
 constexpr bool kErrSticky = ORBX_ERR_STICKY != 0;
+/* Error words of h->err: kErrSticky (word 0) collects the device batch paths' flags until orbx_check_error
+ * takes them; kErrCall (word 1) is the host paths' per-call flag (zeroed and read by each call), so a host
+ * call never erases an unread batch error; kErrTake (word 32) receives the atomic read-and-clear. */
+constexpr int kErrWordSticky = 0, kErrWordCall = 1, kErrWordTake = 32;
 static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
                        orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st,
-                       bool reset_err = true) {
+                       bool host_call = true) {
     Geometry& g = h->geo;
     const ExtractParams& ep = g.ep;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
@@ -566,20 +571,21 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     const bool split = !serial && sched == 1;
     const int ncell0 = split ? g.lv[0].ncells : 0;
     hipStream_t sd = serial ? st : h->side;
-    // the host-buffer paths report the flag per call; the device batch path leaves it sticky until
-    // orbx_check_error reads (and clears) it, so no fill kernel sits on the batch stream every call
-    if (reset_err || !kErrSticky) HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), st));
+    // the host-buffer paths report their own per-call word; the device batch path leaves word 0 sticky
+    // until orbx_check_error takes (and clears) it, so no fill kernel sits on the batch stream every call
+    int* errp = h->err.as<int>() + (host_call ? kErrWordCall : kErrWordSticky);
+    if (host_call || !kErrSticky) HIPR(hipMemsetAsync(errp, 0, sizeof(int), st));
     if (split) {
         HIPR(hipEventRecord(h->ev_fork, st));
         HIPR(hipStreamWaitEvent(sd, h->ev_fork, 0));
         if (launch_fast(h, d_frames, fstride, pitch, 0, ncell0, nframes, sd)) return ORBX_EDEVICE;
     }
     if (prof_mark(h, 0, 0, st)) return ORBX_EDEVICE;
-    if (!skip_warm(1) && launch_pyramid(h, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
+    if (!skip_warm(1) && !(h->skip_mask & 1) && launch_pyramid(h, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 0, 1, st)) return ORBX_EDEVICE;
     auto blur = [&](hipStream_t bs) -> int {
         if (prof_mark(h, 3, 0, bs)) return ORBX_EDEVICE;
-        if (!skip_warm(8))
+        if (!skip_warm(8) && !(h->skip_mask & 8))
             HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                                     nullptr, g.nbjobs, nullptr, nframes, bs));
         return prof_mark(h, 3, 1, bs);
@@ -593,11 +599,11 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         if (blur(st)) return ORBX_EDEVICE;
     }
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
-    if (!skip_warm(2) && launch_fast(h, d_frames, fstride, pitch, ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
+    if (!skip_warm(2) && !(h->skip_mask & 2) && launch_fast(h, d_frames, fstride, pitch, ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 1, 1, st) || prof_mark(h, 2, 0, st)) return ORBX_EDEVICE;
-    if (!skip_warm(4)) HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
+    if (!skip_warm(4) && !(h->skip_mask & 4)) HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                        h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
-                       (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, h->err.as<int>(), nframes, st));
+                       (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st));
     if (prof_mark(h, 2, 1, st)) return ORBX_EDEVICE;
     if (serial) {
         if (!blur_first && blur(st)) return ORBX_EDEVICE;
@@ -605,7 +611,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     }
     if (prof_mark(h, 4, 0, st)) return ORBX_EDEVICE;
-    if (!skip_warm(16)) HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+    if (!skip_warm(16) && !(h->skip_mask & 16)) HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                          h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
                          g.d_ptab.as<int>(), nframes, st));
     if (prof_mark(h, 4, 1, st)) return ORBX_EDEVICE;
@@ -685,10 +691,13 @@ void orbx_destroy(orbx_handle* h) {
 int orbx_check_error(orbx_handle* h, void* stream) {
     if (!h) return ORBX_EARG;
     HIPR(hipSetDevice(h->device));
+    // read and clear in one device atomic (a batch on another stream that raises the flag afterwards
+    // leaves it set for the next check)
     int flag = 0;
-    HIPR(hipMemcpyAsync(&flag, h->err.p, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    int* w = h->err.as<int>();
+    HIPR(launch_flag_take(w + kErrWordSticky, w + kErrWordTake, (hipStream_t)stream));
+    HIPR(hipMemcpyAsync(&flag, w + kErrWordTake, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
     HIPR(hipStreamSynchronize((hipStream_t)stream));
-    if (flag) HIPR(hipMemsetAsync(h->err.p, 0, sizeof(int), (hipStream_t)stream));  // read and clear
     return flag ? ORBX_EDEVICE : 0;
 }
 
@@ -696,6 +705,12 @@ int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, 
     if (!d_in || !d_sin || !d_cos || n < 0) return ORBX_EARG;
     if (n == 0) return 0;
     HIPR(launch_sincos_selftest(d_in, d_sin, d_cos, n, (hipStream_t)stream));
+    return 0;
+}
+
+int orbx_debug_skip_stages(orbx_handle* h, int mask) {
+    if (!h || mask < 0 || mask > 0x1F) return ORBX_EARG;
+    h->skip_mask = mask;
     return 0;
 }
 
@@ -789,7 +804,8 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
                              h->out_desc.as<uint8_t>(), h->out_cnt.as<int32_t>(), K, h->stream);
         if (rc) return rc;
         HIPR(hipMemcpyAsync(h->pin_out, h->out_cnt.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-        HIPR(hipMemcpyAsync(h->pin_out + 4, h->err.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+        HIPR(hipMemcpyAsync(h->pin_out + 4, h->err.as<int>() + kErrWordCall, sizeof(int), hipMemcpyDeviceToHost,
+                            h->stream));
         HIPR(hipMemcpyAsync(o_kps, h->out_kps.p, sizeof(orbx_kp) * (size_t)K, hipMemcpyDeviceToHost, h->stream));
         HIPR(hipMemcpyAsync(o_desc, h->out_desc.p, 32 * (size_t)K, hipMemcpyDeviceToHost, h->stream));
         return 0;
@@ -868,7 +884,7 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int width, int height, size
     if (rc) return rc;
     int cnt = 0, errflag = 0;
     HIPR(hipMemcpyAsync(&cnt, h->out_cnt.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-    HIPR(hipMemcpyAsync(&errflag, h->err.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPR(hipMemcpyAsync(&errflag, h->err.as<int>() + kErrWordCall, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     HIPR(hipStreamSynchronize(h->stream));
     if (errflag) return ORBX_EDEVICE;
     if (cnt > cap) return ORBX_ECAPACITY;
@@ -910,6 +926,21 @@ int orbx_get_scale_tables(const orbx_handle* h, float* scale, float* inv_scale, 
         if (inv_scale) inv_scale[l] = h->T.inv_scale[l];
         if (sigma2) sigma2[l] = h->T.sigma2[l];
         if (inv_sigma2) inv_sigma2[l] = h->T.inv_sigma2[l];
+    }
+    return 0;
+}
+
+int orbx_compute_scale_tables(const orbx_params* p, float* scale, float* inv_scale, float* sigma2,
+                              float* inv_sigma2) {
+    if (!p || p->nlevels < 1 || p->nlevels > kMaxLevels || p->nfeatures < 1 || p->scale_factor <= 1.0f)
+        return ORBX_EARG;
+    Tables T;
+    T.build(*p);
+    for (int l = 0; l < T.nlevels; l++) {
+        if (scale) scale[l] = T.scale[l];
+        if (inv_scale) inv_scale[l] = T.inv_scale[l];
+        if (sigma2) sigma2[l] = T.sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = T.inv_sigma2[l];
     }
     return 0;
 }
@@ -1030,15 +1061,16 @@ int orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orb
         HIPR(hipMemcpyAsync(ddR, descR, 32 * (size_t)nR, hipMemcpyHostToDevice, st));
     }
     HIPR(hipMemcpyAsync(misc, hm, sizeof(hm), hipMemcpyHostToDevice, st));
-    HIPR(hipMemsetAsync(left->err.p, 0, sizeof(int), st));
+    int* cerr = left->err.as<int>() + kErrWordCall;  // the host call's own word (the batch word stays sticky)
+    HIPR(hipMemsetAsync(cerr, 0, sizeof(int), st));
     a.left.nframes = a.right.nframes = 1;
     HIPR(launch_stereo(a, 1, misc, misc + 1, dkL, ddL, misc + 2, dkR, ddR, misc + 3, stride, dur, ddp, misc + 4,
-                       left->err.as<int>(), st));
+                       cerr, st));
     int flag = 0, ns = 0;
     HIPR(hipMemcpyAsync(uright, dur, 4 * (size_t)nL, hipMemcpyDeviceToHost, st));
     HIPR(hipMemcpyAsync(depth, ddp, 4 * (size_t)nL, hipMemcpyDeviceToHost, st));
     HIPR(hipMemcpyAsync(&ns, misc + 4, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPR(hipMemcpyAsync(&flag, left->err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPR(hipMemcpyAsync(&flag, cerr, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPR(hipStreamSynchronize(st));
     if (flag & 2) return ORBX_EARG;
     if (flag) return ORBX_EDEVICE;
@@ -1578,10 +1610,12 @@ int orbx_slot_parse(const uint8_t* slot, size_t slot_bytes, orbx_slot_view* v) {
 int orbm_check_error(orbm_ctx* ctx, void* stream) {
     if (!ctx) return ORBX_EARG;
     HIPR(hipSetDevice(ctx->device));
+    // atomic read-and-clear on the device (word 0 -> word 56; the per-call state is words 16..47)
     int flag = 0;
-    HIPR(hipMemcpyAsync(&flag, ctx->err.p, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    int32_t* w = ctx->err.as<int32_t>();
+    HIPR(launch_flag_take(w, w + 56, (hipStream_t)stream));
+    HIPR(hipMemcpyAsync(&flag, w + 56, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
     HIPR(hipStreamSynchronize((hipStream_t)stream));
-    if (flag) HIPR(hipMemsetAsync(ctx->err.p, 0, sizeof(int), (hipStream_t)stream));
     return flag ? ORBX_EDEVICE : 0;
 }
 

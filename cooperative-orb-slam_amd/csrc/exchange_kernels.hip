@@ -258,8 +258,13 @@ __global__ __launch_bounds__(256) void k_tri_slots_bf(const QueryKF q, const uin
                 const float2 p = s.kun[t0 + j];
                 s_x[j] = p.x;
                 s_y[j] = p.y;
-                s_oct[j] = min(max(s.kps[t0 + j].octave, 0), 15);
-                s_flag[j] = (uint8_t)((s.mpf[t0 + j] & 1) | (s.uright[t0 + j] >= 0.f ? 2 : 0));
+                // an octave outside [0, mnScaleLevels) fails the host parser's contract (orbx_slot_parse):
+                // the candidate is skipped and the slot flagged, as k_tri_slots_bow does
+                const int o2 = s.kps[t0 + j].octave;
+                const bool obad = (unsigned)o2 >= (unsigned)s.nlev;
+                if (obad) atomicOr(err, 4);
+                s_oct[j] = obad ? 0 : o2;
+                s_flag[j] = (uint8_t)((s.mpf[t0 + j] & 1) | (obad ? 1 : 0) | (s.uright[t0 + j] >= 0.f ? 2 : 0));
             }
         }
         __syncthreads();
@@ -317,6 +322,9 @@ __global__ __launch_bounds__(64) void k_tri_slots_bow(const QueryKF q, const uin
         return;
     }
     const int nfv1 = min(max(*q.nfv, 0), q.cap);
+    // query nodes at or above the grid's max_nodes would never be visited: flag it (the caller cannot
+    // cheaply check the device count, as k_tri_slots_bf flags count > cap)
+    if (i == 0 && threadIdx.x == 0 && nfv1 > (int)gridDim.x) atomicOr(err, 2);
     if (i >= nfv1) return;
     const int n1 = min(max(*q.count, 0), q.cap);
     const uint32_t node = q.fv_node[i];
@@ -351,6 +359,8 @@ __global__ __launch_bounds__(64) void k_tri_slots_bow(const QueryKF q, const uin
             const int idx2 = s.fv_feat[ci];
             if ((unsigned)idx2 >= (unsigned)s.n) { atomicOr(err, 4); continue; }
             if (s.mpf[idx2] & 1) continue;  // :722-726
+            const int oct2 = s.kps[idx2].octave;
+            if ((unsigned)oct2 >= (unsigned)s.nlev) { atomicOr(err, 4); continue; }  // as orbx_slot_parse
             const bool st2 = s.uright[idx2] >= 0.f;
             const uint4* cd = (const uint4*)(s.desc + (long long)idx2 * 32);
             const uint4 c0 = cd[0], c1 = cd[1];
@@ -359,7 +369,6 @@ __global__ __launch_bounds__(64) void k_tri_slots_bow(const QueryKF q, const uin
                              __popc(qd[6] ^ c1.z) + __popc(qd[7] ^ c1.w);
             if (dist > 50 || dist > bestDist) continue;
             const float2 p2 = s.kun[idx2];
-            const int oct2 = min(max(s.kps[idx2].octave, 0), s.nlev - 1);
             if (!st1 && !st2) {
                 const float dx = __fsub_rn(ex, p2.x), dy = __fsub_rn(ey, p2.y);
                 if (__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < __fmul_rn(100.f, s.meta->mvScaleFactors[oct2]))
@@ -373,6 +382,20 @@ __global__ __launch_bounds__(64) void k_tri_slots_bow(const QueryKF q, const uin
         out[idx1] = bestIdx2;
         if (bestIdx2 >= 0) atomicAdd(&nmatches[r], 1);
     }
+}
+
+/* ----------------------------------------------------------------------------------- */
+/* Read-and-clear of a sticky device error word in one atomic step (orbx_check_error,      */
+/* orbm_check_error): a kernel on another stream that raises the flag after the exchange    */
+/* leaves it set for the next check instead of racing a host-side clear.                   */
+/* ----------------------------------------------------------------------------------- */
+__global__ void k_flag_take(int32_t* flag, int32_t* out) {
+    if (threadIdx.x == 0) *out = atomicExch(flag, 0);
+}
+
+hipError_t launch_flag_take(int32_t* flag, int32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_flag_take, dim3(1), dim3(64), 0, st, flag, out);
+    return hipGetLastError();
 }
 
 /* ----------------------------------------------------------------------------------- */

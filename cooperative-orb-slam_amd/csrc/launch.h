@@ -61,6 +61,7 @@ hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* task
 hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* angB, int swap, int32_t* nout,
                              hipStream_t st);
 
+hipError_t launch_flag_take(int32_t* flag, int32_t* out, hipStream_t st);
 hipError_t launch_pack_slot(const orbx_kf_source& src, const SlotLayout& L, const orbx_kf_meta& meta, uint8_t* slot,
                             int32_t* err, hipStream_t st);
 hipError_t launch_tri_slots(const QueryKF& q, const uint8_t* slots, long long slot_bytes, int nref,

@@ -22,6 +22,7 @@
 #include "Frame.h"
 #include "KeyFrame.h"
 #include "ORBVocabulary_amd.h"
+#include "orbamd_status.h"
 
 namespace ORB_SLAM2 {
 namespace amd {
@@ -69,7 +70,7 @@ void bow_transform(const ORBVocabulary* pVoc, const cv::Mat& D, DBoW2::BowVector
     orbv_handle* h = amd::DeviceVocabulary(pVoc);
     if (!h) throw std::runtime_error("orbslam_amd: ComputeBoW with an unregistered vocabulary (ORBVocabulary_amd.h)");
     bv.clear();
-    fv.clear();
+    fv.clear();  // a device failure below leaves both empty (no BoW matches), logged, not thrown
     const int n = D.rows;
     if (n == 0) return;
     std::vector<uint8_t> desc((size_t)n * 32);
@@ -83,7 +84,7 @@ void bow_transform(const ORBVocabulary* pVoc, const cv::Mat& D, DBoW2::BowVector
     int nb = 0, nf = 0;
     const int rc = orbv_transform(h, desc.data(), n, levelsup, word.data(), value.data(), &nb, node.data(), off.data(),
                                   feat.data(), &nf);
-    if (rc != ORBX_OK) throw std::runtime_error("orbslam_amd: orbv_transform failed rc=" + std::to_string(rc));
+    if (!amd::StatusOk(rc, "orbv_transform")) return;
     for (int i = 0; i < nb; i++) bv.insert(std::make_pair(word[i], value[i]));  // ascending word id
     for (int j = 0; j < nf; j++)
         fv.insert(std::make_pair(node[j], std::vector<unsigned int>(feat.begin() + off[j], feat.begin() + off[j + 1])));

@@ -3,7 +3,9 @@
  * ORB_SLAM2.1/src/Frame.cc:470-641). The two extractors' pyramids of the
  * stereo pair are still on the device after ExtractORB(0/1) (drop-in ORBextractor), so only the
  * keypoints and descriptors travel; orbx_compute_stereo_matches writes mvuRight / mvDepth.
- * Where the reference would assert (a correlation window outside the level) this throws.
+ * Where the reference would assert (a correlation window outside the level: cv::Mat::rowRange /
+ * colRange CV_Assert, which throws cv::Exception) this throws std::runtime_error (ORBX_EARG); a device
+ * failure does not throw (orbamd_status.h): every keypoint stays without a stereo match (-1).
  */
 #include <cstring>
 #include <stdexcept>
@@ -12,6 +14,7 @@
 
 #include "Frame.h"
 #include "ORBextractor.h"
+#include "orbamd_status.h"
 #include "orbslam_amd.h"
 
 namespace ORB_SLAM2 {
@@ -40,10 +43,20 @@ void Frame::ComputeStereoMatches() {
     cv::Mat dl = mDescriptors.isContinuous() ? mDescriptors : mDescriptors.clone();
     cv::Mat dr = mDescriptorsRight.isContinuous() ? mDescriptorsRight : mDescriptorsRight.clone();
     int nst = 0;
-    const int rc = orbx_compute_stereo_matches(mpORBextractorLeft->DeviceHandle(), mpORBextractorRight->DeviceHandle(),
+    orbx_handle* hl = mpORBextractorLeft->DeviceHandle();
+    orbx_handle* hr = mpORBextractorRight->DeviceHandle();
+    if (!hl || !hr) {  // an extractor without a device handle (its device failed): no stereo matches
+        amd::StatusOk(ORBX_EDEVICE, "ComputeStereoMatches (no device pyramid)");
+        return;
+    }
+    const int rc = orbx_compute_stereo_matches(hl, hr,
                                                kl.data(), dl.data, N, kr.data(), kr.empty() ? nullptr : dr.data,
                                                (int)kr.size(), mbf, mb, mvuRight.data(), mvDepth.data(), &nst);
-    if (rc != ORBX_OK) throw std::runtime_error("orbslam_amd: orbx_compute_stereo_matches failed rc=" + std::to_string(rc));
+    if (rc == ORBX_EARG) throw std::runtime_error("orbslam_amd: orbx_compute_stereo_matches: window outside the level");
+    if (!amd::StatusOk(rc, "orbx_compute_stereo_matches")) {
+        mvuRight.assign(N, -1.0f);
+        mvDepth.assign(N, -1.0f);
+    }
 }
 
 }  // namespace ORB_SLAM2

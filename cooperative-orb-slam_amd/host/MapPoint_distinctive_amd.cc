@@ -9,43 +9,22 @@
  * non-bad observing KeyFrames gathered in mObservations order, exactly as the reference does; the
  * N x N Hamming matrix, the per-row medians (vDists[0.5*(N-1)] of the sorted row) and the first
  * strict minimum run in k_distinctive (orbm_compute_distinctive_descriptors); mDescriptor is set
- * under the lock. A bad point or one without usable observations is left untouched. Device
- * failures throw std::runtime_error. MapPoint.h gains one declaration:
+ * under the lock. A bad point or one without usable observations is left untouched. A device
+ * failure does not throw (orbamd_status.h): every mDescriptor is left unchanged and the status
+ * logged. MapPoint.h gains one declaration:
  *     static void ComputeDistinctiveDescriptorsBatch(const std::vector<MapPoint*>& vpMPs);
  */
 #include <cstdlib>
 #include <map>
 #include <mutex>
-#include <stdexcept>
-#include <string>
 #include <vector>
 
 #include "KeyFrame.h"
 #include "MapPoint.h"
+#include "orbamd_status.h"
 #include "orbslam_amd.h"
 
 namespace ORB_SLAM2 {
-
-namespace {
-
-void dd_ok(int rc, const char* what) {
-    if (rc != ORBX_OK) throw std::runtime_error(std::string("orbslam_amd: ") + what + " failed rc=" + std::to_string(rc));
-}
-
-orbm_ctx* dd_ctx() {
-    struct Holder {
-        orbm_ctx* c = nullptr;
-        ~Holder() { if (c) orbm_destroy(c); }
-    };
-    static thread_local Holder h;
-    if (!h.c) {
-        const char* dev = getenv("ORBAMD_DEVICE");
-        dd_ok(orbm_create(dev ? atoi(dev) : 0, &h.c), "orbm_create");
-    }
-    return h.c;
-}
-
-}  // namespace
 
 void MapPoint::ComputeDistinctiveDescriptors() {
     ComputeDistinctiveDescriptorsBatch(std::vector<MapPoint*>(1, this));
@@ -79,9 +58,11 @@ void MapPoint::ComputeDistinctiveDescriptorsBatch(const std::vector<MapPoint*>& 
     if (pts.empty()) return;
     std::vector<int32_t> best(pts.size());
     std::vector<uint8_t> out(32 * pts.size());
-    dd_ok(orbm_compute_distinctive_descriptors(dd_ctx(), (int)pts.size(), off.data(), desc.data(), best.data(),
-                                               out.data()),
-          "orbm_compute_distinctive_descriptors");
+    orbm_ctx* c = amd::ThreadMatcher();
+    if (!c || !amd::StatusOk(orbm_compute_distinctive_descriptors(c, (int)pts.size(), off.data(), desc.data(),
+                                                                  best.data(), out.data()),
+                             "orbm_compute_distinctive_descriptors"))
+        return;
     for (size_t i = 0; i < pts.size(); i++) {
         std::unique_lock<std::mutex> lock(pts[i]->mMutexFeatures);
         pts[i]->mDescriptor = cv::Mat(1, 32, CV_8U, out.data() + 32 * i).clone();

@@ -8,16 +8,11 @@
 #include <cassert>
 #include <cstdlib>
 #include <cstring>
-#include <stdexcept>
-#include <string>
 
+#include "orbamd_status.h"
 #include "orbslam_amd.h"
 
 namespace ORB_SLAM2 {
-
-static void orbx_ok(int rc, const char* what) {
-    if (rc != ORBX_OK) throw std::runtime_error(std::string("orbslam_amd: ") + what + " failed rc=" + std::to_string(rc));
-}
 
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
     : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
@@ -28,35 +23,62 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
     const char* hp = getenv("ORBAMD_HOST_PYRAMID");
     if (hp && atoi(hp) != 0) mbHostPyramid = true;
     // the tables are computed by the library with the reference's float semantics
-    // (ORBextractor.cc:415-431); a probe handle at 640x480 answers the getters.
-    ensureHandle(640, 480);
-    mvScaleFactor.resize(nlevels);
-    mvInvScaleFactor.resize(nlevels);
-    mvLevelSigma2.resize(nlevels);
-    mvInvLevelSigma2.resize(nlevels);
-    orbx_ok(orbx_get_scale_tables(mpHandle, mvScaleFactor.data(), mvInvScaleFactor.data(), mvLevelSigma2.data(),
-                                  mvInvLevelSigma2.data()),
-            "orbx_get_scale_tables");
-    mvImagePyramid.resize(nlevels);
+    // (ORBextractor.cc:415-431), host-only, so the getters answer even without a usable device; the
+    // device handle is created on the first frame (at that frame's size)
+    mvScaleFactor.assign(nlevels > 0 ? nlevels : 0, 1.f);
+    mvInvScaleFactor.assign(mvScaleFactor.size(), 1.f);
+    mvLevelSigma2.assign(mvScaleFactor.size(), 1.f);
+    mvInvLevelSigma2.assign(mvScaleFactor.size(), 1.f);
+    orbx_params p = params();
+    amd::StatusOk(orbx_compute_scale_tables(&p, mvScaleFactor.data(), mvInvScaleFactor.data(), mvLevelSigma2.data(),
+                                            mvInvLevelSigma2.data()),
+                  "orbx_compute_scale_tables");
+    mvImagePyramid.resize(mvScaleFactor.size());
 }
 
-ORBextractor::~ORBextractor() {
-    if (mpHandle) orbx_destroy(mpHandle);
-}
-
-void ORBextractor::ensureHandle(int width, int height) {
-    if (mpHandle && width <= mHandleW && height <= mHandleH) return;
-    if (mpHandle) orbx_destroy(mpHandle);
-    mpHandle = nullptr;
+orbx_params ORBextractor::params() const {
     orbx_params p;
     p.nfeatures = nfeatures;
     p.scale_factor = (float)scaleFactor;
     p.nlevels = nlevels;
     p.ini_th_fast = iniThFAST;
     p.min_th_fast = minThFAST;
-    orbx_ok(orbx_create(&p, mDevice, width, height, 1, &mpHandle), "orbx_create");
+    return p;
+}
+
+ORBextractor::~ORBextractor() {
+    if (mpHandle) orbx_destroy(mpHandle);
+}
+
+int ORBextractor::ensureHandle(int width, int height) {
+    if (mpHandle && width <= mHandleW && height <= mHandleH) return ORBX_OK;
+    if (mpHandle) orbx_destroy(mpHandle);
+    mpHandle = nullptr;
+    mHandleW = mHandleH = 0;
+    const orbx_params p = params();
+    orbx_handle* h = nullptr;
+    const int rc = orbx_create(&p, mDevice, width, height, 1, &h);
+    if (rc != ORBX_OK) return rc;  // retried on the next frame
+    mpHandle = h;
     mHandleW = width;
     mHandleH = height;
+    return ORBX_OK;
+}
+
+void ORBextractor::failed(int rc, const char* what, std::vector<cv::KeyPoint>& kps, cv::OutputArray desc) {
+    amd::StatusOk(rc, what);
+    mLastStatus = rc;
+    // the reference's zero-keypoint result (ORBextractor.cc:1064-1065, 1075)
+    kps.clear();
+    desc.release();
+    for (size_t l = 0; l < mvImagePyramid.size(); l++) mvImagePyramid[l].release();
+    mbPyramidStale = false;
+    // a device error may have left the handle unusable: start from a fresh one on the next frame
+    if (rc == ORBX_EDEVICE && mpHandle) {
+        orbx_destroy(mpHandle);
+        mpHandle = nullptr;
+        mHandleW = mHandleH = 0;
+    }
 }
 
 void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask, std::vector<cv::KeyPoint>& _keypoints,
@@ -65,14 +87,17 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask, std::
     if (_image.empty()) return;  // ORBextractor.cc:1046-1047
     cv::Mat image = _image.getMat();
     assert(image.type() == CV_8UC1);  // ORBextractor.cc:1050
-    ensureHandle(image.cols, image.rows);
+    int rc = ensureHandle(image.cols, image.rows);
+    if (rc != ORBX_OK) return failed(rc, "orbx_create", _keypoints, _descriptors);
     const int cap = orbx_max_keypoints(mpHandle, image.cols, image.rows);
+    if (cap < 0) return failed(cap, "orbx_max_keypoints", _keypoints, _descriptors);
     mKpBuf.resize(sizeof(orbx_kp) * (size_t)cap);
     mDescBuf.resize(32 * (size_t)cap);
     int n = 0;
-    orbx_ok(orbx_extract(mpHandle, image.data, image.cols, image.rows, image.step, (orbx_kp*)mKpBuf.data(),
-                         mDescBuf.data(), cap, &n),
-            "orbx_extract");
+    rc = orbx_extract(mpHandle, image.data, image.cols, image.rows, image.step, (orbx_kp*)mKpBuf.data(),
+                      mDescBuf.data(), cap, &n);
+    if (rc != ORBX_OK) return failed(rc, "orbx_extract", _keypoints, _descriptors);
+    mLastStatus = ORBX_OK;
     if (n == 0) {
         _descriptors.release();  // ORBextractor.cc:1064-1065
     } else {
@@ -91,14 +116,20 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask, std::
 
 const std::vector<cv::Mat>& ORBextractor::SyncImagePyramid() {
     if (!mbPyramidStale) return mvImagePyramid;
+    mbPyramidStale = false;
     for (int l = 0; l < nlevels; l++) {
         int w = 0, h = 0;
-        orbx_ok(orbx_pyramid_level(mpHandle, 0, l, nullptr, 0, &w, &h), "orbx_pyramid_level");
-        mvImagePyramid[l].create(h, w, CV_8U);
-        orbx_ok(orbx_pyramid_level(mpHandle, 0, l, mvImagePyramid[l].data, mvImagePyramid[l].step, &w, &h),
-                "orbx_pyramid_level");
+        int rc = mpHandle ? orbx_pyramid_level(mpHandle, 0, l, nullptr, 0, &w, &h) : ORBX_EDEVICE;
+        if (rc == ORBX_OK) {
+            mvImagePyramid[l].create(h, w, CV_8U);
+            rc = orbx_pyramid_level(mpHandle, 0, l, mvImagePyramid[l].data, mvImagePyramid[l].step, &w, &h);
+        }
+        if (!amd::StatusOk(rc, "orbx_pyramid_level")) {  // no pyramid rather than a stale one
+            mLastStatus = rc;
+            for (int k = 0; k < nlevels; k++) mvImagePyramid[k].release();
+            break;
+        }
     }
-    mbPyramidStale = false;
     return mvImagePyramid;
 }
 

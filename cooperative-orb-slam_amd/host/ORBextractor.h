@@ -6,8 +6,11 @@
  * 252-258; Tracking.cc:119-125).
  *
  * Error behaviour: like the reference, an empty image returns with outputs untouched and a
- * non-8UC1 image asserts (ORBextractor.cc:1046-1050); a device failure throws
- * std::runtime_error (the reference has no failure mode there; there is no CPU fallback).
+ * non-8UC1 image asserts (ORBextractor.cc:1046-1050). A device failure never throws into the
+ * caller's thread (the reference has no failure mode there and no CPU fallback exists): the call
+ * returns the reference's zero-keypoint result (keypoints cleared, descriptors released,
+ * ORBextractor.cc:1064-1065), logs the status to stderr (orbamd_status.h) and keeps it in
+ * LastStatus(); the next frame retries on a fresh device handle.
  *
  * mvImagePyramid: the pyramid stays on the device. Its one reader in the reference,
  * Frame::ComputeStereoMatches (A1 Frame.cc:474-581), is replaced by host/Frame_stereo_amd.cc, which
@@ -22,7 +25,7 @@
 #include <opencv2/features2d/features2d.hpp>
 #include <vector>
 
-struct orbx_handle;
+#include "orbslam_amd.h"
 
 namespace ORB_SLAM2 {
 
@@ -53,8 +56,13 @@ public:
     // Frame::ComputeStereoMatches, host/Frame_stereo_amd.cc); addition to the reference surface
     orbx_handle* DeviceHandle() const { return mpHandle; }
 
+    // status of the last operator() / SyncImagePyramid (ORBX_OK or a negative ORBX_E* code); addition
+    int LastStatus() const { return mLastStatus; }
+
 protected:
-    void ensureHandle(int width, int height);
+    int ensureHandle(int width, int height);
+    orbx_params params() const;
+    void failed(int rc, const char* what, std::vector<cv::KeyPoint>& kps, cv::OutputArray desc);
 
     int nfeatures;
     double scaleFactor;
@@ -71,6 +79,7 @@ protected:
     int mDevice;
     bool mbHostPyramid;   // ORBAMD_HOST_PYRAMID=1: materialise after every call
     bool mbPyramidStale;  // mvImagePyramid does not hold the last call's levels yet
+    int mLastStatus = 0;
     std::vector<unsigned char> mKpBuf, mDescBuf;
 };
 

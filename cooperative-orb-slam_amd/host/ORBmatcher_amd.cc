@@ -9,37 +9,28 @@
  * locks: GetMapPointMatches, GetRotation/GetTranslation/GetCameraCenter) into an
  * orbm_kf_view and runs the matcher kernels; results are converted back to the reference's
  * containers. One orbm_ctx per calling thread (Tracking, LocalMapping, LoopClosing call
- * concurrently). Device failures throw std::runtime_error -- there is no CPU fallback.
+ * concurrently). A device failure does not throw (orbamd_status.h): the call returns 0 with the
+ * reference's empty result (no pairs / a NULL-filled match vector) and logs the status.
  */
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
-#include <stdexcept>
-#include <string>
 #include <vector>
 
 #include "ORBmatcher.h"
+#include "orbamd_status.h"
 #include "orbslam_amd.h"
 
 namespace ORB_SLAM2 {
 
 namespace {
 
-void amd_ok(int rc, const char* what) {
-    if (rc != ORBX_OK) throw std::runtime_error(std::string("orbslam_amd: ") + what + " failed rc=" + std::to_string(rc));
-}
-
-orbm_ctx* thread_ctx() {
-    struct Holder {
-        orbm_ctx* c = nullptr;
-        ~Holder() { if (c) orbm_destroy(c); }
-    };
-    static thread_local Holder h;
-    if (!h.c) {
-        const char* dev = getenv("ORBAMD_DEVICE");
-        amd_ok(orbm_create(dev ? atoi(dev) : 0, &h.c), "orbm_create");
-    }
-    return h.c;
+/* the call's status through the thread's matcher context (nullptr ctx: the creation failure was
+ * already recorded) */
+template <class F>
+bool run(const char* what, F f) {
+    orbm_ctx* c = amd::ThreadMatcher();
+    return c && amd::StatusOk(f(c), what);
 }
 
 /* host staging of one KeyFrame / Frame (ORBmatcher.cc reads exactly these members) */
@@ -128,10 +119,12 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F
     cv::Mat F = F12.isContinuous() ? F12 : F12.clone();
     std::vector<int32_t> m12((size_t)std::max(pKF1->N, 1));
     int n = 0;
-    amd_ok(orbm_search_for_triangulation(thread_ctx(), &v1.v, &v2.v, F.ptr<float>(), ex, ey, bOnlyStereo ? 1 : 0,
-                                         mbCheckOrientation ? 1 : 0, m12.data(), &n),
-           "orbm_search_for_triangulation");
     vMatchedPairs.clear();
+    if (!run("orbm_search_for_triangulation", [&](orbm_ctx* c) {
+            return orbm_search_for_triangulation(c, &v1.v, &v2.v, F.ptr<float>(), ex, ey, bOnlyStereo ? 1 : 0,
+                                                 mbCheckOrientation ? 1 : 0, m12.data(), &n);
+        }))
+        return 0;
     vMatchedPairs.reserve(n);
     for (int i = 0; i < pKF1->N; i++)
         if (m12[i] >= 0) vMatchedPairs.push_back(std::make_pair((size_t)i, (size_t)m12[i]));
@@ -151,9 +144,11 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpM
     vf.finish(F.N, F.mDescriptors, std::vector<float>(), F.mvScaleFactors, F.mvLevelSigma2, false);
     std::vector<int32_t> mf((size_t)std::max(F.N, 1));
     int n = 0;
-    amd_ok(orbm_search_by_bow_kf_f(thread_ctx(), &vk.v, &vf.v, mfNNratio, mbCheckOrientation ? 1 : 0, mf.data(), &n),
-           "orbm_search_by_bow_kf_f");
-    vpMapPointMatches = std::vector<MapPoint*>(F.N, static_cast<MapPoint*>(NULL));
+    vpMapPointMatches = std::vector<MapPoint*>(F.N, static_cast<MapPoint*>(NULL));  // :163
+    if (!run("orbm_search_by_bow_kf_f", [&](orbm_ctx* c) {
+            return orbm_search_by_bow_kf_f(c, &vk.v, &vf.v, mfNNratio, mbCheckOrientation ? 1 : 0, mf.data(), &n);
+        }))
+        return 0;
     for (int i = 0; i < F.N; i++)
         if (mf[i] >= 0) vpMapPointMatches[i] = vpMapPointsKF[mf[i]];
     return n;
@@ -174,10 +169,11 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint
     v2.finish(pKF2->N, pKF2->mDescriptors, std::vector<float>(), pKF2->mvScaleFactors, pKF2->mvLevelSigma2, true);
     std::vector<int32_t> m12(vpMapPoints1.size() ? vpMapPoints1.size() : 1);
     int n = 0;
-    amd_ok(orbm_search_by_bow_kf_kf(thread_ctx(), &v1.v, &v2.v, mfNNratio, mbCheckOrientation ? 1 : 0, m12.data(),
-                                    &n),
-           "orbm_search_by_bow_kf_kf");
-    vpMatches12 = std::vector<MapPoint*>(vpMapPoints1.size(), static_cast<MapPoint*>(NULL));
+    vpMatches12 = std::vector<MapPoint*>(vpMapPoints1.size(), static_cast<MapPoint*>(NULL));  // :536
+    if (!run("orbm_search_by_bow_kf_kf", [&](orbm_ctx* c) {
+            return orbm_search_by_bow_kf_kf(c, &v1.v, &v2.v, mfNNratio, mbCheckOrientation ? 1 : 0, m12.data(), &n);
+        }))
+        return 0;
     for (size_t i = 0; i < vpMapPoints1.size(); i++)
         if (m12[i] >= 0) vpMatches12[i] = vpMapPoints2[m12[i]];
     return n;

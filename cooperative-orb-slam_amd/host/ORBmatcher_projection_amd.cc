@@ -13,7 +13,8 @@
  * on the host with the reference's float semantics; grid, windowed Hamming search, in-order claims
  * and the rotation histogram on the device) and writes the assignments back. MapPoint's private
  * mfMinDistance / mfMaxDistance are read through GetMinDistance() / GetMaxDistance(), two getters
- * the maintainer adds to MapPoint.h. Device failures throw std::runtime_error.
+ * the maintainer adds to MapPoint.h. A device failure does not throw (orbamd_status.h): the call
+ * returns 0 and leaves the caller's containers and the map untouched.
  * Fuse: the device returns each MapPoint's fused keypoint (orbm_fuse*); the map updates (Replace,
  * AddObservation, AddMapPoint / vpReplacePoint) then run here in the reference's loop order, with the
  * reference's per-iteration isBad() / IsInKeyFrame() test, so an entry changed by an earlier update is
@@ -23,32 +24,20 @@
 #include <cstdlib>
 #include <cstring>
 #include <set>
-#include <stdexcept>
-#include <string>
 #include <vector>
 
 #include "ORBmatcher.h"
+#include "orbamd_status.h"
 #include "orbslam_amd.h"
 
 namespace ORB_SLAM2 {
 
 namespace {
 
-void proj_ok(int rc, const char* what) {
-    if (rc != ORBX_OK) throw std::runtime_error(std::string("orbslam_amd: ") + what + " failed rc=" + std::to_string(rc));
-}
-
-orbm_ctx* proj_ctx() {
-    struct Holder {
-        orbm_ctx* c = nullptr;
-        ~Holder() { if (c) orbm_destroy(c); }
-    };
-    static thread_local Holder h;
-    if (!h.c) {
-        const char* dev = getenv("ORBAMD_DEVICE");
-        proj_ok(orbm_create(dev ? atoi(dev) : 0, &h.c), "orbm_create");
-    }
-    return h.c;
+template <class F>
+bool run(const char* what, F f) {
+    orbm_ctx* c = amd::ThreadMatcher();
+    return c && amd::StatusOk(f(c), what);
 }
 
 /* the Frame / KeyFrame side of a call */
@@ -172,8 +161,10 @@ int ORBmatcher::SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMap
     ps.finish(n);
     std::vector<int32_t> m((size_t)std::max(F.N, 1));
     int nm = 0;
-    proj_ok(orbm_search_by_projection_local(proj_ctx(), &fs.v, &ps.m, th, mfNNratio, m.data(), &nm),
-            "orbm_search_by_projection_local");
+    if (!run("orbm_search_by_projection_local", [&](orbm_ctx* c) {
+            return orbm_search_by_projection_local(c, &fs.v, &ps.m, th, mfNNratio, m.data(), &nm);
+        }))
+        return 0;
     apply(F.mvpMapPoints, m, vpMapPoints);
     return nm;
 }
@@ -198,10 +189,12 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
     cv::Mat kc, kl;
     std::vector<int32_t> m((size_t)std::max(CurrentFrame.N, 1));
     int nm = 0;
-    proj_ok(orbm_search_by_projection_last_frame(proj_ctx(), &fs.v, mat44(CurrentFrame.mTcw, kc), &ps.m,
-                                                 mat44(LastFrame.mTcw, kl), th, bMono ? 1 : 0,
-                                                 mbCheckOrientation ? 1 : 0, m.data(), &nm),
-            "orbm_search_by_projection_last_frame");
+    if (!run("orbm_search_by_projection_last_frame", [&](orbm_ctx* c) {
+            return orbm_search_by_projection_last_frame(c, &fs.v, mat44(CurrentFrame.mTcw, kc), &ps.m,
+                                                       mat44(LastFrame.mTcw, kl), th, bMono ? 1 : 0,
+                                                       mbCheckOrientation ? 1 : 0, m.data(), &nm);
+        }))
+        return 0;
     apply(CurrentFrame.mvpMapPoints, m, LastFrame.mvpMapPoints);
     return nm;
 }
@@ -227,9 +220,11 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std
     cv::Mat kc;
     std::vector<int32_t> m((size_t)std::max(CurrentFrame.N, 1));
     int nm = 0;
-    proj_ok(orbm_search_by_projection_keyframe(proj_ctx(), &fs.v, mat44(CurrentFrame.mTcw, kc), &ps.m, th, ORBdist,
-                                               mbCheckOrientation ? 1 : 0, m.data(), &nm),
-            "orbm_search_by_projection_keyframe");
+    if (!run("orbm_search_by_projection_keyframe", [&](orbm_ctx* c) {
+            return orbm_search_by_projection_keyframe(c, &fs.v, mat44(CurrentFrame.mTcw, kc), &ps.m, th, ORBdist,
+                                                     mbCheckOrientation ? 1 : 0, m.data(), &nm);
+        }))
+        return 0;
     apply(CurrentFrame.mvpMapPoints, m, vpMPs);
     return nm;
 }
@@ -257,8 +252,10 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector
     cv::Mat ks;
     std::vector<int32_t> m(vpMatched.size() ? vpMatched.size() : 1);
     int nm = 0;
-    proj_ok(orbm_search_by_projection_sim3(proj_ctx(), &fs.v, mat44(Scw, ks), &ps.m, th, m.data(), &nm),
-            "orbm_search_by_projection_sim3");
+    if (!run("orbm_search_by_projection_sim3", [&](orbm_ctx* c) {
+            return orbm_search_by_projection_sim3(c, &fs.v, mat44(Scw, ks), &ps.m, th, m.data(), &nm);
+        }))
+        return 0;
     apply(vpMatched, m, vpPoints);
     return nm;
 }
@@ -289,8 +286,10 @@ int ORBmatcher::Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, c
     T[15] = 1.f;
     std::vector<int32_t> best(n ? n : 1);
     int nf = 0;
-    proj_ok(orbm_fuse(proj_ctx(), &fs.v, T, O, &ps.m, th, pKF->mvInvLevelSigma2.data(), best.data(), &nf),
-            "orbm_fuse");
+    if (!run("orbm_fuse", [&](orbm_ctx* c) {
+            return orbm_fuse(c, &fs.v, T, O, &ps.m, th, pKF->mvInvLevelSigma2.data(), best.data(), &nf);
+        }))
+        return 0;
     // the reference's updates, in order (:947-971)
     int nFused = 0;
     for (size_t i = 0; i < n; i++) {
@@ -336,7 +335,10 @@ int ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& v
     cv::Mat ks;
     std::vector<int32_t> best(n ? n : 1);
     int nf = 0;
-    proj_ok(orbm_fuse_sim3(proj_ctx(), &fs.v, mat44(Scw, ks), &ps.m, th, best.data(), &nf), "orbm_fuse_sim3");
+    if (!run("orbm_fuse_sim3", [&](orbm_ctx* c) {
+            return orbm_fuse_sim3(c, &fs.v, mat44(Scw, ks), &ps.m, th, best.data(), &nf);
+        }))
+        return 0;
     int nFused = 0;
     for (size_t i = 0; i < n; i++) {  // :1082-1097, in order
         if (best[i] < 0) continue;

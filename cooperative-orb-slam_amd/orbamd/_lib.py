@@ -102,6 +102,8 @@ SIGNATURES = {
     "orbx_get_scale_factor": (_F, [_P]),
     "orbx_get_scale_tables": (_I, [_P, _P, _P, _P, _P]),
     "orbx_get_feature_split": (_I, [_P, _P, _P]),
+    "orbx_compute_scale_tables": (_I, [C.POINTER(OrbxParams), _P, _P, _P, _P]),
+    "orbx_debug_skip_stages": (_I, [_P, _I]),
     "orbm_create": (_I, [_I, C.POINTER(_P)]),
     "orbm_destroy": (None, [_P]),
     "orbm_descriptor_distance": (_I, [_P, _P]),

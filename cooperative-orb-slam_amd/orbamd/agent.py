@@ -12,6 +12,9 @@ orbx handle, matcher ctx and HIP stream each):
     buffer (orbm_search_for_triangulation_slots_device).
 Graphs are staggered: graph p starts extracting a step once graph p-1 has finished extracting it,
 so one graph's FAST overlaps another's latency-bound tail (octree, describe, matcher).
+The frames live in a pool of `pool` resident batches and consecutive steps process consecutive
+batches, so no step's correct output equals the previous step's: a stage that stopped launching
+leaves stale results that the self-check (oracle/check_schedule.py) sees.
 torch is plumbing only (HBM buffers, streams, torch.distributed); every kernel is liborbamd.so's.
 """
 from .device import BatchPipeline
@@ -19,13 +22,17 @@ from .device import BatchPipeline
 
 class AgentSchedule:
     def __init__(self, torch, frames_np, width, height, pipes, device=0, rank=0, world=1, allgather=None,
-                 stagger="each", exchange=True, priorities=None, nfeatures=1000):
-        """frames_np: uint8 [B, H, W] host frames of this agent (copied to HBM once); allgather(out, inp):
-        all-gather of equal-sized device byte tensors across agents (None at world 1)."""
-        B = len(frames_np)
+                 stagger="each", exchange=True, priorities=None, nfeatures=1000, pool=1):
+        """frames_np: uint8 [pool*B, H, W] host frames of this agent (copied to HBM once), batch r = frames
+        [r*B, (r+1)*B); allgather(out, inp): all-gather of equal-sized device byte tensors across agents
+        (None: no collective, only possible at world 1, where the slot is packed in place)."""
+        assert len(frames_np) % pool == 0
+        B = len(frames_np) // pool
         assert B % pipes == 0, "frames per step must be a multiple of the graph count"
+        assert allgather is not None or world == 1
         self.torch, self.W, self.H, self.B, self.P = torch, width, height, B, pipes
         self.sub = B // pipes
+        self.pool, self.cursor, self.last_batch = pool, 0, None
         self.rank, self.world, self.allgather = rank, world, allgather
         self.stagger, self.exchange_on = stagger, exchange
         dev = torch.device("cuda", device)
@@ -34,12 +41,17 @@ class AgentSchedule:
         # frames live in a pitched HBM buffer: rows padded to 64 bytes when the width is not a multiple of 4
         # (C4's 1241), so every row starts 4-aligned and the whole-frame pyramid kernel applies
         pitch = width if width % 4 == 0 else (width + 63) // 64 * 64
-        self.frames = []
-        for p in range(pipes):
-            buf = torch.zeros((sub, height, pitch), dtype=torch.uint8, device=dev)
-            view = buf[:, :, :width]
-            view.copy_(torch.from_numpy(frames_np[p * sub:(p + 1) * sub]).to(dev))
-            self.frames.append(view)
+        self.pitch = pitch
+        self.frames = []  # [batch r][graph p] -> device view [sub, H, W]
+        for r in range(pool):
+            row = []
+            for p in range(pipes):
+                buf = torch.zeros((sub, height, pitch), dtype=torch.uint8, device=dev)
+                view = buf[:, :, :width]
+                lo = r * B + p * sub
+                view.copy_(torch.from_numpy(frames_np[lo:lo + sub]).to(dev))
+                row.append(view)
+            self.frames.append(row)
         self.nfeatures = nfeatures
         self.pipes = [BatchPipeline(torch, width, height, sub, nfeatures=nfeatures, device=device)
                       for _ in range(pipes)]
@@ -48,11 +60,13 @@ class AgentSchedule:
         self.done = [torch.cuda.Event() for _ in range(pipes)]
         p0 = self.pipes[0]
         self.slot_bytes = p0.slot_bytes()
-        # N = 1: the keyframe is packed straight into the receive buffer (no copy); N > 1: into its own
-        # send buffer for an out-of-place all-gather
+        # without a collective (N = 1) the keyframe is packed straight into the receive buffer (no copy);
+        # with one (N > 1, or N = 1 under torch.distributed: bench.py --dist) into its own send buffer for
+        # an out-of-place all-gather
+        self.collective = allgather is not None
         self.all_slots = torch.zeros(world * self.slot_bytes, dtype=torch.uint8, device=dev)
-        self.my_slot = (self.all_slots if world == 1 else
-                        torch.zeros(self.slot_bytes, dtype=torch.uint8, device=dev))
+        self.my_slot = (torch.zeros(self.slot_bytes, dtype=torch.uint8, device=dev) if self.collective else
+                        self.all_slots)
         self.xmatch = torch.empty((world, p0.stride), dtype=torch.int32, device=dev)
         self.xn = torch.zeros(world, dtype=torch.int32, device=dev)
         self.pack_err = torch.zeros(16, dtype=torch.int32, device=dev)
@@ -69,21 +83,28 @@ class AgentSchedule:
             p0.pack(0, self.my_slot, self.meta, st.cuda_stream, err=self.pack_err, src=self.src0)
             if ag is not None:
                 ag[0].record(st)
-            if self.world > 1:
+            if self.collective:
                 self.allgather(self.all_slots, self.my_slot)
             if ag is not None:
                 ag[1].record(st)
             p0.match_slots(0, self.all_slots, self.world, self.xmatch, self.xn, st.cuda_stream, query=self.src0)
 
-    def step(self, ev=None, xev=None, extract=True, match=True, xchg=True, first=True):
-        """enqueue one step; ev[p] = (start, end) events around graph p's matcher, xev around the exchange"""
+    def step(self, ev=None, xev=None, extract=True, match=True, xchg=True, first=True, batch=None, wait=None):
+        """enqueue one step over the next pool batch (or `batch`); ev[p] = (start, end) events around graph
+        p's matcher, xev around the exchange; wait: an event every graph waits for before extracting (the
+        ingest leg's upload of this batch)"""
         torch = self.torch
+        r = self.cursor % self.pool if batch is None else batch
+        self.cursor += 1
+        self.last_batch = r
         for p in range(self.P):
             st = self.streams[p].cuda_stream
             if extract:
+                if wait is not None:
+                    self.streams[p].wait_event(wait)
                 if p > 0 and (self.stagger == "each" or (self.stagger == "once" and first)):
                     self.streams[p].wait_event(self.done[p - 1])
-                self.pipes[p].extract(self.frames[p], st)
+                self.pipes[p].extract(self.frames[r][p], st)
                 self.done[p].record(self.streams[p])
             if match:
                 if ev is not None:
@@ -113,6 +134,10 @@ class AgentSchedule:
         self.torch.cuda.synchronize(self.dev)
         if int(self.pack_err.max().item()) != 0:
             raise RuntimeError("keyframe pack clamped a count (slot capacity)")
+
+    def frame_index(self, p, b):
+        """index into the host frames (frames_np) of frame b of graph p in the last step's batch"""
+        return (self.last_batch or 0) * self.B + p * self.sub + b
 
     def frame_results(self, p, b):
         """(keypoints, descriptors, match12 vs frame b-1 of the same graph) of frame b of graph p"""

@@ -102,6 +102,10 @@ int orbx_get_levels(const orbx_handle* h);
 float orbx_get_scale_factor(const orbx_handle* h);
 int orbx_get_scale_tables(const orbx_handle* h, float* scale, float* inv_scale, float* sigma2,
                           float* inv_sigma2);
+/* The same four tables from the ctor arguments alone, host-only (no device, no handle): the
+ * drop-in ORBextractor answers its getters from these even when no device is usable. */
+int orbx_compute_scale_tables(const orbx_params* params, float* scale, float* inv_scale, float* sigma2,
+                              float* inv_sigma2);
 /* mnFeaturesPerLevel (ORBextractor.cc:435-446) and umax (ORBextractor.cc:454-469, 16
  * entries) -- exposed for tests. */
 int orbx_get_feature_split(const orbx_handle* h, int32_t* per_level, int32_t* umax16);
@@ -576,6 +580,12 @@ int orbx_synth_frames_shifted(int agent, int t0, int count, int width, int heigh
  * number of profiled extraction calls. */
 int orbx_profile_enable(orbx_handle* h, int on);
 int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls);
+
+/* Test hook: the stages in `mask` (bit k of {pyramid, fast_cells, octree, blur, describe}) are not
+ * launched by subsequent batched extractions of this handle (0 = every stage runs, the default). A
+ * skipped stage leaves its buffers as the previous call left them; the tests use it to prove that
+ * the bench's self-check detects a stage that stopped launching. */
+int orbx_debug_skip_stages(orbx_handle* h, int mask);
 
 /* Test hook: the device's restatement of glibc sinf/cosf (used by computeOrbDescriptor,
  * ORBextractor.cc:113) applied to n device floats; lets tests compare against host libm. */

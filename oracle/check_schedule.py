@@ -33,9 +33,11 @@ def host_threads():
 
 
 def check_schedule(sched, frames_np, samples=None, agent_frames=None, threads=None, nfeatures=None):
-    """samples: list of (graph p, frame b) to check (default: first, middle and last frame of each
-    graph, plus each one's predecessor so the match row can be recomputed); agent_frames(r) -> the
-    keyframe image of agent r (default: frames_np[0] for every agent, i.e. world 1).
+    """Checks the LAST step's batch (sched.last_batch of its frame pool). samples: list of (graph p,
+    frame b) to check (default: first, middle and last frame of each graph, plus each one's
+    predecessor so the match row can be recomputed); agent_frames(r, t) -> the keyframe image of
+    agent r, t = the host frame index of this agent's keyframe (default: frames_np[t] for every
+    agent, i.e. world 1).
     Returns dict(bit_exact, checked_frames, checked_pairs, checked_slots, mismatches[...])."""
     import orbamd
     sub = sched.sub
@@ -57,7 +59,7 @@ def check_schedule(sched, frames_np, samples=None, agent_frames=None, threads=No
 
     threads = threads or host_threads()
     with ThreadPoolExecutor(max_workers=threads) as ex_pool:
-        outs = list(ex_pool.map(lambda pb: extract(frames_np[pb[0] * sub + pb[1]]), need))
+        outs = list(ex_pool.map(lambda pb: extract(frames_np[sched.frame_index(*pb)]), need))
     for pb, o in zip(need, outs):
         local[pb] = o
     mism = []
@@ -72,20 +74,24 @@ def check_schedule(sched, frames_np, samples=None, agent_frames=None, threads=No
         v2 = orbamd.KeyFrameView(kp, dp, tabs["scale"], tabs["sigma2"])
         _, mo = oracle_py.search_for_triangulation(v1, v2, F12, ex, ey, False, False)
         if not np.array_equal(mg, mo):
-            mism.append("match p=%d b=%d vs b-1: %d entries differ" % (p, b, int((mg != mo).sum())))
+            mism.append("match p=%d b=%d vs b-1: %s" % (p, b, "%d entries differ" % int((mg != mo).sum())
+                                                        if mg.shape == mo.shape else "length %d vs %d" % (len(mg), len(mo))))
     nslots = 0
     if sched.exchange_on:
         xm, xn = sched.exchange_results()
-        kq, dq = local.get((0, 0)) or extract(frames_np[0])
+        t_kf = sched.frame_index(0, 0)
+        kq, dq = local.get((0, 0)) or extract(frames_np[t_kf])
         vq = orbamd.KeyFrameView(kq, dq, tabs["scale"], tabs["sigma2"])
         for r in range(sched.world):
-            img = frames_np[0] if agent_frames is None else agent_frames(r)
+            img = frames_np[t_kf] if agent_frames is None else agent_frames(r, t_kf)
             kr, dr = extract(img) if agent_frames is not None else (kq, dq)
             vr = orbamd.KeyFrameView(kr, dr, tabs["scale"], tabs["sigma2"])
             n_o, mo = oracle_py.search_for_triangulation(vq, vr, F12, ex, ey, False, False)
             if not np.array_equal(xm[r], mo) or int(xn[r]) != int(n_o):
-                mism.append("cross-agent match vs agent %d: %d entries differ, count %d vs %d"
-                            % (r, int((xm[r] != mo).sum()), int(xn[r]), int(n_o)))
+                ndiff = int((xm[r] != mo).sum()) if xm[r].shape == mo.shape else -1
+                mism.append("cross-agent match vs agent %d: %s, count %d vs %d"
+                            % (r, "%d entries differ" % ndiff if ndiff >= 0 else
+                               "%d vs %d query keypoints" % (len(xm[r]), len(mo)), int(xn[r]), int(n_o)))
             nslots += 1
     return {"bit_exact": not mism, "checked_frames": len(samples), "checked_pairs": len(samples),
             "checked_slots": nslots, "mismatches": mism[:8]}

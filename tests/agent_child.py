@@ -34,7 +34,7 @@ def main():
     sched.step(first=False)
     torch.cuda.synchronize()
     sched.check_errors()
-    res = check_schedule(sched, frames, agent_frames=lambda r: orbamd.synth_frames(r, 0, 1, W, H)[0])
+    res = check_schedule(sched, frames, agent_frames=lambda r, t: orbamd.synth_frames(r, t, 1, W, H)[0])
     xm, xn = sched.exchange_results()
     print("rank", rank, res, "cross-agent matches", list(xn), flush=True)
     assert res["bit_exact"], res["mismatches"]

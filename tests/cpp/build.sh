@@ -9,9 +9,21 @@ g++ -std=c++14 -O1 -pthread -Wall -Wno-unused-function \
   "$R/cooperative-orb-slam_amd/host/ORBmatcher_amd.cc" "$R/cooperative-orb-slam_amd/host/ORBmatcher_base_amd.cc" \
   "$R/cooperative-orb-slam_amd/host/ORBmatcher_projection_amd.cc" "$R/cooperative-orb-slam_amd/host/Frame_stereo_amd.cc" \
   "$R/cooperative-orb-slam_amd/host/MapPoint_distinctive_amd.cc" "$R/cooperative-orb-slam_amd/host/Frame_bow_amd.cc" \
+  "$R/cooperative-orb-slam_amd/host/orbamd_status.cc" \
   -L "$R/cooperative-orb-slam_amd/lib" -lorbamd -L "$R/oracle/build" -lorb_oracle \
   -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,"$R/oracle/build" -Wl,-rpath,/opt/rocm/lib \
   -o "$R/tests/cpp/build/test_dropin"
+# the drop-ins without a usable device (CPU: must not throw, reference "nothing found" results)
+g++ -std=c++14 -O1 -pthread -Wall -Wno-unused-function \
+  -I "$R/tests/cpp/cvmin" -I "$R/tests/cpp/mock" -I "$R/cooperative-orb-slam_amd/host" -I "$R/include" \
+  "$R/tests/cpp/test_nodevice.cpp" "$R/cooperative-orb-slam_amd/host/ORBextractor.cc" \
+  "$R/cooperative-orb-slam_amd/host/ORBmatcher_amd.cc" "$R/cooperative-orb-slam_amd/host/ORBmatcher_base_amd.cc" \
+  "$R/cooperative-orb-slam_amd/host/ORBmatcher_projection_amd.cc" "$R/cooperative-orb-slam_amd/host/Frame_stereo_amd.cc" \
+  "$R/cooperative-orb-slam_amd/host/MapPoint_distinctive_amd.cc" "$R/cooperative-orb-slam_amd/host/Frame_bow_amd.cc" \
+  "$R/cooperative-orb-slam_amd/host/orbamd_status.cc" \
+  -L "$R/cooperative-orb-slam_amd/lib" -lorbamd \
+  -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,/opt/rocm/lib \
+  -o "$R/tests/cpp/build/test_nodevice"
 # the slot codec (host only, no GPU needed to run)
 g++ -std=c++14 -O1 -Wall -Wno-unused-function \
   -I "$R/tests/cpp/cvmin" -I "$R/tests/cpp/mock" -I "$R/cooperative-orb-slam_amd/host" -I "$R/include" \

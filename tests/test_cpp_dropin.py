@@ -27,6 +27,18 @@ def test_dropin_bit_exact_on_gpu():
     assert r.returncode == 0 and "ALL PASS" in r.stdout
 
 
+def test_dropins_do_not_throw_without_device():
+    """ORBX_EDEVICE from every C ABI call (ORBAMD_DEVICE=99 is out of range on any box): each drop-in returns
+    the reference's "nothing found" result and logs the status instead of throwing into the caller's thread"""
+    _build()
+    env = dict(os.environ, ORBAMD_DEVICE="99")
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "build", "test_nodevice")], capture_output=True,
+                       text=True, timeout=120, env=env)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0 and "ALL PASS" in r.stdout
+    assert "orbslam_amd: orbx_create failed (status -2, device)" in r.stderr
+
+
 def test_slot_codec_roundtrip_cpp():
     """host/KeyFrameSlot_amd.*: receiveKeyframeInfo -> slot -> receiveKeyframeInfo, field for field (CPU)"""
     _build()

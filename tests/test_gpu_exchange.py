@@ -155,12 +155,15 @@ def test_slot_match_equals_oracle(use_bow):
     # query = frame 0 (stereo + MapPoints + FeatureVector); slots = frames 1..3 of agents 0..2
     kq, dq = frames[0]
     eq = _extras(rng, kq)
+    eq["fv"] = _desc_fv(dq)
     srcq, keepq = _device_source(torch, kq, dq, eq)
     slots = torch.zeros(nref * exchange.slot_bytes(cap), dtype=torch.uint8, device="cuda")
     decs = []
     for r in range(nref):
         k, d = frames[1 + r]
         e = _extras(rng, k) if r != 1 else ({"fv": _extras(rng, k)["fv"]} if use_bow else {})  # slot 1 mono
+        if "fv" in e:
+            e["fv"] = _desc_fv(d)  # node ids shared with the query's (common nodes to match over)
         host = exchange.pack_host(_meta(r, tabs), k, d, cap, **e)
         slots[r * host.size:(r + 1) * host.size].copy_(torch.from_numpy(host))
         decs.append(exchange.parse(host))
@@ -204,6 +207,106 @@ def test_slot_match_equals_oracle(use_bow):
     assert np.all(out2[1].cpu().numpy() == -1) and int(nm[1].item()) == 0
     assert torch.equal(out2[0], out[0]) and torch.equal(out2[2], out[2])
     mh.close()
+
+
+def _rot(ax, ay, az):
+    cx, cy, cz, sx, sy, sz = np.cos(ax), np.cos(ay), np.cos(az), np.sin(ax), np.sin(ay), np.sin(az)
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    return (Rz @ Ry @ Rx).astype(np.float32)
+
+
+def _desc_fv(d):
+    """a FeatureVector that, like a vocabulary, tends to put similar descriptors in the same node: node =
+    100 + the top 4 bits of descriptor byte 0 (CSR: ascending node ids, ascending features in a node)"""
+    node = 100 + (d[:, 0] >> 4).astype(np.int64)
+    ids = np.unique(node)
+    feats = [np.nonzero(node == i)[0] for i in ids]
+    off = np.concatenate([[0], np.cumsum([len(f) for f in feats])]).astype(np.int32)
+    return ids.astype(np.uint32), off, np.concatenate(feats).astype(np.int32)
+
+
+@pytest.mark.parametrize("use_bow", [False, True])
+def test_eight_agent_slots_equal_oracle(use_bow):
+    """C5 at 8 agents on one GPU: 8 slots packed from 8 different agents' keyframes (synthetic streams of
+    agents 0..7), each slot with its own pose (F12 / epipole), mixing stereo, mono, MapPoints and BoW
+    FeatureVectors; the product slot matcher over all 8 (one launch) equals the oracle's
+    SearchForTriangulation (ORBmatcher.cc:657-823) row by row, BF and over common BoW nodes."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(88)
+    nref, cap = 8, 1100
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    tabs = orc.tables()
+    kq, dq = orc(orbamd.synth_frames(9, 3, 1, 640, 480)[0])   # the querying agent's keyframe
+    eq = _extras(rng, kq)
+    eq["fv"] = _desc_fv(dq)
+    srcq, keepq = _device_source(torch, kq, dq, eq)
+    sb = exchange.slot_bytes(cap)
+    slots = torch.zeros(nref * sb, dtype=torch.uint8, device="cuda")
+    decs = []
+    for r in range(nref):
+        k, d = orc(orbamd.synth_frames(r, 5 * r, 1, 640, 480)[0])  # agent r's own keyframe
+        kind = r % 4  # 0 full (stereo + MapPoints + BoW), 1 mono + BoW only, 2 stereo without MapPoints, 3 mono bare
+        e = _extras(rng, k)
+        e["fv"] = _desc_fv(d)
+        if kind == 1:
+            e = {"fv": e["fv"], "bow": e["bow"]}
+        elif kind == 2:
+            e.pop("mp_flags"), e.pop("mp_pos")
+        elif kind == 3:
+            e = {"fv": e["fv"]} if use_bow else {}
+        host = exchange.pack_host(_meta(r, tabs), k, d, cap, **e)
+        slots[r * sb:(r + 1) * sb].copy_(torch.from_numpy(host))
+        decs.append(exchange.parse(host))
+    K = np.array([[orbamd.device.FX, 0, orbamd.device.CX], [0, orbamd.device.FY, orbamd.device.CY], [0, 0, 1]],
+                 np.float32)
+    geos = []
+    for r in range(nref):
+        R = _rot(*(rng.standard_normal(3) * 0.02))
+        t = (rng.standard_normal(3) * 0.08).astype(np.float32)
+        F12 = orbamd.matcher.compute_f12(np.eye(3, dtype=np.float32), np.zeros(3, np.float32), R, t, K, K)
+        ex, ey = orbamd.epipole(R, t, np.zeros(3, np.float32), orbamd.device.FX, orbamd.device.FY,
+                                orbamd.device.CX, orbamd.device.CY)
+        geos.append((F12, ex, ey))
+    mh = orbamd.ORBmatcher(0.6, False)
+    out = torch.empty((nref, cap), dtype=torch.int32, device="cuda")
+    nm = torch.zeros(nref, dtype=torch.int32, device="cuda")
+    exchange.match_slots_device(mh._h, srcq, cap, nref, slots, sb, geos, out, nm, use_bow=use_bow,
+                                max_nodes=len(eq["fv"][0]))
+    torch.cuda.synchronize()
+    assert orbamd.load().orbm_check_error(mh._h, None) == 0
+    got, gn = out.cpu().numpy(), nm.cpu().numpy()
+    nonzero = 0
+    for r in range(nref):
+        no, mo = _oracle_slot_match(kq, dq, eq, decs[r], geos[r], use_bow)
+        np.testing.assert_array_equal(got[r, :len(kq)], mo, err_msg="slot %d" % r)
+        assert int(gn[r]) == no, (r, int(gn[r]), no)
+        assert np.all(got[r, len(kq):] == -1)
+        nonzero += no > 0
+    assert nonzero >= 6, "most slots should produce matches"
+    mh.close()
+
+
+def test_bench_rccl_world1():
+    """bench.py under torch.distributed.run with one rank and --dist: the RCCL process group (init with
+    device_id), the out-of-place all_gather_into_tensor of the keyframe slot on the graph stream and the
+    cross-agent match from the receive buffer, as at N>1; the run's self-check must be bit-exact."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--dist", "--steps", "4",
+           "--warmup", "2", "--batch", "256", "--pipes", "2", "--no-cpu", "--sustain", "0", "--ingest-steps", "4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    print(r.stdout[-3000:], r.stderr[-3000:])
+    assert r.returncode == 0
+    import json
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["collective"].startswith("rccl"), res["collective"]
+    assert res["bit_exact"] is True and res["checked_slots"] == 1 and res["device_errors"] is None
+    assert res["ingest"]["bit_exact"] is True
+    assert res["stage_ms_per_step"]["allgather"] > 0
 
 
 def _free_port():

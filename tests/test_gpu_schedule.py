@@ -32,3 +32,32 @@ def test_bench_schedule_bit_exact(W, H, nf, B, P):
     assert res["checked_frames"] == B and res["checked_slots"] == 1
     assert all(int(pp.nmatch.min().item()) > 0 for pp in sched.pipes)
     sched.close()
+
+
+@pytest.mark.parametrize("stage", [2, 16])  # fast_cells, describe (orbx_debug_skip_stages bits)
+def test_skipped_stage_fails_the_self_check(stage):
+    """The bench's stale-output guard: with a 2-batch frame pool a stage that stops launching leaves the
+    previous step's (different) outputs and the oracle check fails; with one repeated batch it would not."""
+    torch = pytest.importorskip("torch")
+    from orbamd.agent import AgentSchedule
+    W, H, B, P = 640, 480, 64, 2
+    lib = orbamd.load()
+    for pool in (2, 1):
+        frames = orbamd.synth_frames(0, 0, pool * B, W, H)
+        sched = AgentSchedule(torch, frames, W, H, P, device=0, nfeatures=1000, pool=pool)
+        sched.step()
+        sched.step(first=False)
+        torch.cuda.synchronize()
+        assert check_schedule(sched, frames)["bit_exact"]
+        for pp in sched.pipes:
+            assert lib.orbx_debug_skip_stages(pp.ext._h, stage) == 0
+        sched.step(first=False)  # the stage does not launch in this step
+        torch.cuda.synchronize()
+        res = check_schedule(sched, frames)
+        for pp in sched.pipes:
+            lib.orbx_debug_skip_stages(pp.ext._h, 0)
+        if pool == 2:
+            assert not res["bit_exact"] and res["mismatches"], "a skipped stage must fail the check"
+        else:
+            assert res["bit_exact"]  # repeated frames hide it: why bench.py uses --pool 2
+        sched.close()

@@ -4,7 +4,7 @@ mkdir -p gpurun_out
 for v in "$@"; do
   ORBAMD_LIB_VARIANT=$v timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_match.py tests/test_cpp_dropin.py > gpurun_out/lat_test_$v.log 2>&1
   rc=$?; echo "variant $v parity rc=$rc: $(tail -n 1 gpurun_out/lat_test_$v.log)"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  if [ $rc -ne 0 ]; then exit $rc; fi  # a variant with broken parity is not timed
 done
 for r in 1 2; do
   for v in "$@"; do
