@@ -1718,22 +1718,25 @@ bool frame_view_ok(const orbm_frame_view* F) {
 #define ORBX_PROJ_DIRECT 1  // Fuse: results written by the scan kernel (0: through k_proj_resolve)
 #endif
 constexpr bool kProjDirect = ORBX_PROJ_DIRECT != 0;
+/* init_n >= 0: SearchForInitialization (k_init_resolve) with F = F2 and match[] = vnMatches12 of F1's init_n
+ * keypoints; otherwise match[] has F->n entries */
 int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb, int accept_th, int ratio,
                    float nnratio, int check_ori, int32_t* match, int* nmatches, const float* inv_sigma2 = nullptr,
-                   int32_t* qres = nullptr) {
+                   int32_t* qres = nullptr, int init_n = -1) {
     HIPR(hipSetDevice(ctx->device));
     const size_t n = (size_t)F->n, nq = pb.q.size();
+    const size_t nout = init_n >= 0 ? (size_t)init_n : n;
     // inputs first (staged in pinned memory, one H2D copy), then outputs (one D2H copy), then scratch
     Carve cv;
     const size_t o_call = cv.take(sizeof(ProjCall)), o_x = cv.take(4 * n), o_y = cv.take(4 * n),
                  o_ang = cv.take(4 * n), o_ur = cv.take(4 * n), o_oct = cv.take(4 * n), o_occ = cv.take(n),
                  o_desc = cv.take(32 * n), o_q = cv.take(sizeof(ProjQuery) * nq), o_qd = cv.take(32 * nq);
     const size_t in_bytes = cv.off;
-    const size_t o_nm = cv.take(4 * n + 4);  // nmatches, then match[n]
+    const size_t o_nm = cv.take(4 * nout + 4);  // nmatches, then match[nout]
     const size_t o_gs = cv.take(4 * (kGridCols * kGridRows + 1)), o_gi = cv.take(2 * n), o_scan = cv.take(32 * nq),
                  o_scnt = cv.take(4 * nq), o_res = cv.take(8 * nq);
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
-    uint8_t* hp = ctx->ensure_pinned(in_bytes + std::max(4 * n + 4, 8 * nq));
+    uint8_t* hp = ctx->ensure_pinned(in_bytes + std::max(4 * nout + 4, 8 * nq));
     if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
     hipStream_t st = ctx->stream;
@@ -1762,6 +1765,7 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     bool claims = false;
     for (const ProjQuery& q : pb.q) claims |= (q.flags & kProjClaims) != 0;
     c.direct = kProjDirect && qres && !ratio && !c.check_ori && !claims;
+    c.n_out = (int)nout;
     c.grid_start = (int*)(base + o_gs);
     c.grid_idx = (uint16_t*)(base + o_gi);
     c.scan = (unsigned long long*)(base + o_scan);
@@ -1786,7 +1790,7 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
         memcpy(hp + o_qd, pb.qdesc.data(), 32 * nq);
     }
     HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, st));
-    HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st, !c.direct));
+    HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st, !c.direct, init_n >= 0));
     uint8_t* ho = hp + in_bytes;
     if (qres) {
         // per-query results (Fuse): res[2 qi] = the accepted feature or -1, reported at the query's src
@@ -1795,9 +1799,9 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
         for (size_t qi = 0; qi < nq; qi++) qres[pb.q[qi].src] = ((const int32_t*)ho)[2 * qi];
         return 0;
     }
-    HIPR(hipMemcpyAsync(ho, base + o_nm, 4 * n + 4, hipMemcpyDeviceToHost, st));
+    HIPR(hipMemcpyAsync(ho, base + o_nm, 4 * nout + 4, hipMemcpyDeviceToHost, st));
     HIPR(hipStreamSynchronize(st));
-    if (n) memcpy(match, ho + 4, 4 * n);
+    if (nout) memcpy(match, ho + 4, 4 * nout);
     if (nmatches) memcpy(nmatches, ho, 4);
     return 0;
 }
@@ -2084,6 +2088,112 @@ int orbm_fuse_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, const float Scw[16]
 /* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307), batched                 */
 /* ===================================================================================== */
 extern "C" {
+
+/* ORBmatcher::SearchForInitialization (ORBmatcher.cc:405-520): one query per F1 keypoint of octave <= 0
+ * (level1 > 0 skips, :421-423) over F2's grid, window prev_xy[i1] +- windowSize at level level1 (:425);
+ * the in-order resolution on the device (k_init_resolve). prev_xy is updated for the matched i1 (:514-517). */
+int orbm_search_for_initialization(orbm_ctx* ctx, const orbm_frame_view* F1, const orbm_frame_view* F2, float* prev_xy,
+                                   int window_size, float nnratio, int check_ori, int32_t* match12, int* nmatches) {
+    if (!ctx || !frame_view_ok(F1) || !frame_view_ok(F2) || (F1->n && (!prev_xy || !match12)) ||
+        (check_ori && ((F1->n && !F1->angle) || (F2->n && !F2->angle))))
+        return ORBX_EARG;
+    if (F1->n > init_max_features() || F2->n > init_max_features()) return ORBX_ECAPACITY;
+    ProjBatch pb;
+    for (int i1 = 0; i1 < F1->n; i1++) {
+        const int level1 = F1->octave[i1];
+        if (level1 > 0) continue;
+        pb.add(make_query(prev_xy[2 * i1], prev_xy[2 * i1 + 1], (float)window_size, level1, level1, 0.f, 0.f,
+                          check_ori ? F1->angle[i1] : 0.f, 0, i1),
+               F1->desc + 32 * (size_t)i1);
+    }
+    int nm = 0;
+    int rc = run_projection(ctx, F2, pb, 50 /*TH_LOW*/, 1, nnratio, check_ori, match12, &nm, nullptr, nullptr, F1->n);
+    if (rc) return rc;
+    for (int i1 = 0; i1 < F1->n; i1++)  // :514-517
+        if (match12[i1] >= 0) {
+            prev_xy[2 * i1] = F2->x[match12[i1]];
+            prev_xy[2 * i1 + 1] = F2->y[match12[i1]];
+        }
+    if (nmatches) *nmatches = nm;
+    return 0;
+}
+
+/* one direction of SearchBySim3 (ORBmatcher.cc:1148-1225, 1228-1305): the prologue of each MapPoint of the
+ * source keyframe on the host (reference float semantics), the windowed first-strict-minimum search with
+ * the octave band [nPredictedLevel-1, nPredictedLevel] on the device (per-query results, no claims) */
+static int sim3_direction(orbm_ctx* ctx, const orbm_frame_view* KF, const float* Tsw, const orbm_mappoints* mp,
+                          const float* sR, const float* t, float fx, float fy, float cx, float cy, float th,
+                          int32_t* vnMatch) {
+    const float Rsw[9] = {Tsw[0], Tsw[1], Tsw[2], Tsw[4], Tsw[5], Tsw[6], Tsw[8], Tsw[9], Tsw[10]};
+    const float tsw[3] = {Tsw[3], Tsw[7], Tsw[11]};
+    ProjBatch pb;
+    for (int i = 0; i < mp->n; i++) {
+        vnMatch[i] = -1;
+        if (flag(mp->skip, i) || flag(mp->bad, i)) continue;  // :1152-1156
+        const float* p3Dw = mp->pos + 3 * (size_t)i;
+        float p3Dcs[3], p3Dct[3];
+        gemm33_fast(Rsw, 3, p3Dw, tsw, p3Dcs);
+        gemm33_fast(sR, 3, p3Dcs, t, p3Dct);
+        if (p3Dct[2] < 0.0) continue;
+        const float invz = 1.0 / p3Dct[2];
+        const float x = p3Dct[0] * invz;
+        const float y = p3Dct[1] * invz;
+        const float u = fx * x + cx;
+        const float v = fy * y + cy;
+        if (!(u >= KF->min_x && u < KF->max_x && v >= KF->min_y && v < KF->max_y)) continue;  // IsInImage
+        const float maxDistance = 1.2f * mp->max_dist[i];
+        const float minDistance = 0.8f * mp->min_dist[i];
+        const float dist3D = norm3(p3Dct);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[i], dist3D, KF);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        pb.add(make_query(u, v, radius, nPredictedLevel - 1, nPredictedLevel, 0.f, 0.f, 0.f, 0, i),
+               mp->desc + 32 * (size_t)i);
+    }
+    if (pb.q.empty()) return 0;
+    return run_projection(ctx, KF, pb, 100 /*TH_HIGH*/, 0, 0.f, 0, nullptr, nullptr, nullptr, vnMatch);
+}
+
+/* ORBmatcher::SearchBySim3 (ORBmatcher.cc:1102-1326) */
+int orbm_search_by_sim3(orbm_ctx* ctx, const orbm_frame_view* KF1, const float T1w[16], const orbm_mappoints* mp1,
+                        const orbm_frame_view* KF2, const float T2w[16], const orbm_mappoints* mp2, float s12,
+                        const float R12[9], const float t12[3], float th, int32_t* match12, int* nfound) {
+    auto mp_ok = [](const orbm_mappoints* m) {
+        return m && m->n >= 0 && (m->n == 0 || (m->desc && m->pos && m->min_dist && m->max_dist));
+    };
+    if (!ctx || !frame_view_ok(KF1) || !frame_view_ok(KF2) || !T1w || !T2w || !mp_ok(mp1) || !mp_ok(mp2) || !R12 ||
+        !t12 || (mp1->n && !match12) || !(s12 != 0.f))
+        return ORBX_EARG;
+    // sR12 = s12*R12, sR21 = (1.0/s12)*R12.t() (convertTo with a float scale), t21 = -sR21*t12 (small-matrix
+    // gemm, alpha = -1) (:1119-1121)
+    float sR12[9], sR21[9], t21[3];
+    const float inv_s = (float)(1.0 / (double)s12);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            sR12[3 * r + c] = R12[3 * r + c] * s12;
+            sR21[3 * r + c] = R12[3 * c + r] * inv_s;
+        }
+    for (int r = 0; r < 3; r++) {
+        const float t0 = sR21[3 * r] * t12[0] + sR21[3 * r + 1] * t12[1] + sR21[3 * r + 2] * t12[2];
+        t21[r] = (float)((double)t0 * -1.0);
+    }
+    std::vector<int32_t> m1((size_t)mp1->n + 1), m2((size_t)mp2->n + 1);
+    // both directions project with pKF1's camera (:1105-1108, 1250-1251)
+    int rc = sim3_direction(ctx, KF2, T1w, mp1, sR21, t21, KF1->fx, KF1->fy, KF1->cx, KF1->cy, th, m1.data());
+    if (!rc) rc = sim3_direction(ctx, KF1, T2w, mp2, sR12, t12, KF1->fx, KF1->fy, KF1->cx, KF1->cy, th, m2.data());
+    if (rc) return rc;
+    int nFound = 0;
+    for (int i1 = 0; i1 < mp1->n; i1++) {  // :1310-1323
+        const int idx2 = m1[i1];
+        match12[i1] = -1;
+        if (idx2 >= 0 && idx2 < mp2->n && m2[idx2] == i1) {
+            match12[i1] = idx2;
+            nFound++;
+        }
+    }
+    if (nfound) *nfound = nFound;
+    return 0;
+}
 
 int orbm_compute_distinctive_descriptors_device(orbm_ctx* ctx, int npoints, const int32_t* d_offsets,
                                                 const uint8_t* d_desc, int32_t* d_best_idx, uint8_t* d_out_desc,

@@ -26,6 +26,9 @@
  *              wave commits 64 queries at a time up to the first such conflict, re-scans that
  *              one query against the live occupancy bitmap, and continues. Then the rotation
  *              histogram + ComputeThreeMaxima (ORBmatcher.cc:1437-1467, 1601-1642).
+ *   k_init_resolve
+ *              SearchForInitialization (ORBmatcher.cc:405-520) on the same grid + scan: in-order
+ *              resolution against vMatchedDistance (accepts may take a feature from an earlier query).
  *   k_distinctive
  *              MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of
  *              MapPoints: one wave per MapPoint, row i of the Hamming distance matrix in LDS,
@@ -419,9 +422,15 @@ __device__ __forceinline__ void topk_insert(unsigned long long k, unsigned long 
     }
 }
 
-template <int G, int K, class Occ>
+struct AnyDist {
+    __device__ bool operator()(int, int) const { return true; }
+};
+
+/* elig(idx, dist): a candidate-specific filter after the distance (SearchForInitialization's
+ * vMatchedDistance[i2] > dist test, ORBmatcher.cc:444-445) */
+template <int G, int K, class Occ, class Elig = AnyDist>
 __device__ __forceinline__ int proj_scan(const ProjCall& c, const ProjQuery& q, const uint4 qd0, const uint4 qd1, int gl,
-                                         Occ occupied, unsigned long long (&top)[K]) {
+                                         Occ occupied, unsigned long long (&top)[K], Elig elig = Elig()) {
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = kNoKey;
     int ncand = 0;
@@ -463,7 +472,7 @@ __device__ __forceinline__ int proj_scan(const ProjCall& c, const ProjQuery& q, 
                 const int dist = __popc(qd0.x ^ f0.x) + __popc(qd0.y ^ f0.y) + __popc(qd0.z ^ f0.z) +
                                  __popc(qd0.w ^ f0.w) + __popc(qd1.x ^ f1.x) + __popc(qd1.y ^ f1.y) +
                                  __popc(qd1.z ^ f1.z) + __popc(qd1.w ^ f1.w);
-                if (dist < 256) {  // bestDist starts at 256 (ORBmatcher.cc:78, 349, 1397, 1550)
+                if (dist < 256 && elig(idx, dist)) {  // bestDist starts at 256 (ORBmatcher.cc:78, 349, 1397, 1550)
                     topk_insert<K>(((unsigned long long)dist << 40) | ((unsigned long long)k << 16) | (unsigned)idx, top);
                     ncand++;
                 }
@@ -722,10 +731,166 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
     if (lane == 0) *c.nmatches = nacc;
 }
 
-hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st, bool resolve) {
+/* ============================ SearchForInitialization ============================ */
+
+/* ORBmatcher::SearchForInitialization (ORBmatcher.cc:405-520) after k_grid + k_proj_scan over F2 with one
+ * query per level-0 keypoint of F1 (window vbPrevMatched[i1] +- windowSize, levels 0..0, q.src = i1).
+ * The reference visits i1 in order; a candidate i2 is usable iff dist < vMatchedDistance[i2] (the best
+ * distance it was matched with so far, :444-445), and an accept steals i2 from its previous i1 (:463-467).
+ * vMatchedDistance only decreases, so a query's ineligible list entries stay ineligible: its decision
+ * (best = first usable entry of its top-K list, best2 = the next one) can only change if an earlier query
+ * takes its best or second entry. One wave, chunks of 64 queries: lanes commit in order up to the first
+ * lane whose best / second entry an earlier uncommitted lane of the chunk takes (LDS claim table), that
+ * lane is re-evaluated next round; a lane whose usable entries ran out in a truncated list is re-scanned
+ * by the whole wave against the live vMatchedDistance. Then the rotation histogram over every accept
+ * (stolen matches stay in their bins, :482) + ComputeThreeMaxima (:489-512). Writes vnMatches12 to
+ * c.match[0 .. c.n_out) and nmatches. */
+constexpr int kInitMaxN = 8192;
+
+__global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict__ calls) {
+    __shared__ uint16_t s_md[kInitMaxN];   // vMatchedDistance (0xffff = INT_MAX)
+    __shared__ int16_t s_v21[kInitMaxN];   // vnMatches21
+    __shared__ int16_t s_v12[kInitMaxN];   // vnMatches12
+    __shared__ int s_claim[kClaimTab];
+    __shared__ int s_hist[32];
+    const ProjCall& c = calls[blockIdx.x];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < c.n; i += 64) {
+        s_md[i] = 0xffff;
+        s_v21[i] = -1;
+    }
+    for (int i = lane; i < c.n_out; i += 64) s_v12[i] = -1;
+    for (int i = lane; i < kClaimTab; i += 64) s_claim[i] = 64;
+    if (lane < 32) s_hist[lane] = 0;
+    wave_lds_sync();
+    auto usable = [](int idx, int dist) { return dist < (int)s_md[idx]; };
+    // accept rule (:459-461): bestDist <= TH_LOW and bestDist < (float)bestDist2 * mfNNratio, bestDist2 =
+    // INT_MAX when there is no second usable candidate
+    auto accept = [&](unsigned long long b, unsigned long long s2) {
+        if (b == kNoKey) return false;
+        const int d1 = (int)(b >> 40);
+        const float d2 = s2 != kNoKey ? (float)(int)(s2 >> 40) : 2147483647.0f;
+        return d1 <= 50 && (float)d1 < __fmul_rn(d2, c.nnratio);
+    };
+    auto commit = [&](int qi, int i1, unsigned long long b, float qang) {
+        const int i2 = (int)(b & 0xffff);
+        const int prev = s_v21[i2];
+        if (prev >= 0) s_v12[prev] = -1;
+        s_v12[i1] = (int16_t)i2;
+        s_v21[i2] = (int16_t)i1;
+        s_md[i2] = (uint16_t)(b >> 40);
+        c.res[2 * qi] = i2;
+        c.res[2 * qi + 1] = c.check_ori ? rot_bin(qang, c.angle[i2]) : 0;
+    };
+    for (int base = 0; base < c.nq; base += 64) {
+        const int qi = base + lane;
+        const bool in = qi < c.nq;
+        unsigned long long top[kProjTopK];
+        int ncand = 0, src = 0;
+        float qang = 0.f;
+#pragma unroll
+        for (int k = 0; k < kProjTopK; k++) top[k] = in ? c.scan[(long long)kProjTopK * qi + k] : kNoKey;
+        if (in) {
+            ncand = c.scan_cnt[qi];
+            src = c.q[qi].src;
+            qang = c.q[qi].angle;
+        }
+        int done = 0;
+        while (done < 64 && base + done < c.nq) {
+            const bool act = in && lane >= done;
+            unsigned long long b = kNoKey, s2 = kNoKey;
+            int found = 0;
+#pragma unroll
+            for (int t = 0; t < kProjTopK; t++) {
+                const unsigned long long k = top[t];
+                if (k == kNoKey || !usable((int)(k & 0xffff), (int)(k >> 40))) continue;
+                if (found == 0) b = k; else if (found == 1) s2 = k;
+                found++;
+            }
+            const bool rescan = act && found < 2 && ncand > kProjTopK;
+            const bool acc = act && !rescan && accept(b, s2);
+            const int bi = b != kNoKey ? (int)(b & 0xffff) : -1;
+            const int si = s2 != kNoKey ? (int)(s2 & 0xffff) : -1;
+            if (acc) atomicMin(&s_claim[bi & (kClaimTab - 1)], lane);
+            wave_lds_sync();
+            bool dirty = rescan;
+            if (act && bi >= 0 && s_claim[bi & (kClaimTab - 1)] < lane) dirty = true;
+            if (act && si >= 0 && s_claim[si & (kClaimTab - 1)] < lane) dirty = true;
+            const unsigned long long dm = __ballot(act && dirty);
+            const int d = dm ? __ffsll((long long)dm) - 1 : 64;
+            wave_lds_sync();
+            if (acc) s_claim[bi & (kClaimTab - 1)] = 64;
+            if (act && lane < d) {
+                if (acc) commit(qi, src, b, qang);
+                else c.res[2 * qi] = -1;
+            }
+            wave_lds_sync();
+            if (d < 64 && __shfl((int)rescan, d)) {  // whole-wave re-scan of query base+d
+                const int qd = base + d;
+                const ProjQuery q = c.q[qd];
+                const uint4* qp = (const uint4*)(c.qdesc + (long long)qd * 32);
+                unsigned long long t2[2];
+                proj_scan<64, 2>(c, q, qp[0], qp[1], lane, [](int) { return false; }, t2, usable);
+                if (lane == 0) {
+                    if (accept(t2[0], t2[1])) commit(qd, q.src, t2[0], q.angle);
+                    else c.res[2 * qd] = -1;
+                }
+                wave_lds_sync();
+                done = d + 1;
+            } else {
+                done = d;
+            }
+        }
+    }
+    __threadfence();
+    if (c.check_ori) {  // every accept is in its bin, stolen ones too (:482); ComputeThreeMaxima (:1601-1642)
+        for (int q = lane; q < c.nq; q += 64)
+            if (c.res[2 * q] >= 0) atomicAdd(&s_hist[c.res[2 * q + 1]], 1);
+        wave_lds_sync();
+        int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;
+        for (int i = 0; i < 30; i++) {
+            const int sz = s_hist[i];
+            if (sz > max1) {
+                max3 = max2; max2 = max1; max1 = sz;
+                ind3 = ind2; ind2 = ind1; ind1 = i;
+            } else if (sz > max2) {
+                max3 = max2; max2 = sz;
+                ind3 = ind2; ind2 = i;
+            } else if (sz > max3) {
+                max3 = sz; ind3 = i;
+            }
+        }
+        if (max2 < __fmul_rn(0.1f, (float)max1)) {
+            ind2 = -1; ind3 = -1;
+        } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
+            ind3 = -1;
+        }
+        for (int q = lane; q < c.nq; q += 64) {  // :497-510 (a stolen i1 is already -1)
+            if (c.res[2 * q] < 0) continue;
+            const int bin = c.res[2 * q + 1];
+            if (bin != ind1 && bin != ind2 && bin != ind3) s_v12[c.q[q].src] = -1;
+        }
+        wave_lds_sync();
+    }
+    int nm = 0;
+    for (int i = lane; i < c.n_out; i += 64) {
+        const int m = s_v12[i];
+        c.match[i] = m;
+        nm += m >= 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o);
+    if (lane == 0) *c.nmatches = nm;
+}
+
+int init_max_features() { return kInitMaxN; }
+
+hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st, bool resolve,
+                             bool init) {
     hipLaunchKernelGGL(k_grid, dim3(ncalls), dim3(1024), 0, st, d_calls);
     if (max_nq > 0) hipLaunchKernelGGL(k_proj_scan, dim3((max_nq + 15) / 16, ncalls), dim3(256), 0, st, d_calls);
-    if (resolve) hipLaunchKernelGGL(k_proj_resolve, dim3(ncalls), dim3(64), 0, st, d_calls);
+    if (init) hipLaunchKernelGGL(k_init_resolve, dim3(ncalls), dim3(64), 0, st, d_calls);
+    else if (resolve) hipLaunchKernelGGL(k_proj_resolve, dim3(ncalls), dim3(64), 0, st, d_calls);
     return hipGetLastError();
 }
 

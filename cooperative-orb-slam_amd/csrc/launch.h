@@ -68,7 +68,9 @@ hipError_t launch_tri_slots(const QueryKF& q, const uint8_t* slots, long long sl
                             const orbm_slot_geom* geom, int use_bow, int max_nodes, int32_t* match,
                             int32_t* nmatches, int32_t* err, hipStream_t st);
 
-hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st, bool resolve = true);
+hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st, bool resolve = true,
+                             bool init = false);
+int init_max_features();
 hipError_t launch_distinctive(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best_idx,
                               uint8_t* out_desc, hipStream_t st);
 int stereo_lds_bytes(int cap, int nrows);

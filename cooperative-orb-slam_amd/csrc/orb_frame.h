@@ -79,6 +79,8 @@ struct ProjCall {
     int32_t* nmatches;
     int direct;                // per-query results only, no claims / ratio / rotation (Fuse): k_proj_scan writes
                                // res[] from its best key and k_proj_resolve is not launched
+    int n_out;                 // SearchForInitialization (k_init_resolve): F1's N, the length of match[] =
+                               // vnMatches12
 };
 
 }  // namespace orbamd

@@ -2,9 +2,9 @@
  * ORBmatcher.h -- drop-in replacement of ORB_SLAM2/include/ORBmatcher.h (class surface of
  * ORBmatcher.h:37-102, unchanged). The hot-path members DescriptorDistance,
  * SearchForTriangulation and both SearchByBoW overloads are defined in ORBmatcher_amd.cc, the
- * four SearchByProjection overloads and both Fuse overloads in ORBmatcher_projection_amd.cc (MI355X
- * through include/orbslam_amd.h); the remaining members (SearchForInitialization, SearchBySim3) keep
- * the reference's definitions in ORB_SLAM2/src/ORBmatcher.cc.
+ * four SearchByProjection overloads, both Fuse overloads, SearchForInitialization and SearchBySim3 in
+ * ORBmatcher_projection_amd.cc (MI355X through include/orbslam_amd.h); every public member runs on the
+ * device.
  */
 #ifndef ORBMATCHER_H
 #define ORBMATCHER_H

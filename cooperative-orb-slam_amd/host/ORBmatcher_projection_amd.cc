@@ -8,6 +8,7 @@
  * and the two Fuse overloads:
  *   Fuse(KeyFrame*, const vector<MapPoint*>&, th)                            ORBmatcher.cc:825-975
  *   Fuse(KeyFrame*, cv::Mat Scw, vpPoints, th, vpReplacePoint)               ORBmatcher.cc:977-1100
+ * and SearchForInitialization (ORBmatcher.cc:405-520) and SearchBySim3 (ORBmatcher.cc:1102-1326).
  * Each call gathers what the reference reads (keypoints, descriptors, mvuRight, grid bounds, the
  * MapPoint state through the same accessors), runs orbm_search_by_projection_* (geometry prologue
  * on the host with the reference's float semantics; grid, windowed Hamming search, in-order claims
@@ -355,6 +356,89 @@ int ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& v
         nFused++;
     }
     return nFused;
+}
+
+// ORBmatcher.cc:405-520 (Tracking::MonocularInitialization, Tracking.cc:600)
+int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& vbPrevMatched,
+                                        std::vector<int>& vnMatches12, int windowSize) {
+    const size_t n1 = F1.mvKeysUn.size();
+    vnMatches12 = std::vector<int>(n1, -1);  // :408
+    FrameSide f1, f2;
+    f1.gather(F1, nullptr, 0.f, 0.f);
+    f2.gather(F2, nullptr, 0.f, 0.f);
+    std::vector<float> prev(2 * n1 + 2);
+    for (size_t i = 0; i < n1; i++) {
+        prev[2 * i] = vbPrevMatched[i].x;
+        prev[2 * i + 1] = vbPrevMatched[i].y;
+    }
+    std::vector<int32_t> m(n1 + 1);
+    int nm = 0;
+    if (!run("orbm_search_for_initialization", [&](orbm_ctx* c) {
+            return orbm_search_for_initialization(c, &f1.v, &f2.v, prev.data(), windowSize, mfNNratio,
+                                                  mbCheckOrientation ? 1 : 0, m.data(), &nm);
+        }))
+        return 0;
+    for (size_t i = 0; i < n1; i++) {  // :514-517 (the updated positions come back in prev)
+        vnMatches12[i] = m[i];
+        if (m[i] >= 0) vbPrevMatched[i] = cv::Point2f(prev[2 * i], prev[2 * i + 1]);
+    }
+    return nm;
+}
+
+// ORBmatcher.cc:1102-1326 (LoopClosing::ComputeSim3)
+int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12, const float& s12,
+                             const cv::Mat& R12, const cv::Mat& t12, const float th) {
+    FrameSide k1, k2;
+    k1.gather(*pKF1, nullptr, 0.f, 0.f);
+    k2.gather(*pKF2, nullptr, 0.f, 0.f);
+    const std::vector<MapPoint*> vpMapPoints1 = pKF1->GetMapPointMatches();
+    const std::vector<MapPoint*> vpMapPoints2 = pKF2->GetMapPointMatches();
+    const size_t N1 = vpMapPoints1.size(), N2 = vpMapPoints2.size();
+    std::vector<uint8_t> already1(N1, 0), already2(N2, 0);  // :1129-1142
+    for (size_t i = 0; i < N1; i++) {
+        MapPoint* pMP = vpMatches12[i];
+        if (pMP) {
+            already1[i] = 1;
+            const int idx2 = pMP->GetIndexInKeyFrame(pKF2);
+            if (idx2 >= 0 && idx2 < (int)N2) already2[idx2] = 1;
+        }
+    }
+    PointSide p1, p2;
+    p1.reserve(N1);
+    p2.reserve(N2);
+    for (size_t i = 0; i < N1; i++) {
+        p1.skip[i] = !vpMapPoints1[i] || already1[i];
+        if (!p1.skip[i]) p1.point(i, vpMapPoints1[i], true);
+    }
+    for (size_t i = 0; i < N2; i++) {
+        p2.skip[i] = !vpMapPoints2[i] || already2[i];
+        if (!p2.skip[i]) p2.point(i, vpMapPoints2[i], true);
+    }
+    p1.finish(N1);
+    p2.finish(N2);
+    float T1[16] = {0}, T2[16] = {0}, R[9], t[3];
+    const cv::Mat R1w = pKF1->GetRotation(), t1w = pKF1->GetTranslation();
+    const cv::Mat R2w = pKF2->GetRotation(), t2w = pKF2->GetTranslation();
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) {
+            T1[4 * r + c] = R1w.at<float>(r, c);
+            T2[4 * r + c] = R2w.at<float>(r, c);
+            R[3 * r + c] = R12.at<float>(r, c);
+        }
+        T1[4 * r + 3] = t1w.at<float>(r, 0);
+        T2[4 * r + 3] = t2w.at<float>(r, 0);
+        t[r] = t12.at<float>(r, 0);
+    }
+    T1[15] = T2[15] = 1.f;
+    std::vector<int32_t> m(N1 + 1);
+    int nFound = 0;
+    if (!run("orbm_search_by_sim3", [&](orbm_ctx* c) {
+            return orbm_search_by_sim3(c, &k1.v, T1, &p1.m, &k2.v, T2, &p2.m, s12, R, t, th, m.data(), &nFound);
+        }))
+        return 0;
+    for (size_t i1 = 0; i1 < N1; i1++)  // :1310-1323
+        if (m[i1] >= 0) vpMatches12[i1] = vpMapPoints2[m[i1]];
+    return nFound;
 }
 
 }  // namespace ORB_SLAM2

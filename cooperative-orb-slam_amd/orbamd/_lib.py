@@ -139,6 +139,8 @@ SIGNATURES = {
     "orbm_search_by_projection_sim3": (_I, [_P, _P, _P, _P, _I, _P, C.POINTER(_I)]),
     "orbm_fuse": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, C.POINTER(_I)]),
     "orbm_fuse_sim3": (_I, [_P, _P, _P, _P, _F, _P, C.POINTER(_I)]),
+    "orbm_search_for_initialization": (_I, [_P, _P, _P, _P, _I, _F, _I, _P, C.POINTER(_I)]),
+    "orbm_search_by_sim3": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _F, _P, C.POINTER(_I)]),
     "orbm_compute_distinctive_descriptors": (_I, [_P, _I, _P, _P, _P, _P]),
     "orbv_load_text": (_I, [C.c_char_p, _I, C.POINTER(_P)]),
     "orbv_create": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _I, C.POINTER(_P)]),

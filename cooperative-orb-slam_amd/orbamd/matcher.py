@@ -199,6 +199,33 @@ class ORBmatcher:
                                        out.ctypes.data, C.byref(n)), "orbm_fuse_sim3")
         return n.value, out[:mps.n]
 
+    # ---- SearchForInitialization (ORBmatcher.cc:405-520): (nmatches, vnMatches12[F1.n], updated vbPrevMatched)
+    def SearchForInitialization(self, F1, F2, prev_xy, windowSize=10):
+        f1, f2 = F1.cstruct(), F2.cstruct()
+        prev = np.ascontiguousarray(prev_xy, np.float32).reshape(F1.n, 2).copy()
+        out = np.empty(max(F1.n, 1), np.int32)
+        n = C.c_int()
+        check(self._lib.orbm_search_for_initialization(self._h, C.byref(f1), C.byref(f2), prev.ctypes.data,
+                                                       int(windowSize), C.c_float(self.mfNNratio),
+                                                       int(self.mbCheckOrientation), out.ctypes.data, C.byref(n)),
+              "orbm_search_for_initialization")
+        return n.value, out[:F1.n], prev
+
+    # ---- SearchBySim3 (ORBmatcher.cc:1102-1326): (nFound, match12[mp1.n]) = agreeing idx2 or -1
+    def SearchBySim3(self, KF1, T1w, mp1, KF2, T2w, mp2, s12, R12, t12, th):
+        k1, k2 = KF1.cstruct(), KF2.cstruct()
+        m1, m2 = mp1.cstruct(), mp2.cstruct()
+        T1 = np.ascontiguousarray(T1w, np.float32).reshape(16)
+        T2 = np.ascontiguousarray(T2w, np.float32).reshape(16)
+        R = np.ascontiguousarray(R12, np.float32).reshape(9)
+        t = np.ascontiguousarray(t12, np.float32).reshape(3)
+        out = np.empty(max(mp1.n, 1), np.int32)
+        n = C.c_int()
+        check(self._lib.orbm_search_by_sim3(self._h, C.byref(k1), T1.ctypes.data, C.byref(m1), C.byref(k2),
+                                            T2.ctypes.data, C.byref(m2), C.c_float(s12), R.ctypes.data, t.ctypes.data,
+                                            C.c_float(th), out.ctypes.data, C.byref(n)), "orbm_search_by_sim3")
+        return n.value, out[:mp1.n]
+
 
 def compute_distinctive_descriptors(offsets, desc, device=0, matcher=None):
     """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of MapPoints:

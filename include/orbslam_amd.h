@@ -327,6 +327,29 @@ int orbm_fuse(orbm_ctx* ctx, const orbm_frame_view* KF, const float Tcw[16], con
 int orbm_fuse_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, const float Scw[16], const orbm_mappoints* mp,
                    float th, int32_t* best_idx, int* nfused);
 
+/* ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>& vbPrevMatched,
+ * vector<int>& vnMatches12, windowSize) (ORBmatcher.cc:405-520; Tracking::MonocularInitialization,
+ * Tracking.cc:600, with ORBmatcher(0.9, true) and windowSize 100). F1: mvKeysUn octave / angle and
+ * mDescriptors (n entries; x / y unused); F2: the grid side (F2.GetFeaturesInArea: x, y, octave, grid
+ * bounds, angle, desc). prev_xy[2*F1.n] = vbPrevMatched (x, y), updated in place for every matched
+ * keypoint; match12[F1.n] = vnMatches12; *nmatches = the reference's return value. Frames of at most
+ * 8192 keypoints (ORBX_ECAPACITY above). */
+int orbm_search_for_initialization(orbm_ctx* ctx, const orbm_frame_view* F1, const orbm_frame_view* F2,
+                                   float* prev_xy, int window_size, float nnratio, int check_ori,
+                                   int32_t* match12, int* nmatches);
+
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.cc:1102-1326;
+ * LoopClosing::ComputeSim3). KF1 / KF2: the keyframes' grid views (mvKeysUn, descriptors, bounds, grid,
+ * camera: both directions project with KF1's fx, fy, cx, cy as the reference does); T1w / T2w = their
+ * poses (4x4 row-major). mp1 / mp2 = pKF1 / pKF2->GetMapPointMatches(): skip = NULL entry or
+ * vbAlreadyMatched1 / 2 (:1129-1142: vpMatches12[i] != NULL, and that MapPoint's index in pKF2), bad, pos,
+ * desc, min_dist, max_dist (mfMinDistance / mfMaxDistance). R12 row-major 3x3, t12[3].
+ * match12[mp1.n] = idx2 where both directions agree (vpMatches12[i1] = vpMapPoints2[idx2]; other entries
+ * of vpMatches12 are left as they were), else -1; *nfound = the reference's return value. */
+int orbm_search_by_sim3(orbm_ctx* ctx, const orbm_frame_view* KF1, const float T1w[16], const orbm_mappoints* mp1,
+                        const orbm_frame_view* KF2, const float T2w[16], const orbm_mappoints* mp2, float s12,
+                        const float R12[9], const float t12[3], float th, int32_t* match12, int* nfound);
+
 /* ------------------------------------------------------------------------------------
  * MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of MapPoints.
  * MapPoint p's observed descriptors (the rows pKF->mDescriptors.row(idx) of its non-bad

@@ -59,6 +59,8 @@ _SIG = {
     "oc_search_by_projection_sim3": (_I, [_P, _P, _P, _I, _P]),
     "oc_fuse": (_I, [_P, _P, _P, _P, _F, _P, _P]),
     "oc_fuse_sim3": (_I, [_P, _P, _P, _F, _P]),
+    "oc_search_for_initialization": (_I, [_P, _P, _P, _I, _F, _I, _P]),
+    "oc_search_by_sim3": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _F, _P]),
     "oc_compute_distinctive_descriptors": (None, [_I, _P, _P, _P]),
     "oc_vocab_create": (_P, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "oc_vocab_destroy": (None, [_P]),
@@ -320,6 +322,30 @@ def fuse_sim3(KF, Scw, mps, th):
     out = np.empty(max(mps.n, 1), np.int32)
     n = load().oc_fuse_sim3(C.byref(fv), S.ctypes.data, C.byref(m), C.c_float(th), out.ctypes.data)
     return n, out[:mps.n]
+
+
+# ---- SearchForInitialization (ORBmatcher.cc:405-520): (nmatches, vnMatches12, updated vbPrevMatched)
+def search_for_initialization(F1, F2, prev_xy, window, nnratio, check_ori):
+    f1, f2 = F1.cstruct(), F2.cstruct()
+    prev = np.ascontiguousarray(prev_xy, np.float32).reshape(F1.n, 2).copy()
+    out = np.empty(max(F1.n, 1), np.int32)
+    n = load().oc_search_for_initialization(C.byref(f1), C.byref(f2), prev.ctypes.data, int(window),
+                                            C.c_float(nnratio), int(check_ori), out.ctypes.data)
+    return n, out[:F1.n], prev
+
+
+# ---- SearchBySim3 (ORBmatcher.cc:1102-1326): (nFound, match12[mp1.n])
+def search_by_sim3(KF1, T1w, mp1, KF2, T2w, mp2, s12, R12, t12, th):
+    k1, k2 = KF1.cstruct(), KF2.cstruct()
+    m1, m2 = mp1.cstruct(), mp2.cstruct()
+    T1 = np.ascontiguousarray(T1w, np.float32).reshape(16)
+    T2 = np.ascontiguousarray(T2w, np.float32).reshape(16)
+    R = np.ascontiguousarray(R12, np.float32).reshape(9)
+    t = np.ascontiguousarray(t12, np.float32).reshape(3)
+    out = np.empty(max(mp1.n, 1), np.int32)
+    n = load().oc_search_by_sim3(C.byref(k1), T1.ctypes.data, C.byref(m1), C.byref(k2), T2.ctypes.data, C.byref(m2),
+                                 C.c_float(s12), R.ctypes.data, t.ctypes.data, C.c_float(th), out.ctypes.data)
+    return n, out[:mp1.n]
 
 
 def compute_distinctive_descriptors(offsets, desc):

@@ -91,6 +91,14 @@ int oc_fuse(const orbm_frame_view* KF, const float* Tcw, const float* Ow, const 
             const float* inv_sigma2, int32_t* best_idx);
 int oc_fuse_sim3(const orbm_frame_view* KF, const float* Scw, const orbm_mappoints* mp, float th, int32_t* best_idx);
 
+/* ORBmatcher::SearchForInitialization (ORBmatcher.cc:405-520); prev_xy updated in place */
+int oc_search_for_initialization(const orbm_frame_view* F1, const orbm_frame_view* F2, float* prev_xy, int windowSize,
+                                 float nnratio, int checkOri, int32_t* match12);
+/* ORBmatcher::SearchBySim3 (ORBmatcher.cc:1102-1326): match12[mp1->n] = agreeing idx2 or -1 */
+int oc_search_by_sim3(const orbm_frame_view* KF1, const float* T1w, const orbm_mappoints* mp1,
+                      const orbm_frame_view* KF2, const float* T2w, const orbm_mappoints* mp2, float s12,
+                      const float* R12, const float* t12, float th, int32_t* match12);
+
 /* DBoW2 vocabulary transform (orb_oracle_voc.c; parity unpinned: DBoW2 is not vendored) */
 typedef struct oc_vocab oc_vocab;
 oc_vocab* oc_vocab_create(int k, int L, int scoring, int weighting, int nlines, const int32_t* parent,

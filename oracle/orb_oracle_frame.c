@@ -200,8 +200,16 @@ int oc_compute_stereo_matches(const oc_extractor* left, const oc_extractor* righ
 #define FRAME_GRID_COLS 64 /* Frame.h:38 */
 #define HISTO_LENGTH 30    /* ORBmatcher.cc:39 */
 
+/* its own push (not rowvec_push through a cast: the two struct types may not alias under -O3's strict
+ * aliasing, which let GCC keep the memset's zero counts of a local ivec2 array across the pushes) */
 typedef struct { int* v; int n, cap; } ivec2;
-static void iv_push(ivec2* s, int x) { rowvec_push((rowvec*)s, x); }
+static void iv_push(ivec2* s, int x) {
+    if (s->n == s->cap) {
+        s->cap = s->cap ? 2 * s->cap : 8;
+        s->v = (int*)realloc(s->v, sizeof(int) * (size_t)s->cap);
+    }
+    s->v[s->n++] = x;
+}
 
 /* Frame::AssignFeaturesToGrid + PosInGrid (Frame.cc:235-250, 391-401): mGrid[ix][iy] lists in
  * feature order. round() of a float (half away from zero). */
@@ -735,6 +743,180 @@ int oc_fuse_sim3(const orbm_frame_view* KF, const float* Scw, const orbm_mappoin
     free(vIndices.v);
     grid_free(g);
     return nFused;
+}
+
+/* ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) (ORBmatcher.cc:405-520).
+ * F1: mvKeysUn octave / angle and mDescriptors (x, y unused); F2: the grid side (F2.GetFeaturesInArea,
+ * mvKeysUn, mDescriptors). prev_xy[2*i1] = vbPrevMatched[i1] (x, y), overwritten with F2.mvKeysUn[match].pt
+ * for every matched i1 (:514-517). match12[F1->n] = vnMatches12. Returns nmatches. */
+int oc_search_for_initialization(const orbm_frame_view* F1, const orbm_frame_view* F2, float* prev_xy, int windowSize,
+                                 float nnratio, int checkOri, int32_t* match12) {
+    int nmatches = 0;
+    for (int i = 0; i < F1->n; i++) match12[i] = -1; /* :408 */
+    ivec2 rotHist[HISTO_LENGTH];
+    memset(rotHist, 0, sizeof(rotHist));
+    const float factor = 1.0f / HISTO_LENGTH; /* :413 */
+    int* vMatchedDistance = (int*)malloc(sizeof(int) * ((size_t)F2->n + 1));
+    int* vnMatches21 = (int*)malloc(sizeof(int) * ((size_t)F2->n + 1));
+    for (int i = 0; i < F2->n; i++) {
+        vMatchedDistance[i] = INT_MAX; /* :415-416 */
+        vnMatches21[i] = -1;
+    }
+    ogrid* g = grid_build(F2);
+    ivec2 vIndices2 = {0};
+    for (int i1 = 0; i1 < F1->n; i1++) { /* :418 */
+        const int level1 = F1->octave[i1];
+        if (level1 > 0) continue;
+        features_in_area(F2, g, prev_xy[2 * i1], prev_xy[2 * i1 + 1], (float)windowSize, level1, level1, &vIndices2);
+        if (vIndices2.n == 0) continue;
+        const uint8_t* d1 = F1->desc + 32 * (size_t)i1;
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+        for (int k = 0; k < vIndices2.n; k++) { /* :436-457 */
+            const int i2 = vIndices2.v[k];
+            const int dist = oc_descriptor_distance(d1, F2->desc + 32 * (size_t)i2);
+            if (vMatchedDistance[i2] <= dist) continue;
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestIdx2 = i2;
+            } else if (dist < bestDist2) {
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_LOW) { /* :459-485 */
+            if ((float)bestDist < (float)bestDist2 * nnratio) {
+                if (vnMatches21[bestIdx2] >= 0) {
+                    match12[vnMatches21[bestIdx2]] = -1;
+                    nmatches--;
+                }
+                match12[i1] = bestIdx2;
+                vnMatches21[bestIdx2] = i1;
+                vMatchedDistance[bestIdx2] = bestDist;
+                nmatches++;
+                if (checkOri) {
+                    float rot = F1->angle[i1] - F2->angle[bestIdx2];
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == HISTO_LENGTH) bin = 0;
+                    iv_push(&rotHist[bin], i1);
+                }
+            }
+        }
+    }
+    if (checkOri) { /* :489-512: the bins keep matches that a later i1 took away (counted by ComputeThreeMaxima) */
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima2(rotHist, HISTO_LENGTH, &ind1, &ind2, &ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int j = 0; j < rotHist[i].n; j++) {
+                const int idx1 = rotHist[i].v[j];
+                if (match12[idx1] >= 0) {
+                    match12[idx1] = -1;
+                    nmatches--;
+                }
+            }
+        }
+    }
+    for (int i1 = 0; i1 < F1->n; i1++) /* :514-517 */
+        if (match12[i1] >= 0) {
+            prev_xy[2 * i1] = F2->x[match12[i1]];
+            prev_xy[2 * i1 + 1] = F2->y[match12[i1]];
+        }
+    for (int i = 0; i < HISTO_LENGTH; i++) free(rotHist[i].v);
+    free(vIndices2.v);
+    free(vMatchedDistance);
+    free(vnMatches21);
+    grid_free(g);
+    return nmatches;
+}
+
+/* one direction of SearchBySim3 (ORBmatcher.cc:1148-1225 / 1228-1305): MapPoints of the source keyframe
+ * (mp: skip = NULL or vbAlreadyMatched, bad, pos, desc, min_dist, max_dist) through Tsw = (Rsw, tsw) into the
+ * source camera, then (sR, t) into the target keyframe KF, projected with the camera (fx, fy, cx, cy) of pKF1
+ * (the reference reads pKF1's intrinsics for both directions, :1105-1108); vnMatch[i] = best KF keypoint
+ * (first strict minimum, octave in [nPredictedLevel-1, nPredictedLevel]) if bestDist <= TH_HIGH, else -1 */
+static void sim3_direction(const orbm_frame_view* KF, const float* Tsw, const orbm_mappoints* mp, const float* sR,
+                           const float* t, float fx, float fy, float cx, float cy, float th, int32_t* vnMatch) {
+    const float Rsw[9] = {Tsw[0], Tsw[1], Tsw[2], Tsw[4], Tsw[5], Tsw[6], Tsw[8], Tsw[9], Tsw[10]};
+    const float tsw[3] = {Tsw[3], Tsw[7], Tsw[11]};
+    ogrid* g = grid_build(KF);
+    ivec2 vIndices = {0};
+    for (int i = 0; i < mp->n; i++) {
+        vnMatch[i] = -1;
+        if (has(mp->skip, i) || has(mp->bad, i)) continue; /* :1152-1156 */
+        const float* p3Dw = mp->pos + 3 * (size_t)i;
+        float p3Dcs[3], p3Dct[3];
+        gemm33_fast(Rsw, 3, p3Dw, tsw, p3Dcs); /* R1w*p3Dw + t1w */
+        gemm33_fast(sR, 3, p3Dcs, t, p3Dct);  /* sR21*p3Dc1 + t21 */
+        if (p3Dct[2] < 0.0) continue;
+        const float invz = (float)(1.0 / (double)p3Dct[2]);
+        const float x = p3Dct[0] * invz;
+        const float y = p3Dct[1] * invz;
+        const float u = fx * x + cx;
+        const float v = fy * y + cy;
+        if (!(u >= KF->min_x && u < KF->max_x && v >= KF->min_y && v < KF->max_y)) continue; /* IsInImage */
+        const float maxDistance = 1.2f * mp->max_dist[i];
+        const float minDistance = 0.8f * mp->min_dist[i];
+        const float dist3D = norm3(p3Dct);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const int nPredictedLevel = predict_scale(mp->max_dist[i], dist3D, KF);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        features_in_area(KF, g, u, v, radius, -1, -1, &vIndices);
+        if (vIndices.n == 0) continue;
+        const uint8_t* dMP = mp->desc + 32 * (size_t)i;
+        int bestDist = INT_MAX, bestIdx = -1;
+        for (int k = 0; k < vIndices.n; k++) {
+            const int idx = vIndices.v[k];
+            const int oct = KF->octave[idx];
+            if (oct < nPredictedLevel - 1 || oct > nPredictedLevel) continue;
+            const int dist = oc_descriptor_distance(dMP, KF->desc + 32 * (size_t)idx);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx = idx;
+            }
+        }
+        if (bestDist <= TH_HIGH) vnMatch[i] = bestIdx;
+    }
+    free(vIndices.v);
+    grid_free(g);
+}
+
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.cc:1102-1326).
+ * T1w / T2w: the keyframes' poses (4x4 row-major; GetRotation / GetTranslation); mp1 / mp2: their
+ * GetMapPointMatches() with skip = NULL entry or vbAlreadyMatched1/2 (:1129-1142). match12[mp1->n] = idx2
+ * where both directions agree (vpMatches12[i1] = vpMapPoints2[idx2], :1310-1323), else -1. Returns nFound. */
+int oc_search_by_sim3(const orbm_frame_view* KF1, const float* T1w, const orbm_mappoints* mp1,
+                      const orbm_frame_view* KF2, const float* T2w, const orbm_mappoints* mp2, float s12,
+                      const float* R12, const float* t12, float th, int32_t* match12) {
+    /* sR12 = s12*R12 and sR21 = (1.0/s12)*R12.t() are MatExpr scalings evaluated by convertTo with a float
+     * scale; t21 = -sR21*t12 is the small-matrix gemm with alpha = -1 (:1119-1121) */
+    float sR12[9], sR21[9], t21[3];
+    const float inv_s = (float)(1.0 / (double)s12);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            sR12[3 * r + c] = R12[3 * r + c] * s12;
+            sR21[3 * r + c] = R12[3 * c + r] * inv_s;
+        }
+    for (int r = 0; r < 3; r++) {
+        const float t0 = sR21[3 * r] * t12[0] + sR21[3 * r + 1] * t12[1] + sR21[3 * r + 2] * t12[2];
+        t21[r] = (float)((double)t0 * -1.0);
+    }
+    int32_t* vnMatch1 = (int32_t*)malloc(sizeof(int32_t) * ((size_t)mp1->n + 1));
+    int32_t* vnMatch2 = (int32_t*)malloc(sizeof(int32_t) * ((size_t)mp2->n + 1));
+    sim3_direction(KF2, T1w, mp1, sR21, t21, KF1->fx, KF1->fy, KF1->cx, KF1->cy, th, vnMatch1);
+    sim3_direction(KF1, T2w, mp2, sR12, t12, KF1->fx, KF1->fy, KF1->cx, KF1->cy, th, vnMatch2);
+    int nFound = 0;
+    for (int i1 = 0; i1 < mp1->n; i1++) { /* :1310-1323 */
+        match12[i1] = -1;
+        const int idx2 = vnMatch1[i1];
+        if (idx2 >= 0 && idx2 < mp2->n && vnMatch2[idx2] == i1) {
+            match12[i1] = idx2;
+            nFound++;
+        }
+    }
+    free(vnMatch1);
+    free(vnMatch2);
+    return nFound;
 }
 
 /* ===================================================================================== */

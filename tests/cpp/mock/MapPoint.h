@@ -33,6 +33,10 @@ public:
     bool isBad() { return bad; }
     /* MapPoint.cc:63-120, 130-170 (Fuse's updates): observations, replacement */
     bool IsInKeyFrame(KeyFrame* pKF) { return mObservations.count(pKF) > 0; }
+    int GetIndexInKeyFrame(KeyFrame* pKF) {  // MapPoint.cc:315-322
+        std::map<KeyFrame*, size_t>::iterator it = mObservations.find(pKF);
+        return it == mObservations.end() ? -1 : (int)it->second;
+    }
     void AddObservation(KeyFrame* pKF, size_t idx);
     void Replace(MapPoint* pMP);
     int Observations() { return nObs; }

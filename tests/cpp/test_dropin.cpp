@@ -337,6 +337,147 @@ static void test_fuse(const std::vector<cv::KeyPoint>& kps, const cv::Mat& desc,
     }
 }
 
+/* ---- SearchForInitialization (ORBmatcher.cc:405-520) and SearchBySim3 (ORBmatcher.cc:1102-1326) through the
+ * drop-in class, vs the oracle on independently gathered views */
+static void grid_frame(Frame& F, const std::vector<cv::KeyPoint>& k, const cv::Mat& d, ORBextractor& ext, int W, int H) {
+    F.N = (int)k.size(); F.mvKeys = k; F.mvKeysUn = k; F.mDescriptors = d;
+    F.mvScaleFactors = ext.GetScaleFactors(); F.mvLevelSigma2 = ext.GetScaleSigmaSquares();
+    F.mnScaleLevels = 8; F.mfLogScaleFactor = logf(1.2f);
+    F.fx = 715.092024f; F.fy = 719.025258f; F.cx = 334.298489f; F.cy = 256.326097f;
+    F.mnMinX = 0.f; F.mnMaxX = (float)W; F.mnMinY = 0.f; F.mnMaxY = (float)H;
+    F.mfGridElementWidthInv = 64.f / (F.mnMaxX - F.mnMinX);
+    F.mfGridElementHeightInv = 48.f / (F.mnMaxY - F.mnMinY);
+}
+struct OFrame {
+    std::vector<float> x, y, a;
+    std::vector<int32_t> o;
+    orbm_frame_view v;
+};
+template <class FK>
+static void oframe(FK& F, OFrame& w) {
+    for (const cv::KeyPoint& k : F.mvKeysUn) { w.x.push_back(k.pt.x); w.y.push_back(k.pt.y); w.a.push_back(k.angle); w.o.push_back(k.octave); }
+    memset(&w.v, 0, sizeof(w.v));
+    w.v.n = (int)F.mvKeysUn.size(); w.v.desc = F.mDescriptors.data; w.v.x = w.x.data(); w.v.y = w.y.data();
+    w.v.octave = w.o.data(); w.v.angle = w.a.data();
+    w.v.min_x = F.mnMinX; w.v.min_y = F.mnMinY; w.v.max_x = F.mnMaxX; w.v.max_y = F.mnMaxY;
+    w.v.grid_w_inv = F.mfGridElementWidthInv; w.v.grid_h_inv = F.mfGridElementHeightInv;
+    w.v.fx = F.fx; w.v.fy = F.fy; w.v.cx = F.cx; w.v.cy = F.cy;
+    w.v.nlevels = (int)F.mvScaleFactors.size(); w.v.scale_factors = F.mvScaleFactors.data();
+    w.v.log_scale_factor = F.mfLogScaleFactor;
+}
+
+static void test_init_sim3(const std::vector<cv::KeyPoint>& k1, const cv::Mat& d1, const std::vector<cv::KeyPoint>& k2,
+                           const cv::Mat& d2, ORBextractor& ext, int W, int H) {
+    Frame F1, F2;
+    grid_frame(F1, k1, d1, ext, W, H);
+    grid_frame(F2, k2, d2, ext, W, H);
+    OFrame o1, o2;
+    oframe(F1, o1);
+    oframe(F2, o2);
+    for (int ori = 0; ori < 2; ori++) {
+        ORBmatcher m(0.9f, ori != 0);
+        std::vector<cv::Point2f> prev;
+        for (const cv::KeyPoint& k : F1.mvKeysUn) prev.push_back(k.pt);
+        std::vector<float> oprev;
+        for (const cv::Point2f& p : prev) { oprev.push_back(p.x); oprev.push_back(p.y); }
+        std::vector<int> v12;
+        const int n = m.SearchForInitialization(F1, F2, prev, v12, 100);
+        std::vector<int32_t> om(F1.N);
+        const int on = oc_search_for_initialization(&o1.v, &o2.v, oprev.data(), 100, 0.9f, ori, om.data());
+        int diff = 0;
+        for (int i = 0; i < F1.N; i++)
+            diff += v12[i] != om[i] || !same_bits(prev[i].x, oprev[2 * i]) || !same_bits(prev[i].y, oprev[2 * i + 1]);
+        CHECK(n == on && n > 50 && diff == 0, "SearchForInitialization ori=%d: %d vs oracle %d, %d diffs", ori, n, on, diff);
+    }
+    // SearchBySim3: KF2 = the same features seen through (s12, R12 = I, t12 = 0): Xc2 = Xc1 / s12
+    KeyFrame kf1, kf2;
+    std::vector<MapPoint> pool1(F1.N), pool2(F1.N);
+    for (KeyFrame* kf : {&kf1, &kf2}) {
+        kf->N = F1.N; kf->mvKeys = F1.mvKeys; kf->mvKeysUn = F1.mvKeysUn; kf->mDescriptors = F1.mDescriptors;
+        kf->mvScaleFactors = F1.mvScaleFactors; kf->mvLevelSigma2 = F1.mvLevelSigma2; kf->mnScaleLevels = 8;
+        kf->mfLogScaleFactor = F1.mfLogScaleFactor; kf->fx = F1.fx; kf->fy = F1.fy; kf->cx = F1.cx; kf->cy = F1.cy;
+        kf->mnMinX = F1.mnMinX; kf->mnMaxX = F1.mnMaxX; kf->mnMinY = F1.mnMinY; kf->mnMaxY = F1.mnMaxY;
+        kf->mfGridElementWidthInv = F1.mfGridElementWidthInv; kf->mfGridElementHeightInv = F1.mfGridElementHeightInv;
+        kf->Rcw = cv::Mat(3, 3, CV_32F); kf->tcw = cv::Mat(3, 1, CV_32F); kf->Ow = cv::Mat(3, 1, CV_32F);
+        for (int i = 0; i < 9; i++) kf->Rcw.at<float>(i / 3, i % 3) = (i % 4 == 0) ? 1.f : 0.f;
+        kf->mvpMapPoints.assign(F1.N, nullptr);
+        kf->mvuRight.assign(F1.N, -1.f);
+    }
+    for (int i = 0; i < 3; i++) { kf1.tcw.at<float>(i, 0) = 0.f; kf2.tcw.at<float>(i, 0) = i == 0 ? 0.1f : 0.f; }
+    const float s12 = 1.1f;
+    uint32_t s = 4242;
+    for (int i = 0; i < F1.N; i++) {
+        const float z = 1.f + (float)(lcg(s) % 1000) * 0.01f;
+        const float X = (F1.mvKeysUn[i].pt.x - F1.cx) / F1.fx * z, Y = (F1.mvKeysUn[i].pt.y - F1.cy) / F1.fy * z;
+        const float sc = powf(1.2f, (float)F1.mvKeysUn[i].octave);
+        for (int side = 0; side < 2; side++) {
+            if (lcg(s) % 10 < 3) continue;  // no MapPoint
+            MapPoint& p = side ? pool2[i] : pool1[i];
+            const float f = side ? 1.f / s12 : 1.f;  // camera coordinates of this side
+            p.mWorldPos = cv::Mat(3, 1, CV_32F);
+            p.mWorldPos.at<float>(0, 0) = X * f - (side ? 0.1f : 0.f);  // Xw = Xc - t (R = I)
+            p.mWorldPos.at<float>(1, 0) = Y * f;
+            p.mWorldPos.at<float>(2, 0) = z * f;
+            p.mDescriptor = cv::Mat(1, 32, CV_8U);
+            memcpy(p.mDescriptor.data, F1.mDescriptors.ptr<unsigned char>(i), 32);
+            for (int b = 0; b < 6; b++) { const uint32_t r = lcg(s) % 256; p.mDescriptor.data[r >> 3] ^= (uint8_t)(1u << (r & 7)); }
+            const float dother = sqrtf(X * X + Y * Y + z * z) * (side ? 1.f : 1.f / s12);
+            p.mfMaxDistance = dother * sc * 1.1f;
+            p.mfMinDistance = p.mfMaxDistance / 3.6f;
+            p.bad = lcg(s) % 20 == 0;
+            (side ? kf2 : kf1).mvpMapPoints[i] = &p;
+        }
+    }
+    // a few pairs already matched (vbAlreadyMatched1/2 through GetIndexInKeyFrame)
+    std::vector<MapPoint*> v12(F1.N, nullptr);
+    for (int i = 0; i < F1.N; i += 37)
+        if (kf1.mvpMapPoints[i] && kf2.mvpMapPoints[i]) {
+            v12[i] = kf2.mvpMapPoints[i];
+            kf2.mvpMapPoints[i]->mObservations[&kf2] = (size_t)i;
+        }
+    const std::vector<MapPoint*> v12_in = v12;
+    cv::Mat R12(3, 3, CV_32F), t12(3, 1, CV_32F);
+    for (int i = 0; i < 9; i++) R12.at<float>(i / 3, i % 3) = (i % 4 == 0) ? 1.f : 0.f;
+    for (int i = 0; i < 3; i++) t12.at<float>(i, 0) = 0.f;
+    ORBmatcher m(0.75f, true);
+    const int n = m.SearchBySim3(&kf1, &kf2, v12, s12, R12, t12, 7.5f);
+    // oracle on independently built inputs
+    auto omp = [&](KeyFrame& kf, std::vector<uint8_t>& skip, std::vector<uint8_t>& bad, std::vector<uint8_t>& desc,
+                   std::vector<float>& pos, std::vector<float>& mind, std::vector<float>& maxd, orbm_mappoints& mp) {
+        const int N = kf.N;
+        bad.assign(N, 0); desc.assign(32 * (size_t)N, 0); pos.assign(3 * (size_t)N, 0.f); mind.assign(N, 0.f); maxd.assign(N, 0.f);
+        for (int i = 0; i < N; i++) {
+            MapPoint* p = kf.mvpMapPoints[i];
+            if (!p) { skip[i] = 1; continue; }
+            bad[i] = p->bad;
+            memcpy(&desc[32 * (size_t)i], p->mDescriptor.data, 32);
+            for (int k = 0; k < 3; k++) pos[3 * i + k] = p->mWorldPos.at<float>(k, 0);
+            mind[i] = p->mfMinDistance; maxd[i] = p->mfMaxDistance;
+        }
+        memset(&mp, 0, sizeof(mp));
+        mp.n = N; mp.desc = desc.data(); mp.pos = pos.data(); mp.min_dist = mind.data(); mp.max_dist = maxd.data();
+        mp.bad = bad.data(); mp.skip = skip.data();
+    };
+    std::vector<uint8_t> sk1(F1.N, 0), sk2(F1.N, 0), b1, b2, de1, de2;
+    std::vector<float> p1, p2, mi1, mi2, ma1, ma2;
+    for (int i = 0; i < F1.N; i++)
+        if (v12_in[i]) { sk1[i] = 1; sk2[i] = 1; }  // GetIndexInKeyFrame(pKF2) == i
+    orbm_mappoints m1, m2;
+    omp(kf1, sk1, b1, de1, p1, mi1, ma1, m1);
+    omp(kf2, sk2, b2, de2, p2, mi2, ma2, m2);
+    OFrame ok1, ok2;
+    oframe(kf1, ok1);
+    oframe(kf2, ok2);
+    float T1[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1}, T2[16] = {1, 0, 0, 0.1f, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    const float R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, t[3] = {0, 0, 0};
+    std::vector<int32_t> om(F1.N);
+    const int on = oc_search_by_sim3(&ok1.v, T1, &m1, &ok2.v, T2, &m2, s12, R, t, 7.5f, om.data());
+    int diff = 0;
+    for (int i = 0; i < F1.N; i++)
+        diff += v12[i] != (om[i] >= 0 ? kf2.mvpMapPoints[om[i]] : v12_in[i]);
+    CHECK(n == on && n > 50 && diff == 0, "SearchBySim3: %d vs oracle %d, %d diffs", n, on, diff);
+}
+
 int main() {
     const int W = 640, H = 480;
     std::vector<uint8_t> frames((size_t)W * H * 3);
@@ -792,6 +933,7 @@ int main() {
         CHECK(bad == 0 && calls == 5 * iters, "concurrent drop-ins: %d of %d calls differ", (int)bad, (int)calls);
     }
     test_fuse(K[2], D[2], ext, W, H);
+    test_init_sim3(K[0], D[0], K[1], D[1], ext, W, H);
     // DescriptorDistance (ORBmatcher.cc:1647-1663)
     int dd = 0;
     for (int i = 0; i + 1 < kf1.N; i += 17)

@@ -204,3 +204,63 @@ def fuse_sim3_scene(seed):
     """Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (LoopClosing::SearchAndFuse)."""
     F, Scw, mps = sim3_scene(seed)
     return F, Scw, mps
+
+
+def init_scene(seed, nfeatures=2000, dt=2, prev_noise=0.0):
+    """SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) (Tracking::
+    MonocularInitialization, Tracking.cc:600): two frames of one synthetic stream, dt steps apart, from
+    the 2000-feature initialisation extractor; vbPrevMatched starts at F1's keypoints (Tracking.cc:583-585),
+    optionally perturbed."""
+    rng = np.random.default_rng(seed)
+    agent, t = seed % 5, 20 + seed
+    k1, d1, scale = frame_features(agent, t, nfeatures)
+    k2, d2, _ = frame_features(agent, t + dt, nfeatures)
+    F1 = orbamd.FrameView(k1, d1, scale, W, H, FX, FY, CX, CY)
+    F2 = orbamd.FrameView(k2, d2, scale, W, H, FX, FY, CX, CY)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    if prev_noise:
+        prev = (prev + rng.normal(0, prev_noise, prev.shape)).astype(np.float32)
+    return F1, F2, prev
+
+
+def sim3_pair_scene(seed, th=7.5):
+    """SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (LoopClosing::ComputeSim3): two keyframes
+    of one image whose MapPoints are one scene seen through the similarity (s12, R12, t12), camera 1 from
+    camera 2: Xc1 = s12 R12 Xc2 + t12. Each keyframe has its own pose, MapPoint subset, descriptor noise,
+    bad flags and already-matched entries (vbAlreadyMatched1/2)."""
+    rng = np.random.default_rng(seed)
+    k, d, scale = frame_features(seed % 5, 30 + seed, 1000)
+    n = len(k)
+    KF1 = orbamd.FrameView(k, d, scale, W, H, FX, FY, CX, CY)
+    KF2 = orbamd.FrameView(k, d, scale, W, H, FX, FY, CX, CY)
+    T1w = pose(rot(rng, 3.0), rng.normal(0, 0.05, 3))
+    T2w = pose(rot(rng, 3.0), rng.normal(0, 0.05, 3))
+    s12 = np.float32(rng.uniform(0.8, 1.25))
+    R12 = rot(rng, 0.3).astype(np.float32)
+    t12 = rng.normal(0, 0.01, 3).astype(np.float32)
+    z = rng.uniform(1.0, 12.0, n)
+    Xc1 = np.stack([(k["x"] - CX) / FX * z, (k["y"] - CY) / FY * z, z], 1)
+    Xc2 = ((Xc1 - t12) @ R12.astype(np.float64)) / float(s12)  # R12^T (Xc1 - t12) / s12
+
+    def to_world(Xc, T):
+        R, t = T[:3, :3].astype(np.float64), T[:3, 3].astype(np.float64)
+        return ((Xc - t) @ R).astype(np.float32)
+
+    def mappoints(Xc_self, Xc_other, T, frac):
+        has = rng.random(n) < frac
+        Xw = to_world(Xc_self + rng.normal(0, 0.002, Xc_self.shape), T)
+        dother = np.linalg.norm(Xc_other, axis=1)
+        maxd = dother * 1.2 ** (k["octave"] + rng.uniform(-0.9, 0.1, n))
+        maxd[rng.random(n) < 0.05] *= 0.5
+        return has, orbamd.MapPoints(n, desc=flip_bits(rng, d, 30), pos=Xw, min_dist=(maxd / 1.2 ** 7).astype(np.float32),
+                                     max_dist=maxd.astype(np.float32), bad=(rng.random(n) < 0.05))
+
+    has1, mp1 = mappoints(Xc1, Xc2, T1w, 0.7)
+    has2, mp2 = mappoints(Xc2, Xc1, T2w, 0.7)
+    # vpMatches12 already set for ~8 % of KF1's MapPoints; vbAlreadyMatched2 at their index in pKF2 (:1129-1142)
+    pre = has1 & (rng.random(n) < 0.08)
+    already2 = np.zeros(n, bool)
+    already2[np.nonzero(pre)[0]] = True
+    mp1.skip = (~has1 | pre).astype(np.uint8)
+    mp2.skip = (~has2 | already2).astype(np.uint8)
+    return KF1, T1w, mp1, KF2, T2w, mp2, s12, R12, t12, th

@@ -127,3 +127,63 @@ def test_fuse_edge_cases():
                            normal=np.repeat(mps.normal[:1], k, 0), min_dist=np.repeat(mps.min_dist[:1], k),
                            max_dist=np.repeat(mps.max_dist[:1], k))
     _same_fuse(mt.Fuse(F, Tcw, Ow, rep, 3.0, inv), oracle_py.fuse(F, Tcw, Ow, rep, 3.0, inv))
+
+
+@pytest.mark.parametrize("seed,noise,check_ori,ratio,window", [(1, 0.0, True, 0.9, 100), (2, 3.0, True, 0.9, 100),
+                                                               (3, 0.0, False, 0.7, 100), (4, 8.0, True, 0.9, 30)])
+def test_search_for_initialization(seed, noise, check_ori, ratio, window):
+    """ORBmatcher::SearchForInitialization (ORBmatcher.cc:405-520) at 640x480 with the 2000-feature
+    initialisation extractor, windowSize 100 as Tracking::MonocularInitialization calls it (Tracking.cc:600):
+    vnMatches12, the count and the updated vbPrevMatched must equal the oracle's (k_init_resolve: in-order
+    resolution with vMatchedDistance stealing)."""
+    F1, F2, prev = ps.init_scene(seed, prev_noise=noise)
+    ng, mg, pg = orbamd.ORBmatcher(ratio, check_ori).SearchForInitialization(F1, F2, prev, window)
+    no, mo, po = oracle_py.search_for_initialization(F1, F2, prev, window, ratio, check_ori)
+    bad = np.nonzero(mg != mo)[0]
+    assert bad.size == 0, "vnMatches12 differs at %s: gpu %s oracle %s" % (bad[:8], mg[bad[:8]], mo[bad[:8]])
+    assert ng == no and ng > 50
+    assert pg.tobytes() == po.tobytes()
+
+
+def test_search_for_initialization_stealing():
+    """many F1 keypoints whose windows hold the same F2 features: a later, closer query takes an F2 feature
+    from an earlier one (ORBmatcher.cc:463-467), repeatedly, inside one 64-query chunk and across chunks"""
+    F1, F2, prev = ps.init_scene(5)
+    rng = np.random.default_rng(5)
+    lvl0 = np.nonzero(F1.octave == 0)[0]
+    tgt = np.nonzero(F2.octave == 0)[0][:20]
+    # every level-0 query looks at one of 20 F2 features with a descriptor 0..40 bits away from it
+    pick = tgt[rng.integers(0, len(tgt), len(lvl0))]
+    F1.desc = F1.desc.copy()  # (the frame cache of proj_scenes is shared)
+    F1.desc[lvl0] = ps.flip_bits(rng, F2.desc[pick], 40)
+    prev[lvl0, 0], prev[lvl0, 1] = F2.x[pick], F2.y[pick]
+    ng, mg, pg = orbamd.ORBmatcher(0.9, True).SearchForInitialization(F1, F2, prev, 100)
+    no, mo, po = oracle_py.search_for_initialization(F1, F2, prev, 100, 0.9, True)
+    np.testing.assert_array_equal(mg, mo)
+    assert ng == no and pg.tobytes() == po.tobytes()
+
+
+@pytest.mark.parametrize("seed,th", [(2, 7.5), (5, 7.5), (8, 3.0)])
+def test_search_by_sim3(seed, th):
+    """ORBmatcher::SearchBySim3 (ORBmatcher.cc:1102-1326): both projections through (s12, R12, t12), the
+    windowed first-strict-minimum search on the device, the mutual-consistency check."""
+    sc = list(ps.sim3_pair_scene(seed))
+    sc[-1] = th
+    ng, mg = orbamd.ORBmatcher(0.75, True).SearchBySim3(*sc)
+    no, mo = oracle_py.search_by_sim3(*sc)
+    bad = np.nonzero(mg != mo)[0]
+    assert bad.size == 0, "match12 differs at %s: gpu %s oracle %s" % (bad[:8], mg[bad[:8]], mo[bad[:8]])
+    assert ng == no and ng > 50
+
+
+def test_search_by_sim3_edge_cases():
+    """no MapPoints on one side; every MapPoint already matched"""
+    KF1, T1w, mp1, KF2, T2w, mp2, s12, R12, t12, th = ps.sim3_pair_scene(3)
+    mt = orbamd.ORBmatcher(0.75, True)
+    empty = orbamd.MapPoints(0, desc=np.zeros((0, 32), np.uint8), pos=np.zeros((0, 3), np.float32), min_dist=[],
+                             max_dist=[])
+    n, m = mt.SearchBySim3(KF1, T1w, mp1, KF2, T2w, empty, s12, R12, t12, th)
+    assert n == 0 and (m == -1).all()
+    mp1.skip = np.ones(mp1.n, np.uint8)
+    n, m = mt.SearchBySim3(KF1, T1w, mp1, KF2, T2w, mp2, s12, R12, t12, th)
+    assert n == 0 and (m == -1).all()

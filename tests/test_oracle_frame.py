@@ -387,3 +387,142 @@ def distinctive_py(off, desc):
 def test_distinctive_oracle_matches_restatement():
     off, desc = distinctive_scene(1)
     np.testing.assert_array_equal(oracle_py.compute_distinctive_descriptors(off, desc), distinctive_py(off, desc))
+
+
+# ------------------------------------------------------------------ SearchForInitialization (ORBmatcher.cc:405-520)
+def init_py(F1, F2, prev, window, nnratio, check_ori):
+    """literal restatement: in-order queries, vMatchedDistance / vnMatches21 with stealing, rotation bins
+    that keep stolen entries, ComputeThreeMaxima, vbPrevMatched update"""
+    g = grid_py(F2)
+    b2 = np.unpackbits(F2.desc, axis=1)
+    m12 = np.full(F1.n, -1, np.int32)
+    md = np.full(F2.n, 2 ** 31 - 1, np.int64)
+    m21 = np.full(F2.n, -1, np.int64)
+    hist = [[] for _ in range(30)]
+    nm = 0
+    for i1 in range(F1.n):
+        l1 = int(F1.octave[i1])
+        if l1 > 0:
+            continue
+        cand = area_py(F2, g, prev[i1, 0], prev[i1, 1], float(window), l1, l1)
+        if not cand:
+            continue
+        qb = np.unpackbits(F1.desc[i1])
+        best, best2, bi = 2 ** 31 - 1, 2 ** 31 - 1, -1
+        for i2 in cand:
+            dist = int(np.count_nonzero(b2[i2] != qb))
+            if md[i2] <= dist:
+                continue
+            if dist < best:
+                best2, best, bi = best, dist, i2
+            elif dist < best2:
+                best2 = dist
+        if best <= 50 and f32(best) < f32(f32(best2) * f32(nnratio)):
+            if m21[bi] >= 0:
+                m12[m21[bi]] = -1
+                nm -= 1
+            m12[i1], m21[bi], md[bi] = bi, i1, best
+            nm += 1
+            if check_ori:
+                rot = f32(F1.angle[i1] - F2.angle[bi])
+                if rot < 0:
+                    rot = f32(rot + f32(360))
+                b = int(roundf(float(f32(rot * f32(1.0 / 30)))))
+                hist[0 if b == 30 else b].append(i1)
+    if check_ori:
+        sizes = [len(h) for h in hist]
+        i1s = [-1, -1, -1]
+        m = [0, 0, 0]
+        for i, sz in enumerate(sizes):
+            if sz > m[0]:
+                m, i1s = [sz, m[0], m[1]], [i, i1s[0], i1s[1]]
+            elif sz > m[1]:
+                m, i1s = [m[0], sz, m[1]], [i1s[0], i, i1s[1]]
+            elif sz > m[2]:
+                m[2], i1s[2] = sz, i
+        if m[1] < f32(f32(0.1) * f32(m[0])):
+            i1s[1] = i1s[2] = -1
+        elif m[2] < f32(f32(0.1) * f32(m[0])):
+            i1s[2] = -1
+        for i in range(30):
+            if i in i1s:
+                continue
+            for idx1 in hist[i]:
+                if m12[idx1] >= 0:
+                    m12[idx1] = -1
+                    nm -= 1
+    prev = prev.copy()
+    for i1 in np.nonzero(m12 >= 0)[0]:
+        prev[i1] = (F2.x[m12[i1]], F2.y[m12[i1]])
+    return nm, m12, prev
+
+
+@pytest.mark.parametrize("seed,noise,check_ori,ratio", [(1, 0.0, True, 0.9), (2, 3.0, True, 0.9), (3, 0.0, False, 0.7)])
+def test_search_for_initialization_oracle_matches_restatement(seed, noise, check_ori, ratio):
+    F1, F2, prev = ps.init_scene(seed, prev_noise=noise)
+    n, m, p = oracle_py.search_for_initialization(F1, F2, prev, 100, ratio, check_ori)
+    n2, m2, p2 = init_py(F1, F2, prev, 100, ratio, check_ori)
+    assert n == n2 and n > 100
+    np.testing.assert_array_equal(m, m2)
+    np.testing.assert_array_equal(p, p2)
+
+
+# ------------------------------------------------------------------ SearchBySim3 (ORBmatcher.cc:1102-1326)
+def sim3_py(KF1, T1w, mp1, KF2, T2w, mp2, s12, R12, t12, th):
+    inv_s = f32(1.0 / float(s12))
+    sR12 = [[f32(R12[r][c] * s12) for c in range(3)] for r in range(3)]
+    sR21 = [[f32(R12[c][r] * inv_s) for c in range(3)] for r in range(3)]
+    t21 = [f32(-float(f32(f32(f32(sR21[r][0] * t12[0]) + f32(sR21[r][1] * t12[1])) + f32(sR21[r][2] * t12[2]))))
+           for r in range(3)]
+    fx, fy, cx, cy = KF1.fx, KF1.fy, KF1.cx, KF1.cy
+
+    def direction(KF, T, mp, sR, t):
+        g = grid_py(KF)
+        bits = np.unpackbits(KF.desc, axis=1)
+        R = [[f32(T[r][c]) for c in range(3)] for r in range(3)]
+        tw = [f32(T[r][3]) for r in range(3)]
+        out = np.full(mp.n, -1, np.int32)
+        for i in range(mp.n):
+            if mp.skip[i] or mp.bad[i]:
+                continue
+            pc = _gemm33_fast(sR, _gemm33_fast(R, [f32(v) for v in mp.pos[i]], tw), t)
+            if pc[2] < 0:
+                continue
+            invz = f32(1.0 / float(pc[2]))
+            u = f32(f32(fx * f32(pc[0] * invz)) + cx)
+            v = f32(f32(fy * f32(pc[1] * invz)) + cy)
+            if not (u >= KF.min_x and u < KF.max_x and v >= KF.min_y and v < KF.max_y):
+                continue
+            d3 = _norm3(pc)
+            if d3 < f32(f32(0.8) * mp.min_dist[i]) or d3 > f32(f32(1.2) * mp.max_dist[i]):
+                continue
+            lvl = _predict_scale(mp.max_dist[i], d3, KF)
+            rad = f32(f32(th) * KF.scale_factors[lvl])
+            qb = np.unpackbits(mp.desc[i])
+            bd, bi = 2 ** 31 - 1, -1
+            for idx in area_py(KF, g, u, v, rad):
+                if KF.octave[idx] < lvl - 1 or KF.octave[idx] > lvl:
+                    continue
+                dist = int(np.count_nonzero(bits[idx] != qb))
+                if dist < bd:
+                    bd, bi = dist, idx
+            if bd <= 100:
+                out[i] = bi
+        return out
+
+    v1 = direction(KF2, T1w, mp1, sR21, t21)
+    v2 = direction(KF1, T2w, mp2, sR12, [f32(x) for x in t12])
+    m12 = np.full(mp1.n, -1, np.int32)
+    for i1 in range(mp1.n):
+        if v1[i1] >= 0 and v2[v1[i1]] == i1:
+            m12[i1] = v1[i1]
+    return int((m12 >= 0).sum()), m12
+
+
+@pytest.mark.parametrize("seed", [2, 5])
+def test_search_by_sim3_oracle_matches_restatement(seed):
+    sc = ps.sim3_pair_scene(seed)
+    n, m = oracle_py.search_by_sim3(*sc)
+    n2, m2 = sim3_py(*sc)
+    assert n == n2 and n > 100
+    np.testing.assert_array_equal(m, m2)
