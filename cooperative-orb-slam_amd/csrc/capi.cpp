@@ -495,8 +495,11 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
     return 0;
 }
 
+/* blur != nullptr: the whole-frame pyramid also blurs every level into it (ORBX_BLUR_IN_PYR); *fused tells
+ * whether it did (the per-level path never does) */
 static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fstride, int pitch, int nframes,
-                          hipStream_t st) {
+                          hipStream_t st, uint8_t* blur = nullptr, bool* fused = nullptr) {
+    if (fused) *fused = false;
     Geometry& g = h->geo;
     const ExtractParams& ep = g.ep;
     // pyramid levels 1..L-1 (ORBextractor.cc:1107-1132): whole-frame kernel for large batches of
@@ -507,7 +510,8 @@ static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fst
         for (int l = 1; l < ep.L; l++) max_groups = std::max(max_groups, (g.lv[l].w + 3) / 4);
         HIPR(launch_pyramid_frames(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, g.d_lv.as<LevelDesc>(),
                                    g.d_ptab.as<int>(), (const int2*)(g.d_ptab.as<int>() + g.pyr_band_off),
-                                   g.pyr_band_rows, max_groups, nframes, st));
+                                   g.pyr_band_rows, max_groups, nframes, st, blur));
+        if (fused) *fused = blur != nullptr;
         return 0;
     }
     for (int l = 1; l < ep.L; l++) {
@@ -552,6 +556,10 @@ static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstrid
 #define ORBX_ERR_STICKY 1  // device batch path: error flag sticky until orbx_check_error (0: reset every call)
 #endif
 constexpr bool kErrSticky = ORBX_ERR_STICKY != 0;
+#ifndef ORBX_BLUR_IN_PYR
+#define ORBX_BLUR_IN_PYR 0  // default of the ORBX_BLUR_IN_PYR env switch (1: blur fused into the whole-frame pyramid, -8.5 %, profiles/r03_ab_blur_in_pyr.log)
+#endif
+constexpr bool kBlurInPyrDefault = ORBX_BLUR_IN_PYR != 0;
 /* Error words of h->err: kErrSticky (word 0) collects the device batch paths' flags until orbx_check_error
  * takes them; kErrCall (word 1) is the host paths' per-call flag (zeroed and read by each call), so a host
  * call never erases an unread batch error; kErrTake (word 32) receives the atomic read-and-clear. */
@@ -581,21 +589,30 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         if (launch_fast(h, d_frames, fstride, pitch, 0, ncell0, nframes, sd)) return ORBX_EDEVICE;
     }
     if (prof_mark(h, 0, 0, st)) return ORBX_EDEVICE;
-    if (!skip_warm(1) && !(h->skip_mask & 1) && launch_pyramid(h, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
+    // the whole-frame pyramid may blur every level itself (ORBX_BLUR_IN_PYR); then no blur launch
+    static const bool blur_in_pyr = [] {
+        const char* e = getenv("ORBX_BLUR_IN_PYR");
+        return e ? atoi(e) != 0 : kBlurInPyrDefault;
+    }();
+    bool fused = false;
+    if (!skip_warm(1) && !(h->skip_mask & 1) &&
+        launch_pyramid(h, d_frames, fstride, pitch, nframes, st, blur_in_pyr ? h->blur.as<uint8_t>() : nullptr, &fused))
+        return ORBX_EDEVICE;
     if (prof_mark(h, 0, 1, st)) return ORBX_EDEVICE;
     auto blur = [&](hipStream_t bs) -> int {
         if (prof_mark(h, 3, 0, bs)) return ORBX_EDEVICE;
-        if (!skip_warm(8) && !(h->skip_mask & 8))
+        if (!fused && !skip_warm(8) && !(h->skip_mask & 8))
             HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                                     nullptr, g.nbjobs, nullptr, nframes, bs));
         return prof_mark(h, 3, 1, bs);
     };
-    if (!serial) {
+    const bool side_blur = !serial && !fused;  // a fused blur is already on `st`, ahead of describe
+    if (side_blur) {
         HIPR(hipEventRecord(h->ev_pyr, st));
         HIPR(hipStreamWaitEvent(sd, h->ev_pyr, 0));
         if (blur(sd)) return ORBX_EDEVICE;
         HIPR(hipEventRecord(h->ev_blur, sd));
-    } else if (blur_first) {
+    } else if (blur_first || (fused && !serial)) {
         if (blur(st)) return ORBX_EDEVICE;
     }
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
@@ -607,7 +624,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     if (prof_mark(h, 2, 1, st)) return ORBX_EDEVICE;
     if (serial) {
         if (!blur_first && blur(st)) return ORBX_EDEVICE;
-    } else {
+    } else if (side_blur) {
         HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     }
     if (prof_mark(h, 4, 0, st)) return ORBX_EDEVICE;

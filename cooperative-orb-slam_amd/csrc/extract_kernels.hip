@@ -209,6 +209,145 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
     }
 }
 
+/* ----------------------------------------------------------------------------------- */
+/* GaussianBlur 7x7, sigma 2, REFLECT_101, 8U fixed point (kernel 18,34,49,55,...; sum  */
+/* 257). Row strips of all levels of all frames in one grid.                            */
+/* ----------------------------------------------------------------------------------- */
+__device__ __forceinline__ int reflect101(int p, int n) {
+    p = p < 0 ? -p : p;
+    p = p >= n ? 2 * n - 2 - p : p;
+    return p;
+}
+
+constexpr int kBlurSeg = 264; // bytes of one staged row segment: strip (256) + 4 left + 4 right
+
+/* One wave per (frame, level, 256-column strip, 64-row chunk); each lane owns 4 adjacent output
+ * columns x0 = sx + 4*lane.
+ *  - Source row segment [sx-4, sx+260) is fetched once per wave with coalesced dword loads
+ *    (addresses clamped into the row), staged in LDS, and the REFLECT_101 halo bytes are
+ *    patched there by three lanes. Rows are prefetched 7 rows ahead into a register ring.
+ *  - Horizontal: the lane's 12 bytes are three LDS dwords; output i's taps are two byte
+ *    windows (alignbyte) dotted with the packed kernel by v_dot4_u32_u8.
+ *  - Vertical: the 7 row sums of the window live in registers as float pairs; the loop is
+ *    unrolled by 7 so the window rotates by renaming. All values are integers < 2^24 and the
+ *    weights are k/2^16, so every packed fma is exact: sf = s / 2^16 exactly.
+ *  - Rounding: OpenCV's SSE2 column path (x < w&~3) rounds s/2^16 half to even = rint(sf),
+ *    v_cvt_pk_u8_f32 (round-to-nearest-even, saturating); the scalar tail rounds half up,
+ *    floor(sf + 0.5) (DESIGN.md "Pinned semantics"; checked by tools/check_cvtpk.hip). */
+__device__ __forceinline__ float2v blur_vsum(const float2v r0, const float2v r1, const float2v r2, const float2v r3,
+                                            const float2v r4, const float2v r5, const float2v r6) {
+    const float k18 = 18.f / 65536.f, k34 = 34.f / 65536.f, k49 = 49.f / 65536.f, k55 = 55.f / 65536.f;
+    float2v v = r3 * (float2v){k55, k55};
+    v = __builtin_elementwise_fma(r2, (float2v){k49, k49}, v);
+    v = __builtin_elementwise_fma(r4, (float2v){k49, k49}, v);
+    v = __builtin_elementwise_fma(r1, (float2v){k34, k34}, v);
+    v = __builtin_elementwise_fma(r5, (float2v){k34, k34}, v);
+    v = __builtin_elementwise_fma(r0, (float2v){k18, k18}, v);
+    v = __builtin_elementwise_fma(r6, (float2v){k18, k18}, v);
+    return v;
+}
+
+/* one blur job: rows [chunk*kBlurRows, +kBlurRows) x columns [strip*256, +256) of a level (img / pitch,
+ * output out with the level's pitch), by one wave; rows = that wave's 7 x kBlurSeg LDS staging slots */
+template <bool kAligned>
+__device__ __forceinline__ void blur_job(const uint8_t* __restrict__ img, int pitch, const LevelDesc& lv,
+                                         uint8_t* __restrict__ out, int strip, int chunk, uint8_t (*rows)[kBlurSeg],
+                                         int lane) {
+    const int w = lv.w, h = lv.h;
+    const int sx = strip * 256;
+    const int x0 = sx + lane * 4;
+    const int ya = chunk * kBlurRows, yb = min(h, ya + kBlurRows);
+    const bool lane_on = x0 < w;
+    const bool tail = x0 + 3 >= lv.blur_vec_end;  // some of this lane's columns take the scalar path
+    const int seg0 = sx - 4;                      // segment byte 0 = column seg0
+    const int need_hi = min(sx + 256, w) + 3;     // columns [sx-3, need_hi) are read
+    // kAligned: every row of every level starts 4-aligned (pyramid levels always do; the
+    // caller's frames are checked at launch), so segment dwords are plain clamped loads
+    const int lastd = (w - 1) & ~3;
+    const int dA = iclamp(seg0 + 4 * lane, 0, lastd);
+    const int dB = lane < 2 ? iclamp(seg0 + 4 * (lane + 64), 0, lastd) : dA;
+    // dwords `lane` and `lane+64` (lanes 0..1) of source row yy's segment
+    auto fetch = [&](int yy, uint32_t& v0, uint32_t& v1) {
+        const uint8_t* row = img + (long long)reflect101(yy, h) * pitch;
+        if (kAligned) {
+            v0 = *(const uint32_t*)(row + dA);
+            v1 = *(const uint32_t*)(row + dB);
+        } else {
+            v0 = load_row_u32_clamped(row, seg0 + 4 * lane, w);
+            v1 = load_row_u32_clamped(row, seg0 + 4 * (lane + 64), w);
+        }
+    };
+    // stage one row into LDS slot k, patch its halo, return the lane's 4 row sums (as floats)
+    auto rowsum = [&](int k, uint32_t v0, uint32_t v1, float2v& lo, float2v& hi) {
+        ((uint32_t*)rows[k])[lane] = v0;
+        if (lane < 2) ((uint32_t*)rows[k])[lane + 64] = v1;
+        wave_sync();
+        // REFLECT_101 halo over the garbage bytes: column -1-q <- 1+q, column w+q <- w-2-q
+        if (lane < 3) {
+            const int q = lane;
+            if (sx == 0) rows[k][(-1 - q) - seg0] = rows[k][(1 + q) - seg0];
+            const int xr = w + q;
+            if (xr >= sx && xr < need_hi) rows[k][xr - seg0] = rows[k][(w - 2 - q) - seg0];
+        }
+        wave_sync();
+        const uint32_t* d = (const uint32_t*)rows[k] + lane;
+        const uint32_t w0 = d[0], w1 = d[1], w2 = d[2];  // columns x0-4 .. x0+7
+        const uint32_t K1 = 18u | 34u << 8 | 49u << 16 | 55u << 24, K2 = 49u | 34u << 8 | 18u << 16;
+        const uint32_t r0 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), K1,
+                                                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), K2, 0u, false), false);
+        const uint32_t r1 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), K1,
+                                                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), K2, 0u, false), false);
+        const uint32_t r2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), K1,
+                                                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), K2, 0u, false), false);
+        const uint32_t r3 = __builtin_amdgcn_udot4(w1, K1, __builtin_amdgcn_udot4(w2, K2, 0u, false), false);
+        lo = (float2v){(float)r0, (float)r1};
+        hi = (float2v){(float)r2, (float)r3};
+    };
+    auto emit = [&](int yo, float2v a, float2v b) {
+        if (!lane_on || yo >= yb) return;
+        float o[4] = {a.x, a.y, b.x, b.y};
+        if (tail) {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (x0 + i >= lv.blur_vec_end) o[i] = floorf(o[i] + 0.5f);
+        }
+        uint32_t packed = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) packed = __builtin_amdgcn_cvt_pk_u8_f32(o[i], (unsigned)i, packed);
+        uint8_t* p = out + (long long)yo * lv.pitch + x0;
+        if (x0 + 4 <= w) {
+            *(uint32_t*)p = packed;
+        } else {
+            for (int i = 0; i < 4 && x0 + i < w; i++) p[i] = (uint8_t)(packed >> (8 * i));
+        }
+    };
+    // window: rows y-3 .. y+3 of output row y live in slots (y - ya) .. (y - ya + 6) mod 7
+    float2v WL[7], WH[7];
+    uint32_t D0[7], D1[7];  // prefetched source rows: row ya+3+m in D[m mod 7]
+#pragma unroll
+    for (int m = 0; m < 6; m++) fetch(ya - 3 + m, D0[m], D1[m]);
+#pragma unroll
+    for (int m = 0; m < 6; m++) rowsum(m, D0[m], D1[m], WL[m], WH[m]);
+#pragma unroll
+    for (int m = 0; m < 7; m++) fetch(ya + 3 + m, D0[m], D1[m]);
+    // straight-line body: every step fetches (rows past the chunk are reflected, valid rows)
+    // and computes; only the stores are masked, so the prefetch waits stay counted (vmcnt(N))
+    for (int yi = ya; yi < yb; yi += 7) {
+#pragma unroll
+        for (int s = 0; s < 7; s++) {
+            const int y = yi + s;
+            const int ns = (s + 6) % 7;  // slot of the new row y+3
+            rowsum(ns, D0[s], D1[s], WL[ns], WH[ns]);
+            fetch(y + 10, D0[s], D1[s]);
+            const float2v a = blur_vsum(WL[s], WL[(s + 1) % 7], WL[(s + 2) % 7], WL[(s + 3) % 7], WL[(s + 4) % 7],
+                                       WL[(s + 5) % 7], WL[ns]);
+            const float2v b = blur_vsum(WH[s], WH[(s + 1) % 7], WH[(s + 2) % 7], WH[(s + 3) % 7], WH[(s + 4) % 7],
+                                       WH[(s + 5) % 7], WH[ns]);
+            emit(y, a, b);
+        }
+    }
+}
+
 /* Whole-pyramid form: one 512-thread workgroup per frame builds levels 1..L-1 in order
  * (level l+1 is read back from L2 right after this CU wrote level l; a workgroup barrier
  * separates the levels). A batch of >= 256 frames fills every CU with equal work, and the
@@ -234,18 +373,36 @@ static_assert(sizeof(PyrColGroup) == 48, "PyrColGroup layout");
  * column per thread leaves NT - (NT / gw) * gw threads idle: 22 % of a 512-thread workgroup at
  * 640x480's level 1); the level's column-group table is staged in LDS beside the row table and read
  * per item. Every output byte is computed by the same operations either way. */
-template <int U, int NT, bool FLAT>
+/* BLUR (ORBX_BLUR_IN_PYR): the workgroup also blurs every level (GaussianBlur 7x7, ORBextractor.cc:
+ * 1085-1086; the blur_job of k_blur_strips, same arithmetic) while the level is L2-resident: level l-1 is
+ * complete once level l's pass starts, so its blur jobs run in that pass after each wave's resize rows
+ * (no extra barrier), and the last level's after the loop. The frame's blurred levels need no separate
+ * launch or HBM re-read. (One band per frame only.) */
+template <int U, int NT, bool FLAT, bool BLUR>
 __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
                                                          int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
                                                          const LevelDesc* __restrict__ levels,
                                                          const int* __restrict__ ptab, const int2* __restrict__ bands,
-                                                         int rt_cap) {
+                                                         int rt_cap, uint8_t* __restrict__ blur) {
     // the current level's row table (this band's rows); sized at launch for the longest band range
     // (rows x 16 B: 6.4 KB at 640x480 with one band) instead of kPyrMaxRows, so the LDS the long-lived
     // pyramid workgroup holds stays free for the other graphs' FAST / describe workgroups beside it
     extern __shared__ int4 s_rt[];
+    __shared__ __align__(16) uint8_t s_blur[BLUR ? NT / 64 : 1][7][kBlurSeg];
     const int f = blockIdx.x / kPyrBands, band = blockIdx.x - f * kPyrBands, tid = threadIdx.x;
     uint8_t* P = pyr + (long long)f * ep.pyr_frame_bytes;
+    auto blur_level = [&](int lb) {
+        if constexpr (BLUR) {
+            const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+            const LevelDesc bl = levels[lb];
+            const uint8_t* img = lb == 0 ? frames + (long long)f * fstride : P + bl.pyr_off;
+            const int pitch = lb == 0 ? pitch0 : bl.pitch;
+            uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + bl.blur_off;
+            const int nstrips = (bl.w + 255) / 256, njobs = nstrips * ((bl.h + kBlurRows - 1) / kBlurRows);
+            for (int j = wave; j < njobs; j += NT / 64) blur_job<true>(img, pitch, bl, out, j % nstrips, j / nstrips,
+                                                                       s_blur[wave], lane);
+        }
+    };
     for (int l = 1; l < ep.L; l++) {
         const LevelDesc sv = levels[l - 1];
         const LevelDesc lv = levels[l];
@@ -333,6 +490,7 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
                     *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
                 }
             }
+            blur_level(l - 1);
             __syncthreads();
             continue;
         }
@@ -391,8 +549,10 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
                 }
             }
         }
+        blur_level(l - 1);
         __syncthreads();
     }
+    blur_level(ep.L - 1);
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -1310,44 +1470,6 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
     }
 }
 
-/* ----------------------------------------------------------------------------------- */
-/* GaussianBlur 7x7, sigma 2, REFLECT_101, 8U fixed point (kernel 18,34,49,55,...; sum  */
-/* 257). Row strips of all levels of all frames in one grid.                            */
-/* ----------------------------------------------------------------------------------- */
-__device__ __forceinline__ int reflect101(int p, int n) {
-    p = p < 0 ? -p : p;
-    p = p >= n ? 2 * n - 2 - p : p;
-    return p;
-}
-
-constexpr int kBlurSeg = 264; // bytes of one staged row segment: strip (256) + 4 left + 4 right
-
-/* One wave per (frame, level, 256-column strip, 64-row chunk); each lane owns 4 adjacent output
- * columns x0 = sx + 4*lane.
- *  - Source row segment [sx-4, sx+260) is fetched once per wave with coalesced dword loads
- *    (addresses clamped into the row), staged in LDS, and the REFLECT_101 halo bytes are
- *    patched there by three lanes. Rows are prefetched 7 rows ahead into a register ring.
- *  - Horizontal: the lane's 12 bytes are three LDS dwords; output i's taps are two byte
- *    windows (alignbyte) dotted with the packed kernel by v_dot4_u32_u8.
- *  - Vertical: the 7 row sums of the window live in registers as float pairs; the loop is
- *    unrolled by 7 so the window rotates by renaming. All values are integers < 2^24 and the
- *    weights are k/2^16, so every packed fma is exact: sf = s / 2^16 exactly.
- *  - Rounding: OpenCV's SSE2 column path (x < w&~3) rounds s/2^16 half to even = rint(sf),
- *    v_cvt_pk_u8_f32 (round-to-nearest-even, saturating); the scalar tail rounds half up,
- *    floor(sf + 0.5) (DESIGN.md "Pinned semantics"; checked by tools/check_cvtpk.hip). */
-__device__ __forceinline__ float2v blur_vsum(const float2v r0, const float2v r1, const float2v r2, const float2v r3,
-                                            const float2v r4, const float2v r5, const float2v r6) {
-    const float k18 = 18.f / 65536.f, k34 = 34.f / 65536.f, k49 = 49.f / 65536.f, k55 = 55.f / 65536.f;
-    float2v v = r3 * (float2v){k55, k55};
-    v = __builtin_elementwise_fma(r2, (float2v){k49, k49}, v);
-    v = __builtin_elementwise_fma(r4, (float2v){k49, k49}, v);
-    v = __builtin_elementwise_fma(r1, (float2v){k34, k34}, v);
-    v = __builtin_elementwise_fma(r5, (float2v){k34, k34}, v);
-    v = __builtin_elementwise_fma(r0, (float2v){k18, k18}, v);
-    v = __builtin_elementwise_fma(r6, (float2v){k18, k18}, v);
-    return v;
-}
-
 template <bool kAligned>
 __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                      const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
@@ -1364,105 +1486,11 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     // (the result of an unused level is never read), so the blur can run before the octree
     if (lvcnt && lvcnt[f * ep.L + l] == 0) return;
     const LevelDesc lv = levels[l];
-    const int w = lv.w, h = lv.h;
-    const int nstrips = (w + 255) / 256;
-    const int strip = j % nstrips, chunk = j / nstrips;
-    const int sx = strip * 256;
-    const int x0 = sx + lane * 4;
-    const int ya = chunk * kBlurRows, yb = min(h, ya + kBlurRows);
+    const int nstrips = (lv.w + 255) / 256;
     const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
     const int pitch = l == 0 ? pitch0 : lv.pitch;
     uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
-    const bool lane_on = x0 < w;
-    const bool tail = x0 + 3 >= lv.blur_vec_end;  // some of this lane's columns take the scalar path
-    const int seg0 = sx - 4;                      // segment byte 0 = column seg0
-    const int need_hi = min(sx + 256, w) + 3;     // columns [sx-3, need_hi) are read
-    uint8_t(*rows)[kBlurSeg] = s_rows[wave];
-    // kAligned: every row of every level starts 4-aligned (pyramid levels always do; the
-    // caller's frames are checked at launch), so segment dwords are plain clamped loads
-    const int lastd = (w - 1) & ~3;
-    const int dA = iclamp(seg0 + 4 * lane, 0, lastd);
-    const int dB = lane < 2 ? iclamp(seg0 + 4 * (lane + 64), 0, lastd) : dA;
-    // dwords `lane` and `lane+64` (lanes 0..1) of source row yy's segment
-    auto fetch = [&](int yy, uint32_t& v0, uint32_t& v1) {
-        const uint8_t* row = img + (long long)reflect101(yy, h) * pitch;
-        if (kAligned) {
-            v0 = *(const uint32_t*)(row + dA);
-            v1 = *(const uint32_t*)(row + dB);
-        } else {
-            v0 = load_row_u32_clamped(row, seg0 + 4 * lane, w);
-            v1 = load_row_u32_clamped(row, seg0 + 4 * (lane + 64), w);
-        }
-    };
-    // stage one row into LDS slot k, patch its halo, return the lane's 4 row sums (as floats)
-    auto rowsum = [&](int k, uint32_t v0, uint32_t v1, float2v& lo, float2v& hi) {
-        ((uint32_t*)rows[k])[lane] = v0;
-        if (lane < 2) ((uint32_t*)rows[k])[lane + 64] = v1;
-        wave_sync();
-        // REFLECT_101 halo over the garbage bytes: column -1-q <- 1+q, column w+q <- w-2-q
-        if (lane < 3) {
-            const int q = lane;
-            if (sx == 0) rows[k][(-1 - q) - seg0] = rows[k][(1 + q) - seg0];
-            const int xr = w + q;
-            if (xr >= sx && xr < need_hi) rows[k][xr - seg0] = rows[k][(w - 2 - q) - seg0];
-        }
-        wave_sync();
-        const uint32_t* d = (const uint32_t*)rows[k] + lane;
-        const uint32_t w0 = d[0], w1 = d[1], w2 = d[2];  // columns x0-4 .. x0+7
-        const uint32_t K1 = 18u | 34u << 8 | 49u << 16 | 55u << 24, K2 = 49u | 34u << 8 | 18u << 16;
-        const uint32_t r0 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), K1,
-                                                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), K2, 0u, false), false);
-        const uint32_t r1 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), K1,
-                                                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), K2, 0u, false), false);
-        const uint32_t r2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), K1,
-                                                   __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), K2, 0u, false), false);
-        const uint32_t r3 = __builtin_amdgcn_udot4(w1, K1, __builtin_amdgcn_udot4(w2, K2, 0u, false), false);
-        lo = (float2v){(float)r0, (float)r1};
-        hi = (float2v){(float)r2, (float)r3};
-    };
-    auto emit = [&](int yo, float2v a, float2v b) {
-        if (!lane_on || yo >= yb) return;
-        float o[4] = {a.x, a.y, b.x, b.y};
-        if (tail) {
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                if (x0 + i >= lv.blur_vec_end) o[i] = floorf(o[i] + 0.5f);
-        }
-        uint32_t packed = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) packed = __builtin_amdgcn_cvt_pk_u8_f32(o[i], (unsigned)i, packed);
-        uint8_t* p = out + (long long)yo * lv.pitch + x0;
-        if (x0 + 4 <= w) {
-            *(uint32_t*)p = packed;
-        } else {
-            for (int i = 0; i < 4 && x0 + i < w; i++) p[i] = (uint8_t)(packed >> (8 * i));
-        }
-    };
-    // window: rows y-3 .. y+3 of output row y live in slots (y - ya) .. (y - ya + 6) mod 7
-    float2v WL[7], WH[7];
-    uint32_t D0[7], D1[7];  // prefetched source rows: row ya+3+m in D[m mod 7]
-#pragma unroll
-    for (int m = 0; m < 6; m++) fetch(ya - 3 + m, D0[m], D1[m]);
-#pragma unroll
-    for (int m = 0; m < 6; m++) rowsum(m, D0[m], D1[m], WL[m], WH[m]);
-#pragma unroll
-    for (int m = 0; m < 7; m++) fetch(ya + 3 + m, D0[m], D1[m]);
-    // straight-line body: every step fetches (rows past the chunk are reflected, valid rows)
-    // and computes; only the stores are masked, so the prefetch waits stay counted (vmcnt(N))
-    for (int yi = ya; yi < yb; yi += 7) {
-#pragma unroll
-        for (int s = 0; s < 7; s++) {
-            const int y = yi + s;
-            const int ns = (s + 6) % 7;  // slot of the new row y+3
-            rowsum(ns, D0[s], D1[s], WL[ns], WH[ns]);
-            fetch(y + 10, D0[s], D1[s]);
-            const float2v a = blur_vsum(WL[s], WL[(s + 1) % 7], WL[(s + 2) % 7], WL[(s + 3) % 7], WL[(s + 4) % 7],
-                                       WL[(s + 5) % 7], WL[ns]);
-            const float2v b = blur_vsum(WH[s], WH[(s + 1) % 7], WH[(s + 2) % 7], WH[(s + 3) % 7], WH[(s + 4) % 7],
-                                       WH[(s + 5) % 7], WH[ns]);
-            emit(y, a, b);
-        }
-    }
+    blur_job<kAligned>(img, pitch, lv, out, j % nstrips, j / nstrips, s_rows[wave], lane);
 }
 
 /* rBRIEF test pairs as floats, one 16-byte load per test; stored (x0, x1, y0, y1) so the two points'
@@ -1773,20 +1801,26 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
                                  const ExtractParams& ep, const LevelDesc* levels, const int* ptab, const int2* bands,
-                                 int max_rows, int max_groups, int nframes, hipStream_t st) {
+                                 int max_rows, int max_groups, int nframes, hipStream_t st, uint8_t* blur) {
     if (max_rows < 1 || max_rows > kPyrMaxRows) return hipErrorInvalidValue;
+    if (blur && kPyrBands != 1) return hipErrorInvalidValue;
     // 512-thread workgroups pack beside the other graphs' kernels while every level
     // keeps >= 2 rows per pass; a level 1 wider than 4 x 256 columns (C4's 1034) would leave half the
     // threads idle, so such geometries take 1024 threads
     const dim3 grid(nframes * kPyrBands);
     // flat items: the row table and the widest level's column-group table (3 int4 per group) in LDS
     const size_t lds = (size_t)max_rows * sizeof(int4) + (kPyrFlatLds ? (size_t)max_groups * 3 * sizeof(int4) : 0);
-    if (max_groups <= kPyrThreads / 2)
-        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads, kPyrFlat>), grid, dim3(kPyrThreads), lds, st, frames,
-                           fstride, pitch0, pyr, ep, levels, ptab, bands, max_rows);
-    else
-        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax, kPyrFlat>), grid, dim3(kPyrThreadsMax), lds, st,
-                           frames, fstride, pitch0, pyr, ep, levels, ptab, bands, max_rows);
+#define ORBX_PYR_LAUNCH(NTH, BL)                                                                               \
+    hipLaunchKernelGGL((k_pyramid_frames<kPyrU, NTH, kPyrFlat, BL>), grid, dim3(NTH), lds, st, frames, fstride, pitch0, \
+                       pyr, ep, levels, ptab, bands, max_rows, blur)
+    if (max_groups <= kPyrThreads / 2) {
+        if (blur) ORBX_PYR_LAUNCH(kPyrThreads, true);
+        else ORBX_PYR_LAUNCH(kPyrThreads, false);
+    } else {
+        if (blur) ORBX_PYR_LAUNCH(kPyrThreadsMax, true);
+        else ORBX_PYR_LAUNCH(kPyrThreadsMax, false);
+    }
+#undef ORBX_PYR_LAUNCH
     return hipGetLastError();
 }
 
