@@ -1140,6 +1140,10 @@ void make_geom(MatchGeom& g, const float F12[9], float ex, float ey, int nlevels
     for (int o = 0; o < 16; o++) {
         g.th100[o] = o < nlevels ? 100 * scale[o] : 0.f;
         g.th384[o] = o < nlevels ? 3.84 * (double)sigma2[o] : 0.0;
+        // the smallest float >= th384: (double)d < th384 <=> d < th384f for every float d
+        float t = (float)g.th384[o];
+        if ((double)t < g.th384[o]) t = std::nextafter(t, INFINITY);
+        g.th384f[o] = t;
     }
 }
 

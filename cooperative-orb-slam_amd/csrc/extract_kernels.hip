@@ -1588,7 +1588,10 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
 #pragma unroll
     for (int q = 0; q < kTab; q++) {
         const int t = min(tid + q * NT, 255);
-        if (!kDescPatGlobal) my_pat[q] = kPatternF.t[t];
+        // the transposed table, read and stored linearly (slot t): the 8 lanes of a ds_write_b128 group
+        // write 128 consecutive bytes (a transposing store, slot (t % 16) * 16 + t / 16, put the group's
+        // eight 16-byte words 256 bytes apart: one bank, an 8-way conflict)
+        if (!kDescPatGlobal) my_pat[q] = kPatternT.t[t];
         my_ic[q] = ((const int2*)(ptab + ep.ic_off))[t];
     }
     const int g = (blk * kDescWaves + wave) * 4 + sub;  // octree output slot of this lane group
@@ -1603,7 +1606,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
     for (int q = 0; q < kTab; q++) {
         const int t = tid + q * NT;
         if (t >= 256) break;
-        if (!kDescPatGlobal) s_pat[(t & 15) * 16 + (t >> 4)] = my_pat[q];  // pair p at (p % 16) * 16 + p / 16
+        if (!kDescPatGlobal) s_pat[t] = my_pat[q];  // pair p at (p % 16) * 16 + p / 16 (kPatternT's order)
         s_ic[t] = my_ic[q];
     }
     if (blk == 0 && tid == 0) {

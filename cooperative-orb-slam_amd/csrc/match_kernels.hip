@@ -42,6 +42,16 @@ __device__ __forceinline__ bool epi_ok(float a, float b, float c, float x2, floa
     return (double)dsqr < th384;
 }
 
+/* the same test against the float threshold thf = 3.84*sigma2 rounded up to a float (MatchGeom::th384f):
+ * for a float dsqr, (double)dsqr < th384 <=> dsqr < thf, so the comparison is exact; thf < 0 rejects */
+__device__ __forceinline__ bool epi_ok_f(float a, float b, float c, float x2, float y2, float thf) {
+    const float num = __fadd_rn(__fadd_rn(__fmul_rn(a, x2), __fmul_rn(b, y2)), c);
+    const float den = __fadd_rn(__fmul_rn(a, a), __fmul_rn(b, b));
+    if (den == 0.f) return false;
+    const float dsqr = __fdiv_rn(__fmul_rn(num, num), den);
+    return dsqr < thf;
+}
+
 __device__ __forceinline__ void epi_line(const MatchGeom& g, float x1, float y1, float* a, float* b, float* c) {
     *a = __fadd_rn(__fadd_rn(__fmul_rn(x1, g.F[0]), __fmul_rn(y1, g.F[3])), g.F[6]);
     *b = __fadd_rn(__fadd_rn(__fmul_rn(x1, g.F[1]), __fmul_rn(y1, g.F[4])), g.F[7]);
@@ -387,7 +397,7 @@ __device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom&
 }
 
 /* fp4 form of tri_mfma_body (same roles and selection): per 64-candidate chunk each */
-/* thread expands 2 descriptor dwords of one candidate (8 KB of fragments in LDS instead of 16),  */
+/* thread expands descriptor dwords of one candidate (8 KB of fragments in LDS instead of 16),    */
 /* each wave runs 4 MFMAs per 32-candidate tile instead of 8, and the packed selection key is the */
 /* f32 accumulator's bit pattern (dot' is an even integer <= 256: its low 14 mantissa bits are     */
 /* zero) OR the tile row, whose signed maximum is the first candidate of maximum dot' = minimum D  */
@@ -397,8 +407,9 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
     static_assert(kMfWaves == 4 || kMfWaves == 8, "fp4 expansion roles: 4 waves (2 dwords per thread) or 8 (1)");
     constexpr int kDw = 512 / kMfThreads;  // descriptor dwords expanded per thread and chunk
     __shared__ v4i s_frag[2][4][64];  // [tile][step][lane] candidate fragments (fp4 +-1)
-    __shared__ float s_x[kMfChunk], s_y[kMfChunk];
-    __shared__ int s_oct[kMfChunk], s_ok[kMfChunk];
+    // per candidate (x, y, epipolar threshold thf or -1 when it is near the epipole / past n2): one
+    // ds_read_b128 per geometric check in the key walk (instead of four b32 reads + a threshold gather)
+    __shared__ float4 s_rec[kMfChunk];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int qblk = blockIdx.x * (32 * kMfWaves);
     if (qblk >= s.n1) return;  // block-uniform
@@ -420,8 +431,11 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
     }
     uint32_t best = 0xFFFFFFFFu;
     // expansion role: candidate ec of the chunk, descriptor dwords ed .. ed + kDw - 1 (dword d = step d / 2,
-    // half d % 2)
-    const int ec = tid / (8 / kDw), ed = (tid % (8 / kDw)) * kDw;
+    // half d % 2). Lanes 8i..8i+7 (one lane group of ds_write_b128) take 8 consecutive candidates of one
+    // dword, so their 16-byte fragment stores land on distinct banks (candidates in a group sharing a
+    // dword would all hit the same four banks: 8-way conflicts)
+    const int ec = (tid >> 6) * (64 / kMfWaves) + (tid & 7) + (kDw == 1 ? 0 : 8 * ((tid >> 5) & 1));
+    const int ed = kDw == 1 ? (tid >> 3) & 7 : 2 * ((tid >> 3) & 3);
     struct DwT { uint32_t w[kDw]; };
     auto load_chunk = [&](int cb, DwT& d, orbx_kp& k2) {
         const int c = min(cb + ec, s.n2 - 1);
@@ -439,11 +453,8 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
             for (int k = 0; k < kDw; k++)
                 s_frag[tile][(ed + k) >> 1][32 * ((ed + k) & 1) + r] = fp4_pm1_dword(on ? pd.w[k] : 0u);
             if (tid < kMfChunk) {
-                const bool on2 = cb + tid < s.n2;
-                s_x[tid] = pk.x;
-                s_y[tid] = pk.y;
-                s_oct[tid] = pk.octave;
-                s_ok[tid] = on2 && !near_epipole(g, pk.x, pk.y, pk.octave);
+                const bool on2 = cb + tid < s.n2 && !near_epipole(g, pk.x, pk.y, pk.octave);
+                s_rec[tid] = make_float4(pk.x, pk.y, on2 ? g.th384f[pk.octave] : -1.0f, 0.0f);
             }
         }
         __syncthreads();
@@ -483,7 +494,8 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
             uint32_t km = key(pmax);
             while (km < best && (km >> 16) <= 50u) {  // TH_LOW (ORBmatcher.cc:715)
                 const int jl = (int)(65535u - (km & 0xFFFFu)) - cb;
-                if (s_ok[jl] && epi_ok(la, lb, lc, s_x[jl], s_y[jl], g.th384[s_oct[jl]])) {
+                const float4 c2 = s_rec[jl];
+                if (epi_ok_f(la, lb, lc, c2.x, c2.y, c2.z)) {
                     best = km;
                     break;
                 }

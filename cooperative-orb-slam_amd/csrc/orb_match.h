@@ -14,6 +14,7 @@ struct MatchGeom {
     float ex, ey;
     float th100[16];
     double th384[16];
+    float th384f[16];  // th384 rounded up to a float: (double)d < th384 <=> d < th384f for a float d
 };
 
 /* device-side copy of an orbm_kf_view */
