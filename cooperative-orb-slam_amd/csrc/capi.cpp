@@ -14,7 +14,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <list>
+#include <memory>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/orbslam_amd.h"
@@ -1111,6 +1114,7 @@ struct orbm_ctx {
     size_t pinned_bytes = 0;
     uint8_t* ensure_pinned(size_t need) {
         if (need <= pinned_bytes) return (uint8_t*)pinned;
+        (void)hipStreamSynchronize(stream);  // the previous call may still be retiring (wait_call)
         if (pinned) (void)hipHostFree(pinned);
         pinned = nullptr;
         pinned_dev = nullptr;
@@ -1131,6 +1135,32 @@ struct orbm_ctx {
 };
 
 namespace {
+
+/* Wait for a per-call matcher launch: its last workgroup stores the match count (>= 0; the host
+ * pre-filled it with -1) into pinned host memory last, with release at system scope (match_kernels.hip
+ * call_tail), so polling that word ends the call ~5 us sooner than hipStreamSynchronize
+ * (tools/latency_floor.hip, profiles/r03_latency_floor.jsonl). The launch needs no further wait: the
+ * next call's copies and launches are ordered behind it on the stream. A stream that drains without
+ * the word, or an error, is ORBX_EDEVICE. ORBX_SYNC_WAIT=1 synchronises the stream instead (A/B). */
+int wait_call(hipStream_t st, const int32_t* word) {
+    static const bool sync_wait = [] {
+        const char* e = getenv("ORBX_SYNC_WAIT");
+        return e && atoi(e) != 0;
+    }();
+    if (!sync_wait) {
+        for (unsigned spins = 1; spins < (1u << 22); spins++) {
+            if (__atomic_load_n(word, __ATOMIC_ACQUIRE) >= 0) return 0;
+            if ((spins & 1023) == 0) {
+                const hipError_t e = hipStreamQuery(st);
+                if (e == hipErrorNotReady) continue;
+                if (e != hipSuccess) return ORBX_EDEVICE;
+                break;  // drained: the word is visible now if the kernel wrote it
+            }
+        }
+    }
+    HIPR(hipStreamSynchronize(st));
+    return __atomic_load_n(word, __ATOMIC_ACQUIRE) >= 0 ? 0 : ORBX_EDEVICE;
+}
 
 void make_geom(MatchGeom& g, const float F12[9], float ex, float ey, int nlevels, const float* scale,
                const float* sigma2) {
@@ -1177,16 +1207,35 @@ bool view_ok(const orbm_kf_view* v) {
            v->scale_factors && v->level_sigma2;
 }
 
+/* One keyframe's immutable per-feature arrays in HBM (orbm_kf_cache): mDescriptors, mvKeysUn (x, y, angle,
+ * octave), mvuRight, the FeatureVector's feature list and, for the projection matchers, its 64x48 feature
+ * grid (k_grid output). A call holds a shared_ptr to the entries it reads until its stream is synchronised,
+ * so an eviction by another thread never frees memory a running kernel reads. */
+struct KfEntry {
+    DevBuf buf;
+    int n = 0, nfeat = 0, n_nodes = 0;
+    bool has_ur = false, has_grid = false;
+    size_t o_desc = 0, o_x = 0, o_y = 0, o_ang = 0, o_oct = 0, o_ur = 0, o_feat = 0, o_gs = 0, o_gi = 0;
+    float min_x = 0, min_y = 0, gw_inv = 0, gh_inv = 0;  // grid bounds / scale the grid was built with
+    const uint8_t* at(size_t o) const { return buf.as<uint8_t>() + o; }
+};
+
 struct ViewPlan {
     size_t desc, x, y, angle, octave, uright, has_mp, mp_bad, feat;
     int nfeat;
 };
 /* geom = false (SearchByBoW): positions, octaves and mvuRight are not uploaded (the BoW matchers read
  * descriptors, MapPoint flags, angles and the node lists only) */
-void plan_view(Carve& c, const orbm_kf_view* v, ViewPlan& p, bool geom = true) {
+void plan_view(Carve& c, const orbm_kf_view* v, ViewPlan& p, bool geom = true, const KfEntry* ce = nullptr) {
     const size_t n = (size_t)std::max(v->n, 1);
     const size_t none = (size_t)-1;
     p.nfeat = v->n_nodes ? v->node_off[v->n_nodes] : 0;
+    if (ce) {  // cached keyframe: only the MapPoint flags (they change between calls) are staged
+        p.desc = p.x = p.y = p.angle = p.octave = p.uright = p.feat = none;
+        p.has_mp = v->has_mp ? c.take(n) : none;
+        p.mp_bad = v->mp_bad ? c.take(n) : none;
+        return;
+    }
     p.desc = c.take(32 * n);
     p.x = geom ? c.take(4 * n) : none;
     p.y = geom ? c.take(4 * n) : none;
@@ -1200,10 +1249,25 @@ void plan_view(Carve& c, const orbm_kf_view* v, ViewPlan& p, bool geom = true) {
 
 /* stage one view into the pinned host image of the scratch (offsets from plan_view) and return
  * the device view of the same offsets: a call then uploads all its inputs with ONE H2D copy */
-DevView stage_view(uint8_t* hbase, uint8_t* dbase, const orbm_kf_view* v, const ViewPlan& p) {
+DevView stage_view(uint8_t* hbase, uint8_t* dbase, const orbm_kf_view* v, const ViewPlan& p,
+                   const KfEntry* ce = nullptr) {
     DevView d;
     const size_t n = (size_t)v->n;
     d.n = v->n;
+    if (ce) {
+        d.desc = ce->at(ce->o_desc);
+        d.x = (const float*)ce->at(ce->o_x);
+        d.y = (const float*)ce->at(ce->o_y);
+        d.angle = (const float*)ce->at(ce->o_ang);
+        d.octave = (const int32_t*)ce->at(ce->o_oct);
+        d.uright = v->uright && ce->has_ur ? (const float*)ce->at(ce->o_ur) : nullptr;
+        d.node_feat = (const int32_t*)ce->at(ce->o_feat);
+        d.has_mp = v->has_mp ? dbase + p.has_mp : nullptr;
+        d.mp_bad = v->mp_bad ? dbase + p.mp_bad : nullptr;
+        if (n && v->has_mp) memcpy(hbase + p.has_mp, v->has_mp, n);
+        if (n && v->mp_bad) memcpy(hbase + p.mp_bad, v->mp_bad, n);
+        return d;
+    }
     d.desc = dbase + p.desc;
     const size_t none = (size_t)-1;
     d.x = p.x != none ? (const float*)(dbase + p.x) : nullptr;
@@ -1290,10 +1354,12 @@ void orbm_epipole(const float R2w[9], const float t2w[3], const float Cw[3], flo
     *ey = fy * C2[1] * invz + cy;
 }
 
-int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2,
-                                  const float F12[9], float ex, float ey, int only_stereo, int check_ori,
-                                  int32_t* match12, int* nmatches) {
-    if (!ctx || !view_ok(kf1) || !view_ok(kf2) || !F12 || !match12) return ORBX_EARG;
+}  // extern "C"
+
+/* c1 / c2: the keyframes' cached device arrays (orbm_kf_cache), or nullptr to upload them with the call */
+static int tri_common(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2, const float F12[9], float ex,
+                      float ey, int only_stereo, int check_ori, int32_t* match12, int* nmatches,
+                      const KfEntry* c1 = nullptr, const KfEntry* c2 = nullptr) {
     HIPR(hipSetDevice(ctx->device));
     std::vector<std::pair<int, int>> common;
     common_nodes(kf1, kf2, common);
@@ -1313,8 +1379,8 @@ int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const 
     // matches into pinned host memory pre-filled with -1, one synchronize
     Carve cv;
     ViewPlan p1, p2;
-    plan_view(cv, kf1, p1);
-    plan_view(cv, kf2, p2);
+    plan_view(cv, kf1, p1, true, c1);
+    plan_view(cv, kf2, p2, true, c2);
     const size_t o_tasks = cv.take(sizeof(NodeTask) * tasks.size());
     const size_t in_bytes = cv.off;
     const size_t o_list = cv.take(16 * (size_t)std::max(n1, 1));
@@ -1323,7 +1389,7 @@ int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const 
     uint8_t* hp = ctx->ensure_pinned(cv.off);
     if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
-    DevView d1 = stage_view(hp, base, kf1, p1), d2 = stage_view(hp, base, kf2, p2);
+    DevView d1 = stage_view(hp, base, kf1, p1, c1), d2 = stage_view(hp, base, kf2, p2, c2);
     memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
     int32_t* res = (int32_t*)(hp + o_res);
     std::fill(res, res + n1 + 1, -1);
@@ -1334,14 +1400,24 @@ int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const 
                         n1, check_ori ? 1 : 0, 0};
     HIPR(launch_tri_nodes(d1, d2, (const NodeTask*)(base + o_tasks), (int)tasks.size(), g, only_stereo, tail,
                           ctx->stream));
-    HIPR(hipStreamSynchronize(ctx->stream));
+    if (const int rc = wait_call(ctx->stream, res)) return rc;
     memcpy(match12, res + 1, 4 * (size_t)n1);
     if (nmatches) *nmatches = res[0];
     return 0;
 }
 
+extern "C" int orbm_search_for_triangulation(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2,
+                                             const float F12[9], float ex, float ey, int only_stereo, int check_ori,
+                                             int32_t* match12, int* nmatches) {
+    if (!ctx || !view_ok(kf1) || !view_ok(kf2) || !F12 || !match12) return ORBX_EARG;
+    return tri_common(ctx, kf1, kf2, F12, ex, ey, only_stereo, check_ori, match12, nmatches);
+}
+
+extern "C" {
+
 static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view* vc, float nnratio, int check_ori,
-                      int mode, int32_t* out, int nout, int* nmatches) {
+                      int mode, int32_t* out, int nout, int* nmatches, const KfEntry* cq = nullptr,
+                      const KfEntry* cc = nullptr) {
     HIPR(hipSetDevice(ctx->device));
     std::vector<std::pair<int, int>> common;
     common_nodes(vq, vc, common);
@@ -1363,8 +1439,8 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
     // matches into pinned host memory pre-filled with -1), one synchronize
     Carve cv;
     ViewPlan pq, pc;
-    plan_view(cv, vq, pq, false);
-    plan_view(cv, vc, pc, false);
+    plan_view(cv, vq, pq, false, cq);
+    plan_view(cv, vc, pc, false, cc);
     const size_t o_tasks = cv.take(sizeof(NodeTask) * tasks.size());
     const size_t in_bytes = cv.off;
     const size_t o_list = cv.take(16 * (size_t)std::max(nout, 1));
@@ -1373,7 +1449,7 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
     uint8_t* hp = ctx->ensure_pinned(cv.off);
     if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
-    DevView dq = stage_view(hp, base, vq, pq), dc = stage_view(hp, base, vc, pc);
+    DevView dq = stage_view(hp, base, vq, pq, cq), dc = stage_view(hp, base, vc, pc, cc);
     memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
     int32_t* res = (int32_t*)(hp + o_res);
     std::fill(res, res + nout + 1, -1);
@@ -1383,7 +1459,7 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
                         dc.angle, nout, check_ori ? 1 : 0, mode == 0 ? 1 : 0};
     HIPR(launch_bow(dq, dc, (const NodeTask*)(base + o_tasks), (int)tasks.size(), max_nc, nnratio, mode, tail,
                     ctx->stream));
-    HIPR(hipStreamSynchronize(ctx->stream));
+    if (const int rc = wait_call(ctx->stream, res)) return rc;
     memcpy(out, res + 1, 4 * (size_t)nout);
     if (nmatches) *nmatches = res[0];
     return 0;
@@ -1741,21 +1817,23 @@ bool frame_view_ok(const orbm_frame_view* F) {
 constexpr bool kProjDirect = ORBX_PROJ_DIRECT != 0;
 /* init_n >= 0: SearchForInitialization (k_init_resolve) with F = F2 and match[] = vnMatches12 of F1's init_n
  * keypoints; otherwise match[] has F->n entries */
+/* ce: the frame's cached device arrays and grid (orbm_kf_cache): only the queries travel, no k_grid */
 int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb, int accept_th, int ratio,
                    float nnratio, int check_ori, int32_t* match, int* nmatches, const float* inv_sigma2 = nullptr,
-                   int32_t* qres = nullptr, int init_n = -1) {
+                   int32_t* qres = nullptr, int init_n = -1, const KfEntry* ce = nullptr) {
     HIPR(hipSetDevice(ctx->device));
     const size_t n = (size_t)F->n, nq = pb.q.size();
     const size_t nout = init_n >= 0 ? (size_t)init_n : n;
+    const size_t nF = ce ? 0 : n;  // per-feature arrays uploaded with the call
     // inputs first (staged in pinned memory, one H2D copy), then outputs (one D2H copy), then scratch
     Carve cv;
-    const size_t o_call = cv.take(sizeof(ProjCall)), o_x = cv.take(4 * n), o_y = cv.take(4 * n),
-                 o_ang = cv.take(4 * n), o_ur = cv.take(4 * n), o_oct = cv.take(4 * n), o_occ = cv.take(n),
-                 o_desc = cv.take(32 * n), o_q = cv.take(sizeof(ProjQuery) * nq), o_qd = cv.take(32 * nq);
+    const size_t o_call = cv.take(sizeof(ProjCall)), o_x = cv.take(4 * nF), o_y = cv.take(4 * nF),
+                 o_ang = cv.take(4 * nF), o_ur = cv.take(4 * nF), o_oct = cv.take(4 * nF), o_occ = cv.take(n),
+                 o_desc = cv.take(32 * nF), o_q = cv.take(sizeof(ProjQuery) * nq), o_qd = cv.take(32 * nq);
     const size_t in_bytes = cv.off;
     const size_t o_nm = cv.take(4 * nout + 4);  // nmatches, then match[nout]
-    const size_t o_gs = cv.take(4 * (kGridCols * kGridRows + 1)), o_gi = cv.take(2 * n), o_scan = cv.take(32 * nq),
-                 o_scnt = cv.take(4 * nq), o_res = cv.take(8 * nq);
+    const size_t o_gs = cv.take(ce ? 0 : 4 * (kGridCols * kGridRows + 1)), o_gi = cv.take(2 * nF),
+                 o_scan = cv.take(32 * nq), o_scnt = cv.take(4 * nq), o_res = cv.take(8 * nq);
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
     uint8_t* hp = ctx->ensure_pinned(in_bytes + std::max(4 * nout + 4, 8 * nq));
     if (!hp) return ORBX_EDEVICE;
@@ -1789,6 +1867,16 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     c.n_out = (int)nout;
     c.grid_start = (int*)(base + o_gs);
     c.grid_idx = (uint16_t*)(base + o_gi);
+    if (ce) {
+        c.x = (const float*)ce->at(ce->o_x);
+        c.y = (const float*)ce->at(ce->o_y);
+        c.angle = (const float*)ce->at(ce->o_ang);
+        c.uright = F->uright && ce->has_ur ? (const float*)ce->at(ce->o_ur) : nullptr;
+        c.octave = (const int32_t*)ce->at(ce->o_oct);
+        c.desc = ce->at(ce->o_desc);
+        c.grid_start = (int*)ce->at(ce->o_gs);
+        c.grid_idx = (uint16_t*)ce->at(ce->o_gi);
+    }
     c.scan = (unsigned long long*)(base + o_scan);
     c.scan_cnt = (int*)(base + o_scnt);
     c.res = (int*)(base + o_res);
@@ -1797,13 +1885,13 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     if (inv_sigma2)
         for (int l = 0; l < F->nlevels; l++) c.inv_sigma2[l] = inv_sigma2[l];
     memcpy(hp + o_call, &c, sizeof(c));
-    if (n) {
+    if (n && F->occupied) memcpy(hp + o_occ, F->occupied, n);
+    if (nF) {
         memcpy(hp + o_x, F->x, 4 * n);
         memcpy(hp + o_y, F->y, 4 * n);
         if (F->angle) memcpy(hp + o_ang, F->angle, 4 * n);
         if (F->uright) memcpy(hp + o_ur, F->uright, 4 * n);
         memcpy(hp + o_oct, F->octave, 4 * n);
-        if (F->occupied) memcpy(hp + o_occ, F->occupied, n);
         memcpy(hp + o_desc, F->desc, 32 * n);
     }
     if (nq) {
@@ -1811,7 +1899,7 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
         memcpy(hp + o_qd, pb.qdesc.data(), 32 * nq);
     }
     HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, st));
-    HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st, !c.direct, init_n >= 0));
+    HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st, !c.direct, init_n >= 0, !ce));
     uint8_t* ho = hp + in_bytes;
     if (qres) {
         // per-query results (Fuse): res[2 qi] = the accepted feature or -1, reported at the query's src
@@ -2006,11 +2094,11 @@ int orbm_search_by_projection_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, con
 /* ===================================================================================== */
 extern "C" {
 
-int orbm_fuse(orbm_ctx* ctx, const orbm_frame_view* KF, const float Tcw[16], const float Ow[3],
-              const orbm_mappoints* mp, float th, const float* inv_level_sigma2, int32_t* best_idx, int* nfused) {
-    if (!ctx || !frame_view_ok(KF) || !Tcw || !Ow || !inv_level_sigma2 || !mp || mp->n < 0 ||
-        (mp->n && (!mp->desc || !mp->pos || !mp->normal || !mp->min_dist || !mp->max_dist || !best_idx)))
-        return ORBX_EARG;
+}  // extern "C"
+
+static int fuse_common(orbm_ctx* ctx, const orbm_frame_view* KF, const float Tcw[16], const float Ow[3],
+                       const orbm_mappoints* mp, float th, const float* inv_level_sigma2, int32_t* best_idx,
+                       int* nfused, const KfEntry* ce = nullptr) {
     const float* Rcw = Tcw;  // ORBmatcher.cc:827-837
     const float tcw[3] = {Tcw[3], Tcw[7], Tcw[11]};
     ProjBatch pb;
@@ -2042,7 +2130,8 @@ int orbm_fuse(orbm_ctx* ctx, const orbm_frame_view* KF, const float Tcw[16], con
     }
     orbm_frame_view K = *KF;
     K.occupied = nullptr;  // Fuse searches every feature
-    const int rc = run_projection(ctx, &K, pb, 50 /*TH_LOW*/, 0, 0.f, 0, nullptr, nullptr, inv_level_sigma2, best_idx);
+    const int rc = run_projection(ctx, &K, pb, 50 /*TH_LOW*/, 0, 0.f, 0, nullptr, nullptr, inv_level_sigma2, best_idx,
+                                  -1, ce);
     if (rc) return rc;
     if (nfused) {
         int nf = 0;
@@ -2051,6 +2140,21 @@ int orbm_fuse(orbm_ctx* ctx, const orbm_frame_view* KF, const float Tcw[16], con
     }
     return 0;
 }
+
+static bool fuse_args_ok(orbm_ctx* ctx, const orbm_frame_view* KF, const float Tcw[16], const float Ow[3],
+                         const orbm_mappoints* mp, const float* inv_level_sigma2, const int32_t* best_idx) {
+    return ctx && frame_view_ok(KF) && Tcw && Ow && inv_level_sigma2 && mp && mp->n >= 0 &&
+           !(mp->n && (!mp->desc || !mp->pos || !mp->normal || !mp->min_dist || !mp->max_dist || !best_idx));
+}
+
+extern "C" int orbm_fuse(orbm_ctx* ctx, const orbm_frame_view* KF, const float Tcw[16], const float Ow[3],
+                         const orbm_mappoints* mp, float th, const float* inv_level_sigma2, int32_t* best_idx,
+                         int* nfused) {
+    if (!fuse_args_ok(ctx, KF, Tcw, Ow, mp, inv_level_sigma2, best_idx)) return ORBX_EARG;
+    return fuse_common(ctx, KF, Tcw, Ow, mp, th, inv_level_sigma2, best_idx, nfused);
+}
+
+extern "C" {
 
 int orbm_fuse_sim3(orbm_ctx* ctx, const orbm_frame_view* KF, const float Scw[16], const orbm_mappoints* mp, float th,
                    int32_t* best_idx, int* nfused) {
@@ -2443,6 +2547,226 @@ int orbv_transform(orbv_handle* h, const uint8_t* desc, int n, int levelsup, uin
     *nbow = nb;
     *nfv = nf;
     return 0;
+}
+
+}  // extern "C"
+
+/* ===================================================================================== */
+/* Keyframe cache (orbm_kf_cache): KeyFrames' immutable per-feature arrays kept in HBM     */
+/* across the per-call matchers (LocalMapping::CreateNewMapPoints matches one KF1 against  */
+/* up to 20 neighbours, LocalMapping.cc:207-268; SearchInNeighbors fuses into them)        */
+/* ===================================================================================== */
+struct orbm_kf_cache {
+    int device = 0;
+    size_t capacity = 0;
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    struct Slot {
+        std::shared_ptr<KfEntry> e;
+        std::list<std::pair<int, uint64_t>>::iterator lru;
+    };
+    // kind 0: matcher views (orbm_kf_view: + FeatureVector), kind 1: projection views (orbm_frame_view: + grid)
+    std::unordered_map<uint64_t, Slot> map[2];
+    std::list<std::pair<int, uint64_t>> lru;  // front = most recently used
+    size_t bytes = 0;
+    long long hits = 0, misses = 0;
+};
+
+namespace {
+
+/* the cached entry for (kind, key) matching this call's view, uploading (or replacing) it when absent or
+ * stale (a different N, FeatureVector size, stereo presence or grid geometry); LRU eviction over the
+ * capacity. Returns nullptr on a device error. */
+std::shared_ptr<KfEntry> cache_get(orbm_kf_cache* c, int kind, uint64_t key, const orbm_kf_view* kv,
+                                   const orbm_frame_view* fv) {
+    const int n = kv ? kv->n : fv->n;
+    const int n_nodes = kv ? kv->n_nodes : 0;
+    const int nfeat = kv && kv->n_nodes ? kv->node_off[kv->n_nodes] : 0;
+    const bool has_ur = kv ? kv->uright != nullptr : fv->uright != nullptr;
+    std::lock_guard<std::mutex> lock(c->mu);
+    auto& m = c->map[kind];
+    auto it = m.find(key);
+    if (it != m.end()) {
+        const KfEntry& e = *it->second.e;
+        const bool same = e.n == n && e.n_nodes == n_nodes && e.nfeat == nfeat && (e.has_ur || !has_ur) &&
+                          (kind == 0 || (e.min_x == fv->min_x && e.min_y == fv->min_y && e.gw_inv == fv->grid_w_inv &&
+                                         e.gh_inv == fv->grid_h_inv));
+        if (same) {
+            c->hits++;
+            c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
+            return it->second.e;
+        }
+        c->bytes -= e.buf.bytes;
+        c->lru.erase(it->second.lru);
+        m.erase(it);  // in-flight calls keep their shared_ptr; the buffer goes with the last one
+    }
+    c->misses++;
+    auto e = std::make_shared<KfEntry>();
+    e->n = n;
+    e->n_nodes = n_nodes;
+    e->nfeat = nfeat;
+    e->has_ur = has_ur;
+    const size_t N = (size_t)std::max(n, 1);
+    Carve cv;
+    e->o_desc = cv.take(32 * N);
+    e->o_x = cv.take(4 * N);
+    e->o_y = cv.take(4 * N);
+    e->o_ang = cv.take(4 * N);
+    e->o_oct = cv.take(4 * N);
+    e->o_ur = cv.take(has_ur ? 4 * N : 0);
+    e->o_feat = cv.take(4 * (size_t)std::max(nfeat, 1));
+    size_t o_call = 0;
+    if (kind == 1) {
+        e->has_grid = true;
+        e->min_x = fv->min_x;
+        e->min_y = fv->min_y;
+        e->gw_inv = fv->grid_w_inv;
+        e->gh_inv = fv->grid_h_inv;
+        e->o_gs = cv.take(4 * (kGridCols * kGridRows + 1));
+        e->o_gi = cv.take(2 * N);
+        o_call = cv.take(sizeof(ProjCall));
+    }
+    if (hipSetDevice(c->device) != hipSuccess || e->buf.ensure(cv.off)) return nullptr;
+    std::vector<uint8_t> h(cv.off, 0);
+    const uint8_t* desc = kv ? kv->desc : fv->desc;
+    const float* x = kv ? kv->x : fv->x;
+    const float* y = kv ? kv->y : fv->y;
+    const float* ang = kv ? kv->angle : fv->angle;
+    const int32_t* oct = kv ? kv->octave : fv->octave;
+    const float* ur = kv ? kv->uright : fv->uright;
+    if (n) {
+        memcpy(h.data() + e->o_desc, desc, 32 * (size_t)n);
+        memcpy(h.data() + e->o_x, x, 4 * (size_t)n);
+        memcpy(h.data() + e->o_y, y, 4 * (size_t)n);
+        if (ang) memcpy(h.data() + e->o_ang, ang, 4 * (size_t)n);
+        memcpy(h.data() + e->o_oct, oct, 4 * (size_t)n);
+        if (has_ur) memcpy(h.data() + e->o_ur, ur, 4 * (size_t)n);
+    }
+    if (nfeat) memcpy(h.data() + e->o_feat, kv->node_feat, 4 * (size_t)nfeat);
+    if (kind == 1) {  // the KeyFrame's grid (AssignFeaturesToGrid), built once by k_grid
+        ProjCall pc;
+        memset(&pc, 0, sizeof(pc));
+        pc.x = (const float*)e->at(e->o_x);
+        pc.y = (const float*)e->at(e->o_y);
+        pc.n = n;
+        pc.min_x = fv->min_x;
+        pc.min_y = fv->min_y;
+        pc.gw_inv = fv->grid_w_inv;
+        pc.gh_inv = fv->grid_h_inv;
+        pc.grid_start = (int*)e->at(e->o_gs);
+        pc.grid_idx = (uint16_t*)e->at(e->o_gi);
+        memcpy(h.data() + o_call, &pc, sizeof(pc));
+    }
+    if (hipMemcpyAsync(e->buf.p, h.data(), cv.off, hipMemcpyHostToDevice, c->stream) != hipSuccess) return nullptr;
+    if (kind == 1 && launch_projection((const ProjCall*)e->at(o_call), 1, 0, c->stream, false) != hipSuccess)
+        return nullptr;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return nullptr;
+    c->lru.push_front({kind, key});
+    m[key] = orbm_kf_cache::Slot{e, c->lru.begin()};
+    c->bytes += e->buf.bytes;
+    while (c->bytes > c->capacity && c->lru.size() > 1) {  // evict the least recently used, never this one
+        const auto victim = c->lru.back();
+        auto& vm = c->map[victim.first];
+        auto vit = vm.find(victim.second);
+        c->bytes -= vit->second.e->buf.bytes;
+        vm.erase(vit);
+        c->lru.pop_back();
+    }
+    return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbm_kf_cache_create(int device, size_t capacity_bytes, orbm_kf_cache** out) {
+    if (!out) return ORBX_EARG;
+    *out = nullptr;
+    if (device < 0 || device >= orbx_device_count()) return ORBX_EDEVICE;
+    HIPR(hipSetDevice(device));
+    orbm_kf_cache* c = new orbm_kf_cache();
+    c->device = device;
+    c->capacity = capacity_bytes ? capacity_bytes : (size_t)1 << 30;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return ORBX_EDEVICE;
+    }
+    *out = c;
+    return 0;
+}
+
+void orbm_kf_cache_destroy(orbm_kf_cache* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->map[0].clear();
+    c->map[1].clear();
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int orbm_kf_cache_erase(orbm_kf_cache* c, uint64_t key) {
+    if (!c) return ORBX_EARG;
+    std::lock_guard<std::mutex> lock(c->mu);
+    for (auto& m : c->map) {
+        auto it = m.find(key);
+        if (it == m.end()) continue;
+        c->bytes -= it->second.e->buf.bytes;
+        c->lru.erase(it->second.lru);
+        m.erase(it);
+    }
+    return 0;
+}
+
+int orbm_kf_cache_stats(orbm_kf_cache* c, int* entries, size_t* bytes, long long* hits, long long* misses) {
+    if (!c) return ORBX_EARG;
+    std::lock_guard<std::mutex> lock(c->mu);
+    if (entries) *entries = (int)(c->map[0].size() + c->map[1].size());
+    if (bytes) *bytes = c->bytes;
+    if (hits) *hits = c->hits;
+    if (misses) *misses = c->misses;
+    return 0;
+}
+
+int orbm_search_for_triangulation_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key1, const orbm_kf_view* kf1,
+                                         uint64_t key2, const orbm_kf_view* kf2, const float F12[9], float ex, float ey,
+                                         int only_stereo, int check_ori, int32_t* match12, int* nmatches) {
+    if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf1) || !view_ok(kf2) || !F12 || !match12)
+        return ORBX_EARG;
+    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr);
+    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr) : nullptr;
+    if (!c1 || !c2) return ORBX_EDEVICE;
+    return tri_common(ctx, kf1, kf2, F12, ex, ey, only_stereo, check_ori, match12, nmatches, c1.get(), c2.get());
+}
+
+int orbm_search_by_bow_kf_kf_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key1, const orbm_kf_view* kf1,
+                                    uint64_t key2, const orbm_kf_view* kf2, float nnratio, int check_ori,
+                                    int32_t* match12, int* nmatches) {
+    if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf1) || !view_ok(kf2) || !match12)
+        return ORBX_EARG;
+    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr);
+    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr) : nullptr;
+    if (!c1 || !c2) return ORBX_EDEVICE;
+    return bow_common(ctx, kf1, kf2, nnratio, check_ori, 1, match12, kf1->n, nmatches, c1.get(), c2.get());
+}
+
+int orbm_search_by_bow_kf_f_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key, const orbm_kf_view* kf,
+                                   const orbm_kf_view* f, float nnratio, int check_ori, int32_t* match_f,
+                                   int* nmatches) {
+    if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf) || !view_ok(f) || !match_f) return ORBX_EARG;
+    const std::shared_ptr<KfEntry> ck = cache_get(cache, 0, key, kf, nullptr);
+    if (!ck) return ORBX_EDEVICE;
+    return bow_common(ctx, kf, f, nnratio, check_ori, 0, match_f, f->n, nmatches, ck.get(), nullptr);
+}
+
+int orbm_fuse_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key, const orbm_frame_view* KF, const float Tcw[16],
+                     const float Ow[3], const orbm_mappoints* mp, float th, const float* inv_level_sigma2,
+                     int32_t* best_idx, int* nfused) {
+    if (!cache || !fuse_args_ok(ctx, KF, Tcw, Ow, mp, inv_level_sigma2, best_idx) || cache->device != ctx->device)
+        return ORBX_EARG;
+    const std::shared_ptr<KfEntry> ck = cache_get(cache, 1, key, nullptr, KF);
+    if (!ck) return ORBX_EDEVICE;
+    return fuse_common(ctx, KF, Tcw, Ow, mp, th, inv_level_sigma2, best_idx, nfused, ck.get());
 }
 
 }  // extern "C"

@@ -886,8 +886,8 @@ __global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict_
 int init_max_features() { return kInitMaxN; }
 
 hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st, bool resolve,
-                             bool init) {
-    hipLaunchKernelGGL(k_grid, dim3(ncalls), dim3(1024), 0, st, d_calls);
+                             bool init, bool grid) {
+    if (grid) hipLaunchKernelGGL(k_grid, dim3(ncalls), dim3(1024), 0, st, d_calls);
     if (max_nq > 0) hipLaunchKernelGGL(k_proj_scan, dim3((max_nq + 15) / 16, ncalls), dim3(256), 0, st, d_calls);
     if (init) hipLaunchKernelGGL(k_init_resolve, dim3(ncalls), dim3(64), 0, st, d_calls);
     else if (resolve) hipLaunchKernelGGL(k_proj_resolve, dim3(ncalls), dim3(64), 0, st, d_calls);

@@ -69,7 +69,7 @@ hipError_t launch_tri_slots(const QueryKF& q, const uint8_t* slots, long long sl
                             int32_t* nmatches, int32_t* err, hipStream_t st);
 
 hipError_t launch_projection(const ProjCall* d_calls, int ncalls, int max_nq, hipStream_t st, bool resolve = true,
-                             bool init = false);
+                             bool init = false, bool grid = true);
 int init_max_features();
 hipError_t launch_distinctive(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best_idx,
                               uint8_t* out_desc, hipStream_t st);

@@ -615,12 +615,15 @@ __device__ void call_tail(const CallTail& t) {
         }
     }
     atomicAdd(&s_cnt, local);
+    __threadfence_system();  // this wave's match writes reach host memory before the count
     __syncthreads();
     if (threadIdx.x < 30) t.state[2 + threadIdx.x] = 0;
     if (threadIdx.x == 0) {
-        t.host_out[0] = s_cnt;
         t.state[1] = 0;
         t.state[0] = 0;
+        // the count is the call's completion word: the host polls it (capi.cpp wait_call) instead of
+        // synchronising the stream, so it is stored last, with release at system scope
+        __hip_atomic_store(t.host_out, s_cnt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

@@ -9,8 +9,10 @@
  * locks: GetMapPointMatches, GetRotation/GetTranslation/GetCameraCenter) into an
  * orbm_kf_view and runs the matcher kernels; results are converted back to the reference's
  * containers. One orbm_ctx per calling thread (Tracking, LocalMapping, LoopClosing call
- * concurrently). A device failure does not throw (orbamd_status.h): the call returns 0 with the
- * reference's empty result (no pairs / a NULL-filled match vector) and logs the status.
+ * concurrently). KeyFrames' immutable arrays are kept in HBM across calls (the process-wide
+ * orbm_kf_cache of orbamd_status.h; ORBAMD_KF_CACHE_MB=0 turns it off). A device failure does not
+ * throw (orbamd_status.h): the call returns 0 with the reference's empty result (no pairs / a
+ * NULL-filled match vector) and logs the status.
  */
 #include <algorithm>
 #include <cstdlib>
@@ -120,7 +122,13 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F
     std::vector<int32_t> m12((size_t)std::max(pKF1->N, 1));
     int n = 0;
     vMatchedPairs.clear();
+    orbm_kf_cache* kc = amd::KeyFrameCache();
     if (!run("orbm_search_for_triangulation", [&](orbm_ctx* c) {
+            if (kc)  // both keyframes' arrays stay in HBM across LocalMapping's ~20 calls per keyframe
+                return orbm_search_for_triangulation_cached(c, kc, amd::KeyFrameKey(pKF1, pKF1->mnId), &v1.v,
+                                                            amd::KeyFrameKey(pKF2, pKF2->mnId), &v2.v, F.ptr<float>(),
+                                                            ex, ey, bOnlyStereo ? 1 : 0, mbCheckOrientation ? 1 : 0,
+                                                            m12.data(), &n);
             return orbm_search_for_triangulation(c, &v1.v, &v2.v, F.ptr<float>(), ex, ey, bOnlyStereo ? 1 : 0,
                                                  mbCheckOrientation ? 1 : 0, m12.data(), &n);
         }))
@@ -145,7 +153,11 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpM
     std::vector<int32_t> mf((size_t)std::max(F.N, 1));
     int n = 0;
     vpMapPointMatches = std::vector<MapPoint*>(F.N, static_cast<MapPoint*>(NULL));  // :163
+    orbm_kf_cache* kc = amd::KeyFrameCache();
     if (!run("orbm_search_by_bow_kf_f", [&](orbm_ctx* c) {
+            if (kc)
+                return orbm_search_by_bow_kf_f_cached(c, kc, amd::KeyFrameKey(pKF, pKF->mnId), &vk.v, &vf.v, mfNNratio,
+                                                      mbCheckOrientation ? 1 : 0, mf.data(), &n);
             return orbm_search_by_bow_kf_f(c, &vk.v, &vf.v, mfNNratio, mbCheckOrientation ? 1 : 0, mf.data(), &n);
         }))
         return 0;
@@ -170,7 +182,12 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint
     std::vector<int32_t> m12(vpMapPoints1.size() ? vpMapPoints1.size() : 1);
     int n = 0;
     vpMatches12 = std::vector<MapPoint*>(vpMapPoints1.size(), static_cast<MapPoint*>(NULL));  // :536
+    orbm_kf_cache* kc = amd::KeyFrameCache();
     if (!run("orbm_search_by_bow_kf_kf", [&](orbm_ctx* c) {
+            if (kc)
+                return orbm_search_by_bow_kf_kf_cached(c, kc, amd::KeyFrameKey(pKF1, pKF1->mnId), &v1.v,
+                                                       amd::KeyFrameKey(pKF2, pKF2->mnId), &v2.v, mfNNratio,
+                                                       mbCheckOrientation ? 1 : 0, m12.data(), &n);
             return orbm_search_by_bow_kf_kf(c, &v1.v, &v2.v, mfNNratio, mbCheckOrientation ? 1 : 0, m12.data(), &n);
         }))
         return 0;

@@ -287,7 +287,11 @@ int ORBmatcher::Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, c
     T[15] = 1.f;
     std::vector<int32_t> best(n ? n : 1);
     int nf = 0;
+    orbm_kf_cache* kc = amd::KeyFrameCache();
     if (!run("orbm_fuse", [&](orbm_ctx* c) {
+            if (kc)  // the keyframe's arrays and feature grid stay in HBM across SearchInNeighbors' calls
+                return orbm_fuse_cached(c, kc, amd::KeyFrameKey(pKF, pKF->mnId), &fs.v, T, O, &ps.m, th,
+                                        pKF->mvInvLevelSigma2.data(), best.data(), &nf);
             return orbm_fuse(c, &fs.v, T, O, &ps.m, th, pKF->mvInvLevelSigma2.data(), best.data(), &nf);
         }))
         return 0;

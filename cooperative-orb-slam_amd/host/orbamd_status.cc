@@ -45,5 +45,19 @@ orbm_ctx* ThreadMatcher() {
     return h.c;
 }
 
+orbm_kf_cache* KeyFrameCache() {
+    static orbm_kf_cache* cache = [] {
+        const char* mb = getenv("ORBAMD_KF_CACHE_MB");
+        const long long cap = mb ? atoll(mb) : 1024;
+        if (cap <= 0) return (orbm_kf_cache*)nullptr;
+        const char* dev = getenv("ORBAMD_DEVICE");
+        orbm_kf_cache* c = nullptr;
+        if (!StatusOk(orbm_kf_cache_create(dev ? atoi(dev) : 0, (size_t)cap << 20, &c), "orbm_kf_cache_create"))
+            return (orbm_kf_cache*)nullptr;
+        return c;
+    }();
+    return cache;
+}
+
 }  // namespace amd
 }  // namespace ORB_SLAM2

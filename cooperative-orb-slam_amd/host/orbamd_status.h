@@ -13,6 +13,8 @@
 #ifndef ORBAMD_STATUS_H
 #define ORBAMD_STATUS_H
 
+#include <stdint.h>
+
 #include "orbslam_amd.h"
 
 namespace ORB_SLAM2 {
@@ -28,6 +30,14 @@ int LastStatus();
  * objects of the Tracking / LocalMapping / LoopClosing threads), created on first use on device
  * ORBAMD_DEVICE (default 0); nullptr (status recorded) when no device is usable. */
 orbm_ctx* ThreadMatcher();
+/* the process-wide keyframe cache of the drop-in matchers (orbm_kf_cache on ORBAMD_DEVICE, capacity
+ * ORBAMD_KF_CACHE_MB MiB, default 1024; ORBAMD_KF_CACHE_MB=0 disables it: nullptr, the uncached calls) */
+orbm_kf_cache* KeyFrameCache();
+/* cache key of a KeyFrame: its address mixed with mnId (ORB-SLAM2 never frees a KeyFrame, and the id
+ * guards against an address reused after one is freed) */
+inline uint64_t KeyFrameKey(const void* pKF, unsigned long mnId) {
+    return (uint64_t)(uintptr_t)pKF ^ ((uint64_t)mnId * 0x9E3779B97F4A7C15ull);
+}
 
 }  // namespace amd
 }  // namespace ORB_SLAM2

@@ -11,7 +11,7 @@ compute calls raise.
 """
 from ._lib import LIB_PATH, KP_FIELDS, load  # noqa: F401
 from .extractor import ORBextractor, synth_frames, kp_dtype  # noqa: F401
-from .matcher import ORBmatcher, KeyFrameView, epipole, compute_f12  # noqa: F401
+from .matcher import ORBmatcher, KeyFrameView, KeyFrameCache, epipole, compute_f12  # noqa: F401
 from . import device, frame, projection  # noqa: F401
 from .projection import FrameView, MapPoints  # noqa: F401
 from .vocabulary import ORBVocabulary  # noqa: F401

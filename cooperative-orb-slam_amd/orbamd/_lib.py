@@ -140,6 +140,17 @@ SIGNATURES = {
     "orbm_fuse": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, C.POINTER(_I)]),
     "orbm_fuse_sim3": (_I, [_P, _P, _P, _P, _F, _P, C.POINTER(_I)]),
     "orbm_search_for_initialization": (_I, [_P, _P, _P, _P, _I, _F, _I, _P, C.POINTER(_I)]),
+    "orbm_kf_cache_create": (_I, [_I, _SZ, C.POINTER(_P)]),
+    "orbm_kf_cache_destroy": (None, [_P]),
+    "orbm_kf_cache_erase": (_I, [_P, C.c_uint64]),
+    "orbm_kf_cache_stats": (_I, [_P, C.POINTER(_I), C.POINTER(_SZ), C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
+    "orbm_search_for_triangulation_cached": (_I, [_P, _P, C.c_uint64, C.POINTER(OrbmKfView), C.c_uint64,
+                                                  C.POINTER(OrbmKfView), _P, _F, _F, _I, _I, _P, C.POINTER(_I)]),
+    "orbm_search_by_bow_kf_kf_cached": (_I, [_P, _P, C.c_uint64, C.POINTER(OrbmKfView), C.c_uint64,
+                                             C.POINTER(OrbmKfView), _F, _I, _P, C.POINTER(_I)]),
+    "orbm_search_by_bow_kf_f_cached": (_I, [_P, _P, C.c_uint64, C.POINTER(OrbmKfView), C.POINTER(OrbmKfView), _F,
+                                            _I, _P, C.POINTER(_I)]),
+    "orbm_fuse_cached": (_I, [_P, _P, C.c_uint64, _P, _P, _P, _P, _F, _P, _P, C.POINTER(_I)]),
     "orbm_search_by_sim3": (_I, [_P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _F, _P, C.POINTER(_I)]),
     "orbm_compute_distinctive_descriptors": (_I, [_P, _I, _P, _P, _P, _P]),
     "orbv_load_text": (_I, [C.c_char_p, _I, C.POINTER(_P)]),

@@ -81,6 +81,37 @@ def compute_f12(R1w, t1w, R2w, t2w, K1, K2):
     return (np.linalg.inv(K1.T) @ tx @ R12 @ np.linalg.inv(K2)).astype(np.float32)
 
 
+class KeyFrameCache:
+    """orbm_kf_cache: keyframes' immutable per-feature arrays kept in HBM across matcher calls (the
+    *Cached matcher methods take it with a 64-bit key per keyframe)."""
+
+    def __init__(self, capacity_bytes=0, device=0):
+        self._lib = load()
+        h = C.c_void_p()
+        check(self._lib.orbm_kf_cache_create(device, capacity_bytes, C.byref(h)), "orbm_kf_cache_create")
+        self._h = h
+
+    def erase(self, key):
+        check(self._lib.orbm_kf_cache_erase(self._h, C.c_uint64(key)), "orbm_kf_cache_erase")
+
+    def stats(self):
+        e, b, hi, mi = C.c_int(), C.c_size_t(), C.c_longlong(), C.c_longlong()
+        check(self._lib.orbm_kf_cache_stats(self._h, C.byref(e), C.byref(b), C.byref(hi), C.byref(mi)),
+              "orbm_kf_cache_stats")
+        return {"entries": e.value, "bytes": b.value, "hits": hi.value, "misses": mi.value}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.orbm_kf_cache_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ORBmatcher:
     """ORB_SLAM2::ORBmatcher(nnratio=0.6, checkOri=true) -- device-backed."""
     TH_HIGH = TH_HIGH
@@ -140,6 +171,47 @@ class ORBmatcher:
                                                 int(self.mbCheckOrientation), out.ctypes.data, C.byref(n)),
               "orbm_search_by_bow_kf_f")
         return n.value, out[:other.n]
+
+    # ---- the same matchers with keyframes held in a KeyFrameCache (identical results)
+    def SearchForTriangulationCached(self, cache, key1, kf1, key2, kf2, F12, ex, ey, bOnlyStereo=False):
+        F = np.ascontiguousarray(F12, np.float32).reshape(9)
+        out = np.empty(max(kf1.n, 1), np.int32)
+        n = C.c_int()
+        v1, v2 = kf1.cview(), kf2.cview()
+        check(self._lib.orbm_search_for_triangulation_cached(self._h, cache._h, key1, C.byref(v1), key2, C.byref(v2),
+                                                             F.ctypes.data, ex, ey, int(bOnlyStereo),
+                                                             int(self.mbCheckOrientation), out.ctypes.data,
+                                                             C.byref(n)), "orbm_search_for_triangulation_cached")
+        return n.value, out[:kf1.n]
+
+    def SearchByBoWCached(self, cache, key, kf, other, other_is_keyframe=False, key2=None):
+        v1, v2 = kf.cview(), other.cview()
+        n = C.c_int()
+        if other_is_keyframe:
+            out = np.empty(max(kf.n, 1), np.int32)
+            check(self._lib.orbm_search_by_bow_kf_kf_cached(self._h, cache._h, key, C.byref(v1), key2, C.byref(v2),
+                                                            self.mfNNratio, int(self.mbCheckOrientation),
+                                                            out.ctypes.data, C.byref(n)),
+                  "orbm_search_by_bow_kf_kf_cached")
+            return n.value, out[:kf.n]
+        out = np.empty(max(other.n, 1), np.int32)
+        check(self._lib.orbm_search_by_bow_kf_f_cached(self._h, cache._h, key, C.byref(v1), C.byref(v2),
+                                                       self.mfNNratio, int(self.mbCheckOrientation), out.ctypes.data,
+                                                       C.byref(n)), "orbm_search_by_bow_kf_f_cached")
+        return n.value, out[:other.n]
+
+    def FuseCached(self, cache, key, KF, Tcw, Ow, mps, th, inv_level_sigma2):
+        m = mps.cstruct()
+        fv = KF.cstruct()
+        T = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+        O = np.ascontiguousarray(Ow, np.float32).reshape(3)
+        inv = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        out = np.empty(max(mps.n, 1), np.int32)
+        n = C.c_int()
+        check(self._lib.orbm_fuse_cached(self._h, cache._h, key, C.byref(fv), T.ctypes.data, O.ctypes.data,
+                                         C.byref(m), C.c_float(th), inv.ctypes.data, out.ctypes.data, C.byref(n)),
+              "orbm_fuse_cached")
+        return n.value, out[:mps.n]
 
     # ---- SearchByProjection x4 (ORBmatcher.cc:45-129, 1328-1470, 1472-1599, 290-403). Each returns
     # (nmatches, match[F.n]): index into the MapPoints of the assignment made to that feature

@@ -351,6 +351,39 @@ int orbm_search_by_sim3(orbm_ctx* ctx, const orbm_frame_view* KF1, const float T
                         const float R12[9], const float t12[3], float th, int32_t* match12, int* nfound);
 
 /* ------------------------------------------------------------------------------------
+ * Keyframe cache: a KeyFrame's descriptors, mvKeysUn (x, y, angle, octave), mvuRight and
+ * FeatureVector never change after KeyFrame::ComputeBoW, but the reference's matchers read them
+ * again on every call (LocalMapping::CreateNewMapPoints matches one keyframe against up to 20
+ * neighbours, LocalMapping.cc:207-268; SearchInNeighbors fuses into each of them, :454-520). The
+ * cache keeps them in HBM across calls and threads (thread-safe, shared by every orbm_ctx of its
+ * device), keyed by a caller-chosen 64-bit key (the drop-ins use the KeyFrame's address and mnId).
+ * The *_cached matchers equal their uncached forms (same arguments, same results); the views must
+ * still be complete: an absent or stale entry (different N, FeatureVector size or grid geometry)
+ * is uploaded from them, and the per-call MapPoint flags (has_mp, mp_bad, occupied) are always
+ * taken from the view. Least-recently-used entries are evicted above capacity_bytes (0 = 1 GiB).
+ * ---------------------------------------------------------------------------------- */
+typedef struct orbm_kf_cache orbm_kf_cache;
+int orbm_kf_cache_create(int device, size_t capacity_bytes, orbm_kf_cache** out);
+void orbm_kf_cache_destroy(orbm_kf_cache* cache);
+/* drop a keyframe's entries (e.g. from KeyFrame::SetBadFlag); unknown keys are ignored */
+int orbm_kf_cache_erase(orbm_kf_cache* cache, uint64_t key);
+int orbm_kf_cache_stats(orbm_kf_cache* cache, int* entries, size_t* bytes, long long* hits, long long* misses);
+int orbm_search_for_triangulation_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key1, const orbm_kf_view* kf1,
+                                         uint64_t key2, const orbm_kf_view* kf2, const float F12[9], float ex,
+                                         float ey, int only_stereo, int check_ori, int32_t* match12, int* nmatches);
+int orbm_search_by_bow_kf_kf_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key1, const orbm_kf_view* kf1,
+                                    uint64_t key2, const orbm_kf_view* kf2, float nnratio, int check_ori,
+                                    int32_t* match12, int* nmatches);
+/* the Frame side is not cached (a Frame is matched once) */
+int orbm_search_by_bow_kf_f_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key, const orbm_kf_view* kf,
+                                   const orbm_kf_view* f, float nnratio, int check_ori, int32_t* match_f,
+                                   int* nmatches);
+/* the keyframe's arrays and its feature grid (AssignFeaturesToGrid) are cached */
+int orbm_fuse_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key, const orbm_frame_view* KF, const float Tcw[16],
+                     const float Ow[3], const orbm_mappoints* mp, float th, const float* inv_level_sigma2,
+                     int32_t* best_idx, int* nfused);
+
+/* ------------------------------------------------------------------------------------
  * MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:242-307) for a batch of MapPoints.
  * MapPoint p's observed descriptors (the rows pKF->mDescriptors.row(idx) of its non-bad
  * observing KeyFrames, in mObservations order) are desc[offsets[p] .. offsets[p+1]) (32 B

@@ -179,6 +179,28 @@ int main(int argc, char** argv) {
         c = time_us(reps / 2, [&] { nc = oc_search_by_bow_kf_kf(&a.v, &b.v, 0.75f, 1, mc.data()); });
         row("bow_kf_kf", "SearchByBoW(KF, KF), ~90 nodes, 80% MapPoints, ratio 0.75 (LoopClosing.cc:267)", g, c,
             ng == nc && mg == mc, ng);
+        // the same three calls with both keyframes held in the device keyframe cache (orbm_kf_cache): the
+        // drop-ins' default (LocalMapping reuses one keyframe for ~20 calls, LocalMapping.cc:207-268)
+        orbm_kf_cache* kc = nullptr;
+        if (orbm_kf_cache_create(0, 0, &kc)) {
+            printf("orbm_kf_cache_create failed\n");
+            return 1;
+        }
+        g = time_us(reps, [&] {
+            orbm_search_for_triangulation_cached(ctx, kc, 1, &av, 2, &bv, F12, ex, ey, 0, 0, mg.data(), &ng);
+        });
+        c = time_us(reps / 2, [&] { nc = oc_search_for_triangulation(&av, &bv, F12, ex, ey, 0, 0, mc.data()); });
+        row("tri_nodes_cached", "SearchForTriangulation over ~90 common BoW nodes, both keyframes in the device cache", g,
+            c, ng == nc && mg == mc, ng);
+        g = time_us(reps, [&] { orbm_search_by_bow_kf_f_cached(ctx, kc, 1, &a.v, &b.v, 0.7f, 1, fg.data(), &ng); });
+        c = time_us(reps / 2, [&] { nc = oc_search_by_bow_kf_f(&a.v, &b.v, 0.7f, 1, fc.data()); });
+        row("bow_kf_f_cached", "SearchByBoW(KF, F), ~90 nodes, the keyframe in the device cache", g, c,
+            ng == nc && fg == fc, ng);
+        g = time_us(reps, [&] { orbm_search_by_bow_kf_kf_cached(ctx, kc, 1, &a.v, 2, &b.v, 0.75f, 1, mg.data(), &ng); });
+        c = time_us(reps / 2, [&] { nc = oc_search_by_bow_kf_kf(&a.v, &b.v, 0.75f, 1, mc.data()); });
+        row("bow_kf_kf_cached", "SearchByBoW(KF, KF), ~90 nodes, both keyframes in the device cache", g, c,
+            ng == nc && mg == mc, ng);
+        orbm_kf_cache_destroy(kc);
     }
     orbm_destroy(ctx);
     oc_destroy(oc);

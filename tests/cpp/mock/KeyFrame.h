@@ -15,6 +15,7 @@ typedef std::map<unsigned int, double> BowVector;
 namespace ORB_SLAM2 {
 class KeyFrame {
 public:
+    long unsigned int mnId = 0;
     int N = 0;
     float fx = 0, fy = 0, cx = 0, cy = 0;
     float mnMinX = 0, mnMaxX = 0, mnMinY = 0, mnMaxY = 0;

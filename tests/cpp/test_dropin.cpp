@@ -17,6 +17,7 @@
 #include "ORBmatcher.h"
 #include "orb_oracle.h"
 #include "orbslam_amd.h"
+#include "orbamd_status.h"
 #include "ORBVocabulary_amd.h"
 
 using namespace ORB_SLAM2;
@@ -81,6 +82,7 @@ static void check_extract(ORBextractor& ext, oc_extractor* orc, const uint8_t* i
  * FeatureVector and MapPoint pattern */
 static void make_kf(KeyFrame& kf, const std::vector<cv::KeyPoint>& kps, const cv::Mat& desc, ORBextractor& ext,
                     int nodes, uint32_t seed, std::vector<MapPoint>& pool, float mp_frac, float stereo_frac) {
+    kf.mnId = 1000 + seed;
     kf.N = (int)kps.size();
     kf.mvKeys = kps;
     kf.mvKeysUn = kps;
@@ -146,6 +148,7 @@ struct FuseWorld {
 static void build_fuse_world(FuseWorld& w, const std::vector<cv::KeyPoint>& kps, const cv::Mat& desc,
                              ORBextractor& ext, int W, int H, uint32_t seed) {
     KeyFrame& kf = w.kf;
+    kf.mnId = seed;  // the drop-ins' keyframe-cache key mixes the address with mnId
     uint32_t s = seed;
     auto urand = [&](float a, float b) { return a + (b - a) * (float)(lcg(s) % 100000) / 100000.f; };
     kf.N = (int)kps.size(); kf.mvKeys = kps; kf.mvKeysUn = kps; kf.mDescriptors = desc;
@@ -931,6 +934,18 @@ int main() {
         th.emplace_back(kf);
         for (std::thread& t : th) t.join();
         CHECK(bad == 0 && calls == 5 * iters, "concurrent drop-ins: %d of %d calls differ", (int)bad, (int)calls);
+        // with the keyframe cache on (the default), the three matcher threads shared kf1's (and kf2's)
+        // device-resident entries: every call after the first of each kind was a hit
+        if (ORB_SLAM2::amd::KeyFrameCache()) {
+            int entries = 0;
+            size_t bytes = 0;
+            long long hits = 0, misses = 0;
+            orbm_kf_cache_stats(ORB_SLAM2::amd::KeyFrameCache(), &entries, &bytes, &hits, &misses);
+            printf("keyframe cache: %d entries, %zu bytes, %lld hits, %lld misses\n", entries, bytes, hits, misses);
+            CHECK(entries >= 2 && hits >= 3 * iters - 3, "keyframe cache not shared: %lld hits", hits);
+        } else {
+            printf("keyframe cache off (ORBAMD_KF_CACHE_MB=0)\n");
+        }
     }
     test_fuse(K[2], D[2], ext, W, H);
     test_init_sim3(K[0], D[0], K[1], D[1], ext, W, H);

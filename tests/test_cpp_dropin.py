@@ -19,9 +19,15 @@ def test_dropin_builds():
 
 
 @pytest.mark.gpu
-def test_dropin_bit_exact_on_gpu():
+@pytest.mark.parametrize("kf_cache_mb", [None, "0"])
+def test_dropin_bit_exact_on_gpu(kf_cache_mb):
+    """with the device keyframe cache (the default; test_dropin checks the matcher threads shared it) and
+    without it (ORBAMD_KF_CACHE_MB=0: every call uploads its keyframes)"""
     _build()
     env = dict(os.environ)
+    env.pop("ORBAMD_KF_CACHE_MB", None)
+    if kf_cache_mb is not None:
+        env["ORBAMD_KF_CACHE_MB"] = kf_cache_mb
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout[-4000:], r.stderr[-2000:])
     assert r.returncode == 0 and "ALL PASS" in r.stdout

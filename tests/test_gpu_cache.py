@@ -1,0 +1,143 @@
+"""GPU: the device-resident keyframe cache (orbm_kf_cache, include/orbslam_amd.h "Keyframe cache").
+
+The *_cached matchers read a keyframe's descriptors / mvKeysUn / mvuRight / FeatureVector (and, for Fuse,
+its feature grid) from HBM instead of uploading them per call. They must equal the oracle exactly, on
+repeated calls (hits), when the per-call MapPoint flags change between calls (the cache never holds
+them), when a key is reused for a different keyframe (stale entry replaced), under eviction, and with
+several threads sharing one cache (LocalMapping, LoopClosing and Tracking do, LocalMapping.cc:207-268)."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_py
+import orbamd
+import proj_scenes as ps
+from orbamd.matcher import KeyFrameView
+
+pytestmark = pytest.mark.gpu
+
+
+def _kfs(agent=2, t=6, seed=5):
+    rng = np.random.default_rng(seed)
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    tabs = orc.tables()
+    out = []
+    for img in orbamd.synth_frames(agent, t, 3, 640, 480):
+        k, d = orc(img)
+        # like a vocabulary, similar descriptors share a node: node = 100 + the top 4 bits of byte 0
+        fv = {}
+        for i in range(len(k)):
+            fv.setdefault(100 + int(d[i, 0] >> 4), []).append(i)
+        ur = np.where(rng.random(len(k)) < 0.3, k["x"] - rng.random(len(k)) * 30, -1).astype(np.float32)
+        out.append(dict(k=k, d=d, fv=fv, ur=ur))
+    return out, tabs, rng
+
+
+def _view(kf, tabs, rng, mp_frac=0.3, stereo=True):
+    n = len(kf["k"])
+    return KeyFrameView(kf["k"], kf["d"], tabs["scale"], tabs["sigma2"], feat_vec=kf["fv"],
+                        uright=kf["ur"] if stereo else None, has_mp=rng.random(n) < mp_frac,
+                        mp_bad=rng.random(n) < 0.05)
+
+
+def test_cached_triangulation_and_bow_equal_oracle():
+    kfs, tabs, rng = _kfs()
+    F12, ex, ey = orbamd.device.default_geometry()
+    cache = orbamd.KeyFrameCache()
+    m = orbamd.ORBmatcher(0.75, True)
+    found = [0, 0]
+    for it in range(4):  # the same keyframes again and again, with new MapPoint flags every call
+        v1, v2 = _view(kfs[0], tabs, rng), _view(kfs[1], tabs, rng)
+        for only_stereo in (False, True):
+            ng, mg = m.SearchForTriangulationCached(cache, 101, v1, 202, v2, F12, ex, ey, only_stereo)
+            no, mo = oracle_py.search_for_triangulation(v1, v2, F12, ex, ey, only_stereo, True)
+            assert ng == no
+            np.testing.assert_array_equal(mg, mo)
+            found[0] += no
+        ng, mg = m.SearchByBoWCached(cache, 101, v1, v2, other_is_keyframe=True, key2=202)
+        no, mo = oracle_py.search_by_bow(v1, v2, 0.75, True, other_is_keyframe=True)
+        assert ng == no
+        np.testing.assert_array_equal(mg, mo)
+        found[1] += no
+        f = _view(kfs[2], tabs, rng, mp_frac=0.0, stereo=False)  # a Frame: not cached
+        ng, mg = m.SearchByBoWCached(cache, 101, v1, f)
+        no, mo = oracle_py.search_by_bow(v1, f, 0.75, True)
+        assert ng == no
+        np.testing.assert_array_equal(mg, mo)
+    assert min(found) > 0, found
+    st = cache.stats()
+    assert st["misses"] == 2 and st["hits"] >= 4 * 4 - 2 and st["entries"] == 2
+    # key 202 reused for a different keyframe (another N): the stale entry is replaced
+    v3 = _view(kfs[2], tabs, rng)
+    ng, mg = m.SearchForTriangulationCached(cache, 101, v1, 202, v3, F12, ex, ey)
+    no, mo = oracle_py.search_for_triangulation(v1, v3, F12, ex, ey, False, True)
+    assert ng == no
+    np.testing.assert_array_equal(mg, mo)
+    assert cache.stats()["misses"] == 3
+    cache.erase(202)
+    assert cache.stats()["entries"] == 1
+    m.close()
+    cache.close()
+
+
+def test_cached_eviction_and_threads():
+    """a 1-byte capacity evicts on every upload (each call still uses its own entries, held by reference);
+    four threads with their own matcher contexts share one cache"""
+    kfs, tabs, rng = _kfs(agent=3, t=2, seed=9)
+    F12, ex, ey = orbamd.device.default_geometry()
+    views = [_view(kf, tabs, rng) for kf in kfs]
+    ref = {}
+    for a in range(3):
+        for b in range(3):
+            if a != b:
+                ref[(a, b)] = oracle_py.search_for_triangulation(views[a], views[b], F12, ex, ey, False, False)
+    tiny = orbamd.KeyFrameCache(capacity_bytes=1)
+    m = orbamd.ORBmatcher(0.6, False)
+    for (a, b), (no, mo) in ref.items():
+        ng, mg = m.SearchForTriangulationCached(tiny, a, views[a], b, views[b], F12, ex, ey)
+        assert ng == no
+        np.testing.assert_array_equal(mg, mo)
+    assert tiny.stats()["entries"] == 1
+    m.close()
+    tiny.close()
+    shared = orbamd.KeyFrameCache()
+    errors = []
+
+    def worker(tid):
+        mt = orbamd.ORBmatcher(0.6, False)
+        try:
+            for it in range(12):
+                a, b = list(ref)[(tid + it) % len(ref)]
+                ng, mg = mt.SearchForTriangulationCached(shared, a, views[a], b, views[b], F12, ex, ey)
+                no, mo = ref[(a, b)]
+                if ng != no or not np.array_equal(mg, mo):
+                    errors.append((tid, it, a, b))
+        finally:
+            mt.close()
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+    assert shared.stats()["entries"] == 3
+    shared.close()
+
+
+@pytest.mark.parametrize("seed,stereo,th", [(3, True, 3.0), (4, False, 3.0)])
+def test_cached_fuse_equals_oracle(seed, stereo, th):
+    """Fuse with the keyframe and its feature grid cached (k_grid runs once, at the first call)"""
+    F, Tcw, Ow, mps, inv = ps.fuse_scene(seed, stereo)
+    cache = orbamd.KeyFrameCache()
+    m = orbamd.ORBmatcher(0.6, True)
+    no, bo = oracle_py.fuse(F, Tcw, Ow, mps, th, inv)
+    for _ in range(3):
+        ng, bg = m.FuseCached(cache, 77, F, Tcw, Ow, mps, th, inv)
+        assert ng == no and no > mps.n // 4
+        np.testing.assert_array_equal(bg, bo)
+    st = cache.stats()
+    assert st["misses"] == 1 and st["hits"] == 2
+    m.close()
+    cache.close()

@@ -14,6 +14,20 @@ __global__ void k_write_host(int* __restrict__ out, const int* __restrict__ in, 
     for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = in[i];
 }
 
+// the completion word of a call: the kernel stores it last, with release at system scope, into fine-grained
+// pinned memory, and the host polls it instead of hipStreamSynchronize
+__global__ void k_signal(int* __restrict__ done, int v) {
+    if (threadIdx.x == 0) __hip_atomic_store(done, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void k_read_host_signal(int* __restrict__ out, const int* __restrict__ in, int n, int* __restrict__ done,
+                                   int v) {
+    int s = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += in[i];
+    out[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 #define CK(x)                                                   \
     do {                                                        \
         hipError_t e = (x);                                     \
@@ -23,7 +37,9 @@ __global__ void k_write_host(int* __restrict__ out, const int* __restrict__ in, 
         }                                                       \
     } while (0)
 
-int main() {
+int main(int argc, char** argv) {
+    // argv[1] == "spin": the runtime spins in hipStreamSynchronize instead of yielding / blocking
+    if (argc > 1 && !strcmp(argv[1], "spin")) CK(hipSetDeviceFlags(hipDeviceScheduleSpin));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     const size_t in_b = 100 << 10, out_b = 4 << 10;
@@ -32,19 +48,33 @@ int main() {
     CK(hipMalloc((void**)&dp, in_b + out_b));
     memset(hp, 0, in_b + out_b);
     const int iters = 2000;
-    auto run = [&](const char* name, auto&& body) -> int {
+    int* done;
+    CK(hipHostMalloc((void**)&done, 64, hipHostMallocCoherent));
+    *done = 0;
+    int seq = 0;
+    const char* mode = argc > 1 ? argv[1] : "default";
+    // sync = false: the body waits for its own completion word
+    auto run_w = [&](const char* name, bool sync, auto&& body) -> int {
         for (int i = 0; i < 200; i++) {
             if (body()) return 1;
-            if (hipStreamSynchronize(st) != hipSuccess) return 1;
+            if (sync && hipStreamSynchronize(st) != hipSuccess) return 1;
         }
         auto t0 = std::chrono::steady_clock::now();
         for (int i = 0; i < iters; i++) {
             if (body()) return 1;
-            if (hipStreamSynchronize(st) != hipSuccess) return 1;
+            if (sync && hipStreamSynchronize(st) != hipSuccess) return 1;
         }
         const double us =
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
-        printf("{\"case\": \"%s\", \"us_per_call\": %.2f}\n", name, us);
+        printf("{\"case\": \"%s\", \"sched\": \"%s\", \"us_per_call\": %.2f}\n", name, mode, us);
+        return 0;
+    };
+    auto run = [&](const char* name, auto&& body) -> int { return run_w(name, true, body); };
+    auto wait_done = [&](int v) -> int {
+        for (long spins = 0; __atomic_load_n((volatile int*)done, __ATOMIC_ACQUIRE) != v; spins++)
+            if ((spins & 4095) == 4095 && hipStreamQuery(st) == hipSuccess &&
+                __atomic_load_n((volatile int*)done, __ATOMIC_ACQUIRE) != v)
+                return 1;  // the stream drained without the word: a failed launch
         return 0;
     };
     int* di = (int*)dp;
@@ -85,6 +115,30 @@ int main() {
         hipLaunchKernelGGL(k_write_host, dim3(1), dim3(256), 0, st, (int*)(hp + in_b), (const int*)hp, (int)(out_b / 4));
         return (int)hipGetLastError();
     });
+    rc |= run_w("1_kernel_poll_word", false, [&] {
+        hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, done, ++seq);
+        if (hipGetLastError()) return 1;
+        return wait_done(seq);
+    });
+    rc |= run_w("h2d_4k+kernel_poll_word", false, [&] {
+        if (hipMemcpyAsync(dp, hp, 4096, hipMemcpyHostToDevice, st)) return 1;
+        hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, done, ++seq);
+        if (hipGetLastError()) return 1;
+        return wait_done(seq);
+    });
+    rc |= run_w("kernel_reads_host_4k_poll_word", false, [&] {
+        hipLaunchKernelGGL(k_read_host_signal, dim3(1), dim3(256), 0, st, di, (const int*)hp, 1024, done, ++seq);
+        if (hipGetLastError()) return 1;
+        return wait_done(seq);
+    });
+    rc |= run_w("h2d_100k+kernel_poll_word", false, [&] {
+        if (hipMemcpyAsync(dp, hp, in_b, hipMemcpyHostToDevice, st)) return 1;
+        hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, done, ++seq);
+        if (hipGetLastError()) return 1;
+        return wait_done(seq);
+    });
+    CK(hipStreamSynchronize(st));
+    (void)hipHostFree(done);
     (void)hipFree(dp);
     (void)hipHostFree(hp);
     (void)hipStreamDestroy(st);
