@@ -1119,7 +1119,8 @@ struct orbm_ctx {
         pinned = nullptr;
         pinned_dev = nullptr;
         pinned_bytes = 0;
-        if (hipHostMalloc(&pinned, need, 0) != hipSuccess) return nullptr;
+        // fine-grained: the per-call kernels' host writes are visible to the polling host at once
+        if (hipHostMalloc(&pinned, need, hipHostMallocCoherent) != hipSuccess) return nullptr;
         if (hipHostGetDevicePointer(&pinned_dev, pinned, 0) != hipSuccess) {
             (void)hipHostFree(pinned);
             pinned = nullptr;
@@ -1130,6 +1131,11 @@ struct orbm_ctx {
     }
     /* device address of byte `off` of the pinned buffer (kernels write results there directly) */
     int32_t* pinned_on_device(size_t off) const { return (int32_t*)((uint8_t*)pinned_dev + off); }
+    uint32_t seq = 0;  // call sequence number of k_bow_small's done words (never 0)
+    uint32_t next_seq() {
+        seq = seq >= kSmallSeqMask ? 1u : seq + 1u;
+        return seq;
+    }
     /* the per-call state words (match_kernels.hip call_tail): ints 16..47 of the zeroed err buffer */
     int32_t* call_state() { return err.as<int32_t>() + 16; }
 };
@@ -1142,24 +1148,51 @@ namespace {
  * (tools/latency_floor.hip, profiles/r03_latency_floor.jsonl). The launch needs no further wait: the
  * next call's copies and launches are ordered behind it on the stream. A stream that drains without
  * the word, or an error, is ORBX_EDEVICE. ORBX_SYNC_WAIT=1 synchronises the stream instead (A/B). */
-int wait_call(hipStream_t st, const int32_t* word) {
+template <class Ready>
+int wait_until(hipStream_t st, Ready ready) {
     static const bool sync_wait = [] {
         const char* e = getenv("ORBX_SYNC_WAIT");
         return e && atoi(e) != 0;
     }();
     if (!sync_wait) {
         for (unsigned spins = 1; spins < (1u << 22); spins++) {
-            if (__atomic_load_n(word, __ATOMIC_ACQUIRE) >= 0) return 0;
+            if (ready()) return 0;
             if ((spins & 1023) == 0) {
                 const hipError_t e = hipStreamQuery(st);
                 if (e == hipErrorNotReady) continue;
                 if (e != hipSuccess) return ORBX_EDEVICE;
-                break;  // drained: the word is visible now if the kernel wrote it
+                break;  // drained: the words are visible now if the kernel wrote them
             }
         }
     }
     HIPR(hipStreamSynchronize(st));
-    return __atomic_load_n(word, __ATOMIC_ACQUIRE) >= 0 ? 0 : ORBX_EDEVICE;
+    return ready() ? 0 : ORBX_EDEVICE;
+}
+
+int wait_call(hipStream_t st, const int32_t* word) {
+    return wait_until(st, [word] { return __atomic_load_n(word, __ATOMIC_ACQUIRE) >= 0; });
+}
+
+/* ComputeThreeMaxima (ORBmatcher.cc:1601-1642) of a 30-bin rotation histogram, for the host-side tail of
+ * k_bow_small (the same comparisons as match_kernels.hip three_maxima) */
+void three_maxima_host(const int* hist, int keep[3]) {
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < 30; i++) {
+        const int s = hist[i];
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s; ind3 = i;
+        }
+    }
+    const float tenth = 0.1f * (float)max1;
+    if ((float)max2 < tenth) ind2 = ind3 = -1;
+    else if ((float)max3 < tenth) ind3 = -1;
+    keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
 }
 
 void make_geom(MatchGeom& g, const float F12[9], float ex, float ey, int nlevels, const float* scale,
@@ -1216,6 +1249,7 @@ struct KfEntry {
     int n = 0, nfeat = 0, n_nodes = 0;
     bool has_ur = false, has_grid = false;
     size_t o_desc = 0, o_x = 0, o_y = 0, o_ang = 0, o_oct = 0, o_ur = 0, o_feat = 0, o_gs = 0, o_gi = 0;
+    size_t o_dnode = 0, o_rnode = 0;  // descriptors / NodeRecs in FeatureVector order (k_bow_small, k_tri_small)
     float min_x = 0, min_y = 0, gw_inv = 0, gh_inv = 0;  // grid bounds / scale the grid was built with
     const uint8_t* at(size_t o) const { return buf.as<uint8_t>() + o; }
 };
@@ -1356,6 +1390,224 @@ void orbm_epipole(const float R2w[9], const float t2w[3], const float Cw[3], flo
 
 }  // extern "C"
 
+static int node_feats(const orbm_kf_view* v) { return v->n_nodes ? v->node_off[v->n_nodes] : 0; }
+
+/* ---- small per-call matchers (k_bow_small / k_tri_small): common nodes and per-call MapPoint bits in the
+ * kernel arguments, node-ordered keyframe data from the keyframe cache or read by the kernel straight from
+ * the pinned staging (zero copy: each element is read once, by one lane, so no H2D copy and no copy kernel
+ * precede the launch; ORBX_SMALL_H2D=1 uploads it first instead, A/B), accepts + per-task done words written
+ * to host memory, the rotation histogram on the host ---- */
+struct SmallSide {
+    const uint4* d = nullptr;
+    const NodeRec* r = nullptr;  // k_tri_small
+    const float* a = nullptr;    // k_bow_small: angles, a[p * a_stride]
+    int a_stride = 1;
+    const int32_t* f = nullptr;
+};
+
+/* carve + stage one side in node order (an uncached view), or take the cached entry's arrays */
+struct SmallPlan {
+    size_t od = 0, orec = 0, of = 0;
+    int nf = 0;
+    bool cached = false, bow = false;
+};
+/* bow: an uncached side stages its angles only (4 bytes a position instead of a NodeRec: the kernel reads
+ * them across PCIe) */
+static void small_plan(Carve& cv, const orbm_kf_view* v, const KfEntry* ce, SmallPlan& p, bool bow) {
+    p.nf = node_feats(v);
+    p.cached = ce != nullptr;
+    p.bow = bow;
+    if (ce) return;
+    const size_t n = (size_t)std::max(p.nf, 1);
+    p.od = cv.take(32 * n);
+    p.orec = cv.take((bow ? 4 : sizeof(NodeRec)) * n);
+    p.of = cv.take(4 * n);
+}
+static NodeRec node_rec(const float* x, const float* y, const float* ang, const int32_t* oct, const float* ur, int f) {
+    NodeRec r;
+    r.x = x ? x[f] : 0.f;
+    r.y = y ? y[f] : 0.f;
+    r.oct = (oct ? oct[f] : 0) | (ur && ur[f] >= 0.f ? 0x100 : 0);
+    r.angle = ang ? ang[f] : 0.f;
+    return r;
+}
+static SmallSide small_stage(const orbm_kf_view* v, const KfEntry* ce, const SmallPlan& p, uint8_t* hp,
+                             uint8_t* dbase) {
+    SmallSide s;
+    if (ce) {
+        s.d = (const uint4*)ce->at(ce->o_dnode);
+        s.r = (const NodeRec*)ce->at(ce->o_rnode);
+        s.a = &s.r->angle;
+        s.a_stride = sizeof(NodeRec) / sizeof(float);
+        s.f = (const int32_t*)ce->at(ce->o_feat);
+        return s;
+    }
+    NodeRec* rec = (NodeRec*)(hp + p.orec);
+    float* ang = (float*)(hp + p.orec);
+    for (int q = 0; q < p.nf; q++) {
+        const int f = v->node_feat[q];
+        memcpy(hp + p.od + 32 * (size_t)q, v->desc + 32 * (size_t)f, 32);
+        if (p.bow) ang[q] = v->angle ? v->angle[f] : 0.f;
+        else rec[q] = node_rec(v->x, v->y, v->angle, v->octave, v->uright, f);
+    }
+    if (p.nf) memcpy(hp + p.of, v->node_feat, 4 * (size_t)p.nf);
+    s.d = (const uint4*)(dbase + p.od);
+    s.r = (const NodeRec*)(dbase + p.orec);
+    s.a = (const float*)(dbase + p.orec);
+    s.f = (const int32_t*)(dbase + p.of);
+    return s;
+}
+static bool small_h2d() {
+    static const bool h2d = [] {
+        const char* e = getenv("ORBX_SMALL_H2D");
+        return e && atoi(e) != 0;
+    }();
+    return h2d;
+}
+/* per node position: bit set when pred(feature index) */
+template <class Pred>
+static void small_bits(const orbm_kf_view* v, uint32_t* bits, Pred pred) {
+    const int nf = node_feats(v);
+    for (int q = 0; q < nf; q++)
+        if (pred(v->node_feat[q])) bits[q >> 5] |= 1u << (q & 31);
+}
+
+/* wait for every task's done word of this call, then the rotation histogram + ComputeThreeMaxima over the
+ * accepts (ORBmatcher.cc:236-285 / 784-819) and the caller's output (out[x] = partner, -1 elsewhere) */
+static int small_finish(orbm_ctx* ctx, const uint8_t* hp, size_t o_out, size_t o_done, const SmallTask* tasks, int nt,
+                        uint32_t seq, int check_ori, int32_t* out, int nout, int* nmatches) {
+    const unsigned long long* done = (const unsigned long long*)(hp + o_done);
+    const unsigned long long* acc = (const unsigned long long*)(hp + o_out);
+    // polled in task order: a done word, then its accepts, each final once it carries this call's seq (the
+    // kernel's stores are unordered: no fence)
+    int next = 0, k = 0;
+    if (const int rc = wait_until(ctx->stream, [&] {
+            for (; next < nt; next++, k = 0) {
+                const unsigned long long d = __atomic_load_n(done + next, __ATOMIC_ACQUIRE);
+                if ((uint32_t)d != seq) return false;
+                for (const int na = (int)(d >> 32); k < na; k++)
+                    if ((uint32_t)(__atomic_load_n(acc + tasks[next].q_begin + k, __ATOMIC_ACQUIRE) >> 37) != seq)
+                        return false;
+            }
+            return true;
+        }))
+        return rc;
+    int hist[30] = {0}, keep[3] = {-2, -2, -2};
+    if (check_ori) {
+        for (int i = 0; i < nt; i++) {
+            const int na = (int)(done[i] >> 32);
+            for (int j = 0; j < na; j++) hist[(acc[tasks[i].q_begin + j] >> 32) & 31]++;
+        }
+        three_maxima_host(hist, keep);
+    }
+    std::fill(out, out + nout, -1);
+    int cnt = 0;
+    for (int i = 0; i < nt; i++) {
+        const int na = (int)(done[i] >> 32);
+        for (int j = 0; j < na; j++) {
+            const unsigned long long e = acc[tasks[i].q_begin + j];
+            const int bin = (int)((e >> 32) & 31);
+            if (check_ori && bin != keep[0] && bin != keep[1] && bin != keep[2]) continue;
+            out[e & 0xFFFF] = (int32_t)((e >> 16) & 0xFFFF);
+            cnt++;
+        }
+    }
+    if (nmatches) *nmatches = cnt;
+    return 0;
+}
+
+/* SearchByBoW through k_bow_small (every common node <= 64 candidates, <= kSmallTasks common nodes, <= 2048
+ * FeatureVector entries a side) */
+static int bow_small(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view* vc, const std::vector<NodeTask>& tasks,
+                     float nnratio, int check_ori, int mode, int32_t* out, int nout, int* nmatches,
+                     const KfEntry* cq, const KfEntry* cc) {
+    const int nt = (int)tasks.size();
+    Carve cv;
+    SmallPlan pq, pc;
+    small_plan(cv, vq, cq, pq, true);
+    small_plan(cv, vc, cc, pc, true);
+    const size_t in_bytes = small_h2d() ? cv.off : 0;
+    const size_t o_out = cv.take(8 * (size_t)std::max(pq.nf, 1));
+    const size_t o_done = cv.take(8 * (size_t)nt);
+    if (in_bytes && ctx->scratch.ensure(in_bytes)) return ORBX_EDEVICE;
+    uint8_t* hp = ctx->ensure_pinned(cv.off);
+    if (!hp) return ORBX_EDEVICE;
+    uint8_t* dbase = in_bytes ? ctx->scratch.as<uint8_t>() : (uint8_t*)ctx->pinned_on_device(0);
+    BowSmall a;
+    memset(&a, 0, sizeof(a));
+    const SmallSide sq = small_stage(vq, cq, pq, hp, dbase), sc = small_stage(vc, cc, pc, hp, dbase);
+    a.qd = sq.d; a.qa = sq.a; a.qa_stride = sq.a_stride; a.qf = sq.f;
+    a.cd = sc.d; a.ca = sc.a; a.ca_stride = sc.a_stride; a.cf = sc.f;
+    auto good = [](const orbm_kf_view* v) {  // a good MapPoint: one, and not bad
+        return [v](int f) { return v->has_mp && v->has_mp[f] && !(v->mp_bad && v->mp_bad[f]); };
+    };
+    small_bits(vq, a.qgood, good(vq));
+    if (mode == 1) small_bits(vc, a.cgood, good(vc));
+    for (int i = 0; i < nt; i++)
+        a.tasks[i] = SmallTask{(uint16_t)tasks[i].q_begin, (uint16_t)tasks[i].q_end, (uint16_t)tasks[i].c_begin,
+                               (uint16_t)tasks[i].c_end};
+    a.out = (unsigned long long*)ctx->pinned_on_device(o_out);
+    a.done = (unsigned long long*)ctx->pinned_on_device(o_done);
+    a.seq = (int)ctx->next_seq();
+    a.ntasks = nt;
+    a.mode = mode;
+    a.check_ori = check_ori ? 1 : 0;
+    a.nnratio = nnratio;
+    if (in_bytes) HIPR(hipMemcpyAsync(dbase, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIPR(launch_bow_small(a, ctx->stream));
+    return small_finish(ctx, hp, o_out, o_done, a.tasks, nt, (uint32_t)a.seq, check_ori, out, nout, nmatches);
+}
+
+/* SearchForTriangulation over common nodes through k_tri_small (<= kSmallTasks 64-query chunks, every common
+ * node <= 256 candidates, <= 2048 FeatureVector entries a side) */
+static int tri_small(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2, const std::vector<NodeTask>& tasks,
+                     const float F12[9], float ex, float ey, int only_stereo, int check_ori, int32_t* match12,
+                     int* nmatches, const KfEntry* c1, const KfEntry* c2) {
+    const int nt = (int)tasks.size();
+    Carve cv;
+    SmallPlan p1, p2;
+    small_plan(cv, kf1, c1, p1, false);
+    small_plan(cv, kf2, c2, p2, false);
+    const size_t in_bytes = small_h2d() ? cv.off : 0;
+    const size_t o_out = cv.take(8 * (size_t)std::max(p1.nf, 1));
+    const size_t o_done = cv.take(8 * (size_t)nt);
+    if (in_bytes && ctx->scratch.ensure(in_bytes)) return ORBX_EDEVICE;
+    uint8_t* hp = ctx->ensure_pinned(cv.off);
+    if (!hp) return ORBX_EDEVICE;
+    uint8_t* dbase = in_bytes ? ctx->scratch.as<uint8_t>() : (uint8_t*)ctx->pinned_on_device(0);
+    TriSmall a;
+    memset(&a, 0, sizeof(a));
+    const SmallSide s1 = small_stage(kf1, c1, p1, hp, dbase), s2 = small_stage(kf2, c2, p2, hp, dbase);
+    a.qd = s1.d; a.qr = s1.r; a.qf = s1.f;
+    a.cd = s2.d; a.cr = s2.r; a.cf = s2.f;
+    auto has_mp = [](const orbm_kf_view* v) { return [v](int f) { return v->has_mp && v->has_mp[f] != 0; }; };
+    small_bits(kf1, a.qmp, has_mp(kf1));
+    small_bits(kf2, a.cmp, has_mp(kf2));
+    for (int i = 0; i < nt; i++)
+        a.tasks[i] = SmallTask{(uint16_t)tasks[i].q_begin, (uint16_t)tasks[i].q_end, (uint16_t)tasks[i].c_begin,
+                               (uint16_t)tasks[i].c_end};
+    a.out = (unsigned long long*)ctx->pinned_on_device(o_out);
+    a.done = (unsigned long long*)ctx->pinned_on_device(o_done);
+    a.seq = (int)ctx->next_seq();
+    a.ntasks = nt;
+    a.check_ori = check_ori ? 1 : 0;
+    a.only_stereo = only_stereo ? 1 : 0;
+    a.q_ur = kf1->uright != nullptr;
+    a.c_ur = kf2->uright != nullptr;
+    make_geom(a.g, F12, ex, ey, kf2->nlevels, kf2->scale_factors, kf2->level_sigma2);
+    if (in_bytes) HIPR(hipMemcpyAsync(dbase, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIPR(launch_tri_small(a, ctx->stream));
+    return small_finish(ctx, hp, o_out, o_done, a.tasks, nt, (uint32_t)a.seq, check_ori, match12, kf1->n, nmatches);
+}
+
+static bool small_off() {
+    static const bool off = [] {
+        const char* e = getenv("ORBX_SMALL");
+        return e && atoi(e) == 0;
+    }();
+    return off;
+}
+
 /* c1 / c2: the keyframes' cached device arrays (orbm_kf_cache), or nullptr to upload them with the call */
 static int tri_common(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2, const float F12[9], float ex,
                       float ey, int only_stereo, int check_ori, int32_t* match12, int* nmatches,
@@ -1375,6 +1627,11 @@ static int tri_common(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view
         if (nmatches) *nmatches = 0;
         return 0;
     }
+    int max_nc = 0;
+    for (const NodeTask& t : tasks) max_nc = std::max(max_nc, t.c_end - t.c_begin);
+    if (!small_off() && max_nc <= 256 && tasks.size() <= (size_t)kSmallTasks && kf1->n <= 65535 && kf2->n <= 65535 &&
+        node_feats(kf1) <= 32 * kSmallBitWords && node_feats(kf2) <= 32 * kSmallBitWords)
+        return tri_small(ctx, kf1, kf2, tasks, F12, ex, ey, only_stereo, check_ori, match12, nmatches, c1, c2);
     // one H2D copy (views, tasks), one launch whose last workgroup writes the (rotation-filtered)
     // matches into pinned host memory pre-filled with -1, one synchronize
     Carve cv;
@@ -1435,6 +1692,9 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
         if (nmatches) *nmatches = 0;
         return 0;
     }
+    if (!small_off() && max_nc <= 64 && vq->n <= 65535 && vc->n <= 65535 && tasks.size() <= (size_t)kSmallTasks && node_feats(vq) <= 32 * kSmallBitWords &&
+        node_feats(vc) <= 32 * kSmallBitWords)
+        return bow_small(ctx, vq, vc, tasks, nnratio, check_ori, mode, out, nout, nmatches, cq, cc);
     // one H2D copy, one launch (greedy per node; the last workgroup's rotation filter writes the
     // matches into pinned host memory pre-filled with -1), one synchronize
     Carve cv;
@@ -2615,6 +2875,10 @@ std::shared_ptr<KfEntry> cache_get(orbm_kf_cache* c, int kind, uint64_t key, con
     e->o_oct = cv.take(4 * N);
     e->o_ur = cv.take(has_ur ? 4 * N : 0);
     e->o_feat = cv.take(4 * (size_t)std::max(nfeat, 1));
+    if (kind == 0) {
+        e->o_dnode = cv.take(32 * (size_t)std::max(nfeat, 1));
+        e->o_rnode = cv.take(sizeof(NodeRec) * (size_t)std::max(nfeat, 1));
+    }
     size_t o_call = 0;
     if (kind == 1) {
         e->has_grid = true;
@@ -2643,6 +2907,13 @@ std::shared_ptr<KfEntry> cache_get(orbm_kf_cache* c, int kind, uint64_t key, con
         if (has_ur) memcpy(h.data() + e->o_ur, ur, 4 * (size_t)n);
     }
     if (nfeat) memcpy(h.data() + e->o_feat, kv->node_feat, 4 * (size_t)nfeat);
+    if (kind == 0)
+        for (int p = 0; p < nfeat; p++) {
+            const int f = kv->node_feat[p];
+            memcpy(h.data() + e->o_dnode + 32 * (size_t)p, desc + 32 * (size_t)f, 32);
+            const NodeRec r = node_rec(x, y, ang, oct, has_ur ? ur : nullptr, f);
+            memcpy(h.data() + e->o_rnode + sizeof(NodeRec) * (size_t)p, &r, sizeof(r));
+        }
     if (kind == 1) {  // the KeyFrame's grid (AssignFeaturesToGrid), built once by k_grid
         ProjCall pc;
         memset(&pc, 0, sizeof(pc));

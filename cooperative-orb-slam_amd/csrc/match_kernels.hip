@@ -985,6 +985,164 @@ __global__ __launch_bounds__(64) void k_bow(const DevView vq, const DevView vc, 
     call_tail(tail);
 }
 
+/* one accept of a small per-call matcher: a single 64-bit store to host memory that carries the call's seq
+ * (orb_match.h small_entry), so the host can tell it has landed whatever order the stores arrive in; no
+ * fence, no L2 write-back in the kernel */
+__device__ __forceinline__ void small_emit(unsigned long long* slot, int x, int y, int bin, int seq) {
+    __hip_atomic_store(slot, small_entry(x, y, bin, (uint32_t)seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+/* Small per-call SearchByBoW (BowSmall, orb_match.h): k_bow's lane-per-candidate greedy chain for nodes of
+ * <= 64 candidates with every input in node order, no global atomics and no last-workgroup tail: a
+ * workgroup emits its node's accepts (with their rotation bin) straight to host memory, then its done word
+ * (the host waits for both). The rotation histogram over all nodes (ORBmatcher.cc:236-246, 1601-1642) is the host's (capi.cpp). */
+__global__ __launch_bounds__(64) void k_bow_small(const BowSmall a) {
+    const SmallTask t = a.tasks[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int nc = t.c_end - t.c_begin;  // <= 64 (host checked)
+    uint32_t cdw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool elig = false;
+    int idxc = -1;
+    float cang = 0.f;
+    if (lane < nc) {
+        const int p = t.c_begin + lane;
+        const uint4 x0 = a.cd[2 * p], x1 = a.cd[2 * p + 1];
+        cdw[0] = x0.x; cdw[1] = x0.y; cdw[2] = x0.z; cdw[3] = x0.w; cdw[4] = x1.x; cdw[5] = x1.y; cdw[6] = x1.z; cdw[7] = x1.w;
+        idxc = a.cf[p];
+        cang = a.ca[p * a.ca_stride];
+        elig = a.mode == 0 || ((a.cgood[p >> 5] >> (p & 31)) & 1u);
+    }
+    int na = 0;
+    for (int qb = t.q_begin; qb < t.q_end; qb += 64) {
+        const int nq = min(64, t.q_end - qb);
+        int myq = -1;
+        float qang = 0.f;
+        uint32_t qdw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (lane < nq) {
+            const int p = qb + lane;
+            const uint4 x0 = a.qd[2 * p], x1 = a.qd[2 * p + 1];
+            qdw[0] = x0.x; qdw[1] = x0.y; qdw[2] = x0.z; qdw[3] = x0.w; qdw[4] = x1.x; qdw[5] = x1.y; qdw[6] = x1.z; qdw[7] = x1.w;
+            myq = ((a.qgood[p >> 5] >> (p & 31)) & 1u) ? a.qf[p] : -1;
+            qang = a.qa[p * a.qa_stride];
+        }
+        for (int k = 0; k < nq; k++) {
+            const int idxq = __builtin_amdgcn_readlane(myq, k);
+            if (idxq < 0) continue;  // no good MapPoint (uniform)
+            int dist = 0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) dist += __popc(cdw[u] ^ (uint32_t)__builtin_amdgcn_readlane((int)qdw[u], k));
+            const uint32_t m1 = wave_min_u32(elig ? ((uint32_t)dist << 6 | (uint32_t)lane) : 0xFFFFFFFFu);
+            if (m1 == 0xFFFFFFFFu) continue;  // no eligible candidate left
+            const int i1 = (int)(m1 & 63u), b1 = (int)(m1 >> 6);
+            const int b2 = (int)wave_min_u32((elig && lane != i1) ? (uint32_t)dist : 256u);
+            const bool ok_th = a.mode == 0 ? (b1 <= 50) : (b1 < 50);  // TH_LOW (ORBmatcher.cc:228 / :598)
+            if (ok_th && __fmul_rn(1.0f, (float)b1) < __fmul_rn(a.nnratio, (float)b2)) {
+                const int idxc_w = __builtin_amdgcn_readlane(idxc, i1);
+                int bin = 0;
+                if (a.check_ori) {  // rot = angle(KF / KF1 keypoint) - angle(F / KF2 keypoint) in both modes
+                    const float qa_k = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, qang), k));
+                    const float ca_i = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cang), i1));
+                    float rot = __fsub_rn(qa_k, ca_i);
+                    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+                    bin = (int)roundf(__fmul_rn(rot, 1.0f / 30));
+                    if (bin == 30) bin = 0;
+                }
+                if (lane == i1) elig = false;
+                if (lane == 0)
+                    small_emit(a.out + t.q_begin + na, a.mode == 0 ? idxc_w : idxq, a.mode == 0 ? idxq : idxc_w, bin,
+                               a.seq);
+                na++;
+            }
+        }
+    }
+    if (lane == 0)
+        __hip_atomic_store(a.done + blockIdx.x, (unsigned long long)(uint32_t)a.seq | (unsigned long long)na << 32,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+/* Small per-call SearchForTriangulation over common BoW nodes (TriSmall, orb_match.h): a wave per 64-query
+ * chunk of a common node, a lane per query; the node's candidates are loaded 64 at a time, one per lane, and
+ * broadcast by readlane, so every lane scans them in node order with the reference's rule (ORBmatcher.cc:
+ * 704-776: skip a MapPoint / non-stereo candidate, dist > TH_LOW or > best; epipole radius for mono pairs;
+ * CheckDistEpipolarLine; accept = new best, ties to the later). Accepts are compacted by ballot into host
+ * memory, then the chunk's done word; the rotation histogram is the host's. */
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+__global__ __launch_bounds__(64) void k_tri_small(const TriSmall a) {
+    const SmallTask t = a.tasks[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int p1 = t.q_begin + lane;
+    bool active = false, st1 = false;
+    int idx1 = -1;
+    float ea = 0.f, eb = 0.f, ec = 0.f, ang1 = 0.f;
+    uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (p1 < t.q_end) {
+        const uint4 x0 = a.qd[2 * p1], x1 = a.qd[2 * p1 + 1];
+        q[0] = x0.x; q[1] = x0.y; q[2] = x0.z; q[3] = x0.w; q[4] = x1.x; q[5] = x1.y; q[6] = x1.z; q[7] = x1.w;
+        const NodeRec r = a.qr[p1];
+        idx1 = a.qf[p1];
+        st1 = a.q_ur && (r.oct & 0x100);
+        active = !((a.qmp[p1 >> 5] >> (p1 & 31)) & 1u) && (!a.only_stereo || st1);
+        ang1 = r.angle;
+        epi_line(a.g, r.x, r.y, &ea, &eb, &ec);
+    }
+    int bestDist = 50, bestIdx2 = -1;  // TH_LOW (ORBmatcher.cc:704)
+    float bestAng = 0.f;
+    for (int cb = t.c_begin; cb < t.c_end; cb += 64) {
+        const int nt = min(64, t.c_end - cb);
+        uint32_t cdw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int coct = -1, cidx = -1;
+        float cx = 0.f, cy = 0.f, cang = 0.f;
+        if (lane < nt) {
+            const int p2 = cb + lane;
+            const uint4 x0 = a.cd[2 * p2], x1 = a.cd[2 * p2 + 1];
+            cdw[0] = x0.x; cdw[1] = x0.y; cdw[2] = x0.z; cdw[3] = x0.w; cdw[4] = x1.x; cdw[5] = x1.y; cdw[6] = x1.z; cdw[7] = x1.w;
+            const NodeRec r = a.cr[p2];
+            cidx = a.cf[p2];
+            const bool st2 = a.c_ur && (r.oct & 0x100);
+            const bool ok = !((a.cmp[p2 >> 5] >> (p2 & 31)) & 1u) && (!a.only_stereo || st2);
+            coct = ok ? ((r.oct & 0xFF) | (st2 ? 0x100 : 0)) : -1;
+            cx = r.x;
+            cy = r.y;
+            cang = r.angle;
+        }
+        for (int j = 0; j < nt; j++) {
+            const int oc = __builtin_amdgcn_readlane(coct, j);
+            if (oc < 0) continue;  // a MapPoint (or mono in stereo mode): uniform
+            int dist = 0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) dist += __popc(q[u] ^ (uint32_t)__builtin_amdgcn_readlane((int)cdw[u], j));
+            const float x2 = readlane_f(cx, j), y2 = readlane_f(cy, j), a2 = readlane_f(cang, j);
+            const int i2 = __builtin_amdgcn_readlane(cidx, j);
+            if (!active || dist > 50 || dist > bestDist) continue;
+            const int oct2 = oc & 0xFF;
+            if (!st1 && !(oc & 0x100) && near_epipole(a.g, x2, y2, oct2)) continue;  // ORBmatcher.cc:743-749
+            if (epi_ok(ea, eb, ec, x2, y2, a.g.th384[oct2])) {
+                bestDist = dist;
+                bestIdx2 = i2;
+                bestAng = a2;
+            }
+        }
+    }
+    const bool acc = active && bestIdx2 >= 0;
+    int bin = 0;
+    if (acc && a.check_ori) {  // rot = kp1.angle - kp2.angle (ORBmatcher.cc:784-792)
+        float rot = __fsub_rn(ang1, bestAng);
+        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+        bin = (int)roundf(__fmul_rn(rot, 1.0f / 30));
+        if (bin == 30) bin = 0;
+    }
+    const unsigned long long m = __ballot(acc);
+    const int rank = __popcll(m & ((1ull << lane) - 1ull));
+    if (acc) small_emit(a.out + t.q_begin + rank, idx1, bestIdx2, bin, a.seq);
+    if (lane == 0)
+        __hip_atomic_store(a.done + blockIdx.x,
+                           (unsigned long long)(uint32_t)a.seq | (unsigned long long)__popcll(m) << 32,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 /* SearchByBoW for a batch of frame pairs with the FeatureVectors of orbv_transform_batch_device on
  * the device: block (i, p) takes node i of the query frame qf[p] and, if the candidate frame cf[p]
  * has the same node (binary search), runs k_bow's node-local greedy (queries in order; best / second
@@ -1214,6 +1372,18 @@ hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* task
     else
         hipLaunchKernelGGL(k_bow<false>, dim3(ntasks), dim3(64), (size_t)max_nc, st, vq, vc, tasks, nnratio, mode,
                            tail);
+    return hipGetLastError();
+}
+
+hipError_t launch_bow_small(const BowSmall& a, hipStream_t st) {
+    if (a.ntasks <= 0 || a.ntasks > kSmallTasks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bow_small, dim3(a.ntasks), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tri_small(const TriSmall& a, hipStream_t st) {
+    if (a.ntasks <= 0 || a.ntasks > kSmallTasks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_tri_small, dim3(a.ntasks), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 

@@ -89,19 +89,32 @@ void make_view(KF& k, const float* scale, const float* sigma2, int nodes, const 
     k.v.level_sigma2 = sigma2;
 }
 
-double time_us(int reps, const std::function<void()>& f) {
+/* per-call wall time: the median over reps (robust to preemption of the host thread on a shared box), and
+ * the mean beside it */
+struct Stat {
+    double median, mean;
+};
+Stat time_us(int reps, const std::function<void()>& f) {
     for (int i = 0; i < std::max(3, reps / 20); i++) f();
-    const auto t0 = std::chrono::steady_clock::now();
-    for (int i = 0; i < reps; i++) f();
-    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / reps;
+    std::vector<double> t(reps);
+    double sum = 0;
+    for (int i = 0; i < reps; i++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        f();
+        t[i] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        sum += t[i];
+    }
+    std::nth_element(t.begin(), t.begin() + reps / 2, t.end());
+    return {t[reps / 2], sum / reps};
 }
 
 int failures = 0;
-void row(const char* name, const char* what, double gpu_us, double cpu_us, bool same, int nmatch) {
+void row(const char* name, const char* what, Stat gpu, Stat cpu, bool same, int nmatch) {
     failures += !same;
     printf("{\"row\": \"%s\", \"workload\": \"%s\", \"gpu_host_api_us_per_call\": %.1f, "
-           "\"cpu_oracle_us_per_call\": %.1f, \"cpu_threads\": 1, \"identical\": %s, \"n\": %d, \"harness\": \"C++\"}\n",
-           name, what, gpu_us, cpu_us, same ? "true" : "false", nmatch);
+           "\"cpu_oracle_us_per_call\": %.1f, \"gpu_mean_us\": %.1f, \"cpu_mean_us\": %.1f, \"stat\": \"median\", "
+           "\"cpu_threads\": 1, \"identical\": %s, \"n\": %d, \"harness\": \"C++\"}\n",
+           name, what, gpu.median, cpu.median, gpu.mean, cpu.mean, same ? "true" : "false", nmatch);
     fflush(stdout);
 }
 
@@ -125,8 +138,8 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> d(32 * (size_t)cap), e(32 * (size_t)cap);
         int n = 0, m = 0;
         bool same = true;
-        const double g = time_us(reps / 4, [&] { orbx_extract(h, img1.data(), W, H, W, kp.data(), d.data(), cap, &n); });
-        const double c = time_us(std::max(20, reps / 100),
+        const Stat g = time_us(reps / 4, [&] { orbx_extract(h, img1.data(), W, H, W, kp.data(), d.data(), cap, &n); });
+        const Stat c = time_us(std::max(20, reps / 100),
                                  [&] { oc_extract(oc, img1.data(), W, H, W, kq.data(), e.data(), cap, &m); });
         same = n == m && memcmp(kp.data(), kq.data(), sizeof(orbx_kp) * n) == 0 && memcmp(d.data(), e.data(), 32 * (size_t)n) == 0;
         row("extract", "ORBextractor::operator(), one 640x480 frame, 1000 features", g, c, same, n);
@@ -162,8 +175,8 @@ int main(int argc, char** argv) {
         int ng = 0, nc = 0;
         orbm_kf_view av = a.v, bv = b.v;
         av.has_mp = bv.has_mp = nullptr;  // triangulation: new points only where no MapPoint (none here)
-        double g = time_us(reps, [&] { orbm_search_for_triangulation(ctx, &av, &bv, F12, ex, ey, 0, 0, mg.data(), &ng); });
-        double c = time_us(std::max(20, reps / (variant == 0 ? 50 : 2)),
+        Stat g = time_us(reps, [&] { orbm_search_for_triangulation(ctx, &av, &bv, F12, ex, ey, 0, 0, mg.data(), &ng); });
+        Stat c = time_us(std::max(20, reps / (variant == 0 ? 50 : 2)),
                            [&] { nc = oc_search_for_triangulation(&av, &bv, F12, ex, ey, 0, 0, mc.data()); });
         row(variant == 0 ? "tri_bf" : "tri_nodes",
             variant == 0 ? "SearchForTriangulation, one node (BF), 640x480, ~1000 features"

@@ -51,12 +51,14 @@ def test_triangulation_bf(check_ori, W, H, nf):
     np.testing.assert_array_equal(mg, mo)
 
 
-def test_triangulation_nodes_mappoints_stereo():
-    rng = np.random.default_rng(3)
+@pytest.mark.parametrize("nodes,stereo2", [(40, True), (8, True), (40, False), (3, True)])
+def test_triangulation_nodes_mappoints_stereo(nodes, stereo2):
+    """40 nodes (~25-50 candidates: the small-call kernel, one candidate chunk), 8 (~125: two chunks), 3 (~330:
+    over the small path's 256-candidate bound, the staged kernel); stereo2 = False: KF2 is monocular"""
+    rng = np.random.default_rng(3 + nodes)
     (k1, d1), (k2, d2) = _frames_kf(1, 4)[0]
     tabs = _frames_kf(1, 4, 1)[1]
     F12, ex, ey = orbamd.device.default_geometry()
-    nodes = 40
     ids = np.sort(rng.choice(5000, nodes, replace=False))
     fv1 = {int(i): [] for i in ids}
     fv2 = {int(i): [] for i in ids[::2]} | {int(i) + 5000: [] for i in ids[1::2]}  # partial overlap
@@ -70,7 +72,7 @@ def test_triangulation_nodes_mappoints_stereo():
     mp1 = rng.random(len(k1)) < 0.2
     mp2 = rng.random(len(k2)) < 0.2
     v1 = _view(k1, d1, tabs, feat_vec=fv1, uright=ur1, has_mp=mp1)
-    v2 = _view(k2, d2, tabs, feat_vec=fv2, uright=ur2, has_mp=mp2)
+    v2 = _view(k2, d2, tabs, feat_vec=fv2, uright=ur2 if stereo2 else None, has_mp=mp2)
     for only_stereo in (False, True):
         for check_ori in (False, True):
             m = orbamd.ORBmatcher(0.6, check_ori)

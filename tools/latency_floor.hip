@@ -28,6 +28,20 @@ __global__ void k_read_host_signal(int* __restrict__ out, const int* __restrict_
     if (threadIdx.x == 0) __hip_atomic_store(done, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// per-call inputs passed by value in the kernel arguments instead of an H2D copy
+template <int WORDS>
+struct ArgBlock {
+    int w[WORDS];
+};
+template <int WORDS>
+__global__ void k_args_signal(ArgBlock<WORDS> a, int* __restrict__ out, int* __restrict__ done, int v) {
+    int s = 0;
+    for (int i = threadIdx.x; i < WORDS; i += blockDim.x) s += a.w[i];
+    out[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 #define CK(x)                                                   \
     do {                                                        \
         hipError_t e = (x);                                     \
@@ -137,6 +151,43 @@ int main(int argc, char** argv) {
         if (hipGetLastError()) return 1;
         return wait_done(seq);
     });
+    static ArgBlock<256> a1;
+    static ArgBlock<768> a3;
+    static ArgBlock<1000> a4;
+    for (int i = 0; i < 1000; i++) a4.w[i] = i;
+    rc |= run_w("kernel_args_1k_poll_word", false, [&] {
+        a1.w[seq & 255]++;
+        hipLaunchKernelGGL(k_args_signal<256>, dim3(1), dim3(256), 0, st, a1, di, done, ++seq);
+        if (hipGetLastError()) return 1;
+        return wait_done(seq);
+    });
+    rc |= run_w("kernel_args_3k_poll_word", false, [&] {
+        a3.w[seq % 768]++;
+        hipLaunchKernelGGL(k_args_signal<768>, dim3(1), dim3(256), 0, st, a3, di, done, ++seq);
+        if (hipGetLastError()) return 1;
+        return wait_done(seq);
+    });
+    rc |= run_w("kernel_args_4000B_poll_word", false, [&] {
+        a4.w[seq % 1000]++;
+        hipLaunchKernelGGL(k_args_signal<1000>, dim3(90), dim3(256), 0, st, a4, di, done, ++seq);
+        if (hipGetLastError()) return 1;
+        return wait_done(seq);
+    });
+    {   // the 4000-byte block arrives intact
+        int* chk;
+        CK(hipHostMalloc((void**)&chk, 4096, hipHostMallocCoherent));
+        memset(chk, 0, 4096);
+        for (int i = 0; i < 1000; i++) a4.w[i] = 3 * i + 1;
+        hipLaunchKernelGGL(k_args_signal<1000>, dim3(1), dim3(256), 0, st, a4, chk, done, ++seq);
+        CK(hipStreamSynchronize(st));
+        long want = 0, got = 0;
+        for (int t = 0; t < 256; t++) {
+            for (int i = t; i < 1000; i += 256) want += 3 * i + 1;
+            got += chk[t];
+        }
+        printf("{\"case\": \"kernel_args_4000B_intact\", \"ok\": %s}\n", want == got ? "true" : "false");
+        (void)hipHostFree(chk);
+    }
     CK(hipStreamSynchronize(st));
     (void)hipHostFree(done);
     (void)hipFree(dp);
