@@ -532,7 +532,8 @@ def main():
             "value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": "median of 5 runs, %d synthetic %dx%d frames in %.1f s in total (extract + BF triangulation vs "
                       "previous) on %d threads (every CPU of the affinity set, capped by the cgroup quota), "
-                      "oracle/orb_oracle.c -O3 -march=x86-64-v3 -ffp-contract=off (a restatement, compiler-vectorised only: no OpenCV SIMD/IPP); "
+                      "oracle/orb_oracle.c -O3 -march=x86-64-v3 -ffp-contract=off (a restatement; cv::FAST in OpenCV's SSE2 "
+                      "vector form (detection + cornerScore), the other stages compiler-vectorised, no IPP); "
                       "1-thread leg: %d frames in %.1f s" % (nfr, W, H, sec, threads, nfr1, sec1),
             "host": info,
             "value_1thread": round(fps1, 2),

@@ -47,6 +47,7 @@ _SIG = {
     "oc_resize_linear": (None, [_P, _I, _I, _SZ, _P, _I, _I, _SZ]),
     "oc_gauss7": (None, [_P, _I, _I, _SZ, _P, _SZ]),
     "oc_fast": (_I, [_P, _I, _I, _SZ, _I, _P, _I]),
+    "oc_set_fast_simd": (None, [_I]),
     "oc_descriptor_distance": (_I, [_P, _P]),
     "oc_sincosf_batch": (None, [_P, _P, _P, _I]),
     "oc_search_for_triangulation": (_I, [C.POINTER(_View), C.POINTER(_View), _P, _F, _F, _I, _I, _P]),
@@ -197,6 +198,11 @@ def gauss_kernel_q8():
     k = np.empty(7, np.int32)
     s = load().oc_gauss_kernel_q8(k.ctypes.data)
     return k, s
+
+
+def set_fast_simd(on):
+    """1: cv::FAST's vector form (AVX2 build), 0: scalar per pixel (same output)"""
+    load().oc_set_fast_simd(1 if on else 0)
 
 
 def fast_atan2(y, x):

@@ -236,6 +236,77 @@ static int corner_score16(const uint8_t* ptr, const int pixel[], int threshold) 
     return -b0 - 1;
 }
 
+/* 1: FAST decides 16 pixels of a row at a time with SSE2, as OpenCV's FAST_t<16> vector form does (the
+ * CPU baseline then times the form the reference runs through OpenCV; unlike OpenCV, a row's tail is one
+ * more, overlapping, vector step instead of scalar pixels); 0: the scalar form for every pixel. Both give
+ * the same keypoints and scores (tests/test_oracle_primitives.py compares them). */
+static int g_fast_simd = 1;
+void oc_set_fast_simd(int on) { g_fast_simd = on; }
+
+#if defined(__SSE2__)
+#include <emmintrin.h>
+/* OpenCV FAST_t<16> vector step over the 16 pixels at ptr: a pixel is a corner when some 9 contiguous
+ * circle pixels (of the 25-long wrapped circle, as the scalar count > K) are all brighter than v+t or all
+ * darker than v-t, with v+t / v-t saturated to [0,255] (an x beyond them never exists, as in the scalar
+ * int comparison). Bytes are compared signed after ^0x80. The cardinal pre-test (two consecutive
+ * cardinal points both brighter / both darker) is necessary for a 9-arc. Returns the 16-bit corner mask. */
+static unsigned fast_sse2_16(const uint8_t* ptr, const int pixel[25], int threshold) {
+    const __m128i delta = _mm_set1_epi8((char)0x80), t = _mm_set1_epi8((char)threshold);
+    const __m128i vv = _mm_loadu_si128((const __m128i*)ptr);
+    const __m128i vlo = _mm_xor_si128(_mm_subs_epu8(vv, t), delta);
+    const __m128i vhi = _mm_xor_si128(_mm_adds_epu8(vv, t), delta);
+#define LDX(k) _mm_xor_si128(_mm_loadu_si128((const __m128i*)(ptr + pixel[k])), delta)
+    const __m128i x0 = LDX(0), x1 = LDX(4), x2 = LDX(8), x3 = LDX(12);
+    const __m128i b0 = _mm_cmpgt_epi8(x0, vhi), b1 = _mm_cmpgt_epi8(x1, vhi), b2 = _mm_cmpgt_epi8(x2, vhi),
+                  b3 = _mm_cmpgt_epi8(x3, vhi);
+    const __m128i d0 = _mm_cmpgt_epi8(vlo, x0), d1 = _mm_cmpgt_epi8(vlo, x1), d2 = _mm_cmpgt_epi8(vlo, x2),
+                  d3 = _mm_cmpgt_epi8(vlo, x3);
+    __m128i m = _mm_or_si128(_mm_and_si128(b0, b1), _mm_and_si128(b1, b2));
+    m = _mm_or_si128(m, _mm_or_si128(_mm_and_si128(b2, b3), _mm_and_si128(b3, b0)));
+    m = _mm_or_si128(m, _mm_or_si128(_mm_and_si128(d0, d1), _mm_and_si128(d1, d2)));
+    m = _mm_or_si128(m, _mm_or_si128(_mm_and_si128(d2, d3), _mm_and_si128(d3, d0)));
+    if (_mm_movemask_epi8(m) == 0) return 0;
+    __m128i c0 = _mm_setzero_si128(), c1 = c0, max0 = c0, max1 = c0;
+    for (int k = 0; k < 25; k++) { /* run lengths: c = (c + 1) & hit, per byte */
+        const __m128i x = LDX(k);
+        const __m128i h0 = _mm_cmpgt_epi8(x, vhi), h1 = _mm_cmpgt_epi8(vlo, x);
+        c0 = _mm_and_si128(_mm_sub_epi8(c0, h0), h0);
+        c1 = _mm_and_si128(_mm_sub_epi8(c1, h1), h1);
+        max0 = _mm_max_epu8(max0, c0);
+        max1 = _mm_max_epu8(max1, c1);
+    }
+#undef LDX
+    max0 = _mm_max_epu8(max0, max1);
+    return (unsigned)_mm_movemask_epi8(_mm_cmpgt_epi8(max0, _mm_set1_epi8(8)));
+}
+
+/* cornerScore<16>, OpenCV's SSE2 form: for the 16 arcs of 9 (8 at a time, as int16 lanes), the dark
+ * bound max_k min(d[k..k+8]) and the bright bound min_k max(d[k..k+8]); score = max(dark, -bright) - 1.
+ * For a corner it equals corner_score16 (whose threshold floor is below both). */
+static int corner_score16_sse2(const uint8_t* ptr, const int pixel[25]) {
+    short d[32];
+    const int v = ptr[0];
+    for (int k = 0; k < 25; k++) d[k] = (short)(v - ptr[pixel[k]]);
+    __m128i q0 = _mm_set1_epi16(-1000), q1 = _mm_set1_epi16(1000);
+    for (int k = 0; k < 16; k += 8) {
+        __m128i a = _mm_loadu_si128((const __m128i*)(d + k + 1)), b = a;
+        for (int q = 2; q <= 8; q++) {
+            const __m128i x = _mm_loadu_si128((const __m128i*)(d + k + q));
+            a = _mm_min_epi16(a, x);
+            b = _mm_max_epi16(b, x);
+        }
+        const __m128i e0 = _mm_loadu_si128((const __m128i*)(d + k)), e9 = _mm_loadu_si128((const __m128i*)(d + k + 9));
+        q0 = _mm_max_epi16(q0, _mm_max_epi16(_mm_min_epi16(a, e0), _mm_min_epi16(a, e9)));
+        q1 = _mm_min_epi16(q1, _mm_min_epi16(_mm_max_epi16(b, e0), _mm_max_epi16(b, e9)));
+    }
+    q0 = _mm_max_epi16(q0, _mm_sub_epi16(_mm_setzero_si128(), q1));
+    q0 = _mm_max_epi16(q0, _mm_unpackhi_epi64(q0, q0));
+    q0 = _mm_max_epi16(q0, _mm_srli_si128(q0, 4));
+    q0 = _mm_max_epi16(q0, _mm_srli_si128(q0, 2));
+    return (short)_mm_cvtsi128_si32(q0) - 1;
+}
+#endif
+
 /* cv::FAST(img, keypoints, threshold, nonmaxSuppression=true), TYPE_9_16: OpenCV 3.x
  * FAST_t<16>. Called per cell at ORBextractor.cc:809-816. */
 int oc_fast(const uint8_t* img, int cols, int rows, size_t step, int threshold, float* xyr,
@@ -251,8 +322,14 @@ int oc_fast(const uint8_t* img, int cols, int rows, size_t step, int threshold, 
     uint8_t tab[512];
     for (i = -255; i <= 255; i++) tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
     if (cols < 7 || rows < 7) return 0;
-    uint8_t* bufmem = (uint8_t*)calloc((size_t)cols * 3, 1);
-    int* cpmem = (int*)malloc(sizeof(int) * (size_t)(cols + 1) * 3);
+    /* row buffers on the stack for a cell-sized ROI, as cv::FAST's AutoBuffer keeps them (no heap
+     * allocation per ORBextractor cell) */
+    uint8_t sbuf[3 * 128];
+    int scp[3 * 129];
+    const int small = cols <= 128;
+    uint8_t* bufmem = small ? sbuf : (uint8_t*)malloc((size_t)cols * 3);
+    int* cpmem = small ? scp : (int*)malloc(sizeof(int) * (size_t)(cols + 1) * 3);
+    memset(bufmem, 0, (size_t)cols * 3);
     uint8_t* buf[3] = {bufmem, bufmem + cols, bufmem + 2 * cols};
     int* cpbuf[3] = {cpmem + 1, cpmem + 1 + (cols + 1), cpmem + 1 + 2 * (cols + 1)};
     for (i = 3; i < rows - 2; i++) {
@@ -262,7 +339,25 @@ int oc_fast(const uint8_t* img, int cols, int rows, size_t step, int threshold, 
         memset(curr, 0, cols);
         int ncorners = 0;
         if (i < rows - 3) {
-            for (j = 3; j < cols - 3; j++, ptr++) {
+            j = 3;
+#if defined(__SSE2__)
+            if (g_fast_simd && cols - 3 - 16 >= 3) {
+                for (; j < cols - 3; j += 16, ptr += 16) {
+                    unsigned skip = 0;  /* the row's tail: one step ending at cols-4, its first columns done */
+                    if (j + 16 > cols - 3) {
+                        skip = (unsigned)(j - (cols - 3 - 16));
+                        ptr -= skip;
+                        j -= (int)skip;
+                    }
+                    for (unsigned m = fast_sse2_16(ptr, pixel, threshold) >> skip << skip; m; m &= m - 1) {
+                        const int b = __builtin_ctz(m);
+                        cornerpos[ncorners++] = j + b;
+                        curr[j + b] = (uint8_t)corner_score16_sse2(ptr + b, pixel);
+                    }
+                }
+            }
+#endif
+            for (; j < cols - 3; j++, ptr++) {
                 int v = ptr[0];
                 const uint8_t* t = tab - v + 255;
                 int d = t[ptr[pixel[0]]] | t[ptr[pixel[8]]];
@@ -326,8 +421,10 @@ int oc_fast(const uint8_t* img, int cols, int rows, size_t step, int threshold, 
             }
         }
     }
-    free(bufmem);
-    free(cpmem);
+    if (!small) {
+        free(bufmem);
+        free(cpmem);
+    }
     return nkp;
 }
 

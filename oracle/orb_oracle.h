@@ -59,6 +59,9 @@ void oc_resize_linear(const uint8_t* src, int sw, int sh, size_t sstep, uint8_t*
 void oc_gauss7(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst, size_t dstep);
 /* cv::FAST(img, kps, th, true) on a w x h view: xyr triplets, returns count */
 int oc_fast(const uint8_t* img, int w, int h, size_t step, int threshold, float* xyr, int cap);
+/* 1 (default): cv::FAST's vector form (AVX2, 32 pixels per step) where built; 0: scalar per pixel.
+ * Same output either way. */
+void oc_set_fast_simd(int on);
 
 void oc_sincosf_batch(const float* in, float* s, float* c, int n);
 

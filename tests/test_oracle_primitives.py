@@ -52,6 +52,34 @@ def test_fast_matches_definition(seed, t):
     assert np.array_equal(got, exp)
 
 
+@pytest.mark.parametrize("t", [0, 7, 20, 60, 255])
+def test_fast_vector_form_equals_scalar(t):
+    """the oracle's AVX2 FAST step (32 pixels, OpenCV FAST_t's vector form) equals its scalar form: noise,
+    flat areas, saturated pixels (v + t > 255, v - t < 0) and every row-tail width; and the whole extractor"""
+    rng = np.random.default_rng(100 + t)
+    imgs = [rng.integers(0, 256, (48, w), dtype=np.uint8) for w in (7, 35, 36, 37, 67, 68, 100)]
+    sat = rng.integers(0, 256, (40, 90), dtype=np.uint8)
+    sat[5:30, 10:80] = np.where(rng.random((25, 70)) < 0.5, 0, 255).astype(np.uint8)
+    imgs.append(sat)
+    try:
+        for img in imgs:
+            oracle_py.set_fast_simd(True)
+            a = oracle_py.fast(img, t)
+            oracle_py.set_fast_simd(False)
+            b = oracle_py.fast(img, t)
+            assert np.array_equal(a, b), img.shape
+        if t == 20:
+            orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+            for img in orbamd.synth_frames(1, 0, 2, 640, 480):
+                oracle_py.set_fast_simd(True)
+                ka, da = orc(img)
+                oracle_py.set_fast_simd(False)
+                kb, db = orc(img)
+                assert np.array_equal(ka.view(np.uint8), kb.view(np.uint8)) and np.array_equal(da, db)
+    finally:
+        oracle_py.set_fast_simd(True)
+
+
 def test_fast_pretest_lerp_exact():
     """k_fast_cells2's byte-SWAR pretest compares with v_lerp_u8 (per byte (a + b + r) >> 1):
     bright = bit 7 of lerp(lerp(c, 255 - v, r_b), 255 - M_b, 1) must equal c > v + t, and
