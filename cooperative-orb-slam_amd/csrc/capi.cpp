@@ -734,6 +734,19 @@ int orbx_debug_skip_stages(orbx_handle* h, int mask) {
     return 0;
 }
 
+int orbx_debug_raise_error(orbx_handle* h, int flag, void* stream) {
+    if (!h || flag <= 0) return ORBX_EARG;
+    HIPR(hipSetDevice(h->device));
+    int cur = 0;
+    hipStream_t st = (hipStream_t)stream;
+    HIPR(hipMemcpyAsync(&cur, h->err.as<int>() + kErrWordSticky, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPR(hipStreamSynchronize(st));
+    cur |= flag;
+    HIPR(hipMemcpyAsync(h->err.as<int>() + kErrWordSticky, &cur, sizeof(int), hipMemcpyHostToDevice, st));
+    HIPR(hipStreamSynchronize(st));
+    return 0;
+}
+
 int orbx_profile_enable(orbx_handle* h, int on) {
     if (!h) return ORBX_EARG;
     h->prof_on = on != 0;

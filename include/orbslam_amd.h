@@ -643,6 +643,11 @@ int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls);
  * the bench's self-check detects a stage that stopped launching. */
 int orbx_debug_skip_stages(orbx_handle* h, int mask);
 
+/* Test hook: ORs `flag` (> 0) into the handle's sticky batch error word, as a failing device batch
+ * would; the tests use it to show that host-path extractions (orbx_extract) neither clear nor hide it
+ * and that orbx_check_error reports and clears it once. */
+int orbx_debug_raise_error(orbx_handle* h, int flag, void* stream);
+
 /* Test hook: the device's restatement of glibc sinf/cosf (used by computeOrbDescriptor,
  * ORBextractor.cc:113) applied to n device floats; lets tests compare against host libm. */
 int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, void* stream);

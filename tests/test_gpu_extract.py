@@ -173,3 +173,19 @@ def test_host_path_graph_replay_and_size_changes():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.loads(r.stdout.strip().splitlines()[-1]) == sums
+
+
+def test_host_path_keeps_the_sticky_batch_error():
+    """an error raised by a device batch stays set across host-path extractions (orbx_extract has its own
+    per-call word) until orbx_check_error reports it, once (the host path used to zero it)"""
+    W, H = 640, 480
+    frames = orbamd.synth_frames(0, 0, 2, W, H)
+    ext = orbamd.ORBextractor(1000, 1.2, 8, 20, 7, max_width=W, max_height=H)
+    lib = orbamd.load()
+    ext(frames[0])
+    assert lib.orbx_check_error(ext._h, None) == 0
+    assert lib.orbx_debug_raise_error(ext._h, 4, None) == 0
+    kg, _ = ext(frames[1])  # a host-path call between the failing batch and the check
+    assert len(kg) > 900
+    assert lib.orbx_check_error(ext._h, None) == -2  # ORBX_EDEVICE
+    assert lib.orbx_check_error(ext._h, None) == 0   # cleared by the read
