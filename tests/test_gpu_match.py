@@ -273,3 +273,44 @@ def test_batch_pairs_crafted_descriptors(W, H, nf, check_ori):
         np.testing.assert_array_equal(mg[p, :v[a].n], mo)
         assert int(pipe.nmatch[p].item()) == no
     pipe.close()
+
+
+def _desc_nodes(d, shift=4):
+    """a FeatureVector keyed like a vocabulary (similar descriptors share a node): node = 100 + the top
+    (8 - shift) bits of descriptor byte 0"""
+    fv = {}
+    for i in range(len(d)):
+        fv.setdefault(100 + int(d[i, 0] >> shift), []).append(i)
+    return fv
+
+
+@pytest.mark.parametrize("W,H,nf,shift", [(1241, 376, 2000, 2), (752, 480, 1200, 3), (1241, 376, 3000, 2)])
+def test_per_call_matchers_large_frames(W, H, nf, shift):
+    """the host-API SearchByBoW ×2 and SearchForTriangulation over nodes at C3 / C4 sizes: 2000 features
+    (the small-call kernels' side limit is 2048 FeatureVector entries) and 3000 (over it: the staged
+    kernels), nodes of ~30-60 features; MapPoints, bad flags, stereo, both rotation settings"""
+    rng = np.random.default_rng(nf + shift)
+    (k1, d1), (k2, d2) = _frames_kf(3, 2, W=W, H=H, nf=nf)[0]
+    tabs = _frames_kf(3, 2, 1, W=W, H=H, nf=nf)[1]
+    F12, ex, ey = orbamd.device.default_geometry()
+    fv1, fv2 = _desc_nodes(d1, shift), _desc_nodes(d2, shift)
+    ur1 = np.where(rng.random(len(k1)) < 0.4, k1["x"] - rng.random(len(k1)) * 40, -1).astype(np.float32)
+    ur2 = np.where(rng.random(len(k2)) < 0.4, k2["x"] - rng.random(len(k2)) * 40, -1).astype(np.float32)
+    for mp_frac in (0.2, 0.8):
+        mp1, mp2 = rng.random(len(k1)) < mp_frac, rng.random(len(k2)) < mp_frac
+        bad1, bad2 = rng.random(len(k1)) < 0.05, rng.random(len(k2)) < 0.05
+        v1 = _view(k1, d1, tabs, feat_vec=fv1, uright=ur1, has_mp=mp1, mp_bad=bad1)
+        v2 = _view(k2, d2, tabs, feat_vec=fv2, uright=ur2, has_mp=mp2, mp_bad=bad2)
+        for ori in (False, True):
+            m = orbamd.ORBmatcher(0.75, ori)
+            for only_stereo in (False, True):
+                ng, mg = m.SearchForTriangulation(v1, v2, F12, ex, ey, only_stereo)
+                no, mo = oracle_py.search_for_triangulation(v1, v2, F12, ex, ey, only_stereo, ori)
+                assert ng == no
+                np.testing.assert_array_equal(mg, mo)
+            for kfkf in (False, True):
+                ng, mg = m.SearchByBoW(v1, v2, other_is_keyframe=kfkf)
+                no, mo = oracle_py.search_by_bow(v1, v2, 0.75, ori, other_is_keyframe=kfkf)
+                assert ng == no and (mp_frac < 0.5 or no > 0)
+                np.testing.assert_array_equal(mg, mo)
+            m.close()
