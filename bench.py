@@ -156,28 +156,30 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000):
     return sum(count) / el, sum(count), el, per
 
 
-def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, dist):
+def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, dist, nstreams=4):
     """The schedule with every step's B frames uploaded from pinned host memory (the frame pool, batch
-    i mod pool at step i) on a copy stream into the device batch the step processes. Upload i waits for
-    step i-pool (the previous user of that device batch) and step i waits for upload i, so an upload
+    i mod pool at step i) into the device batch the step processes: graph p's frames on copy stream
+    p mod nstreams (several DMA engines in flight), and graph p starts extracting as soon as its own frames
+    have arrived. Upload i waits for step i-pool (the previous user of that device batch), so an upload
     overlaps the previous step's compute. Returns frames/s over nsteps after `pool` warm-up steps and the
     H2D rate achieved (W*H bytes per frame, max over ranks)."""
     P, sub, dev = sched.P, sched.sub, sched.dev
     host = [torch.from_numpy(frames_np[r * B:(r + 1) * B]).pin_memory() for r in range(pool)]
-    copy_st = torch.cuda.Stream(dev)
-    up = [torch.cuda.Event() for _ in range(pool)]
+    copy_st = [torch.cuda.Stream(dev) for _ in range(max(1, min(nstreams, P)))]
+    up = [[torch.cuda.Event() for _ in range(P)] for _ in range(pool)]
     done = [[torch.cuda.Event() for _ in range(P)] for _ in range(pool)]
     used = [False] * pool
 
     def one(i):
         r = i % pool
-        with torch.cuda.stream(copy_st):
-            if used[r]:
-                for e in done[r]:
-                    copy_st.wait_event(e)
-            for p in range(P):
+        for p in range(P):
+            cs = copy_st[p % len(copy_st)]
+            with torch.cuda.stream(cs):
+                if used[r]:
+                    for e in done[r]:
+                        cs.wait_event(e)
                 sched.frames[r][p].copy_(host[r][p * sub:(p + 1) * sub], non_blocking=True)
-            up[r].record(copy_st)
+                up[r][p].record(cs)
         sched.step(batch=r, wait=up[r], first=i == 0)
         for p in range(P):
             done[r][p].record(sched.streams[p])
@@ -200,8 +202,10 @@ def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, 
     fps = world * B * nsteps / el
     return {"frames_per_s": round(fps, 1), "per_gpu_frames_per_s": round(fps / world, 1),
             "h2d_GBs_per_gpu": round(B * W * H * nsteps / el / 1e9, 2), "steps": nsteps, "seconds": round(el, 3),
-            "source": "pinned host memory, %d batches of %d frames uploaded round-robin (one batch per step), "
-                      "copy stream overlapped with the previous step's compute" % (pool, B)}
+            "copy_streams": len(copy_st),
+            "source": "pinned host memory, %d batches of %d frames uploaded round-robin (one batch per step) on %d "
+                      "copy streams, overlapped with the previous step's compute; each graph starts on its own "
+                      "frames' arrival" % (pool, B, len(copy_st))}
 
 
 def main():
@@ -233,6 +237,7 @@ def main():
                     help="resident batches of distinct frames; step k processes batch k mod pool (stale-output guard)")
     ap.add_argument("--dist", action="store_true",
                     help="use torch.distributed (RCCL) and the out-of-place all-gather even at world 1")
+    ap.add_argument("--ingest-streams", type=int, default=4, help="copy streams of the ingest leg (<= --pipes)")
     ap.add_argument("--ingest-steps", type=int, default=100,
                     help="steps of the ingest leg (frames uploaded from pinned host memory each step; 0: skip)")
     ap.add_argument("--stagger", choices=("each", "once", "none"), default="each",
@@ -403,7 +408,8 @@ def main():
     if args.ingest_steps > 0:
         if use_dist:
             dist.barrier()
-        ingest = run_ingest(torch, sched, frames_np, args.pool, args.ingest_steps, B, W, H, world, use_dist, dist)
+        ingest = run_ingest(torch, sched, frames_np, args.pool, args.ingest_steps, B, W, H, world, use_dist, dist,
+                            args.ingest_streams)
         if not args.no_check:
             chk = check_schedule(sched, frames_np, nfeatures=cfg["nfeatures"], agent_frames=agent_kf)
             ingest["bit_exact"] = bool(chk["bit_exact"])

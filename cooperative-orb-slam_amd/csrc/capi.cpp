@@ -2108,7 +2108,9 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     const size_t o_gs = cv.take(ce ? 0 : 4 * (kGridCols * kGridRows + 1)), o_gi = cv.take(2 * nF),
                  o_scan = cv.take(32 * nq), o_scnt = cv.take(4 * nq), o_res = cv.take(8 * nq);
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
-    uint8_t* hp = ctx->ensure_pinned(in_bytes + std::max(4 * nout + 4, 8 * nq));
+    // results: written by the kernels straight into the pinned buffer after the inputs (ProjCall::host_out)
+    const size_t n_host = std::max(nout + 1, nq);
+    uint8_t* hp = ctx->ensure_pinned(in_bytes + 8 * n_host);
     if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
     hipStream_t st = ctx->stream;
@@ -2155,6 +2157,8 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     c.res = (int*)(base + o_res);
     c.nmatches = (int32_t*)(base + o_nm);
     c.match = (int32_t*)(base + o_nm + 4);
+    c.host_out = (unsigned long long*)ctx->pinned_on_device(in_bytes);
+    c.seq = (int)ctx->next_seq();
     if (inv_sigma2)
         for (int l = 0; l < F->nlevels; l++) c.inv_sigma2[l] = inv_sigma2[l];
     memcpy(hp + o_call, &c, sizeof(c));
@@ -2173,18 +2177,29 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     }
     HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, st));
     HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st, !c.direct, init_n >= 0, !ce));
-    uint8_t* ho = hp + in_bytes;
+    // poll the results (each carries this call's seq) instead of a D2H copy + stream synchronisation
+    const unsigned long long* ho = (const unsigned long long*)(hp + in_bytes);
+    const uint32_t seq = (uint32_t)c.seq;
+    const size_t nwait = c.direct ? nq : nout + 1;
+    size_t next = 0;
+    if (const int rc = wait_until(st, [&] {
+            while (next < nwait && (uint32_t)(__atomic_load_n(ho + next, __ATOMIC_ACQUIRE) >> 32) == seq) next++;
+            return next == nwait;
+        }))
+        return rc;
     if (qres) {
-        // per-query results (Fuse): res[2 qi] = the accepted feature or -1, reported at the query's src
-        HIPR(hipMemcpyAsync(ho, base + o_res, 8 * nq, hipMemcpyDeviceToHost, st));
-        HIPR(hipStreamSynchronize(st));
-        for (size_t qi = 0; qi < nq; qi++) qres[pb.q[qi].src] = ((const int32_t*)ho)[2 * qi];
+        // per-query results (Fuse): the accepted feature or -1, reported at the query's src
+        if (c.direct)
+            for (size_t qi = 0; qi < nq; qi++) qres[pb.q[qi].src] = (int32_t)(uint32_t)ho[qi];
+        else {  // a resolve launch: per-query results stay on the device (res[2 qi])
+            HIPR(hipMemcpyAsync(hp, base + o_res, 8 * nq, hipMemcpyDeviceToHost, st));
+            HIPR(hipStreamSynchronize(st));
+            for (size_t qi = 0; qi < nq; qi++) qres[pb.q[qi].src] = ((const int32_t*)hp)[2 * qi];
+        }
         return 0;
     }
-    HIPR(hipMemcpyAsync(ho, base + o_nm, 4 * nout + 4, hipMemcpyDeviceToHost, st));
-    HIPR(hipStreamSynchronize(st));
-    if (nout) memcpy(match, ho + 4, 4 * nout);
-    if (nmatches) memcpy(nmatches, ho, 4);
+    for (size_t i = 0; i < nout; i++) match[i] = (int32_t)(uint32_t)ho[i];
+    if (nmatches) *nmatches = (int)(uint32_t)ho[nout];
     return 0;
 }
 

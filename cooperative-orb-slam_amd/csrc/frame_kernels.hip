@@ -493,6 +493,21 @@ __device__ __forceinline__ int proj_scan(const ProjCall& c, const ProjQuery& q, 
 
 constexpr int kProjTopK = 4;
 
+/* one result of a per-call host API launch: a single 64-bit store of (value, call seq) to pinned host memory;
+ * the host takes an entry once it carries its call's seq, whatever order the stores land in */
+__device__ __forceinline__ void host_put(unsigned long long* p, int v, int seq) {
+    __hip_atomic_store(p, (unsigned long long)(uint32_t)v | (unsigned long long)(uint32_t)seq << 32, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+/* the call's match[0 .. n) and nmatches to host_out (the last step of a resolve wave) */
+__device__ __forceinline__ void host_put_matches(const ProjCall& c, int32_t* match, int n, int nm, int lane) {
+    __threadfence();  // this wave's match[] atomics / stores are done at agent scope
+    for (int i = lane; i < n; i += 64)
+        host_put(c.host_out + i, __hip_atomic_load(match + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), c.seq);
+    if (lane == 0) host_put(c.host_out + n, nm, c.seq);
+}
+
 __global__ __launch_bounds__(256) void k_proj_scan(const ProjCall* __restrict__ calls) {
     const ProjCall& c = calls[blockIdx.y];
     const int qi = blockIdx.x * 16 + (threadIdx.x >> 4), gl = threadIdx.x & 15;
@@ -526,8 +541,13 @@ __global__ __launch_bounds__(256) void k_proj_scan(const ProjCall* __restrict__ 
         // excluded by the scan), accepted when bestDist <= the threshold -- what k_proj_resolve would write
         if (c.direct && gl == 0) {
             const bool acc = top[0] != kNoKey && (int)(top[0] >> 40) <= c.accept_th;
-            c.res[2 * qi] = acc ? (int)(top[0] & 0xffff) : -1;
-            c.res[2 * qi + 1] = 0;
+            const int r = acc ? (int)(top[0] & 0xffff) : -1;
+            if (c.host_out) {
+                host_put(c.host_out + qi, r, c.seq);
+            } else {
+                c.res[2 * qi] = r;
+                c.res[2 * qi + 1] = 0;
+            }
         }
     }
 }
@@ -729,6 +749,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
         nacc -= removed;
     }
     if (lane == 0) *c.nmatches = nacc;
+    if (c.host_out) host_put_matches(c, c.match, c.n, nacc, lane);
 }
 
 /* ============================ SearchForInitialization ============================ */
@@ -875,12 +896,16 @@ __global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict_
     int nm = 0;
     for (int i = lane; i < c.n_out; i += 64) {
         const int m = s_v12[i];
-        c.match[i] = m;
+        if (c.host_out) host_put(c.host_out + i, m, c.seq);
+        else c.match[i] = m;
         nm += m >= 0;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o);
-    if (lane == 0) *c.nmatches = nm;
+    if (lane == 0) {
+        if (c.host_out) host_put(c.host_out + c.n_out, nm, c.seq);
+        else *c.nmatches = nm;
+    }
 }
 
 int init_max_features() { return kInitMaxN; }

@@ -81,6 +81,10 @@ struct ProjCall {
                                // res[] from its best key and k_proj_resolve is not launched
     int n_out;                 // SearchForInitialization (k_init_resolve): F1's N, the length of match[] =
                                // vnMatches12
+    unsigned long long* host_out;  // per-call host API (or nullptr): the results written straight to pinned host
+                                   // memory, each entry (uint32 value | seq << 32): direct mode one per query,
+                                   // otherwise match[0 .. n or n_out) then nmatches
+    int seq;                       // this call's sequence number (> 0)
 };
 
 }  // namespace orbamd

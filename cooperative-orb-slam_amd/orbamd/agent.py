@@ -91,8 +91,8 @@ class AgentSchedule:
 
     def step(self, ev=None, xev=None, extract=True, match=True, xchg=True, first=True, batch=None, wait=None):
         """enqueue one step over the next pool batch (or `batch`); ev[p] = (start, end) events around graph
-        p's matcher, xev around the exchange; wait: an event every graph waits for before extracting (the
-        ingest leg's upload of this batch)"""
+        p's matcher, xev around the exchange; wait: an event every graph waits for before extracting, or one
+        event per graph (the ingest leg's upload of that graph's frames)"""
         torch = self.torch
         r = self.cursor % self.pool if batch is None else batch
         self.cursor += 1
@@ -101,7 +101,7 @@ class AgentSchedule:
             st = self.streams[p].cuda_stream
             if extract:
                 if wait is not None:
-                    self.streams[p].wait_event(wait)
+                    self.streams[p].wait_event(wait[p] if isinstance(wait, (list, tuple)) else wait)
                 if p > 0 and (self.stagger == "each" or (self.stagger == "once" and first)):
                     self.streams[p].wait_event(self.done[p - 1])
                 self.pipes[p].extract(self.frames[r][p], st)
