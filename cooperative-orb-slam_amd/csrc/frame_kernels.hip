@@ -332,6 +332,11 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
 /* ============================ SearchByProjection ============================ */
 
 constexpr unsigned long long kNoKey = ~0ull;
+/* a projection-scan candidate key: dist << 40 | cell order << 20 | feature idx << 4 | octave. Keys order by
+ * (dist, cell order, idx) as the reference's scan does (the octave is a function of idx); the octave rides
+ * along so the resolve's ratio test reads no feature array (no dependent global load per round). */
+__device__ __forceinline__ int key_idx(unsigned long long k) { return (int)((k >> 4) & 0xffffu); }
+__device__ __forceinline__ int key_oct(unsigned long long k) { return (int)(k & 15u); }
 
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int o) {
     const int lo = __shfl_xor((int)(uint32_t)v, o), hi = __shfl_xor((int)(uint32_t)(v >> 32), o);
@@ -473,7 +478,8 @@ __device__ __forceinline__ int proj_scan(const ProjCall& c, const ProjQuery& q, 
                                  __popc(qd0.w ^ f0.w) + __popc(qd1.x ^ f1.x) + __popc(qd1.y ^ f1.y) +
                                  __popc(qd1.z ^ f1.z) + __popc(qd1.w ^ f1.w);
                 if (dist < 256 && elig(idx, dist)) {  // bestDist starts at 256 (ORBmatcher.cc:78, 349, 1397, 1550)
-                    topk_insert<K>(((unsigned long long)dist << 40) | ((unsigned long long)k << 16) | (unsigned)idx, top);
+                    topk_insert<K>(((unsigned long long)dist << 40) | ((unsigned long long)k << 20) |
+                                       ((unsigned long long)idx << 4) | (unsigned)oct, top);
                     ncand++;
                 }
             }
@@ -502,10 +508,24 @@ __device__ __forceinline__ void host_put(unsigned long long* p, int v, int seq) 
 
 /* the call's match[0 .. n) and nmatches to host_out (the last step of a resolve wave) */
 __device__ __forceinline__ void host_put_matches(const ProjCall& c, int32_t* match, int n, int nm, int lane) {
-    __threadfence();  // this wave's match[] atomics / stores are done at agent scope
-    for (int i = lane; i < n; i += 64)
-        host_put(c.host_out + i, __hip_atomic_load(match + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), c.seq);
-    if (lane == 0) host_put(c.host_out + n, nm, c.seq);
+    // this wave's own match[] atomics / stores complete before its loads (they were never loaded into L1, so
+    // the loads read them from L2); 8 independent loads per lane in flight before their stores
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    constexpr int U = 8;
+    unsigned long long* const out = c.host_out;
+    const int seq = c.seq;
+    if (n > 0)
+        for (int i0 = 0; i0 < n; i0 += 64 * U) {
+            int v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = match[min(i0 + 64 * u + lane, n - 1)];  // unconditional: no waits
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int i = i0 + 64 * u + lane;
+                if (i < n) host_put(out + i, v[u], seq);
+            }
+        }
+    if (lane == 0) host_put(out + n, nm, seq);
 }
 
 __global__ __launch_bounds__(256) void k_proj_scan(const ProjCall* __restrict__ calls) {
@@ -541,7 +561,7 @@ __global__ __launch_bounds__(256) void k_proj_scan(const ProjCall* __restrict__ 
         // excluded by the scan), accepted when bestDist <= the threshold -- what k_proj_resolve would write
         if (c.direct && gl == 0) {
             const bool acc = top[0] != kNoKey && (int)(top[0] >> 40) <= c.accept_th;
-            const int r = acc ? (int)(top[0] & 0xffff) : -1;
+            const int r = acc ? key_idx(top[0]) : -1;
             if (c.host_out) {
                 host_put(c.host_out + qi, r, c.seq);
             } else {
@@ -559,9 +579,8 @@ __device__ __forceinline__ bool proj_accept(const ProjCall& c, unsigned long lon
     const int dist = (int)(b >> 40);
     if (dist > c.accept_th) return false;
     if (c.ratio) {
-        const int bi = (int)(b & 0xffff);
-        const int level = c.octave[bi];
-        const int level2 = s != kNoKey ? c.octave[(int)(s & 0xffff)] : -1;
+        const int level = key_oct(b);
+        const int level2 = s != kNoKey ? key_oct(s) : -1;
         const int dist2 = s != kNoKey ? (int)(s >> 40) : 256;
         if (level == level2 && (float)dist > __fmul_rn(c.nnratio, (float)dist2)) return false;
     }
@@ -603,7 +622,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
     }
     for (int i = lane; i < c.n; i += 64) c.match[i] = -1;
     if (lane < 32) s_hist[lane] = 0;
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // one wave: order its own global accesses (no L2 write-back)
     wave_lds_sync();
     auto occ_get = [](int i) { return (s_occ[i >> 5] >> (i & 31)) & 1u; };
     const int need = c.ratio ? 2 : 1;  // list entries that decide the result
@@ -613,15 +632,13 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
     // chunk registers; the next chunk's loads are issued before the current chunk's rounds
     unsigned long long top[kProjTopK], ntop[kProjTopK];
     int ncand = 0, flags = 0, src = 0, nncand = 0, nflags = 0, nsrc = 0;
-    float qang = 0.f, nqang = 0.f;
-    auto load_chunk = [&](int b0, unsigned long long (&t)[kProjTopK], int& cnt, int& fl, int& sr, float& an) {
+    auto load_chunk = [&](int b0, unsigned long long (&t)[kProjTopK], int& cnt, int& fl, int& sr) {
         const int qi = b0 + lane;
 #pragma unroll
         for (int k = 0; k < kProjTopK; k++) t[k] = kNoKey;
         cnt = 0;
         fl = 0;
         sr = 0;
-        an = 0.f;
         if (qi < c.nq) {
 #pragma unroll
             for (int k = 0; k < kProjTopK; k++) t[k] = c.scan[(long long)kProjTopK * qi + k];
@@ -629,10 +646,9 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
             const ProjQuery& q = c.q[qi];
             fl = q.flags;
             sr = q.src;
-            an = q.angle;
         }
     };
-    load_chunk(0, ntop, nncand, nflags, nsrc, nqang);
+    load_chunk(0, ntop, nncand, nflags, nsrc);
     for (int base = 0; base < c.nq; base += 64) {
         const int qi = base + lane;
         const bool in = qi < c.nq;
@@ -641,8 +657,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
         ncand = nncand;
         flags = nflags;
         src = nsrc;
-        qang = nqang;
-        if (base + 64 < c.nq) load_chunk(base + 64, ntop, nncand, nflags, nsrc, nqang);
+        if (base + 64 < c.nq) load_chunk(base + 64, ntop, nncand, nflags, nsrc);
         int done = 0;  // lanes < done are committed
         while (done < 64 && base + done < c.nq) {
             const bool act = in && lane >= done;
@@ -651,13 +666,13 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
 #pragma unroll
             for (int t = 0; t < kProjTopK; t++) {
                 const unsigned long long k = top[t];
-                if (k == kNoKey || occ_get((int)(k & 0xffff))) continue;
+                if (k == kNoKey || occ_get(key_idx(k))) continue;
                 if (found == 0) b = k; else if (found == 1) s = k;
                 found++;
             }
             const bool rescan = act && found < need && ncand > kProjTopK;
-            const int bi = b != kNoKey ? (int)(b & 0xffff) : -1;
-            const int si = s != kNoKey ? (int)(s & 0xffff) : -1;
+            const int bi = b != kNoKey ? key_idx(b) : -1;
+            const int si = s != kNoKey ? key_idx(s) : -1;
             const bool acc = act && !rescan && proj_accept(c, b, s);
             const int my_claim = acc && (flags & kProjClaims) ? bi : -1;
             // conflicts with earlier uncommitted claims of this round: claim table (lane ids, hashed by feature;
@@ -675,8 +690,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
                 if (acc) {
                     atomicMax(&c.match[bi], src);
                     if (my_claim >= 0) atomicOr(&s_occ[bi >> 5], 1u << (bi & 31));
-                    c.res[2 * qi] = bi;
-                    c.res[2 * qi + 1] = c.check_ori ? rot_bin(qang, c.angle[bi]) : 0;
+                    c.res[2 * qi] = bi;  // the rotation bin is taken after the chunks (no load in a round)
                     nacc++;
                 } else {
                     c.res[2 * qi] = -1;
@@ -692,11 +706,10 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
                 const bool acc2 = proj_accept(c, t2[0], t2[1]);
                 if (lane == 0) {
                     if (acc2) {
-                        const int bi2 = (int)(t2[0] & 0xffff);
+                        const int bi2 = key_idx(t2[0]);
                         atomicMax(&c.match[bi2], q.src);
                         if (q.flags & kProjClaims) atomicOr(&s_occ[bi2 >> 5], 1u << (bi2 & 31));
                         c.res[2 * qd] = bi2;
-                        c.res[2 * qd + 1] = c.check_ori ? rot_bin(q.angle, c.angle[bi2]) : 0;
                         nacc++;
                     } else {
                         c.res[2 * qd] = -1;
@@ -709,12 +722,17 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
             }
         }
     }
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // one wave: order its own global accesses (no L2 write-back)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) nacc += __shfl_xor(nacc, o);
     if (c.check_ori) {  // rotation consistency (ORBmatcher.cc:1437-1467)
-        for (int q = lane; q < c.nq; q += 64)
-            if (c.res[2 * q] >= 0) atomicAdd(&s_hist[c.res[2 * q + 1]], 1);
+        for (int q = lane; q < c.nq; q += 64) {
+            const int f = c.res[2 * q];
+            if (f < 0) continue;
+            const int bin = rot_bin(c.q[q].angle, c.angle[f]);
+            c.res[2 * q + 1] = bin;
+            atomicAdd(&s_hist[bin], 1);
+        }
         wave_lds_sync();
         int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;  // ComputeThreeMaxima (:1601-1642)
         for (int i = 0; i < 30; i++) {
@@ -793,28 +811,25 @@ __global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict_
         const float d2 = s2 != kNoKey ? (float)(int)(s2 >> 40) : 2147483647.0f;
         return d1 <= 50 && (float)d1 < __fmul_rn(d2, c.nnratio);
     };
-    auto commit = [&](int qi, int i1, unsigned long long b, float qang) {
-        const int i2 = (int)(b & 0xffff);
+    auto commit = [&](int qi, int i1, unsigned long long b) {
+        const int i2 = key_idx(b);
         const int prev = s_v21[i2];
         if (prev >= 0) s_v12[prev] = -1;
         s_v12[i1] = (int16_t)i2;
         s_v21[i2] = (int16_t)i1;
         s_md[i2] = (uint16_t)(b >> 40);
-        c.res[2 * qi] = i2;
-        c.res[2 * qi + 1] = c.check_ori ? rot_bin(qang, c.angle[i2]) : 0;
+        c.res[2 * qi] = i2;  // its rotation bin is taken after the chunks
     };
     for (int base = 0; base < c.nq; base += 64) {
         const int qi = base + lane;
         const bool in = qi < c.nq;
         unsigned long long top[kProjTopK];
         int ncand = 0, src = 0;
-        float qang = 0.f;
 #pragma unroll
         for (int k = 0; k < kProjTopK; k++) top[k] = in ? c.scan[(long long)kProjTopK * qi + k] : kNoKey;
         if (in) {
             ncand = c.scan_cnt[qi];
             src = c.q[qi].src;
-            qang = c.q[qi].angle;
         }
         int done = 0;
         while (done < 64 && base + done < c.nq) {
@@ -824,14 +839,14 @@ __global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict_
 #pragma unroll
             for (int t = 0; t < kProjTopK; t++) {
                 const unsigned long long k = top[t];
-                if (k == kNoKey || !usable((int)(k & 0xffff), (int)(k >> 40))) continue;
+                if (k == kNoKey || !usable(key_idx(k), (int)(k >> 40))) continue;
                 if (found == 0) b = k; else if (found == 1) s2 = k;
                 found++;
             }
             const bool rescan = act && found < 2 && ncand > kProjTopK;
             const bool acc = act && !rescan && accept(b, s2);
-            const int bi = b != kNoKey ? (int)(b & 0xffff) : -1;
-            const int si = s2 != kNoKey ? (int)(s2 & 0xffff) : -1;
+            const int bi = b != kNoKey ? key_idx(b) : -1;
+            const int si = s2 != kNoKey ? key_idx(s2) : -1;
             if (acc) atomicMin(&s_claim[bi & (kClaimTab - 1)], lane);
             wave_lds_sync();
             bool dirty = rescan;
@@ -842,7 +857,7 @@ __global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict_
             wave_lds_sync();
             if (acc) s_claim[bi & (kClaimTab - 1)] = 64;
             if (act && lane < d) {
-                if (acc) commit(qi, src, b, qang);
+                if (acc) commit(qi, src, b);
                 else c.res[2 * qi] = -1;
             }
             wave_lds_sync();
@@ -853,7 +868,7 @@ __global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict_
                 unsigned long long t2[2];
                 proj_scan<64, 2>(c, q, qp[0], qp[1], lane, [](int) { return false; }, t2, usable);
                 if (lane == 0) {
-                    if (accept(t2[0], t2[1])) commit(qd, q.src, t2[0], q.angle);
+                    if (accept(t2[0], t2[1])) commit(qd, q.src, t2[0]);
                     else c.res[2 * qd] = -1;
                 }
                 wave_lds_sync();
@@ -863,10 +878,15 @@ __global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict_
             }
         }
     }
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // one wave: order its own global accesses (no L2 write-back)
     if (c.check_ori) {  // every accept is in its bin, stolen ones too (:482); ComputeThreeMaxima (:1601-1642)
-        for (int q = lane; q < c.nq; q += 64)
-            if (c.res[2 * q] >= 0) atomicAdd(&s_hist[c.res[2 * q + 1]], 1);
+        for (int q = lane; q < c.nq; q += 64) {
+            const int f = c.res[2 * q];
+            if (f < 0) continue;
+            const int bin = rot_bin(c.q[q].angle, c.angle[f]);
+            c.res[2 * q + 1] = bin;
+            atomicAdd(&s_hist[bin], 1);
+        }
         wave_lds_sync();
         int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;
         for (int i = 0; i < 30; i++) {
