@@ -2106,7 +2106,7 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     const size_t in_bytes = cv.off;
     const size_t o_nm = cv.take(4 * nout + 4);  // nmatches, then match[nout]
     const size_t o_gs = cv.take(ce ? 0 : 4 * (kGridCols * kGridRows + 1)), o_gi = cv.take(2 * nF),
-                 o_scan = cv.take(32 * nq), o_scnt = cv.take(4 * nq), o_res = cv.take(8 * nq);
+                 o_scan = cv.take(8 * (size_t)proj_topk() * nq), o_scnt = cv.take(4 * nq), o_res = cv.take(8 * nq);
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
     // results: written by the kernels straight into the pinned buffer after the inputs (ProjCall::host_out)
     const size_t n_host = std::max(nout + 1, nq);

@@ -497,7 +497,12 @@ __device__ __forceinline__ int proj_scan(const ProjCall& c, const ProjQuery& q, 
     return ncand;
 }
 
-constexpr int kProjTopK = 4;
+#ifndef ORBX_PROJ_TOPK
+#define ORBX_PROJ_TOPK 4  // candidate keys kept per query by the scan (A/B: more keys = fewer whole-wave rescans)
+#endif
+constexpr int kProjTopK = ORBX_PROJ_TOPK;
+static_assert(kProjTopK >= 2 && kProjTopK <= 16, "the scan writes one key per lane of a 16-lane query group");
+int proj_topk() { return kProjTopK; }
 
 /* one result of a per-call host API launch: a single 64-bit store of (value, call seq) to pinned host memory;
  * the host takes an entry once it carries its call's seq, whatever order the stores land in */
@@ -598,6 +603,35 @@ __device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:1
 constexpr int kProjMaxFeatures = 65536;
 constexpr int kClaimTab = 2048;  // claim table of one resolve round (power of 2)
 
+/* rotation bins of every accepted query (res[2q] >= 0: bin of q.angle - angle[res[2q]]) into res[2q+1] and the
+ * histogram; kQU queries per lane with their loads in flight together (a per-query loop would pay two
+ * dependent global loads per query) */
+constexpr int kQU = 4;
+__device__ __forceinline__ void rot_bins(const ProjCall& c, int lane, int* hist) {
+    const int nq = c.nq;
+    for (int q0 = 0; q0 < nq; q0 += 64 * kQU) {
+        int f[kQU];
+        float qa[kQU], fa[kQU];
+#pragma unroll
+        for (int u = 0; u < kQU; u++) {
+            const int qc = min(q0 + 64 * u + lane, nq - 1);
+            f[u] = c.res[2 * qc];
+            qa[u] = c.q[qc].angle;
+        }
+#pragma unroll
+        for (int u = 0; u < kQU; u++) fa[u] = c.angle[max(f[u], 0)];
+#pragma unroll
+        for (int u = 0; u < kQU; u++) {
+            const int q = q0 + 64 * u + lane;
+            if (q < nq && f[u] >= 0) {
+                const int bin = rot_bin(qa[u], fa[u]);
+                c.res[2 * q + 1] = bin;
+                atomicAdd(&hist[bin], 1);
+            }
+        }
+    }
+}
+
 /* One wave per call. Chunks of 64 queries (lane j = query base+j) are evaluated in registers: each
  * lane's best / second are the first two entries of its top-K list not occupied in the live bitmap
  * (claims only remove candidates, so the remaining order is unchanged). Lanes commit in order up to
@@ -605,26 +639,44 @@ constexpr int kClaimTab = 2048;  // claim table of one resolve round (power of 2
  * uncommitted lane of the chunk; that lane is re-filtered in the next round against the bitmap that
  * now holds those claims. A lane whose filtered list ran out while the list was truncated (more than
  * K candidates) is re-scanned by the whole wave against the bitmap. */
+#ifndef ORBX_RESOLVE_PROF
+#define ORBX_RESOLVE_PROF 0  // experiment only: call 0 prints its phase times (wall clock, 10 ns) and round counts
+#endif
 __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict__ calls) {
+#if ORBX_RESOLVE_PROF
+    const unsigned long long tp0 = wall_clock64();
+    int prof_rounds = 0, prof_rescans = 0;
+#endif
     __shared__ uint32_t s_occ[kProjMaxFeatures / 32];
     __shared__ int s_claim[kClaimTab];
     __shared__ int s_hist[32];
     const ProjCall& c = calls[blockIdx.x];
     const int lane = threadIdx.x;
-    for (int i = lane; i < (c.n + 31) / 32; i += 64) {
-        uint32_t w = 0;
-        if (c.occ0)
-            for (int k = 0; k < 32; k++) {
-                const int f = 32 * i + k;
-                if (f < c.n && c.occ0[f]) w |= 1u << k;
+    // the occupancy bitmap by ballots over coalesced byte loads, 4 loads per lane in flight (a per-lane loop
+    // over 32 bytes costs one dependent load each)
+    {
+        const int n = c.n;
+        const uint8_t* occ0 = c.occ0;
+        for (int b0 = 0; b0 < n; b0 += 256) {
+            int v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = occ0 ? occ0[min(b0 + 64 * u + lane, max(n - 1, 0))] : 0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int f = b0 + 64 * u + lane;
+                const unsigned long long m = __ballot(f < n && v[u] != 0);
+                if (lane < 2 && f - lane < n) s_occ[(b0 + 64 * u) / 32 + lane] = (uint32_t)(m >> (32 * lane));
             }
-        s_occ[i] = w;
+        }
     }
     for (int i = lane; i < c.n; i += 64) c.match[i] = -1;
     if (lane < 32) s_hist[lane] = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // one wave: order its own global accesses (no L2 write-back)
     wave_lds_sync();
     auto occ_get = [](int i) { return (s_occ[i >> 5] >> (i & 31)) & 1u; };
+#if ORBX_RESOLVE_PROF
+    const unsigned long long tp1 = wall_clock64();
+#endif
     const int need = c.ratio ? 2 : 1;  // list entries that decide the result
     for (int i = lane; i < kClaimTab; i += 64) s_claim[i] = 64;
     wave_lds_sync();
@@ -660,6 +712,9 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
         if (base + 64 < c.nq) load_chunk(base + 64, ntop, nncand, nflags, nsrc);
         int done = 0;  // lanes < done are committed
         while (done < 64 && base + done < c.nq) {
+#if ORBX_RESOLVE_PROF
+            prof_rounds++;
+#endif
             const bool act = in && lane >= done;
             unsigned long long b = kNoKey, s = kNoKey;
             int found = 0;
@@ -698,6 +753,9 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
             }
             wave_lds_sync();
             if (d < 64 && __shfl((int)rescan, d)) {  // whole-wave re-scan of query base+d
+#if ORBX_RESOLVE_PROF
+                prof_rescans++;
+#endif
                 const int qd = base + d;
                 const ProjQuery q = c.q[qd];
                 const uint4* qp = (const uint4*)(c.qdesc + (long long)qd * 32);
@@ -723,16 +781,13 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // one wave: order its own global accesses (no L2 write-back)
+#if ORBX_RESOLVE_PROF
+    const unsigned long long tp2 = wall_clock64();
+#endif
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) nacc += __shfl_xor(nacc, o);
     if (c.check_ori) {  // rotation consistency (ORBmatcher.cc:1437-1467)
-        for (int q = lane; q < c.nq; q += 64) {
-            const int f = c.res[2 * q];
-            if (f < 0) continue;
-            const int bin = rot_bin(c.q[q].angle, c.angle[f]);
-            c.res[2 * q + 1] = bin;
-            atomicAdd(&s_hist[bin], 1);
-        }
+        rot_bins(c, lane, s_hist);
         wave_lds_sync();
         int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;  // ComputeThreeMaxima (:1601-1642)
         for (int i = 0; i < 30; i++) {
@@ -753,21 +808,36 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
             ind3 = -1;
         }
         int removed = 0;
-        for (int q = lane; q < c.nq; q += 64) {
-            const int f = c.res[2 * q];
-            if (f < 0) continue;
-            const int bin = c.res[2 * q + 1];
-            if (bin != ind1 && bin != ind2 && bin != ind3) {
-                c.match[f] = -2;
-                removed++;
+        for (int q0 = 0; q0 < c.nq; q0 += 64 * kQU) {  // kQU queries per lane, their loads in flight together
+            int f[kQU], b[kQU];
+#pragma unroll
+            for (int u = 0; u < kQU; u++) {
+                const int qc = min(q0 + 64 * u + lane, c.nq - 1);
+                f[u] = c.res[2 * qc];
+                b[u] = c.res[2 * qc + 1];
             }
+#pragma unroll
+            for (int u = 0; u < kQU; u++)
+                if (q0 + 64 * u + lane < c.nq && f[u] >= 0 && b[u] != ind1 && b[u] != ind2 && b[u] != ind3) {
+                    c.match[f[u]] = -2;
+                    removed++;
+                }
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) removed += __shfl_xor(removed, o);
         nacc -= removed;
     }
     if (lane == 0) *c.nmatches = nacc;
+#if ORBX_RESOLVE_PROF
+    const unsigned long long tp3 = wall_clock64();
+#endif
     if (c.host_out) host_put_matches(c, c.match, c.n, nacc, lane);
+#if ORBX_RESOLVE_PROF
+    const unsigned long long tp4 = wall_clock64();
+    if (blockIdx.x == 0 && lane == 0)
+        printf("RESOLVE_PROF nq %d init %llu chunks %llu ori %llu out %llu (x10ns) rounds %d rescans %d\n", c.nq,
+               tp1 - tp0, tp2 - tp1, tp3 - tp2, tp4 - tp3, prof_rounds, prof_rescans);
+#endif
 }
 
 /* ============================ SearchForInitialization ============================ */
@@ -880,13 +950,7 @@ __global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict_
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // one wave: order its own global accesses (no L2 write-back)
     if (c.check_ori) {  // every accept is in its bin, stolen ones too (:482); ComputeThreeMaxima (:1601-1642)
-        for (int q = lane; q < c.nq; q += 64) {
-            const int f = c.res[2 * q];
-            if (f < 0) continue;
-            const int bin = rot_bin(c.q[q].angle, c.angle[f]);
-            c.res[2 * q + 1] = bin;
-            atomicAdd(&s_hist[bin], 1);
-        }
+        rot_bins(c, lane, s_hist);
         wave_lds_sync();
         int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;
         for (int i = 0; i < 30; i++) {
@@ -906,10 +970,19 @@ __global__ __launch_bounds__(64) void k_init_resolve(const ProjCall* __restrict_
         } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
             ind3 = -1;
         }
-        for (int q = lane; q < c.nq; q += 64) {  // :497-510 (a stolen i1 is already -1)
-            if (c.res[2 * q] < 0) continue;
-            const int bin = c.res[2 * q + 1];
-            if (bin != ind1 && bin != ind2 && bin != ind3) s_v12[c.q[q].src] = -1;
+        for (int q0 = 0; q0 < c.nq; q0 += 64 * kQU) {  // :497-510 (a stolen i1 is already -1)
+            int f[kQU], b[kQU], src[kQU];
+#pragma unroll
+            for (int u = 0; u < kQU; u++) {
+                const int qc = min(q0 + 64 * u + lane, c.nq - 1);
+                f[u] = c.res[2 * qc];
+                b[u] = c.res[2 * qc + 1];
+                src[u] = c.q[qc].src;
+            }
+#pragma unroll
+            for (int u = 0; u < kQU; u++)
+                if (q0 + 64 * u + lane < c.nq && f[u] >= 0 && b[u] != ind1 && b[u] != ind2 && b[u] != ind3)
+                    s_v12[src[u]] = -1;
         }
         wave_lds_sync();
     }

@@ -59,6 +59,7 @@ hipError_t launch_tri_nodes(const DevView& v1, const DevView& v2, const NodeTask
 hipError_t launch_bow(const DevView& vq, const DevView& vc, const NodeTask* tasks, int ntasks, int max_nc,
                       float nnratio, int mode, const CallTail& tail, hipStream_t st);
 hipError_t launch_bow_small(const BowSmall& a, hipStream_t st);
+int proj_topk();  // candidate keys per query of k_proj_scan (ProjCall::scan holds proj_topk() x nq keys)
 hipError_t launch_tri_small(const TriSmall& a, hipStream_t st);
 hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* angB, int swap, int32_t* nout,
                              hipStream_t st);
