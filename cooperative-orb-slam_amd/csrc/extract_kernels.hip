@@ -391,6 +391,7 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
     __shared__ __align__(16) uint8_t s_blur[BLUR ? NT / 64 : 1][7][kBlurSeg];
     const int f = blockIdx.x / kPyrBands, band = blockIdx.x - f * kPyrBands, tid = threadIdx.x;
     uint8_t* P = pyr + (long long)f * ep.pyr_frame_bytes;
+    if (ORBX_PRIO_PYR > 0) __builtin_amdgcn_s_setprio(ORBX_PRIO_PYR);  // A/B knob: issue priority of the level chain
     auto blur_level = [&](int lb) {
         if constexpr (BLUR) {
             const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -1002,6 +1003,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                                                 int* __restrict__ lvcnt, uint8_t* __restrict__ gscratch,
                                                 long long gscratch_frame_bytes, int NC, int KL,
                                                 int* __restrict__ err) {
+    if (ORBX_PRIO_OCT > 0) __builtin_amdgcn_s_setprio(ORBX_PRIO_OCT);  // A/B knob: issue priority of the barrier chain
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int red[8];
     __shared__ int sh_size, sh_jstar, sh_tc, sh_nexp, sh_ndiv;
@@ -1551,6 +1553,9 @@ constexpr int kDescKps = 4 * kDescWaves;            // keypoints per workgroup
 #endif
 constexpr bool kDescPatGlobal = ORBX_DESC_PAT_GLOBAL != 0;
 
+/* kEvenPitch: every row pitch is even (levels >= 1 always are; level 0 when the caller's pitch is), so the IC rows a
+ * lane reads (2 rows apart) share one misalignment and their addresses are one running 32-bit offset */
+template <bool kEvenPitch>
 __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                   const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   ExtractParams ep, const LevelDesc* __restrict__ levels,
@@ -1638,14 +1643,14 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
     // one memory round trip: the IC_Angle rows of the level image and the blurred 37x37 patch
     // around the keypoint (staged in LDS for the 512 rBRIEF samples)
     const int g4 = ln & 7, r = ln >> 3;
-    const int off0 = (y + r - 15) * pitch + x - 15 + 4 * g4;
+    const int off0 = (y + r - 15) * pitch + x - 15 + 4 * g4;  // >= 0: keypoints lie in [19, dim - 19)
     const uint32_t mis = ((uint32_t)(uintptr_t)img + (uint32_t)off0) & 3u;
-    const uint32_t dmis = (uint32_t)(2 * pitch) & 3u;  // misalignment step between a lane's rows
+    const uint32_t dmis = kEvenPitch ? 0u : (uint32_t)(2 * pitch) & 3u;  // misalignment step between a lane's rows
     uint2 wv[16];
 #pragma unroll
     for (int p = 0; p < 16; p++) {
         const uint32_t al = (mis + (uint32_t)p * dmis) & 3u;
-        wv[p] = *(const uint2*)(img + (off0 + 2 * p * pitch - (int)al));
+        wv[p] = *(const uint2*)(img + ((uint32_t)off0 + (uint32_t)(2 * p * pitch) - al));
     }
     // patch: 37 rows x 5 aligned 8-byte words (row start rounded down to 4; patch column 0 =
     // image column x-18-pmis[row])
@@ -1921,8 +1926,12 @@ hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0,
                            const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,
                            int* out_counts, int kp_stride, const int* ptab, int nframes, hipStream_t st) {
     dim3 grid(((ep.kp_per_frame + kDescKps - 1) / kDescKps) * nframes);
-    hipLaunchKernelGGL(k_describe, grid, dim3(64 * kDescWaves), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels, lvkey,
-                       lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
+    if ((pitch0 & 1) == 0)
+        hipLaunchKernelGGL(k_describe<true>, grid, dim3(64 * kDescWaves), 0, st, frames, fstride, pitch0, pyr, blur, ep,
+                           levels, lvkey, lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
+    else
+        hipLaunchKernelGGL(k_describe<false>, grid, dim3(64 * kDescWaves), 0, st, frames, fstride, pitch0, pyr, blur, ep,
+                           levels, lvkey, lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
     return hipGetLastError();
 }
 

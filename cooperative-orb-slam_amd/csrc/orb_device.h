@@ -49,6 +49,12 @@ constexpr int kPyrThreadsMax = 1024;
 #endif
 constexpr bool kPyrFlat = ORBX_PYR_FLAT != 0;  // k_pyramid_frames: (row, column group) items dealt round-robin
 constexpr bool kPyrFlatLds = ORBX_PYR_FLAT == 1;  // ... with the column-group table staged in LDS (2: read via L1)
+#ifndef ORBX_PRIO_PYR
+#define ORBX_PRIO_PYR 0  // A/B knob: s_setprio of the k_pyramid_frames waves (0 = default priority)
+#endif
+#ifndef ORBX_PRIO_OCT
+#define ORBX_PRIO_OCT 0  // A/B knob: s_setprio of the k_octree waves
+#endif
 #ifndef ORBX_PYR_BANDS
 #define ORBX_PYR_BANDS 1
 #endif

@@ -11,7 +11,7 @@ for v in "$@"; do
   if [ $rc -ne 0 ]; then exit $rc; fi  # a variant with broken parity is not timed
 done
 summ='import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); s=d["stage_ms_per_step"]; print("%.0f" % d["value"], " ".join("%s=%.3f" % (k, s[k]) for k in ("pyramid","fast_cells","octree","blur","describe","match")))'
-for r in 1 2 3; do
+for r in $(seq 1 ${AB_ROUNDS:-3}); do
   for v in "$@"; do
     out=$(ORBAMD_LIB_VARIANT=$v timeout -k 10 120 python bench.py --sustain 0 --no-cpu --steps 30 ${AB_ARGS} | python -c "$summ") || exit $?
     echo "r$r $v overlapped: $out"
