@@ -502,51 +502,79 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
         const int x0 = 4 * xg;
         const bool tail = x0 + 3 >= lv.simd_end;
         __syncthreads();
-        if (ry < R) {
-            for (int y0 = lo + ry; y0 < hi; y0 += U * R) {
-                uint32_t w[U][2][3];
-                int4 rr[U];
+        // one pass = U output rows of this thread's column group: the 2 x 3 source dwords of each (rows clamped,
+        // so every load is valid and unconditional), then the taps
+        struct PassBuf {
+            uint32_t w[U][2][3];
+            int4 rr[U];
+        };
+        auto load_pass = [&](int y0, PassBuf& pb) {
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    rr[u] = s_rt[min(y0 + u * R, hi - 1) - lo];
+            for (int u = 0; u < U; u++) pb.rr[u] = s_rt[min(y0 + u * R, hi - 1) - lo];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const unsigned off = (unsigned)((q ? pb.rr[u].y : pb.rr[u].x) * sp + A);
+                    const uint2 lo2 = *(const uint2*)(src + off);
+                    pb.w[u][q][0] = lo2.x;
+                    pb.w[u][q][1] = lo2.y;
+                    pb.w[u][q][2] =
+                        *(const uint32_t*)(src + min(off + 8u, (unsigned)((q ? pb.rr[u].y : pb.rr[u].x) * sp + cg.pad[0])));
                 }
+            }
+        };
+        auto compute_pass = [&](int y0, const PassBuf& pb) {
 #pragma unroll
-                for (int u = 0; u < U; u++) {
+            for (int u = 0; u < U; u++) {
+                const int y = y0 + u * R;
+                if (y >= hi) break;
+                const short2 b = __builtin_bit_cast(short2, pb.rr[u].z);
+                int h[2][4];
 #pragma unroll
-                    for (int q = 0; q < 2; q++) {
-                        const unsigned off = (unsigned)((q ? rr[u].y : rr[u].x) * sp + A);
-                        const uint2 lo2 = *(const uint2*)(src + off);
-                        w[u][q][0] = lo2.x;
-                        w[u][q][1] = lo2.y;
-                        w[u][q][2] = *(const uint32_t*)(src + min(off + 8u, (unsigned)((q ? rr[u].y : rr[u].x) * sp + cg.pad[0])));
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int y = y0 + u * R;
-                    if (y >= hi) break;
-                    const short2 b = __builtin_bit_cast(short2, rr[u].z);
-                    int h[2][4];
-#pragma unroll
-                    for (int q = 0; q < 2; q++) {
-                        const uint32_t lw = __builtin_amdgcn_alignbyte(w[u][q][1], w[u][q][0], k);
-                        const uint32_t hw = __builtin_amdgcn_alignbyte(w[u][q][2], w[u][q][1], k);
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const uint32_t pr = __builtin_amdgcn_perm(hw, lw, cg.sel[i]);
-                            h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
-                                                             __builtin_bit_cast(short2v, cg.alpha[i]), 0, false);
-                        }
-                    }
-                    uint32_t packed = 0;
+                for (int q = 0; q < 2; q++) {
+                    const uint32_t lw = __builtin_amdgcn_alignbyte(pb.w[u][q][1], pb.w[u][q][0], k);
+                    const uint32_t hw = __builtin_amdgcn_alignbyte(pb.w[u][q][2], pb.w[u][q][1], k);
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
-                        // taps < 2^20, weights <= 2048: 24-bit multiplies (full rate) are exact
-                        int v = ((__mul24(h[0][i] >> 4, (int)b.x) >> 16) + (__mul24(h[1][i] >> 4, (int)b.y) >> 16) + 2) >> 2;
-                        if (tail && x0 + i >= lv.simd_end) v = (__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
-                        packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
+                        const uint32_t pr = __builtin_amdgcn_perm(hw, lw, cg.sel[i]);
+                        h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
+                                                         __builtin_bit_cast(short2v, cg.alpha[i]), 0, false);
                     }
-                    if (xg < gw) *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
+                }
+                uint32_t packed = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    // taps < 2^20, weights <= 2048: 24-bit multiplies (full rate) are exact
+                    int v = ((__mul24(h[0][i] >> 4, (int)b.x) >> 16) + (__mul24(h[1][i] >> 4, (int)b.y) >> 16) + 2) >> 2;
+                    if (tail && x0 + i >= lv.simd_end) v = (__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
+                    packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
+                }
+                if (xg < gw) *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
+            }
+        };
+        if (ry < R) {
+            if (kPyrPipe) {
+                // software pipeline (ORBX_PYR_PIPE): the next pass's loads are issued before this pass's taps, so a
+                // thread always has one pass of rows in flight (two buffers, alternating; no register copies)
+                PassBuf pa, pb;
+                int y0 = lo + ry;
+                load_pass(y0, pa);
+                while (y0 < hi) {
+                    const int y1 = y0 + U * R;
+                    load_pass(y1, pb);  // clamped rows: harmless past the level's end
+                    compute_pass(y0, pa);
+                    if (y1 >= hi) break;
+                    const int y2 = y1 + U * R;
+                    load_pass(y2, pa);
+                    compute_pass(y1, pb);
+                    y0 = y2;
+                }
+            } else {
+                for (int y0 = lo + ry; y0 < hi; y0 += U * R) {
+                    PassBuf pb;
+                    load_pass(y0, pb);
+                    compute_pass(y0, pb);
                 }
             }
         }
@@ -702,6 +730,15 @@ __device__ __forceinline__ bool fast_pretest(const uint8_t* p, int P, int t) {
     return (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
 }
 
+#ifndef ORBX_FAST_PRETEST2
+#define ORBX_FAST_PRETEST2 0  // A/B knob: k_fast_cells2 pretests two row passes per loop iteration
+#endif
+constexpr bool kFastPretest2 = ORBX_FAST_PRETEST2 != 0;
+#ifndef ORBX_FAST_S2
+#define ORBX_FAST_S2 0  // A/B knob: k_fast_cells2 computes the strength of two candidate chunks per loop iteration
+#endif
+constexpr bool kFastStrength2 = ORBX_FAST_S2 != 0;
+
 /* LDS bytes per wave of k_fast_cells2: ROI + S map (RP x RH each) + candidate list (u16 per
  * band pixel; a band is at most (RP-6) x (RH-6)) + 64 per-lane dummy slots of the compaction */
 __host__ __device__ inline int fast_wave_lds(int RP, int RH) {
@@ -808,7 +845,8 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
                 const uint32_t RB = (t & 1) ? 0x01010101u : 0u, RD = RB ^ 0x01010101u;
                 const uint32_t CB = (uint32_t)(255 - min((t + 256 + (t & 1)) >> 1, 255)) * 0x01010101u;
                 const uint32_t CD = (uint32_t)(255 - ((256 - t - (t & 1)) >> 1)) * 0x01010101u;
-                for (int r0 = 0; r0 < bh; r0 += rpc) {
+                // candidate bits of the row pass starting at band row r0 (bit 8 i + 7: pixel i of this lane's dword)
+                auto pretest = [&](int r0) -> uint32_t {
                     const int rr = 3 + r0 + lr;
                     const int rrc = min(rr, bh + 2);
                     const uint8_t* q = roi + rrc * RP + 4 * j;
@@ -831,18 +869,33 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
                     // candidate iff two cyclically adjacent cardinals are both brighter ((b0|b8)&(b4|b12)) or
                     // both darker (NOT((n0&n8)|(n4&n12)))
                     const uint32_t cand = ((b0 | b8) & (b4 | b12)) | ~((n0 & n8) | (n4 & n12));
-                    const uint32_t k = (lane_ok && rr < 3 + bh) ? (cand & colm) : 0u;  // bit 8 i + 7: pixel i
-                    // sparse ordered record of this dword (lanes with a candidate, ~1 in 5): row-major =
-                    // lane order within a row pass; record = candidate bits | group j | ROI row << 8
-                    // (j, rr < 128 fit the 7 free bits of bytes 0 / 1)
+                    // mask, not a branch: the loads of both row passes stay unconditional and in flight together
+                    const uint32_t live = 0u - (uint32_t)(lane_ok && rr < 3 + bh);
+                    return cand & colm & live;
+                };
+                // sparse ordered record of this dword (lanes with a candidate, ~1 in 5): row-major = lane order
+                // within a row pass; record = candidate bits | group j | ROI row << 8 (j, rr < 128 fit the 7 free
+                // bits of bytes 0 / 1)
+                auto record = [&](uint32_t k, int r0) {
                     const unsigned long long Bk = __ballot(k != 0u);
                     if (k != 0u) {
                         const int at = nrec + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(Bk >> 32),
                                                                               __builtin_amdgcn_mbcnt_lo((unsigned)Bk, 0));
-                        rec[at] = k | (uint32_t)j | ((uint32_t)rr << 8);
+                        rec[at] = k | (uint32_t)j | ((uint32_t)(3 + r0 + lr) << 8);
                     }
                     nrec += __popcll(Bk);
+                };
+                int r0 = 0;
+                if (kFastPretest2) {
+                    // two row passes per iteration: both passes' LDS reads are issued before either's record
+                    // store (the store may alias the ROI for the compiler), so their latencies overlap
+                    for (; r0 + rpc < bh; r0 += 2 * rpc) {
+                        const uint32_t ka = pretest(r0), kb = pretest(r0 + rpc);
+                        record(ka, r0);
+                        record(kb, r0 + rpc);
+                    }
                 }
+                for (; r0 < bh; r0 += rpc) record(pretest(r0), r0);
                 wave_sync();
                 // expand the records into the candidate list (order kept: records in order, pixels of a
                 // record ascending); the record area is zeroed behind, so str is the S map again (zero
@@ -877,7 +930,23 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
             // registers for the NMS pass: one dependent LDS read fewer
             const int e0 = lane < ncand ? (int)clist[lane] : 0;
             int s0 = 0;
-            for (int i0 = 0; i0 < ncand; i0 += 64) {
+            int ibeg = 0;
+            if (kFastStrength2) {
+                // two 64-candidate chunks per iteration: every list and ring read of both is issued before either
+                // chunk's S-map store; a lane past the list computes S at a dummy in-band centre (row 3, col 3)
+                for (; ibeg + 64 < ncand; ibeg += 128) {
+                    const int ia = ibeg + lane, ib = ibeg + 64 + lane;
+                    const bool va = ia < ncand, vb = ib < ncand;
+                    const int ea = ibeg == 0 ? e0 : (va ? (int)clist[ia] : 0x303);
+                    const int eb = vb ? (int)clist[ib] : 0x303;
+                    const int oa = (ea >> 8) * RP + (ea & 0xFF), ob = (eb >> 8) * RP + (eb & 0xFF);
+                    const int Sa = fast_strength_h2(roi, oa, RP), Sb = fast_strength_h2(roi, ob, RP);
+                    if (va && Sa > t) str[oa] = (uint8_t)Sa;
+                    if (vb && Sb > t) str[ob] = (uint8_t)Sb;
+                    if (ibeg == 0) s0 = va && Sa > t ? Sa : 0;
+                }
+            }
+            for (int i0 = ibeg; i0 < ncand; i0 += 64) {
                 const int i = i0 + lane;
                 if (i < ncand) {
                     const int e = i0 == 0 ? e0 : (int)clist[i];

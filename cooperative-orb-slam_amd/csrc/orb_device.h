@@ -55,6 +55,10 @@ constexpr bool kPyrFlatLds = ORBX_PYR_FLAT == 1;  // ... with the column-group t
 #ifndef ORBX_PRIO_OCT
 #define ORBX_PRIO_OCT 0  // A/B knob: s_setprio of the k_octree waves
 #endif
+#ifndef ORBX_PYR_PIPE
+#define ORBX_PYR_PIPE 0  // A/B knob: k_pyramid_frames issues the next pass's loads before the current pass's taps
+#endif
+constexpr bool kPyrPipe = ORBX_PYR_PIPE != 0;
 #ifndef ORBX_PYR_BANDS
 #define ORBX_PYR_BANDS 1
 #endif
