@@ -240,9 +240,11 @@ def main():
     ap.add_argument("--ingest-streams", type=int, default=4, help="copy streams of the ingest leg (<= --pipes)")
     ap.add_argument("--ingest-steps", type=int, default=100,
                     help="steps of the ingest leg (frames uploaded from pinned host memory each step; 0: skip)")
-    ap.add_argument("--stagger", choices=("each", "once", "none"), default="each",
+    ap.add_argument("--stagger", choices=("each", "once", "none", "every4", "every8", "every16", "pyr_each", "pyr_every8"),
+                    default="every8",
                     help="graph p starts extracting after graph p-1's extraction: every step / only in the "
-                         "first step of a run (the phase offset then persists) / never")
+                         "first step of a run (the phase offset then persists) / never / in the first step and every "
+                         "K-th step after it")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -488,6 +490,7 @@ def main():
                                                  "SearchForTriangulation vs previous frame + per-step keyframe-slot "
                                                  "all-gather & cross-agent SearchForTriangulation",
                        "config": args.config, "frames_per_step_per_gpu": B, "graphs_per_gpu": P,
+                       "graph_stagger": args.stagger,
                        "parallelism": "agent-per-gpu x%d" % world},
             "bit_exact": bool(ok_all) if check is not None else None,
             "checked_frames": check["checked_frames"] if check else 0,

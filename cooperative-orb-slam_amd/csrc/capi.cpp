@@ -409,6 +409,7 @@ struct orbx_handle {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
     hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_blur = nullptr;
+    hipEvent_t user_ev_pyr = nullptr;  // orbx_set_pyramid_event (caller-owned)
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
     // host-path staging
@@ -602,6 +603,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         launch_pyramid(h, d_frames, fstride, pitch, nframes, st, blur_in_pyr ? h->blur.as<uint8_t>() : nullptr, &fused))
         return ORBX_EDEVICE;
     if (prof_mark(h, 0, 1, st)) return ORBX_EDEVICE;
+    if (!host_call && h->user_ev_pyr) HIPR(hipEventRecord(h->user_ev_pyr, st));
     auto blur = [&](hipStream_t bs) -> int {
         if (prof_mark(h, 3, 0, bs)) return ORBX_EDEVICE;
         if (!fused && !skip_warm(8) && !(h->skip_mask & 8))
@@ -725,6 +727,12 @@ int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, 
     if (!d_in || !d_sin || !d_cos || n < 0) return ORBX_EARG;
     if (n == 0) return 0;
     HIPR(launch_sincos_selftest(d_in, d_sin, d_cos, n, (hipStream_t)stream));
+    return 0;
+}
+
+int orbx_set_pyramid_event(orbx_handle* h, void* event) {
+    if (!h) return ORBX_EARG;
+    h->user_ev_pyr = (hipEvent_t)event;
     return 0;
 }
 

@@ -103,6 +103,7 @@ SIGNATURES = {
     "orbx_get_scale_tables": (_I, [_P, _P, _P, _P, _P]),
     "orbx_get_feature_split": (_I, [_P, _P, _P]),
     "orbx_compute_scale_tables": (_I, [C.POINTER(OrbxParams), _P, _P, _P, _P]),
+    "orbx_set_pyramid_event": (_I, [_P, _P]),
     "orbx_debug_skip_stages": (_I, [_P, _I]),
     "orbx_debug_raise_error": (_I, [_P, _I, _P]),
     "orbm_create": (_I, [_I, C.POINTER(_P)]),

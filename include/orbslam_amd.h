@@ -637,6 +637,12 @@ int orbx_synth_frames_shifted(int agent, int t0, int count, int width, int heigh
 int orbx_profile_enable(orbx_handle* h, int on);
 int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls);
 
+/* Schedule hook: every subsequent batched extraction of this handle records `event` (a hipEvent_t
+ * created by the caller; NULL = off) on its stream right after the pyramid launch, so another stream
+ * can start its own work once this batch's pyramid is done (bench schedules that stagger concurrent
+ * extraction graphs by pyramid rather than by whole extraction). */
+int orbx_set_pyramid_event(orbx_handle* h, void* event);
+
 /* Test hook: the stages in `mask` (bit k of {pyramid, fast_cells, octree, blur, describe}) are not
  * launched by subsequent batched extractions of this handle (0 = every stage runs, the default). A
  * skipped stage leaves its buffers as the previous call left them; the tests use it to prove that

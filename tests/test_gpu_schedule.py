@@ -14,15 +14,16 @@ from check_schedule import check_schedule
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("W,H,nf,B,P", [(640, 480, 1000, 1024, 4), (752, 480, 1200, 128, 2),
-                                         (1241, 376, 2000, 128, 2)])
-def test_bench_schedule_bit_exact(W, H, nf, B, P):
+@pytest.mark.parametrize("W,H,nf,B,P,stagger", [(640, 480, 1000, 1024, 4, "every8"), (640, 480, 1000, 1024, 4, "each"),
+                                                 (752, 480, 1200, 128, 2, "every8"), (1241, 376, 2000, 128, 2, "every8")])
+def test_bench_schedule_bit_exact(W, H, nf, B, P, stagger):
     torch = pytest.importorskip("torch")
-    from orbamd.agent import AgentSchedule
+    from orbamd.agent import AgentSchedule, DEFAULT_STAGGER
+    assert DEFAULT_STAGGER == "every8"  # bench.py's default (--stagger)
     frames = orbamd.synth_frames(0, 0, B, W, H)
-    sched = AgentSchedule(torch, frames, W, H, P, device=0, nfeatures=nf)
-    sched.step()                   # warmup (the first step also builds the geometry tables)
-    sched.step(first=False)        # the checked step, staggered exactly as in bench.py
+    sched = AgentSchedule(torch, frames, W, H, P, device=0, nfeatures=nf, stagger=stagger)
+    sched.step()                   # warmup (the first step also builds the geometry tables; staggered)
+    sched.step(first=False)        # the checked step: free-running under every8, staggered under each
     torch.cuda.synchronize()
     sched.check_errors()
     sub = B // P
