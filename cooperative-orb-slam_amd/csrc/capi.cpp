@@ -408,7 +408,7 @@ struct orbx_handle {
     int max_w = 0, max_h = 0, max_batch = 1;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
-    hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_blur = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_blur = nullptr, ev_fast0 = nullptr;
     hipEvent_t user_ev_pyr = nullptr;  // orbx_set_pyramid_event (caller-owned)
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
@@ -553,7 +553,7 @@ static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstrid
  * barrier/latency-bound); describe joins both. (The reference blurs only levels that kept
  * keypoints (ORBextractor.cc:1081); blurring every level changes no output, since describe
  * reads only levels with keypoints.) ORBX_SCHED=split also starts FAST on level 0 (which needs
- * only the input) beside the pyramid; ORBX_SCHED=serial runs everything on `st` (A/B only), and
+ * only the input) beside the pyramid, and the octree waits for it [ev_fast0]; ORBX_SCHED=serial runs everything on `st` (A/B only), and
  * ORBX_SCHED=serial_blur_first does so with the blur right after the pyramid.
  * With stage profiling on, everything runs in order on `st` between timing events. */
 #ifndef ORBX_ERR_STICKY
@@ -591,6 +591,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         HIPR(hipEventRecord(h->ev_fork, st));
         HIPR(hipStreamWaitEvent(sd, h->ev_fork, 0));
         if (launch_fast(h, d_frames, fstride, pitch, 0, ncell0, nframes, sd)) return ORBX_EDEVICE;
+        HIPR(hipEventRecord(h->ev_fast0, sd));  // the octree (on st) reads level 0's cell keys
     }
     if (prof_mark(h, 0, 0, st)) return ORBX_EDEVICE;
     // the whole-frame pyramid may blur every level itself (ORBX_BLUR_IN_PYR); then no blur launch
@@ -622,6 +623,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     }
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
     if (!skip_warm(2) && !(h->skip_mask & 2) && launch_fast(h, d_frames, fstride, pitch, ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
+    if (split) HIPR(hipStreamWaitEvent(st, h->ev_fast0, 0));
     if (prof_mark(h, 1, 1, st) || prof_mark(h, 2, 0, st)) return ORBX_EDEVICE;
     if (!skip_warm(4) && !(h->skip_mask & 4)) HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                        h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
@@ -676,7 +678,8 @@ int orbx_create(const orbx_params* p, int device, int max_width, int max_height,
         hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_blur, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->ev_blur, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_fast0, hipEventDisableTiming) != hipSuccess) {
         orbx_destroy(h);
         return ORBX_EDEVICE;
     }
@@ -700,7 +703,7 @@ void orbx_destroy(orbx_handle* h) {
     h->geo.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     if (h->side) (void)hipStreamDestroy(h->side);
-    for (hipEvent_t e : {h->ev_fork, h->ev_pyr, h->ev_blur})
+    for (hipEvent_t e : {h->ev_fork, h->ev_pyr, h->ev_blur, h->ev_fast0})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
     if (h->gexec) (void)hipGraphExecDestroy(h->gexec);

@@ -62,3 +62,26 @@ def test_skipped_stage_fails_the_self_check(stage):
         else:
             assert res["bit_exact"]  # repeated frames hide it: why bench.py uses --pool 2
         sched.close()
+
+
+def test_split_schedule_bit_exact():
+    """ORBX_SCHED=split (an A/B switch: FAST on level 0 on the side stream beside the pyramid) in the bench
+    schedule: the octree must wait for the side stream's level-0 cell keys. The switch is read once per
+    process, so the schedule runs in a child process; every frame and match row is checked."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, json; sys.path[:0] = [%r, %r]; import torch, orbamd; "
+            "from orbamd.agent import AgentSchedule; from check_schedule import check_schedule; "
+            "W, H, B, P = 640, 480, 1024, 4; f = orbamd.synth_frames(0, 0, 2 * B, W, H); "
+            "s = AgentSchedule(torch, f, W, H, P, device=0, pool=2); "
+            "[s.step(first=i == 0) for i in range(3)]; torch.cuda.synchronize(); s.check_errors(); "
+            "r = check_schedule(s, f, samples=[(p, b) for p in range(P) for b in range(B // P)]); "
+            "print(json.dumps([bool(r['bit_exact']), r['checked_frames']]))"
+            % (os.path.join(root, "cooperative-orb-slam_amd"), os.path.join(root, "oracle")))
+    env = dict(os.environ, ORBX_SCHED="split")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1]) == [True, 1024]
