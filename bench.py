@@ -229,6 +229,10 @@ def main():
                     help="HIP stream priorities of the graphs: lead = the first half of the staggered graphs (the ones "
                          "in their latency-bound tail stages) high, lead1 = graph 0 only")
     ap.add_argument("--no-exchange", action="store_true")
+    ap.add_argument("--exchange-stream", choices=("auto", "own", "graph0"), default="auto",
+                    help="where the keyframe exchange runs: its own stream, off graph 0's critical path (only the pack + "
+                         "keyframe copy holds graph 0's next extraction), or in order on graph 0's stream; auto = own when "
+                         "a collective runs (N > 1, --dist), graph 0's at N = 1 (profiles/r03_exp_exchange_stream.log)")
     ap.add_argument("--roof-kernel", choices=("pyramid", "fast_cells", "octree", "blur", "describe"),
                     default="fast_cells", help="extraction kernel priced in `roofline` (timed live in the timed region)")
     ap.add_argument("--sustain", type=float, default=6.0,
@@ -288,11 +292,12 @@ def main():
 
     lo_prio, hi_prio = torch.cuda.Stream.priority_range()
     n_hi = {"none": 0, "lead": P // 2, "lead1": 1}[args.prio]
+    async_x = args.exchange_stream == "own" or (args.exchange_stream == "auto" and use_dist)
     sched = AgentSchedule(torch, frames_np, W, H, P, device=local, rank=rank, world=world,
                           allgather=allgather if use_dist else None,
                           stagger=args.stagger, exchange=not args.no_exchange,
                           priorities=[hi_prio if p < n_hi else lo_prio for p in range(P)], nfeatures=cfg["nfeatures"],
-                          pool=args.pool)
+                          pool=args.pool, async_exchange=async_x)
     pipes = sched.pipes
 
     for _ in range(args.warmup):
@@ -491,6 +496,7 @@ def main():
                                                  "all-gather & cross-agent SearchForTriangulation",
                        "config": args.config, "frames_per_step_per_gpu": B, "graphs_per_gpu": P,
                        "graph_stagger": args.stagger,
+                       "exchange_stream": "own" if async_x else "graph 0's",
                        "parallelism": "agent-per-gpu x%d" % world},
             "bit_exact": bool(ok_all) if check is not None else None,
             "checked_frames": check["checked_frames"] if check else 0,

@@ -29,7 +29,8 @@ DEFAULT_STAGGER = "every8"
 
 class AgentSchedule:
     def __init__(self, torch, frames_np, width, height, pipes, device=0, rank=0, world=1, allgather=None,
-                 stagger=DEFAULT_STAGGER, exchange=True, priorities=None, nfeatures=1000, pool=1):
+                 stagger=DEFAULT_STAGGER, exchange=True, priorities=None, nfeatures=1000, pool=1,
+                 async_exchange=False):
         """frames_np: uint8 [pool*B, H, W] host frames of this agent (copied to HBM once), batch r = frames
         [r*B, (r+1)*B); allgather(out, inp): all-gather of equal-sized device byte tensors across agents
         (None: no collective, only possible at world 1, where the slot is packed in place)."""
@@ -97,21 +98,49 @@ class AgentSchedule:
         self.meta = p0.meta(0, agent=rank)
         self.src0 = p0.kf_source(0)
         self.ag_events = []
+        # async_exchange: the exchange runs on its own stream once graph 0 has extracted the keyframe; it packs the
+        # slot and copies the keyframe's query arrays first, and only that (not the all-gather, whose latency at
+        # N > 1 includes waiting for the other agents, nor the slot match) holds graph 0's next extraction, which
+        # overwrites the keyframe's arrays. Without it the exchange runs in order on graph 0's stream (bench.py: own
+        # stream when a collective runs, graph 0's at N = 1, where it measured 0.9 % faster).
+        self.xstream = None
+        if async_exchange and exchange:
+            from .exchange import kf_source
+            self.xstream = torch.cuda.Stream(dev)
+            self.q_kps = torch.empty_like(p0.kps[0])
+            self.q_desc = torch.empty_like(p0.desc[0])
+            self.q_count = torch.empty_like(p0.counts[0:1])
+            self.q_src = kf_source(self.q_kps, self.q_desc, self.q_count)
+            self.kf_released = torch.cuda.Event()
+            self.kf_pending = False
 
     # ------------------------------------------------------------------------------------------
+    def exchange_stream(self):
+        """the stream the exchange runs on"""
+        return self.xstream if self.xstream is not None else self.streams[0]
+
     def exchange(self, ag=None):
         """this agent's keyframe -> slot -> all-gather -> cross-agent SearchForTriangulation"""
-        torch, st = self.torch, self.streams[0]
+        torch = self.torch
         p0 = self.pipes[0]
+        st = self.exchange_stream()
+        query = self.src0
         with torch.cuda.stream(st):
             p0.pack(0, self.my_slot, self.meta, st.cuda_stream, err=self.pack_err, src=self.src0)
+            if self.xstream is not None:
+                self.q_kps.copy_(p0.kps[0])
+                self.q_desc.copy_(p0.desc[0])
+                self.q_count.copy_(p0.counts[0:1])
+                self.kf_released.record(st)  # graph 0 may overwrite its buffers from here on
+                self.kf_pending = True
+                query = self.q_src
             if ag is not None:
                 ag[0].record(st)
             if self.collective:
                 self.allgather(self.all_slots, self.my_slot)
             if ag is not None:
                 ag[1].record(st)
-            p0.match_slots(0, self.all_slots, self.world, self.xmatch, self.xn, st.cuda_stream, query=self.src0)
+            p0.match_slots(0, self.all_slots, self.world, self.xmatch, self.xn, st.cuda_stream, query=query)
 
     def step(self, ev=None, xev=None, extract=True, match=True, xchg=True, first=True, batch=None, wait=None):
         """enqueue one step over the next pool batch (or `batch`); ev[p] = (start, end) events around graph
@@ -133,6 +162,8 @@ class AgentSchedule:
                     self.streams[p].wait_event(wait[p] if isinstance(wait, (list, tuple)) else wait)
                 if p > 0 and stagger_now:
                     self.streams[p].wait_event(self.pyr_done[p - 1] if self.stagger_pyr else self.done[p - 1])
+                if p == 0 and self.xstream is not None and self.kf_pending:
+                    self.streams[0].wait_event(self.kf_released)  # the previous exchange has copied the keyframe
                 self.pipes[p].extract(self.frames[r][p], st)
                 self.done[p].record(self.streams[p])
             if match:
@@ -142,15 +173,17 @@ class AgentSchedule:
                 if ev is not None:
                     ev[p][1].record(self.streams[p])
         if xchg and self.exchange_on:
+            if self.xstream is not None:
+                self.xstream.wait_event(self.done[0])  # graph 0 has extracted this step's keyframe (frame 0)
             if xev is not None:
-                xev[0].record(self.streams[0])
+                xev[0].record(self.exchange_stream())
             ag = None
             if xev is not None:
                 ag = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 self.ag_events.append(ag)
             self.exchange(ag)
             if xev is not None:
-                xev[1].record(self.streams[0])
+                xev[1].record(self.exchange_stream())
 
     # ------------------------------------------------------------------------------------------
     def check_errors(self):

@@ -29,7 +29,9 @@ def main():
         out.copy_(o.to(out.device))
 
     frames = orbamd.synth_frames(rank, 0, B, W, H)
-    sched = AgentSchedule(torch, frames, W, H, P, device=0, rank=rank, world=world, allgather=allgather)
+    # the exchange on its own stream, as bench.py runs it whenever a collective does
+    sched = AgentSchedule(torch, frames, W, H, P, device=0, rank=rank, world=world, allgather=allgather,
+                          async_exchange=True)
     sched.step()
     sched.step(first=False)
     torch.cuda.synchronize()

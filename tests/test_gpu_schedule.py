@@ -14,16 +14,20 @@ from check_schedule import check_schedule
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("W,H,nf,B,P,stagger", [(640, 480, 1000, 1024, 4, "every8"), (640, 480, 1000, 1024, 4, "each"),
-                                                 (752, 480, 1200, 128, 2, "every8"), (1241, 376, 2000, 128, 2, "every8")])
-def test_bench_schedule_bit_exact(W, H, nf, B, P, stagger):
+@pytest.mark.parametrize("W,H,nf,B,P,stagger,async_x", [(640, 480, 1000, 1024, 4, "every8", False),
+                                                         (640, 480, 1000, 1024, 4, "each", False),
+                                                         (640, 480, 1000, 1024, 4, "every8", True),
+                                                         (752, 480, 1200, 128, 2, "every8", False),
+                                                         (1241, 376, 2000, 128, 2, "every8", False)])
+def test_bench_schedule_bit_exact(W, H, nf, B, P, stagger, async_x):
     torch = pytest.importorskip("torch")
     from orbamd.agent import AgentSchedule, DEFAULT_STAGGER
     assert DEFAULT_STAGGER == "every8"  # bench.py's default (--stagger)
     frames = orbamd.synth_frames(0, 0, B, W, H)
-    sched = AgentSchedule(torch, frames, W, H, P, device=0, nfeatures=nf, stagger=stagger)
+    sched = AgentSchedule(torch, frames, W, H, P, device=0, nfeatures=nf, stagger=stagger, async_exchange=async_x)
     sched.step()                   # warmup (the first step also builds the geometry tables; staggered)
-    sched.step(first=False)        # the checked step: free-running under every8, staggered under each
+    sched.step(first=False)        # free-running under every8, staggered under each
+    sched.step(first=False)        # the checked step (with async_x graph 0 first waits for the previous exchange's copy)
     torch.cuda.synchronize()
     sched.check_errors()
     sub = B // P
