@@ -208,6 +208,29 @@ def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, 
                       "frames' arrival" % (pool, B, len(copy_st))}
 
 
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` called directly (no WORLD_SIZE in the environment) with N > 1: start N ranks
+    under torch.distributed.run as a child process and exit with its status (rank 0 prints the JSON line
+    to the inherited stdout). Runs before anything in this process touches the GPU. With the product
+    backend (nccl = RCCL) every rank needs its own visible device."""
+    import socket
+    import subprocess
+    backend = os.environ.get("ORBAMD_DIST_BACKEND", "nccl")
+    if backend == "nccl" and "ORBAMD_BENCH_DEVICE" not in os.environ:
+        import torch  # device_count() does not initialise the GPU on this image
+        ndev = torch.cuda.device_count()
+        if n > ndev:
+            print("bench.py: --gpus %d needs %d visible GPUs (one agent per GPU over RCCL); %d visible"
+                  % (n, n, ndev), file=sys.stderr, flush=True)
+            return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,8 +256,9 @@ def main():
                     help="where the keyframe exchange runs: its own stream, off graph 0's critical path (only the pack + "
                          "keyframe copy holds graph 0's next extraction), or in order on graph 0's stream; auto = own when "
                          "a collective runs (N > 1, --dist), graph 0's at N = 1 (profiles/r03_exp_exchange_stream.log)")
-    ap.add_argument("--roof-kernel", choices=("pyramid", "fast_cells", "octree", "blur", "describe"),
-                    default="fast_cells", help="extraction kernel priced in `roofline` (timed live in the timed region)")
+    ap.add_argument("--roof-kernel", choices=("auto", "pyramid", "fast_cells", "octree", "blur", "describe"),
+                    default="auto", help="extraction kernel priced in `roofline` (timed live in the timed region); auto = "
+                                         "the largest stage of this run's own stage split")
     ap.add_argument("--sustain", type=float, default=6.0,
                     help="seconds of the untimed sustained pass after the timed region (0: skip)")
     ap.add_argument("--pool", type=int, default=2,
@@ -251,6 +275,10 @@ def main():
                          "K-th step after it")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import numpy as np
     import torch
@@ -266,6 +294,9 @@ def main():
     backend = os.environ.get("ORBAMD_DIST_BACKEND", "nccl")
     local = int(os.environ.get("ORBAMD_BENCH_DEVICE", local))
     use_dist = world > 1 or args.dist
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr, flush=True)
+        sys.exit(2)
     if use_dist:
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -361,10 +392,9 @@ def main():
 
     # 1) stage split (untimed): every stage bracketed, same schedule
     _, stage_ms = run_profiled(0x1F, args.steps, False)
-    # the roofline kernel: k_fast_cells2, the largest GPU time of the step in the rocprofv3 kernel trace of this bench
-    # (profiles/r02_kernel_stats.csv, 24 %; isolated 21 %); the event-timed stage split can rank describe first
-    # by a few percent since its events include queueing behind the other graphs
-    dom = args.roof_kernel
+    # the roofline kernel: the extraction stage with the largest live time in this run's own stage split (every
+    # stage bracketed by HIP events on the stream it runs on, same overlapped schedule); --roof-kernel overrides
+    dom = max(stages, key=lambda k: stage_ms[k]) if args.roof_kernel == "auto" else args.roof_kernel
     # 2) timed region: only the dominant kernel bracketed (its live launch duration for the roofline)
     el, dom_live = run_profiled(1 << stages.index(dom), args.steps, True)
     last_batch, prev_batch = sched.last_batch, (sched.last_batch - 1) % args.pool
@@ -464,19 +494,54 @@ def main():
                "frac": round(hbm_gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": per_stage[dom] * sub,
                "measured_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
                "frac_vs_copy": round(hbm_gbs / copy_gbs, 5) if copy_gbs else None}
+        sel = ("largest stage of this run's stage split (%s)" % ", ".join("%s %.3f ms" % (k, stage_ms[k]) for k in stages)
+               if args.roof_kernel == "auto" else "--roof-kernel")
         if valu_gs is not None and valu_gs / VALU_PEAK_GINST > hbm_gbs / HBM_PEAK_GBS:
             # the byte/integer kernels are bound by vector-instruction issue, not HBM
             roof = {"bound": "valu", "kernel": dom, "achieved": round(valu_gs, 1), "peak": VALU_PEAK_GINST,
                     "unit": "G wave64 VALU instr/s", "frac": round(valu_gs / VALU_PEAK_GINST, 4),
                     "traffic": traffic, "valu_insts_per_launch": valu_insts, "launch_ms": round(dom_ms, 4),
-                    "hbm": hbm}
+                    "hbm": hbm, "selected_by": sel}
         else:
             roof = {"bound": "hbm", "kernel": dom, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": hbm["frac"], "traffic": traffic, "launch_ms": round(dom_ms, 4), "hbm": hbm}
+                    "frac": hbm["frac"], "traffic": traffic, "launch_ms": round(dom_ms, 4), "hbm": hbm,
+                    "selected_by": sel}
         # the matcher on the matrix cores (fp4 +-1 operands, v_mfma_scale_f32_32x32x64_f8f6f4): algorithmic ops =
         # n1*n2 distances x 256 bits x 2 per pair
         m_ms = stage_ms.get("match", 0.0)
         m_tops = nkp * nkp * 512 * sub / (m_ms * 1e-3) / 1e12 if m_ms > 0 else 0.0
+        # every stage's roofline at its live launch time in the stage pass (one launch = one graph's sub-batch):
+        # VALU issue and HBM fractions from the counter passes of this configuration, algorithmic bytes beside
+        # them; plus the whole step's VALU issue rate (every stage's VALU wave-instructions x P launches per step
+        # / ms_per_step)
+        stage_roof, step_valu = {}, 0.0
+        pmc = {}
+        if os.path.exists(pmc_path) and sub == 256:
+            try:
+                pmc = json.load(open(pmc_path))
+            except Exception:
+                pmc = {}
+        for k in stages + ["match"]:
+            ms = stage_ms.get(k, 0.0)
+            rec = pmc.get(k, {})
+            vi, hb = rec.get("valu_insts_per_launch"), rec.get("hbm_bytes_per_launch")
+            alg = per_stage.get(k, 0) * sub if k in per_stage else None
+            row = {"launch_ms": round(ms, 4), "valu_insts_per_launch": vi, "hbm_bytes_per_launch": hb}
+            if ms > 0:
+                if vi:
+                    row["valu_frac"] = round(vi / (ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4)
+                if hb:
+                    row["hbm_frac"] = round(hb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                if alg:
+                    row["alg_bytes_per_launch"] = alg
+                    row["alg_hbm_frac"] = round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            if vi:
+                step_valu += vi * P
+            stage_roof[k] = row
+        step_s = el / args.steps
+        step_valu_roof = ({"valu_insts_per_step": step_valu, "achieved": round(step_valu / step_s / 1e9, 1),
+                           "peak": VALU_PEAK_GINST, "unit": "G wave64 VALU instr/s",
+                           "frac": round(step_valu / step_s / 1e9 / VALU_PEAK_GINST, 4)} if step_valu else None)
         result = {
             "metric": "frames/sec ORB extract+match, 640x480 mono, 1000 feat/frame" if args.config == "c2" else
                       "frames/sec ORB extract+match, %dx%d, %d feat/frame" % (W, H, cfg["nfeatures"]),
@@ -507,6 +572,8 @@ def main():
             "match_roofline": {"bound": "mfma", "kernel": "k_tri_mfma", "achieved": round(m_tops, 2),
                                "peak": FP4_MFMA_PEAK_TOPS, "unit": "fp4 TOPS", "frac": round(m_tops / FP4_MFMA_PEAK_TOPS, 4),
                                "launch_ms": round(m_ms, 4)},
+            "stage_rooflines": stage_roof,
+            "step_valu_issue": step_valu_roof,
             "pipeline_hbm": {"bytes_per_frame": b_frame, "achieved_GBs": round(b_frame * value / world / 1e9, 2),
                              "frac": round(b_frame * value / world / 1e9 / HBM_PEAK_GBS, 5)},
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},

@@ -9,7 +9,10 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1179,13 +1182,25 @@ int wait_until(hipStream_t st, Ready ready) {
         return e && atoi(e) != 0;
     }();
     if (!sync_wait) {
-        for (unsigned spins = 1; spins < (1u << 22); spins++) {
+        // spin (with a pause) for the first ~200 us, which covers a call that is not queued behind other GPU
+        // work; after that yield the core to the other SLAM threads between polls instead of burning it
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned spins = 1;; spins++) {
             if (ready()) return 0;
-            if ((spins & 1023) == 0) {
+            const bool late = (spins & 255) == 0 &&
+                              std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200);
+            if (late || (spins & 1023) == 0) {
                 const hipError_t e = hipStreamQuery(st);
-                if (e == hipErrorNotReady) continue;
-                if (e != hipSuccess) return ORBX_EDEVICE;
-                break;  // drained: the words are visible now if the kernel wrote them
+                if (e != hipErrorNotReady) {
+                    if (e != hipSuccess) return ORBX_EDEVICE;
+                    break;  // drained: the words are visible now if the kernel wrote them
+                }
+                if (late) {
+                    sched_yield();
+                    spins = 0;  // next check after another 256 polls
+                }
+            } else {
+                __builtin_ia32_pause();
             }
         }
     }
@@ -1266,8 +1281,10 @@ bool view_ok(const orbm_kf_view* v) {
 
 /* One keyframe's immutable per-feature arrays in HBM (orbm_kf_cache): mDescriptors, mvKeysUn (x, y, angle,
  * octave), mvuRight, the FeatureVector's feature list and, for the projection matchers, its 64x48 feature
- * grid (k_grid output). A call holds a shared_ptr to the entries it reads until its stream is synchronised,
- * so an eviction by another thread never frees memory a running kernel reads. */
+ * grid (k_grid output). A call holds a shared_ptr to the entries it reads until it has its results. Every
+ * per-call kernel writes a result word only after the reads it depends on, and the call returns only once it
+ * has seen every result word, so no read of the entry is outstanding when the call drops its reference; an
+ * eviction on another thread then frees the buffer with hipFree, which in addition waits for the device. */
 struct KfEntry {
     DevBuf buf;
     int n = 0, nfeat = 0, n_nodes = 0;
@@ -1577,6 +1594,9 @@ static int bow_small(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view* 
     a.mode = mode;
     a.check_ori = check_ori ? 1 : 0;
     a.nnratio = nnratio;
+    // the polled words start at 0, which no call carries (seq >= 1): a word left by an earlier call on this
+    // context (another layout, or the same bits by chance) can never read as this call's
+    memset(hp + o_out, 0, cv.off - o_out);
     if (in_bytes) HIPR(hipMemcpyAsync(dbase, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     HIPR(launch_bow_small(a, ctx->stream));
     return small_finish(ctx, hp, o_out, o_done, a.tasks, nt, (uint32_t)a.seq, check_ori, out, nout, nmatches);
@@ -1619,6 +1639,7 @@ static int tri_small(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view*
     a.q_ur = kf1->uright != nullptr;
     a.c_ur = kf2->uright != nullptr;
     make_geom(a.g, F12, ex, ey, kf2->nlevels, kf2->scale_factors, kf2->level_sigma2);
+    memset(hp + o_out, 0, cv.off - o_out);  // polled words: 0 is no call's seq (bow_small)
     if (in_bytes) HIPR(hipMemcpyAsync(dbase, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     HIPR(launch_tri_small(a, ctx->stream));
     return small_finish(ctx, hp, o_out, o_done, a.tasks, nt, (uint32_t)a.seq, check_ori, match12, kf1->n, nmatches);
@@ -2186,12 +2207,14 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
         memcpy(hp + o_q, pb.q.data(), sizeof(ProjQuery) * nq);
         memcpy(hp + o_qd, pb.qdesc.data(), 32 * nq);
     }
+    const size_t nwait = c.direct ? nq : nout + 1;
+    // the polled words start at 0, which no call carries (seq >= 1; see bow_small)
+    memset(hp + in_bytes, 0, 8 * nwait);
     HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, st));
     HIPR(launch_projection((const ProjCall*)(base + o_call), 1, (int)nq, st, !c.direct, init_n >= 0, !ce));
     // poll the results (each carries this call's seq) instead of a D2H copy + stream synchronisation
     const unsigned long long* ho = (const unsigned long long*)(hp + in_bytes);
     const uint32_t seq = (uint32_t)c.seq;
-    const size_t nwait = c.direct ? nq : nout + 1;
     size_t next = 0;
     if (const int rc = wait_until(st, [&] {
             while (next < nwait && (uint32_t)(__atomic_load_n(ho + next, __ATOMIC_ACQUIRE) >> 32) == seq) next++;
@@ -2875,31 +2898,37 @@ namespace {
 
 /* the cached entry for (kind, key) matching this call's view, uploading (or replacing) it when absent or
  * stale (a different N, FeatureVector size, stereo presence or grid geometry); LRU eviction over the
- * capacity. Returns nullptr on a device error. */
+ * capacity. The lookup and the insertion hold the cache's mutex; a miss builds and uploads its entry on the
+ * calling context's stream with the mutex released, so calls of other threads are not held behind the upload
+ * (two threads missing on the same key both upload; the second insertion keeps the first one's entry).
+ * Returns nullptr on a device error. */
 std::shared_ptr<KfEntry> cache_get(orbm_kf_cache* c, int kind, uint64_t key, const orbm_kf_view* kv,
-                                   const orbm_frame_view* fv) {
+                                   const orbm_frame_view* fv, hipStream_t st) {
     const int n = kv ? kv->n : fv->n;
     const int n_nodes = kv ? kv->n_nodes : 0;
     const int nfeat = kv && kv->n_nodes ? kv->node_off[kv->n_nodes] : 0;
     const bool has_ur = kv ? kv->uright != nullptr : fv->uright != nullptr;
-    std::lock_guard<std::mutex> lock(c->mu);
+    auto matches = [&](const KfEntry& e) {
+        return e.n == n && e.n_nodes == n_nodes && e.nfeat == nfeat && (e.has_ur || !has_ur) &&
+               (kind == 0 || (e.min_x == fv->min_x && e.min_y == fv->min_y && e.gw_inv == fv->grid_w_inv &&
+                              e.gh_inv == fv->grid_h_inv));
+    };
     auto& m = c->map[kind];
-    auto it = m.find(key);
-    if (it != m.end()) {
-        const KfEntry& e = *it->second.e;
-        const bool same = e.n == n && e.n_nodes == n_nodes && e.nfeat == nfeat && (e.has_ur || !has_ur) &&
-                          (kind == 0 || (e.min_x == fv->min_x && e.min_y == fv->min_y && e.gw_inv == fv->grid_w_inv &&
-                                         e.gh_inv == fv->grid_h_inv));
-        if (same) {
-            c->hits++;
-            c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
-            return it->second.e;
+    {
+        std::lock_guard<std::mutex> lock(c->mu);
+        auto it = m.find(key);
+        if (it != m.end()) {
+            if (matches(*it->second.e)) {
+                c->hits++;
+                c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
+                return it->second.e;
+            }
+            c->bytes -= it->second.e->buf.bytes;
+            c->lru.erase(it->second.lru);
+            m.erase(it);  // in-flight calls keep their shared_ptr; the buffer goes with the last one
         }
-        c->bytes -= e.buf.bytes;
-        c->lru.erase(it->second.lru);
-        m.erase(it);  // in-flight calls keep their shared_ptr; the buffer goes with the last one
+        c->misses++;
     }
-    c->misses++;
     auto e = std::make_shared<KfEntry>();
     e->n = n;
     e->n_nodes = n_nodes;
@@ -2967,10 +2996,20 @@ std::shared_ptr<KfEntry> cache_get(orbm_kf_cache* c, int kind, uint64_t key, con
         pc.grid_idx = (uint16_t*)e->at(e->o_gi);
         memcpy(h.data() + o_call, &pc, sizeof(pc));
     }
-    if (hipMemcpyAsync(e->buf.p, h.data(), cv.off, hipMemcpyHostToDevice, c->stream) != hipSuccess) return nullptr;
-    if (kind == 1 && launch_projection((const ProjCall*)e->at(o_call), 1, 0, c->stream, false) != hipSuccess)
-        return nullptr;
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return nullptr;
+    if (hipMemcpyAsync(e->buf.p, h.data(), cv.off, hipMemcpyHostToDevice, st) != hipSuccess) return nullptr;
+    if (kind == 1 && launch_projection((const ProjCall*)e->at(o_call), 1, 0, st, false) != hipSuccess) return nullptr;
+    if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(c->mu);
+    auto it = m.find(key);
+    if (it != m.end()) {
+        if (matches(*it->second.e)) {  // another thread inserted the same keyframe meanwhile: share its entry
+            c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
+            return it->second.e;
+        }
+        c->bytes -= it->second.e->buf.bytes;
+        c->lru.erase(it->second.lru);
+        m.erase(it);
+    }
     c->lru.push_front({kind, key});
     m[key] = orbm_kf_cache::Slot{e, c->lru.begin()};
     c->bytes += e->buf.bytes;
@@ -3043,8 +3082,8 @@ int orbm_search_for_triangulation_cached(orbm_ctx* ctx, orbm_kf_cache* cache, ui
                                          int only_stereo, int check_ori, int32_t* match12, int* nmatches) {
     if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf1) || !view_ok(kf2) || !F12 || !match12)
         return ORBX_EARG;
-    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr);
-    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr) : nullptr;
+    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr, ctx->stream);
+    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr, ctx->stream) : nullptr;
     if (!c1 || !c2) return ORBX_EDEVICE;
     return tri_common(ctx, kf1, kf2, F12, ex, ey, only_stereo, check_ori, match12, nmatches, c1.get(), c2.get());
 }
@@ -3054,8 +3093,8 @@ int orbm_search_by_bow_kf_kf_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_
                                     int32_t* match12, int* nmatches) {
     if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf1) || !view_ok(kf2) || !match12)
         return ORBX_EARG;
-    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr);
-    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr) : nullptr;
+    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr, ctx->stream);
+    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr, ctx->stream) : nullptr;
     if (!c1 || !c2) return ORBX_EDEVICE;
     return bow_common(ctx, kf1, kf2, nnratio, check_ori, 1, match12, kf1->n, nmatches, c1.get(), c2.get());
 }
@@ -3064,7 +3103,7 @@ int orbm_search_by_bow_kf_f_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t
                                    const orbm_kf_view* f, float nnratio, int check_ori, int32_t* match_f,
                                    int* nmatches) {
     if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf) || !view_ok(f) || !match_f) return ORBX_EARG;
-    const std::shared_ptr<KfEntry> ck = cache_get(cache, 0, key, kf, nullptr);
+    const std::shared_ptr<KfEntry> ck = cache_get(cache, 0, key, kf, nullptr, ctx->stream);
     if (!ck) return ORBX_EDEVICE;
     return bow_common(ctx, kf, f, nnratio, check_ori, 0, match_f, f->n, nmatches, ck.get(), nullptr);
 }
@@ -3074,7 +3113,7 @@ int orbm_fuse_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key, const or
                      int32_t* best_idx, int* nfused) {
     if (!cache || !fuse_args_ok(ctx, KF, Tcw, Ow, mp, inv_level_sigma2, best_idx) || cache->device != ctx->device)
         return ORBX_EARG;
-    const std::shared_ptr<KfEntry> ck = cache_get(cache, 1, key, nullptr, KF);
+    const std::shared_ptr<KfEntry> ck = cache_get(cache, 1, key, nullptr, KF, ctx->stream);
     if (!ck) return ORBX_EDEVICE;
     return fuse_common(ctx, KF, Tcw, Ow, mp, th, inv_level_sigma2, best_idx, nfused, ck.get());
 }

@@ -20,6 +20,9 @@
 namespace ORB_SLAM2 {
 
 namespace {
+// this definition reads the extractors' device pyramids, so they need not materialise mvImagePyramid
+const bool kReaderRegistered = (amd::RegisterDevicePyramidReader(), true);
+
 void gather_kps(const std::vector<cv::KeyPoint>& k, std::vector<orbx_kp>& out) {
     out.resize(k.size());
     for (size_t i = 0; i < k.size(); i++) {

@@ -16,12 +16,12 @@ namespace ORB_SLAM2 {
 
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
     : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
-      minThFAST(_minThFAST), mpHandle(nullptr), mHandleW(0), mHandleH(0), mDevice(0), mbHostPyramid(false),
+      minThFAST(_minThFAST), mpHandle(nullptr), mHandleW(0), mHandleH(0), mDevice(0), mHostPyramid(-1),
       mbPyramidStale(false) {
     const char* dev = getenv("ORBAMD_DEVICE");
     if (dev) mDevice = atoi(dev);
     const char* hp = getenv("ORBAMD_HOST_PYRAMID");
-    if (hp && atoi(hp) != 0) mbHostPyramid = true;
+    if (hp) mHostPyramid = atoi(hp) != 0 ? 1 : 0;
     // the tables are computed by the library with the reference's float semantics
     // (ORBextractor.cc:415-431), host-only, so the getters answer even without a usable device; the
     // device handle is created on the first frame (at that frame's size)
@@ -111,7 +111,13 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask, std::
     for (int i = 0; i < n; i++)
         _keypoints.push_back(cv::KeyPoint(k[i].x, k[i].y, k[i].size, k[i].angle, k[i].response, k[i].octave, -1));
     mbPyramidStale = true;
-    if (mbHostPyramid) SyncImagePyramid();
+    if (HostPyramidEager()) SyncImagePyramid();
+}
+
+bool ORBextractor::HostPyramidEager() const {
+    // default: eager unless the drop-in Frame::ComputeStereoMatches (the reference's one reader of the
+    // member, which reads the device copy instead) is linked in; ORBAMD_HOST_PYRAMID=1 / 0 forces it
+    return mHostPyramid >= 0 ? mHostPyramid == 1 : !amd::DevicePyramidReaderRegistered();
 }
 
 const std::vector<cv::Mat>& ORBextractor::SyncImagePyramid() {

@@ -12,11 +12,12 @@
  * ORBextractor.cc:1064-1065), logs the status to stderr (orbamd_status.h) and keeps it in
  * LastStatus(); the next frame retries on a fresh device handle.
  *
- * mvImagePyramid: the pyramid stays on the device. Its one reader in the reference,
- * Frame::ComputeStereoMatches (A1 Frame.cc:474-581), is replaced by host/Frame_stereo_amd.cc, which
- * reads the device copy, so no PCIe copy is made by default. A caller that does read the public
- * member calls SyncImagePyramid() first (a lazy copy of the last call's levels, done once per call),
- * or sets ORBAMD_HOST_PYRAMID=1 to have every call materialise it as the reference does.
+ * mvImagePyramid: by default every operator() fills the public member with this frame's levels, as the
+ * reference does (ORBextractor.cc:1107-1132), so stock readers (Frame::ComputeStereoMatches, A1
+ * Frame.cc:474-581) see the current frame. When the drop-in Frame::ComputeStereoMatches
+ * (host/Frame_stereo_amd.cc) is linked in, it registers itself as the reader of the device copy and the
+ * extractor skips the PCIe copy; the member is then filled lazily by SyncImagePyramid() (once per call).
+ * ORBAMD_HOST_PYRAMID=1 / 0 forces the eager / lazy form.
  */
 #ifndef ORBEXTRACTOR_H
 #define ORBEXTRACTOR_H
@@ -59,6 +60,9 @@ public:
     // status of the last operator() / SyncImagePyramid (ORBX_OK or a negative ORBX_E* code); addition
     int LastStatus() const { return mLastStatus; }
 
+    // whether operator() fills mvImagePyramid itself (see above); addition
+    bool HostPyramidEager() const;
+
 protected:
     int ensureHandle(int width, int height);
     orbx_params params() const;
@@ -77,7 +81,7 @@ protected:
     orbx_handle* mpHandle;
     int mHandleW, mHandleH;
     int mDevice;
-    bool mbHostPyramid;   // ORBAMD_HOST_PYRAMID=1: materialise after every call
+    int mHostPyramid;     // ORBAMD_HOST_PYRAMID: 1 eager, 0 lazy, -1 (unset) eager unless a device reader is linked
     bool mbPyramidStale;  // mvImagePyramid does not hold the last call's levels yet
     int mLastStatus = 0;
     std::vector<unsigned char> mKpBuf, mDescBuf;

@@ -4,6 +4,7 @@
  */
 #include "orbamd_status.h"
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 
@@ -57,6 +58,20 @@ orbm_kf_cache* KeyFrameCache() {
         return c;
     }();
     return cache;
+}
+
+namespace {
+std::atomic<bool>& pyramid_reader() {
+    static std::atomic<bool> registered{false};  // function-local: safe from any static initialiser
+    return registered;
+}
+}  // namespace
+
+void RegisterDevicePyramidReader() { pyramid_reader().store(true); }
+bool DevicePyramidReaderRegistered() { return pyramid_reader().load(); }
+
+void ForgetKeyFrame(const void* pKF, unsigned long mnId) {
+    if (orbm_kf_cache* c = KeyFrameCache()) StatusOk(orbm_kf_cache_erase(c, KeyFrameKey(pKF, mnId)), "orbm_kf_cache_erase");
 }
 
 }  // namespace amd

@@ -38,6 +38,15 @@ orbm_kf_cache* KeyFrameCache();
 inline uint64_t KeyFrameKey(const void* pKF, unsigned long mnId) {
     return (uint64_t)(uintptr_t)pKF ^ ((uint64_t)mnId * 0x9E3779B97F4A7C15ull);
 }
+/* the drop-in readers of the device pyramid (host/Frame_stereo_amd.cc, the replacement of the reference's
+ * only reader of ORBextractor::mvImagePyramid, Frame::ComputeStereoMatches) register themselves at static
+ * initialisation. Without one linked in, every ORBextractor::operator() materialises mvImagePyramid on the
+ * host as the reference does (ORBextractor.cc:1107-1132), so a stock reader sees the current frame's levels. */
+void RegisterDevicePyramidReader();
+bool DevicePyramidReaderRegistered();
+/* drop a KeyFrame's cached device arrays (a no-op without the cache): the hook for KeyFrame::SetBadFlag
+ * (KeyFrame.cc, after mbBad = true), so culled keyframes stop holding cache capacity until LRU evicts them */
+void ForgetKeyFrame(const void* pKF, unsigned long mnId);
 
 }  // namespace amd
 }  // namespace ORB_SLAM2

@@ -125,6 +125,8 @@ class AgentSchedule:
         p0 = self.pipes[0]
         st = self.exchange_stream()
         query = self.src0
+        if self.xstream is not None:
+            self.xstream.wait_event(self.done[0])  # graph 0 has extracted this step's keyframe (frame 0)
         with torch.cuda.stream(st):
             p0.pack(0, self.my_slot, self.meta, st.cuda_stream, err=self.pack_err, src=self.src0)
             if self.xstream is not None:
@@ -174,7 +176,7 @@ class AgentSchedule:
                     ev[p][1].record(self.streams[p])
         if xchg and self.exchange_on:
             if self.xstream is not None:
-                self.xstream.wait_event(self.done[0])  # graph 0 has extracted this step's keyframe (frame 0)
+                self.xstream.wait_event(self.done[0])  # before xev[0]: the exchange's time excludes this wait
             if xev is not None:
                 xev[0].record(self.exchange_stream())
             ag = None

@@ -24,6 +24,14 @@ g++ -std=c++14 -O1 -pthread -Wall -Wno-unused-function \
   -L "$R/cooperative-orb-slam_amd/lib" -lorbamd \
   -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,/opt/rocm/lib \
   -o "$R/tests/cpp/build/test_nodevice"
+# a stock reader of mvImagePyramid: the extractor WITHOUT the drop-in stereo (the device pyramid's reader)
+g++ -std=c++14 -O1 -pthread -Wall -Wno-unused-function \
+  -I "$R/tests/cpp/cvmin" -I "$R/tests/cpp/mock" -I "$R/cooperative-orb-slam_amd/host" -I "$R/include" -I "$R/oracle" \
+  "$R/tests/cpp/test_pyramid_reader.cpp" "$R/cooperative-orb-slam_amd/host/ORBextractor.cc" \
+  "$R/cooperative-orb-slam_amd/host/orbamd_status.cc" \
+  -L "$R/cooperative-orb-slam_amd/lib" -lorbamd -L "$R/oracle/build" -lorb_oracle \
+  -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,"$R/oracle/build" -Wl,-rpath,/opt/rocm/lib \
+  -o "$R/tests/cpp/build/test_pyramid_reader"
 # the slot codec (host only, no GPU needed to run)
 g++ -std=c++14 -O1 -Wall -Wno-unused-function \
   -I "$R/tests/cpp/cvmin" -I "$R/tests/cpp/mock" -I "$R/cooperative-orb-slam_amd/host" -I "$R/include" \

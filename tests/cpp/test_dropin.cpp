@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <atomic>
 #include <thread>
@@ -64,7 +65,10 @@ static void check_extract(ORBextractor& ext, oc_extractor* orc, const uint8_t* i
         bad += memcmp(desc.ptr<unsigned char>(i), of.desc.data() + 32 * (size_t)i, 32) != 0;
     }
     CHECK(bad == 0, "%d keypoint/descriptor rows differ", bad);
-    // the host pyramid is lazy (no PCIe copy unless a caller asks for it)
+    // this binary links the drop-in Frame::ComputeStereoMatches (the device pyramid's reader), so the host
+    // pyramid is lazy: no PCIe copy unless a caller asks for it (tests/cpp/test_pyramid_reader.cpp: eager
+    // without it)
+    if (!getenv("ORBAMD_HOST_PYRAMID")) CHECK(!ext.HostPyramidEager(), "host pyramid eager with the drop-in stereo linked");
     ext.SyncImagePyramid();
     for (int l = 0; l < ext.GetLevels(); l++) {
         int w, h;
@@ -943,6 +947,20 @@ int main() {
             orbm_kf_cache_stats(ORB_SLAM2::amd::KeyFrameCache(), &entries, &bytes, &hits, &misses);
             printf("keyframe cache: %d entries, %zu bytes, %lld hits, %lld misses\n", entries, bytes, hits, misses);
             CHECK(entries >= 2 && hits >= 3 * iters - 3, "keyframe cache not shared: %lld hits", hits);
+            // KeyFrame::SetBadFlag's hook drops the keyframe's entry; the next call uploads it again (a miss)
+            ORB_SLAM2::amd::ForgetKeyFrame(&kf1, kf1.mnId);
+            int entries2 = 0;
+            orbm_kf_cache_stats(ORB_SLAM2::amd::KeyFrameCache(), &entries2, nullptr, nullptr, nullptr);
+            CHECK(entries2 == entries - 1, "ForgetKeyFrame: %d entries after, %d before", entries2, entries);
+            {
+                ORBmatcher m(0.75f, true);
+                std::vector<MapPoint*> v;
+                CHECK(m.SearchByBoW(&kf1, &kf2, v) == e_nkk && v == e_kk, "SearchByBoW after ForgetKeyFrame");
+            }
+            long long misses2 = 0;
+            orbm_kf_cache_stats(ORB_SLAM2::amd::KeyFrameCache(), &entries2, nullptr, nullptr, &misses2);
+            CHECK(entries2 == entries && misses2 == misses + 1, "re-upload after ForgetKeyFrame: %d entries, %lld misses",
+                  entries2, misses2);
         } else {
             printf("keyframe cache off (ORBAMD_KF_CACHE_MB=0)\n");
         }

@@ -33,6 +33,20 @@ def test_dropin_bit_exact_on_gpu(kf_cache_mb):
     assert r.returncode == 0 and "ALL PASS" in r.stdout
 
 
+@pytest.mark.gpu
+def test_stock_pyramid_reader_sees_current_frame():
+    """ORBextractor built without the drop-in Frame::ComputeStereoMatches and no ORBAMD_HOST_PYRAMID: a stock
+    reader of mvImagePyramid straight after operator() (A1 Frame.cc:474-581) gets this frame's levels, bit-exact
+    (ORBextractor.cc:1107-1132), with no SyncImagePyramid() call"""
+    _build()
+    env = dict(os.environ)
+    env.pop("ORBAMD_HOST_PYRAMID", None)
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "build", "test_pyramid_reader")], capture_output=True,
+                       text=True, timeout=300, env=env)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0 and "ALL PASS" in r.stdout
+
+
 def test_dropins_do_not_throw_without_device():
     """ORBX_EDEVICE from every C ABI call (ORBAMD_DEVICE=99 is out of range on any box): each drop-in returns
     the reference's "nothing found" result and logs the status instead of throwing into the caller's thread"""

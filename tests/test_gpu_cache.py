@@ -141,3 +141,29 @@ def test_cached_fuse_equals_oracle(seed, stereo, th):
     assert st["misses"] == 1 and st["hits"] == 2
     m.close()
     cache.close()
+
+
+def test_small_bow_and_projection_alternate_on_one_context():
+    """Tracking's order on one thread (Tracking.cc:TrackReferenceKeyFrame / TrackLocalMap): SearchByBoW on the
+    small-call path (k_bow_small: seq in the low bits of its done words, bits 37+ of its accepts), then
+    SearchByProjection (seq in the high 32 bits of its result words), again and again on ONE context, so the
+    reused pinned result buffer always holds the other layout's words from the previous call. Every call must
+    equal the oracle (a stale word read as this call's would hand back a wrong index)."""
+    kfs, tabs, rng = _kfs(seed=11)
+    for kf in kfs:  # 64 nodes of ~16 features: every node within k_bow_small's 64 candidates
+        kf["fv"] = {}
+        for i in range(len(kf["k"])):
+            kf["fv"].setdefault(100 + int(kf["d"][i, 0] >> 2), []).append(i)
+    m = orbamd.ORBmatcher(0.75, True)
+    mp = m  # one context for both kinds of call
+    for it in range(12):
+        v1, v2 = _view(kfs[it % 3], tabs, rng), _view(kfs[(it + 1) % 3], tabs, rng)
+        ng, mg = m.SearchByBoW(v1, v2, other_is_keyframe=False)
+        no, mo = oracle_py.search_by_bow(v1, v2, 0.75, True, other_is_keyframe=False)
+        assert ng == no
+        np.testing.assert_array_equal(mg, mo)
+        F, mps = ps.local_scene(20 + it, it % 2 == 0)
+        (gn, gm), (on, om) = mp.SearchByProjectionLocal(F, mps, 3.0), oracle_py.search_by_projection_local(
+            F, mps, 3.0, 0.75)
+        assert gn == on
+        np.testing.assert_array_equal(gm, om)

@@ -309,6 +309,38 @@ def test_bench_rccl_world1():
     assert res["stage_ms_per_step"]["allgather"] > 0
 
 
+def test_bench_gpus2_launches_ranks():
+    """`bench.py --gpus 2` called directly (as the driver calls it) starts two ranks itself under
+    torch.distributed.run; here both share cuda:0 and exchange over gloo (ORBAMD_DIST_BACKEND /
+    ORBAMD_BENCH_DEVICE, the one-GPU rehearsal hooks): n_gpus 2, both agents' slots checked, bit-exact."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
+           "--batch", "256", "--pipes", "2", "--no-cpu", "--sustain", "0", "--ingest-steps", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(ORBAMD_DIST_BACKEND="gloo", ORBAMD_BENCH_DEVICE="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
+    print(r.stdout[-3000:], r.stderr[-3000:])
+    assert r.returncode == 0
+    import json
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, "rank 0 alone prints the JSON line"
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["checked_slots"] == 2 and res["bit_exact"] is True
+    assert res["collective"].startswith("gloo")
+
+
+def test_bench_gpus2_nccl_needs_two_devices():
+    """with the product backend (RCCL) `--gpus 2` on a one-GPU box fails cleanly before any rank starts"""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one visible GPU")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "ORBAMD_DIST_BACKEND", "ORBAMD_BENCH_DEVICE")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode == 2 and "needs 2 visible GPUs" in r.stderr, r.stderr[-2000:]
+    assert not r.stdout.strip()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
