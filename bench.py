@@ -252,6 +252,9 @@ def main():
                     help="HIP stream priorities of the graphs: lead = the first half of the staggered graphs (the ones "
                          "in their latency-bound tail stages) high, lead1 = graph 0 only")
     ap.add_argument("--no-exchange", action="store_true")
+    ap.add_argument("--serial-stages", action="store_true",
+                    help="measurement hook (orbx_debug_serial): every extraction stage in order on its graph's stream, so "
+                         "a kernel trace times each kernel alone (with --pipes 1)")
     ap.add_argument("--exchange-stream", choices=("auto", "own", "graph0"), default="auto",
                     help="where the keyframe exchange runs: its own stream, off graph 0's critical path (only the pack + "
                          "keyframe copy holds graph 0's next extraction), or in order on graph 0's stream; auto = own when "
@@ -330,6 +333,9 @@ def main():
                           priorities=[hi_prio if p < n_hi else lo_prio for p in range(P)], nfeatures=cfg["nfeatures"],
                           pool=args.pool, async_exchange=async_x)
     pipes = sched.pipes
+    if args.serial_stages:
+        for pp in pipes:
+            assert orbamd.load().orbx_debug_serial(pp.ext._h, 1) == 0
 
     for _ in range(args.warmup):
         sched.step()

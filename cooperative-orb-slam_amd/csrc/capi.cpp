@@ -166,8 +166,7 @@ struct Geometry {
     int tiled_ok[kMaxLevels] = {0};   // level's resize fits the LDS-tiled kernel
     std::vector<int> ptab;            // k_pyramid_frames column-group / row tables
     bool frames_ok = true;            // every level fits k_pyramid_frames
-    int pyr_band_off = 0;             // k_pyramid_frames band ranges: int2 [band][kMaxLevels] in ptab
-    int pyr_band_rows = 1;            // longest band range of any level >= 1 (LDS row table rows)
+    int pyr_rows = 1;                 // tallest level >= 1 (k_pyramid_frames' LDS row table rows)
     DevBuf d_lv, d_cells, d_coef, d_ptab;
 
     int build(const Tables& T, int W_, int H_) {
@@ -351,32 +350,8 @@ struct Geometry {
             ep.kp_off[l] = l < L ? lv[l].kp_off : kp_off;
             ep.bjob_begin[l] = l <= L ? bjob_begin[l] : nbjobs;
         }
-        // k_pyramid_frames bands (top level down): a band's rows of level l are its own share
-        // [b*h/K, (b+1)*h/K) plus every row its range of level l+1 reads (row table r0 / r1)
-        pyr_band_off = (int)ptab.size();
-        pyr_band_rows = 1;
-        ptab.resize(ptab.size() + 2 * (size_t)kPyrBands * kMaxLevels, 0);
-        if (frames_ok) {
-            for (int b = 0; b < kPyrBands; b++) {
-                int* bt = ptab.data() + pyr_band_off + 2 * b * kMaxLevels;
-                for (int l = L - 1; l >= 1; l--) {
-                    const int h = lv[l].h;
-                    int lo = (int)((long long)b * h / kPyrBands), hi = (int)((long long)(b + 1) * h / kPyrBands);
-                    if (l + 1 < L && bt[2 * (l + 1)] < bt[2 * (l + 1) + 1]) {
-                        const int* rt = ptab.data() + lv[l + 1].rt_off;
-                        for (int y = bt[2 * (l + 1)]; y < bt[2 * (l + 1) + 1]; y++) {
-                            lo = std::min(lo, rt[4 * y]);
-                            hi = std::max(hi, rt[4 * y + 1] + 1);
-                        }
-                    }
-                    lo = std::max(lo, 0);
-                    hi = std::min(hi, h);
-                    bt[2 * l] = lo;
-                    bt[2 * l + 1] = std::max(hi, lo);
-                    pyr_band_rows = std::max(pyr_band_rows, hi - lo);
-                }
-            }
-        }
+        pyr_rows = 1;
+        for (int l = 1; l < L; l++) pyr_rows = std::max(pyr_rows, lv[l].h);
         // octree LDS: node arrays (92 B/node, NC pow2) + keys (7 B/key)
         NC = 1;
         while (NC < maxnode) NC <<= 1;
@@ -411,7 +386,7 @@ struct orbx_handle {
     int max_w = 0, max_h = 0, max_batch = 1;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
-    hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_blur = nullptr, ev_fast0 = nullptr;
+    hipEvent_t ev_pyr = nullptr, ev_blur = nullptr;
     hipEvent_t user_ev_pyr = nullptr;  // orbx_set_pyramid_event (caller-owned)
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
@@ -443,26 +418,13 @@ struct orbx_handle {
     int prof_calls = 0;
     double prof_ms[5] = {0, 0, 0, 0, 0};
     int skip_mask = 0;  // orbx_debug_skip_stages (test hook)
+    bool serial = false;  // orbx_debug_serial (measurement hook): every stage in order on the caller's stream
 };
 
 static const int kProfMaxCalls = 4096;
 
 /* stage k = {pyramid, fast_cells, octree, blur, describe}; e = 0 start / 1 end, recorded on the
  * stream the stage's kernel is launched on (the overlapped schedule is kept) */
-/* Marginal-cost experiment only (results of a changing input invalid): with -DORBX_SKIP_WARM=<mask>
- * the stages in the mask (1 pyramid, 2 FAST, 4 octree, 8 blur, 16 describe, 32 batch matcher) are
- * launched only during the first 64 calls. bench.py repeats the same frames every step, so the
- * skipped stages' buffers still hold this step's results and the step times what the others cost. */
-#ifndef ORBX_SKIP_WARM
-#define ORBX_SKIP_WARM 0
-#endif
-static bool skip_warm(int bit) {
-    if (!(ORBX_SKIP_WARM & bit)) return false;
-    static int calls[8] = {0};
-    int& c = calls[__builtin_ctz((unsigned)bit)];
-    return c++ >= 64;
-}
-
 static int prof_mark(orbx_handle* h, int k, int e, hipStream_t st) {
     if (!h->prof_on || !((h->prof_mask >> k) & 1)) return 0;
     if (h->prof_calls >= kProfMaxCalls) return 0;
@@ -502,11 +464,8 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
     return 0;
 }
 
-/* blur != nullptr: the whole-frame pyramid also blurs every level into it (ORBX_BLUR_IN_PYR); *fused tells
- * whether it did (the per-level path never does) */
 static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fstride, int pitch, int nframes,
-                          hipStream_t st, uint8_t* blur = nullptr, bool* fused = nullptr) {
-    if (fused) *fused = false;
+                          hipStream_t st) {
     Geometry& g = h->geo;
     const ExtractParams& ep = g.ep;
     // pyramid levels 1..L-1 (ORBextractor.cc:1107-1132): whole-frame kernel for large batches of
@@ -516,9 +475,7 @@ static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fst
         int max_groups = 1;
         for (int l = 1; l < ep.L; l++) max_groups = std::max(max_groups, (g.lv[l].w + 3) / 4);
         HIPR(launch_pyramid_frames(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, g.d_lv.as<LevelDesc>(),
-                                   g.d_ptab.as<int>(), (const int2*)(g.d_ptab.as<int>() + g.pyr_band_off),
-                                   g.pyr_band_rows, max_groups, nframes, st, blur));
-        if (fused) *fused = blur != nullptr;
+                                   g.d_ptab.as<int>(), g.pyr_rows, max_groups, nframes, st));
         return 0;
     }
     for (int l = 1; l < ep.L; l++) {
@@ -549,24 +506,14 @@ static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstrid
 
 /* ORBextractor::operator() for a batch. Dependencies between the stages:
  *
- *   st   (caller): memset(err) -> pyramid(1..L-1) -> [ev_pyr] FAST(all cells) -> octree -> [ev_blur] describe
- *   side         :                                 [ev_pyr] blur(all levels) ---------> [ev_blur]
+ *   st   (caller): pyramid(1..L-1) -> [ev_pyr] FAST(all cells) -> octree -> [ev_blur] describe
+ *   side         :                   [ev_pyr] blur(all levels) ---------> [ev_blur]
  *
  * The blur needs only the pyramid, so it runs beside FAST and the octree (whose workgroups are
  * barrier/latency-bound); describe joins both. (The reference blurs only levels that kept
  * keypoints (ORBextractor.cc:1081); blurring every level changes no output, since describe
- * reads only levels with keypoints.) ORBX_SCHED=split also starts FAST on level 0 (which needs
- * only the input) beside the pyramid, and the octree waits for it [ev_fast0]; ORBX_SCHED=serial runs everything on `st` (A/B only), and
- * ORBX_SCHED=serial_blur_first does so with the blur right after the pyramid.
- * With stage profiling on, everything runs in order on `st` between timing events. */
-#ifndef ORBX_ERR_STICKY
-#define ORBX_ERR_STICKY 1  // device batch path: error flag sticky until orbx_check_error (0: reset every call)
-#endif
-constexpr bool kErrSticky = ORBX_ERR_STICKY != 0;
-#ifndef ORBX_BLUR_IN_PYR
-#define ORBX_BLUR_IN_PYR 0  // default of the ORBX_BLUR_IN_PYR env switch (1: blur fused into the whole-frame pyramid, -8.5 %, profiles/r03_ab_blur_in_pyr.log)
-#endif
-constexpr bool kBlurInPyrDefault = ORBX_BLUR_IN_PYR != 0;
+ * reads only levels with keypoints.) h->serial (orbx_debug_serial, a measurement hook) runs every
+ * stage in order on `st`, so each kernel runs alone. */
 /* Error words of h->err: kErrSticky (word 0) collects the device batch paths' flags until orbx_check_error
  * takes them; kErrCall (word 1) is the host paths' per-call flag (zeroed and read by each call), so a host
  * call never erases an unread batch error; kErrTake (word 32) receives the atomic read-and-clear. */
@@ -577,70 +524,39 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     Geometry& g = h->geo;
     const ExtractParams& ep = g.ep;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
-    static const int sched = [] {
-        const char* e = getenv("ORBX_SCHED");
-        return !e ? 0 : (!strcmp(e, "split") ? 1 : (!strcmp(e, "serial") ? 2 : (!strcmp(e, "serial_blur_first") ? 3 : 0)));
-    }();
-    const bool serial = sched == 2 || sched == 3;
-    const bool blur_first = sched == 3;
-    const bool split = !serial && sched == 1;
-    const int ncell0 = split ? g.lv[0].ncells : 0;
-    hipStream_t sd = serial ? st : h->side;
+    hipStream_t sd = h->serial ? st : h->side;
     // the host-buffer paths report their own per-call word; the device batch path leaves word 0 sticky
     // until orbx_check_error takes (and clears) it, so no fill kernel sits on the batch stream every call
     int* errp = h->err.as<int>() + (host_call ? kErrWordCall : kErrWordSticky);
-    if (host_call || !kErrSticky) HIPR(hipMemsetAsync(errp, 0, sizeof(int), st));
-    if (split) {
-        HIPR(hipEventRecord(h->ev_fork, st));
-        HIPR(hipStreamWaitEvent(sd, h->ev_fork, 0));
-        if (launch_fast(h, d_frames, fstride, pitch, 0, ncell0, nframes, sd)) return ORBX_EDEVICE;
-        HIPR(hipEventRecord(h->ev_fast0, sd));  // the octree (on st) reads level 0's cell keys
-    }
+    if (host_call) HIPR(hipMemsetAsync(errp, 0, sizeof(int), st));
     if (prof_mark(h, 0, 0, st)) return ORBX_EDEVICE;
-    // the whole-frame pyramid may blur every level itself (ORBX_BLUR_IN_PYR); then no blur launch
-    static const bool blur_in_pyr = [] {
-        const char* e = getenv("ORBX_BLUR_IN_PYR");
-        return e ? atoi(e) != 0 : kBlurInPyrDefault;
-    }();
-    bool fused = false;
-    if (!skip_warm(1) && !(h->skip_mask & 1) &&
-        launch_pyramid(h, d_frames, fstride, pitch, nframes, st, blur_in_pyr ? h->blur.as<uint8_t>() : nullptr, &fused))
-        return ORBX_EDEVICE;
+    if (!(h->skip_mask & 1) && launch_pyramid(h, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 0, 1, st)) return ORBX_EDEVICE;
     if (!host_call && h->user_ev_pyr) HIPR(hipEventRecord(h->user_ev_pyr, st));
-    auto blur = [&](hipStream_t bs) -> int {
-        if (prof_mark(h, 3, 0, bs)) return ORBX_EDEVICE;
-        if (!fused && !skip_warm(8) && !(h->skip_mask & 8))
-            HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                                    nullptr, g.nbjobs, nullptr, nframes, bs));
-        return prof_mark(h, 3, 1, bs);
-    };
-    const bool side_blur = !serial && !fused;  // a fused blur is already on `st`, ahead of describe
-    if (side_blur) {
+    if (!h->serial) {
         HIPR(hipEventRecord(h->ev_pyr, st));
         HIPR(hipStreamWaitEvent(sd, h->ev_pyr, 0));
-        if (blur(sd)) return ORBX_EDEVICE;
-        HIPR(hipEventRecord(h->ev_blur, sd));
-    } else if (blur_first || (fused && !serial)) {
-        if (blur(st)) return ORBX_EDEVICE;
     }
+    if (prof_mark(h, 3, 0, sd)) return ORBX_EDEVICE;
+    if (!(h->skip_mask & 8))
+        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl, nullptr,
+                                g.nbjobs, nullptr, nframes, sd));
+    if (prof_mark(h, 3, 1, sd)) return ORBX_EDEVICE;
+    if (!h->serial) HIPR(hipEventRecord(h->ev_blur, sd));
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
-    if (!skip_warm(2) && !(h->skip_mask & 2) && launch_fast(h, d_frames, fstride, pitch, ncell0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
-    if (split) HIPR(hipStreamWaitEvent(st, h->ev_fast0, 0));
+    if (!(h->skip_mask & 2) && launch_fast(h, d_frames, fstride, pitch, 0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 1, 1, st) || prof_mark(h, 2, 0, st)) return ORBX_EDEVICE;
-    if (!skip_warm(4) && !(h->skip_mask & 4)) HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
-                       h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
-                       (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st));
+    if (!(h->skip_mask & 4))
+        HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
+                           h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
+                           (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st));
     if (prof_mark(h, 2, 1, st)) return ORBX_EDEVICE;
-    if (serial) {
-        if (!blur_first && blur(st)) return ORBX_EDEVICE;
-    } else if (side_blur) {
-        HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
-    }
+    if (!h->serial) HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     if (prof_mark(h, 4, 0, st)) return ORBX_EDEVICE;
-    if (!skip_warm(16) && !(h->skip_mask & 16)) HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                         h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
-                         g.d_ptab.as<int>(), nframes, st));
+    if (!(h->skip_mask & 16))
+        HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                             h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
+                             g.d_ptab.as<int>(), nframes, st));
     if (prof_mark(h, 4, 1, st)) return ORBX_EDEVICE;
     if (h->prof_on && h->prof_calls < kProfMaxCalls) h->prof_calls++;
     h->last_frames = d_frames;
@@ -679,10 +595,8 @@ int orbx_create(const orbx_params* p, int device, int max_width, int max_height,
     h->max_batch = max_batch;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_blur, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_fast0, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->ev_blur, hipEventDisableTiming) != hipSuccess) {
         orbx_destroy(h);
         return ORBX_EDEVICE;
     }
@@ -706,7 +620,7 @@ void orbx_destroy(orbx_handle* h) {
     h->geo.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     if (h->side) (void)hipStreamDestroy(h->side);
-    for (hipEvent_t e : {h->ev_fork, h->ev_pyr, h->ev_blur, h->ev_fast0})
+    for (hipEvent_t e : {h->ev_pyr, h->ev_blur})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
     if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
@@ -745,6 +659,12 @@ int orbx_set_pyramid_event(orbx_handle* h, void* event) {
 int orbx_debug_skip_stages(orbx_handle* h, int mask) {
     if (!h || mask < 0 || mask > 0x1F) return ORBX_EARG;
     h->skip_mask = mask;
+    return 0;
+}
+
+int orbx_debug_serial(orbx_handle* h, int on) {
+    if (!h) return ORBX_EARG;
+    h->serial = on != 0;
     return 0;
 }
 
@@ -923,8 +843,8 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int width, int height, size
         return ORBX_EDEVICE;
     const void* after[4] = {h->in_frame.p, h->out_kps.p, h->out_desc.p, h->out_cnt.p};
     if (memcmp(before, after, sizeof(before))) h->epoch++;
-    static const bool no_graph = getenv("ORBX_NO_GRAPH") != nullptr;
-    if (!no_graph && !h->prof_on) return extract_graph(h, img, width, height, pitch, kps, desc, cap, n);
+    // captured graph, except while stage profiling (its events are recorded per call)
+    if (!h->prof_on) return extract_graph(h, img, width, height, pitch, kps, desc, cap, n);
     HIPR(hipMemcpy2DAsync(h->in_frame.p, width, img, pitch, width, height, hipMemcpyHostToDevice, h->stream));
     rc = run_extract(h, 1, h->in_frame.as<uint8_t>(), (long long)width * height, width, h->out_kps.as<orbx_kp>(),
                      h->out_desc.as<uint8_t>(), h->out_cnt.as<int32_t>(), K, h->stream);
@@ -1174,14 +1094,10 @@ namespace {
  * call_tail), so polling that word ends the call ~5 us sooner than hipStreamSynchronize
  * (tools/latency_floor.hip, profiles/r03_latency_floor.jsonl). The launch needs no further wait: the
  * next call's copies and launches are ordered behind it on the stream. A stream that drains without
- * the word, or an error, is ORBX_EDEVICE. ORBX_SYNC_WAIT=1 synchronises the stream instead (A/B). */
+ * the word, or an error, is ORBX_EDEVICE. */
 template <class Ready>
 int wait_until(hipStream_t st, Ready ready) {
-    static const bool sync_wait = [] {
-        const char* e = getenv("ORBX_SYNC_WAIT");
-        return e && atoi(e) != 0;
-    }();
-    if (!sync_wait) {
+    {
         // spin (with a pause) for the first ~200 us, which covers a call that is not queued behind other GPU
         // work; after that yield the core to the other SLAM threads between polls instead of burning it
         const auto t0 = std::chrono::steady_clock::now();
@@ -1436,7 +1352,7 @@ static int node_feats(const orbm_kf_view* v) { return v->n_nodes ? v->node_off[v
 /* ---- small per-call matchers (k_bow_small / k_tri_small): common nodes and per-call MapPoint bits in the
  * kernel arguments, node-ordered keyframe data from the keyframe cache or read by the kernel straight from
  * the pinned staging (zero copy: each element is read once, by one lane, so no H2D copy and no copy kernel
- * precede the launch; ORBX_SMALL_H2D=1 uploads it first instead, A/B), accepts + per-task done words written
+ * precede the launch), accepts + per-task done words written
  * to host memory, the rotation histogram on the host ---- */
 struct SmallSide {
     const uint4* d = nullptr;
@@ -1497,13 +1413,6 @@ static SmallSide small_stage(const orbm_kf_view* v, const KfEntry* ce, const Sma
     s.a = (const float*)(dbase + p.orec);
     s.f = (const int32_t*)(dbase + p.of);
     return s;
-}
-static bool small_h2d() {
-    static const bool h2d = [] {
-        const char* e = getenv("ORBX_SMALL_H2D");
-        return e && atoi(e) != 0;
-    }();
-    return h2d;
 }
 /* per node position: bit set when pred(feature index) */
 template <class Pred>
@@ -1567,13 +1476,11 @@ static int bow_small(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view* 
     SmallPlan pq, pc;
     small_plan(cv, vq, cq, pq, true);
     small_plan(cv, vc, cc, pc, true);
-    const size_t in_bytes = small_h2d() ? cv.off : 0;
     const size_t o_out = cv.take(8 * (size_t)std::max(pq.nf, 1));
     const size_t o_done = cv.take(8 * (size_t)nt);
-    if (in_bytes && ctx->scratch.ensure(in_bytes)) return ORBX_EDEVICE;
     uint8_t* hp = ctx->ensure_pinned(cv.off);
     if (!hp) return ORBX_EDEVICE;
-    uint8_t* dbase = in_bytes ? ctx->scratch.as<uint8_t>() : (uint8_t*)ctx->pinned_on_device(0);
+    uint8_t* dbase = (uint8_t*)ctx->pinned_on_device(0);
     BowSmall a;
     memset(&a, 0, sizeof(a));
     const SmallSide sq = small_stage(vq, cq, pq, hp, dbase), sc = small_stage(vc, cc, pc, hp, dbase);
@@ -1597,7 +1504,6 @@ static int bow_small(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view* 
     // the polled words start at 0, which no call carries (seq >= 1): a word left by an earlier call on this
     // context (another layout, or the same bits by chance) can never read as this call's
     memset(hp + o_out, 0, cv.off - o_out);
-    if (in_bytes) HIPR(hipMemcpyAsync(dbase, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     HIPR(launch_bow_small(a, ctx->stream));
     return small_finish(ctx, hp, o_out, o_done, a.tasks, nt, (uint32_t)a.seq, check_ori, out, nout, nmatches);
 }
@@ -1612,13 +1518,11 @@ static int tri_small(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view*
     SmallPlan p1, p2;
     small_plan(cv, kf1, c1, p1, false);
     small_plan(cv, kf2, c2, p2, false);
-    const size_t in_bytes = small_h2d() ? cv.off : 0;
     const size_t o_out = cv.take(8 * (size_t)std::max(p1.nf, 1));
     const size_t o_done = cv.take(8 * (size_t)nt);
-    if (in_bytes && ctx->scratch.ensure(in_bytes)) return ORBX_EDEVICE;
     uint8_t* hp = ctx->ensure_pinned(cv.off);
     if (!hp) return ORBX_EDEVICE;
-    uint8_t* dbase = in_bytes ? ctx->scratch.as<uint8_t>() : (uint8_t*)ctx->pinned_on_device(0);
+    uint8_t* dbase = (uint8_t*)ctx->pinned_on_device(0);
     TriSmall a;
     memset(&a, 0, sizeof(a));
     const SmallSide s1 = small_stage(kf1, c1, p1, hp, dbase), s2 = small_stage(kf2, c2, p2, hp, dbase);
@@ -1640,18 +1544,10 @@ static int tri_small(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view*
     a.c_ur = kf2->uright != nullptr;
     make_geom(a.g, F12, ex, ey, kf2->nlevels, kf2->scale_factors, kf2->level_sigma2);
     memset(hp + o_out, 0, cv.off - o_out);  // polled words: 0 is no call's seq (bow_small)
-    if (in_bytes) HIPR(hipMemcpyAsync(dbase, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     HIPR(launch_tri_small(a, ctx->stream));
     return small_finish(ctx, hp, o_out, o_done, a.tasks, nt, (uint32_t)a.seq, check_ori, match12, kf1->n, nmatches);
 }
 
-static bool small_off() {
-    static const bool off = [] {
-        const char* e = getenv("ORBX_SMALL");
-        return e && atoi(e) == 0;
-    }();
-    return off;
-}
 
 /* c1 / c2: the keyframes' cached device arrays (orbm_kf_cache), or nullptr to upload them with the call */
 static int tri_common(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2, const float F12[9], float ex,
@@ -1674,7 +1570,7 @@ static int tri_common(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view
     }
     int max_nc = 0;
     for (const NodeTask& t : tasks) max_nc = std::max(max_nc, t.c_end - t.c_begin);
-    if (!small_off() && max_nc <= 256 && tasks.size() <= (size_t)kSmallTasks && kf1->n <= 65535 && kf2->n <= 65535 &&
+    if (max_nc <= 256 && tasks.size() <= (size_t)kSmallTasks && kf1->n <= 65535 && kf2->n <= 65535 &&
         node_feats(kf1) <= 32 * kSmallBitWords && node_feats(kf2) <= 32 * kSmallBitWords)
         return tri_small(ctx, kf1, kf2, tasks, F12, ex, ey, only_stereo, check_ori, match12, nmatches, c1, c2);
     // one H2D copy (views, tasks), one launch whose last workgroup writes the (rotation-filtered)
@@ -1737,7 +1633,7 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
         if (nmatches) *nmatches = 0;
         return 0;
     }
-    if (!small_off() && max_nc <= 64 && vq->n <= 65535 && vc->n <= 65535 && tasks.size() <= (size_t)kSmallTasks && node_feats(vq) <= 32 * kSmallBitWords &&
+    if (max_nc <= 64 && vq->n <= 65535 && vc->n <= 65535 && tasks.size() <= (size_t)kSmallTasks && node_feats(vq) <= 32 * kSmallBitWords &&
         node_feats(vc) <= 32 * kSmallBitWords)
         return bow_small(ctx, vq, vc, tasks, nnratio, check_ori, mode, out, nout, nmatches, cq, cc);
     // one H2D copy, one launch (greedy per node; the last workgroup's rotation filter writes the
@@ -1795,7 +1691,6 @@ int orbm_triangulation_bf_batch_device(orbm_ctx* ctx, int npairs, const int32_t*
     MatchGeom g;
     make_geom(g, F12, ex, ey, nlevels, scale_factors, level_sigma2);
     hipStream_t st = (hipStream_t)stream;
-    if (skip_warm(32)) return 0;
     HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * npairs, st));
     HIPR(launch_tri_bf(npairs, d_q1, d_q2, d_kps, d_desc, d_counts, kp_stride, g, d_match12, d_nmatches, st));
     if (check_ori)
@@ -2021,6 +1916,34 @@ int orbm_check_error(orbm_ctx* ctx, void* stream) {
     return flag ? ORBX_EDEVICE : 0;
 }
 
+int orbm_search_by_bow_slots_device(orbm_ctx* ctx, const orbx_kf_source* query, int cap1, int nref,
+                                    const uint8_t* d_slots, size_t slot_bytes, float nnratio, int check_ori,
+                                    int max_nodes, int32_t* d_match, int32_t* d_nmatches, void* stream) {
+    if (!ctx || !query || !query->kps || !query->desc || !query->count || !query->fv_node || !query->fv_off ||
+        !query->fv_feat || !query->nfv || cap1 < 1 || cap1 > 65535 || nref < 0 || max_nodes < 0 || max_nodes > cap1 ||
+        (nref > 0 && (!d_slots || !d_match || !d_nmatches)) || slot_bytes < kSlotBodyOff)
+        return ORBX_EARG;
+    if (nref == 0) return 0;
+    HIPR(hipSetDevice(ctx->device));
+    QueryKF q;
+    memset(&q, 0, sizeof(q));
+    q.kps = query->kps;
+    q.mpf = query->mp_flags;
+    q.desc = query->desc;
+    q.count = query->count;
+    q.fv_node = query->fv_node;
+    q.fv_off = query->fv_off;
+    q.fv_feat = query->fv_feat;
+    q.nfv = query->nfv;
+    q.cap = cap1;
+    hipStream_t st = (hipStream_t)stream;
+    HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * (size_t)nref, st));
+    HIPR(hipMemsetAsync(d_match, 0xFF, sizeof(int32_t) * (size_t)nref * cap1, st));
+    HIPR(launch_bow_slots(q, d_slots, (long long)slot_bytes, nref, nnratio, check_ori ? 1 : 0, max_nodes, d_match,
+                          d_nmatches, ctx->err.as<int32_t>(), st));
+    return 0;
+}
+
 int orbm_search_for_triangulation_slots_device(orbm_ctx* ctx, const orbx_kf_source* query, int cap1, int nref,
                                                const uint8_t* d_slots, size_t slot_bytes, const orbm_slot_geom* geom,
                                                int use_bow, int max_nodes, int32_t* d_match, int32_t* d_nmatches,
@@ -2116,10 +2039,7 @@ bool frame_view_ok(const orbm_frame_view* F) {
 }
 
 /* uploads the Frame side + queries, runs k_grid / k_proj_scan / k_proj_resolve, downloads */
-#ifndef ORBX_PROJ_DIRECT
-#define ORBX_PROJ_DIRECT 1  // Fuse: results written by the scan kernel (0: through k_proj_resolve)
-#endif
-constexpr bool kProjDirect = ORBX_PROJ_DIRECT != 0;
+constexpr bool kProjDirect = true;  // Fuse: results written by the scan kernel (no k_proj_resolve wave)
 /* init_n >= 0: SearchForInitialization (k_init_resolve) with F = F2 and match[] = vnMatches12 of F1's init_n
  * keypoints; otherwise match[] has F->n entries */
 /* ce: the frame's cached device arrays and grid (orbm_kf_cache): only the queries travel, no k_grid */

@@ -12,6 +12,11 @@
  *                   16 queries x 16 candidate slices per workgroup, candidate tiles in LDS
  *   k_tri_slots_bow the common BoW nodes of the query's and the slot's FeatureVectors: one
  *                   wave per query node, binary search for the slot's node, lane per query
+ *   k_bow_slots     cross-agent SearchByBoW(KF,KF) (ORBmatcher.cc:522-655), the loop-candidate match
+ *                   LoopClosing::ComputeSim3 runs on a received keyframe (LoopClosing.cc:265): one wave
+ *                   per common node, the node's greedy chain over its queries in order, lane per
+ *                   candidate, best / second best by DPP minima
+ *   k_rot_slots     its rotation histogram + ComputeThreeMaxima filter and the per-slot count
  * Every received slot is validated on the device before use (header, sizes, counts, CSR
  * bounds); a bad slot yields no matches and raises the matcher's error flag.
  */
@@ -20,6 +25,7 @@
 
 #include "../../include/orbslam_amd.h"
 #include "orb_slot.h"
+#include "orb_wave.h"
 
 namespace orbamd {
 
@@ -385,6 +391,154 @@ __global__ __launch_bounds__(64) void k_tri_slots_bow(const QueryKF q, const uin
 }
 
 /* ----------------------------------------------------------------------------------- */
+/* Cross-agent SearchByBoW(KF1 = this agent's keyframe, KF2 = slot r) (ORBmatcher.cc:522-655). */
+/* Block (i, slot) takes query node i; if the slot has the node (the reference's merge walk    */
+/* visits exactly the common node ids), the node's queries run in order (:554): a query with   */
+/* a good MapPoint (:558-562) takes the first strict minimum over the node's not yet matched   */
+/* candidates with a good MapPoint (:571-592; vbMatched2 can only hold this node's candidates: */
+/* a feature sits in one node), best2 = the minimum over the others; accept iff best1 < TH_LOW */
+/* and (float)best1 < nnratio * (float)best2 (:594-598). Lane j holds candidates j, j+64, ...; */
+/* its local first minimum and runner-up merge by two wave minima of (dist << 16 | position).  */
+/* match[r*cap1 + idx1] = the slot keyframe's feature idx2 (preset to -1 by the caller).       */
+/* ----------------------------------------------------------------------------------- */
+__global__ __launch_bounds__(64) void k_bow_slots(const QueryKF q, const uint8_t* __restrict__ slots, long long slot_bytes,
+                                                  int slot0, float nnratio, int lds_cap, int32_t* __restrict__ match,
+                                                  int32_t* __restrict__ err) {
+    extern __shared__ uint8_t matched[];  // per candidate position of the slot's node (vbMatched2)
+    const int gr = blockIdx.y, r = slot0 + gr, i = blockIdx.x, lane = threadIdx.x;
+    SlotRef s;
+    if (!slot_open(slots + (long long)r * slot_bytes, slot_bytes, s)) {
+        if (i == 0 && lane == 0) atomicOr(err, 4);
+        return;
+    }
+    const int nfv1 = min(max(*q.nfv, 0), q.cap);
+    if (i == 0 && lane == 0 && nfv1 > (int)gridDim.x) atomicOr(err, 2);  // query nodes past max_nodes
+    if (i >= nfv1) return;
+    const uint32_t node = q.fv_node[i];
+    int lo = 0, hi = s.nfv;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s.fv_node[mid] < node) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo >= s.nfv || s.fv_node[lo] != node) return;  // not a common node
+    const int cb = min(max(s.fv_off[lo], 0), s.cap);
+    const int ce = min(max(s.fv_off[lo + 1], cb), s.cap);
+    const int nc = ce - cb;
+    if (nc > lds_cap) {
+        if (lane == 0) atomicOr(err, 8);
+        return;
+    }
+    const int qb = min(max(q.fv_off[i], 0), q.cap);
+    const int qe = min(max(q.fv_off[i + 1], qb), q.cap);
+    const int n1 = min(max(*q.count, 0), q.cap);
+    for (int j = lane; j < nc; j += 64) matched[j] = 0;
+    __syncthreads();
+    int32_t* out = match + (long long)r * q.cap;
+    for (int qi = qb; qi < qe; qi++) {  // wave-uniform
+        const int idx1 = q.fv_feat[qi];
+        if ((unsigned)idx1 >= (unsigned)n1) {
+            if (lane == 0) atomicOr(err, 8);
+            continue;
+        }
+        if (!q.mpf || (q.mpf[idx1] & 3) != 1) continue;  // pMP1 NULL or bad (:558-562)
+        const uint4* d = (const uint4*)(q.desc + (long long)idx1 * 32);
+        const uint4 a0 = d[0], a1 = d[1];
+        int b1 = 256, i1 = -1, b2 = 256;
+        for (int j = lane; j < nc; j += 64) {
+            if (matched[j]) continue;
+            const int idx2 = s.fv_feat[cb + j];
+            if ((unsigned)idx2 >= (unsigned)s.n) {
+                atomicOr(err, 4);
+                continue;
+            }
+            if ((s.mpf[idx2] & 3) != 1) continue;  // pMP2 NULL or bad (:575-579)
+            const uint4* cd = (const uint4*)(s.desc + (long long)idx2 * 32);
+            const uint4 c0 = cd[0], c1 = cd[1];
+            const int dist = __popc(a0.x ^ c0.x) + __popc(a0.y ^ c0.y) + __popc(a0.z ^ c0.z) + __popc(a0.w ^ c0.w) +
+                             __popc(a1.x ^ c1.x) + __popc(a1.y ^ c1.y) + __popc(a1.z ^ c1.z) + __popc(a1.w ^ c1.w);
+            if (dist < b1) {
+                b2 = b1;
+                b1 = dist;
+                i1 = j;
+            } else if (dist < b2) {
+                b2 = dist;
+            }
+        }
+        // the first strict minimum over all lanes = min of (dist << 16 | position); best2 = the minimum over every
+        // other eligible candidate: the owner lane's runner-up, every other lane's own minimum
+        const uint32_t k1 = i1 >= 0 ? ((uint32_t)b1 << 16) | (uint32_t)i1 : 0xFFFFFFFFu;
+        const uint32_t kmin = wave_min_u32(k1);
+        const bool owner = kmin != 0xFFFFFFFFu && k1 == kmin;
+        const uint32_t bd2 = wave_min_u32(owner ? (uint32_t)b2 : (uint32_t)b1);
+        if (kmin == 0xFFFFFFFFu) continue;
+        const int best1 = (int)(kmin >> 16), pos = (int)(kmin & 0xFFFFu);
+        if (best1 < 50 && __fmul_rn(1.0f, (float)best1) < __fmul_rn(nnratio, (float)bd2)) {  // TH_LOW, :594-598
+            if (lane == 0) {
+                matched[pos] = 1;
+                out[idx1] = s.fv_feat[cb + pos];
+            }
+            __syncthreads();
+        }
+    }
+}
+
+/* the rotation consistency of k_bow_slots' matches (ORBmatcher.cc:600-611, 633-650): rot = angle1 - angle2,
+ * bin = round(rot / 30) mod 30, ComputeThreeMaxima (:1601-1642), every match outside the three bins dropped;
+ * then nmatches[r] = the matches kept. One workgroup per slot. */
+__global__ __launch_bounds__(256) void k_rot_slots(const QueryKF q, const uint8_t* __restrict__ slots,
+                                                   long long slot_bytes, int slot0, int check_ori,
+                                                   int32_t* __restrict__ match, int32_t* __restrict__ nmatches) {
+    __shared__ int hist[32];
+    __shared__ int keep[3];
+    const int r = slot0 + blockIdx.x, tid = threadIdx.x;
+    SlotRef s;
+    if (!slot_open(slots + (long long)r * slot_bytes, slot_bytes, s)) return;  // flagged by k_bow_slots
+    const int n1 = min(max(*q.count, 0), q.cap);
+    int32_t* m = match + (long long)r * q.cap;
+    auto bin_of = [&](int i, int j) {
+        float rot = __fsub_rn(q.kps[i].angle, s.kps[j].angle);  // vKeysUn angle = vKeys angle
+        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+        const int bin = (int)roundf(__fmul_rn(rot, 1.0f / 30));
+        return bin == 30 ? 0 : bin;
+    };
+    if (tid < 32) hist[tid] = 0;
+    __syncthreads();
+    if (check_ori) {
+        for (int i = tid; i < n1; i += 256)
+            if (m[i] >= 0) atomicAdd(&hist[bin_of(i, m[i])], 1);
+        __syncthreads();
+        if (tid == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int b = 0; b < 30; b++) {
+                const int v = hist[b];
+                if (v > max1) { max3 = max2; max2 = max1; max1 = v; ind3 = ind2; ind2 = ind1; ind1 = b; }
+                else if (v > max2) { max3 = max2; max2 = v; ind3 = ind2; ind2 = b; }
+                else if (v > max3) { max3 = v; ind3 = b; }
+            }
+            if (max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
+            else if (max3 < __fmul_rn(0.1f, (float)max1)) { ind3 = -1; }
+            keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
+        }
+        __syncthreads();
+    }
+    int local = 0;
+    for (int i = tid; i < n1; i += 256) {
+        const int j = m[i];
+        if (j < 0) continue;
+        if (check_ori) {
+            const int bin = bin_of(i, j);
+            if (bin != keep[0] && bin != keep[1] && bin != keep[2]) {
+                m[i] = -1;
+                continue;
+            }
+        }
+        local++;
+    }
+    if (local) atomicAdd(&nmatches[r], local);
+}
+
+/* ----------------------------------------------------------------------------------- */
 /* Read-and-clear of a sticky device error word in one atomic step (orbx_check_error,      */
 /* orbm_check_error): a kernel on another stream that raises the flag after the exchange    */
 /* leaves it set for the next check instead of racing a host-side clear.                   */
@@ -434,6 +588,20 @@ hipError_t launch_tri_slots(const QueryKF& q, const uint8_t* slots, long long sl
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_bow_slots(const QueryKF& q, const uint8_t* slots, long long slot_bytes, int nref, float nnratio,
+                            int check_ori, int max_nodes, int32_t* match, int32_t* nmatches, int32_t* err,
+                            hipStream_t st) {
+    if (nref == 0) return hipSuccess;
+    if (max_nodes > 0) {
+        hipLaunchKernelGGL(k_bow_slots, dim3(max_nodes, nref), dim3(64), (size_t)q.cap, st, q, slots, slot_bytes, 0,
+                           nnratio, q.cap, match, err);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_rot_slots, dim3(nref), dim3(256), 0, st, q, slots, slot_bytes, 0, check_ori, match, nmatches);
+    return hipGetLastError();
 }
 
 }  // namespace orbamd

@@ -21,9 +21,6 @@
 #include "orb_math.h"
 #include "orb_pattern.h"
 
-#ifndef ORBX_FAST_STOP
-#define ORBX_FAST_STOP 0  // phase-cost experiment only (tools/exp_fast_phases.sh): >0 cuts k_fast_cells2 short
-#endif
 
 namespace orbamd {
 
@@ -368,133 +365,27 @@ struct PyrColGroup {
 };
 static_assert(sizeof(PyrColGroup) == 48, "PyrColGroup layout");
 
-/* FLAT (ORBX_PYR_FLAT): items = (row, column group) pairs of the level numbered row-major and dealt
- * to the threads round-robin, so every thread has an item in every pass but the last (the fixed
- * column per thread leaves NT - (NT / gw) * gw threads idle: 22 % of a 512-thread workgroup at
- * 640x480's level 1); the level's column-group table is staged in LDS beside the row table and read
- * per item. Every output byte is computed by the same operations either way. */
-/* BLUR (ORBX_BLUR_IN_PYR): the workgroup also blurs every level (GaussianBlur 7x7, ORBextractor.cc:
- * 1085-1086; the blur_job of k_blur_strips, same arithmetic) while the level is L2-resident: level l-1 is
- * complete once level l's pass starts, so its blur jobs run in that pass after each wave's resize rows
- * (no extra barrier), and the last level's after the loop. The frame's blurred levels need no separate
- * launch or HBM re-read. (One band per frame only.) */
-template <int U, int NT, bool FLAT, bool BLUR>
+template <int U, int NT>
 __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
                                                          int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
                                                          const LevelDesc* __restrict__ levels,
-                                                         const int* __restrict__ ptab, const int2* __restrict__ bands,
-                                                         int rt_cap, uint8_t* __restrict__ blur) {
-    // the current level's row table (this band's rows); sized at launch for the longest band range
-    // (rows x 16 B: 6.4 KB at 640x480 with one band) instead of kPyrMaxRows, so the LDS the long-lived
-    // pyramid workgroup holds stays free for the other graphs' FAST / describe workgroups beside it
+                                                         const int* __restrict__ ptab) {
+    // the current level's row table; sized at launch for the tallest level >= 1 (rows x 16 B: 6.4 KB at
+    // 640x480) instead of kPyrMaxRows, so the LDS the long-lived pyramid workgroup holds stays free for the
+    // other graphs' FAST / describe workgroups beside it
     extern __shared__ int4 s_rt[];
-    __shared__ __align__(16) uint8_t s_blur[BLUR ? NT / 64 : 1][7][kBlurSeg];
-    const int f = blockIdx.x / kPyrBands, band = blockIdx.x - f * kPyrBands, tid = threadIdx.x;
+    const int f = blockIdx.x, tid = threadIdx.x;
     uint8_t* P = pyr + (long long)f * ep.pyr_frame_bytes;
-    if (ORBX_PRIO_PYR > 0) __builtin_amdgcn_s_setprio(ORBX_PRIO_PYR);  // A/B knob: issue priority of the level chain
-    auto blur_level = [&](int lb) {
-        if constexpr (BLUR) {
-            const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-            const LevelDesc bl = levels[lb];
-            const uint8_t* img = lb == 0 ? frames + (long long)f * fstride : P + bl.pyr_off;
-            const int pitch = lb == 0 ? pitch0 : bl.pitch;
-            uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + bl.blur_off;
-            const int nstrips = (bl.w + 255) / 256, njobs = nstrips * ((bl.h + kBlurRows - 1) / kBlurRows);
-            for (int j = wave; j < njobs; j += NT / 64) blur_job<true>(img, pitch, bl, out, j % nstrips, j / nstrips,
-                                                                       s_blur[wave], lane);
-        }
-    };
     for (int l = 1; l < ep.L; l++) {
         const LevelDesc sv = levels[l - 1];
         const LevelDesc lv = levels[l];
         const uint8_t* src = l == 1 ? frames + (long long)f * fstride : P + sv.pyr_off;
         const int sp = l == 1 ? pitch0 : sv.pitch;
         uint8_t* dst = P + lv.pyr_off;
-        // rows [lo, hi) of this level: the band's own rows plus the rows the band's range of level l+1
-        // reads (recomputed here, so bands never wait on each other; overlapping rows are written by
-        // two workgroups with identical bytes)
-        const int2 rg = bands[band * kMaxLevels + l];
-        const int lo = rg.x, hi = rg.y;
+        const int hi = lv.h;
         const int4* rt = (const int4*)(ptab + lv.rt_off);
-        for (int i = tid; i < hi - lo; i += NT) s_rt[i] = rt[lo + i];
+        for (int i = tid; i < hi; i += NT) s_rt[i] = rt[i];
         const int gw = (lv.w + 3) >> 2;
-        if constexpr (FLAT) {
-            // gw x 3 int4: sel[4], alpha[4], (W, clamp dword, -, -); staged in LDS (ORBX_PYR_FLAT=1) or read
-            // through the L1 (2: the workgroup's LDS stays the row table alone)
-            const int4* cgt = (const int4*)(ptab + lv.cg_off);
-            const int4* s_cg = cgt;
-            if (kPyrFlatLds) {
-                int4* c = s_rt + rt_cap;
-                for (int i = tid; i < 3 * gw; i += NT) c[i] = cgt[i];
-                s_cg = c;
-            }
-            __syncthreads();
-            const int n = (hi - lo) * gw;
-            // row = item / gw by a multiply-high: exact for item * (M * gw - 2^32) < 2^32 (items < 2^21, gw < 2^10)
-            const uint32_t M = (uint32_t)((0x100000000ull + gw - 1) / gw);
-            for (int i0 = tid; i0 < n; i0 += U * NT) {
-                uint32_t w[U][2][3];
-                int4 rr[U];
-                int4 cs[U], ca[U];
-                int xg[U];
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int it = min(i0 + u * NT, n - 1);
-                    const int ry = (int)__umulhi((uint32_t)it, M);
-                    xg[u] = it - ry * gw;
-                    rr[u] = s_rt[ry];
-                    cs[u] = s_cg[3 * xg[u]];
-                    ca[u] = s_cg[3 * xg[u] + 1];
-                    const int2 wc = *(const int2*)&s_cg[3 * xg[u] + 2];
-                    const int A = wc.x & ~3;
-#pragma unroll
-                    for (int q = 0; q < 2; q++) {
-                        const int r = q ? rr[u].y : rr[u].x;
-                        const unsigned off = (unsigned)(r * sp + A);
-                        const uint2 lo2 = *(const uint2*)(src + off);
-                        w[u][q][0] = lo2.x;
-                        w[u][q][1] = lo2.y;
-                        w[u][q][2] = *(const uint32_t*)(src + min(off + 8u, (unsigned)(r * sp + wc.y)));
-                    }
-                    cs[u].w = (cs[u].w & 0x0F0F0F0F) | ((wc.x & 3) << 4);  // keep k = W & 3 beside sel[3]
-                }
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int it = i0 + u * NT;
-                    if (it >= n) break;
-                    const int y = lo + (int)__umulhi((uint32_t)it, M);
-                    const int x0 = 4 * xg[u];
-                    const int k = (cs[u].w >> 4) & 3;
-                    const int sel[4] = {cs[u].x, cs[u].y, cs[u].z, cs[u].w & 0x0F0F0F0F};
-                    const int alpha[4] = {ca[u].x, ca[u].y, ca[u].z, ca[u].w};
-                    const short2 b = __builtin_bit_cast(short2, rr[u].z);
-                    int h[2][4];
-#pragma unroll
-                    for (int q = 0; q < 2; q++) {
-                        const uint32_t lw = __builtin_amdgcn_alignbyte(w[u][q][1], w[u][q][0], k);
-                        const uint32_t hw = __builtin_amdgcn_alignbyte(w[u][q][2], w[u][q][1], k);
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const uint32_t pr = __builtin_amdgcn_perm(hw, lw, sel[i]);
-                            h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
-                                                             __builtin_bit_cast(short2v, alpha[i]), 0, false);
-                        }
-                    }
-                    const bool tail = x0 + 3 >= lv.simd_end;
-                    uint32_t packed = 0;
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        int v = ((__mul24(h[0][i] >> 4, (int)b.x) >> 16) + (__mul24(h[1][i] >> 4, (int)b.y) >> 16) + 2) >> 2;
-                        if (tail && x0 + i >= lv.simd_end) v = (__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
-                        packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
-                    }
-                    *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
-                }
-            }
-            blur_level(l - 1);
-            __syncthreads();
-            continue;
-        }
         const int R = NT / gw;  // rows per pass
         const int ry = tid / gw, xg = tid - ry * gw;
         const PyrColGroup cg = ((const PyrColGroup*)(ptab + lv.cg_off))[min(xg, gw - 1)];
@@ -504,84 +395,56 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
         __syncthreads();
         // one pass = U output rows of this thread's column group: the 2 x 3 source dwords of each (rows clamped,
         // so every load is valid and unconditional), then the taps
-        struct PassBuf {
-            uint32_t w[U][2][3];
-            int4 rr[U];
-        };
-        auto load_pass = [&](int y0, PassBuf& pb) {
+        if (ry < R) {
+            for (int y0 = ry; y0 < hi; y0 += U * R) {
+                uint32_t w[U][2][3];
+                int4 rr[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) pb.rr[u] = s_rt[min(y0 + u * R, hi - 1) - lo];
+                for (int u = 0; u < U; u++) rr[u] = s_rt[min(y0 + u * R, hi - 1)];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
+                for (int u = 0; u < U; u++) {
 #pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    const unsigned off = (unsigned)((q ? pb.rr[u].y : pb.rr[u].x) * sp + A);
-                    const uint2 lo2 = *(const uint2*)(src + off);
-                    pb.w[u][q][0] = lo2.x;
-                    pb.w[u][q][1] = lo2.y;
-                    pb.w[u][q][2] =
-                        *(const uint32_t*)(src + min(off + 8u, (unsigned)((q ? pb.rr[u].y : pb.rr[u].x) * sp + cg.pad[0])));
-                }
-            }
-        };
-        auto compute_pass = [&](int y0, const PassBuf& pb) {
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int y = y0 + u * R;
-                if (y >= hi) break;
-                const short2 b = __builtin_bit_cast(short2, pb.rr[u].z);
-                int h[2][4];
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    const uint32_t lw = __builtin_amdgcn_alignbyte(pb.w[u][q][1], pb.w[u][q][0], k);
-                    const uint32_t hw = __builtin_amdgcn_alignbyte(pb.w[u][q][2], pb.w[u][q][1], k);
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const uint32_t pr = __builtin_amdgcn_perm(hw, lw, cg.sel[i]);
-                        h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
-                                                         __builtin_bit_cast(short2v, cg.alpha[i]), 0, false);
+                    for (int q = 0; q < 2; q++) {
+                        const int r = q ? rr[u].y : rr[u].x;
+                        const unsigned off = (unsigned)(r * sp + A);
+                        const uint2 lo2 = *(const uint2*)(src + off);
+                        w[u][q][0] = lo2.x;
+                        w[u][q][1] = lo2.y;
+                        w[u][q][2] = *(const uint32_t*)(src + min(off + 8u, (unsigned)(r * sp + cg.pad[0])));
                     }
                 }
-                uint32_t packed = 0;
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    // taps < 2^20, weights <= 2048: 24-bit multiplies (full rate) are exact
-                    int v = ((__mul24(h[0][i] >> 4, (int)b.x) >> 16) + (__mul24(h[1][i] >> 4, (int)b.y) >> 16) + 2) >> 2;
-                    if (tail && x0 + i >= lv.simd_end) v = (__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
-                    packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
-                }
-                if (xg < gw) *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
-            }
-        };
-        if (ry < R) {
-            if (kPyrPipe) {
-                // software pipeline (ORBX_PYR_PIPE): the next pass's loads are issued before this pass's taps, so a
-                // thread always has one pass of rows in flight (two buffers, alternating; no register copies)
-                PassBuf pa, pb;
-                int y0 = lo + ry;
-                load_pass(y0, pa);
-                while (y0 < hi) {
-                    const int y1 = y0 + U * R;
-                    load_pass(y1, pb);  // clamped rows: harmless past the level's end
-                    compute_pass(y0, pa);
-                    if (y1 >= hi) break;
-                    const int y2 = y1 + U * R;
-                    load_pass(y2, pa);
-                    compute_pass(y1, pb);
-                    y0 = y2;
-                }
-            } else {
-                for (int y0 = lo + ry; y0 < hi; y0 += U * R) {
-                    PassBuf pb;
-                    load_pass(y0, pb);
-                    compute_pass(y0, pb);
+                for (int u = 0; u < U; u++) {
+                    const int y = y0 + u * R;
+                    if (y >= hi) break;
+                    const short2 b = __builtin_bit_cast(short2, rr[u].z);
+                    int h[2][4];
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const uint32_t lw = __builtin_amdgcn_alignbyte(w[u][q][1], w[u][q][0], k);
+                        const uint32_t hw = __builtin_amdgcn_alignbyte(w[u][q][2], w[u][q][1], k);
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const uint32_t pr = __builtin_amdgcn_perm(hw, lw, cg.sel[i]);
+                            h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
+                                                             __builtin_bit_cast(short2v, cg.alpha[i]), 0, false);
+                        }
+                    }
+                    uint32_t packed = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        // taps < 2^20, weights <= 2048: 24-bit multiplies (full rate) are exact
+                        int v = ((__mul24(h[0][i] >> 4, (int)b.x) >> 16) + (__mul24(h[1][i] >> 4, (int)b.y) >> 16) + 2) >> 2;
+                        if (tail && x0 + i >= lv.simd_end)
+                            v = (__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
+                        packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
+                    }
+                    if (xg < gw) *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
                 }
             }
         }
-        blur_level(l - 1);
         __syncthreads();
     }
-    blur_level(ep.L - 1);
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -589,86 +452,10 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
 /* A pixel is a cv::FAST corner at threshold t iff S > t, and then cornerScore<16> = S-1  */
 /* (threshold-independent), so one S map serves both thresholds of the cell fallback.    */
 /* ----------------------------------------------------------------------------------- */
-__device__ __forceinline__ int fast_strength(const uint8_t* p, int P) {
-    const int v = p[0];
-    int d[16];
-    d[0] = v - p[3 * P];
-    d[1] = v - p[1 + 3 * P];
-    d[2] = v - p[2 + 2 * P];
-    d[3] = v - p[3 + 1 * P];
-    d[4] = v - p[3];
-    d[5] = v - p[3 - 1 * P];
-    d[6] = v - p[2 - 2 * P];
-    d[7] = v - p[1 - 3 * P];
-    d[8] = v - p[-3 * P];
-    d[9] = v - p[-1 - 3 * P];
-    d[10] = v - p[-2 - 2 * P];
-    d[11] = v - p[-3 - 1 * P];
-    d[12] = v - p[-3];
-    d[13] = v - p[-3 + 1 * P];
-    d[14] = v - p[-2 + 2 * P];
-    d[15] = v - p[-1 + 3 * P];
-    int mn2[16], mx2[16], mn4[16], mx4[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
-    }
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-    }
-    int A = -1024, Bm = 1024;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        A = max(A, mn9);
-        Bm = min(Bm, mx9);
-    }
-    int S = max(A, -Bm);
-    return S < 0 ? 0 : S;
-}
-
-/* fast_strength with the dark and bright sides in the two i16 halves of one register:
- * X_k = (v - r_k, r_k - v), so one packed min/max chain yields (A, B') with
- * A = max_arc min(v - ring) and B' = max_arc min(ring - v) = -Bm; S = max(A, B', 0). */
-__device__ __forceinline__ int fast_strength_pk(const uint8_t* roi, int o, int P) {
-    int ow = o - 3 * P - 3;  // 7x7 window origin: every ring offset is a non-negative immediate
-    asm volatile("" : "+v"(ow));  // keep the origin as the DS base (no re-association into negative offsets)
-    const uint8_t* w = roi + ow;
-    const int v = w[3 * P + 3];
-    const short2v vp = {(short)v, (short)-v};
-    const short2v sg = {(short)-1, (short)1};
-    const int off[16] = {6 * P + 3, 6 * P + 4, 5 * P + 5, 4 * P + 6, 3 * P + 6, 2 * P + 6, P + 5, 4,
-                         3, 2, P + 1, 2 * P, 3 * P, 4 * P, 5 * P + 1, 6 * P + 2};
-    short2v x[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const short r = (short)w[off[k]];
-        const short2v rr = {r, r};
-        x[k] = rr * sg + vp;
-    }
-    short2v m2[16], m4[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(x[k], x[(k + 1) & 15]);
-#pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-    short2v a = {(short)-1024, (short)-1024};
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const short2v m9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), x[(k + 8) & 15]);
-        a = __builtin_elementwise_max(a, m9);
-    }
-    const int S = max((int)a.x, (int)a.y);
-    return S < 0 ? 0 : S;
-}
-
-/* fast_strength as packed f16 (integers in [-255, 255] are exact in f16, and min/max are exact):
+/* FAST strength S as packed f16 (integers in [-255, 255] are exact in f16, and min/max are exact):
  * X_k = (v - r_k, r_k - v) from the byte r_k as f16(1024 + r_k) = bits 0x6400 | r_k (one v_perm) and one
  * v_pk_fma_f16; every 9-arc minimum is min3(min3 of 3 consecutive) and the arc maximum a max3 tree, on
- * gfx950's v_pk_minimum3_f16 / v_pk_maximum3_f16: about half the min/max instructions of the i16 form. */
+ * gfx950's v_pk_minimum3_f16 / v_pk_maximum3_f16: about half the min/max instructions of a packed-i16 form. */
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int fast_strength_h2(const uint8_t* roi, int o, int P) {
     int ow = o - 3 * P - 3;  // 7x7 window origin: every ring offset is a non-negative immediate
@@ -714,30 +501,6 @@ __device__ __forceinline__ bool fast_survivor_c(const uint8_t* s, int P, int t, 
     const int mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
     return c > t && c > 1 && mx < c;
 }
-
-/* Candidate form (k_fast_cells2): a necessary condition for S > t_lo (any 9-arc contains two
- * cyclically adjacent cardinal ring points 0/4/8/12, so both are brighter or both darker) is
- * tested on every band pixel; survivors are compacted in row-major order with ballot+mbcnt
- * into an LDS list; S is computed only for them (full lanes), and the NMS/emission passes walk
- * the list, so emission order is still the reference's row-major order. Pixels that fail the
- * test have S <= t_lo <= t and are zero in the NMS buffer, exactly as in cv::FAST. */
-__device__ __forceinline__ bool fast_pretest(const uint8_t* p, int P, int t) {
-    const int v = p[0];
-    const int c0 = p[3 * P], c4 = p[3], c8 = p[-3 * P], c12 = p[-3];
-    const int hi = v + t, lo = v - t;
-    const bool b0 = c0 > hi, b4 = c4 > hi, b8 = c8 > hi, b12 = c12 > hi;
-    const bool d0 = c0 < lo, d4 = c4 < lo, d8 = c8 < lo, d12 = c12 < lo;
-    return (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
-}
-
-#ifndef ORBX_FAST_PRETEST2
-#define ORBX_FAST_PRETEST2 0  // A/B knob: k_fast_cells2 pretests two row passes per loop iteration
-#endif
-constexpr bool kFastPretest2 = ORBX_FAST_PRETEST2 != 0;
-#ifndef ORBX_FAST_S2
-#define ORBX_FAST_S2 0  // A/B knob: k_fast_cells2 computes the strength of two candidate chunks per loop iteration
-#endif
-constexpr bool kFastStrength2 = ORBX_FAST_S2 != 0;
 
 /* LDS bytes per wave of k_fast_cells2: ROI + S map (RP x RH each) + candidate list (u16 per
  * band pixel; a band is at most (RP-6) x (RH-6)) + 64 per-lane dummy slots of the compaction */
@@ -807,10 +570,6 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
         }
     }
     wave_sync();
-#if ORBX_FAST_STOP == 1
-    if (lane == 0) cellcnt[(long long)f * ep.ncells + ci] = 0;
-    return;
-#endif
     const int bw = c.w - 6, bh = c.h - 6;
     int total = 0;
     if (bw > 0 && bh > 0) {
@@ -885,17 +644,7 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
                     }
                     nrec += __popcll(Bk);
                 };
-                int r0 = 0;
-                if (kFastPretest2) {
-                    // two row passes per iteration: both passes' LDS reads are issued before either's record
-                    // store (the store may alias the ROI for the compiler), so their latencies overlap
-                    for (; r0 + rpc < bh; r0 += 2 * rpc) {
-                        const uint32_t ka = pretest(r0), kb = pretest(r0 + rpc);
-                        record(ka, r0);
-                        record(kb, r0 + rpc);
-                    }
-                }
-                for (; r0 < bh; r0 += rpc) record(pretest(r0), r0);
+                for (int r0 = 0; r0 < bh; r0 += rpc) record(pretest(r0), r0);
                 wave_sync();
                 // expand the records into the candidate list (order kept: records in order, pixels of a
                 // record ascending); the record area is zeroed behind, so str is the S map again (zero
@@ -930,23 +679,7 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
             // registers for the NMS pass: one dependent LDS read fewer
             const int e0 = lane < ncand ? (int)clist[lane] : 0;
             int s0 = 0;
-            int ibeg = 0;
-            if (kFastStrength2) {
-                // two 64-candidate chunks per iteration: every list and ring read of both is issued before either
-                // chunk's S-map store; a lane past the list computes S at a dummy in-band centre (row 3, col 3)
-                for (; ibeg + 64 < ncand; ibeg += 128) {
-                    const int ia = ibeg + lane, ib = ibeg + 64 + lane;
-                    const bool va = ia < ncand, vb = ib < ncand;
-                    const int ea = ibeg == 0 ? e0 : (va ? (int)clist[ia] : 0x303);
-                    const int eb = vb ? (int)clist[ib] : 0x303;
-                    const int oa = (ea >> 8) * RP + (ea & 0xFF), ob = (eb >> 8) * RP + (eb & 0xFF);
-                    const int Sa = fast_strength_h2(roi, oa, RP), Sb = fast_strength_h2(roi, ob, RP);
-                    if (va && Sa > t) str[oa] = (uint8_t)Sa;
-                    if (vb && Sb > t) str[ob] = (uint8_t)Sb;
-                    if (ibeg == 0) s0 = va && Sa > t ? Sa : 0;
-                }
-            }
-            for (int i0 = ibeg; i0 < ncand; i0 += 64) {
+            for (int i0 = 0; i0 < ncand; i0 += 64) {
                 const int i = i0 + lane;
                 if (i < ncand) {
                     const int e = i0 == 0 ? e0 : (int)clist[i];
@@ -1039,25 +772,6 @@ __device__ __forceinline__ int block_sum(int v, int* red) {
  *   sortkey   : NC x u64                                   =  8 NC
  *   keys      : KL x (4 + 2 + 1) (if n <= KL, else global scratch)
  */
-#ifndef ORBX_DESC_STOP
-#define ORBX_DESC_STOP 0  // phase-cost experiment only: >0 cuts k_describe short (results invalid)
-#endif
-#ifndef ORBX_OCT_STOP
-#define ORBX_OCT_STOP 0  // phase-cost experiment only: >0 cuts k_octree short (results invalid)
-#endif
-#ifndef ORBX_OCT_FLAT
-#define ORBX_OCT_FLAT 1
-#endif
-constexpr bool kOctFlatGather = ORBX_OCT_FLAT != 0;  // A/B switch (tools/build_variant.sh -DORBX_OCT_FLAT=0)
-#ifndef ORBX_OCT_FAST1
-#define ORBX_OCT_FAST1 1
-#endif
-constexpr bool kOctFastPhase1 = ORBX_OCT_FAST1 != 0;  // A/B switch (-DORBX_OCT_FAST1=0: general rounds only)
-#ifndef ORBX_OCT_RANK
-#define ORBX_OCT_RANK 1
-#endif
-constexpr bool kOctRankSort = ORBX_OCT_RANK != 0;  // A/B switch (-DORBX_OCT_RANK=0: bitonic phase-2 sort)
-
 /* node rectangles as u16 (level coordinates < 4096, the 12-bit key fields): 76 B of LDS per node
  * instead of 92, so a 256-node table plus 1888 keys fits 32 KB and five workgroups share a CU with
  * the other graphs' kernels */
@@ -1072,7 +786,6 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                                                 int* __restrict__ lvcnt, uint8_t* __restrict__ gscratch,
                                                 long long gscratch_frame_bytes, int NC, int KL,
                                                 int* __restrict__ err) {
-    if (ORBX_PRIO_OCT > 0) __builtin_amdgcn_s_setprio(ORBX_PRIO_OCT);  // A/B knob: issue priority of the barrier chain
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int red[8];
     __shared__ int sh_size, sh_jstar, sh_tc, sh_nexp, sh_ndiv;
@@ -1117,7 +830,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
     struct KeysGlobal { uint32_t* key; uint16_t* label; uint8_t* quad; };
     auto tail = [&](auto K) {
         carry = 0;
-        if (kOctFlatGather && 2 * lv.ncells + 2 <= 4 * NC) {
+        if (2 * lv.ncells + 2 <= 4 * NC) {
             // flat gather: the cells' key offsets and slots go to LDS (cnt4's space, unused until the roots),
             // then thread t copies keys t, t+256, ... finding each key's cell by a fixed-trip binary search, four
             // keys in flight per thread. (A thread per cell copying its keys one by one waited on one global
@@ -1178,10 +891,6 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         }
         __syncthreads();
         uint32_t* outk = lvkey + (long long)f * ep.kp_per_frame + lv.kp_off;
-#if ORBX_OCT_STOP == 1
-        if (tid == 0) lvcnt[f * ep.L + l] = 0;
-        return;
-#endif
         if (n == 0) {
             if (tid == 0) lvcnt[f * ep.L + l] = 0;
             return;
@@ -1221,10 +930,6 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         }
         __syncthreads();
         for (int i = tid; i < n; i += 256) K.label[i] = (uint16_t)spos[K.label[i]];
-#if ORBX_OCT_STOP == 2
-        if (tid == 0) lvcnt[f * ep.L + l] = 0;
-        return;
-#endif
         if (size > NC) {  // capacity overflow: flag it and leave this level empty (never a stale count)
             if (tid == 0) { atomicOr(err, 2); lvcnt[f * ep.L + l] = 0; }
             return;
@@ -1244,7 +949,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 __syncthreads();
             }
             cnt_clean = false;
-            if (kOctFastPhase1 && phase == 1 && size <= 256) {
+            if (phase == 1 && size <= 256) {
                 // Phase-1 round with every node in one thread (slot s = tid): every node with > 1 key divides,
                 // in list order, so one packed scan gives the children's creation indices, the survivors'
                 // positions and the number of children with > 1 key at once (4 barriers per round instead of
@@ -1354,13 +1059,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
             }
             __syncthreads();
             if (nD == 0) break;  // cannot happen while size changes, kept for safety
-#if ORBX_OCT_STOP == 3
             if (phase == 2) {
-                if (tid == 0) lvcnt[f * ep.L + l] = 0;
-                return;
-            }
-#endif
-            if (phase == 2 && kOctRankSort) {
                 // processing order = descending (size, creation) key; keys are unique (seq), so a node's
                 // rank is the number of larger keys: nD broadcast LDS reads per node and two barriers
                 // instead of a bitonic network's log2(P)(log2(P)+1)/2 barriers
@@ -1372,45 +1071,6 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 }
                 __syncthreads();
                 for (int j = tid; j < nD; j += 256) dflag[j] = dbase[j];
-                __syncthreads();
-            } else if (phase == 2) {
-                // bitonic sort of skey[0..P) descending; pad with 0
-                int P2 = 1;
-                while (P2 < nD) P2 <<= 1;
-                for (int i = nD + tid; i < P2; i += 256) skey[i] = 0ull;
-                __syncthreads();
-                for (int k = 2; k <= P2; k <<= 1) {
-                    for (int j = k >> 1; j > 0; j >>= 1) {
-                        for (int i = tid; i < P2; i += 256) {
-                            const int ixj = i ^ j;
-                            if (ixj > i) {
-                                const unsigned long long a = skey[i], b = skey[ixj];
-                                const bool desc = (i & k) == 0;
-                                if (desc ? (a < b) : (a > b)) { skey[i] = b; skey[ixj] = a; }
-                            }
-                        }
-                        __syncthreads();
-                    }
-                }
-                // map sorted keys back to slots: seq is unique -> search by seq
-                for (int j = tid; j < nD; j += 256) dbase[j] = 0;
-                __syncthreads();
-                for (int s = tid; s < size; s += 256) spos[s] = -1;
-                __syncthreads();
-                // slot lookup: for each D slot (in dflag), find its rank via binary search over skey
-                for (int j = tid; j < nD; j += 256) {
-                    const int s = dflag[j];
-                    const unsigned long long key = ((unsigned long long)(uint32_t)A.nk[s] << 32) | A.seq[s];
-                    int lo = 0, hi = nD - 1;
-                    while (lo < hi) {  // descending array: find index of key
-                        const int mid = (lo + hi) >> 1;
-                        if (skey[mid] > key) lo = mid + 1; else hi = mid;
-                    }
-                    spos[s] = lo;  // processing rank of slot s
-                }
-                __syncthreads();
-                for (int s = tid; s < size; s += 256)
-                    if (spos[s] >= 0) dflag[spos[s]] = s;
                 __syncthreads();
             }
             // children counts per processing position; prefix -> creation indices
@@ -1609,30 +1269,20 @@ __device__ constexpr PatTable kPatternT = make_pattern_table_t();
 constexpr int kDescPatchR = 18;                   // |round(rotated pattern coordinate)| <= 13*sqrt(2)
 constexpr int kDescPatchRows = 2 * kDescPatchR + 1;  // 37
 constexpr int kDescPatchPitch = 40;                 // 10 dwords: 37 columns + up to 3 bytes misalignment
-#ifndef ORBX_DESC_WAVES
-#define ORBX_DESC_WAVES 4
-#endif
-constexpr int kDescWaves = ORBX_DESC_WAVES;         // waves (x 4 keypoints) per k_describe workgroup
+constexpr int kDescWaves = 4;                      // waves (x 4 keypoints) per k_describe workgroup
 constexpr int kDescKps = 4 * kDescWaves;            // keypoints per workgroup
-#ifndef ORBX_DESC_PAT_GLOBAL
-#define ORBX_DESC_PAT_GLOBAL 0  // 1: rBRIEF pairs read from global (L1/L2) instead of an LDS copy (4 KB less LDS)
-#endif
-#ifndef ORBX_DESC_MINW
-#define ORBX_DESC_MINW 1        // __launch_bounds__ min waves per SIMD (6: VGPR budget 80)
-#endif
-constexpr bool kDescPatGlobal = ORBX_DESC_PAT_GLOBAL != 0;
 
 /* kEvenPitch: every row pitch is even (levels >= 1 always are; level 0 when the caller's pitch is), so the IC rows a
  * lane reads (2 rows apart) share one misalignment and their addresses are one running 32-bit offset */
 template <bool kEvenPitch>
-__global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
+__global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                   const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   ExtractParams ep, const LevelDesc* __restrict__ levels,
                                                   const uint32_t* __restrict__ lvkey, const int* __restrict__ lvcnt,
                                                   orbx_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
                                                   int* __restrict__ out_counts, int kp_stride,
                                                   const int* __restrict__ ptab) {
-    __shared__ PatPt s_pat[kDescPatGlobal ? 1 : 256];
+    __shared__ PatPt s_pat[256];
     __shared__ int2 s_ic[256];
     __shared__ __align__(8) uint8_t s_patch[kDescKps][kDescPatchRows * kDescPatchPitch];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1665,7 +1315,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
         // the transposed table, read and stored linearly (slot t): the 8 lanes of a ds_write_b128 group
         // write 128 consecutive bytes (a transposing store, slot (t % 16) * 16 + t / 16, put the group's
         // eight 16-byte words 256 bytes apart: one bank, an 8-way conflict)
-        if (!kDescPatGlobal) my_pat[q] = kPatternT.t[t];
+        my_pat[q] = kPatternT.t[t];
         my_ic[q] = ((const int2*)(ptab + ep.ic_off))[t];
     }
     const int g = (blk * kDescWaves + wave) * 4 + sub;  // octree output slot of this lane group
@@ -1680,7 +1330,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
     for (int q = 0; q < kTab; q++) {
         const int t = tid + q * NT;
         if (t >= 256) break;
-        if (!kDescPatGlobal) s_pat[t] = my_pat[q];  // pair p at (p % 16) * 16 + p / 16 (kPatternT's order)
+        s_pat[t] = my_pat[q];  // pair p at (p % 16) * 16 + p / 16 (kPatternT's order)
         s_ic[t] = my_ic[q];
     }
     if (blk == 0 && tid == 0) {
@@ -1755,11 +1405,6 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
             }
         }
     }
-#if ORBX_DESC_STOP == 1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase-cost experiment: staging only
-    if (wv[0].x == 0x12345678u && wv[15].y == 0x9abcdef0u) out_counts[f] = -1;  // keep the loads alive
-    return;
-#endif
     int m10, m01;
     {
         // per row ri = r + 2p: A' += sum (u+15) I, S += sum I, M' += 2p * sum I (24-bit multiply by a
@@ -1792,10 +1437,6 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
     float sa, ca;
     glibc_sincosf(theta, &sa, &ca);
     const float a = ca, b = sa;
-#if ORBX_DESC_STOP == 2
-    if (a == 12345.f && b == 54321.f) out_counts[f] = -1;  // phase-cost experiment: up to the angle / sincos
-    return;
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA patch writes have landed
     wave_sync();  // patch stores of the other lanes of this group
     const uint8_t* pc0 = patch + kDescPatchR * kDescPatchPitch + kDescPatchR + pmis;  // keypoint
@@ -1814,8 +1455,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_MINW) void k_describe(co
         for (int j = 0; j < 16; j++) {
             // global table: pairs fetched 4 steps at a time (a scheduling fence per group keeps the compiler
             // from hoisting all 16 loads, i.e. 64 live VGPRs)
-            if (kDescPatGlobal && (j & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-            const PatPt pp = kDescPatGlobal ? kPatternT.t[16 * j + ln] : s_pat[16 * j + ln];  // pair 16ln + j (transposed)
+            const PatPt pp = s_pat[16 * j + ln];  // pair 16ln + j (transposed)
             const float2v X = {pp.x0, pp.x1}, Y = {pp.y0, pp.y1};
             float2v R = (X * B2 + Y * A2) + MAG;  // rows    round(x*b + y*a) of points 0, 1
             float2v C = (X * A2 - Y * B2) + MAG;  // columns round(x*a - y*b)
@@ -1877,27 +1517,19 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 }
 
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
-                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, const int2* bands,
-                                 int max_rows, int max_groups, int nframes, hipStream_t st, uint8_t* blur) {
+                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int max_rows,
+                                 int max_groups, int nframes, hipStream_t st) {
     if (max_rows < 1 || max_rows > kPyrMaxRows) return hipErrorInvalidValue;
-    if (blur && kPyrBands != 1) return hipErrorInvalidValue;
     // 512-thread workgroups pack beside the other graphs' kernels while every level
     // keeps >= 2 rows per pass; a level 1 wider than 4 x 256 columns (C4's 1034) would leave half the
     // threads idle, so such geometries take 1024 threads
-    const dim3 grid(nframes * kPyrBands);
-    // flat items: the row table and the widest level's column-group table (3 int4 per group) in LDS
-    const size_t lds = (size_t)max_rows * sizeof(int4) + (kPyrFlatLds ? (size_t)max_groups * 3 * sizeof(int4) : 0);
-#define ORBX_PYR_LAUNCH(NTH, BL)                                                                               \
-    hipLaunchKernelGGL((k_pyramid_frames<kPyrU, NTH, kPyrFlat, BL>), grid, dim3(NTH), lds, st, frames, fstride, pitch0, \
-                       pyr, ep, levels, ptab, bands, max_rows, blur)
-    if (max_groups <= kPyrThreads / 2) {
-        if (blur) ORBX_PYR_LAUNCH(kPyrThreads, true);
-        else ORBX_PYR_LAUNCH(kPyrThreads, false);
-    } else {
-        if (blur) ORBX_PYR_LAUNCH(kPyrThreadsMax, true);
-        else ORBX_PYR_LAUNCH(kPyrThreadsMax, false);
-    }
-#undef ORBX_PYR_LAUNCH
+    const size_t lds = (size_t)max_rows * sizeof(int4);
+    if (max_groups <= kPyrThreads / 2)
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), dim3(nframes), dim3(kPyrThreads), lds, st, frames,
+                           fstride, pitch0, pyr, ep, levels, ptab);
+    else
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), dim3(nframes), dim3(kPyrThreadsMax), lds, st,
+                           frames, fstride, pitch0, pyr, ep, levels, ptab);
     return hipGetLastError();
 }
 
@@ -1934,10 +1566,7 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
                               int cell_hi, int nframes, hipStream_t st) {
     if (cell_hi <= cell_lo) return hipSuccess;
     dim3 grid((cell_hi - cell_lo + 3) / 4, nframes);
-#ifndef ORBX_FAST_LDS_MIN
-#define ORBX_FAST_LDS_MIN 0  // A/B knob: minimum LDS bytes per FAST workgroup (caps FAST's workgroups per CU)
-#endif
-    const size_t lds = std::max<size_t>(4 * (size_t)fast_wave_lds(RP, RH), ORBX_FAST_LDS_MIN);
+    const size_t lds = 4 * (size_t)fast_wave_lds(RP, RH);
 #define ORBX_FAST(MP, RPC)                                                                                        \
     hipLaunchKernelGGL((k_fast_cells2<MP, RPC>), grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, \
                        cells, cellkey, cellcnt, RP, RH, cell_lo, cell_hi)

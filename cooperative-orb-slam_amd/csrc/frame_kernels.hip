@@ -497,10 +497,7 @@ __device__ __forceinline__ int proj_scan(const ProjCall& c, const ProjQuery& q, 
     return ncand;
 }
 
-#ifndef ORBX_PROJ_TOPK
-#define ORBX_PROJ_TOPK 4  // candidate keys kept per query by the scan (A/B: more keys = fewer whole-wave rescans)
-#endif
-constexpr int kProjTopK = ORBX_PROJ_TOPK;
+constexpr int kProjTopK = 4;  // candidate keys kept per query by the scan (more keys = fewer whole-wave rescans)
 static_assert(kProjTopK >= 2 && kProjTopK <= 16, "the scan writes one key per lane of a 16-lane query group");
 int proj_topk() { return kProjTopK; }
 
@@ -639,14 +636,7 @@ __device__ __forceinline__ void rot_bins(const ProjCall& c, int lane, int* hist)
  * uncommitted lane of the chunk; that lane is re-filtered in the next round against the bitmap that
  * now holds those claims. A lane whose filtered list ran out while the list was truncated (more than
  * K candidates) is re-scanned by the whole wave against the bitmap. */
-#ifndef ORBX_RESOLVE_PROF
-#define ORBX_RESOLVE_PROF 0  // experiment only: call 0 prints its phase times (wall clock, 10 ns) and round counts
-#endif
 __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict__ calls) {
-#if ORBX_RESOLVE_PROF
-    const unsigned long long tp0 = wall_clock64();
-    int prof_rounds = 0, prof_rescans = 0;
-#endif
     __shared__ uint32_t s_occ[kProjMaxFeatures / 32];
     __shared__ int s_claim[kClaimTab];
     __shared__ int s_hist[32];
@@ -674,9 +664,6 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // one wave: order its own global accesses (no L2 write-back)
     wave_lds_sync();
     auto occ_get = [](int i) { return (s_occ[i >> 5] >> (i & 31)) & 1u; };
-#if ORBX_RESOLVE_PROF
-    const unsigned long long tp1 = wall_clock64();
-#endif
     const int need = c.ratio ? 2 : 1;  // list entries that decide the result
     for (int i = lane; i < kClaimTab; i += 64) s_claim[i] = 64;
     wave_lds_sync();
@@ -712,9 +699,6 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
         if (base + 64 < c.nq) load_chunk(base + 64, ntop, nncand, nflags, nsrc);
         int done = 0;  // lanes < done are committed
         while (done < 64 && base + done < c.nq) {
-#if ORBX_RESOLVE_PROF
-            prof_rounds++;
-#endif
             const bool act = in && lane >= done;
             unsigned long long b = kNoKey, s = kNoKey;
             int found = 0;
@@ -753,9 +737,6 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
             }
             wave_lds_sync();
             if (d < 64 && __shfl((int)rescan, d)) {  // whole-wave re-scan of query base+d
-#if ORBX_RESOLVE_PROF
-                prof_rescans++;
-#endif
                 const int qd = base + d;
                 const ProjQuery q = c.q[qd];
                 const uint4* qp = (const uint4*)(c.qdesc + (long long)qd * 32);
@@ -781,9 +762,6 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // one wave: order its own global accesses (no L2 write-back)
-#if ORBX_RESOLVE_PROF
-    const unsigned long long tp2 = wall_clock64();
-#endif
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) nacc += __shfl_xor(nacc, o);
     if (c.check_ori) {  // rotation consistency (ORBmatcher.cc:1437-1467)
@@ -828,16 +806,7 @@ __global__ __launch_bounds__(64) void k_proj_resolve(const ProjCall* __restrict_
         nacc -= removed;
     }
     if (lane == 0) *c.nmatches = nacc;
-#if ORBX_RESOLVE_PROF
-    const unsigned long long tp3 = wall_clock64();
-#endif
     if (c.host_out) host_put_matches(c, c.match, c.n, nacc, lane);
-#if ORBX_RESOLVE_PROF
-    const unsigned long long tp4 = wall_clock64();
-    if (blockIdx.x == 0 && lane == 0)
-        printf("RESOLVE_PROF nq %d init %llu chunks %llu ori %llu out %llu (x10ns) rounds %d rescans %d\n", c.nq,
-               tp1 - tp0, tp2 - tp1, tp3 - tp2, tp4 - tp3, prof_rounds, prof_rescans);
-#endif
 }
 
 /* ============================ SearchForInitialization ============================ */

@@ -15,8 +15,8 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
                          long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
                          int simd_end, int nframes, hipStream_t st);
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
-                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, const int2* bands,
-                                 int max_rows, int max_groups, int nframes, hipStream_t st, uint8_t* blur = nullptr);
+                                 const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int max_rows,
+                                 int max_groups, int nframes, hipStream_t st);
 hipError_t launch_resize_tiled(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
                                long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
                                int simd_end, int nframes, hipStream_t st);
@@ -67,6 +67,9 @@ hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* 
 hipError_t launch_flag_take(int32_t* flag, int32_t* out, hipStream_t st);
 hipError_t launch_pack_slot(const orbx_kf_source& src, const SlotLayout& L, const orbx_kf_meta& meta, uint8_t* slot,
                             int32_t* err, hipStream_t st);
+hipError_t launch_bow_slots(const QueryKF& q, const uint8_t* slots, long long slot_bytes, int nref, float nnratio,
+                            int check_ori, int max_nodes, int32_t* match, int32_t* nmatches, int32_t* err,
+                            hipStream_t st);
 hipError_t launch_tri_slots(const QueryKF& q, const uint8_t* slots, long long slot_bytes, int nref,
                             const orbm_slot_geom* geom, int use_bow, int max_nodes, int32_t* match,
                             int32_t* nmatches, int32_t* err, hipStream_t st);

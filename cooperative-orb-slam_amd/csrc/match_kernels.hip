@@ -1,10 +1,10 @@
 /*
  * match_kernels.hip -- gfx950 kernels for ORBmatcher (ORBmatcher.cc).
  *
- *   k_tri_bf          SearchForTriangulation, one FeatureVector node holding every feature
- *                     (BASELINE "BF"), batch of frame pairs; lane = query idx1, candidate
- *                     KF2 tile staged in LDS, descriptors compared as 8 x u32 XOR+popcount
- *                     (v_bcnt_u32_b32) -- ORBmatcher.cc:657-823, 1647-1663.
+ *   k_tri_mfma        SearchForTriangulation, one FeatureVector node holding every feature
+ *                     (BASELINE "BF"), batch of frame pairs: Hamming distances as a +-1 fp4
+ *                     GEMM on the matrix cores, then the reference's selection
+ *                     -- ORBmatcher.cc:657-823, 1647-1663.
  *   k_tri_nodes       SearchForTriangulation over common BoW nodes (general form).
  *   k_tri_nodes_pairs the same for a batch of frame pairs, FeatureVectors on the device.
  *   k_bow_pairs       SearchByBoW (KF,F) / (KF,KF) for a batch of frame pairs, FeatureVectors on the device.
@@ -64,8 +64,6 @@ __device__ __forceinline__ bool near_epipole(const MatchGeom& g, float x2, float
     return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < g.th100[oct2];
 }
 
-constexpr int kTile = 512;
-
 /* Pair p: KF1 = (kps1, desc1, n1), KF2 = (kps2, desc2, n2) resolved by the caller-side
  * accessor; every keypoint mono, no MapPoints (BF bench configuration). */
 struct PairSrc {
@@ -73,115 +71,15 @@ struct PairSrc {
     const orbx_kp* kps2; const uint8_t* desc2; int n2;
 };
 
-/* 256 threads = SPLIT parts x Q queries (Q = 256/SPLIT). Part k scans the k-th slice of
- * every candidate tile in order with the reference's rule (accept dist <= best, so ties go to
- * the later candidate); slices are merged with min distance, ties -> larger idx2, which is
- * exactly the sequential scan's result (DESIGN.md "Matcher semantics"). */
-template <int SPLIT>
-__device__ __forceinline__ void tri_bf_body(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
-                                            int32_t* __restrict__ nmatch) {
-    constexpr int Q = 256 / SPLIT;
-    constexpr int SL = kTile / SPLIT;
-    __shared__ uint4 s_desc[kTile * 2];
-    __shared__ float s_x[kTile], s_y[kTile];
-    __shared__ int s_oct[kTile];
-    __shared__ int s_bd[SPLIT > 1 ? SPLIT : 1][Q], s_bi[SPLIT > 1 ? SPLIT : 1][Q];
-    const int tid = threadIdx.x;
-    const int ql = tid % Q, part = tid / Q;
-    const int q0 = blockIdx.x * Q;
-    if (q0 >= s.n1) return;  // block-uniform
-    const int idx1 = q0 + ql;
-    const bool active = idx1 < s.n1;
-    uint32_t q[8];
-    float a = 0.f, b = 0.f, c = 0.f;
-    if (active) {
-        const uint4* qd = (const uint4*)(s.desc1 + (long long)idx1 * 32);
-        const uint4 q0v = qd[0], q1v = qd[1];
-        q[0] = q0v.x; q[1] = q0v.y; q[2] = q0v.z; q[3] = q0v.w;
-        q[4] = q1v.x; q[5] = q1v.y; q[6] = q1v.z; q[7] = q1v.w;
-        epi_line(g, s.kps1[idx1].x, s.kps1[idx1].y, &a, &b, &c);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 8; k++) q[k] = 0;
-    }
-    int bestDist = 50, bestIdx2 = -1;  // TH_LOW (ORBmatcher.cc:715)
-    for (int t0 = 0; t0 < s.n2; t0 += kTile) {
-        const int nt = min(kTile, s.n2 - t0);
-        __syncthreads();
-        {
-            // kTile/256 candidates per thread: unconditional clamped loads, masked LDS stores
-            constexpr int kPerT = kTile / 256;
-            uint4 d0[kPerT], d1[kPerT];
-            orbx_kp kp[kPerT];
-#pragma unroll
-            for (int u = 0; u < kPerT; u++) {
-                const int j = min(tid + u * 256, nt - 1);
-                const uint4* cd = (const uint4*)(s.desc2 + (long long)(t0 + j) * 32);
-                d0[u] = cd[0];
-                d1[u] = cd[1];
-                kp[u] = s.kps2[t0 + j];
-            }
-#pragma unroll
-            for (int u = 0; u < kPerT; u++) {
-                const int j = tid + u * 256;
-                if (j < nt) {
-                    s_desc[2 * j] = d0[u];
-                    s_desc[2 * j + 1] = d1[u];
-                    s_x[j] = kp[u].x; s_y[j] = kp[u].y; s_oct[j] = kp[u].octave;
-                }
-            }
-        }
-        __syncthreads();
-        if (active) {
-            const int jb = part * SL, je = min(nt, jb + SL);
-            for (int j = jb; j < je; j++) {
-                const uint4 c0 = s_desc[2 * j], c1 = s_desc[2 * j + 1];
-                const int dist = __popc(q[0] ^ c0.x) + __popc(q[1] ^ c0.y) + __popc(q[2] ^ c0.z) +
-                                 __popc(q[3] ^ c0.w) + __popc(q[4] ^ c1.x) + __popc(q[5] ^ c1.y) +
-                                 __popc(q[6] ^ c1.z) + __popc(q[7] ^ c1.w);
-                if (dist > 50 || dist > bestDist) continue;
-                const float x2 = s_x[j], y2 = s_y[j];
-                const int oct2 = s_oct[j];
-                if (near_epipole(g, x2, y2, oct2)) continue;
-                if (epi_ok(a, b, c, x2, y2, g.th384[oct2])) {
-                    bestIdx2 = t0 + j;
-                    bestDist = dist;
-                }
-            }
-        }
-    }
-    if (SPLIT > 1) {
-        s_bd[part][ql] = bestDist;
-        s_bi[part][ql] = bestIdx2;
-        __syncthreads();
-        if (part != 0) return;
-        for (int k = 1; k < SPLIT; k++) {
-            const int d = s_bd[k][ql], i = s_bi[k][ql];
-            if (i >= 0 && (bestIdx2 < 0 || d < bestDist || (d == bestDist && i > bestIdx2))) {
-                bestDist = d;
-                bestIdx2 = i;
-            }
-        }
-    }
-    if (active) {
-        out[idx1] = bestIdx2;
-        if (bestIdx2 >= 0) atomicAdd(nmatch, 1);
-    }
-}
-
 /* ----------------------------------------------------------------------------------- */
-/* MFMA form of the BF SearchForTriangulation scan (this i8 form with ORBX_MATCH_FP4=0;    */
-/* the default fp4 form, tri_mfma_body_fp4 below, takes both operands as +-1 on the        */
-/* MX-scaled f8f6f4 instruction at K = 64 and the same selection).                        */
+/* MFMA form of the BF SearchForTriangulation scan.                                      */
 /*                                                                                       */
-/* Hamming distance as an int8 GEMM: with candidate bits a in {0,1} and query bits mapped  */
-/* to b' = 2b-1 in {-1,+1},  sum_k a_k b'_k = 2|a&b| - |a|, so                             */
-/*     D(a, b) = |a| + |b| - 2|a&b| = |b| - dot(a, b')                                     */
-/* and |b| is a per-query (per-lane) constant. v_mfma_i32_32x32x32_i8 computes a 32        */
-/* candidate x 32 query tile of dot(a, b') per 32 descriptor bits; 8 steps cover 256 bits. */
-/* Lane l holds query (l & 31) and candidates (reg&3) + 8(reg>>2) + 4(l>>5) of the tile.  */
-/* Both operands map fragment element j of lane half h to descriptor bit 32s + 16h + j,    */
-/* so the k order inside the instruction is irrelevant (a dot product).                    */
+/* Hamming distance as a +-1 GEMM: with both operands mapped to (2b-1) in {-1,+1},        */
+/*     dot' = sum_k (2a_k-1)(2b_k-1) = 256 - 2 D(a, b)                                    */
+/* v_mfma_scale_f32_32x32x64_f8f6f4 on fp4 (e2m1) operands computes a 32 candidate x 32  */
+/* query tile of dot' per 64 descriptor bits (exact in the f32 accumulator); 4 steps     */
+/* cover 256 bits. Lane l holds query (l & 31) and candidates (reg&3) + 8(reg>>2) +     */
+/* 4(l>>5) of the tile.                                                                  */
 /*                                                                                       */
 /* Selection: key = D << 16 | (65535 - idx2); the reference's scan (accept dist <= best,   */
 /* geometric checks only for those) returns the valid candidate of minimum key             */
@@ -190,14 +88,6 @@ __device__ __forceinline__ void tri_bf_body(const PairSrc& s, const MatchGeom& g
 /* radius, CheckDistEpipolarLine), walking up the lane's keys until one passes.           */
 /* ----------------------------------------------------------------------------------- */
 typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ uint32_t spread01(uint32_t nib) {  // 4 bits -> 4 bytes of 0/1
-    return (nib * 0x00204081u) & 0x01010101u;
-}
-__device__ __forceinline__ uint32_t spread_pm1(uint32_t nib) {  // 4 bits -> 4 bytes of +1/-1
-    return ~(spread01(nib) * 0xFEu);
-}
 
 /* fp4 form: both operands as +-1 (e2m1 nibbles: +1.0 = 0x2, -1.0 = 0xA, block scale 2^0), so the  */
 /* 32x32x64 product gives dot' = sum (2a-1)(2b-1) = 256 - 2 D over 256 bits in 4 instructions    */
@@ -220,188 +110,14 @@ __device__ __forceinline__ v8i fp4_operand(v4i a) {  // fp4 reads only the low 4
 }
 
 constexpr int kMfChunk = 64;  // candidates staged per step (two 32-row tiles)
-#ifndef ORBX_MATCH_STOP
-#define ORBX_MATCH_STOP 0  // phase-cost experiment only (tools/exp_phases.sh): >0 cuts k_tri_mfma short (results invalid)
-#endif
-
-#ifndef ORBX_MATCH_WAVES
-#define ORBX_MATCH_WAVES 8  // query waves per workgroup (32 queries each); they share each chunk's expansion
-#endif
-constexpr int kMfWaves = ORBX_MATCH_WAVES;
-#ifndef ORBX_MATCH_PACKED_MAX
-#define ORBX_MATCH_PACKED_MAX 1  // selection by one packed (dot, row) maximum per tile (0: threshold pass + key pass)
-#endif
-#ifndef ORBX_MATCH_FP4
-#define ORBX_MATCH_FP4 1  // 1: fp4 (e2m1) +-1 operands on v_mfma_scale_f32_32x32x64_f8f6f4 (K = 64); 0: the i8 form
-#endif
-constexpr bool kMfFp4 = ORBX_MATCH_FP4 != 0;
+constexpr int kMfWaves = 8;    // query waves per workgroup (32 queries each); they share each chunk's expansion
 constexpr int kMfThreads = 64 * kMfWaves;
-static_assert(kMfWaves == 4 || kMfWaves == 8 || kMfWaves == 16, "ORBX_MATCH_WAVES: 4, 8 or 16");
-// expansion units: 16 descriptor bits of one candidate (one half h of one 32-bit step); a chunk has
-// 64 x 16 of them, each thread expands kMfUnits consecutive units of one candidate
-constexpr int kMfUnits = 64 * 16 / kMfThreads;
 
-template <int U> struct ChunkBits;
-template <> struct ChunkBits<4> { uint2 v; };
-template <> struct ChunkBits<2> { uint32_t v; };
-template <> struct ChunkBits<1> { uint16_t v; };
-__device__ __forceinline__ uint32_t unit_bits(const ChunkBits<4>& b, int u) { return ((u >> 1) ? b.v.y : b.v.x) >> (16 * (u & 1)); }
-__device__ __forceinline__ uint32_t unit_bits(const ChunkBits<2>& b, int u) { return b.v >> (16 * u); }
-__device__ __forceinline__ uint32_t unit_bits(const ChunkBits<1>& b, int) { return b.v; }
-
-__device__ __forceinline__ void tri_mfma_body(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
-                                              int32_t* __restrict__ nmatch) {
-    __shared__ v4i s_frag[2][8][64];  // [tile][step][lane] candidate fragments (0/1 bytes)
-    __shared__ float s_x[kMfChunk], s_y[kMfChunk];
-    __shared__ int s_oct[kMfChunk], s_ok[kMfChunk];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int qblk = blockIdx.x * (32 * kMfWaves);
-    if (qblk >= s.n1) return;  // block-uniform
-    const int h = lane >> 5;
-    const int qi = qblk + wave * 32 + (lane & 31);
-    const bool qon = qi < s.n1;
-    // query fragments (+1/-1 bytes), popcount and epipolar line
-    v4i bq[8];
-    int pb = 0;
-    float la = 0.f, lb = 0.f, lc = 0.f;
-    {
-        const int qc = qon ? qi : 0;
-        const uint4* qd = (const uint4*)(s.desc1 + (long long)qc * 32);
-        const uint4 d0 = qd[0], d1 = qd[1];
-        const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-#pragma unroll
-        for (int st = 0; st < 8; st++) {
-            pb += __popc(dw[st]);
-            const uint32_t b16 = dw[st] >> (16 * h);
-            bq[st] = (v4i){(int)spread_pm1(b16 & 15), (int)spread_pm1((b16 >> 4) & 15),
-                           (int)spread_pm1((b16 >> 8) & 15), (int)spread_pm1((b16 >> 12) & 15)};
-        }
-        const orbx_kp k1 = s.kps1[qc];
-        epi_line(g, k1.x, k1.y, &la, &lb, &lc);
-    }
-    uint32_t best = 0xFFFFFFFFu;
-    // expansion role of this thread: candidate c = ec of the chunk, units eu..eu+kMfUnits-1 (unit
-    // u = descriptor bits 16u..16u+15); the next chunk's bits (and, for tid < 64, keypoint) are
-    // prefetched into registers while the current chunk is multiplied
-    constexpr int kTPC = 16 / kMfUnits;  // threads per candidate
-    const int ec = tid / kTPC, eu = (tid % kTPC) * kMfUnits;
-    auto load_chunk = [&](int cb, ChunkBits<kMfUnits>& d, orbx_kp& k2) {
-        const int c = min(cb + ec, s.n2 - 1);
-        d = *(const ChunkBits<kMfUnits>*)(s.desc2 + (long long)c * 32 + 2 * eu);
-        k2 = s.kps2[min(cb + (tid & (kMfChunk - 1)), s.n2 - 1)];
-    };
-    ChunkBits<kMfUnits> pd;
-    orbx_kp pk;
-    load_chunk(0, pd, pk);
-    for (int cb = 0; cb < s.n2; cb += kMfChunk) {
-        {
-            const bool on = cb + ec < s.n2;
-            const int tile = ec >> 5, r = ec & 31;
-#pragma unroll
-            for (int k = 0; k < kMfUnits; k++) {
-                const int u = eu + k, st = u >> 1, hh = u & 1;
-                const uint32_t b16 = on ? unit_bits(pd, k) : 0u;
-                s_frag[tile][st][32 * hh + r] =
-                    (v4i){(int)spread01(b16 & 15), (int)spread01((b16 >> 4) & 15), (int)spread01((b16 >> 8) & 15),
-                          (int)spread01((b16 >> 12) & 15)};
-            }
-            if (tid < kMfChunk) {
-                const bool on2 = cb + tid < s.n2;
-                s_x[tid] = pk.x;
-                s_y[tid] = pk.y;
-                s_oct[tid] = pk.octave;
-                s_ok[tid] = on2 && !near_epipole(g, pk.x, pk.y, pk.octave);
-            }
-        }
-        __syncthreads();
-        if (cb + kMfChunk < s.n2) load_chunk(cb + kMfChunk, pd, pk);
-#if ORBX_MATCH_STOP == 1
-        best ^= (uint32_t)s_frag[lane & 1][lane & 7][lane].x;  // staging + expansion only
-        __syncthreads();
-        continue;
-#endif
-        v16i acc0 = (v16i)0, acc1 = (v16i)0;
-#pragma unroll
-        for (int st = 0; st < 8; st++) {
-            acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(s_frag[0][st][lane], bq[st], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(s_frag[1][st][lane], bq[st], acc1, 0, 0, 0);
-        }
-#if ORBX_MATCH_STOP == 2
-        best ^= (uint32_t)(acc0[lane & 15] + acc1[(lane + 3) & 15]);  // + MFMA, no selection
-        __syncthreads();
-        continue;
-#endif
-#pragma unroll
-        for (int tile = 0; tile < 2; tile++) {
-            const v16i acc = tile ? acc1 : acc0;
-            // key = D << 16 | (65535 - idx2) = kbase - P with P = acc << 16 | row (signed; rows are
-            // distinct per lane), so the lane's minimum key is kbase - max P: one v_lshl_add per
-            // accumulator and a v_max3 chain, no separate threshold pass
-            const uint32_t kbase = ((uint32_t)pb << 16) + 65535u - (uint32_t)(cb + 32 * tile + 4 * h);
-#if ORBX_MATCH_PACKED_MAX
-            auto pk = [&](int rg) { return (int)(((uint32_t)acc[rg] << 16) + (uint32_t)((rg & 3) + 8 * (rg >> 2))); };
-            int pmax = pk(0);
-#pragma unroll
-            for (int rg = 1; rg < 16; rg++) pmax = max(pmax, pk(rg));
-            uint32_t km = kbase - (uint32_t)pmax;
-            while (km < best && (km >> 16) <= 50u) {  // TH_LOW (ORBmatcher.cc:715)
-                const int jl = (int)(65535u - (km & 0xFFFFu)) - cb;
-                if (s_ok[jl] && epi_ok(la, lb, lc, s_x[jl], s_y[jl], g.th384[s_oct[jl]])) {
-                    best = km;
-                    break;
-                }
-                // next key of the lane = largest P below the rejected one
-                const int cur = (int)(kbase - km);
-                int nx = INT_MIN;
-#pragma unroll
-                for (int rg = 0; rg < 16; rg++) nx = pk(rg) < cur ? max(nx, pk(rg)) : nx;
-                km = nx == INT_MIN ? 0xFFFFFFFFu : kbase - (uint32_t)nx;
-            }
-#else
-            // cheap filter: the lane's best dot in this tile (D = pb - dot)
-            int amax = acc[0];
-#pragma unroll
-            for (int rg = 1; rg < 16; rg++) amax = max(amax, acc[rg]);
-            const int lim = min(50, (int)(best >> 16));  // TH_LOW (ORBmatcher.cc:715)
-            if (pb - amax > lim) continue;
-            // keys are recomputed from the accumulators where needed (not kept: 16 fewer live VGPRs)
-            auto key = [&](int rg) {
-                const uint32_t row = (uint32_t)((rg & 3) + 8 * (rg >> 2));
-                return kbase - (((uint32_t)acc[rg] << 16) + row);
-            };
-            uint32_t kmin = 0xFFFFFFFFu;
-#pragma unroll
-            for (int rg = 0; rg < 16; rg++) kmin = min(kmin, key(rg));
-            uint32_t km = kmin;
-            while (km < best && (km >> 16) <= 50u) {
-                const int jl = (int)(65535u - (km & 0xFFFFu)) - cb;
-                if (s_ok[jl] && epi_ok(la, lb, lc, s_x[jl], s_y[jl], g.th384[s_oct[jl]])) {
-                    best = km;
-                    break;
-                }
-                uint32_t nx = 0xFFFFFFFFu;
-#pragma unroll
-                for (int rg = 0; rg < 16; rg++) nx = key(rg) > km ? min(nx, key(rg)) : nx;
-                km = nx;
-            }
-#endif
-        }
-        __syncthreads();
-    }
-    best = min(best, (uint32_t)__shfl_xor((int)best, 32, 64));
-    if (qon && h == 0) {
-        const int idx2 = (best >> 16) <= 50u ? (int)(65535u - (best & 0xFFFFu)) : -1;
-        out[qi] = idx2;
-        if (idx2 >= 0) atomicAdd(nmatch, 1);
-    }
-}
-
-/* fp4 form of tri_mfma_body (same roles and selection): per 64-candidate chunk each */
-/* thread expands descriptor dwords of one candidate (8 KB of fragments in LDS instead of 16),    */
-/* each wave runs 4 MFMAs per 32-candidate tile instead of 8, and the packed selection key is the */
-/* f32 accumulator's bit pattern (dot' is an even integer <= 256: its low 14 mantissa bits are     */
-/* zero) OR the tile row, whose signed maximum is the first candidate of maximum dot' = minimum D  */
-/* with ties to the later row, as the i8 form's (dot << 16 | row).                                */
+/* Per 64-candidate chunk each thread expands descriptor dwords of one candidate (8 KB of fp4     */
+/* fragments in LDS), each wave runs 4 MFMAs per 32-candidate tile, and the packed selection key   */
+/* is the f32 accumulator's bit pattern (dot' is an even integer <= 256: its low 14 mantissa bits  */
+/* are zero) OR the tile row, whose signed maximum is the first candidate of maximum dot' =        */
+/* minimum D with ties to the later row.                                                          */
 __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
                                                   int32_t* __restrict__ nmatch) {
     static_assert(kMfWaves == 4 || kMfWaves == 8, "fp4 expansion roles: 4 waves (2 dwords per thread) or 8 (1)");
@@ -459,11 +175,6 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
         }
         __syncthreads();
         if (cb + kMfChunk < s.n2) load_chunk(cb + kMfChunk, pd, pk);
-#if ORBX_MATCH_STOP == 1
-        best ^= (uint32_t)s_frag[lane & 1][lane & 3][lane].x;  // staging + expansion only
-        __syncthreads();
-        continue;
-#endif
         v16f acc0 = (v16f)0.f, acc1 = (v16f)0.f;
 #pragma unroll
         for (int st = 0; st < 4; st++) {
@@ -473,11 +184,6 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
             acc1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_operand(s_frag[1][st][lane]), fp4_operand(bq[st]),
                                                                    acc1, 4, 4, 0, 127, 0, 127);
         }
-#if ORBX_MATCH_STOP == 2
-        best ^= (uint32_t)__float_as_int(acc0[lane & 15] + acc1[(lane + 3) & 15]);  // + MFMA, no selection
-        __syncthreads();
-        continue;
-#endif
 #pragma unroll
         for (int tile = 0; tile < 2; tile++) {
             const v16f acc = tile ? acc1 : acc0;
@@ -528,24 +234,7 @@ __global__ __launch_bounds__(kMfThreads) void k_tri_mfma(const int32_t* __restri
     PairSrc s;
     s.kps1 = kps + (long long)f1 * kp_stride; s.desc1 = desc + (long long)f1 * kp_stride * 32; s.n1 = counts[f1];
     s.kps2 = kps + (long long)f2 * kp_stride; s.desc2 = desc + (long long)f2 * kp_stride * 32; s.n2 = counts[f2];
-#if ORBX_MATCH_FP4
     tri_mfma_body_fp4(s, g, match12 + (long long)p * kp_stride, nmatches + p);
-#else
-    tri_mfma_body(s, g, match12 + (long long)p * kp_stride, nmatches + p);
-#endif
-}
-
-template <int SPLIT>
-__global__ __launch_bounds__(256) void k_tri_bf(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
-                                                const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
-                                                const int32_t* __restrict__ counts, int kp_stride, MatchGeom g,
-                                                int32_t* __restrict__ match12, int32_t* __restrict__ nmatches) {
-    const int p = blockIdx.y;
-    const int f1 = q1[p], f2 = q2[p];
-    PairSrc s;
-    s.kps1 = kps + (long long)f1 * kp_stride; s.desc1 = desc + (long long)f1 * kp_stride * 32; s.n1 = counts[f1];
-    s.kps2 = kps + (long long)f2 * kp_stride; s.desc2 = desc + (long long)f2 * kp_stride * 32; s.n2 = counts[f2];
-    tri_bf_body<SPLIT>(s, g, match12 + (long long)p * kp_stride, nmatches + p);
 }
 
 /* rotation bin of a match (ORBmatcher.cc:236-246): rot = angA[a] - angB[b], (a,b) = (i, j) or,
@@ -794,9 +483,6 @@ __device__ __forceinline__ Top2 top2_merge(Top2 A, Top2 B) {
     return r;
 }
 
-#ifndef ORBX_BOW_LANE
-#define ORBX_BOW_LANE 1  // nodes of <= 64 candidates: candidate per lane, DPP reductions (0: LDS + shuffles)
-#endif
 
 /* STAGED (node of <= kBowStage candidates, the common case: ~10 per node at levelsup 4): the node's
  * candidate descriptors and eligibility and, 64 at a time, its queries' descriptors are staged in LDS
@@ -817,7 +503,7 @@ __global__ __launch_bounds__(64) void k_bow(const DevView vq, const DevView vc, 
     const int lane = threadIdx.x;
     const int nc = t.c_end - t.c_begin;
     uint8_t* mflag = STAGED ? s_cm : matched;
-    if (STAGED && ORBX_BOW_LANE && nc <= 64) {
+    if (STAGED && nc <= 64) {
         // candidate j = lane, its descriptor in registers; query k's descriptor broadcast by readlane. Per
         // query: best1 = the first strict minimum = min over eligible lanes of dist << 6 | j; best2 = min dist
         // of the other eligible lanes (ORBmatcher.cc:205-225); a claimed candidate drops out of its lane
@@ -1254,7 +940,7 @@ __global__ __launch_bounds__(256) void k_rot_filter(int n, int32_t* __restrict__
     if (nout) atomicAdd(nout, local);
 }
 
-/* batch form of the rotation filter for k_tri_bf output: one workgroup per pair */
+/* batch form of the rotation filter for k_tri_mfma output: one workgroup per pair */
 __global__ __launch_bounds__(256) void k_rot_filter_pairs(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
                                                           const orbx_kp* __restrict__ kps, const int32_t* __restrict__ counts,
                                                           int kp_stride, int32_t* __restrict__ match12,
@@ -1304,22 +990,9 @@ namespace orbamd {
 hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
                          int32_t* nmatches, hipStream_t st) {
-    if (!getenv("ORBX_TRI_SIMT")) {
-        dim3 grid((kp_stride + 32 * kMfWaves - 1) / (32 * kMfWaves), npairs);
-        hipLaunchKernelGGL(k_tri_mfma, grid, dim3(kMfThreads), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
-                           nmatches);
-        return hipGetLastError();
-    }
-    // few pairs: split the candidate scan over 4 parts for more waves; many pairs: 256 queries per block
-    if (npairs * ((kp_stride + 255) / 256) < 2048) {
-        dim3 grid((kp_stride + 63) / 64, npairs);
-        hipLaunchKernelGGL(k_tri_bf<4>, grid, dim3(256), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
-                           nmatches);
-    } else {
-        dim3 grid((kp_stride + 255) / 256, npairs);
-        hipLaunchKernelGGL(k_tri_bf<1>, grid, dim3(256), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
-                           nmatches);
-    }
+    dim3 grid((kp_stride + 32 * kMfWaves - 1) / (32 * kMfWaves), npairs);
+    hipLaunchKernelGGL(k_tri_mfma, grid, dim3(kMfThreads), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
+                       nmatches);
     return hipGetLastError();
 }
 

@@ -26,49 +26,16 @@ constexpr int kPatchSize = 31;      // ORBextractor.cc:72
 constexpr int kHalfPatch = 15;      // ORBextractor.cc:73
 constexpr int kRoiMax = 72;         // max FAST cell ROI side (cells are < 60+6 px)
 constexpr int kRoiPitch = 72;
-#ifndef ORBX_BLUR_ROWS
-#define ORBX_BLUR_ROWS 63
-#endif
-constexpr int kBlurRows = ORBX_BLUR_ROWS;  // blur strip chunk height: 9 x 7 (the 7-row window loop has no partial step)
+constexpr int kBlurRows = 63;  // blur strip chunk height: 9 x 7 (the 7-row window loop has no partial step)
 static_assert(kBlurRows % 7 == 0, "blur chunk height must be a multiple of 7");
 constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity (levels >= 1)
-#ifndef ORBX_PYR_U
-#define ORBX_PYR_U 4
-#endif
-constexpr int kPyrU = ORBX_PYR_U;   // k_pyramid_frames: rows in flight per thread
-#ifndef ORBX_PYR_NT
-#define ORBX_PYR_NT 512
-#endif
+constexpr int kPyrU = 4;            // k_pyramid_frames: rows in flight per thread
 // k_pyramid_frames: threads per frame's workgroup. kPyrThreads is used when every level's 4-column
 // group count fits half of it (>= 2 rows per pass); wider levels take kPyrThreadsMax, the limit the
 // whole-frame kernel accepts (>= column groups of every level)
-constexpr int kPyrThreads = ORBX_PYR_NT;
+constexpr int kPyrThreads = 512;
 constexpr int kPyrThreadsMax = 1024;
-#ifndef ORBX_PYR_FLAT
-#define ORBX_PYR_FLAT 0  // A/B knob: 1 = table in LDS, 2 = via L1 (both slower overlapped)
-#endif
-constexpr bool kPyrFlat = ORBX_PYR_FLAT != 0;  // k_pyramid_frames: (row, column group) items dealt round-robin
-constexpr bool kPyrFlatLds = ORBX_PYR_FLAT == 1;  // ... with the column-group table staged in LDS (2: read via L1)
-#ifndef ORBX_PRIO_PYR
-#define ORBX_PRIO_PYR 0  // A/B knob: s_setprio of the k_pyramid_frames waves (0 = default priority)
-#endif
-#ifndef ORBX_PRIO_OCT
-#define ORBX_PRIO_OCT 0  // A/B knob: s_setprio of the k_octree waves
-#endif
-#ifndef ORBX_PYR_PIPE
-#define ORBX_PYR_PIPE 0  // A/B knob: k_pyramid_frames issues the next pass's loads before the current pass's taps
-#endif
-constexpr bool kPyrPipe = ORBX_PYR_PIPE != 0;
-#ifndef ORBX_PYR_BANDS
-#define ORBX_PYR_BANDS 1
-#endif
-// k_pyramid_frames: workgroups per frame; each builds every level for one horizontal band of rows,
-// recomputing the few rows its next level reads across the band edge
-constexpr int kPyrBands = ORBX_PYR_BANDS;
-#ifndef ORBX_PYR_MIN_BATCH
-#define ORBX_PYR_MIN_BATCH 64
-#endif
-constexpr int kPyrFramesMinBatch = ORBX_PYR_MIN_BATCH;  // batches below this use the per-level pyramid kernels
+constexpr int kPyrFramesMinBatch = 64;  // batches below this use the per-level pyramid kernels
 
 struct LevelDesc {
     int w, h, pitch;

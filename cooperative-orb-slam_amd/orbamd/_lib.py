@@ -105,6 +105,7 @@ SIGNATURES = {
     "orbx_compute_scale_tables": (_I, [C.POINTER(OrbxParams), _P, _P, _P, _P]),
     "orbx_set_pyramid_event": (_I, [_P, _P]),
     "orbx_debug_skip_stages": (_I, [_P, _I]),
+    "orbx_debug_serial": (_I, [_P, _I]),
     "orbx_debug_raise_error": (_I, [_P, _I, _P]),
     "orbm_create": (_I, [_I, C.POINTER(_P)]),
     "orbm_destroy": (None, [_P]),
@@ -117,6 +118,7 @@ SIGNATURES = {
                                                 _P]),
     "orbm_search_for_triangulation_slots_device": (_I, [_P, C.POINTER(OrbxKfSource), _I, _I, _P, _SZ,
                                                         C.POINTER(OrbmSlotGeom), _I, _I, _P, _P, _P]),
+    "orbm_search_by_bow_slots_device": (_I, [_P, C.POINTER(OrbxKfSource), _I, _I, _P, _SZ, _F, _I, _I, _P, _P, _P]),
     "orbm_check_error": (_I, [_P, _P]),
     "orbm_triangulation_nodes_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P, _F, _F,
                                                    _I, _P, _P, _I, _P, _P, _P]),

@@ -6,10 +6,12 @@ orbx handle, matcher ctx and HIP stream each):
   * ORBextractor::operator() on every frame (orbx_extract_batch_device);
   * SearchForTriangulation of frame b against frame b-1 of the same graph (one node holding every
     feature, mono, no MapPoints: the BASELINE "BF" configuration);
-  * the cooperative exchange: graph 0's frame 0 is this agent's keyframe; it is packed into a
-    keyframe slot (orbx_pack_keyframe_device), all-gathered across the agents (RCCL over xGMI at
+  * the cooperative exchange: graph 0's frame 0 is this agent's keyframe; its BoW / FeatureVector is
+    computed on the device (orbv_transform_batch_device), it is packed into a keyframe slot with its
+    MapPoint records (orbx_pack_keyframe_device), all-gathered across the agents (RCCL over xGMI at
     N > 1, a local copy at N = 1), and matched against every agent's slot straight from the receive
-    buffer (orbm_search_for_triangulation_slots_device).
+    buffer: SearchForTriangulation (orbm_search_for_triangulation_slots_device, LocalMapping) and the
+    loop-candidate SearchByBoW(KF,KF) (orbm_search_by_bow_slots_device, LoopClosing).
 Graphs are staggered: in a staggered step graph p starts extracting once graph p-1 has finished extracting
 it, so one graph's FAST overlaps another's latency-bound tail (octree, describe, matcher); the offset is
 imposed in the first step of a pass and every 8th step after it (DEFAULT_STAGGER) and persists in between.
@@ -25,6 +27,20 @@ from .device import BatchPipeline
 # step drains as a 4-graph chain, and +1.0 % over it in the ~2000-step sustained pass, where a stagger imposed
 # only once lets the graphs' phases drift)
 DEFAULT_STAGGER = "every8"
+SYNTH_VOC_SEED = 7    # the exchange's synthetic vocabulary (ORBvoc.txt's shape; ORBvoc.txt is absent)
+KF_LEVELSUP = 4       # KeyFrame::ComputeBoW's levelsup (Frame.cc:400-407)
+LOOP_NNRATIO = 0.75   # LoopClosing::ComputeSim3's ORBmatcher(0.75, true) (LoopClosing.cc:239)
+
+
+def kf_mp_flags(n):
+    """Synthetic MapPoint records of the bench keyframe (the slot's MPFLAGS: bit 0 = mvpMapPoints[i] != NULL,
+    bit 1 = isBad()): about 80 % of the features carry a MapPoint, about 5 % of those bad; a fixed hash of the
+    feature index, so the oracle check rebuilds them."""
+    import numpy as np
+    h = (np.arange(n, dtype=np.uint64) * np.uint64(2654435761)) & np.uint64(0xFFFFFFFF)
+    mp = ((h >> np.uint64(8)) % np.uint64(10)) < np.uint64(8)
+    bad = mp & (((h >> np.uint64(20)) % np.uint64(20)) == np.uint64(0))
+    return (mp.astype(np.uint8) | (bad.astype(np.uint8) << 1)).astype(np.uint8)
 
 
 class AgentSchedule:
@@ -92,27 +108,49 @@ class AgentSchedule:
         self.all_slots = torch.zeros(world * self.slot_bytes, dtype=torch.uint8, device=dev)
         self.my_slot = (torch.zeros(self.slot_bytes, dtype=torch.uint8, device=dev) if self.collective else
                         self.all_slots)
-        self.xmatch = torch.empty((world, p0.stride), dtype=torch.int32, device=dev)
+        S = p0.stride
+        self.xmatch = torch.empty((world, S), dtype=torch.int32, device=dev)
         self.xn = torch.zeros(world, dtype=torch.int32, device=dev)
+        self.xbow = torch.empty((world, S), dtype=torch.int32, device=dev)
+        self.xbn = torch.zeros(world, dtype=torch.int32, device=dev)
         self.pack_err = torch.zeros(16, dtype=torch.int32, device=dev)
         self.meta = p0.meta(0, agent=rank)
-        self.src0 = p0.kf_source(0)
         self.ag_events = []
-        # async_exchange: the exchange runs on its own stream once graph 0 has extracted the keyframe; it packs the
-        # slot and copies the keyframe's query arrays first, and only that (not the all-gather, whose latency at
-        # N > 1 includes waiting for the other agents, nor the slot match) holds graph 0's next extraction, which
-        # overwrites the keyframe's arrays. Without it the exchange runs in order on graph 0's stream (bench.py: own
-        # stream when a collective runs, graph 0's at N = 1, where it measured 0.9 % faster).
+        # async_exchange: the exchange runs on its own stream once graph 0 has extracted the keyframe; it first
+        # copies the keyframe's arrays, and only that copy (not the BoW transform, the pack, the all-gather, whose
+        # latency at N > 1 includes waiting for the other agents, nor the slot matchers) holds graph 0's next
+        # extraction, which overwrites them. Without it the exchange runs in order on graph 0's stream (bench.py:
+        # own stream when a collective runs, graph 0's at N = 1, where it measured 0.9 % faster).
         self.xstream = None
+        kps, desc, count = p0.kps[0], p0.desc[0], p0.counts[0:1]
         if async_exchange and exchange:
-            from .exchange import kf_source
             self.xstream = torch.cuda.Stream(dev)
             self.q_kps = torch.empty_like(p0.kps[0])
             self.q_desc = torch.empty_like(p0.desc[0])
             self.q_count = torch.empty_like(p0.counts[0:1])
-            self.q_src = kf_source(self.q_kps, self.q_desc, self.q_count)
+            kps, desc, count = self.q_kps, self.q_desc, self.q_count
             self.kf_released = torch.cuda.Event()
             self.kf_pending = False
+        self.kf_arrays = (kps, desc, count)
+        # the keyframe as a KeyFrame of the map: Frame::ComputeBoW on the device against the vocabulary (a
+        # deterministic synthetic one of ORBvoc.txt's shape, k = 10, L = 6: ORBvoc.txt is absent; levelsup 4,
+        # KeyFrame::ComputeBoW) and the synthetic MapPoint flags of kf_mp_flags, so the slot carries mBowVec /
+        # mFeatVec / the MapPoint records and the receiving agents' loop-candidate SearchByBoW(KF,KF) has work
+        if exchange:
+            from .exchange import kf_source
+            from .vocabulary import L1_NORM, TF_IDF, ORBVocabulary, synth_vocabulary_full
+            self.voc_arrays = synth_vocabulary_full(seed=SYNTH_VOC_SEED)
+            k, L, par, leaf, vdesc, w = self.voc_arrays
+            self.voc = ORBVocabulary.from_arrays(k, L, L1_NORM, TF_IDF, par, leaf, vdesc, w, device=device)
+            z = lambda *sh, dt=torch.int32: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
+            self.kf_word, self.kf_word_w, self.kf_word_nid = z(S), z(S, dt=torch.float64), z(S)
+            self.kf_bow_word, self.kf_bow_val, self.kf_nbow = z(S), z(S, dt=torch.float64), z(1)
+            self.kf_fv_node, self.kf_fv_off, self.kf_fv_feat, self.kf_nfv = z(S), z(S + 1), z(S), z(1)
+            self.kf_mpf = torch.from_numpy(kf_mp_flags(S)).to(dev)
+            self.bow_max_nodes = int(min(S, k ** max(L - KF_LEVELSUP, 0)))
+            self.kf_src = kf_source(kps, desc, count, mp_flags=self.kf_mpf, bow_word=self.kf_bow_word,
+                                    bow_value=self.kf_bow_val, nbow=self.kf_nbow, fv_node=self.kf_fv_node,
+                                    fv_off=self.kf_fv_off, fv_feat=self.kf_fv_feat, nfv=self.kf_nfv)
 
     # ------------------------------------------------------------------------------------------
     def exchange_stream(self):
@@ -120,29 +158,41 @@ class AgentSchedule:
         return self.xstream if self.xstream is not None else self.streams[0]
 
     def exchange(self, ag=None):
-        """this agent's keyframe -> slot -> all-gather -> cross-agent SearchForTriangulation"""
+        """this agent's keyframe -> BoW -> slot -> all-gather -> cross-agent SearchForTriangulation (LocalMapping's
+        CreateNewMapPoints on a received keyframe) and SearchByBoW(KF,KF) (LoopClosing's loop-candidate match,
+        ORBmatcher(0.75, true): LoopClosing.cc:239-265) against every agent's slot"""
+        from ._lib import check, load
+        from .exchange import bow_slots_device, pack_device
         torch = self.torch
         p0 = self.pipes[0]
         st = self.exchange_stream()
-        query = self.src0
+        kps, desc, count = self.kf_arrays
         if self.xstream is not None:
             self.xstream.wait_event(self.done[0])  # graph 0 has extracted this step's keyframe (frame 0)
         with torch.cuda.stream(st):
-            p0.pack(0, self.my_slot, self.meta, st.cuda_stream, err=self.pack_err, src=self.src0)
             if self.xstream is not None:
-                self.q_kps.copy_(p0.kps[0])
-                self.q_desc.copy_(p0.desc[0])
-                self.q_count.copy_(p0.counts[0:1])
+                kps.copy_(p0.kps[0])
+                desc.copy_(p0.desc[0])
+                count.copy_(p0.counts[0:1])
                 self.kf_released.record(st)  # graph 0 may overwrite its buffers from here on
                 self.kf_pending = True
-                query = self.q_src
+            S = p0.stride
+            check(load().orbv_transform_batch_device(
+                self.voc._h, 1, desc.data_ptr(), count.data_ptr(), S, KF_LEVELSUP, self.kf_word.data_ptr(),
+                self.kf_word_w.data_ptr(), self.kf_word_nid.data_ptr(), self.kf_bow_word.data_ptr(),
+                self.kf_bow_val.data_ptr(), self.kf_nbow.data_ptr(), self.kf_fv_node.data_ptr(),
+                self.kf_fv_off.data_ptr(), self.kf_fv_feat.data_ptr(), self.kf_nfv.data_ptr(), st.cuda_stream),
+                "orbv_transform_batch_device")
+            pack_device(self.kf_src, self.meta, S, self.my_slot, self.pack_err, st.cuda_stream)
             if ag is not None:
                 ag[0].record(st)
             if self.collective:
                 self.allgather(self.all_slots, self.my_slot)
             if ag is not None:
                 ag[1].record(st)
-            p0.match_slots(0, self.all_slots, self.world, self.xmatch, self.xn, st.cuda_stream, query=query)
+            p0.match_slots(0, self.all_slots, self.world, self.xmatch, self.xn, st.cuda_stream, query=self.kf_src)
+            bow_slots_device(p0.mh, self.kf_src, S, self.world, self.all_slots, self.slot_bytes, self.xbow, self.xbn,
+                             LOOP_NNRATIO, True, self.bow_max_nodes, st.cuda_stream)
 
     def step(self, ev=None, xev=None, extract=True, match=True, xchg=True, first=True, batch=None, wait=None):
         """enqueue one step over the next pool batch (or `batch`); ev[p] = (start, end) events around graph
@@ -208,9 +258,11 @@ class AgentSchedule:
         return self.pipes[p].host_results(b)
 
     def exchange_results(self):
-        """match rows [world, n] of this agent's keyframe against every agent's slot"""
+        """(triangulation rows [world, n], counts [world], SearchByBoW rows [world, n], counts [world]) of this agent's
+        keyframe against every agent's slot"""
         n = int(self.pipes[0].counts[0].item())
-        return self.xmatch[:, :n].cpu().numpy(), self.xn.cpu().numpy()
+        return (self.xmatch[:, :n].cpu().numpy(), self.xn.cpu().numpy(), self.xbow[:, :n].cpu().numpy(),
+                self.xbn.cpu().numpy())
 
     def close(self):
         if self.pyr_done is not None:
@@ -219,3 +271,6 @@ class AgentSchedule:
                 load().orbx_set_pyramid_event(pp.ext._h, None)
         for pp in self.pipes:
             pp.close()
+        if getattr(self, "voc", None) is not None:
+            self.voc.close()
+            self.voc = None

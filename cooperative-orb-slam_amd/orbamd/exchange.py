@@ -264,3 +264,12 @@ def match_slots_device(mh, query, cap1, nref, d_slots, slot_nbytes, geoms, d_mat
                                                             int(slot_nbytes), g, int(bool(use_bow)), int(max_nodes),
                                                             _ptr(d_match), _ptr(d_nmatch), stream),
           "orbm_search_for_triangulation_slots_device")
+
+
+def bow_slots_device(mh, query, cap1, nref, d_slots, slot_nbytes, d_match, d_nmatch, nnratio=0.75, check_ori=True,
+                     max_nodes=0, stream=None):
+    """orbm_search_by_bow_slots_device (cross-agent SearchByBoW(KF,KF), LoopClosing's loop-candidate match)."""
+    check(load().orbm_search_by_bow_slots_device(mh, C.byref(query), int(cap1), int(nref), _ptr(d_slots),
+                                                 int(slot_nbytes), float(nnratio), int(bool(check_ori)),
+                                                 int(max_nodes), _ptr(d_match), _ptr(d_nmatch), stream),
+          "orbm_search_by_bow_slots_device")

@@ -582,6 +582,21 @@ int orbm_search_for_triangulation_slots_device(orbm_ctx* ctx, const orbx_kf_sour
                                                const orbm_slot_geom* geom, int use_bow, int max_nodes,
                                                int32_t* d_match, int32_t* d_nmatches, void* stream);
 
+/* Cross-agent ORBmatcher::SearchByBoW(query KF, slot KF, vpMatches12) (ORBmatcher.cc:522-655):
+ * the loop-candidate match the receiving agent runs on a received keyframe (it goes to
+ * LoopClosing::InsertKeyFrame, ORB_SLAM2/Examples/ROS/ORB_SLAM2/src/ros_mono.cc:3530, and
+ * LoopClosing::ComputeSim3 calls SearchByBoW(mpCurrentKF, pKF) with ORBmatcher(0.75, true),
+ * LoopClosing.cc:239, 265), of this agent's keyframe (`query`, device arrays: kps/desc/count,
+ * mp_flags (bit 0 a MapPoint, bit 1 bad; NULL = none) and its FeatureVector) against nref
+ * received slots at d_slots + r*slot_bytes, straight from device memory, over the common nodes
+ * of the two FeatureVectors (query nodes <= max_nodes). Outputs d_match[r*cap1 + idx1] = the
+ * slot keyframe's feature idx2 whose MapPoint vpMatches12[idx1] is (or -1), after the
+ * rotation filter when check_ori, and d_nmatches[r]. A slot that fails validation contributes
+ * no matches and raises the ctx's device error flag (orbm_check_error). */
+int orbm_search_by_bow_slots_device(orbm_ctx* ctx, const orbx_kf_source* query, int cap1, int nref,
+                                    const uint8_t* d_slots, size_t slot_bytes, float nnratio, int check_ori,
+                                    int max_nodes, int32_t* d_match, int32_t* d_nmatches, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * Stereo -- replaces Frame::ComputeStereoMatches (ORB_SLAM2.1/src/Frame.cc:470-641, the
  * stereo Frame constructor's step after ExtractORB(0/1), Frame.cc:80-98), reading the two
@@ -648,6 +663,11 @@ int orbx_set_pyramid_event(orbx_handle* h, void* event);
  * skipped stage leaves its buffers as the previous call left them; the tests use it to prove that
  * the bench's self-check detects a stage that stopped launching. */
 int orbx_debug_skip_stages(orbx_handle* h, int mask);
+
+/* Measurement hook: on != 0 runs every stage of this handle's subsequent extractions in order on the
+ * caller's stream (no side stream for the blur), so a kernel trace times each kernel alone; 0 = the
+ * default fork/join schedule. Outputs are identical either way. */
+int orbx_debug_serial(orbx_handle* h, int on);
 
 /* Test hook: ORs `flag` (> 0) into the handle's sticky batch error word, as a failing device batch
  * would; the tests use it to show that host-path extractions (orbx_extract) neither clear nor hide it

@@ -4,7 +4,9 @@ Used by tests/test_gpu_schedule.py and by bench.py after its timed region (the o
 checker here, never the measured path): recomputes, for sampled frames of an
 orbamd.agent.AgentSchedule step, ORBextractor::operator() (oracle/orb_oracle.c) and the BF
 SearchForTriangulation against the previous frame of the same graph, and the cross-agent
-SearchForTriangulation of this agent's keyframe against every agent's keyframe, and compares
+SearchForTriangulation and SearchByBoW(KF,KF) of this agent's keyframe against every agent's keyframe
+(their FeatureVectors from the oracle vocabulary transform, their MapPoint records from
+orbamd.agent.kf_mp_flags), and compares
 every keypoint field (raw float bits), descriptor byte and match index with the device results.
 """
 import os
@@ -77,21 +79,55 @@ def check_schedule(sched, frames_np, samples=None, agent_frames=None, threads=No
             mism.append("match p=%d b=%d vs b-1: %s" % (p, b, "%d entries differ" % int((mg != mo).sum())
                                                         if mg.shape == mo.shape else "length %d vs %d" % (len(mg), len(mo))))
     nslots = 0
+    bow_counts = []
     if sched.exchange_on:
-        xm, xn = sched.exchange_results()
+        from orbamd.agent import KF_LEVELSUP, LOOP_NNRATIO, kf_mp_flags
+        xm, xn, xb, xbn = sched.exchange_results()
         t_kf = sched.frame_index(0, 0)
         kq, dq = local.get((0, 0)) or extract(frames_np[t_kf])
-        vq = orbamd.KeyFrameView(kq, dq, tabs["scale"], tabs["sigma2"])
+        voc = _oracle_vocabulary(sched)
+
+        def kf_view(k, d, with_fv):
+            """the keyframe as the slot carries it: MapPoint records (kf_mp_flags) and, for SearchByBoW, the
+            FeatureVector of the vocabulary transform (KeyFrame::ComputeBoW, levelsup 4)"""
+            f = kf_mp_flags(len(k))
+            fv = voc.transform(d, KF_LEVELSUP)[1] if with_fv else None
+            return orbamd.KeyFrameView(k, d, tabs["scale"], tabs["sigma2"], feat_vec=fv, has_mp=(f & 1).astype(bool),
+                                       mp_bad=((f >> 1) & 1).astype(bool))
+        vq, vq_bow = kf_view(kq, dq, False), kf_view(kq, dq, True)
         for r in range(sched.world):
             img = frames_np[t_kf] if agent_frames is None else agent_frames(r, t_kf)
             kr, dr = extract(img) if agent_frames is not None else (kq, dq)
-            vr = orbamd.KeyFrameView(kr, dr, tabs["scale"], tabs["sigma2"])
+            vr, vr_bow = (vq, vq_bow) if agent_frames is None else (kf_view(kr, dr, False), kf_view(kr, dr, True))
+            # LocalMapping's SearchForTriangulation (features with a MapPoint skipped on both sides, :699-726)
             n_o, mo = oracle_py.search_for_triangulation(vq, vr, F12, ex, ey, False, False)
             if not np.array_equal(xm[r], mo) or int(xn[r]) != int(n_o):
                 ndiff = int((xm[r] != mo).sum()) if xm[r].shape == mo.shape else -1
-                mism.append("cross-agent match vs agent %d: %s, count %d vs %d"
+                mism.append("cross-agent triangulation vs agent %d: %s, count %d vs %d"
                             % (r, "%d entries differ" % ndiff if ndiff >= 0 else
                                "%d vs %d query keypoints" % (len(xm[r]), len(mo)), int(xn[r]), int(n_o)))
+            # LoopClosing's SearchByBoW(KF,KF) (ORBmatcher(0.75, true))
+            nb_o, mb = oracle_py.search_by_bow(vq_bow, vr_bow, LOOP_NNRATIO, True, other_is_keyframe=True)
+            if not np.array_equal(xb[r], mb) or int(xbn[r]) != int(nb_o):
+                ndiff = int((xb[r] != mb).sum()) if xb[r].shape == mb.shape else -1
+                mism.append("cross-agent SearchByBoW vs agent %d: %s, count %d vs %d"
+                            % (r, "%d entries differ" % ndiff if ndiff >= 0 else
+                               "%d vs %d query keypoints" % (len(xb[r]), len(mb)), int(xbn[r]), int(nb_o)))
+            bow_counts.append(int(nb_o))
             nslots += 1
     return {"bit_exact": not mism, "checked_frames": len(samples), "checked_pairs": len(samples),
-            "checked_slots": nslots, "mismatches": mism[:8]}
+            "checked_slots": nslots, "slot_bow_matches": bow_counts, "mismatches": mism[:8]}
+
+
+_VOC = {}
+
+
+def _oracle_vocabulary(sched):
+    """the oracle restatement of the schedule's (synthetic) vocabulary, built once per process"""
+    from orbamd.vocabulary import L1_NORM, TF_IDF
+    key = id(sched.voc_arrays)
+    if key not in _VOC:
+        k, L, par, leaf, desc, w = sched.voc_arrays
+        _VOC.clear()
+        _VOC[key] = oracle_py.OracleVocabulary(k, L, L1_NORM, TF_IDF, par, leaf, desc, w)
+    return _VOC[key]

@@ -37,10 +37,11 @@ def main():
     torch.cuda.synchronize()
     sched.check_errors()
     res = check_schedule(sched, frames, agent_frames=lambda r, t: orbamd.synth_frames(r, t, 1, W, H)[0])
-    xm, xn = sched.exchange_results()
-    print("rank", rank, res, "cross-agent matches", list(xn), flush=True)
+    xm, xn, xb, xbn = sched.exchange_results()
+    print("rank", rank, res, "cross-agent matches", list(xn), "SearchByBoW", list(xbn), flush=True)
     assert res["bit_exact"], res["mismatches"]
     assert res["checked_slots"] == world and all(int(v) > 0 for v in xn)
+    assert int(xbn[rank]) > 0  # its own keyframe: the loop-candidate match finds it
     sched.close()
     dist.barrier()
     dist.destroy_process_group()

@@ -369,3 +369,78 @@ def test_two_agents_exchange_on_device():
         print(o[-3000:])
         assert p.returncode == 0, "rank %d failed" % r
         assert "AGENT OK" in o
+
+
+def _oracle_slot_bow(kq, dq, eq, dec, nnratio, check_ori):
+    """oracle SearchByBoW(query KF, slot KF) (ORBmatcher.cc:522-655) on the decoded slot"""
+    def view(k, d, mpf, fvd):
+        node, off, feat = fvd
+        fv = {int(node[i]): list(feat[off[i]:off[i + 1]]) for i in range(len(node))}
+        has_mp = None if mpf is None else (mpf & 1).astype(bool)
+        bad = None if mpf is None else ((mpf >> 1) & 1).astype(bool)
+        return KeyFrameView(k, d, np.ones(8, np.float32), np.ones(8, np.float32), feat_vec=fv, has_mp=has_mp,
+                            mp_bad=bad)
+    vq = view(kq, dq, eq.get("mp_flags"), eq["fv"])
+    vs = view(dec["kps"], dec["desc"], dec["mp_flags"], (dec["fv_node"], dec["fv_off"], dec["fv_feat"]))
+    return oracle_py.search_by_bow(vq, vs, nnratio, check_ori, other_is_keyframe=True)
+
+
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_eight_agent_slots_search_by_bow_equals_oracle(check_ori):
+    """The loop-candidate match of the exchange (LoopClosing::ComputeSim3's SearchByBoW(KF,KF), ORBmatcher(0.75,
+    true), LoopClosing.cc:239-265) of the querying agent's keyframe against 8 slots straight from the receive
+    buffer: the query itself, a shifted view of it and six other agents' keyframes, MapPoints (some bad) on both
+    sides, one slot without MapPoints, one malformed. Row by row the oracle's SearchByBoW (ORBmatcher.cc:522-655)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(5)
+    nref, cap = 8, 1100
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    tabs = orc.tables()
+    img_q = orbamd.synth_frames(9, 3, 1, 640, 480)[0]
+    kq, dq = orc(img_q)
+
+    def mp(n):
+        return ((rng.random(n) < 0.8).astype(np.uint8) | ((rng.random(n) < 0.05).astype(np.uint8) << 1))
+    eq = {"mp_flags": mp(len(kq)), "fv": _desc_fv(dq)}
+    srcq, keepq = _device_source(torch, kq, dq, eq)
+    sb = exchange.slot_bytes(cap)
+    slots = torch.zeros(nref * sb, dtype=torch.uint8, device="cuda")
+    decs = []
+    for r in range(nref):
+        if r == 0:
+            k, d = kq, dq
+        elif r == 1:
+            k, d = orc(orbamd.synth_frames(9, 3, 1, 640, 480, dx=3)[0])
+        else:
+            k, d = orc(orbamd.synth_frames(r, 5 * r, 1, 640, 480)[0])
+        e = {"fv": _desc_fv(d)}
+        if r != 5:
+            e["mp_flags"] = mp(len(k))
+        host = exchange.pack_host(_meta(r, tabs), k, d, cap, **e)
+        slots[r * sb:(r + 1) * sb].copy_(torch.from_numpy(host))
+        decs.append(exchange.parse(host))
+    mh = orbamd.ORBmatcher(0.75, True)
+    out = torch.empty((nref, cap), dtype=torch.int32, device="cuda")
+    nm = torch.zeros(nref, dtype=torch.int32, device="cuda")
+    exchange.bow_slots_device(mh._h, srcq, cap, nref, slots, sb, out, nm, 0.75, check_ori, max_nodes=len(eq["fv"][0]))
+    torch.cuda.synchronize()
+    assert orbamd.load().orbm_check_error(mh._h, None) == 0
+    got, gn = out.cpu().numpy(), nm.cpu().numpy()
+    counts = []
+    for r in range(nref):
+        no, mo = _oracle_slot_bow(kq, dq, eq, decs[r], 0.75, check_ori)
+        np.testing.assert_array_equal(got[r, :len(kq)], mo, err_msg="slot %d" % r)
+        assert int(gn[r]) == no, (r, int(gn[r]), no)
+        assert np.all(got[r, len(kq):] == -1)
+        counts.append(no)
+    assert counts[0] > 300 and counts[1] > 50 and counts[5] == 0, counts
+    # a malformed slot (foreign version): no matches, the error flag, the other rows unchanged
+    bad = slots.clone()
+    bad[2 * sb + 4:2 * sb + 8] = torch.tensor([1, 0, 0, 0], dtype=torch.uint8)
+    out2 = torch.empty_like(out)
+    exchange.bow_slots_device(mh._h, srcq, cap, nref, bad, sb, out2, nm, 0.75, check_ori, max_nodes=len(eq["fv"][0]))
+    torch.cuda.synchronize()
+    assert orbamd.load().orbm_check_error(mh._h, None) == -2
+    assert np.all(out2[2].cpu().numpy() == -1) and int(nm[2].item()) == 0
+    assert torch.equal(out2[0], out[0]) and torch.equal(out2[7], out[7])
+    mh.close()

@@ -145,11 +145,7 @@ def test_extract_other_parameters(W, H, nf, sf, nl, ini, mini):
 def test_host_path_graph_replay_and_size_changes():
     """orbx_extract captures its per-frame work as a hipGraph (eager first call per geometry, captured
     second, replayed after): many frames and alternating frame sizes on one handle, every call
-    bit-exact vs the oracle, and the eager path (ORBX_NO_GRAPH=1, a child process) gives the same."""
-    import json
-    import os
-    import subprocess
-    import sys
+    bit-exact vs the oracle, and the eager path (stage profiling on) gives the same."""
     ext = orbamd.ORBextractor(1000, 1.2, 8, 20, 7, max_width=752, max_height=480)
     orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
     a = orbamd.synth_frames(0, 3, 4, 640, 480)
@@ -162,17 +158,11 @@ def test_host_path_graph_replay_and_size_changes():
         _compare(kg, dg, ko, do)
         sums.append(int(dg.astype(np.int64).sum()))
     ext.close()
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = ("import sys, json; sys.path.insert(0, %r); import orbamd, numpy as np; "
-            "e = orbamd.ORBextractor(1000, 1.2, 8, 20, 7, max_width=752, max_height=480); "
-            "a = orbamd.synth_frames(0, 3, 4, 640, 480); b = orbamd.synth_frames(1, 5, 3, 752, 480); "
-            "seq = [a[0], a[1], a[2], b[0], b[1], a[3], b[2]]; "
-            "print(json.dumps([int(e(i)[1].astype(np.int64).sum()) for i in seq]))"
-            % os.path.join(root, "cooperative-orb-slam_amd"))
-    env = dict(os.environ, ORBX_NO_GRAPH="1")
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert json.loads(r.stdout.strip().splitlines()[-1]) == sums
+    # the eager path (every call launched stage by stage: stage profiling on disables the graph)
+    e2 = orbamd.ORBextractor(1000, 1.2, 8, 20, 7, max_width=752, max_height=480)
+    assert orbamd.load().orbx_profile_enable(e2._h, 0x1F) == 0
+    assert [int(e2(i)[1].astype(np.int64).sum()) for i in seq] == sums
+    e2.close()
 
 
 def test_host_path_keeps_the_sticky_batch_error():

@@ -35,6 +35,7 @@ def test_bench_schedule_bit_exact(W, H, nf, B, P, stagger, async_x):
     res = check_schedule(sched, frames, samples=samples, nfeatures=nf)
     assert res["bit_exact"], res["mismatches"]
     assert res["checked_frames"] == B and res["checked_slots"] == 1
+    assert res["slot_bow_matches"][0] > 100  # SearchByBoW(KF,KF) of the keyframe against its own slot
     assert all(int(pp.nmatch.min().item()) > 0 for pp in sched.pipes)
     sched.close()
 
@@ -68,24 +69,22 @@ def test_skipped_stage_fails_the_self_check(stage):
         sched.close()
 
 
-def test_split_schedule_bit_exact():
-    """ORBX_SCHED=split (an A/B switch: FAST on level 0 on the side stream beside the pyramid) in the bench
-    schedule: the octree must wait for the side stream's level-0 cell keys. The switch is read once per
-    process, so the schedule runs in a child process; every frame and match row is checked."""
-    import json
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = ("import sys, json; sys.path[:0] = [%r, %r]; import torch, orbamd; "
-            "from orbamd.agent import AgentSchedule; from check_schedule import check_schedule; "
-            "W, H, B, P = 640, 480, 1024, 4; f = orbamd.synth_frames(0, 0, 2 * B, W, H); "
-            "s = AgentSchedule(torch, f, W, H, P, device=0, pool=2); "
-            "[s.step(first=i == 0) for i in range(3)]; torch.cuda.synchronize(); s.check_errors(); "
-            "r = check_schedule(s, f, samples=[(p, b) for p in range(P) for b in range(B // P)]); "
-            "print(json.dumps([bool(r['bit_exact']), r['checked_frames']]))"
-            % (os.path.join(root, "cooperative-orb-slam_amd"), os.path.join(root, "oracle")))
-    env = dict(os.environ, ORBX_SCHED="split")
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert json.loads(r.stdout.strip().splitlines()[-1]) == [True, 1024]
+def test_serial_measurement_hook_bit_exact():
+    """orbx_debug_serial (the measurement hook that runs every stage in order on one stream, so a kernel
+    trace times each kernel alone) changes no output: the bench schedule with it on, every frame checked"""
+    torch = pytest.importorskip("torch")
+    from orbamd.agent import AgentSchedule
+    W, H, B, P = 640, 480, 512, 2
+    lib = orbamd.load()
+    frames = orbamd.synth_frames(0, 0, 2 * B, W, H)
+    sched = AgentSchedule(torch, frames, W, H, P, device=0, pool=2)
+    for pp in sched.pipes:
+        assert lib.orbx_debug_serial(pp.ext._h, 1) == 0
+    for i in range(3):
+        sched.step(first=i == 0)
+    torch.cuda.synchronize()
+    sched.check_errors()
+    res = check_schedule(sched, frames, samples=[(p, b) for p in range(P) for b in range(B // P)])
+    assert res["bit_exact"], res["mismatches"]
+    assert res["checked_frames"] == B
+    sched.close()

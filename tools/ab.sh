@@ -18,6 +18,6 @@ for r in $(seq 1 ${AB_ROUNDS:-3}); do
   done
 done
 for v in "$@"; do
-  out=$(ORBAMD_LIB_VARIANT=$v ORBX_SCHED=serial timeout -k 10 120 python bench.py --sustain 0 --no-cpu --steps 30 ${AB_ARGS} --pipes 1 --batch 256 | python -c "$summ") || exit $?
+  out=$(ORBAMD_LIB_VARIANT=$v timeout -k 10 120 python bench.py --sustain 0 --no-cpu --steps 30 ${AB_ARGS} --pipes 1 --batch 256 --serial-stages | python -c "$summ") || exit $?
   echo "$v serial-1graph: $out"
 done

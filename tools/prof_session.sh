@@ -8,9 +8,7 @@ R=$GRAFT_REPO_ROOT
 tools/gpu_run.sh "300 ${T}_bench python3 bench.py" || exit $?
 cp gpurun_out/${T}_bench.log gpurun_out/${T}_bench.json
 tools/prof_round.sh "$T" || exit $?
-export ORBX_SCHED=serial
 tools/gpu_run.sh \
-  "300 ${T}_iso rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${T}_iso -o run -- python3 bench.py --pipes 1 --batch 256 --no-cpu --steps 10 --sustain 0" || exit $?
-unset ORBX_SCHED
+  "300 ${T}_iso rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${T}_iso -o run -- python3 bench.py --pipes 1 --batch 256 --serial-stages --no-cpu --steps 10 --sustain 0" || exit $?
 tools/gpu_run.sh \
   "300 ${T}_rows rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${T}_rows -o run -- python3 tools/bench_rows.py"
