@@ -79,7 +79,9 @@ def algorithmic_bytes(W, H, nkp):
         "fast_cells": sum(px),                   # read every level once
         "octree": 0,                             # candidate keys only (reported, not priced)
         "blur": 2 * sum(px),                     # read + write every level
-        "describe": nkp * (31 * 31 + 37 * 37 + 56),  # IC patch + BRIEF patch + 24B kp + 32B desc
+        # the unblurred levels (IC_Angle patches) and the blurred levels (rBRIEF patches) read once each, 24 B
+        # keypoint + 32 B descriptor written per keypoint (overlapping patches re-read from L2 are not HBM bytes)
+        "describe": 2 * sum(px) + 56 * nkp,
     }
     return total, per_stage
 
@@ -252,6 +254,10 @@ def main():
                     help="HIP stream priorities of the graphs: lead = the first half of the staggered graphs (the ones "
                          "in their latency-bound tail stages) high, lead1 = graph 0 only")
     ap.add_argument("--no-exchange", action="store_true")
+    ap.add_argument("--alias-frames", action="store_true",
+                    help="measurement hook (orbx_debug_alias_frames): every frame of a graph's batch is its frame 0 and "
+                         "shares one pyramid / blur buffer, so every stage reads L2-resident data (the L2-residency "
+                         "bound, DESIGN.md 6.0); outputs are frame 0's, the self-check is skipped")
     ap.add_argument("--serial-stages", action="store_true",
                     help="measurement hook (orbx_debug_serial): every extraction stage in order on its graph's stream, so "
                          "a kernel trace times each kernel alone (with --pipes 1)")
@@ -336,6 +342,10 @@ def main():
     if args.serial_stages:
         for pp in pipes:
             assert orbamd.load().orbx_debug_serial(pp.ext._h, 1) == 0
+    if args.alias_frames:
+        args.no_check = True
+        for pp in pipes:
+            assert orbamd.load().orbx_debug_alias_frames(pp.ext._h, 1) == 0
 
     for _ in range(args.warmup):
         sched.step()
@@ -563,8 +573,9 @@ def main():
             "dtype": "u8",
             "data": "synthetic (deterministic textured pan, SURVEY.md 8(d)); resident in HBM",
             "config": {"workload": cfg["name"] + ", scale 1.2, 8 levels, FAST 20/7; extract + BF "
-                                                 "SearchForTriangulation vs previous frame + per-step keyframe-slot "
-                                                 "all-gather & cross-agent SearchForTriangulation",
+                                                 "SearchForTriangulation vs previous frame + per-step keyframe "
+                                                 "BoW + slot all-gather & cross-agent SearchForTriangulation and "
+                                                 "SearchByBoW(KF,KF)",
                        "config": args.config, "frames_per_step_per_gpu": B, "graphs_per_gpu": P,
                        "graph_stagger": args.stagger,
                        "exchange_stream": "own" if async_x else "graph 0's",
@@ -573,6 +584,7 @@ def main():
             "checked_frames": check["checked_frames"] if check else 0,
             "checked_pairs": check["checked_pairs"] if check else 0,
             "checked_slots": check["checked_slots"] if check else 0,
+            "slot_bow_matches": check.get("slot_bow_matches") if check else None,
             "device_errors": err_msg,
             "roofline": roof,
             "match_roofline": {"bound": "mfma", "kernel": "k_tri_mfma", "achieved": round(m_tops, 2),

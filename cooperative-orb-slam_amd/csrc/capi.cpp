@@ -387,6 +387,9 @@ struct orbx_handle {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
     hipEvent_t ev_pyr = nullptr, ev_blur = nullptr;
+    // the per-level branches of small batches (run_extract_levels): a stream and fork / join events per level
+    hipStream_t lst[kMaxLevels] = {};
+    hipEvent_t lfork[kMaxLevels] = {}, ljoin[kMaxLevels] = {};
     hipEvent_t user_ev_pyr = nullptr;  // orbx_set_pyramid_event (caller-owned)
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
@@ -419,6 +422,7 @@ struct orbx_handle {
     double prof_ms[5] = {0, 0, 0, 0, 0};
     int skip_mask = 0;  // orbx_debug_skip_stages (test hook)
     bool serial = false;  // orbx_debug_serial (measurement hook): every stage in order on the caller's stream
+    bool alias = false;   // orbx_debug_alias_frames (measurement hook): every frame of a batch is frame 0
 };
 
 static const int kProfMaxCalls = 4096;
@@ -464,10 +468,9 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
     return 0;
 }
 
-static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fstride, int pitch, int nframes,
-                          hipStream_t st) {
+static int launch_pyramid(orbx_handle* h, const ExtractParams& ep, const uint8_t* d_frames, long long fstride,
+                          int pitch, int nframes, hipStream_t st) {
     Geometry& g = h->geo;
-    const ExtractParams& ep = g.ep;
     // pyramid levels 1..L-1 (ORBextractor.cc:1107-1132): whole-frame kernel for large batches of
     // 4-byte-aligned frames, per-level kernels otherwise
     const bool aligned = ((uintptr_t)d_frames & 3) == 0 && (fstride & 3) == 0 && (pitch & 3) == 0;
@@ -495,10 +498,10 @@ static int launch_pyramid(orbx_handle* h, const uint8_t* d_frames, long long fst
     return 0;
 }
 
-static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstride, int pitch, int cell_lo,
-                       int cell_hi, int nframes, hipStream_t st) {
+static int launch_fast(orbx_handle* h, const ExtractParams& ep, const uint8_t* d_frames, long long fstride, int pitch,
+                       int cell_lo, int cell_hi, int nframes, hipStream_t st) {
     Geometry& g = h->geo;
-    HIPR(launch_fast_cells2(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), g.ep, g.d_lv.as<LevelDesc>(),
+    HIPR(launch_fast_cells2(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, g.d_lv.as<LevelDesc>(),
                             g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), g.roi_pitch,
                             g.roi_rows, g.max_pass, cell_lo, cell_hi, nframes, st));
     return 0;
@@ -518,19 +521,102 @@ static int launch_fast(orbx_handle* h, const uint8_t* d_frames, long long fstrid
  * takes them; kErrCall (word 1) is the host paths' per-call flag (zeroed and read by each call), so a host
  * call never erases an unread batch error; kErrTake (word 32) receives the atomic read-and-clear. */
 constexpr int kErrWordSticky = 0, kErrWordCall = 1, kErrWordTake = 32;
+/* Small batches (the Tracking thread's one frame per call, ORBextractor.cc:1043-1105): the pyramid is a chain of
+ * per-level launches, and every level's FAST, octree and blur depend on that level alone, so each level runs as
+ * its own branch as soon as its resize is done (level 0 at once, beside the whole chain):
+ *
+ *   st  : resize 1 -> resize 2 -> ... -> resize L-1 ------------------------------> [join 0..L-1] describe
+ *   lst0: FAST(level 0) -> octree(0) -> blur(0) -> [join 0]
+ *   lstl:   [after resize l] FAST(l) -> octree(l) -> blur(l) -> [join l]
+ *
+ * The critical path is the longest branch (level 0's octree over ~1,240 keys) instead of the whole chain plus
+ * one FAST, octree and blur launch over every level. */
+static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nframes, const uint8_t* d_frames,
+                              long long fstride, int pitch, orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
+                              int kp_stride, hipStream_t st, int* errp) {
+    Geometry& g = h->geo;
+    const LevelDesc* dl = g.d_lv.as<LevelDesc>();
+    for (int l = 0; l < ep.L; l++) {
+        if (!h->lst[l]) HIPR(hipStreamCreateWithFlags(&h->lst[l], hipStreamNonBlocking));
+        if (!h->lfork[l]) HIPR(hipEventCreateWithFlags(&h->lfork[l], hipEventDisableTiming));
+        if (!h->ljoin[l]) HIPR(hipEventCreateWithFlags(&h->ljoin[l], hipEventDisableTiming));
+    }
+    auto branch = [&](int l) -> int {
+        hipStream_t ls = h->lst[l];
+        HIPR(hipEventRecord(h->lfork[l], st));
+        HIPR(hipStreamWaitEvent(ls, h->lfork[l], 0));
+        const LevelDesc& lv = g.lv[l];
+        if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, lv.cell_begin, lv.cell_begin + lv.ncells,
+                                               nframes, ls))
+            return ORBX_EDEVICE;
+        if (!(h->skip_mask & 4))
+            HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
+                               h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
+                               (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, ls, l, 1));
+        if (!(h->skip_mask & 8))
+            HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                                    g.bjob_begin[l], g.bjob_begin[l + 1], nullptr, nframes, ls));
+        HIPR(hipEventRecord(h->ljoin[l], ls));
+        return 0;
+    };
+    if (branch(0)) return ORBX_EDEVICE;
+    for (int l = 1; l < ep.L; l++) {
+        if (!(h->skip_mask & 1)) {
+            const LevelDesc& s = g.lv[l - 1];
+            const LevelDesc& d = g.lv[l];
+            const uint8_t* src = l == 1 ? d_frames : h->pyr.as<uint8_t>() + s.pyr_off;
+            const long long sfs = l == 1 ? fstride : ep.pyr_frame_bytes;
+            const int sp = l == 1 ? pitch : s.pitch;
+            if (g.tiled_ok[l])
+                HIPR(launch_resize_tiled(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes,
+                                         d.pitch, d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end,
+                                         nframes, st));
+            else
+                HIPR(launch_resize(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes,
+                                   d.pitch, d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, st));
+        }
+        if (branch(l)) return ORBX_EDEVICE;
+    }
+    for (int l = 0; l < ep.L; l++) HIPR(hipStreamWaitEvent(st, h->ljoin[l], 0));
+    if (!(h->skip_mask & 16))
+        HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                             h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
+                             g.d_ptab.as<int>(), nframes, st));
+    return 0;
+}
+
 static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
                        orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st,
                        bool host_call = true) {
     Geometry& g = h->geo;
-    const ExtractParams& ep = g.ep;
+    // the L2-residency bound (orbx_debug_alias_frames): every frame of the batch reads frame 0's image and
+    // shares one pyramid / blur buffer, so the stages read lines other workgroups of the launch keep in L2
+    ExtractParams ep_alias = g.ep;
+    if (h->alias) {
+        ep_alias.pyr_frame_bytes = 0;
+        ep_alias.blur_frame_bytes = 0;
+        fstride = 0;
+    }
+    const ExtractParams& ep = ep_alias;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
     hipStream_t sd = h->serial ? st : h->side;
     // the host-buffer paths report their own per-call word; the device batch path leaves word 0 sticky
     // until orbx_check_error takes (and clears) it, so no fill kernel sits on the batch stream every call
     int* errp = h->err.as<int>() + (host_call ? kErrWordCall : kErrWordSticky);
     if (host_call) HIPR(hipMemsetAsync(errp, 0, sizeof(int), st));
+    if (nframes < kPyrFramesMinBatch && !h->serial && !h->prof_on && !h->alias) {
+        if (run_extract_levels(h, ep, nframes, d_frames, fstride, pitch, d_kps, d_desc, d_counts, kp_stride, st, errp))
+            return ORBX_EDEVICE;
+        if (!host_call && h->user_ev_pyr) HIPR(hipEventRecord(h->user_ev_pyr, st));
+        h->last_frames = d_frames;
+        h->last_fstride = fstride;
+        h->last_pitch = pitch;
+        h->last_nframes = nframes;
+        h->last_stream = st;
+        return 0;
+    }
     if (prof_mark(h, 0, 0, st)) return ORBX_EDEVICE;
-    if (!(h->skip_mask & 1) && launch_pyramid(h, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
+    if (!(h->skip_mask & 1) && launch_pyramid(h, ep, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 0, 1, st)) return ORBX_EDEVICE;
     if (!host_call && h->user_ev_pyr) HIPR(hipEventRecord(h->user_ev_pyr, st));
     if (!h->serial) {
@@ -539,12 +625,12 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     }
     if (prof_mark(h, 3, 0, sd)) return ORBX_EDEVICE;
     if (!(h->skip_mask & 8))
-        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl, nullptr,
+        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl, 0,
                                 g.nbjobs, nullptr, nframes, sd));
     if (prof_mark(h, 3, 1, sd)) return ORBX_EDEVICE;
     if (!h->serial) HIPR(hipEventRecord(h->ev_blur, sd));
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
-    if (!(h->skip_mask & 2) && launch_fast(h, d_frames, fstride, pitch, 0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
+    if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 1, 1, st) || prof_mark(h, 2, 0, st)) return ORBX_EDEVICE;
     if (!(h->skip_mask & 4))
         HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
@@ -614,6 +700,8 @@ void orbx_destroy(orbx_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->side) (void)hipStreamSynchronize(h->side);
+    for (hipStream_t ls : h->lst)
+        if (ls) (void)hipStreamSynchronize(ls);
     for (DevBuf* b : {&h->pyr, &h->blur, &h->cellkey, &h->cellcnt, &h->lvkey, &h->lvcnt, &h->gscratch, &h->err,
                       &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt, &h->st_buf})
         b->release();
@@ -622,6 +710,11 @@ void orbx_destroy(orbx_handle* h) {
     if (h->side) (void)hipStreamDestroy(h->side);
     for (hipEvent_t e : {h->ev_pyr, h->ev_blur})
         if (e) (void)hipEventDestroy(e);
+    for (int l = 0; l < kMaxLevels; l++) {
+        if (h->lst[l]) (void)hipStreamDestroy(h->lst[l]);
+        if (h->lfork[l]) (void)hipEventDestroy(h->lfork[l]);
+        if (h->ljoin[l]) (void)hipEventDestroy(h->ljoin[l]);
+    }
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
     if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
     if (h->graph) (void)hipGraphDestroy(h->graph);
@@ -665,6 +758,12 @@ int orbx_debug_skip_stages(orbx_handle* h, int mask) {
 int orbx_debug_serial(orbx_handle* h, int on) {
     if (!h) return ORBX_EARG;
     h->serial = on != 0;
+    return 0;
+}
+
+int orbx_debug_alias_frames(orbx_handle* h, int on) {
+    if (!h) return ORBX_EARG;
+    h->alias = on != 0;
     return 0;
 }
 

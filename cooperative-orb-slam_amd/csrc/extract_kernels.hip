@@ -784,13 +784,13 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                                                 const uint32_t* __restrict__ cellkey,
                                                 const int* __restrict__ cellcnt, uint32_t* __restrict__ lvkey,
                                                 int* __restrict__ lvcnt, uint8_t* __restrict__ gscratch,
-                                                long long gscratch_frame_bytes, int NC, int KL,
+                                                long long gscratch_frame_bytes, int NC, int KL, int level0,
                                                 int* __restrict__ err) {
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int red[8];
     __shared__ int sh_size, sh_jstar, sh_tc, sh_nexp, sh_ndiv;
     const int tid = threadIdx.x;
-    const int l = blockIdx.x, f = blockIdx.y;
+    const int l = level0 + blockIdx.x, f = blockIdx.y;
     const LevelDesc lv = levels[l];
     // --- carve LDS
     uint8_t* p = lds;
@@ -1205,12 +1205,12 @@ template <bool kAligned>
 __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
                                                      const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                      ExtractParams ep, const LevelDesc* __restrict__ levels,
-                                                     const int* __restrict__ lvcnt) {
+                                                     int job0, int job1, const int* __restrict__ lvcnt) {
     __shared__ __align__(16) uint8_t s_rows[4][7][kBlurSeg];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int f = blockIdx.y;
-    int j = blockIdx.x * 4 + wave;
-    if (j >= ep.bjob_begin[ep.L]) return;
+    int j = job0 + blockIdx.x * 4 + wave;
+    if (j >= job1) return;
     const int l = level_of(ep.bjob_begin, ep.L, j);
     j -= ep.bjob_begin[l];
     // the reference blurs only levels with keypoints (:1081); lvcnt == nullptr blurs every level
@@ -1598,24 +1598,27 @@ hipError_t octree_setup(int lds_bytes) {
 hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                          const uint32_t* cellkey, const int* cellcnt, uint32_t* lvkey, int* lvcnt,
                          uint8_t* gscratch, long long gscratch_frame_bytes, int NC, int KL, int lds_bytes,
-                         int* err, int nframes, hipStream_t st) {
-    dim3 grid(ep.L, nframes);
+                         int* err, int nframes, hipStream_t st, int level0, int nlevels) {
+    if (nlevels < 0) nlevels = ep.L - level0;
+    if (level0 < 0 || nlevels < 1 || level0 + nlevels > ep.L) return hipErrorInvalidValue;
+    dim3 grid(nlevels, nframes);
     hipLaunchKernelGGL(k_octree, grid, dim3(256), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey, lvcnt,
-                       gscratch, gscratch_frame_bytes, NC, KL, err);
+                       gscratch, gscratch_frame_bytes, NC, KL, level0, err);
     return hipGetLastError();
 }
 
 hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
-                              const ExtractParams& ep, const LevelDesc* levels, const int* job_begin, int njobs,
-                              const int* lvcnt, int nframes, hipStream_t st) {
-    dim3 grid((njobs + 3) / 4, nframes);
+                              const ExtractParams& ep, const LevelDesc* levels, int job0, int job1, const int* lvcnt,
+                              int nframes, hipStream_t st) {
+    if (job1 <= job0) return hipSuccess;
+    dim3 grid((job1 - job0 + 3) / 4, nframes);
     const bool aligned = (((uintptr_t)frames | (uintptr_t)fstride | (uintptr_t)pitch0) & 3) == 0;
     if (aligned)
         hipLaunchKernelGGL(k_blur_strips<true>, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
-                           lvcnt);
+                           job0, job1, lvcnt);
     else
         hipLaunchKernelGGL(k_blur_strips<false>, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
-                           lvcnt);
+                           job0, job1, lvcnt);
     return hipGetLastError();
 }
 

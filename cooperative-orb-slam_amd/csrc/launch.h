@@ -30,10 +30,11 @@ hipError_t launch_sincos_selftest(const float* in, float* so, float* co, int n, 
 hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                          const uint32_t* cellkey, const int* cellcnt, uint32_t* lvkey, int* lvcnt,
                          uint8_t* gscratch, long long gscratch_frame_bytes, int NC, int KL, int lds_bytes,
-                         int* err, int nframes, hipStream_t st);
+                         int* err, int nframes, hipStream_t st, int level0 = 0, int nlevels = -1);
+/* blur jobs [job0, job1) (ExtractParams::bjob_begin numbers every level's strips) */
 hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
-                              const ExtractParams& ep, const LevelDesc* levels, const int* job_begin, int njobs,
-                              const int* lvcnt, int nframes, hipStream_t st);
+                              const ExtractParams& ep, const LevelDesc* levels, int job0, int job1, const int* lvcnt,
+                              int nframes, hipStream_t st);
 hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                            const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
                            const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,

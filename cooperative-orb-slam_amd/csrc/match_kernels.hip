@@ -990,6 +990,7 @@ namespace orbamd {
 hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
                          int32_t* nmatches, hipStream_t st) {
+    if (npairs == 0) return hipSuccess;
     dim3 grid((kp_stride + 32 * kMfWaves - 1) / (32 * kMfWaves), npairs);
     hipLaunchKernelGGL(k_tri_mfma, grid, dim3(kMfThreads), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
                        nmatches);

@@ -106,6 +106,7 @@ SIGNATURES = {
     "orbx_set_pyramid_event": (_I, [_P, _P]),
     "orbx_debug_skip_stages": (_I, [_P, _I]),
     "orbx_debug_serial": (_I, [_P, _I]),
+    "orbx_debug_alias_frames": (_I, [_P, _I]),
     "orbx_debug_raise_error": (_I, [_P, _I, _P]),
     "orbm_create": (_I, [_I, C.POINTER(_P)]),
     "orbm_destroy": (None, [_P]),

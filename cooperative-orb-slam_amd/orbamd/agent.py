@@ -34,11 +34,12 @@ LOOP_NNRATIO = 0.75   # LoopClosing::ComputeSim3's ORBmatcher(0.75, true) (LoopC
 
 def kf_mp_flags(n):
     """Synthetic MapPoint records of the bench keyframe (the slot's MPFLAGS: bit 0 = mvpMapPoints[i] != NULL,
-    bit 1 = isBad()): about 80 % of the features carry a MapPoint, about 5 % of those bad; a fixed hash of the
+    bit 1 = isBad()): about half of the features carry a MapPoint (the loop-candidate SearchByBoW matches those),
+    about 5 % of them bad; the other half are what SearchForTriangulation may triangulate. A fixed hash of the
     feature index, so the oracle check rebuilds them."""
     import numpy as np
     h = (np.arange(n, dtype=np.uint64) * np.uint64(2654435761)) & np.uint64(0xFFFFFFFF)
-    mp = ((h >> np.uint64(8)) % np.uint64(10)) < np.uint64(8)
+    mp = ((h >> np.uint64(8)) % np.uint64(10)) < np.uint64(5)
     bad = mp & (((h >> np.uint64(20)) % np.uint64(20)) == np.uint64(0))
     return (mp.astype(np.uint8) | (bad.astype(np.uint8) << 1)).astype(np.uint8)
 

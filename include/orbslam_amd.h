@@ -669,6 +669,12 @@ int orbx_debug_skip_stages(orbx_handle* h, int mask);
  * default fork/join schedule. Outputs are identical either way. */
 int orbx_debug_serial(orbx_handle* h, int on);
 
+/* Measurement hook (the L2-residency bound of DESIGN.md 6.0): on != 0 makes every frame of this
+ * handle's subsequent batched extractions read frame 0's image and share one pyramid and one blurred
+ * pyramid, so every stage reads data the launch keeps in L2; each frame's outputs are then frame 0's.
+ * Never on in the product; 0 = off (the default). */
+int orbx_debug_alias_frames(orbx_handle* h, int on);
+
 /* Test hook: ORs `flag` (> 0) into the handle's sticky batch error word, as a failing device batch
  * would; the tests use it to show that host-path extractions (orbx_extract) neither clear nor hide it
  * and that orbx_check_error reports and clears it once. */

@@ -40,8 +40,8 @@ def main():
     xm, xn, xb, xbn = sched.exchange_results()
     print("rank", rank, res, "cross-agent matches", list(xn), "SearchByBoW", list(xbn), flush=True)
     assert res["bit_exact"], res["mismatches"]
-    assert res["checked_slots"] == world and all(int(v) > 0 for v in xn)
-    assert int(xbn[rank]) > 0  # its own keyframe: the loop-candidate match finds it
+    # every slot checked bit-exact above; its own keyframe gives both matchers work
+    assert res["checked_slots"] == world and int(xn[rank]) > 0 and int(xbn[rank]) > 0
     sched.close()
     dist.barrier()
     dist.destroy_process_group()

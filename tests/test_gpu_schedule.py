@@ -88,3 +88,23 @@ def test_serial_measurement_hook_bit_exact():
     assert res["bit_exact"], res["mismatches"]
     assert res["checked_frames"] == B
     sched.close()
+
+
+def test_alias_frames_measurement_hook():
+    """orbx_debug_alias_frames (the L2-residency bound of DESIGN.md 6.0): every frame of a batch then yields
+    frame 0's keypoints and descriptors, equal to the oracle's on frame 0"""
+    torch = pytest.importorskip("torch")
+    import numpy as np
+    import oracle_py
+    from orbamd.device import BatchPipeline
+    W, H, B = 640, 480, 64
+    frames = orbamd.synth_frames(0, 0, B, W, H)
+    pp = BatchPipeline(torch, W, H, B)
+    assert orbamd.load().orbx_debug_alias_frames(pp.ext._h, 1) == 0
+    pp.extract(torch.from_numpy(frames).cuda())
+    torch.cuda.synchronize()
+    ko, do = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)(frames[0])
+    for b in (0, 1, 33, B - 1):
+        kg, dg, _ = pp.host_results(b)
+        assert kg.tobytes() == ko.tobytes() and np.array_equal(dg, do), b
+    pp.close()
