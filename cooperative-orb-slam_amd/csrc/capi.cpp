@@ -387,7 +387,7 @@ struct orbx_handle {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
     hipEvent_t ev_pyr = nullptr, ev_blur = nullptr;
-    // the per-level branches of small batches (run_extract_levels): a stream and fork / join events per level
+    // the level-0 branch of small batches (run_extract_levels) uses entry 0: a stream, fork / join events
     hipStream_t lst[kMaxLevels] = {};
     hipEvent_t lfork[kMaxLevels] = {}, ljoin[kMaxLevels] = {};
     hipEvent_t user_ev_pyr = nullptr;  // orbx_set_pyramid_event (caller-owned)
@@ -413,6 +413,7 @@ struct orbx_handle {
     int graph_warm = 0;         // eager runs at the current epoch (the first one runs uncaptured)
     uint8_t* pin_in = nullptr;  // W*H frame
     uint8_t* pin_out = nullptr; // {cnt, err} + K orbx_kp + K x 32 descriptors
+    uint8_t* pin_out_dev = nullptr;  // its device-mapped address: the graph's kernels write the results there
     size_t pin_in_bytes = 0, pin_out_bytes = 0;
     // stage profiling (orbx_profile_*)
     bool prof_on = false;
@@ -518,66 +519,57 @@ static int launch_fast(orbx_handle* h, const ExtractParams& ep, const uint8_t* d
  * reads only levels with keypoints.) h->serial (orbx_debug_serial, a measurement hook) runs every
  * stage in order on `st`, so each kernel runs alone. */
 /* Error words of h->err: kErrSticky (word 0) collects the device batch paths' flags until orbx_check_error
- * takes them; kErrCall (word 1) is the host paths' per-call flag (zeroed and read by each call), so a host
- * call never erases an unread batch error; kErrTake (word 32) receives the atomic read-and-clear. */
-constexpr int kErrWordSticky = 0, kErrWordCall = 1, kErrWordTake = 32;
+ * takes them (kErrTake, word 32, receives the atomic read-and-clear); kErrExtract (word 2) is the host-buffer
+ * extraction's per-call flag, read and cleared by the call's last launch (k_flag_take), so it is clean for the
+ * next call; kErrCall (word 1) is the stereo host call's (zeroed and read by that call). A host call never
+ * erases an unread batch error. */
+constexpr int kErrWordSticky = 0, kErrWordCall = 1, kErrWordExtract = 2, kErrWordTake = 32, kErrWordExtractTake = 33;
 /* Small batches (the Tracking thread's one frame per call, ORBextractor.cc:1043-1105): the pyramid is a chain of
- * per-level launches, and every level's FAST, octree and blur depend on that level alone, so each level runs as
- * its own branch as soon as its resize is done (level 0 at once, beside the whole chain):
+ * per-level launches and level 0 needs none of it, so level 0's FAST and octree (the longest octree: ~1,240 keys
+ * at 640x480) run on a side branch from the start, beside the chain:
  *
- *   st  : resize 1 -> resize 2 -> ... -> resize L-1 ------------------------------> [join 0..L-1] describe
- *   lst0: FAST(level 0) -> octree(0) -> blur(0) -> [join 0]
- *   lstl:   [after resize l] FAST(l) -> octree(l) -> blur(l) -> [join l]
+ *   st  : resize 1 .. L-1 -> [ev_pyr] FAST(levels 1..L-1) -> octree(1..L-1) -> [ev_blur, join 0] describe
+ *   lst0: FAST(level 0) -> octree(0) -> [join 0]
+ *   side:                    [ev_pyr] blur(all levels) -> [ev_blur]
  *
- * The critical path is the longest branch (level 0's octree over ~1,240 keys) instead of the whole chain plus
- * one FAST, octree and blur launch over every level. */
+ * (A branch per level, each with its own FAST, octree and blur, measured 2x slower: 4 hardware queues serialise
+ * the branches and every level's blur launch costs a strip's ~23 us chain; profiles/r04_latency_branches.log.) */
 static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nframes, const uint8_t* d_frames,
                               long long fstride, int pitch, orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
                               int kp_stride, hipStream_t st, int* errp) {
     Geometry& g = h->geo;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
-    for (int l = 0; l < ep.L; l++) {
-        if (!h->lst[l]) HIPR(hipStreamCreateWithFlags(&h->lst[l], hipStreamNonBlocking));
-        if (!h->lfork[l]) HIPR(hipEventCreateWithFlags(&h->lfork[l], hipEventDisableTiming));
-        if (!h->ljoin[l]) HIPR(hipEventCreateWithFlags(&h->ljoin[l], hipEventDisableTiming));
-    }
-    auto branch = [&](int l) -> int {
-        hipStream_t ls = h->lst[l];
-        HIPR(hipEventRecord(h->lfork[l], st));
-        HIPR(hipStreamWaitEvent(ls, h->lfork[l], 0));
-        const LevelDesc& lv = g.lv[l];
-        if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, lv.cell_begin, lv.cell_begin + lv.ncells,
-                                               nframes, ls))
-            return ORBX_EDEVICE;
+    if (!h->lst[0]) HIPR(hipStreamCreateWithFlags(&h->lst[0], hipStreamNonBlocking));
+    if (!h->lfork[0]) HIPR(hipEventCreateWithFlags(&h->lfork[0], hipEventDisableTiming));
+    if (!h->ljoin[0]) HIPR(hipEventCreateWithFlags(&h->ljoin[0], hipEventDisableTiming));
+    auto octree = [&](int l0, int nl, hipStream_t s2) -> int {
         if (!(h->skip_mask & 4))
             HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                                h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
-                               (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, ls, l, 1));
-        if (!(h->skip_mask & 8))
-            HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                                    g.bjob_begin[l], g.bjob_begin[l + 1], nullptr, nframes, ls));
-        HIPR(hipEventRecord(h->ljoin[l], ls));
+                               (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, s2, l0, nl));
         return 0;
     };
-    if (branch(0)) return ORBX_EDEVICE;
-    for (int l = 1; l < ep.L; l++) {
-        if (!(h->skip_mask & 1)) {
-            const LevelDesc& s = g.lv[l - 1];
-            const LevelDesc& d = g.lv[l];
-            const uint8_t* src = l == 1 ? d_frames : h->pyr.as<uint8_t>() + s.pyr_off;
-            const long long sfs = l == 1 ? fstride : ep.pyr_frame_bytes;
-            const int sp = l == 1 ? pitch : s.pitch;
-            if (g.tiled_ok[l])
-                HIPR(launch_resize_tiled(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes,
-                                         d.pitch, d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end,
-                                         nframes, st));
-            else
-                HIPR(launch_resize(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes,
-                                   d.pitch, d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, st));
-        }
-        if (branch(l)) return ORBX_EDEVICE;
+    const int nc0 = g.lv[0].ncells;
+    hipStream_t l0s = h->lst[0];
+    HIPR(hipEventRecord(h->lfork[0], st));
+    HIPR(hipStreamWaitEvent(l0s, h->lfork[0], 0));
+    if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, nc0, nframes, l0s)) return ORBX_EDEVICE;
+    if (octree(0, 1, l0s)) return ORBX_EDEVICE;
+    HIPR(hipEventRecord(h->ljoin[0], l0s));
+    if (!(h->skip_mask & 1) && launch_pyramid(h, ep, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
+    HIPR(hipEventRecord(h->ev_pyr, st));
+    HIPR(hipStreamWaitEvent(h->side, h->ev_pyr, 0));
+    if (!(h->skip_mask & 8))
+        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl, 0, g.nbjobs,
+                                nullptr, nframes, h->side));
+    HIPR(hipEventRecord(h->ev_blur, h->side));
+    if (ep.L > 1) {
+        if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, nc0, ep.ncells, nframes, st))
+            return ORBX_EDEVICE;
+        if (octree(1, ep.L - 1, st)) return ORBX_EDEVICE;
     }
-    for (int l = 0; l < ep.L; l++) HIPR(hipStreamWaitEvent(st, h->ljoin[l], 0));
+    HIPR(hipStreamWaitEvent(st, h->ljoin[0], 0));
+    HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     if (!(h->skip_mask & 16))
         HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                              h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
@@ -602,8 +594,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     hipStream_t sd = h->serial ? st : h->side;
     // the host-buffer paths report their own per-call word; the device batch path leaves word 0 sticky
     // until orbx_check_error takes (and clears) it, so no fill kernel sits on the batch stream every call
-    int* errp = h->err.as<int>() + (host_call ? kErrWordCall : kErrWordSticky);
-    if (host_call) HIPR(hipMemsetAsync(errp, 0, sizeof(int), st));
+    int* errp = h->err.as<int>() + (host_call ? kErrWordExtract : kErrWordSticky);
     if (nframes < kPyrFramesMinBatch && !h->serial && !h->prof_on && !h->alias) {
         if (run_extract_levels(h, ep, nframes, d_frames, fstride, pitch, d_kps, d_desc, d_counts, kp_stride, st, errp))
             return ORBX_EDEVICE;
@@ -859,21 +850,22 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
         h->pin_out_bytes = 0;
         HIPR(hipHostMalloc((void**)&h->pin_out, out_bytes, hipHostMallocDefault));
         h->pin_out_bytes = out_bytes;
+        HIPR(hipHostGetDevicePointer((void**)&h->pin_out_dev, h->pin_out, 0));
         h->epoch++;
     }
     for (int y = 0; y < height; y++) memcpy(h->pin_in + (size_t)y * width, img + (size_t)y * pitch, width);
     uint8_t* o_kps = h->pin_out + 64;
     uint8_t* o_desc = o_kps + sizeof(orbx_kp) * (size_t)K;
+    // describe writes the count, keypoints and descriptors straight into the pinned buffer (its device-mapped
+    // address: 56 B per keypoint over PCIe inside the kernel, no D2H copies), and the last launch moves the
+    // call's error word there and clears it for the next call
+    uint8_t* d_out = h->pin_out_dev;
     auto enqueue = [&]() -> int {
         HIPR(hipMemcpyAsync(h->in_frame.p, h->pin_in, in_bytes, hipMemcpyHostToDevice, h->stream));
-        int rc = run_extract(h, 1, h->in_frame.as<uint8_t>(), (long long)in_bytes, width, h->out_kps.as<orbx_kp>(),
-                             h->out_desc.as<uint8_t>(), h->out_cnt.as<int32_t>(), K, h->stream);
+        int rc = run_extract(h, 1, h->in_frame.as<uint8_t>(), (long long)in_bytes, width, (orbx_kp*)(d_out + 64),
+                             d_out + 64 + sizeof(orbx_kp) * (size_t)K, (int32_t*)d_out, K, h->stream);
         if (rc) return rc;
-        HIPR(hipMemcpyAsync(h->pin_out, h->out_cnt.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-        HIPR(hipMemcpyAsync(h->pin_out + 4, h->err.as<int>() + kErrWordCall, sizeof(int), hipMemcpyDeviceToHost,
-                            h->stream));
-        HIPR(hipMemcpyAsync(o_kps, h->out_kps.p, sizeof(orbx_kp) * (size_t)K, hipMemcpyDeviceToHost, h->stream));
-        HIPR(hipMemcpyAsync(o_desc, h->out_desc.p, 32 * (size_t)K, hipMemcpyDeviceToHost, h->stream));
+        HIPR(launch_flag_take(h->err.as<int32_t>() + kErrWordExtract, (int32_t*)(d_out + 4), h->stream));
         return 0;
     };
     const bool valid = h->gexec && h->graph_w == width && h->graph_h == height && h->graph_epoch == h->epoch;
@@ -950,7 +942,8 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int width, int height, size
     if (rc) return rc;
     int cnt = 0, errflag = 0;
     HIPR(hipMemcpyAsync(&cnt, h->out_cnt.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-    HIPR(hipMemcpyAsync(&errflag, h->err.as<int>() + kErrWordCall, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPR(launch_flag_take(h->err.as<int32_t>() + kErrWordExtract, h->err.as<int32_t>() + kErrWordExtractTake, h->stream));
+    HIPR(hipMemcpyAsync(&errflag, h->err.as<int>() + kErrWordExtractTake, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     HIPR(hipStreamSynchronize(h->stream));
     if (errflag) return ORBX_EDEVICE;
     if (cnt > cap) return ORBX_ECAPACITY;
