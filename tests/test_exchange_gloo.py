@@ -1,7 +1,8 @@
 """Multi-agent exchange on CPU: world_size-2 gloo all-gather of keyframe slots (packed by the
-library's host packer, orbx_pack_keyframe_host; decoded by its validating parser, orbx_slot_parse)
-and the cross-agent SearchForTriangulation (oracle as the matcher) equal a single-process run that
-matches the concatenated buffers."""
+library's host packer, orbx_pack_keyframe_host, with the keyframe's FeatureVector and MapPoint records
+as the bench's exchange packs them; decoded by its validating parser, orbx_slot_parse) and the
+cross-agent SearchForTriangulation and loop-candidate SearchByBoW(KF,KF) (oracle as the matcher) equal
+a single-process run that matches the concatenated buffers."""
 import os
 import socket
 
@@ -28,24 +29,60 @@ def _agent_keyframe(agent):
     return k, d, orc.tables()
 
 
+_VOC = []
+
+
+def _vocabulary():
+    """a small synthetic vocabulary (k = 10, L = 4) on the oracle, built once per process"""
+    if not _VOC:
+        import oracle_py
+        from orbamd.vocabulary import L1_NORM, TF_IDF, synth_vocabulary
+        k, L, par, leaf, desc, w = synth_vocabulary(k=10, L=4, seed=3)
+        _VOC.append(oracle_py.OracleVocabulary(k, L, L1_NORM, TF_IDF, par, leaf, desc, w))
+    return _VOC[0]
+
+
+def _fv_csr(fv):
+    ids = sorted(fv)
+    off = np.concatenate([[0], np.cumsum([len(fv[i]) for i in ids])]).astype(np.int32)
+    feat = np.concatenate([np.asarray(fv[i], np.int32) for i in ids]) if ids else np.zeros(0, np.int32)
+    return np.asarray(ids, np.uint32), off, feat
+
+
 def _pack(agent, k, d, tabs, cap):
     from orbamd import exchange
+    from orbamd.agent import kf_mp_flags
     meta = exchange.make_meta(agent=agent, mnId=agent, scale=tabs["scale"], sigma2=tabs["sigma2"])
-    return exchange.pack_host(meta, k, d, cap)
+    bow, fv = _vocabulary().transform(d, 2)
+    return exchange.pack_host(meta, k, d, cap, mp_flags=kf_mp_flags(len(k)), bow=bow, fv=_fv_csr(fv))
 
 
 def _cross_match(kq, dq, tabs, slots):
+    """per slot: SearchForTriangulation (features with a MapPoint skipped on both sides) and SearchByBoW(KF,KF)
+    (ORBmatcher(0.75, true), LoopClosing's loop-candidate match) of the querying keyframe, from the decoded slot"""
     import oracle_py
     import orbamd
     from orbamd import exchange
+    from orbamd.agent import kf_mp_flags
     F12, ex, ey = orbamd.device.default_geometry()
     out = []
-    vq = orbamd.KeyFrameView(kq, dq, tabs["scale"], tabs["sigma2"])
+    fq = kf_mp_flags(len(kq))
+    fvq = _vocabulary().transform(dq, 2)[1]
+    vq = orbamd.KeyFrameView(kq, dq, tabs["scale"], tabs["sigma2"], has_mp=(fq & 1).astype(bool),
+                             mp_bad=((fq >> 1) & 1).astype(bool))
+    vqb = orbamd.KeyFrameView(kq, dq, tabs["scale"], tabs["sigma2"], feat_vec=fvq, has_mp=(fq & 1).astype(bool),
+                              mp_bad=((fq >> 1) & 1).astype(bool))
     for buf in slots:
         got = exchange.parse(buf)
-        k2, d2 = got["kps"], got["desc"]
-        v2 = orbamd.KeyFrameView(k2, d2, got["meta"].mvScaleFactors[:8], got["meta"].mvLevelSigma2[:8])
+        k2, d2, f2 = got["kps"], got["desc"], got["mp_flags"]
+        sc, sg = got["meta"].mvScaleFactors[:8], got["meta"].mvLevelSigma2[:8]
+        mp2, bad2 = (f2 & 1).astype(bool), ((f2 >> 1) & 1).astype(bool)
+        fv2 = {int(got["fv_node"][i]): list(got["fv_feat"][got["fv_off"][i]:got["fv_off"][i + 1]])
+               for i in range(len(got["fv_node"]))}
+        v2 = orbamd.KeyFrameView(k2, d2, sc, sg, has_mp=mp2, mp_bad=bad2)
+        v2b = orbamd.KeyFrameView(k2, d2, sc, sg, feat_vec=fv2, has_mp=mp2, mp_bad=bad2)
         out.append(oracle_py.search_for_triangulation(vq, v2, F12, ex, ey, False, False)[1])
+        out.append(oracle_py.search_by_bow(vqb, v2b, 0.75, True, other_is_keyframe=True)[1])
     return out
 
 
@@ -89,4 +126,7 @@ def test_gloo_allgather_cross_agent_match():
     for r in range(world):
         exp = _cross_match(kfs[r][0], kfs[r][1], kfs[r][2], slots)
         assert [e.tolist() for e in exp] == got[r]
-        assert sum(x >= 0 for x in got[r][r]) > 0.5 * len(kfs[r][0])  # self-match sanity
+        # self-match sanity: the features without a MapPoint triangulate against themselves, those with a good one
+        # are found by the loop-candidate SearchByBoW
+        assert sum(x >= 0 for x in got[r][2 * r]) > 0.3 * len(kfs[r][0])
+        assert sum(x >= 0 for x in got[r][2 * r + 1]) > 0.3 * len(kfs[r][0])
