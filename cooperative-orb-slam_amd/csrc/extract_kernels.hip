@@ -736,6 +736,7 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
 /* divides them by (size desc, creation desc) and stops at the first division that      */
 /* reaches N (ORBextractor.cc:676-737; pointer tie-break pinned to creation order).      */
 /* ----------------------------------------------------------------------------------- */
+template <int NW>
 __device__ int block_scan_excl(int v, int* total, int* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int inc = v;
@@ -748,7 +749,7 @@ __device__ int block_scan_excl(int v, int* total, int* red) {
     __syncthreads();
     int woff = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < NW; i++) {
         const int s = red[i];
         woff += (i < w) ? s : 0;
         tot += s;
@@ -758,9 +759,10 @@ __device__ int block_scan_excl(int v, int* total, int* red) {
     return woff + inc - v;
 }
 
+template <int NW>
 __device__ __forceinline__ int block_sum(int v, int* red) {
     int tot;
-    block_scan_excl(v, &tot, red);
+    block_scan_excl<NW>(v, &tot, red);
     return tot;
 }
 
@@ -779,7 +781,8 @@ struct NodeT {
     uint16_t* x0; uint16_t* y0; uint16_t* x1; uint16_t* y1; int* nk; uint32_t* seq;
 };
 
-__global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDesc* __restrict__ levels,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc* __restrict__ levels,
                                                 const CellDesc* __restrict__ cells,
                                                 const uint32_t* __restrict__ cellkey,
                                                 const int* __restrict__ cellcnt, uint32_t* __restrict__ lvkey,
@@ -787,7 +790,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                                                 long long gscratch_frame_bytes, int NC, int KL, int level0,
                                                 int* __restrict__ err) {
     extern __shared__ __align__(16) uint8_t lds[];
-    __shared__ int red[8];
+    __shared__ int red[16];
     __shared__ int sh_size, sh_jstar, sh_tc, sh_nexp, sh_ndiv;
     const int tid = threadIdx.x;
     const int l = level0 + blockIdx.x, f = blockIdx.y;
@@ -814,11 +817,11 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
     // cell offsets -> reuse dbase/spos as temp (ncells may exceed NC: chunked)
     __syncthreads();
     int n = 0;
-    for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
+    for (int c0 = 0; c0 < lv.ncells; c0 += NT) {
         const int c = c0 + tid;
         const int v = c < lv.ncells ? ccnt[c] : 0;
         int tot;
-        const int off = block_scan_excl(v, &tot, red) + carry;
+        const int off = block_scan_excl<NT / 64>(v, &tot, red) + carry;
         carry += tot;
         (void)off;
     }
@@ -832,17 +835,17 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         carry = 0;
         if (2 * lv.ncells + 2 <= 4 * NC) {
             // flat gather: the cells' key offsets and slots go to LDS (cnt4's space, unused until the roots),
-            // then thread t copies keys t, t+256, ... finding each key's cell by a fixed-trip binary search, four
+            // then thread t copies keys t, t+NT, ... finding each key's cell by a fixed-trip binary search, four
             // keys in flight per thread. (A thread per cell copying its keys one by one waited on one global
             // load per key of the level's fullest cell: the level-0 workgroup's long pole.)
             int* coff = cnt4;                   // [ncells + 1]
             int* cslot = cnt4 + lv.ncells + 1;  // [ncells]
-            for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
+            for (int c0 = 0; c0 < lv.ncells; c0 += NT) {
                 const int c = c0 + tid;
                 const int v = c < lv.ncells ? ccnt[c] : 0;
                 const int sl = c < lv.ncells ? cells[lv.cell_begin + c].slot : 0;
                 int tot;
-                const int off = block_scan_excl(v, &tot, red) + carry;
+                const int off = block_scan_excl<NT / 64>(v, &tot, red) + carry;
                 if (c < lv.ncells) {
                     coff[c] = off;
                     cslot[c] = sl;
@@ -854,14 +857,14 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
             int top = 1;
             while (top < lv.ncells) top <<= 1;
             constexpr int kG = 4;
-            for (int i0 = tid; i0 < n; i0 += 256 * kG) {
+            for (int i0 = tid; i0 < n; i0 += NT * kG) {
                 int pos[kG];
 #pragma unroll
                 for (int g = 0; g < kG; g++) pos[g] = 0;
                 for (int step = top >> 1; step > 0; step >>= 1) {  // largest c with coff[c] <= i
 #pragma unroll
                     for (int g = 0; g < kG; g++) {
-                        const int i = min(i0 + 256 * g, n - 1);
+                        const int i = min(i0 + NT * g, n - 1);
                         const int q = pos[g] + step;
                         if (q < lv.ncells && coff[q] <= i) pos[g] = q;
                     }
@@ -869,19 +872,19 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 uint32_t kv[kG];
 #pragma unroll
                 for (int g = 0; g < kG; g++) {
-                    const int i = min(i0 + 256 * g, n - 1);
+                    const int i = min(i0 + NT * g, n - 1);
                     kv[g] = ckey[cslot[pos[g]] + (i - coff[pos[g]])];
                 }
 #pragma unroll
                 for (int g = 0; g < kG; g++)
-                    if (i0 + 256 * g < n) K.key[i0 + 256 * g] = kv[g];
+                    if (i0 + NT * g < n) K.key[i0 + NT * g] = kv[g];
             }
         } else {
-            for (int c0 = 0; c0 < lv.ncells; c0 += 256) {
+            for (int c0 = 0; c0 < lv.ncells; c0 += NT) {
                 const int c = c0 + tid;
                 const int v = c < lv.ncells ? ccnt[c] : 0;
                 int tot;
-                const int off = block_scan_excl(v, &tot, red) + carry;
+                const int off = block_scan_excl<NT / 64>(v, &tot, red) + carry;
                 if (c < lv.ncells) {
                     const uint32_t* src = ckey + cells[lv.cell_begin + c].slot;
                     for (int k = 0; k < v; k++) K.key[off + k] = src[k];
@@ -897,9 +900,9 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         }
         // --- 2. roots (ORBextractor.cc:542-585)
         const int nIni = lv.nIni;
-        for (int s = tid; s < nIni; s += 256) cnt4[s] = 0;
+        for (int s = tid; s < nIni; s += NT) cnt4[s] = 0;
         __syncthreads();
-        for (int i = tid; i < n; i += 256) {
+        for (int i = tid; i < n; i += NT) {
             const float x = (float)(K.key[i] & 0xFFF);
             int r = (int)__fdiv_rn(x, lv.hX);
             if (r >= nIni) { atomicOr(err, 1); r = nIni - 1; }
@@ -910,11 +913,11 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         int size = 0;
         {
             int carry2 = 0;
-            for (int r0 = 0; r0 < nIni; r0 += 256) {
+            for (int r0 = 0; r0 < nIni; r0 += NT) {
                 const int r = r0 + tid;
                 const int nonempty = (r < nIni && cnt4[r] > 0) ? 1 : 0;
                 int tot;
-                const int pos = block_scan_excl(nonempty, &tot, red) + carry2;
+                const int pos = block_scan_excl<NT / 64>(nonempty, &tot, red) + carry2;
                 if (nonempty) {
                     spos[r] = pos;
                     A.x0[pos] = (int)__fmul_rn(lv.hX, (float)r);
@@ -929,7 +932,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
             size = carry2;
         }
         __syncthreads();
-        for (int i = tid; i < n; i += 256) K.label[i] = (uint16_t)spos[K.label[i]];
+        for (int i = tid; i < n; i += NT) K.label[i] = (uint16_t)spos[K.label[i]];
         if (size > NC) {  // capacity overflow: flag it and leave this level empty (never a stale count)
             if (tid == 0) { atomicOr(err, 2); lvcnt[f * ep.L + l] = 0; }
             return;
@@ -943,7 +946,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         for (int iter = 0; iter < 100000; iter++) {
             const int prevSize = size;
             if (!cnt_clean) {
-                for (int s = tid; s < size; s += 256) {
+                for (int s = tid; s < size; s += NT) {
                     cnt4[4 * s] = 0; cnt4[4 * s + 1] = 0; cnt4[4 * s + 2] = 0; cnt4[4 * s + 3] = 0;
                 }
                 __syncthreads();
@@ -954,7 +957,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 // in list order, so one packed scan gives the children's creation indices, the survivors'
                 // positions and the number of children with > 1 key at once (4 barriers per round instead of
                 // ~20 for the general path below, which phase 2 and tables of > 256 nodes take).
-                for (int i = tid; i < n; i += 256) {
+                for (int i = tid; i < n; i += NT) {
                     const int s = K.label[i];
                     if (A.nk[s] >= 2) {
                         const uint32_t kk = K.key[i];
@@ -980,7 +983,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 // fields: children (<= 1024, bits 0-10), survivors (<= 256, bits 11-19), children with
                 // > 1 key (<= 1024, bits 20-30)
                 int tot;
-                const int ex = block_scan_excl(nc | (sv << 11) | (ne << 20), &tot, red);
+                const int ex = block_scan_excl<NT / 64>(nc | (sv << 11) | (ne << 20), &tot, red);
                 const int TC = tot & 0x7FF, nsurv = (tot >> 11) & 0x1FF, nToExpand = tot >> 20;
                 const int newSize = TC + nsurv;
                 if (newSize > NC) {
@@ -1013,12 +1016,12 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                     spos[s] = np;
                 }
                 __syncthreads();
-                for (int i = tid; i < n; i += 256) {
+                for (int i = tid; i < n; i += NT) {
                     const int s2 = K.label[i];
                     const int np = spos[s2];
                     K.label[i] = (uint16_t)(np >= 0 ? np : cpos[4 * s2 + K.quad[i]]);
                 }
-                for (int i = tid; i < 4 * newSize; i += 256) cnt4[i] = 0;  // for the next round's count pass
+                for (int i = tid; i < 4 * newSize; i += NT) cnt4[i] = 0;  // for the next round's count pass
                 __syncthreads();
                 cnt_clean = true;
                 { NodeT t = A; A = Bt; Bt = t; }
@@ -1028,7 +1031,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 if (size + nToExpand * 3 > N) phase = 2;
                 continue;
             }
-            for (int i = tid; i < n; i += 256) {
+            for (int i = tid; i < n; i += NT) {
                 const int s = K.label[i];
                 if (A.nk[s] >= 2) {
                     const uint32_t kk = K.key[i];
@@ -1044,11 +1047,11 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
             int nD;
             {
                 int carry3 = 0;
-                for (int s0 = 0; s0 < size; s0 += 256) {
+                for (int s0 = 0; s0 < size; s0 += NT) {
                     const int s = s0 + tid;
                     const int isD = (s < size && A.nk[s] >= 2) ? 1 : 0;
                     int tot;
-                    const int pos = block_scan_excl(isD, &tot, red) + carry3;
+                    const int pos = block_scan_excl<NT / 64>(isD, &tot, red) + carry3;
                     if (isD) {
                         dflag[pos] = s;  // D array (slot ids) in list order
                         skey[pos] = ((unsigned long long)(uint32_t)A.nk[s] << 32) | A.seq[s];
@@ -1063,14 +1066,14 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 // processing order = descending (size, creation) key; keys are unique (seq), so a node's
                 // rank is the number of larger keys: nD broadcast LDS reads per node and two barriers
                 // instead of a bitonic network's log2(P)(log2(P)+1)/2 barriers
-                for (int j = tid; j < nD; j += 256) {
+                for (int j = tid; j < nD; j += NT) {
                     const unsigned long long key = skey[j];
                     int rank = 0;
                     for (int i = 0; i < nD; i++) rank += skey[i] > key ? 1 : 0;
                     dbase[rank] = dflag[j];
                 }
                 __syncthreads();
-                for (int j = tid; j < nD; j += 256) dflag[j] = dbase[j];
+                for (int j = tid; j < nD; j += NT) dflag[j] = dbase[j];
                 __syncthreads();
             }
             // children counts per processing position; prefix -> creation indices
@@ -1079,7 +1082,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 int carry4 = 0, carryG = 0;
                 if (tid == 0) sh_jstar = nD - 1;
                 __syncthreads();
-                for (int j0 = 0; j0 < nD; j0 += 256) {
+                for (int j0 = 0; j0 < nD; j0 += NT) {
                     const int j = j0 + tid;
                     int nc = 0;
                     if (j < nD) {
@@ -1087,9 +1090,9 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                         nc = (cnt4[4 * s] > 0) + (cnt4[4 * s + 1] > 0) + (cnt4[4 * s + 2] > 0) + (cnt4[4 * s + 3] > 0);
                     }
                     int tot;
-                    const int excl = block_scan_excl(nc, &tot, red) + carry4;
+                    const int excl = block_scan_excl<NT / 64>(nc, &tot, red) + carry4;
                     int tot2;
-                    const int excl2 = block_scan_excl(nc - 1, &tot2, red) + carryG;
+                    const int excl2 = block_scan_excl<NT / 64>(nc - 1, &tot2, red) + carryG;
                     if (j < nD) {
                         dbase[j] = excl;
                         if (phase == 2) {
@@ -1107,18 +1110,18 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
             }
             const int ndiv = jstar + 1;
             // survivors = live slots not divided, in list order
-            for (int s = tid; s < size; s += 256) spos[s] = 0;
+            for (int s = tid; s < size; s += NT) spos[s] = 0;
             __syncthreads();
-            for (int j = tid; j < ndiv; j += 256) spos[dflag[j]] = -1;  // mark divided
+            for (int j = tid; j < ndiv; j += NT) spos[dflag[j]] = -1;  // mark divided
             __syncthreads();
             int nsurv;
             {
                 int carry5 = 0;
-                for (int s0 = 0; s0 < size; s0 += 256) {
+                for (int s0 = 0; s0 < size; s0 += NT) {
                     const int s = s0 + tid;
                     const int sv = (s < size && spos[s] == 0) ? 1 : 0;
                     int tot;
-                    const int pos = block_scan_excl(sv, &tot, red) + carry5;
+                    const int pos = block_scan_excl<NT / 64>(sv, &tot, red) + carry5;
                     __syncthreads();
                     if (s < size) spos[s] = sv ? (TC + pos) : -1;
                     carry5 += tot;
@@ -1132,7 +1135,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 return;
             }
             // write new table: survivors copy, children created
-            for (int s = tid; s < size; s += 256) {
+            for (int s = tid; s < size; s += NT) {
                 const int np = spos[s];
                 if (np >= 0) {
                     Bt.x0[np] = A.x0[s]; Bt.y0[np] = A.y0[s]; Bt.x1[np] = A.x1[s]; Bt.y1[np] = A.y1[s];
@@ -1140,7 +1143,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                 }
             }
             int nexp_local = 0;
-            for (int j = tid; j < ndiv; j += 256) {
+            for (int j = tid; j < ndiv; j += NT) {
                 const int s = dflag[j];
                 const int x0 = A.x0[s], y0 = A.y0[s], x1 = A.x1[s], y1 = A.y1[s];
                 const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;
@@ -1160,9 +1163,9 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
                     }
                 }
             }
-            const int nToExpand = block_sum(nexp_local, red);
+            const int nToExpand = block_sum<NT / 64>(nexp_local, red);
             // relabel keys
-            for (int i = tid; i < n; i += 256) {
+            for (int i = tid; i < n; i += NT) {
                 const int s = K.label[i];
                 const int np = spos[s];
                 K.label[i] = (uint16_t)(np >= 0 ? np : cpos[4 * s + K.quad[i]]);
@@ -1177,15 +1180,15 @@ __global__ __launch_bounds__(256) void k_octree(ExtractParams ep, const LevelDes
         }
         // --- 4. keep the best key of each node (first max response, ORBextractor.cc:741-760)
         uint32_t* best = (uint32_t*)cnt4;
-        for (int s = tid; s < size; s += 256) best[s] = 0u;
+        for (int s = tid; s < size; s += NT) best[s] = 0u;
         __syncthreads();
-        for (int i = tid; i < n; i += 256) {
+        for (int i = tid; i < n; i += NT) {
             const uint32_t kk = K.key[i];
             atomicMax(&best[K.label[i]], (kk & 0xFF000000u) | (0xFFFFFFu - (uint32_t)i));
         }
         __syncthreads();
         if (size > lv.kp_cap) { if (tid == 0) atomicOr(err, 8); size = lv.kp_cap; }
-        for (int s = tid; s < size; s += 256) {
+        for (int s = tid; s < size; s += NT) {
             const int i = (int)(0xFFFFFFu - (best[s] & 0xFFFFFFu));
             const uint32_t kk = K.key[i];
             const uint32_t x = (kk & 0xFFF) + (uint32_t)lv.minX, y = ((kk >> 12) & 0xFFF) + (uint32_t)lv.minY;
@@ -1592,7 +1595,10 @@ hipError_t launch_sincos_selftest(const float* in, float* so, float* co, int n, 
 }
 
 hipError_t octree_setup(int lds_bytes) {
-    return hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    const hipError_t e = hipFuncSetAttribute((const void*)k_octree<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             lds_bytes);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)k_octree<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
 hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
@@ -1602,8 +1608,14 @@ hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const
     if (nlevels < 0) nlevels = ep.L - level0;
     if (level0 < 0 || nlevels < 1 || level0 + nlevels > ep.L) return hipErrorInvalidValue;
     dim3 grid(nlevels, nframes);
-    hipLaunchKernelGGL(k_octree, grid, dim3(256), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey, lvcnt,
-                       gscratch, gscratch_frame_bytes, NC, KL, level0, err);
+    // a small batch (one frame per Tracking call) has a workgroup per level and nothing beside it: 16 waves walk
+    // each round's keys in a quarter of the iterations; batches pack four 256-thread workgroups per CU instead
+    if (nframes < kPyrFramesMinBatch)
+        hipLaunchKernelGGL(k_octree<1024>, grid, dim3(1024), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey,
+                           lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err);
+    else
+        hipLaunchKernelGGL(k_octree<256>, grid, dim3(256), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey,
+                           lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err);
     return hipGetLastError();
 }
 
