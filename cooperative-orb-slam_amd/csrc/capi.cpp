@@ -387,9 +387,9 @@ struct orbx_handle {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
     hipEvent_t ev_pyr = nullptr, ev_blur = nullptr;
-    // the level-0 branch of small batches (run_extract_levels) uses entry 0: a stream, fork / join events
-    hipStream_t lst[kMaxLevels] = {};
-    hipEvent_t lfork[kMaxLevels] = {}, ljoin[kMaxLevels] = {};
+    // the level-0 branch of small batches (run_extract_levels): its stream, fork and join events
+    hipStream_t l0_stream = nullptr;
+    hipEvent_t ev_l0_fork = nullptr, ev_l0_join = nullptr;
     hipEvent_t user_ev_pyr = nullptr;  // orbx_set_pyramid_event (caller-owned)
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
@@ -539,9 +539,9 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
                               int kp_stride, hipStream_t st, int* errp) {
     Geometry& g = h->geo;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
-    if (!h->lst[0]) HIPR(hipStreamCreateWithFlags(&h->lst[0], hipStreamNonBlocking));
-    if (!h->lfork[0]) HIPR(hipEventCreateWithFlags(&h->lfork[0], hipEventDisableTiming));
-    if (!h->ljoin[0]) HIPR(hipEventCreateWithFlags(&h->ljoin[0], hipEventDisableTiming));
+    if (!h->l0_stream) HIPR(hipStreamCreateWithFlags(&h->l0_stream, hipStreamNonBlocking));
+    if (!h->ev_l0_fork) HIPR(hipEventCreateWithFlags(&h->ev_l0_fork, hipEventDisableTiming));
+    if (!h->ev_l0_join) HIPR(hipEventCreateWithFlags(&h->ev_l0_join, hipEventDisableTiming));
     auto octree = [&](int l0, int nl, hipStream_t s2) -> int {
         if (!(h->skip_mask & 4))
             HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
@@ -550,12 +550,12 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
         return 0;
     };
     const int nc0 = g.lv[0].ncells;
-    hipStream_t l0s = h->lst[0];
-    HIPR(hipEventRecord(h->lfork[0], st));
-    HIPR(hipStreamWaitEvent(l0s, h->lfork[0], 0));
+    hipStream_t l0s = h->l0_stream;
+    HIPR(hipEventRecord(h->ev_l0_fork, st));
+    HIPR(hipStreamWaitEvent(l0s, h->ev_l0_fork, 0));
     if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, nc0, nframes, l0s)) return ORBX_EDEVICE;
     if (octree(0, 1, l0s)) return ORBX_EDEVICE;
-    HIPR(hipEventRecord(h->ljoin[0], l0s));
+    HIPR(hipEventRecord(h->ev_l0_join, l0s));
     if (!(h->skip_mask & 1) && launch_pyramid(h, ep, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
     HIPR(hipEventRecord(h->ev_pyr, st));
     HIPR(hipStreamWaitEvent(h->side, h->ev_pyr, 0));
@@ -568,7 +568,7 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
             return ORBX_EDEVICE;
         if (octree(1, ep.L - 1, st)) return ORBX_EDEVICE;
     }
-    HIPR(hipStreamWaitEvent(st, h->ljoin[0], 0));
+    HIPR(hipStreamWaitEvent(st, h->ev_l0_join, 0));
     HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     if (!(h->skip_mask & 16))
         HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
@@ -691,8 +691,7 @@ void orbx_destroy(orbx_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->side) (void)hipStreamSynchronize(h->side);
-    for (hipStream_t ls : h->lst)
-        if (ls) (void)hipStreamSynchronize(ls);
+    if (h->l0_stream) (void)hipStreamSynchronize(h->l0_stream);
     for (DevBuf* b : {&h->pyr, &h->blur, &h->cellkey, &h->cellcnt, &h->lvkey, &h->lvcnt, &h->gscratch, &h->err,
                       &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt, &h->st_buf})
         b->release();
@@ -701,11 +700,9 @@ void orbx_destroy(orbx_handle* h) {
     if (h->side) (void)hipStreamDestroy(h->side);
     for (hipEvent_t e : {h->ev_pyr, h->ev_blur})
         if (e) (void)hipEventDestroy(e);
-    for (int l = 0; l < kMaxLevels; l++) {
-        if (h->lst[l]) (void)hipStreamDestroy(h->lst[l]);
-        if (h->lfork[l]) (void)hipEventDestroy(h->lfork[l]);
-        if (h->ljoin[l]) (void)hipEventDestroy(h->ljoin[l]);
-    }
+    if (h->l0_stream) (void)hipStreamDestroy(h->l0_stream);
+    for (hipEvent_t e : {h->ev_l0_fork, h->ev_l0_join})
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
     if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
     if (h->graph) (void)hipGraphDestroy(h->graph);
