@@ -525,15 +525,18 @@ static int launch_fast(orbx_handle* h, const ExtractParams& ep, const uint8_t* d
  * erases an unread batch error. */
 constexpr int kErrWordSticky = 0, kErrWordCall = 1, kErrWordExtract = 2, kErrWordTake = 32, kErrWordExtractTake = 33;
 /* Small batches (the Tracking thread's one frame per call, ORBextractor.cc:1043-1105): the pyramid is a chain of
- * per-level launches and level 0 needs none of it, so level 0's FAST and octree (the longest octree: ~1,240 keys
- * at 640x480) run on a side branch from the start, beside the chain:
+ * per-level launches, and the two largest levels' FAST + octree (level 0 needs no resize, level 1 one) run on a
+ * side branch beside the rest of the chain:
  *
- *   st  : resize 1 .. L-1 -> [ev_pyr] FAST(levels 1..L-1) -> octree(1..L-1) -> [ev_blur, join 0] describe
- *   lst0: FAST(level 0) -> octree(0) -> [join 0]
- *   side:                    [ev_pyr] blur(all levels) -> [ev_blur]
+ *   st  : resize 1 -> [fork] resize 2 .. L-1 -> [ev_pyr] FAST(levels 2..) -> octree(2..) -> [ev_blur, join] describe
+ *   l0  :             [fork] FAST(levels 0, 1) -> octree(0, 1) -> [join]
+ *   side:                                         [ev_pyr] blur(all levels) -> [ev_blur]
  *
- * (A branch per level, each with its own FAST, octree and blur, measured 2x slower: 4 hardware queues serialise
- * the branches and every level's blur launch costs a strip's ~23 us chain; profiles/r04_latency_branches.log.) */
+ * The fork comes after resize 1 on purpose: the graph executor turns an edge between queues into a marker
+ * behind everything already submitted to the source queue, so a branch forked before the chain's first launch
+ * delayed the whole chain until it had finished (profiles/r04_latency_branches.log). (A branch per level, each
+ * with its own FAST, octree and blur, measured 2x slower: 4 hardware queues serialise the branches and every
+ * level's blur launch costs a strip's ~23 us chain.) */
 static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nframes, const uint8_t* d_frames,
                               long long fstride, int pitch, orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
                               int kp_stride, hipStream_t st, int* errp) {
@@ -542,32 +545,50 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
     if (!h->l0_stream) HIPR(hipStreamCreateWithFlags(&h->l0_stream, hipStreamNonBlocking));
     if (!h->ev_l0_fork) HIPR(hipEventCreateWithFlags(&h->ev_l0_fork, hipEventDisableTiming));
     if (!h->ev_l0_join) HIPR(hipEventCreateWithFlags(&h->ev_l0_join, hipEventDisableTiming));
-    auto octree = [&](int l0, int nl, hipStream_t s2) -> int {
+    auto resize = [&](int l) -> int {
+        if (h->skip_mask & 1) return 0;
+        const LevelDesc& s = g.lv[l - 1];
+        const LevelDesc& d = g.lv[l];
+        const uint8_t* src = l == 1 ? d_frames : h->pyr.as<uint8_t>() + s.pyr_off;
+        const long long sfs = l == 1 ? fstride : ep.pyr_frame_bytes;
+        const int sp = l == 1 ? pitch : s.pitch;
+        if (g.tiled_ok[l])
+            HIPR(launch_resize_tiled(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes,
+                                     d.pitch, d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes,
+                                     st));
+        else
+            HIPR(launch_resize(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes, d.pitch,
+                               d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, st));
+        return 0;
+    };
+    // levels [0, k) on the branch, [k, L) on the chain
+    auto fast_octree = [&](int l0, int l1, hipStream_t s2) -> int {
+        if (l1 <= l0) return 0;
+        const int c0 = g.lv[l0].cell_begin, c1 = l1 < ep.L ? g.lv[l1].cell_begin : ep.ncells;
+        if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, c0, c1, nframes, s2)) return ORBX_EDEVICE;
         if (!(h->skip_mask & 4))
             HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                                h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
-                               (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, s2, l0, nl));
+                               (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, s2, l0,
+                               l1 - l0));
         return 0;
     };
-    const int nc0 = g.lv[0].ncells;
-    hipStream_t l0s = h->l0_stream;
+    const int k = std::min(2, ep.L);
+    for (int l = 1; l < k; l++)
+        if (resize(l)) return ORBX_EDEVICE;
     HIPR(hipEventRecord(h->ev_l0_fork, st));
-    HIPR(hipStreamWaitEvent(l0s, h->ev_l0_fork, 0));
-    if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, nc0, nframes, l0s)) return ORBX_EDEVICE;
-    if (octree(0, 1, l0s)) return ORBX_EDEVICE;
-    HIPR(hipEventRecord(h->ev_l0_join, l0s));
-    if (!(h->skip_mask & 1) && launch_pyramid(h, ep, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
+    HIPR(hipStreamWaitEvent(h->l0_stream, h->ev_l0_fork, 0));
+    if (fast_octree(0, k, h->l0_stream)) return ORBX_EDEVICE;
+    HIPR(hipEventRecord(h->ev_l0_join, h->l0_stream));
+    for (int l = k; l < ep.L; l++)
+        if (resize(l)) return ORBX_EDEVICE;
     HIPR(hipEventRecord(h->ev_pyr, st));
     HIPR(hipStreamWaitEvent(h->side, h->ev_pyr, 0));
     if (!(h->skip_mask & 8))
         HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl, 0, g.nbjobs,
                                 nullptr, nframes, h->side));
     HIPR(hipEventRecord(h->ev_blur, h->side));
-    if (ep.L > 1) {
-        if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, nc0, ep.ncells, nframes, st))
-            return ORBX_EDEVICE;
-        if (octree(1, ep.L - 1, st)) return ORBX_EDEVICE;
-    }
+    if (fast_octree(k, ep.L, st)) return ORBX_EDEVICE;
     HIPR(hipStreamWaitEvent(st, h->ev_l0_join, 0));
     HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     if (!(h->skip_mask & 16))
