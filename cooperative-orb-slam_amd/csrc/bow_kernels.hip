@@ -8,7 +8,8 @@
  *                  scored with the 256-bit Hamming distance (FORB::distance), the group minimum of
  *                  (dist, child position) is DBoW2's first strict minimum; the descent stops at a
  *                  node without children (Node::isLeaf) and records the word id, its weight and
- *                  the node at level L - levelsup (the FeatureVector key).
+ *                  the node at level L - levelsup (the FeatureVector key). The children's descriptors
+ *                  and records sit in child-slot order, so a level is one round of independent loads.
  *   k_voc_bow      one workgroup per frame: stable LDS bitonic sorts of (node, feature) and (word,
  *                  feature) keys build FeatureVector::addFeature's map (ascending node id, ascending
  *                  feature per node) and BowVector's map; a word's weights are added in feature
@@ -28,7 +29,7 @@ __global__ __launch_bounds__(256) void k_voc_descend(VocDev v, int levelsup, con
                                                      int32_t* __restrict__ word, double* __restrict__ weight,
                                                      uint32_t* __restrict__ nid_out) {
     const int f = blockIdx.y;
-    const int i = blockIdx.x * 16 + (threadIdx.x >> 4), gl = threadIdx.x & 15;
+    const int i = blockIdx.x * 16 + (threadIdx.x >> 4), gl = threadIdx.x & 15, gbase = threadIdx.x & ~15;
     const int n = counts[f];
     if (blockIdx.x * 16 >= n) return;  // block-uniform
     const bool in = i < n;
@@ -37,38 +38,51 @@ __global__ __launch_bounds__(256) void k_voc_descend(VocDev v, int levelsup, con
     const uint4 q0 = q[0], q1 = q[1];
     const int nid_level = v.L - levelsup;
     uint32_t nid = 0;  // root (also what a branch shallower than nid_level reports)
-    int final_id = 0, level = 0;
-    for (int step = 0; step < v.n; step++) {  // node ids strictly increase along a path
-        const int c0 = v.child_off[final_id], nc = v.child_off[final_id + 1] - c0;
-        if (nc == 0) break;  // Node::isLeaf
+    int final_id = 0, w_id = 0, level = 0;
+    double w = 0.0;
+    int c0 = v.root_c0, nc = v.root_nc;
+    for (int step = 0; step < v.n && nc > 0; step++) {  // nc == 0: Node::isLeaf; node ids strictly increase
         ++level;
         uint32_t best = 0xffffffffu;
+        VocChild br{};
         for (int j = gl; j < nc; j += 16) {
-            const int id = v.child[c0 + j];
-            const uint4* d = (const uint4*)(v.desc + (long long)id * 32);
+            const uint4* d = (const uint4*)(v.cdesc + (long long)(c0 + j) * 32);
             const uint4 d0 = d[0], d1 = d[1];
+            const VocChild r = v.crec[c0 + j];
             const int dist = __popc(q0.x ^ d0.x) + __popc(q0.y ^ d0.y) + __popc(q0.z ^ d0.z) + __popc(q0.w ^ d0.w) +
                              __popc(q1.x ^ d1.x) + __popc(q1.y ^ d1.y) + __popc(q1.z ^ d1.z) + __popc(q1.w ^ d1.w);
-            best = min(best, ((uint32_t)dist << 16) | (uint32_t)j);
+            const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)j;  // first strict minimum: lowest j on ties
+            if (key < best) {
+                best = key;
+                br = r;
+            }
         }
 #pragma unroll
         for (int o = 8; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o));
-        final_id = v.child[c0 + (int)(best & 0xffff)];
+        const int src = gbase + (int)(best & 15u);  // child j was scored by lane j mod 16
+        final_id = __shfl(br.id, src);
+        c0 = __shfl(br.c0, src);
+        nc = __shfl(br.nc, src);
+        w_id = __shfl(br.word, src);
+        w = __shfl(br.weight, src);
         if (level == nid_level) nid = (uint32_t)final_id;
     }
     if (in && gl == 0) {
-        word[fi] = v.word_id[final_id];
-        weight[fi] = v.weight[final_id];
+        word[fi] = w_id;
+        weight[fi] = w;
         nid_out[fi] = nid;
     }
 }
 
-/* ascending bitonic sort of n2 (power of two) u64 keys in LDS by 256 threads */
+constexpr int kVocThreads = 1024;  // k_voc_bow: one compare-exchange per thread per bitonic stage at 2048 keys
+constexpr int kVocWaves = kVocThreads / 64;
+
+/* ascending bitonic sort of n2 (power of two) u64 keys in LDS by kVocThreads threads */
 __device__ void lds_bitonic_u64(unsigned long long* a, int n2) {
     for (int size = 2; size <= n2; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
             __syncthreads();
-            for (int t = threadIdx.x; t < n2 / 2; t += 256) {
+            for (int t = threadIdx.x; t < n2 / 2; t += kVocThreads) {
                 const int lo = 2 * t - (t & (stride - 1));
                 const int hi = lo + stride;
                 const bool up = (lo & size) == 0;
@@ -88,7 +102,7 @@ __device__ void lds_bitonic_u64(unsigned long long* a, int n2) {
 __device__ int lds_segments(const unsigned long long* a, int n, int* s_start, int* s_tmp) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int carry = 0;
-    for (int base = 0; base < n; base += 256) {
+    for (int base = 0; base < n; base += kVocThreads) {
         const int i = base + tid;
         const int head = i < n && (i == 0 || (a[i] >> 32) != (a[i - 1] >> 32));
         int incl = head;
@@ -101,7 +115,9 @@ __device__ int lds_segments(const unsigned long long* a, int n, int* s_start, in
         __syncthreads();
         int off = carry;
         for (int w = 0; w < wv; w++) off += s_tmp[w];
-        const int tot = s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
+        int tot = 0;
+#pragma unroll
+        for (int w = 0; w < kVocWaves; w++) tot += s_tmp[w];
         if (i < n && head) s_start[off + incl - 1] = i;
         carry += tot;
         __syncthreads();
@@ -109,7 +125,7 @@ __device__ int lds_segments(const unsigned long long* a, int n, int* s_start, in
     return carry;
 }
 
-__global__ __launch_bounds__(256) void k_voc_bow(VocDev v, const int32_t* __restrict__ counts, int stride,
+__global__ __launch_bounds__(kVocThreads) void k_voc_bow(VocDev v, const int32_t* __restrict__ counts, int stride,
                                                  const int32_t* __restrict__ word, const double* __restrict__ weight,
                                                  const uint32_t* __restrict__ nid, uint32_t* __restrict__ bow_word,
                                                  double* __restrict__ bow_value, int32_t* __restrict__ nbow,
@@ -117,7 +133,7 @@ __global__ __launch_bounds__(256) void k_voc_bow(VocDev v, const int32_t* __rest
                                                  int32_t* __restrict__ fv_feat, int32_t* __restrict__ nfv) {
     __shared__ unsigned long long s_key[kVocMaxFeatures];
     __shared__ int s_start[kVocMaxFeatures + 1];
-    __shared__ int s_tmp[8];
+    __shared__ int s_tmp[2 * kVocWaves];
     __shared__ double s_norm;
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = counts[f];
@@ -125,19 +141,21 @@ __global__ __launch_bounds__(256) void k_voc_bow(VocDev v, const int32_t* __rest
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
     // ---- FeatureVector: stable by (node id, feature index); stopped features (weight <= 0) sort last
-    for (int i = tid; i < n2; i += 256)
+    for (int i = tid; i < n2; i += kVocThreads)
         s_key[i] = i < n && weight[fb + i] > 0 ? ((unsigned long long)nid[fb + i] << 32) | (unsigned)i : ~0ull;
     lds_bitonic_u64(s_key, n2);
     int kept = 0;
-    for (int i = tid; i < n; i += 256) kept += s_key[i] != ~0ull;
+    for (int i = tid; i < n; i += kVocThreads) kept += s_key[i] != ~0ull;
     for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
-    if ((tid & 63) == 0) s_tmp[4 + (tid >> 6)] = kept;
+    if ((tid & 63) == 0) s_tmp[kVocWaves + (tid >> 6)] = kept;
     __syncthreads();
-    const int m = s_tmp[4] + s_tmp[5] + s_tmp[6] + s_tmp[7];
+    int m = 0;
+#pragma unroll
+    for (int w = 0; w < kVocWaves; w++) m += s_tmp[kVocWaves + w];
     __syncthreads();
     const int nseg = lds_segments(s_key, m, s_start, s_tmp);
-    for (int i = tid; i < m; i += 256) fv_feat[fb + i] = (int32_t)(s_key[i] & 0xffffffffu);
-    for (int s = tid; s < nseg; s += 256) {
+    for (int i = tid; i < m; i += kVocThreads) fv_feat[fb + i] = (int32_t)(s_key[i] & 0xffffffffu);
+    for (int s = tid; s < nseg; s += kVocThreads) {
         fv_node[fb + s] = (uint32_t)(s_key[s_start[s]] >> 32);
         fv_off[(long long)f * (stride + 1) + s] = s_start[s];
     }
@@ -147,7 +165,7 @@ __global__ __launch_bounds__(256) void k_voc_bow(VocDev v, const int32_t* __rest
     }
     __syncthreads();
     // ---- BowVector: stable by (word id, feature index)
-    for (int i = tid; i < n2; i += 256)
+    for (int i = tid; i < n2; i += kVocThreads)
         s_key[i] = i < n && weight[fb + i] > 0 ? ((unsigned long long)(uint32_t)word[fb + i] << 32) | (unsigned)i : ~0ull;
     lds_bitonic_u64(s_key, n2);
     const int nw = lds_segments(s_key, m, s_start, s_tmp);
@@ -155,7 +173,7 @@ __global__ __launch_bounds__(256) void k_voc_bow(VocDev v, const int32_t* __rest
     __syncthreads();
     const bool add = v.weighting == 0 || v.weighting == 1;  // TF_IDF / TF: addWeight; IDF / BINARY: addIfNotExist
     const bool must = v.scoring != 5;                       // every scoring but DOT_PRODUCT normalises
-    for (int s = tid; s < nw; s += 256) {
+    for (int s = tid; s < nw; s += kVocThreads) {
         const int b = s_start[s], e = s_start[s + 1];
         double val = weight[fb + (int)(s_key[b] & 0xffffffffu)];
         if (add)
@@ -167,20 +185,30 @@ __global__ __launch_bounds__(256) void k_voc_bow(VocDev v, const int32_t* __rest
     __threadfence_block();
     __syncthreads();
     if (must) {
-        if (tid == 0) {  // BowVector::normalize: sum in ascending word order, as the map iteration
+        if (tid < 64) {  // BowVector::normalize: sum in ascending word order, as the map iteration. Wave 0 loads
+                         // 64 words per coalesced read and lane-broadcasts them into one in-order f64 chain
+                         // (uncontracted, as the oracle's -ffp-contract=off build) -- not one load per add
+            const bool l2 = v.scoring == 1;
             double norm = 0.0;
-            if (v.scoring == 1) {
-                for (int s = 0; s < nw; s++) norm += bow_value[fb + s] * bow_value[fb + s];
-                norm = sqrt(norm);
-            } else {
-                for (int s = 0; s < nw; s++) norm += fabs(bow_value[fb + s]);
+            for (int base = 0; base < nw; base += 64) {
+                const int s = base + tid;
+                const double x = s < nw ? bow_value[fb + s] : 0.0;
+                const double t = l2 ? __dmul_rn(x, x) : fabs(x);
+                const int cnt = min(64, nw - base);
+                const unsigned long long tb = (unsigned long long)__double_as_longlong(t);
+                const int lo = (int)(uint32_t)tb, hi = (int)(uint32_t)(tb >> 32);
+                for (int j = 0; j < cnt; j++) {
+                    const unsigned long long u = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(hi, j) << 32) |
+                                                 (uint32_t)__builtin_amdgcn_readlane(lo, j);
+                    norm = __dadd_rn(norm, __longlong_as_double((long long)u));
+                }
             }
-            s_norm = norm;
+            if (tid == 0) s_norm = l2 ? sqrt(norm) : norm;
         }
         __syncthreads();
         const double norm = s_norm;
         if (norm > 0.0)
-            for (int s = tid; s < nw; s += 256) bow_value[fb + s] = bow_value[fb + s] / norm;
+            for (int s = tid; s < nw; s += kVocThreads) bow_value[fb + s] = bow_value[fb + s] / norm;
     }
     if (tid == 0) nbow[f] = nw;
 }
@@ -193,7 +221,7 @@ hipError_t launch_voc_transform(const VocDev& v, int levelsup, int nframes, cons
     if (max_n > 0)
         hipLaunchKernelGGL(k_voc_descend, dim3((max_n + 15) / 16, nframes), dim3(256), 0, st, v, levelsup, desc, counts,
                            stride, word, weight, nid);
-    hipLaunchKernelGGL(k_voc_bow, dim3(nframes), dim3(256), 0, st, v, counts, stride, word, weight, nid, bow_word,
+    hipLaunchKernelGGL(k_voc_bow, dim3(nframes), dim3(kVocThreads), 0, st, v, counts, stride, word, weight, nid, bow_word,
                        bow_value, nbow, fv_node, fv_off, fv_feat, nfv);
     return hipGetLastError();
 }

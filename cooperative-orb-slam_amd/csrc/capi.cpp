@@ -387,9 +387,9 @@ struct orbx_handle {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
     hipEvent_t ev_pyr = nullptr, ev_blur = nullptr;
-    // the level-0 branch of small batches (run_extract_levels): its stream, fork and join events
+    // small batches (run_extract_levels): the pyramid + blur list's stream and its fork event
     hipStream_t l0_stream = nullptr;
-    hipEvent_t ev_l0_fork = nullptr, ev_l0_join = nullptr;
+    hipEvent_t ev_l0_fork = nullptr;
     hipEvent_t user_ev_pyr = nullptr;  // orbx_set_pyramid_event (caller-owned)
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
@@ -524,19 +524,21 @@ static int launch_fast(orbx_handle* h, const ExtractParams& ep, const uint8_t* d
  * next call; kErrCall (word 1) is the stereo host call's (zeroed and read by that call). A host call never
  * erases an unread batch error. */
 constexpr int kErrWordSticky = 0, kErrWordCall = 1, kErrWordExtract = 2, kErrWordTake = 32, kErrWordExtractTake = 33;
+constexpr int kErrWordExtractSeq = 40;  // the host extraction's call counter (k_call_done's done word)
 /* Small batches (the Tracking thread's one frame per call, ORBextractor.cc:1043-1105): the pyramid is a chain of
- * per-level launches, and the two largest levels' FAST + octree (level 0 needs no resize, level 1 one) run on a
- * side branch beside the rest of the chain:
+ * per-level launches. The graph executor maps a captured graph to queues by a depth-first walk: a node's first
+ * captured child continues its parent's queue, every other child starts a new list on another queue, and an edge
+ * between lists is a marker behind everything already submitted to the source queue; streams share the
+ * process's 4 hardware queues, so a third list may land behind another on one queue. Two lists, then:
  *
- *   st  : resize 1 -> [fork] resize 2 .. L-1 -> [ev_pyr] FAST(levels 2..) -> octree(2..) -> [ev_blur, join] describe
- *   l0  :             [fork] FAST(levels 0, 1) -> octree(0, 1) -> [join]
- *   side:                                         [ev_pyr] blur(all levels) -> [ev_blur]
+ *   st  : resize 1 -> FAST(levels 0, 1) -> octree(0, 1) -> [ev_pyr] FAST(2..) -> octree(2..) -> [ev_blur] describe
+ *   l0  :    [fork] resize 2 .. L-1 -> [ev_pyr] blur(all levels) -> [ev_blur]
  *
- * The fork comes after resize 1 on purpose: the graph executor turns an edge between queues into a marker
- * behind everything already submitted to the source queue, so a branch forked before the chain's first launch
- * delayed the whole chain until it had finished (profiles/r04_latency_branches.log). (A branch per level, each
- * with its own FAST, octree and blur, measured 2x slower: 4 hardware queues serialise the branches and every
- * level's blur launch costs a strip's ~23 us chain.) */
+ * Levels 0 and 1 need no more of the pyramid than resize 1, so their FAST and octree (level 0's is the longest
+ * single workgroup) run while the other queue builds the rest of the pyramid and then blurs it; FAST and octree
+ * of levels 2.. follow once the pyramid is complete. (A branch per level measured 2x slower, and so did a single
+ * launch for levels 2.. whose tiles wait on each other's counters: each level hand-off is an agent-scope
+ * release / acquire pair across XCDs, profiles/r04_latency_branches.log, r04i_branch_ab.log.) */
 static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nframes, const uint8_t* d_frames,
                               long long fstride, int pitch, orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
                               int kp_stride, hipStream_t st, int* errp) {
@@ -544,8 +546,7 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
     if (!h->l0_stream) HIPR(hipStreamCreateWithFlags(&h->l0_stream, hipStreamNonBlocking));
     if (!h->ev_l0_fork) HIPR(hipEventCreateWithFlags(&h->ev_l0_fork, hipEventDisableTiming));
-    if (!h->ev_l0_join) HIPR(hipEventCreateWithFlags(&h->ev_l0_join, hipEventDisableTiming));
-    auto resize = [&](int l) -> int {
+    auto resize = [&](int l, hipStream_t s2) -> int {
         if (h->skip_mask & 1) return 0;
         const LevelDesc& s = g.lv[l - 1];
         const LevelDesc& d = g.lv[l];
@@ -555,13 +556,13 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
         if (g.tiled_ok[l])
             HIPR(launch_resize_tiled(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes,
                                      d.pitch, d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes,
-                                     st));
+                                     s2));
         else
             HIPR(launch_resize(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes, d.pitch,
-                               d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, st));
+                               d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, s2));
         return 0;
     };
-    // levels [0, k) on the branch, [k, L) on the chain
+    // FAST + octree of levels [l0, l1) on stream s2
     auto fast_octree = [&](int l0, int l1, hipStream_t s2) -> int {
         if (l1 <= l0) return 0;
         const int c0 = g.lv[l0].cell_begin, c1 = l1 < ep.L ? g.lv[l1].cell_begin : ep.ncells;
@@ -575,21 +576,19 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
     };
     const int k = std::min(2, ep.L);
     for (int l = 1; l < k; l++)
-        if (resize(l)) return ORBX_EDEVICE;
+        if (resize(l, st)) return ORBX_EDEVICE;
     HIPR(hipEventRecord(h->ev_l0_fork, st));
+    if (fast_octree(0, k, st)) return ORBX_EDEVICE;  // captured first: resize 1's queue continues with it
     HIPR(hipStreamWaitEvent(h->l0_stream, h->ev_l0_fork, 0));
-    if (fast_octree(0, k, h->l0_stream)) return ORBX_EDEVICE;
-    HIPR(hipEventRecord(h->ev_l0_join, h->l0_stream));
     for (int l = k; l < ep.L; l++)
-        if (resize(l)) return ORBX_EDEVICE;
-    HIPR(hipEventRecord(h->ev_pyr, st));
-    HIPR(hipStreamWaitEvent(h->side, h->ev_pyr, 0));
+        if (resize(l, h->l0_stream)) return ORBX_EDEVICE;
+    HIPR(hipEventRecord(h->ev_pyr, h->l0_stream));
     if (!(h->skip_mask & 8))
         HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl, 0, g.nbjobs,
-                                nullptr, nframes, h->side));
-    HIPR(hipEventRecord(h->ev_blur, h->side));
+                                nullptr, nframes, h->l0_stream));
+    HIPR(hipEventRecord(h->ev_blur, h->l0_stream));
+    HIPR(hipStreamWaitEvent(st, h->ev_pyr, 0));
     if (fast_octree(k, ep.L, st)) return ORBX_EDEVICE;
-    HIPR(hipStreamWaitEvent(st, h->ev_l0_join, 0));
     HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     if (!(h->skip_mask & 16))
         HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
@@ -600,7 +599,7 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
 
 static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
                        orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st,
-                       bool host_call = true) {
+                       bool host_call = true, bool mapped_out = false) {
     Geometry& g = h->geo;
     // the L2-residency bound (orbx_debug_alias_frames): every frame of the batch reads frame 0's image and
     // shares one pyramid / blur buffer, so the stages read lines other workgroups of the launch keep in L2
@@ -610,6 +609,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         ep_alias.blur_frame_bytes = 0;
         fstride = 0;
     }
+    ep_alias.host_out = mapped_out ? 1 : 0;
     const ExtractParams& ep = ep_alias;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
     hipStream_t sd = h->serial ? st : h->side;
@@ -722,8 +722,7 @@ void orbx_destroy(orbx_handle* h) {
     for (hipEvent_t e : {h->ev_pyr, h->ev_blur})
         if (e) (void)hipEventDestroy(e);
     if (h->l0_stream) (void)hipStreamDestroy(h->l0_stream);
-    for (hipEvent_t e : {h->ev_l0_fork, h->ev_l0_join})
-        if (e) (void)hipEventDestroy(e);
+    if (h->ev_l0_fork) (void)hipEventDestroy(h->ev_l0_fork);
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
     if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
     if (h->graph) (void)hipGraphDestroy(h->graph);
@@ -845,6 +844,47 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
                        (hipStream_t)stream, false);
 }
 
+extern "C++" {
+namespace {
+
+/* Wait for a per-call matcher launch: its last workgroup stores the match count (>= 0; the host
+ * pre-filled it with -1) into pinned host memory last, with release at system scope (match_kernels.hip
+ * call_tail), so polling that word ends the call ~5 us sooner than hipStreamSynchronize
+ * (tools/latency_floor.hip, profiles/r03_latency_floor.jsonl). The launch needs no further wait: the
+ * next call's copies and launches are ordered behind it on the stream. A stream that drains without
+ * the word, or an error, is ORBX_EDEVICE. */
+template <class Ready>
+int wait_until(hipStream_t st, Ready ready) {
+    {
+        // spin (with a pause) for the first ~200 us, which covers a call that is not queued behind other GPU
+        // work; after that yield the core to the other SLAM threads between polls instead of burning it
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned spins = 1;; spins++) {
+            if (ready()) return 0;
+            const bool late = (spins & 255) == 0 &&
+                              std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200);
+            if (late || (spins & 1023) == 0) {
+                const hipError_t e = hipStreamQuery(st);
+                if (e != hipErrorNotReady) {
+                    if (e != hipSuccess) return ORBX_EDEVICE;
+                    break;  // drained: the words are visible now if the kernel wrote them
+                }
+                if (late) {
+                    sched_yield();
+                    spins = 0;  // next check after another 256 polls
+                }
+            } else {
+                __builtin_ia32_pause();
+            }
+        }
+    }
+    HIPR(hipStreamSynchronize(st));
+    return ready() ? 0 : ORBX_EDEVICE;
+}
+
+}  // namespace
+}  // extern "C++"
+
 /* The captured host path: pinned H2D -> run_extract -> one pinned D2H of {count, error flag, K
  * keypoints, K descriptors}, as one hipGraph per geometry (replayed: no per-kernel launch cost on
  * the calling thread, one synchronisation per frame). The first call at a new geometry/buffer epoch
@@ -867,6 +907,7 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
         h->pin_out = nullptr;
         h->pin_out_bytes = 0;
         HIPR(hipHostMalloc((void**)&h->pin_out, out_bytes, hipHostMallocDefault));
+        memset(h->pin_out, 0, out_bytes);  // done word 0: the device counter's first value is 1
         h->pin_out_bytes = out_bytes;
         HIPR(hipHostGetDevicePointer((void**)&h->pin_out_dev, h->pin_out, 0));
         h->epoch++;
@@ -881,11 +922,15 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
     auto enqueue = [&]() -> int {
         HIPR(hipMemcpyAsync(h->in_frame.p, h->pin_in, in_bytes, hipMemcpyHostToDevice, h->stream));
         int rc = run_extract(h, 1, h->in_frame.as<uint8_t>(), (long long)in_bytes, width, (orbx_kp*)(d_out + 64),
-                             d_out + 64 + sizeof(orbx_kp) * (size_t)K, (int32_t*)d_out, K, h->stream);
+                             d_out + 64 + sizeof(orbx_kp) * (size_t)K, (int32_t*)d_out, K, h->stream, true, true);
         if (rc) return rc;
-        HIPR(launch_flag_take(h->err.as<int32_t>() + kErrWordExtract, (int32_t*)(d_out + 4), h->stream));
+        HIPR(launch_call_done(h->err.as<int32_t>() + kErrWordExtract, (int32_t*)(d_out + 4),
+                              h->err.as<int32_t>() + kErrWordExtractSeq, (int32_t*)(d_out + 8), h->stream));
         return 0;
     };
+    // the done word before this call's launch (the previous call's value): the call is over when it changes
+    const int32_t* done = (const int32_t*)(h->pin_out + 8);
+    const int32_t done0 = __atomic_load_n(done, __ATOMIC_ACQUIRE);
     const bool valid = h->gexec && h->graph_w == width && h->graph_h == height && h->graph_epoch == h->epoch;
     if (!valid) {
         if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
@@ -918,7 +963,7 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
         }
         HIPR(hipGraphLaunch(h->gexec, h->stream));
     }
-    HIPR(hipStreamSynchronize(h->stream));
+    if (const int rc = wait_until(h->stream, [&] { return __atomic_load_n(done, __ATOMIC_ACQUIRE) != done0; })) return rc;
     h->last_frames = h->in_frame.as<uint8_t>();
     h->last_fstride = (long long)in_bytes;
     h->last_pitch = width;
@@ -1198,41 +1243,6 @@ struct orbm_ctx {
 };
 
 namespace {
-
-/* Wait for a per-call matcher launch: its last workgroup stores the match count (>= 0; the host
- * pre-filled it with -1) into pinned host memory last, with release at system scope (match_kernels.hip
- * call_tail), so polling that word ends the call ~5 us sooner than hipStreamSynchronize
- * (tools/latency_floor.hip, profiles/r03_latency_floor.jsonl). The launch needs no further wait: the
- * next call's copies and launches are ordered behind it on the stream. A stream that drains without
- * the word, or an error, is ORBX_EDEVICE. */
-template <class Ready>
-int wait_until(hipStream_t st, Ready ready) {
-    {
-        // spin (with a pause) for the first ~200 us, which covers a call that is not queued behind other GPU
-        // work; after that yield the core to the other SLAM threads between polls instead of burning it
-        const auto t0 = std::chrono::steady_clock::now();
-        for (unsigned spins = 1;; spins++) {
-            if (ready()) return 0;
-            const bool late = (spins & 255) == 0 &&
-                              std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200);
-            if (late || (spins & 1023) == 0) {
-                const hipError_t e = hipStreamQuery(st);
-                if (e != hipErrorNotReady) {
-                    if (e != hipSuccess) return ORBX_EDEVICE;
-                    break;  // drained: the words are visible now if the kernel wrote them
-                }
-                if (late) {
-                    sched_yield();
-                    spins = 0;  // next check after another 256 polls
-                }
-            } else {
-                __builtin_ia32_pause();
-            }
-        }
-    }
-    HIPR(hipStreamSynchronize(st));
-    return ready() ? 0 : ORBX_EDEVICE;
-}
 
 int wait_call(hipStream_t st, const int32_t* word) {
     return wait_until(st, [word] { return __atomic_load_n(word, __ATOMIC_ACQUIRE) >= 0; });
@@ -2723,7 +2733,7 @@ struct orbv_handle {
     int device = 0;
     int k = 0, L = 0, scoring = 0, weighting = 0, nnodes = 0, nwords = 0;
     hipStream_t stream = nullptr;
-    DevBuf nodes;    // desc | weight | word_id | child_off | child
+    DevBuf nodes;    // child-slot descriptors | child-slot records (VocChild)
     DevBuf scratch;  // per-call staging
     VocDev v{};
 };
@@ -2752,31 +2762,36 @@ int orbv_create(int k, int L, int scoring, int weighting, int nlines, const int3
     }
     for (int i = 0; i < n; i++) child_off[i + 1] += child_off[i];
     for (int i = 1; i < n; i++) child[child_off[parent[i - 1]] + fill[parent[i - 1]]++] = i;  // push_back order
+    // child-slot order: slot c holds node child[c]'s descriptor and record (the kernels never read by node id)
+    const int ns = std::max(n - 1, 1);
+    std::vector<uint8_t> cd(32 * (size_t)ns, 0);
+    std::vector<VocChild> cr(ns);
+    for (int c = 0; c < n - 1; c++) {
+        const int id = child[c];
+        memcpy(&cd[32 * (size_t)c], &d[32 * (size_t)id], 32);
+        VocChild r{};
+        r.id = id, r.c0 = child_off[id], r.nc = child_off[id + 1] - child_off[id], r.word = word[id], r.weight = w[id];
+        cr[c] = r;
+    }
     HIPR(hipSetDevice(device));
     orbv_handle* h = new orbv_handle();
     h->device = device;
     h->k = k, h->L = L, h->scoring = scoring, h->weighting = weighting, h->nnodes = n, h->nwords = nwords;
     Carve cv;
-    const size_t o_d = cv.take(32 * (size_t)n), o_w = cv.take(8 * (size_t)n), o_word = cv.take(4 * (size_t)n),
-                 o_co = cv.take(4 * ((size_t)n + 1)), o_c = cv.take(4 * (size_t)n);
+    const size_t o_d = cv.take(32 * (size_t)ns), o_r = cv.take(sizeof(VocChild) * (size_t)ns);
     if (h->nodes.ensure(cv.off) || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         orbv_destroy(h);
         return ORBX_EDEVICE;
     }
     uint8_t* b = h->nodes.as<uint8_t>();
-    if (hipMemcpy(b + o_d, d.data(), 32 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(b + o_w, w.data(), 8 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(b + o_word, word.data(), 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(b + o_co, child_off.data(), 4 * ((size_t)n + 1), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(b + o_c, child.data(), 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(b + o_d, cd.data(), 32 * (size_t)ns, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(b + o_r, cr.data(), sizeof(VocChild) * (size_t)ns, hipMemcpyHostToDevice) != hipSuccess) {
         orbv_destroy(h);
         return ORBX_EDEVICE;
     }
-    h->v.desc = b + o_d;
-    h->v.weight = (const double*)(b + o_w);
-    h->v.word_id = (const int32_t*)(b + o_word);
-    h->v.child_off = (const int32_t*)(b + o_co);
-    h->v.child = (const int32_t*)(b + o_c);
+    h->v.cdesc = b + o_d;
+    h->v.crec = (const VocChild*)(b + o_r);
+    h->v.root_c0 = child_off[0], h->v.root_nc = child_off[1] - child_off[0];
     h->v.n = n, h->v.L = L, h->v.scoring = scoring, h->v.weighting = weighting;
     *out = h;
     return 0;

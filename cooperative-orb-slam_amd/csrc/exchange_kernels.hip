@@ -397,14 +397,21 @@ __global__ __launch_bounds__(64) void k_tri_slots_bow(const QueryKF q, const uin
 /* a good MapPoint (:558-562) takes the first strict minimum over the node's not yet matched   */
 /* candidates with a good MapPoint (:571-592; vbMatched2 can only hold this node's candidates: */
 /* a feature sits in one node), best2 = the minimum over the others; accept iff best1 < TH_LOW */
-/* and (float)best1 < nnratio * (float)best2 (:594-598). Lane j holds candidates j, j+64, ...; */
-/* its local first minimum and runner-up merge by two wave minima of (dist << 16 | position).  */
+/* and (float)best1 < nnratio * (float)best2 (:594-598). The node's candidates are staged once */
+/* in LDS (descriptor, feature index or -1 when it has no good MapPoint or is matched), 64     */
+/* queries at a time sit one per lane and are broadcast by readlane, so the greedy walk's      */
+/* per-query step reads only LDS. Lane j holds candidates j, j+64, ...; its local first        */
+/* minimum and runner-up merge by two wave minima of (dist << 16 | position).                  */
 /* match[r*cap1 + idx1] = the slot keyframe's feature idx2 (preset to -1 by the caller).       */
 /* ----------------------------------------------------------------------------------- */
+__device__ __forceinline__ uint32_t rl(uint32_t v, int t) { return (uint32_t)__builtin_amdgcn_readlane((int)v, t); }
+
 __global__ __launch_bounds__(64) void k_bow_slots(const QueryKF q, const uint8_t* __restrict__ slots, long long slot_bytes,
                                                   int slot0, float nnratio, int lds_cap, int32_t* __restrict__ match,
                                                   int32_t* __restrict__ err) {
-    extern __shared__ uint8_t matched[];  // per candidate position of the slot's node (vbMatched2)
+    extern __shared__ __align__(16) uint8_t lds[];  // [lds_cap] x 2 uint4 descriptors | [lds_cap] int candidates
+    uint4* s_cd = (uint4*)lds;
+    int* s_ci = (int*)(lds + 32 * (size_t)lds_cap);  // feature index, -1: no good MapPoint or matched (vbMatched2)
     const int gr = blockIdx.y, r = slot0 + gr, i = blockIdx.x, lane = threadIdx.x;
     SlotRef s;
     if (!slot_open(slots + (long long)r * slot_bytes, slot_bytes, s)) {
@@ -432,53 +439,74 @@ __global__ __launch_bounds__(64) void k_bow_slots(const QueryKF q, const uint8_t
     const int qb = min(max(q.fv_off[i], 0), q.cap);
     const int qe = min(max(q.fv_off[i + 1], qb), q.cap);
     const int n1 = min(max(*q.count, 0), q.cap);
-    for (int j = lane; j < nc; j += 64) matched[j] = 0;
+    for (int j = lane; j < nc; j += 64) {
+        const int idx2 = s.fv_feat[cb + j];
+        int ci = -1;
+        if ((unsigned)idx2 >= (unsigned)s.n) {
+            atomicOr(err, 4);
+        } else if ((s.mpf[idx2] & 3) == 1) {  // pMP2 NULL or bad (:575-579)
+            const uint4* cd = (const uint4*)(s.desc + (long long)idx2 * 32);
+            s_cd[2 * j] = cd[0];
+            s_cd[2 * j + 1] = cd[1];
+            ci = idx2;
+        }
+        s_ci[j] = ci;
+    }
     __syncthreads();
     int32_t* out = match + (long long)r * q.cap;
-    for (int qi = qb; qi < qe; qi++) {  // wave-uniform
-        const int idx1 = q.fv_feat[qi];
-        if ((unsigned)idx1 >= (unsigned)n1) {
-            if (lane == 0) atomicOr(err, 8);
-            continue;
-        }
-        if (!q.mpf || (q.mpf[idx1] & 3) != 1) continue;  // pMP1 NULL or bad (:558-562)
-        const uint4* d = (const uint4*)(q.desc + (long long)idx1 * 32);
-        const uint4 a0 = d[0], a1 = d[1];
-        int b1 = 256, i1 = -1, b2 = 256;
-        for (int j = lane; j < nc; j += 64) {
-            if (matched[j]) continue;
-            const int idx2 = s.fv_feat[cb + j];
-            if ((unsigned)idx2 >= (unsigned)s.n) {
-                atomicOr(err, 4);
-                continue;
-            }
-            if ((s.mpf[idx2] & 3) != 1) continue;  // pMP2 NULL or bad (:575-579)
-            const uint4* cd = (const uint4*)(s.desc + (long long)idx2 * 32);
-            const uint4 c0 = cd[0], c1 = cd[1];
-            const int dist = __popc(a0.x ^ c0.x) + __popc(a0.y ^ c0.y) + __popc(a0.z ^ c0.z) + __popc(a0.w ^ c0.w) +
-                             __popc(a1.x ^ c1.x) + __popc(a1.y ^ c1.y) + __popc(a1.z ^ c1.z) + __popc(a1.w ^ c1.w);
-            if (dist < b1) {
-                b2 = b1;
-                b1 = dist;
-                i1 = j;
-            } else if (dist < b2) {
-                b2 = dist;
+    for (int q0 = qb; q0 < qe; q0 += 64) {
+        // this lane's query of the next 64: feature index (-1: no good MapPoint, :558-562) and descriptor
+        int idx1 = -1;
+        uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+        if (q0 + lane < qe) {
+            idx1 = q.fv_feat[q0 + lane];
+            if ((unsigned)idx1 >= (unsigned)n1) {
+                atomicOr(err, 8);
+                idx1 = -1;
+            } else if (!q.mpf || (q.mpf[idx1] & 3) != 1) {
+                idx1 = -1;
+            } else {
+                const uint4* d = (const uint4*)(q.desc + (long long)idx1 * 32);
+                a0 = d[0];
+                a1 = d[1];
             }
         }
-        // the first strict minimum over all lanes = min of (dist << 16 | position); best2 = the minimum over every
-        // other eligible candidate: the owner lane's runner-up, every other lane's own minimum
-        const uint32_t k1 = i1 >= 0 ? ((uint32_t)b1 << 16) | (uint32_t)i1 : 0xFFFFFFFFu;
-        const uint32_t kmin = wave_min_u32(k1);
-        const bool owner = kmin != 0xFFFFFFFFu && k1 == kmin;
-        const uint32_t bd2 = wave_min_u32(owner ? (uint32_t)b2 : (uint32_t)b1);
-        if (kmin == 0xFFFFFFFFu) continue;
-        const int best1 = (int)(kmin >> 16), pos = (int)(kmin & 0xFFFFu);
-        if (best1 < 50 && __fmul_rn(1.0f, (float)best1) < __fmul_rn(nnratio, (float)bd2)) {  // TH_LOW, :594-598
-            if (lane == 0) {
-                matched[pos] = 1;
-                out[idx1] = s.fv_feat[cb + pos];
+        const int nq = min(64, qe - q0);
+        for (int t = 0; t < nq; t++) {  // the node's queries in order (wave-uniform)
+            const int i1 = (int)rl((uint32_t)idx1, t);
+            if (i1 < 0) continue;
+            const uint32_t x0 = rl(a0.x, t), x1 = rl(a0.y, t), x2 = rl(a0.z, t), x3 = rl(a0.w, t);
+            const uint32_t x4 = rl(a1.x, t), x5 = rl(a1.y, t), x6 = rl(a1.z, t), x7 = rl(a1.w, t);
+            int b1 = 256, j1 = -1, b2 = 256;
+            for (int j = lane; j < nc; j += 64) {
+                if (s_ci[j] < 0) continue;
+                const uint4 c0 = s_cd[2 * j], c1 = s_cd[2 * j + 1];
+                const int dist = __popc(x0 ^ c0.x) + __popc(x1 ^ c0.y) + __popc(x2 ^ c0.z) + __popc(x3 ^ c0.w) +
+                                 __popc(x4 ^ c1.x) + __popc(x5 ^ c1.y) + __popc(x6 ^ c1.z) + __popc(x7 ^ c1.w);
+                if (dist < b1) {
+                    b2 = b1;
+                    b1 = dist;
+                    j1 = j;
+                } else if (dist < b2) {
+                    b2 = dist;
+                }
             }
-            __syncthreads();
+            // the first strict minimum over all lanes = min of (dist << 16 | position); best2 = the minimum over
+            // every other eligible candidate: the owner lane's runner-up, every other lane's own minimum
+            const uint32_t k1 = j1 >= 0 ? ((uint32_t)b1 << 16) | (uint32_t)j1 : 0xFFFFFFFFu;
+            const uint32_t kmin = wave_min_u32(k1);
+            const bool owner = kmin != 0xFFFFFFFFu && k1 == kmin;
+            const uint32_t bd2 = wave_min_u32(owner ? (uint32_t)b2 : (uint32_t)b1);
+            if (kmin == 0xFFFFFFFFu) continue;
+            const int best1 = (int)(kmin >> 16), pos = (int)(kmin & 0xFFFFu);
+            if (best1 < 50 && __fmul_rn(1.0f, (float)best1) < __fmul_rn(nnratio, (float)bd2)) {  // TH_LOW, :594-598
+                __syncthreads();  // every lane has read s_ci[pos] for this query
+                if (lane == 0) {
+                    out[i1] = s_ci[pos];
+                    s_ci[pos] = -1;  // vbMatched2
+                }
+                __syncthreads();
+            }
         }
     }
 }
@@ -552,6 +580,24 @@ hipError_t launch_flag_take(int32_t* flag, int32_t* out, hipStream_t st) {
     return hipGetLastError();
 }
 
+/* The host extraction's last launch: takes the call's error word into mapped host memory like k_flag_take, then
+ * stores the call's done word there (the device call counter + 1, never the value the host read before the
+ * launch), last, with release at system scope: the host polls it instead of synchronising the stream. */
+__global__ void k_call_done(int32_t* flag, int32_t* out_err, int32_t* seq, int32_t* out_done) {
+    if (threadIdx.x == 0) {
+        *out_err = atomicExch(flag, 0);
+        const int32_t s = *seq >= (1 << 30) ? 1 : *seq + 1;
+        *seq = s;
+        __threadfence_system();
+        __hip_atomic_store(out_done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+hipError_t launch_call_done(int32_t* flag, int32_t* out_err, int32_t* seq, int32_t* out_done, hipStream_t st) {
+    hipLaunchKernelGGL(k_call_done, dim3(1), dim3(64), 0, st, flag, out_err, seq, out_done);
+    return hipGetLastError();
+}
+
 /* ----------------------------------------------------------------------------------- */
 hipError_t launch_pack_slot(const orbx_kf_source& src, const SlotLayout& L, const orbx_kf_meta& meta, uint8_t* slot,
                             int32_t* err, hipStream_t st) {
@@ -595,8 +641,17 @@ hipError_t launch_bow_slots(const QueryKF& q, const uint8_t* slots, long long sl
                             hipStream_t st) {
     if (nref == 0) return hipSuccess;
     if (max_nodes > 0) {
-        hipLaunchKernelGGL(k_bow_slots, dim3(max_nodes, nref), dim3(64), (size_t)q.cap, st, q, slots, slot_bytes, 0,
-                           nnratio, q.cap, match, err);
+        // the node's candidates in LDS: 36 bytes each, up to the query keyframe's capacity (a node holds at most
+        // every feature; a slot node past it is flagged)
+        const size_t lds = 36 * (size_t)q.cap;
+        if (lds > 160 * 1024) return hipErrorInvalidValue;
+        if (lds > 65536) {  // past the 64 KB default (a host-side attribute of the current device's function)
+            const hipError_t e = hipFuncSetAttribute((const void*)k_bow_slots, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_bow_slots, dim3(max_nodes, nref), dim3(64), lds, st, q, slots, slot_bytes, 0, nnratio,
+                           q.cap, match, err);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -127,17 +127,15 @@ __global__ __launch_bounds__(256) void k_resize_level(
  * then each thread produces kRsTH/4 rows of one column from LDS. Every table load (window
  * bounds, xofs/alpha of the thread's column, yofs/beta of its rows) is issued before the
  * staging loads, so a tile costs two memory round trips (tables, source). */
-constexpr int kRsTW = 64, kRsTH = 32, kRsW = 144, kRsH = 48, kRsRows = kRsTH / 4;
+constexpr int kRsTW = kRsTileW, kRsTH = kRsTileH, kRsW = 144, kRsH = 48, kRsRows = kRsTH / 4;
 
-__global__ __launch_bounds__(256) void k_resize_tiled(
-    const uint8_t* __restrict__ src, long long src_fstride, int src_pitch, int sw, int sh,
-    uint8_t* __restrict__ dst, long long dst_fstride, int dst_pitch, int dw, int dh,
-    const int* __restrict__ xofs, const short2* __restrict__ alpha, const int* __restrict__ yofs,
-    const short2* __restrict__ beta, int xmax, int simd_end) {
-    __shared__ __align__(16) uint8_t tile[kRsH][kRsW];
-    const int c0 = blockIdx.x * kRsTW, r0 = blockIdx.y * kRsTH;
+__device__ __forceinline__ void resize_tile(const uint8_t* __restrict__ S, int src_pitch, int sw, int sh,
+                                            uint8_t* __restrict__ D, int dst_pitch, int dw, int dh,
+                                            const int* __restrict__ xofs, const short2* __restrict__ alpha,
+                                            const int* __restrict__ yofs, const short2* __restrict__ beta, int xmax,
+                                            int simd_end, int bx, int by, uint8_t (*tile)[kRsW]) {
+    const int c0 = bx * kRsTW, r0 = by * kRsTH;
     const int c1 = min(c0 + kRsTW, dw), r1 = min(r0 + kRsTH, dh);
-    const uint8_t* S = src + (long long)blockIdx.z * src_fstride;
     const int tid = threadIdx.x;
     // this thread's column and rows (indices clamped so every load is unconditional)
     const int c = c0 + (tid & 63);
@@ -180,12 +178,11 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
             if (slot[k] >= 0) *(uint32_t*)(&tile[0][0] + slot[k]) = v[k];
     }
     __syncthreads();
-    if (c >= c1) return;
+    if (c >= c1) return;  // (no barrier follows inside the tile)
     // LDS column of source x in row r: (x - sx_lo) + mis(r), mis = misalignment of that row's start
     const int a0 = c < xmax ? al.x : 2048, a1 = c < xmax ? al.y : 0;
     const int sxn = c < xmax ? sx + 1 : sx;
     const int mis0 = (int)((uintptr_t)(S + sx_lo) & 3);
-    uint8_t* D = dst + (long long)blockIdx.z * dst_fstride;
 #pragma unroll
     for (int k = 0; k < kRsRows; k++) {
         const int y = yr0 + k;
@@ -204,6 +201,17 @@ __global__ __launch_bounds__(256) void k_resize_tiled(
             v = (__mul24(h0, (int)b.x) + __mul24(h1, (int)b.y) + (1 << 21)) >> 22;
         D[(long long)y * dst_pitch + c] = (uint8_t)iclamp(v, 0, 255);
     }
+}
+
+
+__global__ __launch_bounds__(256) void k_resize_tiled(
+    const uint8_t* __restrict__ src, long long src_fstride, int src_pitch, int sw, int sh,
+    uint8_t* __restrict__ dst, long long dst_fstride, int dst_pitch, int dw, int dh,
+    const int* __restrict__ xofs, const short2* __restrict__ alpha, const int* __restrict__ yofs,
+    const short2* __restrict__ beta, int xmax, int simd_end) {
+    __shared__ __align__(16) uint8_t tile[kRsH][kRsW];
+    resize_tile(src + (long long)blockIdx.z * src_fstride, src_pitch, sw, sh, dst + (long long)blockIdx.z * dst_fstride,
+                dst_pitch, dw, dh, xofs, alpha, yofs, beta, xmax, simd_end, blockIdx.x, blockIdx.y, tile);
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -1341,6 +1349,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
 #pragma unroll
         for (int q = 0; q < kMaxLevels; q++) tot += cl[q];
         out_counts[f] = tot;
+        if (ep.host_out) __threadfence_system();
     }
     __syncthreads();
     if (__ballot(g < ep.kp_per_frame) == 0) return;  // wave-uniform
@@ -1489,6 +1498,9 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
             out_kps[o] = kp;
         }
     }
+    // the host path's results land in mapped host memory: visible to the CPU before the call's done word
+    // (k_call_done, a later launch) is
+    if (ep.host_out) __threadfence_system();
 }
 
 /* self-test hook: the device restatement of glibc sinf/cosf on an array (tests only) */

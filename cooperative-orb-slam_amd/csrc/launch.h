@@ -66,6 +66,7 @@ hipError_t launch_rot_filter(int n, int32_t* m, const float* angA, const float* 
                              hipStream_t st);
 
 hipError_t launch_flag_take(int32_t* flag, int32_t* out, hipStream_t st);
+hipError_t launch_call_done(int32_t* flag, int32_t* out_err, int32_t* seq, int32_t* out_done, hipStream_t st);
 hipError_t launch_pack_slot(const orbx_kf_source& src, const SlotLayout& L, const orbx_kf_meta& meta, uint8_t* slot,
                             int32_t* err, hipStream_t st);
 hipError_t launch_bow_slots(const QueryKF& q, const uint8_t* slots, long long slot_bytes, int nref, float nnratio,

@@ -9,12 +9,22 @@ namespace orbamd {
 
 constexpr int kVocMaxFeatures = 4096;  // descriptors per frame of one transform (LDS sort capacity)
 
+/* a node as its parent's child: the descent reads, for every child of the current node, the child's
+ * descriptor and this record in one round of independent loads, and takes the next node's children from the
+ * winning lane's record -- one dependent round per level instead of three (child_off -> child -> desc) */
+struct VocChild {
+    int32_t id;      // node id (file order)
+    int32_t c0, nc;  // its children: child slots c0 .. c0 + nc - 1 (file order)
+    int32_t word;    // word id (Node() default 0 for nodes not flagged as words)
+    double weight;
+    int32_t pad[2];
+};
+static_assert(sizeof(VocChild) == 32, "one 32-byte record per child slot");
+
 struct VocDev {
-    const uint8_t* desc;       // [n][32] node descriptors (node 0 = root)
-    const double* weight;      // [n]
-    const int32_t* word_id;    // [n] (Node() default 0 for nodes not flagged as words)
-    const int32_t* child_off;  // [n+1] children of node i: child[child_off[i] .. child_off[i+1]) in file order
-    const int32_t* child;      // [n]
+    const uint8_t* cdesc;      // [child slot][32] descriptor of the node in that slot (root's children first)
+    const VocChild* crec;      // [child slot]
+    int root_c0, root_nc;      // the root's children
     int n, L, scoring, weighting;
 };
 

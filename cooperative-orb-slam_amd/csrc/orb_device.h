@@ -36,6 +36,7 @@ constexpr int kPyrU = 4;            // k_pyramid_frames: rows in flight per thre
 constexpr int kPyrThreads = 512;
 constexpr int kPyrThreadsMax = 1024;
 constexpr int kPyrFramesMinBatch = 64;  // batches below this use the per-level pyramid kernels
+constexpr int kRsTileW = 64, kRsTileH = 32;  // k_resize_tiled output tile
 
 struct LevelDesc {
     int w, h, pitch;
@@ -85,6 +86,7 @@ struct ExtractParams {
     int kp_off[kMaxLevels + 1];      // level l's octree output slots start (kp_off[L] = kp_per_frame)
     int bjob_begin[kMaxLevels + 1];  // blur strip jobs prefix
     int ic_off;                      // IC_Angle mask table (int2 pairs) inside the ptab buffer
+    int host_out;                    // describe writes into mapped host memory: system-scope fence after the writes
 };
 
 /* level containing index g of a per-level prefix table (no dependent loads: unrolled compares

@@ -80,14 +80,19 @@ def test_extract_noise_and_flat_edge_cases():
     _compare(kg, dg, ko, do)
 
 
-def test_batch_device_matches_host_path():
+@pytest.mark.parametrize("B", [6, 4, 2])
+def test_batch_device_matches_host_path(B):
+    """small batches (< 64 frames: run_extract_levels' two queue lists) at several sizes, three steps on one
+    pipeline (the graph replays), every frame against the oracle and the device error word clean"""
     torch = pytest.importorskip("torch")
-    W, H, B = 640, 480, 6
+    W, H = 640, 480
     frames = orbamd.synth_frames(2, 10, B, W, H)
     pipe = orbamd.device.BatchPipeline(torch, W, H, B)
     fr = torch.from_numpy(frames).cuda()
-    pipe.step(fr)
+    for _ in range(3):
+        pipe.step(fr)
     torch.cuda.synchronize()
+    pipe.check_error()
     orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
     for b in range(B):
         kg, dg, _ = pipe.host_results(b)
