@@ -158,14 +158,17 @@ struct Geometry {
     std::vector<LevelDesc> lv;
     std::vector<CellDesc> cells;
     std::vector<int> coef;
-    std::vector<int> bjob_begin;  // blur strip jobs (256 cols x 64 rows) per level
+    std::vector<int> bjob_begin;  // blur strip jobs (256 cols x kBlurRows rows) per level
     int nbjobs = 0;
+    int bjob_small[kMaxLevels + 1] = {0};  // the same in kBlurRowsSmall-row chunks (run_extract_levels)
+    int nbjobs_small = 0;
     int NC = 0, KL = 0, lds_bytes = 0;
     int roi_pitch = 0, roi_rows = 0;  // FAST cell LDS staging (max cell ROI)
     int max_pass = 1;                 // ROI staging passes (rows per 64-lane dword pass)
     int tiled_ok[kMaxLevels] = {0};   // level's resize fits the LDS-tiled kernel
     std::vector<int> ptab;            // k_pyramid_frames column-group / row tables
     bool frames_ok = true;            // every level fits k_pyramid_frames
+    int band_off = 0;                 // ptab offset of the small-batch row bands ([kPyrBands][kMaxLevels] int2)
     int pyr_rows = 1;                 // tallest level >= 1 (k_pyramid_frames' LDS row table rows)
     DevBuf d_lv, d_cells, d_coef, d_ptab;
 
@@ -346,12 +349,43 @@ struct Geometry {
         for (int l = 0; l < L; l++)
             bjob_begin[l + 1] = bjob_begin[l] + ((lv[l].w + 255) / 256) * ((lv[l].h + kBlurRows - 1) / kBlurRows);
         nbjobs = bjob_begin[L];
+        int bs = 0;  // the same jobs in kBlurRowsSmall-row chunks (small batches)
         for (int l = 0; l <= kMaxLevels; l++) {
             ep.kp_off[l] = l < L ? lv[l].kp_off : kp_off;
             ep.bjob_begin[l] = l <= L ? bjob_begin[l] : nbjobs;
+            bjob_small[l] = bs;
+            if (l < L) bs += ((lv[l].w + 255) / 256) * ((lv[l].h + kBlurRowsSmall - 1) / kBlurRowsSmall);
         }
+        nbjobs_small = bjob_small[L];
         pyr_rows = 1;
         for (int l = 1; l < L; l++) pyr_rows = std::max(pyr_rows, lv[l].h);
+        // row bands of the small-batch pyramid (kPyrBands): band b owns rows [b h / B, (b + 1) h / B) of every
+        // level and also makes the rows its own higher levels read (the (r0, r1) of k_pyramid_frames' row
+        // table), so each workgroup only reads back rows it wrote itself
+        band_off = (int)ptab.size();
+        if (frames_ok) {
+            std::vector<int> bt(2 * kPyrBands * kMaxLevels, 0);
+            for (int b = 0; b < kPyrBands; b++) {
+                int nlo = 0, nhi = 0;  // rows of level l that level l + 1's range reads ([nlo, nhi), empty at the top)
+                for (int l = L - 1; l >= 1; l--) {
+                    const int h = lv[l].h;
+                    int lo = (int)((long long)b * h / kPyrBands), hi = (int)((long long)(b + 1) * h / kPyrBands);
+                    if (nhi > nlo) {
+                        lo = hi > lo ? std::min(lo, nlo) : nlo;
+                        hi = std::max(hi, nhi);
+                    }
+                    bt[2 * (b * kMaxLevels + l)] = lo;
+                    bt[2 * (b * kMaxLevels + l) + 1] = hi;
+                    nlo = nhi = 0;
+                    if (hi > lo && l > 1) {  // this range's source rows in level l - 1
+                        const int* rt = &ptab[lv[l].rt_off];
+                        nlo = rt[4 * lo];
+                        nhi = rt[4 * (hi - 1) + 1] + 1;
+                    }
+                }
+            }
+            ptab.insert(ptab.end(), bt.begin(), bt.end());
+        }
         // octree LDS: node arrays (92 B/node, NC pow2) + keys (7 B/key)
         NC = 1;
         while (NC < maxnode) NC <<= 1;
@@ -387,9 +421,6 @@ struct orbx_handle {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
     hipEvent_t ev_pyr = nullptr, ev_blur = nullptr;
-    // small batches (run_extract_levels): the pyramid + blur list's stream and its fork event
-    hipStream_t l0_stream = nullptr;
-    hipEvent_t ev_l0_fork = nullptr;
     hipEvent_t user_ev_pyr = nullptr;  // orbx_set_pyramid_event (caller-owned)
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
@@ -472,14 +503,16 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
 static int launch_pyramid(orbx_handle* h, const ExtractParams& ep, const uint8_t* d_frames, long long fstride,
                           int pitch, int nframes, hipStream_t st) {
     Geometry& g = h->geo;
-    // pyramid levels 1..L-1 (ORBextractor.cc:1107-1132): whole-frame kernel for large batches of
-    // 4-byte-aligned frames, per-level kernels otherwise
+    // pyramid levels 1..L-1 (ORBextractor.cc:1107-1132) of 4-byte-aligned frames: whole-frame workgroups for
+    // large batches, row-band workgroups (kPyrBands per frame) for small ones; per-level kernels otherwise
     const bool aligned = ((uintptr_t)d_frames & 3) == 0 && (fstride & 3) == 0 && (pitch & 3) == 0;
-    if (g.frames_ok && aligned && nframes >= kPyrFramesMinBatch && ep.L > 1) {
+    if (g.frames_ok && aligned && ep.L > 1) {
         int max_groups = 1;
         for (int l = 1; l < ep.L; l++) max_groups = std::max(max_groups, (g.lv[l].w + 3) / 4);
+        const bool banded = nframes < kPyrFramesMinBatch;
         HIPR(launch_pyramid_frames(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, g.d_lv.as<LevelDesc>(),
-                                   g.d_ptab.as<int>(), g.pyr_rows, max_groups, nframes, st));
+                                   g.d_ptab.as<int>(), g.pyr_rows, max_groups, nframes, st,
+                                   banded ? (const int2*)(g.d_ptab.as<int>() + g.band_off) : nullptr));
         return 0;
     }
     for (int l = 1; l < ep.L; l++) {
@@ -525,71 +558,38 @@ static int launch_fast(orbx_handle* h, const ExtractParams& ep, const uint8_t* d
  * erases an unread batch error. */
 constexpr int kErrWordSticky = 0, kErrWordCall = 1, kErrWordExtract = 2, kErrWordTake = 32, kErrWordExtractTake = 33;
 constexpr int kErrWordExtractSeq = 40;  // the host extraction's call counter (k_call_done's done word)
-/* Small batches (the Tracking thread's one frame per call, ORBextractor.cc:1043-1105): the pyramid is a chain of
- * per-level launches. The graph executor maps a captured graph to queues by a depth-first walk: a node's first
- * captured child continues its parent's queue, every other child starts a new list on another queue, and an edge
- * between lists is a marker behind everything already submitted to the source queue; streams share the
- * process's 4 hardware queues, so a third list may land behind another on one queue. Two lists, then:
- *
- *   st  : resize 1 -> FAST(levels 0, 1) -> octree(0, 1) -> [ev_pyr] FAST(2..) -> octree(2..) -> [ev_blur] describe
- *   l0  :    [fork] resize 2 .. L-1 -> [ev_pyr] blur(all levels) -> [ev_blur]
- *
- * Levels 0 and 1 need no more of the pyramid than resize 1, so their FAST and octree (level 0's is the longest
- * single workgroup) run while the other queue builds the rest of the pyramid and then blurs it; FAST and octree
- * of levels 2.. follow once the pyramid is complete. (A branch per level measured 2x slower, and so did a single
- * launch for levels 2.. whose tiles wait on each other's counters: each level hand-off is an agent-scope
- * release / acquire pair across XCDs, profiles/r04_latency_branches.log, r04i_branch_ab.log.) */
+/* Small batches (the Tracking thread's one frame per call, ORBextractor.cc:1043-1105): every stage in order on the
+ * caller's queue -- the pyramid in kPyrBands row bands per frame (one launch); FAST over every cell and the blur
+ * in 14-row chunks (4.5x the waves of the batch form's 63-row chunks: one frame's blur is one chunk's row chain)
+ * in one launch (k_fast_blur); the octree over every level; describe. A single queue because the graph executor turns every edge between queues into a
+ * marker behind all the work already submitted to the source queue (~10 us per hop in the kernel trace, and a
+ * side branch started only once its marker came up), and streams share the process's 4 hardware queues; every
+ * branch layout measured slower than the one queue (profiles/r04_latency_branches.log, r04_latency_lists.log,
+ * r04m_latency_ab.log), and so did a single launch for levels 2.. whose tiles wait on each other's counters
+ * (r04_latency_chain_reverted.log). */
 static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nframes, const uint8_t* d_frames,
                               long long fstride, int pitch, orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
                               int kp_stride, hipStream_t st, int* errp) {
     Geometry& g = h->geo;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
-    if (!h->l0_stream) HIPR(hipStreamCreateWithFlags(&h->l0_stream, hipStreamNonBlocking));
-    if (!h->ev_l0_fork) HIPR(hipEventCreateWithFlags(&h->ev_l0_fork, hipEventDisableTiming));
-    auto resize = [&](int l, hipStream_t s2) -> int {
-        if (h->skip_mask & 1) return 0;
-        const LevelDesc& s = g.lv[l - 1];
-        const LevelDesc& d = g.lv[l];
-        const uint8_t* src = l == 1 ? d_frames : h->pyr.as<uint8_t>() + s.pyr_off;
-        const long long sfs = l == 1 ? fstride : ep.pyr_frame_bytes;
-        const int sp = l == 1 ? pitch : s.pitch;
-        if (g.tiled_ok[l])
-            HIPR(launch_resize_tiled(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes,
-                                     d.pitch, d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes,
-                                     s2));
-        else
-            HIPR(launch_resize(src, sfs, sp, s.w, s.h, h->pyr.as<uint8_t>() + d.pyr_off, ep.pyr_frame_bytes, d.pitch,
-                               d.w, d.h, g.d_coef.as<int>() + d.coef_off, d.xmax, d.simd_end, nframes, s2));
-        return 0;
-    };
-    // FAST + octree of levels [l0, l1) on stream s2
-    auto fast_octree = [&](int l0, int l1, hipStream_t s2) -> int {
-        if (l1 <= l0) return 0;
-        const int c0 = g.lv[l0].cell_begin, c1 = l1 < ep.L ? g.lv[l1].cell_begin : ep.ncells;
-        if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, c0, c1, nframes, s2)) return ORBX_EDEVICE;
-        if (!(h->skip_mask & 4))
-            HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
-                               h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
-                               (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, s2, l0,
-                               l1 - l0));
-        return 0;
-    };
-    const int k = std::min(2, ep.L);
-    for (int l = 1; l < k; l++)
-        if (resize(l, st)) return ORBX_EDEVICE;
-    HIPR(hipEventRecord(h->ev_l0_fork, st));
-    if (fast_octree(0, k, st)) return ORBX_EDEVICE;  // captured first: resize 1's queue continues with it
-    HIPR(hipStreamWaitEvent(h->l0_stream, h->ev_l0_fork, 0));
-    for (int l = k; l < ep.L; l++)
-        if (resize(l, h->l0_stream)) return ORBX_EDEVICE;
-    HIPR(hipEventRecord(h->ev_pyr, h->l0_stream));
-    if (!(h->skip_mask & 8))
-        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl, 0, g.nbjobs,
-                                nullptr, nframes, h->l0_stream));
-    HIPR(hipEventRecord(h->ev_blur, h->l0_stream));
-    HIPR(hipStreamWaitEvent(st, h->ev_pyr, 0));
-    if (fast_octree(k, ep.L, st)) return ORBX_EDEVICE;
-    HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
+    if (!(h->skip_mask & 1) && launch_pyramid(h, ep, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
+    ExtractParams eb = ep;  // the blur's short-chunk job table
+    for (int i = 0; i <= kMaxLevels; i++) eb.bjob_begin[i] = g.bjob_small[i];
+    if (!(h->skip_mask & 2) && !(h->skip_mask & 8)) {  // FAST and the blur in one launch
+        HIPR(launch_fast_blur(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, g.d_cells.as<CellDesc>(),
+                              h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), g.roi_pitch, g.roi_rows, g.max_pass,
+                              h->blur.as<uint8_t>(), eb, g.nbjobs_small, nframes, st));
+    } else {
+        if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, ep.ncells, nframes, st))
+            return ORBX_EDEVICE;
+        if (!(h->skip_mask & 8))
+            HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), eb, dl, 0,
+                                    g.nbjobs_small, nullptr, nframes, st, kBlurRowsSmall));
+    }
+    if (!(h->skip_mask & 4))
+        HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
+                           h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
+                           (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st));
     if (!(h->skip_mask & 16))
         HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                              h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
@@ -712,7 +712,6 @@ void orbx_destroy(orbx_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->side) (void)hipStreamSynchronize(h->side);
-    if (h->l0_stream) (void)hipStreamSynchronize(h->l0_stream);
     for (DevBuf* b : {&h->pyr, &h->blur, &h->cellkey, &h->cellcnt, &h->lvkey, &h->lvcnt, &h->gscratch, &h->err,
                       &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt, &h->st_buf})
         b->release();
@@ -721,8 +720,6 @@ void orbx_destroy(orbx_handle* h) {
     if (h->side) (void)hipStreamDestroy(h->side);
     for (hipEvent_t e : {h->ev_pyr, h->ev_blur})
         if (e) (void)hipEventDestroy(e);
-    if (h->l0_stream) (void)hipStreamDestroy(h->l0_stream);
-    if (h->ev_l0_fork) (void)hipEventDestroy(h->ev_l0_fork);
     for (hipEvent_t e : h->prof_ev) (void)hipEventDestroy(e);
     if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
     if (h->graph) (void)hipGraphDestroy(h->graph);

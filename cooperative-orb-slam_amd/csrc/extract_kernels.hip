@@ -252,16 +252,16 @@ __device__ __forceinline__ float2v blur_vsum(const float2v r0, const float2v r1,
     return v;
 }
 
-/* one blur job: rows [chunk*kBlurRows, +kBlurRows) x columns [strip*256, +256) of a level (img / pitch,
+/* one blur job: rows [chunk*kRows, +kRows) x columns [strip*256, +256) of a level (img / pitch,
  * output out with the level's pitch), by one wave; rows = that wave's 7 x kBlurSeg LDS staging slots */
-template <bool kAligned>
+template <bool kAligned, int kRows>
 __device__ __forceinline__ void blur_job(const uint8_t* __restrict__ img, int pitch, const LevelDesc& lv,
                                          uint8_t* __restrict__ out, int strip, int chunk, uint8_t (*rows)[kBlurSeg],
                                          int lane) {
     const int w = lv.w, h = lv.h;
     const int sx = strip * 256;
     const int x0 = sx + lane * 4;
-    const int ya = chunk * kBlurRows, yb = min(h, ya + kBlurRows);
+    const int ya = chunk * kRows, yb = min(h, ya + kRows);
     const bool lane_on = x0 < w;
     const bool tail = x0 + 3 >= lv.blur_vec_end;  // some of this lane's columns take the scalar path
     const int seg0 = sx - 4;                      // segment byte 0 = column seg0
@@ -377,12 +377,16 @@ template <int U, int NT>
 __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
                                                          int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
                                                          const LevelDesc* __restrict__ levels,
-                                                         const int* __restrict__ ptab) {
+                                                         const int* __restrict__ ptab,
+                                                         const int2* __restrict__ bands) {
     // the current level's row table; sized at launch for the tallest level >= 1 (rows x 16 B: 6.4 KB at
     // 640x480) instead of kPyrMaxRows, so the LDS the long-lived pyramid workgroup holds stays free for the
     // other graphs' FAST / describe workgroups beside it
     extern __shared__ int4 s_rt[];
-    const int f = blockIdx.x, tid = threadIdx.x;
+    // whole frames: block = frame; row bands (small batches): block (band, frame), rows [x, y) of each level
+    // from the host's cone table (every row a band's next level reads was made by this workgroup, so the
+    // read-back after the level barrier is of its own writes)
+    const int f = bands ? blockIdx.y : blockIdx.x, band = bands ? blockIdx.x : 0, tid = threadIdx.x;
     uint8_t* P = pyr + (long long)f * ep.pyr_frame_bytes;
     for (int l = 1; l < ep.L; l++) {
         const LevelDesc sv = levels[l - 1];
@@ -390,9 +394,14 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
         const uint8_t* src = l == 1 ? frames + (long long)f * fstride : P + sv.pyr_off;
         const int sp = l == 1 ? pitch0 : sv.pitch;
         uint8_t* dst = P + lv.pyr_off;
-        const int hi = lv.h;
-        const int4* rt = (const int4*)(ptab + lv.rt_off);
-        for (int i = tid; i < hi; i += NT) s_rt[i] = rt[i];
+        int lo = 0, hi = lv.h;
+        if (bands) {
+            const int2 r = bands[band * kMaxLevels + l];
+            lo = r.x;
+            hi = r.y;
+        }
+        const int4* rt = (const int4*)(ptab + lv.rt_off) + lo;
+        for (int i = tid; i < hi - lo; i += NT) s_rt[i] = rt[i];
         const int gw = (lv.w + 3) >> 2;
         const int R = NT / gw;  // rows per pass
         const int ry = tid / gw, xg = tid - ry * gw;
@@ -404,11 +413,11 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
         // one pass = U output rows of this thread's column group: the 2 x 3 source dwords of each (rows clamped,
         // so every load is valid and unconditional), then the taps
         if (ry < R) {
-            for (int y0 = ry; y0 < hi; y0 += U * R) {
+            for (int y0 = lo + ry; y0 < hi; y0 += U * R) {
                 uint32_t w[U][2][3];
                 int4 rr[U];
 #pragma unroll
-                for (int u = 0; u < U; u++) rr[u] = s_rt[min(y0 + u * R, hi - 1)];
+                for (int u = 0; u < U; u++) rr[u] = s_rt[min(y0 + u * R, hi - 1) - lo];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
 #pragma unroll
@@ -517,19 +526,18 @@ __host__ __device__ inline int fast_wave_lds(int RP, int RH) {
 }
 
 template <int kMaxPass, int kRP>
-__global__ __launch_bounds__(256) void k_fast_cells2(
+__device__ __forceinline__ void fast_cells_body(
     const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
-    ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
-    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi) {
+    const ExtractParams& ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
+    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi, int bx,
+    int f, uint8_t* lds) {
     // compile-time ROI pitch for the common geometries: every LDS offset of the ring/NMS reads becomes an
     // instruction immediate
     const int RP = kRP ? kRP : RP_;
-    extern __shared__ __align__(16) uint8_t lds[];
     // wave index through readfirstlane: the cell descriptor, loop bounds and addressing are wave-uniform
     // (scalar loads / SALU) instead of per-lane VALU
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int f = blockIdx.y;
-    const int ci = cell_lo + blockIdx.x * 4 + wave;
+    const int ci = cell_lo + bx * 4 + wave;
     if (ci >= cell_hi) return;  // wave-uniform; no block barriers in this kernel
     const int roi_bytes = RP * RH;
     uint8_t* roi = lds + wave * fast_wave_lds(RP, RH);
@@ -734,6 +742,16 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
     if (lane == 0) cellcnt[(long long)f * ep.ncells + ci] = total;
 }
 
+template <int kMaxPass, int kRP>
+__global__ __launch_bounds__(256) void k_fast_cells2(
+    const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
+    ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
+    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    fast_cells_body<kMaxPass, kRP>(frames, fstride, pitch0, pyr, ep, levels, cells, cellkey, cellcnt, RP_, RH, cell_lo,
+                                   cell_hi, blockIdx.x, blockIdx.y, lds);
+}
+
 /* ----------------------------------------------------------------------------------- */
 /* DistributeOctTree, one 256-thread workgroup per (frame, level).                       */
 /*                                                                                       */
@@ -789,6 +807,12 @@ struct NodeT {
     uint16_t* x0; uint16_t* y0; uint16_t* x1; uint16_t* y1; int* nk; uint32_t* seq;
 };
 
+#ifdef ORBX_OCT_TRACE
+__device__ unsigned long long g_oct_trace[kMaxLevels][40];
+#define OCT_T(k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_oct_trace[l][(k)] = wall_clock64(); } while (0)
+#else
+#define OCT_T(k) do { } while (0)
+#endif
 template <int NT>
 __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc* __restrict__ levels,
                                                 const CellDesc* __restrict__ cells,
@@ -802,6 +826,7 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
     __shared__ int sh_size, sh_jstar, sh_tc, sh_nexp, sh_ndiv;
     const int tid = threadIdx.x;
     const int l = level0 + blockIdx.x, f = blockIdx.y;
+    OCT_T(0);
     const LevelDesc lv = levels[l];
     // --- carve LDS
     uint8_t* p = lds;
@@ -834,6 +859,7 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
         (void)off;
     }
     n = carry;
+    OCT_T(1);
     // The rest runs with the keys either in LDS (n <= KL) or in global scratch; the two
     // instantiations keep every key access a plain ds_* or global_* instruction (a pointer
     // that may be either would make all of them flat accesses).
@@ -906,6 +932,7 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
             if (tid == 0) lvcnt[f * ep.L + l] = 0;
             return;
         }
+        OCT_T(2);
         // --- 2. roots (ORBextractor.cc:542-585)
         const int nIni = lv.nIni;
         for (int s = tid; s < nIni; s += NT) cnt4[s] = 0;
@@ -949,9 +976,13 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
         uint32_t next_seq = (uint32_t)nIni;
         int phase = 1;
         const int N = lv.N;
+        OCT_T(3);
         // --- 3. division rounds (ORBextractor.cc:594-739)
         bool cnt_clean = false;  // cnt4[0, 4 size) already zero (cleared by the previous fast round)
+        int iters = 0;
         for (int iter = 0; iter < 100000; iter++) {
+            if (iter < 30) OCT_T(4 + iter);
+            iters = iter + 1;
             const int prevSize = size;
             if (!cnt_clean) {
                 for (int s = tid; s < size; s += NT) {
@@ -1186,6 +1217,11 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
             if (size >= N || size == prevSize) break;
             if (phase == 1 && size + nToExpand * 3 > N) phase = 2;
         }
+        OCT_T(34);
+#ifdef ORBX_OCT_TRACE
+        if (threadIdx.x == 0 && blockIdx.y == 0) g_oct_trace[l][36] = (unsigned long long)iters | ((unsigned long long)n << 16) | ((unsigned long long)phase << 40) | ((unsigned long long)size << 48);
+#endif
+        (void)iters;
         // --- 4. keep the best key of each node (first max response, ORBextractor.cc:741-760)
         uint32_t* best = (uint32_t*)cnt4;
         for (int s = tid; s < size; s += NT) best[s] = 0u;
@@ -1203,6 +1239,7 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
             outk[s] = x | (y << 12) | (kk & 0xFF000000u);
         }
         if (tid == 0) lvcnt[f * ep.L + l] = size;
+        OCT_T(35);
     };
     if (n <= KL) {
         tail(KeysLds{(uint32_t*)kbase, (uint16_t*)(kbase + 4 * KL), kbase + 6 * KL});
@@ -1212,15 +1249,14 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
     }
 }
 
-template <bool kAligned>
-__global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
-                                                     const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                     ExtractParams ep, const LevelDesc* __restrict__ levels,
-                                                     int job0, int job1, const int* __restrict__ lvcnt) {
-    __shared__ __align__(16) uint8_t s_rows[4][7][kBlurSeg];
+template <bool kAligned, int kRows>
+__device__ __forceinline__ void blur_strips_body(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
+                                                 const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                 const ExtractParams& ep, const LevelDesc* __restrict__ levels,
+                                                 int job0, int job1, const int* __restrict__ lvcnt, int bx, int f,
+                                                 uint8_t (*s_rows)[7][kBlurSeg]) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int f = blockIdx.y;
-    int j = job0 + blockIdx.x * 4 + wave;
+    int j = job0 + bx * 4 + wave;
     if (j >= job1) return;
     const int l = level_of(ep.bjob_begin, ep.L, j);
     j -= ep.bjob_begin[l];
@@ -1232,7 +1268,35 @@ __global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__
     const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
     const int pitch = l == 0 ? pitch0 : lv.pitch;
     uint8_t* out = blur + (long long)f * ep.blur_frame_bytes + lv.blur_off;
-    blur_job<kAligned>(img, pitch, lv, out, j % nstrips, j / nstrips, s_rows[wave], lane);
+    blur_job<kAligned, kRows>(img, pitch, lv, out, j % nstrips, j / nstrips, s_rows[wave], lane);
+}
+
+template <bool kAligned, int kRows>
+__global__ __launch_bounds__(256) void k_blur_strips(const uint8_t* __restrict__ frames, long long fstride, int pitch0,
+                                                     const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                     ExtractParams ep, const LevelDesc* __restrict__ levels,
+                                                     int job0, int job1, const int* __restrict__ lvcnt) {
+    __shared__ __align__(16) uint8_t s_rows[4][7][kBlurSeg];
+    blur_strips_body<kAligned, kRows>(frames, fstride, pitch0, pyr, blur, ep, levels, job0, job1, lvcnt, blockIdx.x,
+                                      blockIdx.y, s_rows);
+}
+
+/* FAST and the blur in one launch (small batches: both need only the pyramid, and one frame's FAST cells and
+ * blur chunks each fill a few dozen CUs): blocks [0, nfast) take FAST cells as k_fast_cells2, the rest take
+ * blur jobs (kBlurRowsSmall-row chunks, job table in eb) as k_blur_strips; every wave works alone */
+template <int kMaxPass, int kRP, bool kAligned>
+__global__ __launch_bounds__(256) void k_fast_blur(
+    const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
+    ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
+    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi, int nfast,
+    uint8_t* __restrict__ blur, ExtractParams eb, int njobs) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    if ((int)blockIdx.x < nfast)
+        fast_cells_body<kMaxPass, kRP>(frames, fstride, pitch0, pyr, ep, levels, cells, cellkey, cellcnt, RP_, RH,
+                                       cell_lo, cell_hi, blockIdx.x, blockIdx.y, lds);
+    else
+        blur_strips_body<kAligned, kBlurRowsSmall>(frames, fstride, pitch0, pyr, blur, eb, levels, 0, njobs, nullptr,
+                                                   blockIdx.x - nfast, blockIdx.y, (uint8_t(*)[7][kBlurSeg])lds);
 }
 
 /* rBRIEF test pairs as floats, one 16-byte load per test; stored (x0, x1, y0, y1) so the two points'
@@ -1533,18 +1597,23 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
                                  const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int max_rows,
-                                 int max_groups, int nframes, hipStream_t st) {
+                                 int max_groups, int nframes, hipStream_t st, const int2* bands) {
     if (max_rows < 1 || max_rows > kPyrMaxRows) return hipErrorInvalidValue;
+    const size_t lds = (size_t)max_rows * sizeof(int4);
+    if (bands) {  // row bands of a few frames: 1024 threads, so a band's rows of a level are one or two passes
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), dim3(kPyrBands, nframes), dim3(kPyrThreadsMax),
+                           lds, st, frames, fstride, pitch0, pyr, ep, levels, ptab, bands);
+        return hipGetLastError();
+    }
     // 512-thread workgroups pack beside the other graphs' kernels while every level
     // keeps >= 2 rows per pass; a level 1 wider than 4 x 256 columns (C4's 1034) would leave half the
     // threads idle, so such geometries take 1024 threads
-    const size_t lds = (size_t)max_rows * sizeof(int4);
     if (max_groups <= kPyrThreads / 2)
         hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), dim3(nframes), dim3(kPyrThreads), lds, st, frames,
-                           fstride, pitch0, pyr, ep, levels, ptab);
+                           fstride, pitch0, pyr, ep, levels, ptab, (const int2*)nullptr);
     else
         hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), dim3(nframes), dim3(kPyrThreadsMax), lds, st,
-                           frames, fstride, pitch0, pyr, ep, levels, ptab);
+                           frames, fstride, pitch0, pyr, ep, levels, ptab, (const int2*)nullptr);
     return hipGetLastError();
 }
 
@@ -1601,6 +1670,39 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
     return hipGetLastError();
 }
 
+hipError_t launch_fast_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                            const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells, uint32_t* cellkey,
+                            int* cellcnt, int RP, int RH, int max_pass, uint8_t* blur, const ExtractParams& eb,
+                            int njobs, int nframes, hipStream_t st) {
+    const int nfast = (ep.ncells + 3) / 4;
+    dim3 grid(nfast + (njobs + 3) / 4, nframes);
+    const size_t lds = std::max((size_t)4 * fast_wave_lds(RP, RH), sizeof(uint8_t) * 4 * 7 * kBlurSeg);
+    const bool aligned = (((uintptr_t)frames | (uintptr_t)fstride | (uintptr_t)pitch0) & 3) == 0;
+#define ORBX_FAST(MP, RPC)                                                                                          \
+    do {                                                                                                            \
+        if (aligned)                                                                                                \
+            hipLaunchKernelGGL((k_fast_blur<MP, RPC, true>), grid, dim3(256), lds, st, frames, fstride, pitch0, pyr,  \
+                               ep, levels, cells, cellkey, cellcnt, RP, RH, 0, ep.ncells, nfast, blur, eb, njobs);   \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_fast_blur<MP, RPC, false>), grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, \
+                               ep, levels, cells, cellkey, cellcnt, RP, RH, 0, ep.ncells, nfast, blur, eb, njobs);   \
+    } while (0)
+    if (max_pass <= 8 && RP == 40)
+        ORBX_FAST(8, 40);
+    else if (max_pass <= 8 && RP == 44)
+        ORBX_FAST(8, 44);
+    else if (max_pass <= 8 && RP == 48)
+        ORBX_FAST(8, 48);
+    else if (max_pass <= 8)
+        ORBX_FAST(8, 0);
+    else if (max_pass <= 12)
+        ORBX_FAST(12, 0);
+    else
+        ORBX_FAST(24, 0);
+#undef ORBX_FAST
+    return hipGetLastError();
+}
+
 hipError_t launch_sincos_selftest(const float* in, float* so, float* co, int n, hipStream_t st) {
     hipLaunchKernelGGL(k_sincos_selftest, dim3((n + 255) / 256), dim3(256), 0, st, in, so, co, n);
     return hipGetLastError();
@@ -1633,16 +1735,27 @@ hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const
 
 hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
                               const ExtractParams& ep, const LevelDesc* levels, int job0, int job1, const int* lvcnt,
-                              int nframes, hipStream_t st) {
+                              int nframes, hipStream_t st, int rows) {
     if (job1 <= job0) return hipSuccess;
+    if (rows != kBlurRows && rows != kBlurRowsSmall) return hipErrorInvalidValue;
     dim3 grid((job1 - job0 + 3) / 4, nframes);
     const bool aligned = (((uintptr_t)frames | (uintptr_t)fstride | (uintptr_t)pitch0) & 3) == 0;
-    if (aligned)
-        hipLaunchKernelGGL(k_blur_strips<true>, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
-                           job0, job1, lvcnt);
-    else
-        hipLaunchKernelGGL(k_blur_strips<false>, grid, dim3(256), 0, st, frames, fstride, pitch0, pyr, blur, ep, levels,
-                           job0, job1, lvcnt);
+    // ep.bjob_begin must be the job table of `rows`-row chunks (Geometry::bjob_begin / bjob_small)
+    if (rows == kBlurRows) {
+        if (aligned)
+            hipLaunchKernelGGL((k_blur_strips<true, kBlurRows>), grid, dim3(256), 0, st, frames, fstride, pitch0, pyr,
+                               blur, ep, levels, job0, job1, lvcnt);
+        else
+            hipLaunchKernelGGL((k_blur_strips<false, kBlurRows>), grid, dim3(256), 0, st, frames, fstride, pitch0, pyr,
+                               blur, ep, levels, job0, job1, lvcnt);
+    } else {
+        if (aligned)
+            hipLaunchKernelGGL((k_blur_strips<true, kBlurRowsSmall>), grid, dim3(256), 0, st, frames, fstride, pitch0,
+                               pyr, blur, ep, levels, job0, job1, lvcnt);
+        else
+            hipLaunchKernelGGL((k_blur_strips<false, kBlurRowsSmall>), grid, dim3(256), 0, st, frames, fstride, pitch0,
+                               pyr, blur, ep, levels, job0, job1, lvcnt);
+    }
     return hipGetLastError();
 }
 
@@ -1661,3 +1774,9 @@ hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0,
 }
 
 }  // namespace orbamd
+
+#ifdef ORBX_OCT_TRACE
+extern "C" int orbx_debug_octree_trace(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbamd::g_oct_trace), sizeof(orbamd::g_oct_trace)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -16,7 +16,8 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
                          int simd_end, int nframes, hipStream_t st);
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
                                  const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int max_rows,
-                                 int max_groups, int nframes, hipStream_t st);
+                                 int max_groups, int nframes, hipStream_t st,
+                                 const int2* bands = nullptr);
 hipError_t launch_resize_tiled(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
                                long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
                                int simd_end, int nframes, hipStream_t st);
@@ -32,9 +33,14 @@ hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const
                          uint8_t* gscratch, long long gscratch_frame_bytes, int NC, int KL, int lds_bytes,
                          int* err, int nframes, hipStream_t st, int level0 = 0, int nlevels = -1);
 /* blur jobs [job0, job1) (ExtractParams::bjob_begin numbers every level's strips) */
+/* FAST over every cell + the blur in kBlurRowsSmall-row chunks (job table eb) in one launch (small batches) */
+hipError_t launch_fast_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                            const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells, uint32_t* cellkey,
+                            int* cellcnt, int RP, int RH, int max_pass, uint8_t* blur, const ExtractParams& eb,
+                            int njobs, int nframes, hipStream_t st);
 hipError_t launch_blur_strips(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr, uint8_t* blur,
                               const ExtractParams& ep, const LevelDesc* levels, int job0, int job1, const int* lvcnt,
-                              int nframes, hipStream_t st);
+                              int nframes, hipStream_t st, int rows = kBlurRows);
 hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
                            const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
                            const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,

@@ -28,6 +28,8 @@ constexpr int kRoiMax = 72;         // max FAST cell ROI side (cells are < 60+6 
 constexpr int kRoiPitch = 72;
 constexpr int kBlurRows = 63;  // blur strip chunk height: 9 x 7 (the 7-row window loop has no partial step)
 static_assert(kBlurRows % 7 == 0, "blur chunk height must be a multiple of 7");
+constexpr int kBlurRowsSmall = 14;  // small batches (run_extract_levels): short chunks, 4.5x the waves of one frame
+static_assert(kBlurRowsSmall % 7 == 0, "blur chunk height must be a multiple of 7");
 constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity (levels >= 1)
 constexpr int kPyrU = 4;            // k_pyramid_frames: rows in flight per thread
 // k_pyramid_frames: threads per frame's workgroup. kPyrThreads is used when every level's 4-column
@@ -35,7 +37,11 @@ constexpr int kPyrU = 4;            // k_pyramid_frames: rows in flight per thre
 // whole-frame kernel accepts (>= column groups of every level)
 constexpr int kPyrThreads = 512;
 constexpr int kPyrThreadsMax = 1024;
-constexpr int kPyrFramesMinBatch = 64;  // batches below this use the per-level pyramid kernels
+constexpr int kPyrFramesMinBatch = 64;  // batches below this build the pyramid in row bands (below)
+// small batches: k_pyramid_frames over kPyrBands row bands per frame, each band's workgroup computing every level's
+// rows its band owns plus the rows its higher levels read (the band's dependency cone; overlapping rows are
+// written by two workgroups with the same bytes): one launch instead of a dependent launch per level
+constexpr int kPyrBands = 32;
 constexpr int kRsTileW = 64, kRsTileH = 32;  // k_resize_tiled output tile
 
 struct LevelDesc {
