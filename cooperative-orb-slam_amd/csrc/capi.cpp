@@ -757,18 +757,21 @@ int orbx_set_pyramid_event(orbx_handle* h, void* event) {
 int orbx_debug_skip_stages(orbx_handle* h, int mask) {
     if (!h || mask < 0 || mask > 0x1F) return ORBX_EARG;
     h->skip_mask = mask;
+    h->epoch++;  // a captured host-call graph holds the schedule it was captured with
     return 0;
 }
 
 int orbx_debug_serial(orbx_handle* h, int on) {
     if (!h) return ORBX_EARG;
     h->serial = on != 0;
+    h->epoch++;
     return 0;
 }
 
 int orbx_debug_alias_frames(orbx_handle* h, int on) {
     if (!h) return ORBX_EARG;
     h->alias = on != 0;
+    h->epoch++;
     return 0;
 }
 

@@ -847,18 +847,27 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
     const int* ccnt = cellcnt + (long long)f * ep.ncells + lv.cell_begin;
     const uint32_t* ckey = cellkey + (long long)f * ep.keys_per_frame;
     int carry = 0;
-    // cell offsets -> reuse dbase/spos as temp (ncells may exceed NC: chunked)
+    // the level's key count; for the flat gather below also each cell's key offset and slot, in LDS (cnt4's space,
+    // unused until the roots): the counts and slots come in one round of loads, with one scan
+    const bool flat = 2 * lv.ncells + 2 <= 4 * NC;
+    int* coff = cnt4;                   // [ncells + 1]
+    int* cslot = cnt4 + lv.ncells + 1;  // [ncells]
     __syncthreads();
     int n = 0;
     for (int c0 = 0; c0 < lv.ncells; c0 += NT) {
         const int c = c0 + tid;
         const int v = c < lv.ncells ? ccnt[c] : 0;
+        const int sl = flat && c < lv.ncells ? cells[lv.cell_begin + c].slot : 0;
         int tot;
         const int off = block_scan_excl<NT / 64>(v, &tot, red) + carry;
+        if (flat && c < lv.ncells) {
+            coff[c] = off;
+            cslot[c] = sl;
+        }
         carry += tot;
-        (void)off;
     }
     n = carry;
+    if (flat && tid == 0) coff[lv.ncells] = n;
     OCT_T(1);
     // The rest runs with the keys either in LDS (n <= KL) or in global scratch; the two
     // instantiations keep every key access a plain ds_* or global_* instruction (a pointer
@@ -867,26 +876,11 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
     struct KeysGlobal { uint32_t* key; uint16_t* label; uint8_t* quad; };
     auto tail = [&](auto K) {
         carry = 0;
-        if (2 * lv.ncells + 2 <= 4 * NC) {
-            // flat gather: the cells' key offsets and slots go to LDS (cnt4's space, unused until the roots),
-            // then thread t copies keys t, t+NT, ... finding each key's cell by a fixed-trip binary search, four
-            // keys in flight per thread. (A thread per cell copying its keys one by one waited on one global
-            // load per key of the level's fullest cell: the level-0 workgroup's long pole.)
-            int* coff = cnt4;                   // [ncells + 1]
-            int* cslot = cnt4 + lv.ncells + 1;  // [ncells]
-            for (int c0 = 0; c0 < lv.ncells; c0 += NT) {
-                const int c = c0 + tid;
-                const int v = c < lv.ncells ? ccnt[c] : 0;
-                const int sl = c < lv.ncells ? cells[lv.cell_begin + c].slot : 0;
-                int tot;
-                const int off = block_scan_excl<NT / 64>(v, &tot, red) + carry;
-                if (c < lv.ncells) {
-                    coff[c] = off;
-                    cslot[c] = sl;
-                }
-                carry += tot;
-            }
-            if (tid == 0) coff[lv.ncells] = carry;
+        if (flat) {
+            // flat gather: thread t copies keys t, t+NT, ... finding each key's cell by a fixed-trip binary search
+            // over the cell offsets (in LDS since the count pass), four keys in flight per thread. (A thread per
+            // cell copying its keys one by one waited on one global load per key of the level's fullest cell: the
+            // level-0 workgroup's long pole.)
             __syncthreads();
             int top = 1;
             while (top < lv.ncells) top <<= 1;
@@ -937,12 +931,29 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
         const int nIni = lv.nIni;
         for (int s = tid; s < nIni; s += NT) cnt4[s] = 0;
         __syncthreads();
-        for (int i = tid; i < n; i += NT) {
-            const float x = (float)(K.key[i] & 0xFFF);
-            int r = (int)__fdiv_rn(x, lv.hX);
-            if (r >= nIni) { atomicOr(err, 1); r = nIni - 1; }
-            K.label[i] = (uint16_t)r;
-            atomicAdd(&cnt4[r], 1);
+        if (nIni <= 8) {  // a handful of roots (1 at 4:3, 3 at C4's 3.3:1): one LDS atomic per wave and root
+            for (int i0 = 0; i0 < n; i0 += NT) {
+                const int i = i0 + tid;
+                int r = -1;
+                if (i < n) {
+                    const float x = (float)(K.key[i] & 0xFFF);
+                    r = (int)__fdiv_rn(x, lv.hX);
+                    if (r >= nIni) { atomicOr(err, 1); r = nIni - 1; }
+                    K.label[i] = (uint16_t)r;
+                }
+                for (int q = 0; q < nIni; q++) {
+                    const unsigned long long m = __ballot(r == q);
+                    if ((tid & 63) == 0 && m) atomicAdd(&cnt4[q], (int)__popcll(m));
+                }
+            }
+        } else {
+            for (int i = tid; i < n; i += NT) {
+                const float x = (float)(K.key[i] & 0xFFF);
+                int r = (int)__fdiv_rn(x, lv.hX);
+                if (r >= nIni) { atomicOr(err, 1); r = nIni - 1; }
+                K.label[i] = (uint16_t)r;
+                atomicAdd(&cnt4[r], 1);
+            }
         }
         __syncthreads();
         int size = 0;
@@ -1118,7 +1129,7 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
             // children counts per processing position; prefix -> creation indices
             int TC = 0, jstar = nD - 1;
             {
-                int carry4 = 0, carryG = 0;
+                int carry4 = 0;
                 if (tid == 0) sh_jstar = nD - 1;
                 __syncthreads();
                 for (int j0 = 0; j0 < nD; j0 += NT) {
@@ -1130,8 +1141,7 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
                     }
                     int tot;
                     const int excl = block_scan_excl<NT / 64>(nc, &tot, red) + carry4;
-                    int tot2;
-                    const int excl2 = block_scan_excl<NT / 64>(nc - 1, &tot2, red) + carryG;
+                    const int excl2 = excl - j;  // sum of (children - 1) before position j (active j only)
                     if (j < nD) {
                         dbase[j] = excl;
                         if (phase == 2) {
@@ -1141,7 +1151,6 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
                         }
                     }
                     carry4 += tot;
-                    carryG += tot2;
                 }
                 __syncthreads();
                 jstar = sh_jstar;
