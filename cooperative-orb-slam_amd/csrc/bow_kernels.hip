@@ -77,11 +77,27 @@ __global__ __launch_bounds__(256) void k_voc_descend(VocDev v, int levelsup, con
 constexpr int kVocThreads = 1024;  // k_voc_bow: one compare-exchange per thread per bitonic stage at 2048 keys
 constexpr int kVocWaves = kVocThreads / 64;
 
-/* ascending bitonic sort of n2 (power of two) u64 keys in LDS by kVocThreads threads */
+/* LDS writes of this wave's lanes visible to its other lanes (no other wave involved) */
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* ascending bitonic sort of n2 (power of two) u64 keys in LDS by kVocThreads threads. A stage of stride < 64 pairs
+ * elements of one 128-element block, and wave w owns the blocks w, w + kVocWaves, ... (pair t = the thread's
+ * index + k kVocThreads), so such a stage after another one only needs its own wave's writes: a workgroup barrier
+ * only before a stage of stride >= 64 and before the first stage after one (~20 instead of 55 barriers at 1024
+ * keys) */
 __device__ void lds_bitonic_u64(unsigned long long* a, int n2) {
     for (int size = 2; size <= n2; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            __syncthreads();
+            // the previous stage's stride: 2 stride inside a size, 1 (the last stage of the smaller size) at its start
+            const bool cross = stride >= 64 || (stride * 2 < size && stride * 2 >= 64) || size == 2;
+            if (cross)
+                __syncthreads();
+            else
+                wave_lds_sync();
             for (int t = threadIdx.x; t < n2 / 2; t += kVocThreads) {
                 const int lo = 2 * t - (t & (stride - 1));
                 const int hi = lo + stride;

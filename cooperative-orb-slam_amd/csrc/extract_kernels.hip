@@ -785,6 +785,21 @@ __device__ int block_scan_excl(int v, int* total, int* red) {
     return woff + inc - v;
 }
 
+/* how many of the first m LDS keys are above `key` (rank counting): 8 independent broadcast reads in flight per
+ * step -- one dependent read per key waited out the LDS latency m times */
+__device__ __forceinline__ int count_above(const unsigned long long* a, int m, unsigned long long key) {
+    int c = 0, t = 0;
+    for (; t + 8 <= m; t += 8) {
+        unsigned long long v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = a[t + k];
+#pragma unroll
+        for (int k = 0; k < 8; k++) c += v[k] > key ? 1 : 0;
+    }
+    for (; t < m; t++) c += a[t] > key ? 1 : 0;
+    return c;
+}
+
 template <int NW>
 __device__ __forceinline__ int block_sum(int v, int* red) {
     int tot;
@@ -990,12 +1005,14 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
         OCT_T(3);
         // --- 3. division rounds (ORBextractor.cc:594-739)
         bool cnt_clean = false;  // cnt4[0, 4 size) already zero (cleared by the previous fast round)
+        bool counted = false;    // this round's quadrant counts are in cntc already (the previous round's relabel)
+        int* cntc = cnt4;        // this round's counts (cnt4, or dflag..skey when a relabel pass counted there)
         int iters = 0;
         for (int iter = 0; iter < 100000; iter++) {
             if (iter < 30) OCT_T(4 + iter);
             iters = iter + 1;
             const int prevSize = size;
-            if (!cnt_clean) {
+            if (!cnt_clean && !counted) {
                 for (int s = tid; s < size; s += NT) {
                     cnt4[4 * s] = 0; cnt4[4 * s + 1] = 0; cnt4[4 * s + 2] = 0; cnt4[4 * s + 3] = 0;
                 }
@@ -1006,26 +1023,30 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
                 // Phase-1 round with every node in one thread (slot s = tid): every node with > 1 key divides,
                 // in list order, so one packed scan gives the children's creation indices, the survivors'
                 // positions and the number of children with > 1 key at once (4 barriers per round instead of
-                // ~20 for the general path below, which phase 2 and tables of > 256 nodes take).
-                for (int i = tid; i < n; i += NT) {
-                    const int s = K.label[i];
-                    if (A.nk[s] >= 2) {
-                        const uint32_t kk = K.key[i];
-                        const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF);
-                        const int hx = (A.x1[s] - A.x0[s] + 1) >> 1, hy = (A.y1[s] - A.y0[s] + 1) >> 1;
-                        const int q = (x >= A.x0[s] + hx ? 1 : 0) + (y >= A.y0[s] + hy ? 2 : 0);
-                        K.quad[i] = (uint8_t)q;
-                        atomicAdd(&cnt4[4 * s + q], 1);
+                // ~20 for the general path below, which phase 2 and tables of > 256 nodes take). When the next
+                // round is one of these too, this round's relabel pass also counts the keys' quadrants in the new
+                // table (into the other counts buffer), so that round has no count pass of its own.
+                if (!counted) {
+                    for (int i = tid; i < n; i += NT) {
+                        const int s = K.label[i];
+                        if (A.nk[s] >= 2) {
+                            const uint32_t kk = K.key[i];
+                            const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF);
+                            const int hx = (A.x1[s] - A.x0[s] + 1) >> 1, hy = (A.y1[s] - A.y0[s] + 1) >> 1;
+                            const int q = (x >= A.x0[s] + hx ? 1 : 0) + (y >= A.y0[s] + hy ? 2 : 0);
+                            K.quad[i] = (uint8_t)q;
+                            atomicAdd(&cntc[4 * s + q], 1);
+                        }
                     }
+                    __syncthreads();
                 }
-                __syncthreads();
                 const int s = tid;
                 const bool live = s < size;
                 const bool isD = live && A.nk[s] >= 2;
                 int c4[4] = {0, 0, 0, 0};
                 if (isD) {
 #pragma unroll
-                    for (int q = 0; q < 4; q++) c4[q] = cnt4[4 * s + q];
+                    for (int q = 0; q < 4; q++) c4[q] = cntc[4 * s + q];
                 }
                 const int nc = (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0);
                 const int ne = (c4[0] > 1) + (c4[1] > 1) + (c4[2] > 1) + (c4[3] > 1);
@@ -1065,6 +1086,141 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
                     Bt.nk[np] = A.nk[s]; Bt.seq[np] = A.seq[s];
                     spos[s] = np;
                 }
+                // the next round is a phase-1 round of this form: count its quadrants in the relabel pass below, into
+                // the buffer this round did not use (cnt4, or the phase-2 arrays dflag..skey, idle in phase 1)
+                const bool fuse = !(newSize >= N || newSize == prevSize) && !(newSize + nToExpand * 3 > N) &&
+                                  newSize <= 256;
+                int* cntn = cntc == cnt4 ? dflag : cnt4;
+                if (fuse)
+                    for (int i = tid; i < 4 * newSize; i += NT) cntn[i] = 0;
+                __syncthreads();
+                for (int i = tid; i < n; i += NT) {
+                    const int s2 = K.label[i];
+                    const int np0 = spos[s2];
+                    const int np = np0 >= 0 ? np0 : cpos[4 * s2 + K.quad[i]];
+                    K.label[i] = (uint16_t)np;
+                    if (fuse && Bt.nk[np] >= 2) {
+                        const uint32_t kk = K.key[i];
+                        const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF);
+                        const int hx = (Bt.x1[np] - Bt.x0[np] + 1) >> 1, hy = (Bt.y1[np] - Bt.y0[np] + 1) >> 1;
+                        const int q = (x >= Bt.x0[np] + hx ? 1 : 0) + (y >= Bt.y0[np] + hy ? 2 : 0);
+                        K.quad[i] = (uint8_t)q;
+                        atomicAdd(&cntn[4 * np + q], 1);
+                    }
+                }
+                if (!fuse)
+                    for (int i = tid; i < 4 * newSize; i += NT) cnt4[i] = 0;  // for the next round's count pass
+                __syncthreads();
+                cnt_clean = !fuse;
+                counted = fuse;
+                cntc = fuse ? cntn : cnt4;
+                { NodeT t = A; A = Bt; Bt = t; }
+                next_seq += (uint32_t)TC;
+                size = newSize;
+                if (size >= N || size == prevSize) break;
+                if (size + nToExpand * 3 > N) phase = 2;
+                continue;
+            }
+            if (phase == 2 && size <= NT) {
+                // Phase-2 round with every node in one thread (slot s = tid): the divisible nodes' processing order
+                // is their rank by (size, creation) descending (rank counting over the LDS keys), one scan in that
+                // order finds the first division reaching N and the children's creation indices, one packed scan in
+                // list order gives the survivors' positions and the children with > 1 key: 11 barriers per round
+                // instead of the general path's ~20 (the same table, the same order).
+                for (int i = tid; i < n; i += NT) {
+                    const int s = K.label[i];
+                    if (A.nk[s] >= 2) {
+                        const uint32_t kk = K.key[i];
+                        const int x = (int)(kk & 0xFFF), y = (int)((kk >> 12) & 0xFFF);
+                        const int hx = (A.x1[s] - A.x0[s] + 1) >> 1, hy = (A.y1[s] - A.y0[s] + 1) >> 1;
+                        const int q = (x >= A.x0[s] + hx ? 1 : 0) + (y >= A.y0[s] + hy ? 2 : 0);
+                        K.quad[i] = (uint8_t)q;
+                        atomicAdd(&cnt4[4 * s + q], 1);
+                    }
+                }
+                __syncthreads();
+                const int s = tid;
+                const bool live = s < size;
+                const bool isD = live && A.nk[s] >= 2;
+                int nc = 0, ne = 0;
+                if (isD) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int cq = cnt4[4 * s + q];
+                        nc += cq > 0;
+                        ne += cq > 1;
+                    }
+                }
+                const unsigned long long key = isD ? ((unsigned long long)(uint32_t)A.nk[s] << 32) | A.seq[s] : 0ull;
+                if (live) skey[s] = key;  // 0 for a node that does not divide: below every divisible key
+                if (tid == 0) sh_tc = -1;
+                int nD;
+                block_scan_excl<NT / 64>(isD ? 1 : 0, &nD, red);  // (its barriers publish skey / sh_tc)
+                if (nD == 0) break;  // cannot happen while size changes, kept for safety
+                int rank = 0;
+                if (isD)
+                    rank = count_above(skey, size, key);
+                if (isD) {
+                    dflag[rank] = s;
+                    dbase[rank] = nc;
+                }
+                if (tid == 0) sh_jstar = nD - 1;
+                __syncthreads();
+                // processing position r = tid: children before it and the first division that reaches N
+                const int r = tid;
+                const int ncr = r < nD ? dbase[r] : 0;
+                int TCall;
+                const int exr = block_scan_excl<NT / 64>(ncr, &TCall, red);
+                if (r < nD) {
+                    const int before = prevSize + exr - r, after = before + ncr - 1;
+                    if (after >= N && before < N) {  // first crossing (unique)
+                        sh_jstar = r;
+                        sh_tc = exr + ncr;
+                    }
+                }
+                __syncthreads();
+                const int jstar = sh_jstar;
+                const int TC = sh_tc >= 0 ? sh_tc : TCall;
+                // survivors in list order + children with > 1 key of the divided nodes, one packed scan
+                const bool divided = isD && rank <= jstar;
+                const bool sv = live && !divided;
+                int tot;
+                const int ex = block_scan_excl<NT / 64>((sv ? 1 : 0) | ((divided ? ne : 0) << 16), &tot, red);
+                const int nsurv = tot & 0xFFFF, nToExpand = tot >> 16;
+                const int newSize = TC + nsurv;
+                if (newSize > NC) {
+                    if (tid == 0) { atomicOr(err, 4); lvcnt[f * ep.L + l] = 0; }
+                    return;
+                }
+                if (sv) {
+                    const int np = TC + (ex & 0xFFFF);
+                    Bt.x0[np] = A.x0[s]; Bt.y0[np] = A.y0[s]; Bt.x1[np] = A.x1[s]; Bt.y1[np] = A.y1[s];
+                    Bt.nk[np] = A.nk[s]; Bt.seq[np] = A.seq[s];
+                    spos[s] = np;
+                } else if (divided) {
+                    spos[s] = -1;
+                }
+                if (r <= jstar) {  // the node at processing position r divides: its children pushed to the front
+                    const int d = dflag[r];
+                    const int x0 = A.x0[d], y0 = A.y0[d], x1 = A.x1[d], y1 = A.y1[d];
+                    const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;
+                    int ci = exr;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int cn = cnt4[4 * d + q];
+                        if (cn > 0) {
+                            const int np = TC - 1 - ci;
+                            Bt.x0[np] = (q & 1) ? x0 + hx : x0;
+                            Bt.x1[np] = (q & 1) ? x1 : x0 + hx;
+                            Bt.y0[np] = (q & 2) ? y0 + hy : y0;
+                            Bt.y1[np] = (q & 2) ? y1 : y0 + hy;
+                            Bt.nk[np] = cn;
+                            Bt.seq[np] = next_seq + (uint32_t)ci;
+                            cpos[4 * d + q] = (uint16_t)np;
+                            ci++;
+                        }
+                    }
+                }
                 __syncthreads();
                 for (int i = tid; i < n; i += NT) {
                     const int s2 = K.label[i];
@@ -1077,8 +1233,8 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
                 { NodeT t = A; A = Bt; Bt = t; }
                 next_seq += (uint32_t)TC;
                 size = newSize;
+                (void)nToExpand;
                 if (size >= N || size == prevSize) break;
-                if (size + nToExpand * 3 > N) phase = 2;
                 continue;
             }
             for (int i = tid; i < n; i += NT) {
@@ -1118,8 +1274,7 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
                 // instead of a bitonic network's log2(P)(log2(P)+1)/2 barriers
                 for (int j = tid; j < nD; j += NT) {
                     const unsigned long long key = skey[j];
-                    int rank = 0;
-                    for (int i = 0; i < nD; i++) rank += skey[i] > key ? 1 : 0;
+                    const int rank = count_above(skey, nD, key);
                     dbase[rank] = dflag[j];
                 }
                 __syncthreads();
