@@ -141,6 +141,13 @@ __device__ int lds_segments(const unsigned long long* a, int n, int* s_start, in
     return carry;
 }
 
+#ifdef ORBX_BOW_TRACE
+__device__ unsigned long long g_bow_trace[16];
+#define BOW_T(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_bow_trace[(k)] = wall_clock64(); } while (0)
+#else
+#define BOW_T(k) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(kVocThreads) void k_voc_bow(VocDev v, const int32_t* __restrict__ counts, int stride,
                                                  const int32_t* __restrict__ word, const double* __restrict__ weight,
                                                  const uint32_t* __restrict__ nid, uint32_t* __restrict__ bow_word,
@@ -156,10 +163,13 @@ __global__ __launch_bounds__(kVocThreads) void k_voc_bow(VocDev v, const int32_t
     const long long fb = (long long)f * stride;
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
+    BOW_T(0);
     // ---- FeatureVector: stable by (node id, feature index); stopped features (weight <= 0) sort last
     for (int i = tid; i < n2; i += kVocThreads)
         s_key[i] = i < n && weight[fb + i] > 0 ? ((unsigned long long)nid[fb + i] << 32) | (unsigned)i : ~0ull;
+    BOW_T(1);
     lds_bitonic_u64(s_key, n2);
+    BOW_T(2);
     int kept = 0;
     for (int i = tid; i < n; i += kVocThreads) kept += s_key[i] != ~0ull;
     for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
@@ -180,53 +190,72 @@ __global__ __launch_bounds__(kVocThreads) void k_voc_bow(VocDev v, const int32_t
         nfv[f] = nseg;
     }
     __syncthreads();
+    BOW_T(3);
     // ---- BowVector: stable by (word id, feature index)
     for (int i = tid; i < n2; i += kVocThreads)
         s_key[i] = i < n && weight[fb + i] > 0 ? ((unsigned long long)(uint32_t)word[fb + i] << 32) | (unsigned)i : ~0ull;
+    BOW_T(4);
     lds_bitonic_u64(s_key, n2);
+    BOW_T(5);
     const int nw = lds_segments(s_key, m, s_start, s_tmp);
     if (tid == 0) s_start[nw] = m;
     __syncthreads();
     const bool add = v.weighting == 0 || v.weighting == 1;  // TF_IDF / TF: addWeight; IDF / BINARY: addIfNotExist
     const bool must = v.scoring != 5;                       // every scoring but DOT_PRODUCT normalises
-    for (int s = tid; s < nw; s += kVocThreads) {
-        const int b = s_start[s], e = s_start[s + 1];
-        double val = weight[fb + (int)(s_key[b] & 0xffffffffu)];
-        if (add)
-            for (int i = b + 1; i < e; i++) val += weight[fb + (int)(s_key[i] & 0xffffffffu)];
-        if (add && !must) val /= (double)nw;
-        bow_word[fb + s] = (uint32_t)(s_key[b] >> 32);
-        bow_value[fb + s] = val;
+    constexpr int kPer = kVocMaxFeatures / kVocThreads;  // words per thread (word s = tid + k kVocThreads)
+    double vals[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const int s = tid + k * kVocThreads;
+        vals[k] = 0.0;
+        if (s < nw) {
+            const int b = s_start[s], e = s_start[s + 1];
+            double val = weight[fb + (int)(s_key[b] & 0xffffffffu)];
+            if (add)
+                for (int i = b + 1; i < e; i++) val += weight[fb + (int)(s_key[i] & 0xffffffffu)];
+            if (add && !must) val /= (double)nw;
+            bow_word[fb + s] = (uint32_t)(s_key[b] >> 32);
+            vals[k] = val;
+            if (!must) bow_value[fb + s] = val;
+        }
     }
-    __threadfence_block();
-    __syncthreads();
+    BOW_T(6);
     if (must) {
-        if (tid < 64) {  // BowVector::normalize: sum in ascending word order, as the map iteration. Wave 0 loads
-                         // 64 words per coalesced read and lane-broadcasts them into one in-order f64 chain
-                         // (uncontracted, as the oracle's -ffp-contract=off build) -- not one load per add
+        // BowVector::normalize: the sum in ascending word order, as the map iteration, one in-order f64 chain
+        // (uncontracted, as the oracle's -ffp-contract=off build) by one lane over the values staged in LDS (the
+        // sorted keys' space, read above), eight loads in flight ahead of the adds
+        __syncthreads();
+        double* s_val = (double*)s_key;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int s = tid + k * kVocThreads;
+            if (s < nw) s_val[s] = vals[k];
+        }
+        __syncthreads();
+        if (tid == 0) {
             const bool l2 = v.scoring == 1;
             double norm = 0.0;
-            for (int base = 0; base < nw; base += 64) {
-                const int s = base + tid;
-                const double x = s < nw ? bow_value[fb + s] : 0.0;
-                const double t = l2 ? __dmul_rn(x, x) : fabs(x);
-                const int cnt = min(64, nw - base);
-                const unsigned long long tb = (unsigned long long)__double_as_longlong(t);
-                const int lo = (int)(uint32_t)tb, hi = (int)(uint32_t)(tb >> 32);
-                for (int j = 0; j < cnt; j++) {
-                    const unsigned long long u = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(hi, j) << 32) |
-                                                 (uint32_t)__builtin_amdgcn_readlane(lo, j);
-                    norm = __dadd_rn(norm, __longlong_as_double((long long)u));
-                }
+            int s = 0;
+            for (; s + 8 <= nw; s += 8) {
+                double t[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) t[k] = s_val[s + k];
+#pragma unroll
+                for (int k = 0; k < 8; k++) norm = __dadd_rn(norm, l2 ? __dmul_rn(t[k], t[k]) : fabs(t[k]));
             }
-            if (tid == 0) s_norm = l2 ? sqrt(norm) : norm;
+            for (; s < nw; s++) norm = __dadd_rn(norm, l2 ? __dmul_rn(s_val[s], s_val[s]) : fabs(s_val[s]));
+            s_norm = l2 ? sqrt(norm) : norm;
         }
         __syncthreads();
         const double norm = s_norm;
-        if (norm > 0.0)
-            for (int s = tid; s < nw; s += kVocThreads) bow_value[fb + s] = bow_value[fb + s] / norm;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int s = tid + k * kVocThreads;
+            if (s < nw) bow_value[fb + s] = norm > 0.0 ? vals[k] / norm : vals[k];
+        }
     }
     if (tid == 0) nbow[f] = nw;
+    BOW_T(7);
 }
 
 hipError_t launch_voc_transform(const VocDev& v, int levelsup, int nframes, const uint8_t* desc, const int32_t* counts,
@@ -243,3 +272,9 @@ hipError_t launch_voc_transform(const VocDev& v, int levelsup, int nframes, cons
 }
 
 }  // namespace orbamd
+
+#ifdef ORBX_BOW_TRACE
+extern "C" int orbx_debug_bow_trace(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbamd::g_bow_trace), sizeof(orbamd::g_bow_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
