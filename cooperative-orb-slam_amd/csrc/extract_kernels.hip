@@ -1019,7 +1019,9 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
                 __syncthreads();
             }
             cnt_clean = false;
-            if (phase == 1 && size <= 256) {
+            // node-per-thread rounds: slot s = tid (size <= NT), and the packed scan's survivor field holds 9 bits
+            constexpr int kFast1 = NT < 512 ? NT : 511;
+            if (phase == 1 && size <= kFast1) {
                 // Phase-1 round with every node in one thread (slot s = tid): every node with > 1 key divides,
                 // in list order, so one packed scan gives the children's creation indices, the survivors'
                 // positions and the number of children with > 1 key at once (4 barriers per round instead of
@@ -1089,7 +1091,7 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
                 // the next round is a phase-1 round of this form: count its quadrants in the relabel pass below, into
                 // the buffer this round did not use (cnt4, or the phase-2 arrays dflag..skey, idle in phase 1)
                 const bool fuse = !(newSize >= N || newSize == prevSize) && !(newSize + nToExpand * 3 > N) &&
-                                  newSize <= 256;
+                                  newSize <= kFast1;
                 int* cntn = cntc == cnt4 ? dflag : cnt4;
                 if (fuse)
                     for (int i = tid; i < 4 * newSize; i += NT) cntn[i] = 0;
@@ -1873,8 +1875,9 @@ hipError_t launch_sincos_selftest(const float* in, float* so, float* co, int n, 
 }
 
 hipError_t octree_setup(int lds_bytes) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_octree<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             lds_bytes);
+    hipError_t e = hipFuncSetAttribute((const void*)k_octree<256>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void*)k_octree<512>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
     if (e != hipSuccess) return e;
     return hipFuncSetAttribute((const void*)k_octree<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
@@ -1890,6 +1893,9 @@ hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const
     // each round's keys in a quarter of the iterations; batches pack four 256-thread workgroups per CU instead
     if (nframes < kPyrFramesMinBatch)
         hipLaunchKernelGGL(k_octree<1024>, grid, dim3(1024), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey,
+                           lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err);
+    else if (NC > 256)  // levels of up to 512 live nodes (C4's 2000 features): every round node-per-thread
+        hipLaunchKernelGGL(k_octree<512>, grid, dim3(512), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey,
                            lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err);
     else
         hipLaunchKernelGGL(k_octree<256>, grid, dim3(256), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey,
