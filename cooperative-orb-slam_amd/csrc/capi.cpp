@@ -359,17 +359,17 @@ struct Geometry {
         nbjobs_small = bjob_small[L];
         pyr_rows = 1;
         for (int l = 1; l < L; l++) pyr_rows = std::max(pyr_rows, lv[l].h);
-        // row bands of the small-batch pyramid (kPyrBands): band b owns rows [b h / B, (b + 1) h / B) of every
-        // level and also makes the rows its own higher levels read (the (r0, r1) of k_pyramid_frames' row
-        // table), so each workgroup only reads back rows it wrote itself
-        band_off = (int)ptab.size();
-        if (frames_ok) {
-            std::vector<int> bt(2 * kPyrBands * kMaxLevels, 0);
-            for (int b = 0; b < kPyrBands; b++) {
+        // row bands of the banded pyramid: band b of B owns rows [b h / B, (b + 1) h / B) of every level and also
+        // makes the rows its own higher levels read (the (r0, r1) of k_pyramid_frames' row table), so each
+        // workgroup only reads back rows it wrote itself
+        auto band_table = [&](int B) {
+            const int off = (int)ptab.size();
+            std::vector<int> bt(2 * B * kMaxLevels, 0);
+            for (int b = 0; b < B; b++) {
                 int nlo = 0, nhi = 0;  // rows of level l that level l + 1's range reads ([nlo, nhi), empty at the top)
                 for (int l = L - 1; l >= 1; l--) {
                     const int h = lv[l].h;
-                    int lo = (int)((long long)b * h / kPyrBands), hi = (int)((long long)(b + 1) * h / kPyrBands);
+                    int lo = (int)((long long)b * h / B), hi = (int)((long long)(b + 1) * h / B);
                     if (nhi > nlo) {
                         lo = hi > lo ? std::min(lo, nlo) : nlo;
                         hi = std::max(hi, nhi);
@@ -385,7 +385,9 @@ struct Geometry {
                 }
             }
             ptab.insert(ptab.end(), bt.begin(), bt.end());
-        }
+            return off;
+        };
+        band_off = frames_ok ? band_table(kPyrBands) : 0;
         // octree LDS: node arrays (92 B/node, NC pow2) + keys (7 B/key)
         NC = 1;
         while (NC < maxnode) NC <<= 1;
@@ -512,7 +514,8 @@ static int launch_pyramid(orbx_handle* h, const ExtractParams& ep, const uint8_t
         const bool banded = nframes < kPyrFramesMinBatch;
         HIPR(launch_pyramid_frames(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, g.d_lv.as<LevelDesc>(),
                                    g.d_ptab.as<int>(), g.pyr_rows, max_groups, nframes, st,
-                                   banded ? (const int2*)(g.d_ptab.as<int>() + g.band_off) : nullptr));
+                                   banded ? (const int2*)(g.d_ptab.as<int>() + g.band_off) : nullptr,
+                                   banded ? kPyrBands : 0));
         return 0;
     }
     for (int l = 1; l < ep.L; l++) {

@@ -1763,11 +1763,12 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
                                  const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int max_rows,
-                                 int max_groups, int nframes, hipStream_t st, const int2* bands) {
+                                 int max_groups, int nframes, hipStream_t st, const int2* bands, int nbands) {
     if (max_rows < 1 || max_rows > kPyrMaxRows) return hipErrorInvalidValue;
     const size_t lds = (size_t)max_rows * sizeof(int4);
-    if (bands) {  // row bands of a few frames: 1024 threads, so a band's rows of a level are one or two passes
-        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), dim3(kPyrBands, nframes), dim3(kPyrThreadsMax),
+    if (bands) {  // row bands: 1024 threads, so a band's rows of a level are one or two passes
+        if (nbands < 1) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), dim3(nbands, nframes), dim3(kPyrThreadsMax),
                            lds, st, frames, fstride, pitch0, pyr, ep, levels, ptab, bands);
         return hipGetLastError();
     }

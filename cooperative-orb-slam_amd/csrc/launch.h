@@ -17,7 +17,7 @@ hipError_t launch_resize(const uint8_t* src, long long src_fstride, int src_pitc
 hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int pitch0, uint8_t* pyr,
                                  const ExtractParams& ep, const LevelDesc* levels, const int* ptab, int max_rows,
                                  int max_groups, int nframes, hipStream_t st,
-                                 const int2* bands = nullptr);
+                                 const int2* bands = nullptr, int nbands = 0);
 hipError_t launch_resize_tiled(const uint8_t* src, long long src_fstride, int src_pitch, int sw, int sh, uint8_t* dst,
                                long long dst_fstride, int dst_pitch, int dw, int dh, const int* coef, int xmax,
                                int simd_end, int nframes, hipStream_t st);

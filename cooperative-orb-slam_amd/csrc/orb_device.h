@@ -41,7 +41,7 @@ constexpr int kPyrFramesMinBatch = 64;  // batches below this build the pyramid 
 // small batches: k_pyramid_frames over kPyrBands row bands per frame, each band's workgroup computing every level's
 // rows its band owns plus the rows its higher levels read (the band's dependency cone; overlapping rows are
 // written by two workgroups with the same bytes): one launch instead of a dependent launch per level
-constexpr int kPyrBands = 32;
+constexpr int kPyrBands = 32;  // (batches in 2-8 bands measured slower in the overlapped schedule: whole frames)
 constexpr int kRsTileW = 64, kRsTileH = 32;  // k_resize_tiled output tile
 
 struct LevelDesc {
