@@ -10,7 +10,7 @@
  *                  node without children (Node::isLeaf) and records the word id, its weight and
  *                  the node at level L - levelsup (the FeatureVector key). The children's descriptors
  *                  and records sit in child-slot order, so a level is one round of independent loads.
- *   k_voc_bow      one workgroup per frame: stable LDS bitonic sorts of (node, feature) and (word,
+ *   k_voc_bow      one workgroup per frame: stable bitonic sorts (registers + LDS) of (node, feature) and (word,
  *                  feature) keys build FeatureVector::addFeature's map (ascending node id, ascending
  *                  feature per node) and BowVector's map; a word's weights are added in feature
  *                  order (addWeight) or the first kept (addIfNotExist), the TF division by the word
@@ -77,27 +77,51 @@ __global__ __launch_bounds__(256) void k_voc_descend(VocDev v, int levelsup, con
 constexpr int kVocThreads = 1024;  // k_voc_bow: one compare-exchange per thread per bitonic stage at 2048 keys
 constexpr int kVocWaves = kVocThreads / 64;
 
-/* LDS writes of this wave's lanes visible to its other lanes (no other wave involved) */
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long x, int m) {
+    const int lo = __shfl_xor((int)(uint32_t)x, m), hi = __shfl_xor((int)(uint32_t)(x >> 32), m);
+    return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-/* ascending bitonic sort of n2 (power of two) u64 keys in LDS by kVocThreads threads. A stage of stride < 64 pairs
- * elements of one 128-element block, and wave w owns the blocks w, w + kVocWaves, ... (pair t = the thread's
- * index + k kVocThreads), so such a stage after another one only needs its own wave's writes: a workgroup barrier
- * only before a stage of stride >= 64 and before the first stage after one (~20 instead of 55 barriers at 1024
- * keys) */
+/* the bitonic stages of strides 64 .. 1 of sorting size `size` over a 128-key block held in registers: key g0 =
+ * base + lane in x0, g0 + 64 in x1 (stride 64 pairs a lane's own two keys, the smaller strides the lanes lane ^ s) */
+__device__ __forceinline__ void reg_bitonic_tail(unsigned long long& x0, unsigned long long& x1, int base, int size,
+                                                 int top) {
+    const int lane = threadIdx.x & 63, g0 = base + lane, g1 = g0 + 64;
+    if (top >= 64) {
+        const bool up = (g0 & size) == 0;  // g0 and g1 share the bit for size >= 128
+        const unsigned long long lo = x0 < x1 ? x0 : x1, hi = x0 < x1 ? x1 : x0;
+        x0 = up ? lo : hi;
+        x1 = up ? hi : lo;
+    }
+    for (int st = (top < 32 ? top : 32); st > 0; st >>= 1) {
+        const bool lower = (lane & st) == 0;
+        const unsigned long long y0 = shfl_xor_u64(x0, st), y1 = shfl_xor_u64(x1, st);
+        const bool up0 = (g0 & size) == 0, up1 = (g1 & size) == 0;
+        const unsigned long long mn0 = x0 < y0 ? x0 : y0, mx0 = x0 < y0 ? y0 : x0;
+        const unsigned long long mn1 = x1 < y1 ? x1 : y1, mx1 = x1 < y1 ? y1 : x1;
+        x0 = (lower == up0) ? mn0 : mx0;
+        x1 = (lower == up1) ? mn1 : mx1;
+    }
+}
+
+/* ascending bitonic sort of n2 (power of two, >= 128) u64 keys in LDS by kVocThreads threads. Every stage of stride
+ * <= 64 stays inside a 128-key block, which one wave holds in registers (two keys per lane): sizes 2..128 run there
+ * from one load, and after the LDS stages of stride >= 128 of every larger size, its strides 64..1 run there too
+ * (log2(n2/128) + 1 register passes and (log2(n2/128)) (log2(n2/128) + 1) / 2 LDS stages, the only workgroup
+ * barriers; 55 LDS stages at 1024 keys before) */
 __device__ void lds_bitonic_u64(unsigned long long* a, int n2) {
-    for (int size = 2; size <= n2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            // the previous stage's stride: 2 stride inside a size, 1 (the last stage of the smaller size) at its start
-            const bool cross = stride >= 64 || (stride * 2 < size && stride * 2 >= 64) || size == 2;
-            if (cross)
-                __syncthreads();
-            else
-                wave_lds_sync();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int nb = n2 >> 7;
+    __syncthreads();  // the keys written by every thread
+    for (int b = wv; b < nb; b += kVocWaves) {
+        unsigned long long x0 = a[b * 128 + lane], x1 = a[b * 128 + 64 + lane];
+        for (int size = 2; size <= 128; size <<= 1) reg_bitonic_tail(x0, x1, b * 128, size, size >> 1);
+        a[b * 128 + lane] = x0;
+        a[b * 128 + 64 + lane] = x1;
+    }
+    for (int size = 256; size <= n2; size <<= 1) {
+        for (int stride = size >> 1; stride >= 128; stride >>= 1) {
+            __syncthreads();
             for (int t = threadIdx.x; t < n2 / 2; t += kVocThreads) {
                 const int lo = 2 * t - (t & (stride - 1));
                 const int hi = lo + stride;
@@ -108,6 +132,13 @@ __device__ void lds_bitonic_u64(unsigned long long* a, int n2) {
                     a[hi] = x;
                 }
             }
+        }
+        __syncthreads();
+        for (int b = wv; b < nb; b += kVocWaves) {
+            unsigned long long x0 = a[b * 128 + lane], x1 = a[b * 128 + 64 + lane];
+            reg_bitonic_tail(x0, x1, b * 128, size, 64);
+            a[b * 128 + lane] = x0;
+            a[b * 128 + 64 + lane] = x1;
         }
     }
     __syncthreads();
@@ -141,6 +172,34 @@ __device__ int lds_segments(const unsigned long long* a, int n, int* s_start, in
     return carry;
 }
 
+/* BowVector::normalize's sum over n values in LDS, in order, one f64 add after another (uncontracted, as the oracle's
+ * -ffp-contract=off build): L2 the squares, L1 the magnitudes. One lane; the next 8 values are loaded while the
+ * current 8 are added, so the chain waits on the adds alone (16 in flight measured slower in the schedule: the
+ * kernel's 84 VGPRs against 54 make its 1024-thread workgroup harder to place beside the other graphs' kernels) */
+template <bool L2>
+__device__ double norm_chain(const double* __restrict__ s_val, int n) {
+    constexpr int kQ = 8;
+    double norm = 0.0;
+    const int nfull = n & ~(kQ - 1);
+    double t[kQ];
+    if (nfull) {
+#pragma unroll
+        for (int k = 0; k < kQ; k++) t[k] = s_val[k];
+    }
+    for (int s = 0; s < nfull; s += kQ) {
+        const int nx = s + kQ < nfull ? s + kQ : s;  // the last chunk re-reads itself
+        double u[kQ];
+#pragma unroll
+        for (int k = 0; k < kQ; k++) u[k] = s_val[nx + k];
+#pragma unroll
+        for (int k = 0; k < kQ; k++) norm = __dadd_rn(norm, L2 ? __dmul_rn(t[k], t[k]) : fabs(t[k]));
+#pragma unroll
+        for (int k = 0; k < kQ; k++) t[k] = u[k];
+    }
+    for (int s = nfull; s < n; s++) norm = __dadd_rn(norm, L2 ? __dmul_rn(s_val[s], s_val[s]) : fabs(s_val[s]));
+    return norm;
+}
+
 #ifdef ORBX_BOW_TRACE
 __device__ unsigned long long g_bow_trace[16];
 #define BOW_T(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_bow_trace[(k)] = wall_clock64(); } while (0)
@@ -161,7 +220,7 @@ __global__ __launch_bounds__(kVocThreads) void k_voc_bow(VocDev v, const int32_t
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = counts[f];
     const long long fb = (long long)f * stride;
-    int n2 = 1;
+    int n2 = 128;  // the sort's block: 128 keys (padding sorts last)
     while (n2 < n) n2 <<= 1;
     BOW_T(0);
     // ---- FeatureVector: stable by (node id, feature index); stopped features (weight <= 0) sort last
@@ -221,9 +280,8 @@ __global__ __launch_bounds__(kVocThreads) void k_voc_bow(VocDev v, const int32_t
     }
     BOW_T(6);
     if (must) {
-        // BowVector::normalize: the sum in ascending word order, as the map iteration, one in-order f64 chain
-        // (uncontracted, as the oracle's -ffp-contract=off build) by one lane over the values staged in LDS (the
-        // sorted keys' space, read above), eight loads in flight ahead of the adds
+        // BowVector::normalize: the sum in ascending word order, as the map iteration, by one lane over the values
+        // staged in LDS (the sorted keys' space, read above)
         __syncthreads();
         double* s_val = (double*)s_key;
 #pragma unroll
@@ -232,20 +290,7 @@ __global__ __launch_bounds__(kVocThreads) void k_voc_bow(VocDev v, const int32_t
             if (s < nw) s_val[s] = vals[k];
         }
         __syncthreads();
-        if (tid == 0) {
-            const bool l2 = v.scoring == 1;
-            double norm = 0.0;
-            int s = 0;
-            for (; s + 8 <= nw; s += 8) {
-                double t[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++) t[k] = s_val[s + k];
-#pragma unroll
-                for (int k = 0; k < 8; k++) norm = __dadd_rn(norm, l2 ? __dmul_rn(t[k], t[k]) : fabs(t[k]));
-            }
-            for (; s < nw; s++) norm = __dadd_rn(norm, l2 ? __dmul_rn(s_val[s], s_val[s]) : fabs(s_val[s]));
-            s_norm = l2 ? sqrt(norm) : norm;
-        }
+        if (tid == 0) s_norm = v.scoring == 1 ? sqrt(norm_chain<true>(s_val, nw)) : norm_chain<false>(s_val, nw);
         __syncthreads();
         const double norm = s_norm;
 #pragma unroll

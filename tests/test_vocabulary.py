@@ -152,3 +152,23 @@ def test_vocab_batch_device_matches_host():
         w2, wt2, nid2 = ov.descend(descs[b], 2)
         assert np.array_equal(word[b, :cnt[b]].cpu().numpy(), w2)
         assert np.array_equal(nid[b, :cnt[b]].cpu().numpy(), nid2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [VOCABS[0], VOCABS[2]])
+def test_vocab_transform_gpu_sort_sizes(cfg):
+    """k_voc_bow's sort blocks (128 keys in registers, LDS stages above): descriptor counts either side of every
+    block and register boundary up to the 4096 capacity, with repeated descriptors (equal words and nodes)"""
+    k, L, seed, ragged, scoring, weighting, levelsup = cfg
+    v = synth_vocabulary(k, L, seed, ragged=ragged)
+    ov = oracle_py.OracleVocabulary(k, L, scoring, weighting, *v[2:])
+    gv = orbamd.ORBVocabulary.from_arrays(k, L, scoring, weighting, *v[2:])
+    rng = np.random.default_rng(seed)
+    pool = rng.integers(0, 256, (5000, 32), dtype=np.uint8)
+    for n in (1, 2, 63, 64, 65, 127, 128, 129, 255, 256, 257, 1000, 1024, 1025, 2048, 2049, 4095, 4096):
+        d = pool[:n].copy() if n % 2 else pool[rng.integers(0, max(n // 3, 1), n)]
+        (bw, bv), fv = gv.transform(d, levelsup)
+        (bw2, bv2), fv2 = ov.transform(d, levelsup)
+        np.testing.assert_array_equal(bw, bw2, err_msg="n=%d" % n)
+        np.testing.assert_array_equal(bv.view(np.uint64), bv2.view(np.uint64), err_msg="n=%d" % n)
+        assert fv == fv2, n
