@@ -2735,7 +2735,11 @@ int orbm_compute_distinctive_descriptors(orbm_ctx* ctx, int npoints, const int32
 struct orbv_handle {
     int device = 0;
     int k = 0, L = 0, scoring = 0, weighting = 0, nnodes = 0, nwords = 0;
+    // the host transform's stream, created at its first call: the device paths run on the caller's stream, and one
+    // more HIP stream in the process costs the bench's four graph streams 3.7 % of their step rate even idle
+    // (profiles/r04_idle_stream_cost.log)
     hipStream_t stream = nullptr;
+    std::mutex mu;   // the host transform's stream and staging
     DevBuf nodes;    // child-slot descriptors | child-slot records (VocChild)
     DevBuf scratch;  // per-call staging
     VocDev v{};
@@ -2782,7 +2786,7 @@ int orbv_create(int k, int L, int scoring, int weighting, int nlines, const int3
     h->k = k, h->L = L, h->scoring = scoring, h->weighting = weighting, h->nnodes = n, h->nwords = nwords;
     Carve cv;
     const size_t o_d = cv.take(32 * (size_t)ns), o_r = cv.take(sizeof(VocChild) * (size_t)ns);
-    if (h->nodes.ensure(cv.off) || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (h->nodes.ensure(cv.off)) {
         orbv_destroy(h);
         return ORBX_EDEVICE;
     }
@@ -2886,6 +2890,8 @@ int orbv_transform(orbv_handle* h, const uint8_t* desc, int n, int levelsup, uin
     // TemplatedVocabulary::empty(): no nodes under the root
     if (n == 0 || h->nnodes <= 1) return 0;
     HIPR(hipSetDevice(h->device));
+    std::lock_guard<std::mutex> lock(h->mu);
+    if (!h->stream) HIPR(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     const size_t N = (size_t)n;
     Carve cv;
     const size_t o_desc = cv.take(32 * N), o_cnt = cv.take(4), o_word = cv.take(4 * N), o_w = cv.take(8 * N),
