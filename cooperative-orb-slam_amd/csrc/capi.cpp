@@ -1211,6 +1211,12 @@ int orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orb
 struct orbm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // the host calls' stream, created at the first one: the *_device paths run on the caller's stream, and an idle
+    // HIP stream costs the bench's graph streams their step rate (profiles/r04_idle_stream_cost.log)
+    hipStream_t s() {
+        if (!stream) (void)hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+        return stream;
+    }
     DevBuf scratch;
     DevBuf err;  // device error flag of the *_device calls that validate their input (orbm_check_error)
     std::vector<uint8_t> host;
@@ -1219,7 +1225,7 @@ struct orbm_ctx {
     size_t pinned_bytes = 0;
     uint8_t* ensure_pinned(size_t need) {
         if (need <= pinned_bytes) return (uint8_t*)pinned;
-        (void)hipStreamSynchronize(stream);  // the previous call may still be retiring (wait_call)
+        if (stream) (void)hipStreamSynchronize(stream);  // the previous call may still be retiring (wait_call)
         if (pinned) (void)hipHostFree(pinned);
         pinned = nullptr;
         pinned_dev = nullptr;
@@ -1417,10 +1423,6 @@ int orbm_create(int device, orbm_ctx** out) {
     HIPR(hipSetDevice(device));
     orbm_ctx* c = new orbm_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
-        return ORBX_EDEVICE;
-    }
     if (c->err.ensure(256) || hipMemset(c->err.p, 0, 256) != hipSuccess) {
         orbm_destroy(c);
         return ORBX_EDEVICE;
@@ -1554,7 +1556,7 @@ static int small_finish(orbm_ctx* ctx, const uint8_t* hp, size_t o_out, size_t o
     // polled in task order: a done word, then its accepts, each final once it carries this call's seq (the
     // kernel's stores are unordered: no fence)
     int next = 0, k = 0;
-    if (const int rc = wait_until(ctx->stream, [&] {
+    if (const int rc = wait_until(ctx->s(), [&] {
             for (; next < nt; next++, k = 0) {
                 const unsigned long long d = __atomic_load_n(done + next, __ATOMIC_ACQUIRE);
                 if ((uint32_t)d != seq) return false;
@@ -1627,7 +1629,7 @@ static int bow_small(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view* 
     // the polled words start at 0, which no call carries (seq >= 1): a word left by an earlier call on this
     // context (another layout, or the same bits by chance) can never read as this call's
     memset(hp + o_out, 0, cv.off - o_out);
-    HIPR(launch_bow_small(a, ctx->stream));
+    HIPR(launch_bow_small(a, ctx->s()));
     return small_finish(ctx, hp, o_out, o_done, a.tasks, nt, (uint32_t)a.seq, check_ori, out, nout, nmatches);
 }
 
@@ -1667,7 +1669,7 @@ static int tri_small(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view*
     a.c_ur = kf2->uright != nullptr;
     make_geom(a.g, F12, ex, ey, kf2->nlevels, kf2->scale_factors, kf2->level_sigma2);
     memset(hp + o_out, 0, cv.off - o_out);  // polled words: 0 is no call's seq (bow_small)
-    HIPR(launch_tri_small(a, ctx->stream));
+    HIPR(launch_tri_small(a, ctx->s()));
     return small_finish(ctx, hp, o_out, o_done, a.tasks, nt, (uint32_t)a.seq, check_ori, match12, kf1->n, nmatches);
 }
 
@@ -1714,14 +1716,14 @@ static int tri_common(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view
     memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
     int32_t* res = (int32_t*)(hp + o_res);
     std::fill(res, res + n1 + 1, -1);
-    HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, ctx->s()));
     MatchGeom g;
     make_geom(g, F12, ex, ey, kf2->nlevels, kf2->scale_factors, kf2->level_sigma2);
     const CallTail tail{ctx->call_state(), (int32_t*)(base + o_list), ctx->pinned_on_device(o_res), d1.angle, d2.angle,
                         n1, check_ori ? 1 : 0, 0};
     HIPR(launch_tri_nodes(d1, d2, (const NodeTask*)(base + o_tasks), (int)tasks.size(), g, only_stereo, tail,
-                          ctx->stream));
-    if (const int rc = wait_call(ctx->stream, res)) return rc;
+                          ctx->s()));
+    if (const int rc = wait_call(ctx->s(), res)) return rc;
     memcpy(match12, res + 1, 4 * (size_t)n1);
     if (nmatches) *nmatches = res[0];
     return 0;
@@ -1777,13 +1779,13 @@ static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view*
     memcpy(hp + o_tasks, tasks.data(), sizeof(NodeTask) * tasks.size());
     int32_t* res = (int32_t*)(hp + o_res);
     std::fill(res, res + nout + 1, -1);
-    HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIPR(hipMemcpyAsync(base, hp, in_bytes, hipMemcpyHostToDevice, ctx->s()));
     // mode 0: out indexed by the F idx, partner = KF idx -> rot = angKF[m] - angF[i] (swap)
     const CallTail tail{ctx->call_state(), (int32_t*)(base + o_list), ctx->pinned_on_device(o_res), dq.angle,
                         dc.angle, nout, check_ori ? 1 : 0, mode == 0 ? 1 : 0};
     HIPR(launch_bow(dq, dc, (const NodeTask*)(base + o_tasks), (int)tasks.size(), max_nc, nnratio, mode, tail,
-                    ctx->stream));
-    if (const int rc = wait_call(ctx->stream, res)) return rc;
+                    ctx->s()));
+    if (const int rc = wait_call(ctx->s(), res)) return rc;
     memcpy(out, res + 1, 4 * (size_t)nout);
     if (nmatches) *nmatches = res[0];
     return 0;
@@ -2188,7 +2190,7 @@ int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb,
     uint8_t* hp = ctx->ensure_pinned(in_bytes + 8 * n_host);
     if (!hp) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
-    hipStream_t st = ctx->stream;
+    hipStream_t st = ctx->s();
     ProjCall c;
     memset(&c, 0, sizeof(c));
     c.x = (const float*)(base + o_x);
@@ -2710,7 +2712,7 @@ int orbm_compute_distinctive_descriptors(orbm_ctx* ctx, int npoints, const int32
                  o_out = cv.take(32 * (size_t)npoints);
     if (ctx->scratch.ensure(cv.off)) return ORBX_EDEVICE;
     uint8_t* base = ctx->scratch.as<uint8_t>();
-    hipStream_t st = ctx->stream;
+    hipStream_t st = ctx->s();
     HIPR(hipMemcpyAsync(base + o_off, offsets, 4 * ((size_t)npoints + 1), hipMemcpyHostToDevice, st));
     if (nrows) HIPR(hipMemcpyAsync(base + o_desc, desc, 32 * nrows, hipMemcpyHostToDevice, st));
     HIPR(launch_distinctive(npoints, (const int32_t*)(base + o_off), base + o_desc, (int32_t*)(base + o_best),
@@ -3136,8 +3138,8 @@ int orbm_search_for_triangulation_cached(orbm_ctx* ctx, orbm_kf_cache* cache, ui
                                          int only_stereo, int check_ori, int32_t* match12, int* nmatches) {
     if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf1) || !view_ok(kf2) || !F12 || !match12)
         return ORBX_EARG;
-    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr, ctx->stream);
-    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr, ctx->stream) : nullptr;
+    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr, ctx->s());
+    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr, ctx->s()) : nullptr;
     if (!c1 || !c2) return ORBX_EDEVICE;
     return tri_common(ctx, kf1, kf2, F12, ex, ey, only_stereo, check_ori, match12, nmatches, c1.get(), c2.get());
 }
@@ -3147,8 +3149,8 @@ int orbm_search_by_bow_kf_kf_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_
                                     int32_t* match12, int* nmatches) {
     if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf1) || !view_ok(kf2) || !match12)
         return ORBX_EARG;
-    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr, ctx->stream);
-    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr, ctx->stream) : nullptr;
+    const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr, ctx->s());
+    const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr, ctx->s()) : nullptr;
     if (!c1 || !c2) return ORBX_EDEVICE;
     return bow_common(ctx, kf1, kf2, nnratio, check_ori, 1, match12, kf1->n, nmatches, c1.get(), c2.get());
 }
@@ -3157,7 +3159,7 @@ int orbm_search_by_bow_kf_f_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t
                                    const orbm_kf_view* f, float nnratio, int check_ori, int32_t* match_f,
                                    int* nmatches) {
     if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf) || !view_ok(f) || !match_f) return ORBX_EARG;
-    const std::shared_ptr<KfEntry> ck = cache_get(cache, 0, key, kf, nullptr, ctx->stream);
+    const std::shared_ptr<KfEntry> ck = cache_get(cache, 0, key, kf, nullptr, ctx->s());
     if (!ck) return ORBX_EDEVICE;
     return bow_common(ctx, kf, f, nnratio, check_ori, 0, match_f, f->n, nmatches, ck.get(), nullptr);
 }
@@ -3167,7 +3169,7 @@ int orbm_fuse_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key, const or
                      int32_t* best_idx, int* nfused) {
     if (!cache || !fuse_args_ok(ctx, KF, Tcw, Ow, mp, inv_level_sigma2, best_idx) || cache->device != ctx->device)
         return ORBX_EARG;
-    const std::shared_ptr<KfEntry> ck = cache_get(cache, 1, key, nullptr, KF, ctx->stream);
+    const std::shared_ptr<KfEntry> ck = cache_get(cache, 1, key, nullptr, KF, ctx->s());
     if (!ck) return ORBX_EDEVICE;
     return fuse_common(ctx, KF, Tcw, Ow, mp, th, inv_level_sigma2, best_idx, nfused, ck.get());
 }
