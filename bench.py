@@ -86,6 +86,39 @@ def algorithmic_bytes(W, H, nkp):
     return total, per_stage
 
 
+def describe_touched_bytes(sched, W, H, fused):
+    """describe's algorithmic HBM bytes per frame, from this run's keypoints (first / middle / last frame of every
+    graph in the last step): the union, per level, of the level pixels its patches read, each read once (patches of
+    neighbouring keypoints overlap; the overlap is an L2 hit, not HBM traffic), plus 56 B written per keypoint
+    (24 B keypoint + 32 B descriptor). Fused (k_describe_blur): the unblurred 43x43 window around each keypoint
+    (the blur's source rows and columns +-21, which contain IC_Angle's 31x31 window); separate blur: the unblurred
+    31x31 IC_Angle window plus the blurred 37x37 rBRIEF window."""
+    import numpy as np
+    ls = level_sizes(W, H)
+    scale = [np.float32(1.0)]
+    for _ in range(1, len(ls)):
+        scale.append(np.float32(np.float64(scale[-1]) * np.float64(np.float32(1.2))))
+    tot, nfr = 0.0, 0
+    for p in range(sched.P):
+        for b in sorted({0, sched.sub // 2, sched.sub - 1}):
+            k = sched.frame_results(p, b)[0]
+            nb = 56 * len(k)
+            for lv, (w, h) in enumerate(ls):
+                sel = k[k["octave"] == lv]
+                if not len(sel):
+                    continue
+                xs = np.rint(sel["x"] / scale[lv]).astype(np.int64)
+                ys = np.rint(sel["y"] / scale[lv]).astype(np.int64)
+                for r in ((21,) if fused else (15, 18)):
+                    m = np.zeros((h, w), bool)
+                    for x, y in zip(xs, ys):
+                        m[max(y - r, 0):y + r + 1, max(x - r, 0):x + r + 1] = True
+                    nb += int(m.sum())
+            tot += nb
+            nfr += 1
+    return tot / max(nfr, 1)
+
+
 def host_cpu_info():
     """nproc / affinity / cgroup quota / CPU model of the host this process runs on."""
     info = {"cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": None,
@@ -277,6 +310,11 @@ def main():
     ap.add_argument("--ingest-streams", type=int, default=4, help="copy streams of the ingest leg (<= --pipes)")
     ap.add_argument("--ingest-steps", type=int, default=100,
                     help="steps of the ingest leg (frames uploaded from pinned host memory each step; 0: skip)")
+    ap.add_argument("--scene", choices=("shared", "private"), default="shared",
+                    help="shared: every agent (rank) views one synthetic environment from its own crop offset "
+                         "(orbx_synth_scene_frames, 12 px per agent along the pan), so the cross-agent matchers find the "
+                         "other agents' features as A1 does on A2's keyframes; private: a texture per agent. Rank 0's "
+                         "frames are the same in both modes")
     ap.add_argument("--stagger", choices=("each", "once", "none", "every4", "every8", "every16", "pyr_each", "pyr_every8"),
                     default="every8",
                     help="graph p starts extracting after graph p-1's extraction: every step / only in the "
@@ -320,7 +358,8 @@ def main():
     assert B % P == 0, "--batch must be a multiple of --pipes"
     assert args.pool >= 1
     sub = B // P
-    frames_np = orbamd.synth_frames(rank, 0, args.pool * B, W, H)  # agent = rank; pool batches back to back
+    scene = 0 if args.scene == "shared" else None
+    frames_np = orbamd.synth_frames(rank, 0, args.pool * B, W, H, scene=scene)  # agent = rank; pool batches back to back
     def allgather(out, inp):
         # RCCL over xGMI; gloo (the one-GPU rehearsal): through host memory
         if backend == "nccl":
@@ -410,9 +449,13 @@ def main():
     _, stage_ms = run_profiled(0x1F, args.steps, False)
     # the roofline kernel: the extraction stage with the largest live time in this run's own stage split (every
     # stage bracketed by HIP events on the stream it runs on, same overlapped schedule); --roof-kernel overrides
-    dom = max(stages, key=lambda k: stage_ms[k]) if args.roof_kernel == "auto" else args.roof_kernel
-    # 2) timed region: only the dominant kernel bracketed (its live launch duration for the roofline)
-    el, dom_live = run_profiled(1 << stages.index(dom), args.steps, True)
+    ranked = sorted(stages, key=lambda k: -stage_ms[k])
+    dom = ranked[0] if args.roof_kernel == "auto" else args.roof_kernel
+    # a second stage within 5 % of the largest is priced beside it (`roofline.co_dominant`): the split's event pairs
+    # cannot rank two stages that close (round-4 review)
+    co = (ranked[1] if args.roof_kernel == "auto" and stage_ms[ranked[1]] >= 0.95 * stage_ms[dom] else None)
+    # 2) timed region: only the priced kernels bracketed (their live launch durations for the roofline)
+    el, dom_live = run_profiled((1 << stages.index(dom)) | ((1 << stages.index(co)) if co else 0), args.steps, True)
     last_batch, prev_batch = sched.last_batch, (sched.last_batch - 1) % args.pool
     if use_dist:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -426,7 +469,7 @@ def main():
     except RuntimeError as e:
         err_msg = str(e)
     check = None
-    agent_kf = lambda r, t: orbamd.synth_frames(r, t, 1, W, H)[0]  # noqa: E731 (agent r's keyframe image)
+    agent_kf = lambda r, t: orbamd.synth_frames(r, t, 1, W, H, scene=scene)[0]  # noqa: E731 (agent r's keyframe image)
     if not args.no_check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from check_schedule import check_schedule
@@ -490,38 +533,51 @@ def main():
     result = None
     if rank == 0:
         b_frame, per_stage = algorithmic_bytes(W, H, nkp)
-        dom_ms = dom_live[dom]
-        # one launch of the dominant kernel processes one graph's sub-batch (B / P frames)
-        hbm_gbs = per_stage[dom] * sub / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 and per_stage[dom] > 0 else 0.0
-        traffic = valu_insts = None
+        # describe's bytes from this run's keypoints: the union of the pixels its patches read (the blur folded into
+        # describe when no separate blur stage ran)
+        fused = stage_ms.get("blur", 0.0) == 0.0
+        per_stage["describe"] = describe_touched_bytes(sched, W, H, fused)
+        if fused:
+            per_stage["blur"] = 0
         # counter passes of this configuration (tools/prof_round.sh for c2, tools/pmc_config.sh for c3 / c4), taken
         # at 256 frames per launch
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if args.config == "c2" else
                                 "pmc_traffic_%s.json" % args.config)
+        pmc = {}
         if os.path.exists(pmc_path) and sub == 256:
             try:
-                rec = json.load(open(pmc_path)).get(dom, {})
-                traffic = rec.get("hbm_bytes_per_launch")
-                valu_insts = rec.get("valu_insts_per_launch")
+                pmc = json.load(open(pmc_path))
             except Exception:
-                traffic = valu_insts = None
-        valu_gs = valu_insts / (dom_ms * 1e-3) / 1e9 if valu_insts and dom_ms > 0 else None
-        hbm = {"achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": round(hbm_gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": per_stage[dom] * sub,
-               "measured_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
-               "frac_vs_copy": round(hbm_gbs / copy_gbs, 5) if copy_gbs else None}
+                pmc = {}
         sel = ("largest stage of this run's stage split (%s)" % ", ".join("%s %.3f ms" % (k, stage_ms[k]) for k in stages)
                if args.roof_kernel == "auto" else "--roof-kernel")
-        if valu_gs is not None and valu_gs / VALU_PEAK_GINST > hbm_gbs / HBM_PEAK_GBS:
-            # the byte/integer kernels are bound by vector-instruction issue, not HBM
-            roof = {"bound": "valu", "kernel": dom, "achieved": round(valu_gs, 1), "peak": VALU_PEAK_GINST,
-                    "unit": "G wave64 VALU instr/s", "frac": round(valu_gs / VALU_PEAK_GINST, 4),
-                    "traffic": traffic, "valu_insts_per_launch": valu_insts, "launch_ms": round(dom_ms, 4),
-                    "hbm": hbm, "selected_by": sel}
-        else:
-            roof = {"bound": "hbm", "kernel": dom, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": hbm["frac"], "traffic": traffic, "launch_ms": round(dom_ms, 4), "hbm": hbm,
-                    "selected_by": sel}
+
+        def price(kern):
+            """the kernel's roofline at its live launch duration in the timed region (one launch = one graph's
+            sub-batch of B / P frames): VALU issue from the counter pass, algorithmic bytes against HBM"""
+            k_ms = dom_live[kern]
+            hbm_gbs = per_stage[kern] * sub / (k_ms * 1e-3) / 1e9 if k_ms > 0 and per_stage[kern] > 0 else 0.0
+            rec = pmc.get(kern, {})
+            traffic, valu_insts = rec.get("hbm_bytes_per_launch"), rec.get("valu_insts_per_launch")
+            valu_gs = valu_insts / (k_ms * 1e-3) / 1e9 if valu_insts and k_ms > 0 else None
+            hbm = {"achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(hbm_gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": round(per_stage[kern] * sub),
+                   "measured_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
+                   "frac_vs_copy": round(hbm_gbs / copy_gbs, 5) if copy_gbs else None}
+            if valu_gs is not None and valu_gs / VALU_PEAK_GINST > hbm_gbs / HBM_PEAK_GBS:
+                # the byte/integer kernels are bound by vector-instruction issue, not HBM (DESIGN.md 6.0)
+                return {"bound": "valu", "kernel": kern, "achieved": round(valu_gs, 1), "peak": VALU_PEAK_GINST,
+                        "unit": "G wave64 VALU instr/s", "frac": round(valu_gs / VALU_PEAK_GINST, 4),
+                        "traffic": traffic, "valu_insts_per_launch": valu_insts, "launch_ms": round(k_ms, 4),
+                        "hbm": hbm}
+            return {"bound": "hbm", "kernel": kern, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm["frac"], "traffic": traffic, "launch_ms": round(k_ms, 4), "hbm": hbm}
+
+        roof = price(dom)
+        roof["selected_by"] = sel
+        roof["describe_form"] = "k_describe_blur (blur fused)" if fused else "k_blur_strips + k_describe"
+        if co:
+            roof["co_dominant"] = price(co)
         # the matcher on the matrix cores (fp4 +-1 operands, v_mfma_scale_f32_32x32x64_f8f6f4): algorithmic ops =
         # n1*n2 distances x 256 bits x 2 per pair
         m_ms = stage_ms.get("match", 0.0)
@@ -534,17 +590,11 @@ def main():
         # them; plus the whole step's VALU issue rate (every stage's VALU wave-instructions x P launches per step
         # / ms_per_step)
         stage_roof, step_valu = {}, 0.0
-        pmc = {}
-        if os.path.exists(pmc_path) and sub == 256:
-            try:
-                pmc = json.load(open(pmc_path))
-            except Exception:
-                pmc = {}
         for k in stages + ["match"]:
             ms = stage_ms.get(k, 0.0)
             rec = pmc.get(k, {})
             vi, hb = rec.get("valu_insts_per_launch"), rec.get("hbm_bytes_per_launch")
-            alg = per_stage.get(k, 0) * sub if k in per_stage else None
+            alg = round(per_stage.get(k, 0) * sub) if k in per_stage else None
             row = {"launch_ms": round(ms, 4), "valu_insts_per_launch": vi, "hbm_bytes_per_launch": hb}
             if ms > 0:
                 if vi:
@@ -580,7 +630,7 @@ def main():
                                                  "BoW + slot all-gather & cross-agent SearchForTriangulation and "
                                                  "SearchByBoW(KF,KF)",
                        "config": args.config, "frames_per_step_per_gpu": B, "graphs_per_gpu": P,
-                       "graph_stagger": args.stagger,
+                       "graph_stagger": args.stagger, "scene": args.scene,
                        "exchange_stream": "own" if async_x else "graph 0's",
                        "parallelism": "agent-per-gpu x%d" % world},
             "bit_exact": bool(ok_all) if check is not None else None,

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/orbslam_amd.h"
+#include "orbslam_amd_testing.h"
 #include "launch.h"
 #include "orb_device.h"
 #include "orb_match.h"
@@ -448,6 +449,12 @@ struct orbx_handle {
     uint8_t* pin_out = nullptr; // {cnt, err} + K orbx_kp + K x 32 descriptors
     uint8_t* pin_out_dev = nullptr;  // its device-mapped address: the graph's kernels write the results there
     size_t pin_in_bytes = 0, pin_out_bytes = 0;
+    // orbx_set_host_pyramid: the host path also delivers levels 1..L-1 (device layout of one frame) into pin_pyr
+    bool host_pyr = false;
+    bool host_pyr_valid = false;  // pin_in / pin_pyr hold the last orbx_extract's levels
+    uint8_t* pin_pyr = nullptr;
+    uint8_t* pin_pyr_dev = nullptr;
+    size_t pin_pyr_bytes = 0;
     // stage profiling (orbx_profile_*)
     bool prof_on = false;
     int prof_mask = 0;  // stages with event pairs (bit k = stage k)
@@ -460,6 +467,7 @@ struct orbx_handle {
 };
 
 static const int kProfMaxCalls = 4096;
+static const int kHostCopyBlocks = 16;  // octree-launch workgroups (1024 threads) copying the host path's pyramid
 
 /* stage k = {pyramid, fast_cells, octree, blur, describe}; e = 0 start / 1 end, recorded on the
  * stream the stage's kernel is launched on (the overlapped schedule is kept) */
@@ -570,12 +578,38 @@ constexpr int kErrWordExtractSeq = 40;  // the host extraction's call counter (k
  * branch layout measured slower than the one queue (profiles/r04_latency_branches.log, r04_latency_lists.log,
  * r04m_latency_ab.log), and so did a single launch for levels 2.. whose tiles wait on each other's counters
  * (r04_latency_chain_reverted.log). */
+/* the blur inside describe (k_describe_blur, no blurred pyramid in HBM) takes every frame whose level-0 rows are
+ * 4-byte aligned; other frames blur each level in k_blur_strips and describe from it */
+static bool use_describe_blur(const uint8_t* d_frames, long long fstride, int pitch) {
+#ifdef ORBX_AB_DESCRIBE_BLUR  // A/B build (tools/build_variant.sh) while the fused form is measured
+    return describe_blur_ok(d_frames, fstride, pitch);
+#else
+    (void)d_frames, (void)fstride, (void)pitch;
+    return false;
+#endif
+}
+
 static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nframes, const uint8_t* d_frames,
                               long long fstride, int pitch, orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
-                              int kp_stride, hipStream_t st, int* errp) {
+                              int kp_stride, hipStream_t st, int* errp, hipEvent_t ev_pyr, const HostCopy* copy) {
     Geometry& g = h->geo;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
     if (!(h->skip_mask & 1) && launch_pyramid(h, ep, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
+    if (ev_pyr) HIPR(hipEventRecord(ev_pyr, st));  // orbx_set_pyramid_event: right after the pyramid launch
+    if (use_describe_blur(d_frames, fstride, pitch)) {  // FAST -> octree -> blur + describe
+        if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, ep.ncells, nframes, st))
+            return ORBX_EDEVICE;
+        if (!(h->skip_mask & 4))
+            HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
+                               h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
+                               (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st, 0, -1,
+                               copy));
+        if (!(h->skip_mask & 16))
+            HIPR(launch_describe_blur(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, h->lvkey.as<uint32_t>(),
+                                      h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride, g.d_ptab.as<int>(),
+                                      nframes, st));
+        return 0;
+    }
     ExtractParams eb = ep;  // the blur's short-chunk job table
     for (int i = 0; i <= kMaxLevels; i++) eb.bjob_begin[i] = g.bjob_small[i];
     if (!(h->skip_mask & 2) && !(h->skip_mask & 8)) {  // FAST and the blur in one launch
@@ -592,7 +626,8 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
     if (!(h->skip_mask & 4))
         HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                            h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
-                           (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st));
+                           (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st, 0, -1,
+                           copy));
     if (!(h->skip_mask & 16))
         HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
                              h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
@@ -600,9 +635,21 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
     return 0;
 }
 
+/* a handle's own HIP stream (h->stream: host calls; h->side: the separate blur of frames the fused describe cannot
+ * take), created on the handle's device at its first use */
+static int ensure_stream(orbx_handle* h, hipStream_t* s) {
+    if (*s) return 0;
+    HIPR(hipSetDevice(h->device));
+    if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) {
+        *s = nullptr;
+        return ORBX_EDEVICE;
+    }
+    return 0;
+}
+
 static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, long long fstride, int pitch,
                        orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts, int kp_stride, hipStream_t st,
-                       bool host_call = true, bool mapped_out = false) {
+                       bool host_call = true, bool mapped_out = false, const HostCopy* copy = nullptr) {
     Geometry& g = h->geo;
     // the L2-residency bound (orbx_debug_alias_frames): every frame of the batch reads frame 0's image and
     // shares one pyramid / blur buffer, so the stages read lines other workgroups of the launch keep in L2
@@ -615,14 +662,13 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     ep_alias.host_out = mapped_out ? 1 : 0;
     const ExtractParams& ep = ep_alias;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
-    hipStream_t sd = h->serial ? st : h->side;
     // the host-buffer paths report their own per-call word; the device batch path leaves word 0 sticky
     // until orbx_check_error takes (and clears) it, so no fill kernel sits on the batch stream every call
     int* errp = h->err.as<int>() + (host_call ? kErrWordExtract : kErrWordSticky);
     if (nframes < kPyrFramesMinBatch && !h->serial && !h->prof_on && !h->alias) {
-        if (run_extract_levels(h, ep, nframes, d_frames, fstride, pitch, d_kps, d_desc, d_counts, kp_stride, st, errp))
+        if (run_extract_levels(h, ep, nframes, d_frames, fstride, pitch, d_kps, d_desc, d_counts, kp_stride, st, errp,
+                               host_call ? nullptr : h->user_ev_pyr, copy))
             return ORBX_EDEVICE;
-        if (!host_call && h->user_ev_pyr) HIPR(hipEventRecord(h->user_ev_pyr, st));
         h->last_frames = d_frames;
         h->last_fstride = fstride;
         h->last_pitch = pitch;
@@ -630,20 +676,27 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         h->last_stream = st;
         return 0;
     }
+    const bool fused = use_describe_blur(d_frames, fstride, pitch);
+    if (!fused && !h->serial && ensure_stream(h, &h->side)) return ORBX_EDEVICE;
+    const hipStream_t sd = h->serial ? st : h->side;
     if (prof_mark(h, 0, 0, st)) return ORBX_EDEVICE;
     if (!(h->skip_mask & 1) && launch_pyramid(h, ep, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 0, 1, st)) return ORBX_EDEVICE;
     if (!host_call && h->user_ev_pyr) HIPR(hipEventRecord(h->user_ev_pyr, st));
-    if (!h->serial) {
-        HIPR(hipEventRecord(h->ev_pyr, st));
-        HIPR(hipStreamWaitEvent(sd, h->ev_pyr, 0));
+    if (!fused) {
+        if (!h->serial) {
+            HIPR(hipEventRecord(h->ev_pyr, st));
+            HIPR(hipStreamWaitEvent(sd, h->ev_pyr, 0));
+        }
+        if (prof_mark(h, 3, 0, sd)) return ORBX_EDEVICE;
+        if (!(h->skip_mask & 8))
+            HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl, 0,
+                                    g.nbjobs, nullptr, nframes, sd));
+        if (prof_mark(h, 3, 1, sd)) return ORBX_EDEVICE;
+        if (!h->serial) HIPR(hipEventRecord(h->ev_blur, sd));
+    } else if (prof_mark(h, 3, 0, st) || prof_mark(h, 3, 1, st)) {  // no blur stage: a zero-length pair
+        return ORBX_EDEVICE;
     }
-    if (prof_mark(h, 3, 0, sd)) return ORBX_EDEVICE;
-    if (!(h->skip_mask & 8))
-        HIPR(launch_blur_strips(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl, 0,
-                                g.nbjobs, nullptr, nframes, sd));
-    if (prof_mark(h, 3, 1, sd)) return ORBX_EDEVICE;
-    if (!h->serial) HIPR(hipEventRecord(h->ev_blur, sd));
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
     if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 1, 1, st) || prof_mark(h, 2, 0, st)) return ORBX_EDEVICE;
@@ -652,12 +705,18 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
                            h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
                            (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st));
     if (prof_mark(h, 2, 1, st)) return ORBX_EDEVICE;
-    if (!h->serial) HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
+    if (!h->serial && !fused) HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     if (prof_mark(h, 4, 0, st)) return ORBX_EDEVICE;
-    if (!(h->skip_mask & 16))
-        HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
-                             h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
-                             g.d_ptab.as<int>(), nframes, st));
+    if (!(h->skip_mask & 16)) {
+        if (fused)
+            HIPR(launch_describe_blur(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, h->lvkey.as<uint32_t>(),
+                                      h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride, g.d_ptab.as<int>(),
+                                      nframes, st));
+        else
+            HIPR(launch_describe(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), h->blur.as<uint8_t>(), ep, dl,
+                                 h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), d_kps, d_desc, d_counts, kp_stride,
+                                 g.d_ptab.as<int>(), nframes, st));
+    }
     if (prof_mark(h, 4, 1, st)) return ORBX_EDEVICE;
     if (h->prof_on && h->prof_calls < kProfMaxCalls) h->prof_calls++;
     h->last_frames = d_frames;
@@ -694,9 +753,10 @@ int orbx_create(const orbx_params* p, int device, int max_width, int max_height,
     h->max_w = max_width;
     h->max_h = max_height;
     h->max_batch = max_batch;
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess ||
+    // no HIP stream here: the host-call stream and the blur's side stream are created at their first use
+    // (ensure_stream), since every idle stream in the process costs the batch schedule's graph streams their step
+    // rate (profiles/r04_idle_stream_cost.log) and a device batch on the caller's stream needs neither
+    if (hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_blur, hipEventDisableTiming) != hipSuccess) {
         orbx_destroy(h);
         return ORBX_EDEVICE;
@@ -728,6 +788,7 @@ void orbx_destroy(orbx_handle* h) {
     if (h->graph) (void)hipGraphDestroy(h->graph);
     if (h->pin_in) (void)hipHostFree(h->pin_in);
     if (h->pin_out) (void)hipHostFree(h->pin_out);
+    if (h->pin_pyr) (void)hipHostFree(h->pin_pyr);
     delete h;
 }
 
@@ -909,11 +970,30 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
         if (h->pin_out) (void)hipHostFree(h->pin_out);
         h->pin_out = nullptr;
         h->pin_out_bytes = 0;
-        HIPR(hipHostMalloc((void**)&h->pin_out, out_bytes, hipHostMallocDefault));
+        // fine-grained (coherent) like the matchers' polled buffers: the kernels' writes of the results and of the
+        // done word are visible to the polling host without relying on an L2 writeback
+        HIPR(hipHostMalloc((void**)&h->pin_out, out_bytes, hipHostMallocMapped | hipHostMallocCoherent));
         memset(h->pin_out, 0, out_bytes);  // done word 0: the device counter's first value is 1
         h->pin_out_bytes = out_bytes;
         HIPR(hipHostGetDevicePointer((void**)&h->pin_out_dev, h->pin_out, 0));
         h->epoch++;
+    }
+    // mvImagePyramid for the host (orbx_set_host_pyramid): extra workgroups of the octree launch copy levels 1..L-1
+    // of this frame into mapped pinned memory while the octree runs; level 0 is pin_in itself
+    const bool copies = h->host_pyr && !h->serial && !h->alias && h->geo.ep.L > 1;
+    HostCopy hc{nullptr, nullptr, 0, 0};
+    if (copies) {
+        const size_t pb = (size_t)h->geo.ep.pyr_frame_bytes;
+        if (h->pin_pyr_bytes < pb) {
+            if (h->pin_pyr) (void)hipHostFree(h->pin_pyr);
+            h->pin_pyr = h->pin_pyr_dev = nullptr;
+            h->pin_pyr_bytes = 0;
+            HIPR(hipHostMalloc((void**)&h->pin_pyr, pb, hipHostMallocMapped | hipHostMallocCoherent));
+            h->pin_pyr_bytes = pb;
+            HIPR(hipHostGetDevicePointer((void**)&h->pin_pyr_dev, h->pin_pyr, 0));
+            h->epoch++;
+        }
+        hc = HostCopy{(const uint4*)h->pyr.p, (uint4*)h->pin_pyr_dev, (long long)(pb / 16), kHostCopyBlocks};
     }
     for (int y = 0; y < height; y++) memcpy(h->pin_in + (size_t)y * width, img + (size_t)y * pitch, width);
     uint8_t* o_kps = h->pin_out + 64;
@@ -925,7 +1005,8 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
     auto enqueue = [&]() -> int {
         HIPR(hipMemcpyAsync(h->in_frame.p, h->pin_in, in_bytes, hipMemcpyHostToDevice, h->stream));
         int rc = run_extract(h, 1, h->in_frame.as<uint8_t>(), (long long)in_bytes, width, (orbx_kp*)(d_out + 64),
-                             d_out + 64 + sizeof(orbx_kp) * (size_t)K, (int32_t*)d_out, K, h->stream, true, true);
+                             d_out + 64 + sizeof(orbx_kp) * (size_t)K, (int32_t*)d_out, K, h->stream, true, true,
+                             copies ? &hc : nullptr);
         if (rc) return rc;
         HIPR(launch_call_done(h->err.as<int32_t>() + kErrWordExtract, (int32_t*)(d_out + 4),
                               h->err.as<int32_t>() + kErrWordExtractSeq, (int32_t*)(d_out + 8), h->stream));
@@ -967,6 +1048,7 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
         HIPR(hipGraphLaunch(h->gexec, h->stream));
     }
     if (const int rc = wait_until(h->stream, [&] { return __atomic_load_n(done, __ATOMIC_ACQUIRE) != done0; })) return rc;
+    h->host_pyr_valid = copies;
     h->last_frames = h->in_frame.as<uint8_t>();
     h->last_fstride = (long long)in_bytes;
     h->last_pitch = width;
@@ -991,6 +1073,8 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int width, int height, size
     if (width <= 0 || height <= 0 || !img) return 0;  // empty image: outputs untouched (:1046-1047)
     if (pitch < (size_t)width) return ORBX_EARG;
     HIPR(hipSetDevice(h->device));
+    h->host_pyr_valid = false;
+    if (ensure_stream(h, &h->stream)) return ORBX_EDEVICE;
     int rc = ensure_geometry(h, width, height, 1);
     if (rc) return rc;
     const int K = h->geo.ep.kp_per_frame;
@@ -1033,11 +1117,30 @@ int orbx_pyramid_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_
     // wait for this handle's own last extraction only (the stream it was enqueued on and the handle's side
     // stream), not for every stream on the device (other extractor / matcher threads)
     HIPR(hipStreamSynchronize(h->last_stream));
-    HIPR(hipStreamSynchronize(h->side));
+    if (h->side) HIPR(hipStreamSynchronize(h->side));
     const uint8_t* src = level == 0 ? h->last_frames + frame * h->last_fstride
                                     : h->pyr.as<uint8_t>() + frame * h->geo.ep.pyr_frame_bytes + d.pyr_off;
     const size_t sp = level == 0 ? (size_t)h->last_pitch : (size_t)d.pitch;
     HIPR(hipMemcpy2D(dst, pitch, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int orbx_set_host_pyramid(orbx_handle* h, int on) {
+    if (!h) return ORBX_EARG;
+    h->host_pyr = on != 0;
+    h->host_pyr_valid = false;
+    h->epoch++;  // the captured host-call graph holds whether the octree launch carries the copy
+    return 0;
+}
+
+int orbx_host_pyramid_level(orbx_handle* h, int level, const uint8_t** data, size_t* pitch, int* width, int* height) {
+    if (!h || !data || !pitch || level < 0 || level >= h->T.nlevels || !h->geo.W || !h->host_pyr_valid)
+        return ORBX_EARG;
+    const LevelDesc& d = h->geo.lv[level];
+    *data = level == 0 ? h->pin_in : h->pin_pyr + d.pyr_off;
+    *pitch = level == 0 ? (size_t)d.w : (size_t)d.pitch;
+    if (width) *width = d.w;
+    if (height) *height = d.h;
     return 0;
 }
 
@@ -1176,9 +1279,12 @@ int orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orb
     float* ddp = dur + stride;
     int32_t* misc = (int32_t*)(ddp + stride);
     const int32_t hm[4] = {0, 0, nL, nR};
+    if (ensure_stream(left, &left->stream)) return ORBX_EDEVICE;
     hipStream_t st = left->stream;
-    // the right extraction ran on the right handle's stream
-    HIPR(hipStreamSynchronize(right->stream));
+    // the right extraction ran on the stream of the right handle's last call (its own, after a host call), and a
+    // batch's blur on its side stream
+    HIPR(hipStreamSynchronize(right->last_stream));
+    if (right->side) HIPR(hipStreamSynchronize(right->side));
     HIPR(hipMemcpyAsync(dkL, kpsL, sizeof(orbx_kp) * nL, hipMemcpyHostToDevice, st));
     HIPR(hipMemcpyAsync(ddL, descL, 32 * (size_t)nL, hipMemcpyHostToDevice, st));
     if (nR) {
@@ -1212,11 +1318,18 @@ struct orbm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     // the host calls' stream, created at the first one: the *_device paths run on the caller's stream, and an idle
-    // HIP stream costs the bench's graph streams their step rate (profiles/r04_idle_stream_cost.log)
-    hipStream_t s() {
-        if (!stream) (void)hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
-        return stream;
+    // HIP stream costs the bench's graph streams their step rate (profiles/r04_idle_stream_cost.log). Every host
+    // entry point calls ready() first: it makes the context's device current (whatever the calling thread had) and
+    // creates the stream there, or fails the call with ORBX_EDEVICE
+    int ready() {
+        HIPR(hipSetDevice(device));
+        if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+            stream = nullptr;
+            return ORBX_EDEVICE;
+        }
+        return 0;
     }
+    hipStream_t s() const { return stream; }
     DevBuf scratch;
     DevBuf err;  // device error flag of the *_device calls that validate their input (orbm_check_error)
     std::vector<uint8_t> host;
@@ -1678,7 +1791,7 @@ static int tri_small(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view*
 static int tri_common(orbm_ctx* ctx, const orbm_kf_view* kf1, const orbm_kf_view* kf2, const float F12[9], float ex,
                       float ey, int only_stereo, int check_ori, int32_t* match12, int* nmatches,
                       const KfEntry* c1 = nullptr, const KfEntry* c2 = nullptr) {
-    HIPR(hipSetDevice(ctx->device));
+    if (const int rc_ = ctx->ready()) return rc_;
     std::vector<std::pair<int, int>> common;
     common_nodes(kf1, kf2, common);
     std::vector<NodeTask> tasks;
@@ -1741,7 +1854,7 @@ extern "C" {
 static int bow_common(orbm_ctx* ctx, const orbm_kf_view* vq, const orbm_kf_view* vc, float nnratio, int check_ori,
                       int mode, int32_t* out, int nout, int* nmatches, const KfEntry* cq = nullptr,
                       const KfEntry* cc = nullptr) {
-    HIPR(hipSetDevice(ctx->device));
+    if (const int rc_ = ctx->ready()) return rc_;
     std::vector<std::pair<int, int>> common;
     common_nodes(vq, vc, common);
     std::vector<NodeTask> tasks;
@@ -2171,7 +2284,7 @@ constexpr bool kProjDirect = true;  // Fuse: results written by the scan kernel 
 int run_projection(orbm_ctx* ctx, const orbm_frame_view* F, const ProjBatch& pb, int accept_th, int ratio,
                    float nnratio, int check_ori, int32_t* match, int* nmatches, const float* inv_sigma2 = nullptr,
                    int32_t* qres = nullptr, int init_n = -1, const KfEntry* ce = nullptr) {
-    HIPR(hipSetDevice(ctx->device));
+    if (const int rc_ = ctx->ready()) return rc_;
     const size_t n = (size_t)F->n, nq = pb.q.size();
     const size_t nout = init_n >= 0 ? (size_t)init_n : n;
     const size_t nF = ce ? 0 : n;  // per-feature arrays uploaded with the call
@@ -2706,7 +2819,7 @@ int orbm_compute_distinctive_descriptors(orbm_ctx* ctx, int npoints, const int32
         if (offsets[p + 1] < offsets[p]) return ORBX_EARG;
     const size_t nrows = (size_t)offsets[npoints];
     if (nrows && !desc) return ORBX_EARG;
-    HIPR(hipSetDevice(ctx->device));
+    if (const int rc_ = ctx->ready()) return rc_;
     Carve cv;
     const size_t o_off = cv.take(4 * ((size_t)npoints + 1)), o_desc = cv.take(32 * nrows), o_best = cv.take(4 * (size_t)npoints),
                  o_out = cv.take(32 * (size_t)npoints);
@@ -3138,6 +3251,7 @@ int orbm_search_for_triangulation_cached(orbm_ctx* ctx, orbm_kf_cache* cache, ui
                                          int only_stereo, int check_ori, int32_t* match12, int* nmatches) {
     if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf1) || !view_ok(kf2) || !F12 || !match12)
         return ORBX_EARG;
+    if (const int rc_ = ctx->ready()) return rc_;
     const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr, ctx->s());
     const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr, ctx->s()) : nullptr;
     if (!c1 || !c2) return ORBX_EDEVICE;
@@ -3149,6 +3263,7 @@ int orbm_search_by_bow_kf_kf_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_
                                     int32_t* match12, int* nmatches) {
     if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf1) || !view_ok(kf2) || !match12)
         return ORBX_EARG;
+    if (const int rc_ = ctx->ready()) return rc_;
     const std::shared_ptr<KfEntry> c1 = cache_get(cache, 0, key1, kf1, nullptr, ctx->s());
     const std::shared_ptr<KfEntry> c2 = c1 ? cache_get(cache, 0, key2, kf2, nullptr, ctx->s()) : nullptr;
     if (!c1 || !c2) return ORBX_EDEVICE;
@@ -3159,6 +3274,7 @@ int orbm_search_by_bow_kf_f_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t
                                    const orbm_kf_view* f, float nnratio, int check_ori, int32_t* match_f,
                                    int* nmatches) {
     if (!ctx || !cache || cache->device != ctx->device || !view_ok(kf) || !view_ok(f) || !match_f) return ORBX_EARG;
+    if (const int rc_ = ctx->ready()) return rc_;
     const std::shared_ptr<KfEntry> ck = cache_get(cache, 0, key, kf, nullptr, ctx->s());
     if (!ck) return ORBX_EDEVICE;
     return bow_common(ctx, kf, f, nnratio, check_ori, 0, match_f, f->n, nmatches, ck.get(), nullptr);
@@ -3169,6 +3285,7 @@ int orbm_fuse_cached(orbm_ctx* ctx, orbm_kf_cache* cache, uint64_t key, const or
                      int32_t* best_idx, int* nfused) {
     if (!cache || !fuse_args_ok(ctx, KF, Tcw, Ow, mp, inv_level_sigma2, best_idx) || cache->device != ctx->device)
         return ORBX_EARG;
+    if (const int rc_ = ctx->ready()) return rc_;
     const std::shared_ptr<KfEntry> ck = cache_get(cache, 1, key, nullptr, KF, ctx->s());
     if (!ck) return ORBX_EDEVICE;
     return fuse_common(ctx, KF, Tcw, Ow, mp, th, inv_level_sigma2, best_idx, nfused, ck.get());

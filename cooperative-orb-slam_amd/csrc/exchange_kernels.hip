@@ -641,17 +641,29 @@ hipError_t launch_bow_slots(const QueryKF& q, const uint8_t* slots, long long sl
                             hipStream_t st) {
     if (nref == 0) return hipSuccess;
     if (max_nodes > 0) {
-        // the node's candidates in LDS: 36 bytes each, up to the query keyframe's capacity (a node holds at most
-        // every feature; a slot node past it is flagged)
-        const size_t lds = 36 * (size_t)q.cap;
-        if (lds > 160 * 1024) return hipErrorInvalidValue;
+        // the node's candidates in LDS: 36 bytes each, up to the largest capacity a slot of slot_bytes can carry (a
+        // node holds at most every feature of its slot, whatever the query keyframe's own capacity), bounded by the
+        // 160 KB of a CU (4551 candidates; a node past the bound is flagged, error 8)
+        int slot_cap = 0;
+        for (int lo = 0, hi = kSlotMaxCap; lo <= hi;) {  // largest cap whose layout fits slot_bytes
+            const int mid = (lo + hi) / 2;
+            uint32_t off[ORBX_SLOT_NSECTIONS], total = 0;
+            if (slot_offsets(mid, off, &total) && (long long)total <= slot_bytes) {
+                slot_cap = mid;
+                lo = mid + 1;
+            } else {
+                hi = mid - 1;
+            }
+        }
+        const int lds_cap = std::min(std::max(q.cap, slot_cap), 160 * 1024 / 36);
+        const size_t lds = 36 * (size_t)lds_cap;
         if (lds > 65536) {  // past the 64 KB default (a host-side attribute of the current device's function)
             const hipError_t e = hipFuncSetAttribute((const void*)k_bow_slots, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      (int)lds);
             if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL(k_bow_slots, dim3(max_nodes, nref), dim3(64), lds, st, q, slots, slot_bytes, 0, nnratio,
-                           q.cap, match, err);
+                           lds_cap, match, err);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

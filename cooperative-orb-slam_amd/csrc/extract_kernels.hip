@@ -835,11 +835,21 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
                                                 const int* __restrict__ cellcnt, uint32_t* __restrict__ lvkey,
                                                 int* __restrict__ lvcnt, uint8_t* __restrict__ gscratch,
                                                 long long gscratch_frame_bytes, int NC, int KL, int level0,
-                                                int* __restrict__ err) {
+                                                int* __restrict__ err, HostCopy hc) {
     extern __shared__ __align__(16) uint8_t lds[];
     __shared__ int red[16];
     __shared__ int sh_size, sh_jstar, sh_tc, sh_nexp, sh_ndiv;
     const int tid = threadIdx.x;
+    if ((int)blockIdx.x >= (int)gridDim.x - hc.nblocks) {
+        // the host path's mvImagePyramid (orbx_set_host_pyramid): this frame's levels 1..L-1 into mapped pinned host
+        // memory, beside the octree's few barrier-chained workgroups; visible to the host before the call's done
+        // word (k_call_done, a later launch on the same queue)
+        const long long stride = (long long)hc.nblocks * NT;
+        for (long long i = (long long)(blockIdx.x - (gridDim.x - hc.nblocks)) * NT + tid; i < hc.n16; i += stride)
+            hc.dst[i] = hc.src[i];
+        __threadfence_system();
+        return;
+    }
     const int l = level0 + blockIdx.x, f = blockIdx.y;
     OCT_T(0);
     const LevelDesc lv = levels[l];
@@ -1733,6 +1743,309 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
     if (ep.host_out) __threadfence_system();
 }
 
+/* ----------------------------------------------------------------------------------- */
+/* GaussianBlur + IC_Angle + rBRIEF in one kernel: no blurred pyramid in HBM.            */
+/*                                                                                       */
+/*  Per keypoint (x, y) the unblurred neighbourhood rows y-21..y+21 x 12 dwords from      */
+/*  column cx0 = (x-22) & ~3 is staged in LDS by LDS-DMA (pitch 48; rows REFLECT_101 by   */
+/*  address, columns clamped into the row and the two halo columns on either side        */
+/*  patched as REFLECT_101 for keypoints near an edge). IC_Angle (ORBextractor.cc:77-104) */
+/*  reads its 31x31 window there. Then 10 of the keypoint's 16 lanes blur the patch in    */
+/*  place (ORBextractor.cc:1085-1086): lane = 4 output columns (dword g = 1..10), a 7-row  */
+/*  register window of float row sums walking the 43 rows; output row r (image row        */
+/*  y-18+r) overwrites source row r, which no later row sum reads (the lanes of a wave    */
+/*  issue in lockstep and LDS operations of a wave complete in order). The row sums are    */
+/*  ten v_dot4 per 4 outputs on the three aligned dwords around them (no alignbyte); the   */
+/*  vertical sums, the rounding (SSE2 column path RNE, scalar tail half-up) are those of   */
+/*  k_blur_strips, so every blurred byte rBRIEF samples equals the whole-level blur's.     */
+/*  rBRIEF (ORBextractor.cc:107-147) then samples rows 0..36 as k_describe does.          */
+/*  Requires 4-aligned level-0 rows (the DMA moves dwords); launch_describe falls back to */
+/*  k_blur_strips + k_describe otherwise.                                                  */
+/* ----------------------------------------------------------------------------------- */
+constexpr int kFusedRows = 43;   // source rows y-21 .. y+21
+constexpr int kFusedPitch = 48;  // 12 dwords: columns cx0 .. cx0+47 cover x-21 .. x+21 for any (x-22) & 3
+constexpr int kFusedDwords = kFusedRows * kFusedPitch / 4;  // 516 per keypoint
+
+#ifndef ORBX_FUSED_WAVES
+#define ORBX_FUSED_WAVES 4
+#endif
+constexpr int kFusedWaves = ORBX_FUSED_WAVES;  // waves (x 4 keypoints) per k_describe_blur workgroup
+constexpr int kFusedKps = 4 * kFusedWaves;
+
+__global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
+    const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
+    ExtractParams ep, const LevelDesc* __restrict__ levels, const uint32_t* __restrict__ lvkey,
+    const int* __restrict__ lvcnt, orbx_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
+    int* __restrict__ out_counts, int kp_stride, const int* __restrict__ ptab) {
+    __shared__ PatPt s_pat[256];
+    __shared__ int2 s_ic[256];
+    __shared__ __align__(16) uint8_t s_patch[kFusedKps][kFusedRows * kFusedPitch];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int sub = lane >> 4, ln = lane & 15;
+    // XCD-aware block mapping as k_describe: every workgroup of a frame on one XCD
+    const int G = (ep.kp_per_frame + kFusedKps - 1) / kFusedKps;
+    int f, blk;
+    {
+        const int b = blockIdx.x;
+        if ((gridDim.x / G) % 8 == 0) {
+            const int k = b >> 3;
+            f = (b & 7) + 8 * (k / G);
+            blk = k % G;
+        } else {
+            f = b / G;
+            blk = b % G;
+        }
+    }
+    constexpr int NT = 64 * kFusedWaves;
+    constexpr int kTab = (256 + NT - 1) / NT;
+    PatPt my_pat[kTab];
+    int2 my_ic[kTab];
+#pragma unroll
+    for (int q = 0; q < kTab; q++) {
+        const int t = min(tid + q * NT, 255);
+        my_pat[q] = kPatternT.t[t];
+        my_ic[q] = ((const int2*)(ptab + ep.ic_off))[t];
+    }
+    const int g = (blk * kFusedWaves + wave) * 4 + sub;
+    const int gc = min(g, ep.kp_per_frame - 1);
+    const uint32_t kk_raw = lvkey[(long long)f * ep.kp_per_frame + gc];
+    const int* cnt = lvcnt + f * ep.L;
+    int cl[kMaxLevels];
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;
+#pragma unroll
+    for (int q = 0; q < kTab; q++) {
+        const int t = tid + q * NT;
+        if (t >= 256) break;
+        s_pat[t] = my_pat[q];
+        s_ic[t] = my_ic[q];
+    }
+    if (blk == 0 && tid == 0) {
+        int tot = 0;
+#pragma unroll
+        for (int q = 0; q < kMaxLevels; q++) tot += cl[q];
+        out_counts[f] = tot;
+        if (ep.host_out) __threadfence_system();
+    }
+    __syncthreads();
+    if (__ballot(g < ep.kp_per_frame) == 0) return;  // wave-uniform
+    const int l = level_of(ep.kp_off, ep.L, gc);
+    const int k = gc - ep.kp_off[l];
+    int mycnt = 0, outidx = k;
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; q++) {
+        mycnt = q == l ? cl[q] : mycnt;
+        outidx += q < l ? cl[q] : 0;
+    }
+    const bool valid = g < ep.kp_per_frame && k < mycnt;
+    if (__ballot(valid) == 0) return;  // wave-uniform
+    const LevelDesc lv = levels[l];
+    const uint32_t kk = valid ? kk_raw : 0u;
+    const int x = valid ? (int)(kk & 0xFFF) : 32, y = valid ? (int)((kk >> 12) & 0xFFF) : 32;
+    const int resp = (int)(kk >> 24);
+    const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
+    const int pitch = l == 0 ? pitch0 : lv.pitch;
+    const int cx0 = (x - 22) & ~3;  // image column of patch column 0
+    const int pm = (x - 22) & 3;    // x = cx0 + 22 + pm
+    const int lastd = (lv.w - 1) & ~3;
+    // a patch that reaches past an image edge (REFLECT_101 rows or halo columns) or whose last dword lies past the
+    // row's last valid dword takes the clamped / reflected staging
+    const int edge = (y < 21 || y + 21 >= lv.h || x < 22 || x + 21 >= lv.w || cx0 + 44 > lastd) ? 1 : 0;
+    uint8_t* patch = s_patch[wave * 4 + sub];
+    {
+        int rq[9], cq[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+            const int d = 64 * q + lane;
+            rq[q] = d / 12;
+            cq[q] = 4 * (d - 12 * rq[q]);
+        }
+        const uint64_t ib = (uint64_t)(uintptr_t)img;
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ib, 16 * s);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ib >> 32), 16 * s);
+            const uint8_t* sb = (const uint8_t*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+            const int sp = __builtin_amdgcn_readlane(pitch, 16 * s);
+            const int sy = __builtin_amdgcn_readlane(y, 16 * s);
+            const int scx = __builtin_amdgcn_readlane(cx0, 16 * s);
+            uint8_t* dst = s_patch[wave * 4 + s];
+            if (__builtin_amdgcn_readlane(edge, 16 * s) == 0) {
+                const uint8_t* b0 = sb + (long long)(sy - 21) * sp + scx;
+#pragma unroll
+                for (int q = 0; q < 9; q++) {
+                    if (64 * q + lane < kFusedDwords)
+                        __builtin_amdgcn_global_load_lds(
+                            (__attribute__((address_space(1))) void*)(b0 + (unsigned)(rq[q] * sp + cq[q])),
+                            (__attribute__((address_space(3))) void*)(dst + 256 * q), 4, 0, 0);
+                }
+            } else {
+                const int sh = __builtin_amdgcn_readlane(lv.h, 16 * s);
+                const int sld = __builtin_amdgcn_readlane(lastd, 16 * s);
+#pragma unroll
+                for (int q = 0; q < 9; q++) {
+                    if (64 * q + lane < kFusedDwords) {
+                        const int rr = reflect101(sy - 21 + rq[q], sh);
+                        const int cc = iclamp(scx + cq[q], 0, sld);
+                        __builtin_amdgcn_global_load_lds(
+                            (__attribute__((address_space(1))) void*)(sb + (long long)rr * sp + cc),
+                            (__attribute__((address_space(3))) void*)(dst + 256 * q), 4, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA writes have landed
+    wave_sync();
+    // REFLECT_101 halo columns of edge patches: image columns -1, -2 <- 1, 2 and w, w+1 <- w-2, w-3
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        if (__builtin_amdgcn_readlane(edge, 16 * s) == 0) continue;
+        const int scx = __builtin_amdgcn_readlane(cx0, 16 * s);
+        const int sw = __builtin_amdgcn_readlane(lv.w, 16 * s);
+        if (lane < kFusedRows) {
+            uint8_t* row = s_patch[wave * 4 + s] + lane * kFusedPitch;
+#pragma unroll
+            for (int q = 1; q <= 2; q++) {
+                const int lc = -q - scx;
+                if (lc >= 0) row[lc] = row[q - scx];
+            }
+#pragma unroll
+            for (int q = 0; q <= 1; q++) {
+                const int lc = sw + q - scx;
+                if (lc < kFusedPitch) row[lc] = row[sw - 2 - q - scx];
+            }
+        }
+    }
+    wave_sync();
+    int m10, m01;
+    {
+        // IC_Angle window: image rows y-15+ri = patch row ri+6, columns x-15+4g4.. = patch column 7+pm+4g4
+        const int g4 = ln & 7, r = ln >> 3;
+        const int c0 = 7 + pm + 4 * g4;
+        const uint32_t al = (uint32_t)c0 & 3u;
+        const uint32_t* pw = (const uint32_t*)patch + (c0 >> 2);
+        uint32_t Ap = 0, S = 0, Mp = 0;
+#pragma unroll
+        for (int p = 0; p < 16; p++) {
+            const int ri = r + 2 * p;
+            const uint32_t w0 = pw[(ri + 6) * (kFusedPitch / 4)], w1 = pw[(ri + 6) * (kFusedPitch / 4) + 1];
+            const uint32_t I4 = __builtin_amdgcn_alignbyte(w1, w0, al);
+            const int2 msk = s_ic[ri * 8 + g4];
+            const uint32_t sI = __builtin_amdgcn_udot4(I4, (uint32_t)msk.y, 0u, false);
+            Ap = __builtin_amdgcn_udot4(I4, (uint32_t)msk.x, Ap, false);
+            S += sI;
+            Mp += __umul24(sI, 2u * (uint32_t)p);
+        }
+        int A = (int)Ap - 15 * (int)S, M = (int)Mp + (r - 15) * (int)S;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+            A += __shfl_xor(A, o, 16);
+            M += __shfl_xor(M, o, 16);
+        }
+        m10 = A;
+        m01 = M;
+    }
+    // blur in place: lanes ln < 10 own output dword g = ln + 1 (columns 4g..4g+3 of the patch)
+    if (ln < 10) {
+        const int gd = ln + 1;
+        const uint32_t* src = (const uint32_t*)patch + (gd - 1);
+        uint32_t* dsw = (uint32_t*)patch + gd;
+        const int col0 = cx0 + 4 * gd;  // image column of this lane's first output
+        const bool tail = col0 + 3 >= lv.blur_vec_end;
+        // taps 18 34 49 55 49 34 18 against bytes of dwords g-1 (a), g (b), g+1 (c): output j sums bytes j+1 .. j+7
+        constexpr uint32_t A0 = 18u << 8 | 34u << 16 | 49u << 24, B0 = 55u | 49u << 8 | 34u << 16 | 18u << 24;
+        constexpr uint32_t A1 = 18u << 16 | 34u << 24, B1 = 49u | 55u << 8 | 49u << 16 | 34u << 24, C1 = 18u;
+        constexpr uint32_t A2 = 18u << 24, B2 = 34u | 49u << 8 | 55u << 16 | 49u << 24, C2 = 34u | 18u << 8;
+        constexpr uint32_t B3 = 18u | 34u << 8 | 49u << 16 | 55u << 24, C3 = 49u | 34u << 8 | 18u << 16;
+        auto rowsum = [&](int i, float2v& lo, float2v& hi) {
+            const uint32_t a = src[i * (kFusedPitch / 4)], b = src[i * (kFusedPitch / 4) + 1],
+                           c = src[i * (kFusedPitch / 4) + 2];
+            const uint32_t o0 = __builtin_amdgcn_udot4(a, A0, __builtin_amdgcn_udot4(b, B0, 0u, false), false);
+            const uint32_t o1 = __builtin_amdgcn_udot4(
+                a, A1, __builtin_amdgcn_udot4(b, B1, __builtin_amdgcn_udot4(c, C1, 0u, false), false), false);
+            const uint32_t o2 = __builtin_amdgcn_udot4(
+                a, A2, __builtin_amdgcn_udot4(b, B2, __builtin_amdgcn_udot4(c, C2, 0u, false), false), false);
+            const uint32_t o3 = __builtin_amdgcn_udot4(b, B3, __builtin_amdgcn_udot4(c, C3, 0u, false), false);
+            lo = (float2v){(float)o0, (float)o1};
+            hi = (float2v){(float)o2, (float)o3};
+        };
+        float2v WL[7], WH[7];
+#pragma unroll
+        for (int m = 0; m < 6; m++) rowsum(m, WL[m], WH[m]);
+        for (int r0 = 0; r0 < kDescPatchRows; r0 += 7) {
+#pragma unroll
+            for (int s = 0; s < 7; s++) {
+                const int r = r0 + s;
+                if (r < kDescPatchRows) {
+                    const int ns = (s + 6) % 7;
+                    rowsum(r + 6, WL[ns], WH[ns]);
+                    const float2v av = blur_vsum(WL[s], WL[(s + 1) % 7], WL[(s + 2) % 7], WL[(s + 3) % 7],
+                                                 WL[(s + 4) % 7], WL[(s + 5) % 7], WL[ns]);
+                    const float2v bv = blur_vsum(WH[s], WH[(s + 1) % 7], WH[(s + 2) % 7], WH[(s + 3) % 7],
+                                                 WH[(s + 4) % 7], WH[(s + 5) % 7], WH[ns]);
+                    float o[4] = {av.x, av.y, bv.x, bv.y};
+                    if (tail) {
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (col0 + i >= lv.blur_vec_end) o[i] = floorf(o[i] + 0.5f);
+                    }
+                    uint32_t packed = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) packed = __builtin_amdgcn_cvt_pk_u8_f32(o[i], (unsigned)i, packed);
+                    dsw[r * (kFusedPitch / 4)] = packed;
+                }
+            }
+        }
+    }
+    wave_sync();
+    const float angle = fast_atan2((float)m01, (float)m10);
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float theta = __fmul_rn(angle, factorPI);
+    float sa, ca;
+    glibc_sincosf(theta, &sa, &ca);
+    const float a = ca, b = sa;
+    // blurred row r = image row y-18+r; image column x+dx = patch column 22+pm+dx
+    const uint8_t* pc0 = patch + kDescPatchR * kFusedPitch + 22 + pm;
+    uint32_t myword = 0;
+    {
+#pragma clang fp contract(off)
+        const float2v A2v = {a, a}, B2v = {b, b};
+        const float2v MAG = {12582912.f, 12582912.f};
+        constexpr uint32_t K = 0x400000u * (uint32_t)kFusedPitch + 0x4B400000u;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const PatPt pp = s_pat[16 * j + ln];
+            const float2v X = {pp.x0, pp.x1}, Y = {pp.y0, pp.y1};
+            float2v R = (X * B2v + Y * A2v) + MAG;
+            float2v C = (X * A2v - Y * B2v) + MAG;
+            asm("" : "+v"(R), "+v"(C));
+            const uint2v RB = __builtin_bit_cast(uint2v, R), CB = __builtin_bit_cast(uint2v, C);
+            const uint32_t o0 = (RB.x & 0xFFFFFFu) * (uint32_t)kFusedPitch + CB.x - K;
+            const uint32_t o1 = (RB.y & 0xFFFFFFu) * (uint32_t)kFusedPitch + CB.y - K;
+            const int t0 = pc0[(int)o0];
+            const int t1 = pc0[(int)o1];
+            myword |= (uint32_t)(t0 < t1) << j;
+        }
+    }
+    if (valid) {
+        const long long o = (long long)f * kp_stride + outidx;
+        ((uint16_t*)(out_desc + o * 32))[ln] = (uint16_t)myword;
+        if (ln == 0) {
+            orbx_kp kp;
+            const float fx = (float)x, fy = (float)y;
+            kp.x = l ? __fmul_rn(fx, lv.scale) : fx;
+            kp.y = l ? __fmul_rn(fy, lv.scale) : fy;
+            kp.size = lv.patch_size;
+            kp.angle = angle;
+            kp.response = (float)resp;
+            kp.octave = l;
+            out_kps[o] = kp;
+        }
+    }
+    if (ep.host_out) __threadfence_system();
+}
+
 /* self-test hook: the device restatement of glibc sinf/cosf on an array (tests only) */
 __global__ void k_sincos_selftest(const float* __restrict__ in, float* __restrict__ s, float* __restrict__ c, int n) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1886,21 +2199,27 @@ hipError_t octree_setup(int lds_bytes) {
 hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                          const uint32_t* cellkey, const int* cellcnt, uint32_t* lvkey, int* lvcnt,
                          uint8_t* gscratch, long long gscratch_frame_bytes, int NC, int KL, int lds_bytes,
-                         int* err, int nframes, hipStream_t st, int level0, int nlevels) {
+                         int* err, int nframes, hipStream_t st, int level0, int nlevels, const HostCopy* copy) {
     if (nlevels < 0) nlevels = ep.L - level0;
     if (level0 < 0 || nlevels < 1 || level0 + nlevels > ep.L) return hipErrorInvalidValue;
-    dim3 grid(nlevels, nframes);
+    HostCopy hc{nullptr, nullptr, 0, 0};
+    if (copy) {
+        // one frame only: the copy blocks sit at the end of grid.x, and grid.y would repeat them per frame
+        if (nframes != 1 || copy->nblocks < 1 || copy->n16 < 0) return hipErrorInvalidValue;
+        hc = *copy;
+    }
+    dim3 grid(nlevels + hc.nblocks, nframes);
     // a small batch (one frame per Tracking call) has a workgroup per level and nothing beside it: 16 waves walk
     // each round's keys in a quarter of the iterations; batches pack four 256-thread workgroups per CU instead
     if (nframes < kPyrFramesMinBatch)
         hipLaunchKernelGGL(k_octree<1024>, grid, dim3(1024), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey,
-                           lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err);
+                           lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err, hc);
     else if (NC > 256)  // levels of up to 512 live nodes (C4's 2000 features): every round node-per-thread
         hipLaunchKernelGGL(k_octree<512>, grid, dim3(512), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey,
-                           lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err);
+                           lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err, hc);
     else
         hipLaunchKernelGGL(k_octree<256>, grid, dim3(256), lds_bytes, st, ep, levels, cells, cellkey, cellcnt, lvkey,
-                           lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err);
+                           lvcnt, gscratch, gscratch_frame_bytes, NC, KL, level0, err, hc);
     return hipGetLastError();
 }
 
@@ -1941,6 +2260,21 @@ hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0,
     else
         hipLaunchKernelGGL(k_describe<false>, grid, dim3(64 * kDescWaves), 0, st, frames, fstride, pitch0, pyr, blur, ep,
                            levels, lvkey, lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
+    return hipGetLastError();
+}
+
+bool describe_blur_ok(const uint8_t* frames, long long fstride, int pitch0) {
+    return ((((uintptr_t)frames | (uintptr_t)fstride | (uintptr_t)pitch0) & 3) == 0);
+}
+
+hipError_t launch_describe_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                                const ExtractParams& ep, const LevelDesc* levels, const uint32_t* lvkey,
+                                const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc, int* out_counts, int kp_stride,
+                                const int* ptab, int nframes, hipStream_t st) {
+    if (!describe_blur_ok(frames, fstride, pitch0)) return hipErrorInvalidValue;
+    dim3 grid(((ep.kp_per_frame + kFusedKps - 1) / kFusedKps) * nframes);
+    hipLaunchKernelGGL(k_describe_blur, grid, dim3(64 * kFusedWaves), 0, st, frames, fstride, pitch0, pyr, ep, levels,
+                       lvkey, lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
     return hipGetLastError();
 }
 

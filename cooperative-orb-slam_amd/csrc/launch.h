@@ -31,7 +31,8 @@ hipError_t launch_sincos_selftest(const float* in, float* so, float* co, int n, 
 hipError_t launch_octree(const ExtractParams& ep, const LevelDesc* levels, const CellDesc* cells,
                          const uint32_t* cellkey, const int* cellcnt, uint32_t* lvkey, int* lvcnt,
                          uint8_t* gscratch, long long gscratch_frame_bytes, int NC, int KL, int lds_bytes,
-                         int* err, int nframes, hipStream_t st, int level0 = 0, int nlevels = -1);
+                         int* err, int nframes, hipStream_t st, int level0 = 0, int nlevels = -1,
+                         const HostCopy* copy = nullptr);
 /* blur jobs [job0, job1) (ExtractParams::bjob_begin numbers every level's strips) */
 /* FAST over every cell + the blur in kBlurRowsSmall-row chunks (job table eb) in one launch (small batches) */
 hipError_t launch_fast_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
@@ -45,6 +46,12 @@ hipError_t launch_describe(const uint8_t* frames, long long fstride, int pitch0,
                            const uint8_t* blur, const ExtractParams& ep, const LevelDesc* levels,
                            const uint32_t* lvkey, const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc,
                            int* out_counts, int kp_stride, const int* ptab, int nframes, hipStream_t st);
+/* the blur folded into describe (k_describe_blur): level-0 rows must be 4-aligned (describe_blur_ok) */
+bool describe_blur_ok(const uint8_t* frames, long long fstride, int pitch0);
+hipError_t launch_describe_blur(const uint8_t* frames, long long fstride, int pitch0, const uint8_t* pyr,
+                                const ExtractParams& ep, const LevelDesc* levels, const uint32_t* lvkey,
+                                const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc, int* out_counts, int kp_stride,
+                                const int* ptab, int nframes, hipStream_t st);
 
 hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,

@@ -95,6 +95,15 @@ struct ExtractParams {
     int host_out;                    // describe writes into mapped host memory: system-scope fence after the writes
 };
 
+/* extra workgroups of a launch that copy n16 16-byte words src -> dst (mapped pinned host memory): the host path's
+ * delivery of mvImagePyramid (orbx_set_host_pyramid), carried by the one-frame octree launch */
+struct HostCopy {
+    const uint4* src;
+    uint4* dst;
+    long long n16;
+    int nblocks;
+};
+
 /* level containing index g of a per-level prefix table (no dependent loads: unrolled compares
  * against kernel-argument values) */
 __host__ __device__ inline int level_of(const int* begin, int L, int g) {

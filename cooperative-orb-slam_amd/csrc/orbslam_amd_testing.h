@@ -1,0 +1,43 @@
+/*
+ * orbslam_amd_testing.h -- test and measurement hooks of liborbamd.so. Internal: not part of the
+ * drop-in ABI (include/orbslam_amd.h). The tests and bench.py bind them through ctypes
+ * (orbamd/_lib.py); no reference member maps to them and the product never calls them.
+ */
+#ifndef ORBSLAM_AMD_TESTING_H
+#define ORBSLAM_AMD_TESTING_H
+#include "../../include/orbslam_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Test hook: the stages in `mask` (bit k of {pyramid, fast_cells, octree, blur, describe}) are not
+ * launched by subsequent batched extractions of this handle (0 = every stage runs, the default). A
+ * skipped stage leaves its buffers as the previous call left them; the tests use it to prove that
+ * the bench's self-check detects a stage that stopped launching. */
+int orbx_debug_skip_stages(orbx_handle* h, int mask);
+
+/* Measurement hook: on != 0 runs every stage of this handle's subsequent extractions in order on the
+ * caller's stream (no side stream for the blur), so a kernel trace times each kernel alone; 0 = the
+ * default fork/join schedule. Outputs are identical either way. */
+int orbx_debug_serial(orbx_handle* h, int on);
+
+/* Measurement hook (the L2-residency bound of DESIGN.md 6.0): on != 0 makes every frame of this
+ * handle's subsequent batched extractions read frame 0's image and share one pyramid and one blurred
+ * pyramid, so every stage reads data the launch keeps in L2; each frame's outputs are then frame 0's.
+ * Never on in the product; 0 = off (the default). */
+int orbx_debug_alias_frames(orbx_handle* h, int on);
+
+/* Test hook: ORs `flag` (> 0) into the handle's sticky batch error word, as a failing device batch
+ * would; the tests use it to show that host-path extractions (orbx_extract) neither clear nor hide it
+ * and that orbx_check_error reports and clears it once. */
+int orbx_debug_raise_error(orbx_handle* h, int flag, void* stream);
+
+/* Test hook: the device's restatement of glibc sinf/cosf (used by computeOrbDescriptor,
+ * ORBextractor.cc:113) applied to n device floats; lets tests compare against host libm. */
+int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBSLAM_AMD_TESTING_H */

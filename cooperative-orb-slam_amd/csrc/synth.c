@@ -9,7 +9,9 @@
  * 20x15 random grid, values 40..215) + rectangles (8..64 px, intensity 0..255; 400 per
  * 640x480 of texture area) + per-pixel noise in [-3,3]; seed 0x5EED0000 + 1000003*a.
  * Frame t = W x H crop at (16 + (2t mod 600), 8 + (t mod 7)): a slow pan, so consecutive
- * frames share most features (realistic work for the triangulation matcher).
+ * frames share most features (realistic work for the triangulation matcher). Shared-scene
+ * mode (orbx_synth_scene_frames): every agent views one texture from its own crop offset, as
+ * the reference's two agents map one environment (the bench's default at N > 1).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -65,20 +67,30 @@ static uint8_t* make_texture(int agent, int tw, int th) {
     return t;
 }
 
-int orbx_synth_frames_shifted(int agent, int t0, int count, int width, int height, int dx, uint8_t* out) {
-    if (width <= 0 || height <= 0 || count < 0 || !out || agent < 0 || t0 < 0 || dx < 0 || dx > 26)
+/* frame t of view `view` of the texture of `scene`: the crop of view v starts kViewStep*v pixels further along the
+ * pan (modulo the pan's 600 px), so the views of one scene are agents looking at one environment from places a
+ * few dozen pixels apart; view 0 is the scene's own stream (orbx_synth_frames_shifted(scene, ...)) */
+enum { kViewStep = 12 };
+
+int orbx_synth_scene_frames(int scene, int view, int t0, int count, int width, int height, int dx, uint8_t* out) {
+    if (width <= 0 || height <= 0 || count < 0 || !out || scene < 0 || view < 0 || view > 4096 || t0 < 0 || dx < 0 ||
+        dx > 26)
         return ORBX_EARG;
     const int tw = width + 640, th = height + 32;
-    uint8_t* tex = make_texture(agent, tw, th);
+    uint8_t* tex = make_texture(scene, tw, th);
     if (!tex) return ORBX_EARG;
     for (int f = 0; f < count; f++) {
         int t = t0 + f;
-        int ox = 16 + (2 * t) % 600 + dx, oy = 8 + t % 7;
+        int ox = 16 + (int)((2ll * t + (long long)kViewStep * view) % 600) + dx, oy = 8 + t % 7;
         for (int y = 0; y < height; y++)
             memcpy(out + ((size_t)f * height + y) * width, tex + (size_t)(oy + y) * tw + ox, (size_t)width);
     }
     free(tex);
     return ORBX_OK;
+}
+
+int orbx_synth_frames_shifted(int agent, int t0, int count, int width, int height, int dx, uint8_t* out) {
+    return orbx_synth_scene_frames(agent, 0, t0, count, width, height, dx, out);
 }
 
 int orbx_synth_frames(int agent, int t0, int count, int width, int height, uint8_t* out) {

@@ -62,6 +62,9 @@ int ORBextractor::ensureHandle(int width, int height) {
     mpHandle = h;
     mHandleW = width;
     mHandleH = height;
+    // eager mvImagePyramid: every call also delivers the levels into the handle's pinned memory (copied beside the
+    // octree on the device), so SyncImagePyramid only points the member's Mats at them
+    if (HostPyramidEager()) amd::StatusOk(orbx_set_host_pyramid(h, 1), "orbx_set_host_pyramid");
     return ORBX_OK;
 }
 
@@ -123,6 +126,20 @@ bool ORBextractor::HostPyramidEager() const {
 const std::vector<cv::Mat>& ORBextractor::SyncImagePyramid() {
     if (!mbPyramidStale) return mvImagePyramid;
     mbPyramidStale = false;
+    // the levels the last call delivered to pinned host memory (orbx_set_host_pyramid): the member's Mats are headers
+    // over them (no copy). Like the reference's member they hold this frame's levels until the next operator() call.
+    bool mapped = mpHandle != nullptr;
+    for (int l = 0; l < nlevels && mapped; l++) {
+        const uint8_t* p = nullptr;
+        size_t step = 0;
+        int w = 0, h = 0;
+        if (orbx_host_pyramid_level(mpHandle, l, &p, &step, &w, &h) != ORBX_OK) {
+            mapped = false;
+            break;
+        }
+        mvImagePyramid[l] = cv::Mat(h, w, CV_8U, (void*)p, step);
+    }
+    if (mapped) return mvImagePyramid;
     for (int l = 0; l < nlevels; l++) {
         int w = 0, h = 0;
         int rc = mpHandle ? orbx_pyramid_level(mpHandle, 0, l, nullptr, 0, &w, &h) : ORBX_EDEVICE;

@@ -14,7 +14,10 @@
  *
  * mvImagePyramid: by default every operator() fills the public member with this frame's levels, as the
  * reference does (ORBextractor.cc:1107-1132), so stock readers (Frame::ComputeStereoMatches, A1
- * Frame.cc:474-581) see the current frame. When the drop-in Frame::ComputeStereoMatches
+ * Frame.cc:474-581) see the current frame: the device writes the levels into the handle's pinned host
+ * memory during the call (orbx_set_host_pyramid) and the member's Mats are headers over that memory,
+ * holding this frame's levels until the next operator() call on this extractor (a reader that keeps a
+ * level past that must clone it). When the drop-in Frame::ComputeStereoMatches
  * (host/Frame_stereo_amd.cc) is linked in, it registers itself as the reader of the device copy and the
  * extractor skips the PCIe copy; the member is then filled lazily by SyncImagePyramid() (once per call).
  * ORBAMD_HOST_PYRAMID=1 / 0 forces the eager / lazy form.

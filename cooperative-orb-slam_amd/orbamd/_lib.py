@@ -98,6 +98,8 @@ SIGNATURES = {
     "orbx_extract": (_I, [_P, _P, _I, _I, _SZ, _P, _P, _I, C.POINTER(_I)]),
     "orbx_extract_batch_device": (_I, [_P, _I, _P, _SZ, _I, _I, _SZ, _P, _P, _P, _I, _P]),
     "orbx_pyramid_level": (_I, [_P, _I, _I, _P, _SZ, C.POINTER(_I), C.POINTER(_I)]),
+    "orbx_set_host_pyramid": (_I, [_P, _I]),
+    "orbx_host_pyramid_level": (_I, [_P, _I, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_I), C.POINTER(_I)]),
     "orbx_get_levels": (_I, [_P]),
     "orbx_get_scale_factor": (_F, [_P]),
     "orbx_get_scale_tables": (_I, [_P, _P, _P, _P, _P]),
@@ -134,6 +136,7 @@ SIGNATURES = {
     "orbx_synth_frame": (_I, [_I, _I, _I, _I, _P]),
     "orbx_synth_frames": (_I, [_I, _I, _I, _I, _I, _P]),
     "orbx_synth_frames_shifted": (_I, [_I, _I, _I, _I, _I, _I, _P]),
+    "orbx_synth_scene_frames": (_I, [_I, _I, _I, _I, _I, _I, _I, _P]),
     "orbx_compute_stereo_matches": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _P, _P, C.POINTER(_I)]),
     "orbx_stereo_matches_batch_device": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _P, _P, _P,
                                               _P]),

@@ -14,13 +14,19 @@ from ._lib import KP_FIELDS, OrbxParams, check, load
 kp_dtype = np.dtype(KP_FIELDS)
 
 
-def synth_frames(agent, t0, count, width, height, dx=0):
+def synth_frames(agent, t0, count, width, height, dx=0, scene=None):
     """Deterministic synthetic frames; returns uint8 [count, H, W]. dx > 0 gives the
-    right image of a rectified stereo pair (the same crop shifted by dx px: disparity dx)."""
+    right image of a rectified stereo pair (the same crop shifted by dx px: disparity dx). scene=None: agent's
+    own texture; scene=s: agent's view of the shared texture of scene s (orbx_synth_scene_frames: the agents'
+    crops 12 px apart along the pan, overlapping views of one environment)."""
     lib = load()
     out = np.empty((count, height, width), np.uint8)
-    check(lib.orbx_synth_frames_shifted(agent, t0, count, width, height, dx, out.ctypes.data),
-          "orbx_synth_frames_shifted")
+    if scene is None:
+        check(lib.orbx_synth_frames_shifted(agent, t0, count, width, height, dx, out.ctypes.data),
+              "orbx_synth_frames_shifted")
+    else:
+        check(lib.orbx_synth_scene_frames(scene, agent, t0, count, width, height, dx, out.ctypes.data),
+              "orbx_synth_scene_frames")
     return out
 
 

@@ -95,6 +95,19 @@ int orbx_check_error(orbx_handle* h, void* stream);
 int orbx_pyramid_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t pitch,
                        int* width, int* height);
 
+/* public ORBextractor::mvImagePyramid (ORBextractor.h:85, filled by ComputePyramid in every
+ * operator() call, ORBextractor.cc:1107-1132) delivered eagerly for the host path without a
+ * copy after the call: with on != 0 every subsequent orbx_extract on `h` also writes the frame's
+ * levels 1..L-1 into pinned host memory from extra workgroups of its octree launch (they copy
+ * while the octree runs, so the call's latency does not grow), and orbx_host_pyramid_level then
+ * points at level `level` of the last orbx_extract (level 0: the call's pinned copy of the
+ * input image). The memory belongs to the handle: valid until the next orbx_extract,
+ * orbx_set_host_pyramid or orbx_destroy on it. ORBX_EARG when the last call delivered none
+ * (host pyramid off, or a stage-profiled call). */
+int orbx_set_host_pyramid(orbx_handle* h, int on);
+int orbx_host_pyramid_level(orbx_handle* h, int level, const uint8_t** data, size_t* pitch,
+                            int* width, int* height);
+
 /* ORBextractor getters (ORBextractor.h:63-81): GetLevels, GetScaleFactor,
  * GetScaleFactors, GetInverseScaleFactors, GetScaleSigmaSquares,
  * GetInverseScaleSigmaSquares. Arrays have nlevels entries. */
@@ -592,7 +605,9 @@ int orbm_search_for_triangulation_slots_device(orbm_ctx* ctx, const orbx_kf_sour
  * of the two FeatureVectors (query nodes <= max_nodes). Outputs d_match[r*cap1 + idx1] = the
  * slot keyframe's feature idx2 whose MapPoint vpMatches12[idx1] is (or -1), after the
  * rotation filter when check_ori, and d_nmatches[r]. A slot that fails validation contributes
- * no matches and raises the ctx's device error flag (orbm_check_error). */
+ * no matches and raises the ctx's device error flag (orbm_check_error). Slots may carry a
+ * larger capacity than the query (agents with other feature counts): a common node is matched
+ * whole up to 4551 candidates (one CU's LDS); a node past that raises the error flag. */
 int orbm_search_by_bow_slots_device(orbm_ctx* ctx, const orbx_kf_source* query, int cap1, int nref,
                                     const uint8_t* d_slots, size_t slot_bytes, float nnratio, int check_ori,
                                     int max_nodes, int32_t* d_match, int32_t* d_nmatches, void* stream);
@@ -641,6 +656,11 @@ int orbx_synth_frames(int agent, int t0, int count, int width, int height, uint8
  * in x (0 <= dx <= 26), i.e. a fronto-parallel scene at disparity dx. */
 int orbx_synth_frames_shifted(int agent, int t0, int count, int width, int height, int dx,
                               uint8_t* out);
+/* shared-scene frames: view `view` (an agent) of the texture of `scene`, its crop 12*view pixels
+ * further along the pan (mod 600), so several agents see overlapping parts of one environment as
+ * A1 and A2 do; view 0 equals orbx_synth_frames_shifted(scene, ...). */
+int orbx_synth_scene_frames(int scene, int view, int t0, int count, int width, int height, int dx,
+                            uint8_t* out);
 
 /* Stage profiling: a pair of HIP events brackets each stage's kernel on the stream it is
  * launched on (the overlapped schedule is kept, so a stage's time includes sharing the GPU
@@ -657,32 +677,6 @@ int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls);
  * can start its own work once this batch's pyramid is done (bench schedules that stagger concurrent
  * extraction graphs by pyramid rather than by whole extraction). */
 int orbx_set_pyramid_event(orbx_handle* h, void* event);
-
-/* Test hook: the stages in `mask` (bit k of {pyramid, fast_cells, octree, blur, describe}) are not
- * launched by subsequent batched extractions of this handle (0 = every stage runs, the default). A
- * skipped stage leaves its buffers as the previous call left them; the tests use it to prove that
- * the bench's self-check detects a stage that stopped launching. */
-int orbx_debug_skip_stages(orbx_handle* h, int mask);
-
-/* Measurement hook: on != 0 runs every stage of this handle's subsequent extractions in order on the
- * caller's stream (no side stream for the blur), so a kernel trace times each kernel alone; 0 = the
- * default fork/join schedule. Outputs are identical either way. */
-int orbx_debug_serial(orbx_handle* h, int on);
-
-/* Measurement hook (the L2-residency bound of DESIGN.md 6.0): on != 0 makes every frame of this
- * handle's subsequent batched extractions read frame 0's image and share one pyramid and one blurred
- * pyramid, so every stage reads data the launch keeps in L2; each frame's outputs are then frame 0's.
- * Never on in the product; 0 = off (the default). */
-int orbx_debug_alias_frames(orbx_handle* h, int on);
-
-/* Test hook: ORs `flag` (> 0) into the handle's sticky batch error word, as a failing device batch
- * would; the tests use it to show that host-path extractions (orbx_extract) neither clear nor hide it
- * and that orbx_check_error reports and clears it once. */
-int orbx_debug_raise_error(orbx_handle* h, int flag, void* stream);
-
-/* Test hook: the device's restatement of glibc sinf/cosf (used by computeOrbDescriptor,
- * ORBextractor.cc:113) applied to n device floats; lets tests compare against host libm. */
-int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, void* stream);
 
 /* Library/version and device probe. */
 const char* orbx_version(void);

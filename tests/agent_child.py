@@ -28,7 +28,8 @@ def main():
         dist.all_gather_into_tensor(o, inp.cpu().clone())
         out.copy_(o.to(out.device))
 
-    frames = orbamd.synth_frames(rank, 0, B, W, H)
+    # both agents view one synthetic environment (shared scene, crops 12 px apart), as A1 and A2 do
+    frames = orbamd.synth_frames(rank, 0, B, W, H, scene=0)
     # the exchange on its own stream, as bench.py runs it whenever a collective does
     sched = AgentSchedule(torch, frames, W, H, P, device=0, rank=rank, world=world, allgather=allgather,
                           async_exchange=True)
@@ -36,12 +37,13 @@ def main():
     sched.step(first=False)
     torch.cuda.synchronize()
     sched.check_errors()
-    res = check_schedule(sched, frames, agent_frames=lambda r, t: orbamd.synth_frames(r, t, 1, W, H)[0])
+    res = check_schedule(sched, frames, agent_frames=lambda r, t: orbamd.synth_frames(r, t, 1, W, H, scene=0)[0])
     xm, xn, xb, xbn = sched.exchange_results()
     print("rank", rank, res, "cross-agent matches", list(xn), "SearchByBoW", list(xbn), flush=True)
     assert res["bit_exact"], res["mismatches"]
-    # every slot checked bit-exact above; its own keyframe gives both matchers work
-    assert res["checked_slots"] == world and int(xn[rank]) > 0 and int(xbn[rank]) > 0
+    # every slot checked bit-exact above; every agent's keyframe (a view of the same scene) gives both matchers work
+    assert res["checked_slots"] == world
+    assert all(int(v) > 0 for v in xn) and all(int(v) > 0 for v in xbn), (list(xn), list(xbn))
     sched.close()
     dist.barrier()
     dist.destroy_process_group()

@@ -44,3 +44,11 @@ g++ -std=c++14 -O2 -Wall -I "$R/include" -I "$R/oracle" "$R/tests/cpp/bench_late
   -L "$R/cooperative-orb-slam_amd/lib" -lorbamd -L "$R/oracle/build" -lorb_oracle \
   -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,"$R/oracle/build" -Wl,-rpath,/opt/rocm/lib \
   -o "$R/tests/cpp/build/bench_latency"
+# the drop-in class's per-call latency in its default (eager mvImagePyramid) form, and a stereo pair on two threads
+g++ -std=c++14 -O2 -pthread -Wall -Wno-unused-function \
+  -I "$R/tests/cpp/cvmin" -I "$R/cooperative-orb-slam_amd/host" -I "$R/include" -I "$R/oracle" \
+  "$R/tests/cpp/bench_dropin_latency.cpp" "$R/cooperative-orb-slam_amd/host/ORBextractor.cc" \
+  "$R/cooperative-orb-slam_amd/host/orbamd_status.cc" \
+  -L "$R/cooperative-orb-slam_amd/lib" -lorbamd -L "$R/oracle/build" -lorb_oracle \
+  -Wl,-rpath,"$R/cooperative-orb-slam_amd/lib" -Wl,-rpath,"$R/oracle/build" -Wl,-rpath,/opt/rocm/lib \
+  -o "$R/tests/cpp/build/bench_dropin_latency"

@@ -45,6 +45,19 @@ def test_synth_frames_deterministic():
     assert 60 < a.mean() < 190 and a.std() > 20
 
 
+def test_synth_scene_views_overlap():
+    """Shared-scene mode: view 0 of scene s is agent s's own stream; view v is the same texture with the crop
+    12*v px further along the pan, so two agents' frames at one time step overlap by all but 12*|dv| columns."""
+    W, H = 640, 480
+    a0 = orbamd.synth_frames(0, 4, 2, W, H)
+    assert np.array_equal(orbamd.synth_frames(0, 4, 2, W, H, scene=0), a0)
+    v2 = orbamd.synth_frames(2, 4, 2, W, H, scene=0)
+    assert not np.array_equal(v2, a0)
+    assert np.array_equal(v2[:, :, :W - 24], a0[:, :, 24:])  # view 2 starts 24 px to the right
+    assert np.array_equal(orbamd.synth_frames(3, 4, 1, W, H, dx=5, scene=0)[0, :, :W - 5],
+                          orbamd.synth_frames(3, 4, 1, W, H, scene=0)[0, :, 5:])
+
+
 def test_descriptor_distance_host():
     rng = np.random.default_rng(0)
     for _ in range(100):

@@ -23,7 +23,7 @@ def _free_port():
 def _agent_keyframe(agent):
     import oracle_py
     import orbamd
-    img = orbamd.synth_frames(agent, 0, 1, 640, 480)[0]
+    img = orbamd.synth_frames(agent, 0, 1, 640, 480, scene=0)[0]  # the agents' views of one scene
     orc = oracle_py.OracleExtractor()
     k, d = orc(img)
     return k, d, orc.tables()
@@ -130,3 +130,7 @@ def test_gloo_allgather_cross_agent_match():
         # are found by the loop-candidate SearchByBoW
         assert sum(x >= 0 for x in got[r][2 * r]) > 0.3 * len(kfs[r][0])
         assert sum(x >= 0 for x in got[r][2 * r + 1]) > 0.3 * len(kfs[r][0])
+        # and the other agent's view of the scene gives both cross-agent matchers real work
+        o = 1 - r
+        assert sum(x >= 0 for x in got[r][2 * o]) > 0.1 * len(kfs[r][0]), sum(x >= 0 for x in got[r][2 * o])
+        assert sum(x >= 0 for x in got[r][2 * o + 1]) > 0.1 * len(kfs[r][0]), sum(x >= 0 for x in got[r][2 * o + 1])

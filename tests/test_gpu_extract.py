@@ -184,3 +184,44 @@ def test_host_path_keeps_the_sticky_batch_error():
     assert len(kg) > 900
     assert lib.orbx_check_error(ext._h, None) == -2  # ORBX_EDEVICE
     assert lib.orbx_check_error(ext._h, None) == 0   # cleared by the read
+
+
+def test_host_pyramid_delivery():
+    """orbx_set_host_pyramid (the eager mvImagePyramid of the host path, ORBextractor.cc:1107-1132): the levels the
+    octree launch's extra workgroups copy into pinned host memory equal the oracle's pyramid on consecutive distinct
+    frames (captured-graph replays included) and the device copy (orbx_pyramid_level); ORBX_EARG when off, before the
+    first call and for a stage-profiled call; the keypoints stay bit-exact with the copy on."""
+    import ctypes as C
+    W, H = 752, 480
+    frames = orbamd.synth_frames(3, 7, 4, W, H)
+    ext = orbamd.ORBextractor(1200, 1.2, 8, 20, 7, max_width=W, max_height=H)
+    orc = oracle_py.OracleExtractor(1200, 1.2, 8, 20, 7)
+    lib = orbamd.load()
+    p, pitch, w, h = C.c_void_p(), C.c_size_t(), C.c_int(), C.c_int()
+
+    def level(lv):
+        rc = lib.orbx_host_pyramid_level(ext._h, lv, C.byref(p), C.byref(pitch), C.byref(w), C.byref(h))
+        if rc:
+            return rc
+        buf = (C.c_uint8 * (pitch.value * h.value)).from_address(p.value)
+        return np.frombuffer(buf, np.uint8).reshape(h.value, pitch.value)[:, :w.value].copy()
+
+    assert lib.orbx_set_host_pyramid(ext._h, 1) == 0
+    assert level(0) == -1  # nothing delivered yet
+    for f in range(frames.shape[0]):
+        kg, dg = ext(frames[f])
+        ko, do = orc(frames[f])
+        _compare(kg, dg, ko, do)
+        for lv in range(8):
+            got = level(lv)
+            assert isinstance(got, np.ndarray), (f, lv, got)
+            np.testing.assert_array_equal(got, orc.pyramid(lv), err_msg="frame %d level %d" % (f, lv))
+            np.testing.assert_array_equal(got, ext.pyramid_level(lv))
+    assert lib.orbx_set_host_pyramid(ext._h, 0) == 0
+    ext(frames[0])
+    assert level(1) == -1  # off: no host copy
+    assert lib.orbx_set_host_pyramid(ext._h, 1) == 0
+    assert lib.orbx_profile_enable(ext._h, 0x1F) == 0
+    ext(frames[1])
+    assert level(1) == -1  # a stage-profiled call delivers none
+    ext.close()
