@@ -272,8 +272,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
-    ap.add_argument("--batch", type=int, default=1024, help="frames per step per GPU")
-    ap.add_argument("--pipes", type=int, default=4,
+    ap.add_argument("--batch", type=int, default=2304, help="frames per step per GPU")
+    ap.add_argument("--pipes", type=int, default=3,
                     help="concurrent extraction+match graphs per GPU (each over batch/pipes frames, own handle "
                          "and HIP stream), staggered: graph p starts a step when graph p-1 finished extracting it")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="all-cores CPU leg: total seconds (5 runs)")
@@ -320,8 +320,14 @@ def main():
                     help="graph p starts extracting after graph p-1's extraction: every step / only in the "
                          "first step of a run (the phase offset then persists) / never / in the first step and every "
                          "K-th step after it")
+    ap.add_argument("--launch-frames", action="store_true",
+                    help="print the frames one stage launch processes (--batch / --pipes) and the graph count, and exit "
+                         "(no GPU use)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    if args.launch_frames:
+        print(args.batch // args.pipes, args.pipes)
+        return
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -544,10 +550,12 @@ def main():
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if args.config == "c2" else
                                 "pmc_traffic_%s.json" % args.config)
         pmc = {}
-        if os.path.exists(pmc_path) and sub == 256:
+        if os.path.exists(pmc_path):
             try:
                 pmc = json.load(open(pmc_path))
             except Exception:
+                pmc = {}
+            if pmc.get("frames_per_launch", 256) != sub:  # counters of another launch size do not price this one
                 pmc = {}
         sel = ("largest stage of this run's stage split (%s)" % ", ".join("%s %.3f ms" % (k, stage_ms[k]) for k in stages)
                if args.roof_kernel == "auto" else "--roof-kernel")

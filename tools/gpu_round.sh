@@ -27,9 +27,11 @@ for step in "$@"; do
     prof)
       tools/prof_round.sh $T || exit $?
       kt=$(find gpurun_out/${T}_kt -name '*kernel_trace.csv' | head -n 1)
-      python3 tools/trace_segments.py "$kt" 10 2 > gpurun_out/${T}_timed_region_kernels.txt || exit $?
+      read sub pipes < <(python3 bench.py --launch-frames)
+      python3 tools/trace_segments.py "$kt" 10 2 $pipes > gpurun_out/${T}_timed_region_kernels.txt || exit $?
       python3 tools/exchange_kernels.py "$kt" > gpurun_out/${T}_exchange_kernels.txt || exit $?
-      tools/prof_reduce.sh $T ;;
+      python3 tools/queue_map.py "$kt" > gpurun_out/${T}_queue_map.txt || exit $?
+      tools/prof_reduce.sh $T $sub ;;
     bench_driver) tools/gpu_run.sh "300 ${T}_bench_driver python3 bench.py --gpus 1 --steps 20 --warmup 5" || exit $? ;;
     bench) tools/gpu_run.sh "300 ${T}_bench python3 bench.py" || exit $? ;;
     c3) tools/gpu_run.sh "300 ${T}_bench_c3 python3 bench.py --config c3 --gpus 1 --steps 20 --warmup 5" || exit $? ;;

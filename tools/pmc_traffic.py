@@ -6,7 +6,8 @@ For a stage launched with different grids (FAST: level-0 and other-level launche
 overlapped schedule, one whole-grid launch in the stage-serial profiling pass) the whole-grid
 launch is reported, which is the launch bench.py's roofline times.
 Optionally a counter pass with SQ_INSTS_VALU adds the VALU instructions per launch.
-usage: pmc_traffic.py fetch.csv write.csv out.json [valu_pass.csv]"""
+usage: pmc_traffic.py fetch.csv write.csv out.json [valu_pass.csv [frames_per_launch]]
+(frames_per_launch, default 256: the bench's B / P, recorded so bench.py prices launches of that size only)"""
 import collections
 import csv
 import json
@@ -43,8 +44,11 @@ for st in STAGES:
                "WRITE_SIZE_KiB_avg_per_dispatch": w, "hbm_bytes_per_launch": (f + w) * 1024.0}
     if (st, g) in valu:
         out[st]["valu_insts_per_launch"] = sum(valu[(st, g)]) / len(valu[(st, g)])
+out["frames_per_launch"] = int(sys.argv[5]) if len(sys.argv) > 5 else 256
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 for k, v in out.items():
+    if not isinstance(v, dict):
+        continue
     print("%-10s grid %9d  fetch %10.0f KiB  write %9.0f KiB  -> %.1f MB/launch" % (
         k, v["grid"], v["FETCH_SIZE_KiB_avg_per_dispatch"], v["WRITE_SIZE_KiB_avg_per_dispatch"],
         v["hbm_bytes_per_launch"] / 1e6))
