@@ -272,7 +272,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
-    ap.add_argument("--batch", type=int, default=2304, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=3072, help="frames per step per GPU")
     ap.add_argument("--pipes", type=int, default=3,
                     help="concurrent extraction+match graphs per GPU (each over batch/pipes frames, own handle "
                          "and HIP stream), staggered: graph p starts a step when graph p-1 finished extracting it")

@@ -2,14 +2,16 @@
  * extract_kernels.hip -- gfx950 kernels for ORBextractor::operator() (ORBextractor.cc:1043-1105).
  *
  * One launch per stage over a whole batch of frames (grid.y / grid.z = frame):
- *   k_resize_tiled   ComputePyramid, one launch per level 1..L-1      (ORBextractor.cc:1107-1132)
- *                    (k_resize_level: untiled form for windows that do not fit the LDS tile)
+ *   k_pyramid_frames ComputePyramid, one workgroup per frame (or row band)  (ORBextractor.cc:1107-1132)
+ *                    (k_resize_tiled / k_resize_level: per-level forms for geometries it does not fit)
  *   k_fast_cells2    per-cell cv::FAST + 3x3 NMS + threshold fallback (ORBextractor.cc:789-829)
  *   k_octree         DistributeOctTree, one workgroup per (frame,level) (ORBextractor.cc:539-763)
- *   k_blur_strips    GaussianBlur 7x7 sigma 2 REFLECT_101 per level   (ORBextractor.cc:1085-1086)
- *   k_describe       IC_Angle + rBRIEF + output assembly, one wave per keypoint
- *                    (ORBextractor.cc:77-147, 851-852, 1075-1104)
- * capi.cpp runs them as a fork/join graph on two streams (DESIGN.md "Schedule").
+ *   k_describe_blur  GaussianBlur 7x7 sigma 2 REFLECT_101 of each keypoint's window + IC_Angle + rBRIEF +
+ *                    output assembly, 16 lanes per keypoint (ORBextractor.cc:77-147, 851-852, 1075-1104)
+ *   k_blur_strips +  the same as two stages (whole-level blur, then describe) for frames whose level-0 rows
+ *   k_describe       are not 4-aligned
+ * capi.cpp runs them in order on the caller's stream (the separate blur on a side stream beside FAST and the
+ * octree; DESIGN.md "Schedule").
  * All of it is integer/byte work bounded by HBM/LDS and VALU issue; no MFMA.
  * Exact-semantics notes live in DESIGN.md "Pinned semantics".
  */
@@ -1768,10 +1770,7 @@ constexpr int kFusedRows = 43;   // source rows y-21 .. y+21
 constexpr int kFusedPitch = 48;  // 12 dwords: columns cx0 .. cx0+47 cover x-21 .. x+21 for any (x-22) & 3
 constexpr int kFusedDwords = kFusedRows * kFusedPitch / 4;  // 516 per keypoint
 
-#ifndef ORBX_FUSED_WAVES
-#define ORBX_FUSED_WAVES 4
-#endif
-constexpr int kFusedWaves = ORBX_FUSED_WAVES;  // waves (x 4 keypoints) per k_describe_blur workgroup
+constexpr int kFusedWaves = 4;  // waves (x 4 keypoints) per k_describe_blur workgroup (2 and 1 measured: +-1 %, -5 %)
 constexpr int kFusedKps = 4 * kFusedWaves;
 
 __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
@@ -2048,241 +2047,6 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     if (ep.host_out) __threadfence_system();
 }
 
-/* ----------------------------------------------------------------------------------- */
-/* The same fusion with the source rows streamed through registers (no LDS staging of    */
-/* the unblurred window): lane ln (0..11) of a keypoint's 16 loads dword ln of each       */
-/* source row y-21..y+21 (columns cx0 + 4 ln, cx0 = (x-22) & ~3; 7 rows in flight), and    */
-/* gets dwords ln-1 / ln+1 of its neighbours by DPP row_shr / row_shl (a keypoint's 16     */
-/* lanes are one DPP row), so the row sums need no LDS at all; lanes 1..10 walk the 7-row */
-/* window and write the blurred 37 x 40 patch straight into k_describe's LDS layout       */
-/* (dword ln-1 of patch row r; cx0 + 4 = x - 18 - pmis), which rBRIEF samples as there.   */
-/* IC_Angle reads the unblurred rows from the level as k_describe does. LDS per keypoint */
-/* is k_describe's 1480 B (5 workgroups per CU). Edge keypoints (source window past an    */
-/* image edge) assemble each lane's dword from four REFLECT_101 byte loads.               */
-/* ----------------------------------------------------------------------------------- */
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void k_describe_blur_rs(
-    const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
-    ExtractParams ep, const LevelDesc* __restrict__ levels, const uint32_t* __restrict__ lvkey,
-    const int* __restrict__ lvcnt, orbx_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
-    int* __restrict__ out_counts, int kp_stride, const int* __restrict__ ptab) {
-    constexpr int KPS = 4 * NW;
-    __shared__ PatPt s_pat[256];
-    __shared__ int2 s_ic[256];
-    __shared__ __align__(8) uint8_t s_patch[KPS][kDescPatchRows * kDescPatchPitch];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int sub = lane >> 4, ln = lane & 15;
-    const int G = (ep.kp_per_frame + KPS - 1) / KPS;
-    int f, blk;
-    {
-        const int b = blockIdx.x;
-        if ((gridDim.x / G) % 8 == 0) {
-            const int k = b >> 3;
-            f = (b & 7) + 8 * (k / G);
-            blk = k % G;
-        } else {
-            f = b / G;
-            blk = b % G;
-        }
-    }
-    constexpr int NT = 64 * NW;
-    constexpr int kTab = (256 + NT - 1) / NT;
-    PatPt my_pat[kTab];
-    int2 my_ic[kTab];
-#pragma unroll
-    for (int q = 0; q < kTab; q++) {
-        const int t = min(tid + q * NT, 255);
-        my_pat[q] = kPatternT.t[t];
-        my_ic[q] = ((const int2*)(ptab + ep.ic_off))[t];
-    }
-    const int g = (blk * NW + wave) * 4 + sub;
-    const int gc = min(g, ep.kp_per_frame - 1);
-    const uint32_t kk_raw = lvkey[(long long)f * ep.kp_per_frame + gc];
-    const int* cnt = lvcnt + f * ep.L;
-    int cl[kMaxLevels];
-#pragma unroll
-    for (int q = 0; q < kMaxLevels; q++) cl[q] = q < ep.L ? cnt[q] : 0;
-#pragma unroll
-    for (int q = 0; q < kTab; q++) {
-        const int t = tid + q * NT;
-        if (t >= 256) break;
-        s_pat[t] = my_pat[q];
-        s_ic[t] = my_ic[q];
-    }
-    if (blk == 0 && tid == 0) {
-        int tot = 0;
-#pragma unroll
-        for (int q = 0; q < kMaxLevels; q++) tot += cl[q];
-        out_counts[f] = tot;
-        if (ep.host_out) __threadfence_system();
-    }
-    __syncthreads();
-    if (__ballot(g < ep.kp_per_frame) == 0) return;  // wave-uniform
-    const int l = level_of(ep.kp_off, ep.L, gc);
-    const int k = gc - ep.kp_off[l];
-    int mycnt = 0, outidx = k;
-#pragma unroll
-    for (int q = 0; q < kMaxLevels; q++) {
-        mycnt = q == l ? cl[q] : mycnt;
-        outidx += q < l ? cl[q] : 0;
-    }
-    const bool valid = g < ep.kp_per_frame && k < mycnt;
-    if (__ballot(valid) == 0) return;  // wave-uniform
-    const LevelDesc lv = levels[l];
-    const uint32_t kk = valid ? kk_raw : 0u;
-    const int x = valid ? (int)(kk & 0xFFF) : 32, y = valid ? (int)((kk >> 12) & 0xFFF) : 32;
-    const int resp = (int)(kk >> 24);
-    const uint8_t* img = l == 0 ? frames + (long long)f * fstride : pyr + (long long)f * ep.pyr_frame_bytes + lv.pyr_off;
-    const int pitch = l == 0 ? pitch0 : lv.pitch;  // every row 4-aligned (describe_blur_ok)
-    // IC_Angle rows (unblurred level), one load round as k_describe<true>
-    const int g4 = ln & 7, r = ln >> 3;
-    const int off0 = (y + r - 15) * pitch + x - 15 + 4 * g4;
-    const uint32_t mis = ((uint32_t)(uintptr_t)img + (uint32_t)off0) & 3u;
-    uint2 wv[16];
-#pragma unroll
-    for (int p = 0; p < 16; p++) wv[p] = *(const uint2*)(img + ((uint32_t)off0 + (uint32_t)(2 * p * pitch) - mis));
-    // blur source: dword ln of rows y-21 .. y+21, columns cx0 + 4 ln (lanes 12..15 repeat dword 11, unused)
-    const int cx0 = (x - 22) & ~3;
-    const int pmis = (x - 18) & 3;  // cx0 + 4 = x - 18 - pmis: k_describe's patch origin
-    const int lastd = (lv.w - 1) & ~3;
-    const int ldw = min(ln, 11);
-    const bool edge = y < 21 || y + 21 >= lv.h || x < 22 || x + 21 >= lv.w || cx0 + 44 > lastd;
-    const uint8_t* rowbase = img + (long long)(y - 21) * pitch + cx0 + 4 * ldw;
-    auto ld = [&](int i) -> uint32_t {
-        if (!edge) return *(const uint32_t*)(rowbase + (long long)i * pitch);
-        const uint8_t* row = img + (long long)reflect101(y - 21 + i, lv.h) * pitch;
-        uint32_t v = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) v |= (uint32_t)row[reflect101(cx0 + 4 * ldw + b, lv.w)] << (8 * b);
-        return v;
-    };
-    uint32_t D[7];  // source row i in D[i % 7]
-#pragma unroll
-    for (int m = 0; m < 7; m++) D[m] = ld(m);
-    int m10, m01;
-    {
-        uint32_t Ap = 0, S = 0, Mp = 0;
-#pragma unroll
-        for (int p = 0; p < 16; p++) {
-            const int ri = r + 2 * p;
-            const uint32_t I4 = __builtin_amdgcn_alignbyte(wv[p].y, wv[p].x, mis);
-            const int2 msk = s_ic[ri * 8 + g4];
-            const uint32_t sI = __builtin_amdgcn_udot4(I4, (uint32_t)msk.y, 0u, false);
-            Ap = __builtin_amdgcn_udot4(I4, (uint32_t)msk.x, Ap, false);
-            S += sI;
-            Mp += __umul24(sI, 2u * (uint32_t)p);
-        }
-        int A = (int)Ap - 15 * (int)S, M = (int)Mp + (r - 15) * (int)S;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) {
-            A += __shfl_xor(A, o, 16);
-            M += __shfl_xor(M, o, 16);
-        }
-        m10 = A;
-        m01 = M;
-    }
-    uint8_t* patch = s_patch[wave * 4 + sub];
-    {
-        const int col0 = cx0 + 4 * ln;  // image column of this lane's first output (lanes 1..10 own outputs)
-        const bool tail = col0 + 3 >= lv.blur_vec_end;
-        const bool owner = ln >= 1 && ln <= 10;
-        uint32_t* dsw = (uint32_t*)patch + (ln - 1);
-        constexpr uint32_t A0 = 18u << 8 | 34u << 16 | 49u << 24, B0 = 55u | 49u << 8 | 34u << 16 | 18u << 24;
-        constexpr uint32_t A1 = 18u << 16 | 34u << 24, B1 = 49u | 55u << 8 | 49u << 16 | 34u << 24, C1 = 18u;
-        constexpr uint32_t A2 = 18u << 24, B2 = 34u | 49u << 8 | 55u << 16 | 49u << 24, C2 = 34u | 18u << 8;
-        constexpr uint32_t B3 = 18u | 34u << 8 | 49u << 16 | 55u << 24, C3 = 49u | 34u << 8 | 18u << 16;
-        auto rowsum = [&](uint32_t b, float2v& lo, float2v& hi) {
-            // dwords ln-1 and ln+1 from the neighbouring lanes of this keypoint's DPP row
-            const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0x111, 0xF, 0xF, false);  // row_shr:1
-            const uint32_t c = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0x101, 0xF, 0xF, false);  // row_shl:1
-            const uint32_t o0 = __builtin_amdgcn_udot4(a, A0, __builtin_amdgcn_udot4(b, B0, 0u, false), false);
-            const uint32_t o1 = __builtin_amdgcn_udot4(
-                a, A1, __builtin_amdgcn_udot4(b, B1, __builtin_amdgcn_udot4(c, C1, 0u, false), false), false);
-            const uint32_t o2 = __builtin_amdgcn_udot4(
-                a, A2, __builtin_amdgcn_udot4(b, B2, __builtin_amdgcn_udot4(c, C2, 0u, false), false), false);
-            const uint32_t o3 = __builtin_amdgcn_udot4(b, B3, __builtin_amdgcn_udot4(c, C3, 0u, false), false);
-            lo = (float2v){(float)o0, (float)o1};
-            hi = (float2v){(float)o2, (float)o3};
-        };
-        float2v WL[7], WH[7];
-#pragma unroll
-        for (int m = 0; m < 6; m++) {
-            rowsum(D[m], WL[m], WH[m]);
-            D[m] = ld(m + 7);
-        }
-        for (int r0 = 0; r0 < kDescPatchRows; r0 += 7) {
-#pragma unroll
-            for (int s = 0; s < 7; s++) {
-                const int rr = r0 + s;
-                if (rr < kDescPatchRows) {
-                    const int ns = (s + 6) % 7;
-                    rowsum(D[ns], WL[ns], WH[ns]);  // source row rr + 6
-                    D[ns] = ld(min(rr + 13, kFusedRows - 1));
-                    const float2v av = blur_vsum(WL[s], WL[(s + 1) % 7], WL[(s + 2) % 7], WL[(s + 3) % 7],
-                                                 WL[(s + 4) % 7], WL[(s + 5) % 7], WL[ns]);
-                    const float2v bv = blur_vsum(WH[s], WH[(s + 1) % 7], WH[(s + 2) % 7], WH[(s + 3) % 7],
-                                                 WH[(s + 4) % 7], WH[(s + 5) % 7], WH[ns]);
-                    float o[4] = {av.x, av.y, bv.x, bv.y};
-                    if (tail) {
-#pragma unroll
-                        for (int i = 0; i < 4; i++)
-                            if (col0 + i >= lv.blur_vec_end) o[i] = floorf(o[i] + 0.5f);
-                    }
-                    uint32_t packed = 0;
-#pragma unroll
-                    for (int i = 0; i < 4; i++) packed = __builtin_amdgcn_cvt_pk_u8_f32(o[i], (unsigned)i, packed);
-                    if (owner) dsw[rr * (kDescPatchPitch / 4)] = packed;
-                }
-            }
-        }
-    }
-    wave_sync();  // the patch rows of this keypoint's other lanes
-    const float angle = fast_atan2((float)m01, (float)m10);
-    const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    const float theta = __fmul_rn(angle, factorPI);
-    float sa, ca;
-    glibc_sincosf(theta, &sa, &ca);
-    const float a = ca, b = sa;
-    const uint8_t* pc0 = patch + kDescPatchR * kDescPatchPitch + kDescPatchR + pmis;  // keypoint
-    uint32_t myword = 0;
-    {
-#pragma clang fp contract(off)
-        const float2v A2v = {a, a}, B2v = {b, b};
-        const float2v MAG = {12582912.f, 12582912.f};
-        constexpr uint32_t K = 0x400000u * (uint32_t)kDescPatchPitch + 0x4B400000u;
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const PatPt pp = s_pat[16 * j + ln];
-            const float2v X = {pp.x0, pp.x1}, Y = {pp.y0, pp.y1};
-            float2v R = (X * B2v + Y * A2v) + MAG;
-            float2v C = (X * A2v - Y * B2v) + MAG;
-            asm("" : "+v"(R), "+v"(C));
-            const uint2v RB = __builtin_bit_cast(uint2v, R), CB = __builtin_bit_cast(uint2v, C);
-            const uint32_t o0 = (RB.x & 0xFFFFFFu) * (uint32_t)kDescPatchPitch + CB.x - K;
-            const uint32_t o1 = (RB.y & 0xFFFFFFu) * (uint32_t)kDescPatchPitch + CB.y - K;
-            const int t0 = pc0[(int)o0];
-            const int t1 = pc0[(int)o1];
-            myword |= (uint32_t)(t0 < t1) << j;
-        }
-    }
-    if (valid) {
-        const long long o = (long long)f * kp_stride + outidx;
-        ((uint16_t*)(out_desc + o * 32))[ln] = (uint16_t)myword;
-        if (ln == 0) {
-            orbx_kp kp;
-            const float fx = (float)x, fy = (float)y;
-            kp.x = l ? __fmul_rn(fx, lv.scale) : fx;
-            kp.y = l ? __fmul_rn(fy, lv.scale) : fy;
-            kp.size = lv.patch_size;
-            kp.angle = angle;
-            kp.response = (float)resp;
-            kp.octave = l;
-            out_kps[o] = kp;
-        }
-    }
-    if (ep.host_out) __threadfence_system();
-}
-
 /* self-test hook: the device restatement of glibc sinf/cosf on an array (tests only) */
 __global__ void k_sincos_selftest(const float* __restrict__ in, float* __restrict__ s, float* __restrict__ c, int n) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -2509,15 +2273,9 @@ hipError_t launch_describe_blur(const uint8_t* frames, long long fstride, int pi
                                 const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc, int* out_counts, int kp_stride,
                                 const int* ptab, int nframes, hipStream_t st) {
     if (!describe_blur_ok(frames, fstride, pitch0)) return hipErrorInvalidValue;
-#ifdef ORBX_FUSED_RS  // A/B: the source rows through registers (k_describe_blur_rs)
-    dim3 grid(((ep.kp_per_frame + kFusedKps - 1) / kFusedKps) * nframes);
-    hipLaunchKernelGGL(k_describe_blur_rs<kFusedWaves>, grid, dim3(64 * kFusedWaves), 0, st, frames, fstride, pitch0,
-                       pyr, ep, levels, lvkey, lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
-#else
     dim3 grid(((ep.kp_per_frame + kFusedKps - 1) / kFusedKps) * nframes);
     hipLaunchKernelGGL(k_describe_blur, grid, dim3(64 * kFusedWaves), 0, st, frames, fstride, pitch0, pyr, ep, levels,
                        lvkey, lvcnt, out_kps, out_desc, out_counts, kp_stride, ptab);
-#endif
     return hipGetLastError();
 }
 

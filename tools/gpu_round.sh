@@ -11,6 +11,7 @@
 #   bench         bench.py at its defaults (C2)                    -> <tag>_bench.log
 #   c3 / c4       bench.py --config c3 / c4 at the driver's arguments
 #   latency       the one-frame / per-call C++ latency rows (tests/cpp/build/bench_latency 2000)
+#   dropin        the drop-in ORBextractor's eager operator() and a two-thread stereo pair (bench_dropin_latency)
 # A failing test or smoke step ends the recipe before any bench runs.
 export TMPDIR=/tmp
 T=$1
@@ -37,6 +38,7 @@ for step in "$@"; do
     c3) tools/gpu_run.sh "300 ${T}_bench_c3 python3 bench.py --config c3 --gpus 1 --steps 20 --warmup 5" || exit $? ;;
     c4) tools/gpu_run.sh "300 ${T}_bench_c4 python3 bench.py --config c4 --gpus 1 --steps 20 --warmup 5" || exit $? ;;
     latency) tools/gpu_run.sh "300 ${T}_latency tests/cpp/build/bench_latency 2000" || exit $? ;;
+    dropin) tools/gpu_run.sh "300 ${T}_dropin_latency tests/cpp/build/bench_dropin_latency 2000" || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
