@@ -822,6 +822,10 @@ int orbx_set_pyramid_event(orbx_handle* h, void* event) {
     return 0;
 }
 
+int orbx_describe_blur_fused(const void* frames, size_t frame_stride, size_t pitch) {
+    return use_describe_blur((const uint8_t*)frames, (long long)frame_stride, (int)pitch) ? 1 : 0;
+}
+
 int orbx_debug_skip_stages(orbx_handle* h, int mask) {
     if (!h || mask < 0 || mask > 0x1F) return ORBX_EARG;
     h->skip_mask = mask;

@@ -33,6 +33,11 @@ int orbx_debug_alias_frames(orbx_handle* h, int on);
  * and that orbx_check_error reports and clears it once. */
 int orbx_debug_raise_error(orbx_handle* h, int flag, void* stream);
 
+/* Measurement query (host-only): 1 if a batched extraction of frames at `frames` (device pointer value, frame stride
+ * and row pitch in bytes) blurs inside describe (k_describe_blur: level-0 rows 4-aligned), 0 if it takes the separate
+ * blur (k_blur_strips + k_describe); bench.py prices describe's bytes by the form that ran. */
+int orbx_describe_blur_fused(const void* frames, size_t frame_stride, size_t pitch);
+
 /* Test hook: the device's restatement of glibc sinf/cosf (used by computeOrbDescriptor,
  * ORBextractor.cc:113) applied to n device floats; lets tests compare against host libm. */
 int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, void* stream);

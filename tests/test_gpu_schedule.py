@@ -1,7 +1,8 @@
 """GPU: the exact schedule bench.py times (orbamd.agent.AgentSchedule) checked against the oracle.
 
-The headline configuration: 1024 frames per step as 4 staggered 256-frame graphs on 4 streams, with
-the keyframe-slot exchange; every graph's device error flags, then EVERY frame's keypoints and
+The headline configuration: 3072 frames per step as 3 staggered 1024-frame graphs on 3 streams (bench.py's
+default; the round-4 shape, 4 x 256 frames, beside it), with the keyframe-slot exchange; every graph's device
+error flags, then EVERY frame's keypoints and
 descriptors (raw bits), every frame's SearchForTriangulation row against its predecessor, and the
 cross-agent match row are compared with the oracle (ORBextractor.cc:1043-1105,
 ORBmatcher.cc:657-823). The BASELINE configs C3 (752x480, 1200 features) and C4 (1241x376, 2000
@@ -14,7 +15,8 @@ from check_schedule import check_schedule
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("W,H,nf,B,P,stagger,async_x", [(640, 480, 1000, 1024, 4, "every8", False),
+@pytest.mark.parametrize("W,H,nf,B,P,stagger,async_x", [(640, 480, 1000, 3072, 3, "every8", False),
+                                                         (640, 480, 1000, 1024, 4, "every8", False),
                                                          (640, 480, 1000, 1024, 4, "each", False),
                                                          (640, 480, 1000, 1024, 4, "every8", True),
                                                          (752, 480, 1200, 128, 2, "every8", False),
