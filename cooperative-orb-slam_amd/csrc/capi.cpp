@@ -164,6 +164,8 @@ struct Geometry {
     int bjob_small[kMaxLevels + 1] = {0};  // the same in kBlurRowsSmall-row chunks (run_extract_levels)
     int nbjobs_small = 0;
     int NC = 0, KL = 0, lds_bytes = 0;
+    int oct_split = 0;                      // batches: levels [0, oct_split) use NC/KL, [oct_split, L) NC_lo/KL_lo
+    int NC_lo = 0, KL_lo = 0, lds_lo = 0;
     int roi_pitch = 0, roi_rows = 0;  // FAST cell LDS staging (max cell ROI)
     int max_pass = 1;                 // ROI staging passes (rows per 64-lane dword pass)
     int tiled_ok[kMaxLevels] = {0};   // level's resize fits the LDS-tiled kernel
@@ -397,9 +399,30 @@ struct Geometry {
         // fits 32 KB when that still leaves >= 1024 keys (five octree workgroups per CU beside the other
         // graphs' kernels; 1888 keys at NC = 256 cover a 640x480 / 1000-feature level 0), else up to 2048.
         if (node_bytes + 7 * 256 > 160 * 1024) return ORBX_EARG;
-        const int kl32 = ((32 * 1024 - node_bytes - 64) / 7) & ~15;
-        KL = kl32 >= 1024 ? std::min(2048, kl32) : std::min(2048, ((160 * 1024 - node_bytes) / 7) & ~15);
-        lds_bytes = node_bytes + 7 * KL;
+        auto key_lds = [](int nc, int* kl, int* lds) {
+            const int nb = 76 * nc;
+            const int kl32 = ((32 * 1024 - nb - 64) / 7) & ~15;
+            *kl = kl32 >= 1024 ? std::min(2048, kl32) : std::min(2048, ((160 * 1024 - nb) / 7) & ~15);
+            *lds = nb + 7 * *kl;
+        };
+        key_lds(NC, &KL, &lds_bytes);
+        // batches: the levels whose node tables fit 256 entries (all but level 0 of a 1200- or 2000-feature
+        // extractor) take their own launch with 256-node tables and 256-thread workgroups, instead of every level
+        // carrying the largest level's 512-node tables and 53 KB of LDS (C3 / C4: 2.4 ms per 1024-frame launch)
+        oct_split = L;
+        while (oct_split > 0 && lv[oct_split - 1].node_cap <= 256) oct_split--;
+        NC_lo = NC;
+        KL_lo = KL;
+        lds_lo = lds_bytes;
+        if (oct_split > 0 && oct_split < L) {
+            int mx = 0;
+            for (int l = oct_split; l < L; l++) mx = std::max(mx, lv[l].node_cap);
+            NC_lo = 1;
+            while (NC_lo < mx) NC_lo <<= 1;
+            key_lds(NC_lo, &KL_lo, &lds_lo);
+        } else {
+            oct_split = 0;  // one launch: every level fits the same tables
+        }
         // upload
         if (d_lv.ensure(sizeof(LevelDesc) * L) || d_cells.ensure(sizeof(CellDesc) * cells.size()) ||
             d_coef.ensure(sizeof(int) * std::max<size_t>(coef.size(), 1)) ||
@@ -700,10 +723,18 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
     if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
     if (prof_mark(h, 1, 1, st) || prof_mark(h, 2, 0, st)) return ORBX_EDEVICE;
-    if (!(h->skip_mask & 4))
+    if (!(h->skip_mask & 4)) {
+        const int split = g.oct_split;  // 0: one launch over every level
         HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                            h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
-                           (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st));
+                           (long long)ep.keys_per_frame * 8, g.NC, g.KL, g.lds_bytes, errp, nframes, st, 0,
+                           split ? split : -1));
+        if (split)
+            HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
+                               h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
+                               (long long)ep.keys_per_frame * 8, g.NC_lo, g.KL_lo, g.lds_lo, errp, nframes, st,
+                               split, ep.L - split));
+    }
     if (prof_mark(h, 2, 1, st)) return ORBX_EDEVICE;
     if (!h->serial && !fused) HIPR(hipStreamWaitEvent(st, h->ev_blur, 0));
     if (prof_mark(h, 4, 0, st)) return ORBX_EDEVICE;

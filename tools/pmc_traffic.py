@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of each pipeline stage from separate FETCH_SIZE / WRITE_SIZE
-rocprofv3 --pmc passes (MI355X_MICROARCH.md: both counters are in KiB -> x1024 bytes; the
-half-rule correction applies only to 16-B/lane streams, which these byte/dword kernels are not).
+rocprofv3 --pmc passes. Both counters are in KiB (x1024 bytes). FETCH_SIZE reports exactly half the bytes
+read on gfx950 for every load width these kernels use (1, 4, 8, 16 B per lane and 4-B LDS-DMA, measured by
+tools/fetch_calib.hip over a 1 GiB buffer: profiles/r05_fetch_size_calibration.txt; MI355X_MICROARCH.md
+documents the half for 16-B lanes), so it is doubled here; WRITE_SIZE reads the bytes exactly.
 For a stage launched with different grids (FAST: level-0 and other-level launches in the
 overlapped schedule, one whole-grid launch in the stage-serial profiling pass) the whole-grid
 launch is reported, which is the launch bench.py's roofline times.
@@ -38,9 +40,9 @@ for st in STAGES:
     if not grids:
         continue
     g = grids[-1]
-    f = sum(fetch[(st, g)]) / len(fetch[(st, g)])
+    f = 2.0 * sum(fetch[(st, g)]) / len(fetch[(st, g)])  # calibrated: FETCH_SIZE tallies half the bytes
     w = sum(write.get((st, g), [0.0])) / max(len(write.get((st, g), [0.0])), 1)
-    out[st] = {"grid": g, "dispatches": len(fetch[(st, g)]), "FETCH_SIZE_KiB_avg_per_dispatch": f,
+    out[st] = {"grid": g, "dispatches": len(fetch[(st, g)]), "fetch_KiB_avg_per_dispatch_corrected": f,
                "WRITE_SIZE_KiB_avg_per_dispatch": w, "hbm_bytes_per_launch": (f + w) * 1024.0}
     if (st, g) in valu:
         out[st]["valu_insts_per_launch"] = sum(valu[(st, g)]) / len(valu[(st, g)])
@@ -50,5 +52,5 @@ for k, v in out.items():
     if not isinstance(v, dict):
         continue
     print("%-10s grid %9d  fetch %10.0f KiB  write %9.0f KiB  -> %.1f MB/launch" % (
-        k, v["grid"], v["FETCH_SIZE_KiB_avg_per_dispatch"], v["WRITE_SIZE_KiB_avg_per_dispatch"],
+        k, v["grid"], v["fetch_KiB_avg_per_dispatch_corrected"], v["WRITE_SIZE_KiB_avg_per_dispatch"],
         v["hbm_bytes_per_launch"] / 1e6))
