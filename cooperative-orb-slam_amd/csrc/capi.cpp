@@ -604,12 +604,7 @@ constexpr int kErrWordExtractSeq = 40;  // the host extraction's call counter (k
 /* the blur inside describe (k_describe_blur, no blurred pyramid in HBM) takes every frame whose level-0 rows are
  * 4-byte aligned; other frames blur each level in k_blur_strips and describe from it */
 static bool use_describe_blur(const uint8_t* d_frames, long long fstride, int pitch) {
-#ifdef ORBX_AB_NO_DESCRIBE_BLUR  // A/B build (tools/build_variant.sh): the round-4 separate blur
-    (void)d_frames, (void)fstride, (void)pitch;
-    return false;
-#else
     return describe_blur_ok(d_frames, fstride, pitch);
-#endif
 }
 
 static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nframes, const uint8_t* d_frames,
@@ -787,10 +782,6 @@ int orbx_create(const orbx_params* p, int device, int max_width, int max_height,
     // no HIP stream here: the host-call stream and the blur's side stream are created at their first use
     // (ensure_stream), since every idle stream in the process costs the batch schedule's graph streams their step
     // rate (profiles/r04_idle_stream_cost.log) and a device batch on the caller's stream needs neither
-#ifdef ORBX_AB_EAGER_STREAMS  // A/B build: the round-4 form (both streams at creation)
-    (void)ensure_stream(h, &h->stream);
-    (void)ensure_stream(h, &h->side);
-#endif
     if (hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_blur, hipEventDisableTiming) != hipSuccess) {
         orbx_destroy(h);

@@ -752,27 +752,8 @@ __global__ __launch_bounds__(256) void k_fast_cells2(
     ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
     uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi) {
     extern __shared__ __align__(16) uint8_t lds[];
-#ifdef ORBX_AB_FAST_XCD
-    // XCD-aware 1-D grid (G cell groups x F frames, as k_describe): workgroups are dispatched to the 8 XCDs round-robin,
-    // so with F % 8 == 0 every cell group of a frame runs on XCD f % 8 and neighbouring cells' overlapping ROIs
-    // (each cell reads a 6-px overlap and a 3-px FAST border around its 31 x 32 px) hit that XCD's L2
-    const int G = (cell_hi - cell_lo + 3) / 4;
-    int f, bx;
-    const int b = blockIdx.x;
-    if ((gridDim.x / G) % 8 == 0) {
-        const int k = b >> 3;
-        f = (b & 7) + 8 * (k / G);
-        bx = k % G;
-    } else {
-        f = b / G;
-        bx = b % G;
-    }
-    fast_cells_body<kMaxPass, kRP>(frames, fstride, pitch0, pyr, ep, levels, cells, cellkey, cellcnt, RP_, RH, cell_lo,
-                                   cell_hi, bx, f, lds);
-#else
     fast_cells_body<kMaxPass, kRP>(frames, fstride, pitch0, pyr, ep, levels, cells, cellkey, cellcnt, RP_, RH, cell_lo,
                                    cell_hi, blockIdx.x, blockIdx.y, lds);
-#endif
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -2151,11 +2132,7 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
                               uint32_t* cellkey, int* cellcnt, int RP, int RH, int max_pass, int cell_lo,
                               int cell_hi, int nframes, hipStream_t st) {
     if (cell_hi <= cell_lo) return hipSuccess;
-#ifdef ORBX_AB_FAST_XCD
-    dim3 grid(((cell_hi - cell_lo + 3) / 4) * nframes);
-#else
     dim3 grid((cell_hi - cell_lo + 3) / 4, nframes);
-#endif
     const size_t lds = 4 * (size_t)fast_wave_lds(RP, RH);
 #define ORBX_FAST(MP, RPC)                                                                                        \
     hipLaunchKernelGGL((k_fast_cells2<MP, RPC>), grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, \
