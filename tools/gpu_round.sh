@@ -7,6 +7,7 @@
 #   smoke         __graft_entry__.smoke()                          -> <tag>_smoke.log
 #   prof          kernel trace + PMC passes (tools/prof_round.sh), the timed region's per-kernel averages and the
 #                 exchange kernels, reduced to <tag>_pmc_traffic.json / _pmc_summary.txt / _timed_region_kernels.txt
+#   prof_cfg      the counter passes of C3 and C4 (tools/pmc_config.sh) -> profiles/pmc_traffic_c3.json, _c4.json
 #   bench_driver  bench.py at the driver's arguments (C2)          -> <tag>_bench_driver.log
 #   bench         bench.py at its defaults (C2)                    -> <tag>_bench.log
 #   c3 / c4       bench.py --config c3 / c4 at the driver's arguments
@@ -32,7 +33,9 @@ for step in "$@"; do
       python3 tools/trace_segments.py "$kt" 10 2 $pipes > gpurun_out/${T}_timed_region_kernels.txt || exit $?
       python3 tools/exchange_kernels.py "$kt" > gpurun_out/${T}_exchange_kernels.txt || exit $?
       python3 tools/queue_map.py "$kt" > gpurun_out/${T}_queue_map.txt || exit $?
-      tools/prof_reduce.sh $T $sub ;;
+      tools/prof_reduce.sh $T $sub
+      cp gpurun_out/${T}_pmc_traffic.json profiles/pmc_traffic.json ;;  # the bench steps that follow read it
+    prof_cfg) for c in c3 c4; do tools/pmc_config.sh $c || exit $?; done ;;
     bench_driver) tools/gpu_run.sh "300 ${T}_bench_driver python3 bench.py --gpus 1 --steps 20 --warmup 5" || exit $? ;;
     bench) tools/gpu_run.sh "300 ${T}_bench python3 bench.py" || exit $? ;;
     c3) tools/gpu_run.sh "300 ${T}_bench_c3 python3 bench.py --config c3 --gpus 1 --steps 20 --warmup 5" || exit $? ;;

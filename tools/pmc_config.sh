@@ -12,7 +12,9 @@ tools/gpu_run.sh \
   "300 pmc_${C}_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_${C}_write -o run -- $B" || exit $?
 one() { find "$1" -name "$2" 2>/dev/null | head -n 1; }
 O=gpurun_out
+read sub pipes < <(python3 bench.py --config $C --launch-frames)
 python3 tools/pmc_traffic.py "$(one $O/pmc_${C}_fetch '*counter_collection.csv')" "$(one $O/pmc_${C}_write '*counter_collection.csv')" \
-  $O/pmc_traffic_${C}.json "$(one $O/pmc_${C}_a '*counter_collection.csv')" || exit $?
+  $O/pmc_traffic_${C}.json "$(one $O/pmc_${C}_a '*counter_collection.csv')" $sub || exit $?
+cp $O/pmc_traffic_${C}.json profiles/pmc_traffic_${C}.json  # the bench lines that follow on this box read it
 python3 tools/pmc_summary.py "$(one $O/pmc_${C}_a '*counter_collection.csv')" > $O/pmc_summary_${C}.txt
 rm -rf $O/pmc_${C}_a $O/pmc_${C}_fetch $O/pmc_${C}_write
