@@ -315,11 +315,13 @@ def main():
                          "(orbx_synth_scene_frames, 12 px per agent along the pan), so the cross-agent matchers find the "
                          "other agents' features as A1 does on A2's keyframes; private: a texture per agent. Rank 0's "
                          "frames are the same in both modes")
-    ap.add_argument("--stagger", choices=("each", "once", "none", "every4", "every8", "every16", "pyr_each", "pyr_every8"),
+    ap.add_argument("--stagger", choices=("each", "once", "none", "every4", "every8", "every16", "pyr_each", "pyr_every8",
+                                          "fast_each", "fast_every8", "fast_once"),
                     default="every8",
                     help="graph p starts extracting after graph p-1's extraction: every step / only in the "
                          "first step of a run (the phase offset then persists) / never / in the first step and every "
-                         "K-th step after it")
+                         "K-th step after it; pyr_ / fast_: after graph p-1's pyramid / FAST instead (a third of the step "
+                         "apart at 3 graphs)")
     ap.add_argument("--launch-frames", action="store_true",
                     help="print the frames one stage launch processes (--batch / --pipes) and the graph count, and exit "
                          "(no GPU use)")

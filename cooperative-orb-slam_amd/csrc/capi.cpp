@@ -447,7 +447,8 @@ struct orbx_handle {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // branches of the extraction graph (run_extract)
     hipEvent_t ev_pyr = nullptr, ev_blur = nullptr;
-    hipEvent_t user_ev_pyr = nullptr;  // orbx_set_pyramid_event (caller-owned)
+    hipEvent_t user_ev_pyr = nullptr;   // orbx_set_stage_event(0) / orbx_set_pyramid_event (caller-owned)
+    hipEvent_t user_ev_fast = nullptr;  // orbx_set_stage_event(1) (caller-owned)
     Geometry geo;
     DevBuf pyr, blur, cellkey, cellcnt, lvkey, lvcnt, gscratch, err;
     // host-path staging
@@ -593,9 +594,10 @@ static int launch_fast(orbx_handle* h, const ExtractParams& ep, const uint8_t* d
 constexpr int kErrWordSticky = 0, kErrWordCall = 1, kErrWordExtract = 2, kErrWordTake = 32, kErrWordExtractTake = 33;
 constexpr int kErrWordExtractSeq = 40;  // the host extraction's call counter (k_call_done's done word)
 /* Small batches (the Tracking thread's one frame per call, ORBextractor.cc:1043-1105): every stage in order on the
- * caller's queue -- the pyramid in kPyrBands row bands per frame (one launch); FAST over every cell and the blur
- * in 14-row chunks (4.5x the waves of the batch form's 63-row chunks: one frame's blur is one chunk's row chain)
- * in one launch (k_fast_blur); the octree over every level; describe. A single queue because the graph executor turns every edge between queues into a
+ * caller's queue -- the pyramid in kPyrBands row bands per frame (one launch); FAST over every cell; the octree over
+ * every level; the blur inside describe (k_describe_blur). Unaligned frames run FAST and the blur in 14-row chunks
+ * (4.5x the waves of the batch form's 63-row chunks: one frame's blur is one chunk's row chain) in one launch
+ * (k_fast_blur), then describe. A single queue because the graph executor turns every edge between queues into a
  * marker behind all the work already submitted to the source queue (~10 us per hop in the kernel trace, and a
  * side branch started only once its marker came up), and streams share the process's 4 hardware queues; every
  * branch layout measured slower than the one queue (profiles/r04_latency_branches.log, r04_latency_lists.log,
@@ -609,7 +611,8 @@ static bool use_describe_blur(const uint8_t* d_frames, long long fstride, int pi
 
 static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nframes, const uint8_t* d_frames,
                               long long fstride, int pitch, orbx_kp* d_kps, uint8_t* d_desc, int32_t* d_counts,
-                              int kp_stride, hipStream_t st, int* errp, hipEvent_t ev_pyr, const HostCopy* copy) {
+                              int kp_stride, hipStream_t st, int* errp, hipEvent_t ev_pyr, hipEvent_t ev_fast,
+                              const HostCopy* copy) {
     Geometry& g = h->geo;
     const LevelDesc* dl = g.d_lv.as<LevelDesc>();
     if (!(h->skip_mask & 1) && launch_pyramid(h, ep, d_frames, fstride, pitch, nframes, st)) return ORBX_EDEVICE;
@@ -617,6 +620,7 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
     if (use_describe_blur(d_frames, fstride, pitch)) {  // FAST -> octree -> blur + describe
         if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, ep.ncells, nframes, st))
             return ORBX_EDEVICE;
+        if (ev_fast) HIPR(hipEventRecord(ev_fast, st));
         if (!(h->skip_mask & 4))
             HIPR(launch_octree(ep, dl, g.d_cells.as<CellDesc>(), h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(),
                                h->lvkey.as<uint32_t>(), h->lvcnt.as<int>(), h->gscratch.as<uint8_t>(),
@@ -634,6 +638,7 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
         HIPR(launch_fast_blur(d_frames, fstride, pitch, h->pyr.as<uint8_t>(), ep, dl, g.d_cells.as<CellDesc>(),
                               h->cellkey.as<uint32_t>(), h->cellcnt.as<int>(), g.roi_pitch, g.roi_rows, g.max_pass,
                               h->blur.as<uint8_t>(), eb, g.nbjobs_small, nframes, st));
+        if (ev_fast) HIPR(hipEventRecord(ev_fast, st));
     } else {
         if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, ep.ncells, nframes, st))
             return ORBX_EDEVICE;
@@ -685,7 +690,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     int* errp = h->err.as<int>() + (host_call ? kErrWordExtract : kErrWordSticky);
     if (nframes < kPyrFramesMinBatch && !h->serial && !h->prof_on && !h->alias) {
         if (run_extract_levels(h, ep, nframes, d_frames, fstride, pitch, d_kps, d_desc, d_counts, kp_stride, st, errp,
-                               host_call ? nullptr : h->user_ev_pyr, copy))
+                               host_call ? nullptr : h->user_ev_pyr, host_call ? nullptr : h->user_ev_fast, copy))
             return ORBX_EDEVICE;
         h->last_frames = d_frames;
         h->last_fstride = fstride;
@@ -717,6 +722,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
     }
     if (prof_mark(h, 1, 0, st)) return ORBX_EDEVICE;
     if (!(h->skip_mask & 2) && launch_fast(h, ep, d_frames, fstride, pitch, 0, ep.ncells, nframes, st)) return ORBX_EDEVICE;
+    if (!host_call && h->user_ev_fast) HIPR(hipEventRecord(h->user_ev_fast, st));
     if (prof_mark(h, 1, 1, st) || prof_mark(h, 2, 0, st)) return ORBX_EDEVICE;
     if (!(h->skip_mask & 4)) {
         const int split = g.oct_split;  // 0: one launch over every level
@@ -838,9 +844,11 @@ int orbx_selftest_sincosf(const float* d_in, float* d_sin, float* d_cos, int n, 
     return 0;
 }
 
-int orbx_set_pyramid_event(orbx_handle* h, void* event) {
-    if (!h) return ORBX_EARG;
-    h->user_ev_pyr = (hipEvent_t)event;
+int orbx_set_pyramid_event(orbx_handle* h, void* event) { return orbx_set_stage_event(h, 0, event); }
+
+int orbx_set_stage_event(orbx_handle* h, int stage, void* event) {
+    if (!h || stage < 0 || stage > 1) return ORBX_EARG;
+    (stage == 0 ? h->user_ev_pyr : h->user_ev_fast) = (hipEvent_t)event;
     return 0;
 }
 

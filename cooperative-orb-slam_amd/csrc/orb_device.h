@@ -35,11 +35,7 @@ constexpr int kPyrU = 4;            // k_pyramid_frames: rows in flight per thre
 // k_pyramid_frames: threads per frame's workgroup. kPyrThreads is used when every level's 4-column
 // group count fits half of it (>= 2 rows per pass); wider levels take kPyrThreadsMax, the limit the
 // whole-frame kernel accepts (>= column groups of every level)
-#ifdef ORBX_AB_PYR1024
-constexpr int kPyrThreads = 1024;
-#else
-constexpr int kPyrThreads = 512;
-#endif
+constexpr int kPyrThreads = 512;  // (1024 at the round-5 step: -4.5 %, profiles/r05_ab_pyr1024.log)
 constexpr int kPyrThreadsMax = 1024;
 constexpr int kPyrFramesMinBatch = 64;  // batches below this build the pyramid in row bands (below)
 // small batches: k_pyramid_frames over kPyrBands row bands per frame, each band's workgroup computing every level's

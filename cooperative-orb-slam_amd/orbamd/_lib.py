@@ -106,6 +106,7 @@ SIGNATURES = {
     "orbx_get_feature_split": (_I, [_P, _P, _P]),
     "orbx_compute_scale_tables": (_I, [C.POINTER(OrbxParams), _P, _P, _P, _P]),
     "orbx_set_pyramid_event": (_I, [_P, _P]),
+    "orbx_set_stage_event": (_I, [_P, _I, _P]),
     "orbx_debug_skip_stages": (_I, [_P, _I]),
     "orbx_describe_blur_fused": (_I, [_P, _SZ, _SZ]),
     "orbx_debug_serial": (_I, [_P, _I]),

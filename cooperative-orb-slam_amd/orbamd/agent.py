@@ -62,9 +62,10 @@ class AgentSchedule:
         # stagger: "each" step, "once" (the first step of a pass only) or "everyK" (the first step of a pass and
         # every K-th step after it: the graphs' phase offset is re-imposed periodically, and the other steps carry
         # no cross-graph wait)
-        # a "pyr_" prefix staggers graph p behind graph p-1's pyramid instead of its whole extraction
-        self.stagger_pyr = stagger.startswith("pyr_")
-        mode = stagger[4:] if self.stagger_pyr else stagger
+        # a "pyr_" / "fast_" prefix staggers graph p behind graph p-1's pyramid / FAST instead of its whole extraction
+        self.stagger_stage = 0 if stagger.startswith("pyr_") else 1 if stagger.startswith("fast_") else None
+        self.stagger_pyr = self.stagger_stage is not None  # graph p waits for an event inside graph p-1's extraction
+        mode = stagger.split("_", 1)[1] if self.stagger_pyr else stagger
         assert mode in ("each", "once", "none") or (mode.startswith("every") and int(mode[5:]) > 0)
         self.stagger, self.exchange_on = mode, exchange
         self.stagger_every = int(mode[5:]) if mode.startswith("every") else 0
@@ -99,7 +100,7 @@ class AgentSchedule:
             self.pyr_done = [torch.cuda.Event() for _ in range(pipes)]
             for p in range(pipes):
                 self.pyr_done[p].record(self.streams[p])  # materialise the HIP event
-                assert lib.orbx_set_pyramid_event(self.pipes[p].ext._h, self.pyr_done[p].cuda_event) == 0
+                assert lib.orbx_set_stage_event(self.pipes[p].ext._h, self.stagger_stage, self.pyr_done[p].cuda_event) == 0
         p0 = self.pipes[0]
         self.slot_bytes = p0.slot_bytes()
         # without a collective (N = 1) the keyframe is packed straight into the receive buffer (no copy);
@@ -269,7 +270,7 @@ class AgentSchedule:
         if self.pyr_done is not None:
             from ._lib import load
             for pp in self.pipes:
-                load().orbx_set_pyramid_event(pp.ext._h, None)
+                load().orbx_set_stage_event(pp.ext._h, self.stagger_stage, None)
         for pp in self.pipes:
             pp.close()
         if getattr(self, "voc", None) is not None:

@@ -677,6 +677,10 @@ int orbx_profile_read(orbx_handle* h, double* ms, int* ncalls);
  * can start its own work once this batch's pyramid is done (bench schedules that stagger concurrent
  * extraction graphs by pyramid rather than by whole extraction). */
 int orbx_set_pyramid_event(orbx_handle* h, void* event);
+/* The same for any of the first two stages: stage 0 = after the pyramid launch (orbx_set_pyramid_event), 1 = after
+ * the FAST launch; one event per stage, NULL = off. The bench staggers its graphs by FAST: graph p starts a step
+ * once graph p-1's FAST is done, a third of the step apart at 3 graphs. */
+int orbx_set_stage_event(orbx_handle* h, int stage, void* event);
 
 /* Library/version and device probe. */
 const char* orbx_version(void);
