@@ -1769,6 +1769,10 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
 constexpr int kFusedRows = 43;   // source rows y-21 .. y+21
 constexpr int kFusedPitch = 48;  // 12 dwords: columns cx0 .. cx0+47 cover x-21 .. x+21 for any (x-22) & 3
 constexpr int kFusedDwords = kFusedRows * kFusedPitch / 4;  // 516 per keypoint
+#ifndef ORBX_FUSED_STRIDE
+#define ORBX_FUSED_STRIDE (kFusedRows * kFusedPitch)
+#endif
+constexpr int kFusedStride = ORBX_FUSED_STRIDE;  // bytes between the keypoints' patches in LDS
 
 // waves (x 4 keypoints) per k_describe_blur workgroup (2 waves: -0.2 %, 1 wave: -5 %, profiles/r05_ab_mf4_fw2.log,
 // r05_ab_graphs_batch2.log)
@@ -1782,7 +1786,7 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     int* __restrict__ out_counts, int kp_stride, const int* __restrict__ ptab) {
     __shared__ PatPt s_pat[256];
     __shared__ int2 s_ic[256];
-    __shared__ __align__(16) uint8_t s_patch[kFusedKps][kFusedRows * kFusedPitch];
+    __shared__ __align__(16) uint8_t s_patch[kFusedKps][kFusedStride];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int sub = lane >> 4, ln = lane & 15;
     // XCD-aware block mapping as k_describe: every workgroup of a frame on one XCD
