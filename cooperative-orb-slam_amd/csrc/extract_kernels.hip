@@ -1769,15 +1769,81 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
 constexpr int kFusedRows = 43;   // source rows y-21 .. y+21
 constexpr int kFusedPitch = 48;  // 12 dwords: columns cx0 .. cx0+47 cover x-21 .. x+21 for any (x-22) & 3
 constexpr int kFusedDwords = kFusedRows * kFusedPitch / 4;  // 516 per keypoint
+#ifndef ORBX_XBLUR
+#define ORBX_XBLUR 1
+#endif
 #ifndef ORBX_FUSED_STRIDE
+#if ORBX_XBLUR
+#define ORBX_FUSED_STRIDE 2088  // 522 dwords = 10 banks mod 64: the blur's 60 lanes of a wave hit 60 distinct banks
+#else
 #define ORBX_FUSED_STRIDE (kFusedRows * kFusedPitch)
+#endif
 #endif
 constexpr int kFusedStride = ORBX_FUSED_STRIDE;  // bytes between the keypoints' patches in LDS
 
 // waves (x 4 keypoints) per k_describe_blur workgroup (2 waves: -0.2 %, 1 wave: -5 %, profiles/r05_ab_mf4_fw2.log,
 // r05_ab_graphs_batch2.log)
-constexpr int kFusedWaves = 4;
+#ifndef ORBX_FUSED_WAVES
+#define ORBX_FUSED_WAVES 4
+#endif
+constexpr int kFusedWaves = ORBX_FUSED_WAVES;
 constexpr int kFusedKps = 4 * kFusedWaves;
+
+/* One lane's share of the in-place patch blur of k_describe_blur: output dword gd (patch columns 4gd..4gd+3,
+ * image column col0 of the first) of rows 0..36 from source rows 0..42, walking down with a 7-row register
+ * window. In place: output row r overwrites source row r after every lane of the wave read it (row sum r was
+ * taken at step r-6), so all lanes of one patch must be lanes of one wave. */
+__device__ __forceinline__ void blur_patch_column(uint8_t* patch, int gd, int col0, int vec_end) {
+    {
+        const uint32_t* src = (const uint32_t*)patch + (gd - 1);
+        uint32_t* dsw = (uint32_t*)patch + gd;
+        const bool tail = col0 + 3 >= vec_end;
+        // taps 18 34 49 55 49 34 18 against bytes of dwords g-1 (a), g (b), g+1 (c): output j sums bytes j+1 .. j+7
+        constexpr uint32_t A0 = 18u << 8 | 34u << 16 | 49u << 24, B0 = 55u | 49u << 8 | 34u << 16 | 18u << 24;
+        constexpr uint32_t A1 = 18u << 16 | 34u << 24, B1 = 49u | 55u << 8 | 49u << 16 | 34u << 24, C1 = 18u;
+        constexpr uint32_t A2 = 18u << 24, B2 = 34u | 49u << 8 | 55u << 16 | 49u << 24, C2 = 34u | 18u << 8;
+        constexpr uint32_t B3 = 18u | 34u << 8 | 49u << 16 | 55u << 24, C3 = 49u | 34u << 8 | 18u << 16;
+        auto rowsum = [&](int i, float2v& lo, float2v& hi) {
+            const uint32_t a = src[i * (kFusedPitch / 4)], b = src[i * (kFusedPitch / 4) + 1],
+                           c = src[i * (kFusedPitch / 4) + 2];
+            const uint32_t o0 = __builtin_amdgcn_udot4(a, A0, __builtin_amdgcn_udot4(b, B0, 0u, false), false);
+            const uint32_t o1 = __builtin_amdgcn_udot4(
+                a, A1, __builtin_amdgcn_udot4(b, B1, __builtin_amdgcn_udot4(c, C1, 0u, false), false), false);
+            const uint32_t o2 = __builtin_amdgcn_udot4(
+                a, A2, __builtin_amdgcn_udot4(b, B2, __builtin_amdgcn_udot4(c, C2, 0u, false), false), false);
+            const uint32_t o3 = __builtin_amdgcn_udot4(b, B3, __builtin_amdgcn_udot4(c, C3, 0u, false), false);
+            lo = (float2v){(float)o0, (float)o1};
+            hi = (float2v){(float)o2, (float)o3};
+        };
+        float2v WL[7], WH[7];
+#pragma unroll
+        for (int m = 0; m < 6; m++) rowsum(m, WL[m], WH[m]);
+        for (int r0 = 0; r0 < kDescPatchRows; r0 += 7) {
+#pragma unroll
+            for (int s = 0; s < 7; s++) {
+                const int r = r0 + s;
+                if (r < kDescPatchRows) {
+                    const int ns = (s + 6) % 7;
+                    rowsum(r + 6, WL[ns], WH[ns]);
+                    const float2v av = blur_vsum(WL[s], WL[(s + 1) % 7], WL[(s + 2) % 7], WL[(s + 3) % 7],
+                                                 WL[(s + 4) % 7], WL[(s + 5) % 7], WL[ns]);
+                    const float2v bv = blur_vsum(WH[s], WH[(s + 1) % 7], WH[(s + 2) % 7], WH[(s + 3) % 7],
+                                                 WH[(s + 4) % 7], WH[(s + 5) % 7], WH[ns]);
+                    float o[4] = {av.x, av.y, bv.x, bv.y};
+                    if (tail) {
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (col0 + i >= vec_end) o[i] = floorf(o[i] + 0.5f);
+                    }
+                    uint32_t packed = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) packed = __builtin_amdgcn_cvt_pk_u8_f32(o[i], (unsigned)i, packed);
+                    dsw[r * (kFusedPitch / 4)] = packed;
+                }
+            }
+        }
+    }
+}
 
 __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
@@ -1787,6 +1853,9 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     __shared__ PatPt s_pat[256];
     __shared__ int2 s_ic[256];
     __shared__ __align__(16) uint8_t s_patch[kFusedKps][kFusedStride];
+#if ORBX_XBLUR
+    __shared__ int s_bcx[kFusedKps], s_bve[kFusedKps];  // per patch: cx0, blur_vec_end (-1: no keypoint)
+#endif
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int sub = lane >> 4, ln = lane & 15;
     // XCD-aware block mapping as k_describe: every workgroup of a frame on one XCD
@@ -1835,7 +1904,9 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
         if (ep.host_out) __threadfence_system();
     }
     __syncthreads();
+#if !ORBX_XBLUR
     if (__ballot(g < ep.kp_per_frame) == 0) return;  // wave-uniform
+#endif
     const int l = level_of(ep.kp_off, ep.L, gc);
     const int k = gc - ep.kp_off[l];
     int mycnt = 0, outidx = k;
@@ -1845,7 +1916,10 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
         outidx += q < l ? cl[q] : 0;
     }
     const bool valid = g < ep.kp_per_frame && k < mycnt;
-    if (__ballot(valid) == 0) return;  // wave-uniform
+    const bool wave_on = __ballot(valid) != 0;  // wave-uniform
+#if !ORBX_XBLUR
+    if (!wave_on) return;
+#endif
     const LevelDesc lv = levels[l];
     const uint32_t kk = valid ? kk_raw : 0u;
     const int x = valid ? (int)(kk & 0xFFF) : 32, y = valid ? (int)((kk >> 12) & 0xFFF) : 32;
@@ -1859,7 +1933,7 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     // row's last valid dword takes the clamped / reflected staging
     const int edge = (y < 21 || y + 21 >= lv.h || x < 22 || x + 21 >= lv.w || cx0 + 44 > lastd) ? 1 : 0;
     uint8_t* patch = s_patch[wave * 4 + sub];
-    {
+    if (wave_on) {  // a wave without keypoints (only with ORBX_XBLUR) stages nothing
         int rq[9], cq[9];
 #pragma unroll
         for (int q = 0; q < 9; q++) {
@@ -1953,58 +2027,27 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
         m10 = A;
         m01 = M;
     }
-    // blur in place: lanes ln < 10 own output dword g = ln + 1 (columns 4g..4g+3 of the patch)
-    if (ln < 10) {
-        const int gd = ln + 1;
-        const uint32_t* src = (const uint32_t*)patch + (gd - 1);
-        uint32_t* dsw = (uint32_t*)patch + gd;
-        const int col0 = cx0 + 4 * gd;  // image column of this lane's first output
-        const bool tail = col0 + 3 >= lv.blur_vec_end;
-        // taps 18 34 49 55 49 34 18 against bytes of dwords g-1 (a), g (b), g+1 (c): output j sums bytes j+1 .. j+7
-        constexpr uint32_t A0 = 18u << 8 | 34u << 16 | 49u << 24, B0 = 55u | 49u << 8 | 34u << 16 | 18u << 24;
-        constexpr uint32_t A1 = 18u << 16 | 34u << 24, B1 = 49u | 55u << 8 | 49u << 16 | 34u << 24, C1 = 18u;
-        constexpr uint32_t A2 = 18u << 24, B2 = 34u | 49u << 8 | 55u << 16 | 49u << 24, C2 = 34u | 18u << 8;
-        constexpr uint32_t B3 = 18u | 34u << 8 | 49u << 16 | 55u << 24, C3 = 49u | 34u << 8 | 18u << 16;
-        auto rowsum = [&](int i, float2v& lo, float2v& hi) {
-            const uint32_t a = src[i * (kFusedPitch / 4)], b = src[i * (kFusedPitch / 4) + 1],
-                           c = src[i * (kFusedPitch / 4) + 2];
-            const uint32_t o0 = __builtin_amdgcn_udot4(a, A0, __builtin_amdgcn_udot4(b, B0, 0u, false), false);
-            const uint32_t o1 = __builtin_amdgcn_udot4(
-                a, A1, __builtin_amdgcn_udot4(b, B1, __builtin_amdgcn_udot4(c, C1, 0u, false), false), false);
-            const uint32_t o2 = __builtin_amdgcn_udot4(
-                a, A2, __builtin_amdgcn_udot4(b, B2, __builtin_amdgcn_udot4(c, C2, 0u, false), false), false);
-            const uint32_t o3 = __builtin_amdgcn_udot4(b, B3, __builtin_amdgcn_udot4(c, C3, 0u, false), false);
-            lo = (float2v){(float)o0, (float)o1};
-            hi = (float2v){(float)o2, (float)o3};
-        };
-        float2v WL[7], WH[7];
-#pragma unroll
-        for (int m = 0; m < 6; m++) rowsum(m, WL[m], WH[m]);
-        for (int r0 = 0; r0 < kDescPatchRows; r0 += 7) {
-#pragma unroll
-            for (int s = 0; s < 7; s++) {
-                const int r = r0 + s;
-                if (r < kDescPatchRows) {
-                    const int ns = (s + 6) % 7;
-                    rowsum(r + 6, WL[ns], WH[ns]);
-                    const float2v av = blur_vsum(WL[s], WL[(s + 1) % 7], WL[(s + 2) % 7], WL[(s + 3) % 7],
-                                                 WL[(s + 4) % 7], WL[(s + 5) % 7], WL[ns]);
-                    const float2v bv = blur_vsum(WH[s], WH[(s + 1) % 7], WH[(s + 2) % 7], WH[(s + 3) % 7],
-                                                 WH[(s + 4) % 7], WH[(s + 5) % 7], WH[ns]);
-                    float o[4] = {av.x, av.y, bv.x, bv.y};
-                    if (tail) {
-#pragma unroll
-                        for (int i = 0; i < 4; i++)
-                            if (col0 + i >= lv.blur_vec_end) o[i] = floorf(o[i] + 0.5f);
-                    }
-                    uint32_t packed = 0;
-#pragma unroll
-                    for (int i = 0; i < 4; i++) packed = __builtin_amdgcn_cvt_pk_u8_f32(o[i], (unsigned)i, packed);
-                    dsw[r * (kFusedPitch / 4)] = packed;
-                }
-            }
+#if ORBX_XBLUR
+    // blur across the workgroup: wave w blurs patches 6w .. 6w+5 with 10 lanes each (60 of 64 lanes busy,
+    // 3 waves for 16 patches instead of 4 at 10 of 16), after every wave's IC_Angle read its raw rows
+    if (ln == 0) {
+        s_bcx[wave * 4 + sub] = cx0;  // negative near the left edge
+        s_bve[wave * 4 + sub] = valid ? lv.blur_vec_end : -1;
+    }
+    __syncthreads();
+    {
+        const int kq = wave * 6 + lane / 10, gd = lane - 10 * (lane / 10) + 1;
+        if (lane < 60 && kq < kFusedKps) {
+            const int bve = s_bve[kq];
+            if (bve >= 0) blur_patch_column(s_patch[kq], gd, s_bcx[kq] + 4 * gd, bve);
         }
     }
+    __syncthreads();
+    if (!wave_on) return;  // wave-uniform, past the last barrier
+#else
+    // blur in place: lanes ln < 10 own output dword g = ln + 1 (columns 4g..4g+3 of the patch)
+    if (ln < 10) blur_patch_column(patch, ln + 1, cx0 + 4 * (ln + 1), lv.blur_vec_end);
+#endif
     wave_sync();
     const float angle = fast_atan2((float)m01, (float)m10);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
