@@ -377,6 +377,9 @@ struct PyrColGroup {
 };
 static_assert(sizeof(PyrColGroup) == 48, "PyrColGroup layout");
 
+#ifndef ORBX_PYR_MULHI
+#define ORBX_PYR_MULHI 1
+#endif
 template <int U, int NT>
 __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
                                                          int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
@@ -447,11 +450,32 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
                             const uint32_t pr = __builtin_amdgcn_perm(hw, lw, cg.sel[i]);
+#if ORBX_PYR_MULHI
+                            // VOP3P v_dot2_i32_i16 with an inline-zero accumulator (the builtin becomes a v_mov + v_dot2c)
+                            asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(h[q][i]) : "v"(pr), "v"(cg.alpha[i]));
+#else
                             h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
                                                              __builtin_bit_cast(short2v, cg.alpha[i]), 0, false);
+#endif
                         }
                     }
                     uint32_t packed = 0;
+#if ORBX_PYR_MULHI
+                    // (b * (h >> 4)) >> 16 as the high word of a 24 x 24-bit product: (h & ~15) * (b << 12) >> 32, one
+                    // full-rate v_mul_hi_u32_u24 and an and for the shift-multiply-shift (h < 2^20, b <= 2049 < 2^12).
+                    // No clamp: the weights of a row (a0 + a1) and of a column pair (b0 + b1) are >= 0 and sum to at
+                    // most 2049, so every result lies in [0, 255] (the SSE2 path's saturation never engages)
+                    const uint64_t B0 = (uint64_t)(((uint32_t)b.x & 0xFFFu) << 12), B1 = (uint64_t)(((uint32_t)b.y & 0xFFFu) << 12);
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const uint64_t t0 = (uint64_t)((uint32_t)h[0][i] & 0xFFFF0u) * B0;
+                        const uint64_t t1 = (uint64_t)((uint32_t)h[1][i] & 0xFFFF0u) * B1;
+                        uint32_t v = ((uint32_t)(t0 >> 32) + (uint32_t)(t1 >> 32) + 2u) >> 2;
+                        if (tail && x0 + i >= lv.simd_end)
+                            v = (uint32_t)(__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
+                        packed |= v << (8 * i);
+                    }
+#else
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         // taps < 2^20, weights <= 2048: 24-bit multiplies (full rate) are exact
@@ -460,6 +484,7 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
                             v = (__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
                         packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
                     }
+#endif
                     if (xg < gw) *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
                 }
             }

@@ -31,7 +31,10 @@ static_assert(kBlurRows % 7 == 0, "blur chunk height must be a multiple of 7");
 constexpr int kBlurRowsSmall = 14;  // small batches (run_extract_levels): short chunks, 4.5x the waves of one frame
 static_assert(kBlurRowsSmall % 7 == 0, "blur chunk height must be a multiple of 7");
 constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity (levels >= 1)
-constexpr int kPyrU = 4;            // k_pyramid_frames: rows in flight per thread
+#ifndef ORBX_PYR_U
+#define ORBX_PYR_U 4
+#endif
+constexpr int kPyrU = ORBX_PYR_U;  // k_pyramid_frames: rows in flight per thread
 // k_pyramid_frames: threads per frame's workgroup. kPyrThreads is used when every level's 4-column
 // group count fits half of it (>= 2 rows per pass); wider levels take kPyrThreadsMax, the limit the
 // whole-frame kernel accepts (>= column groups of every level)
