@@ -32,9 +32,11 @@ constexpr int kBlurRowsSmall = 14;  // small batches (run_extract_levels): short
 static_assert(kBlurRowsSmall % 7 == 0, "blur chunk height must be a multiple of 7");
 constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity (levels >= 1)
 #ifndef ORBX_PYR_U
-#define ORBX_PYR_U 4
+#define ORBX_PYR_U 6
 #endif
-constexpr int kPyrU = ORBX_PYR_U;  // k_pyramid_frames: rows in flight per thread
+// k_pyramid_frames: rows in flight per thread (round 5, with the v_mul_hi vertical pass: 6 beats 2/4/5/7/8 by
+// 0.3-2.5 % at the bench step, pyramid alone -10 % against 4; profiles/r05_ab_pyr_rows.log)
+constexpr int kPyrU = ORBX_PYR_U;
 // k_pyramid_frames: threads per frame's workgroup. kPyrThreads is used when every level's 4-column
 // group count fits half of it (>= 2 rows per pass); wider levels take kPyrThreadsMax, the limit the
 // whole-frame kernel accepts (>= column groups of every level)
