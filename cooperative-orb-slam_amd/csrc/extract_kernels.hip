@@ -1880,6 +1880,7 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     __shared__ __align__(16) uint8_t s_patch[kFusedKps][kFusedStride];
 #if ORBX_XBLUR
     __shared__ int s_bcx[kFusedKps], s_bve[kFusedKps];  // per patch: cx0, blur_vec_end (-1: no keypoint)
+    __shared__ float4 s_trig[kFusedKps];  // per patch: (m10, m01) after IC_Angle, then (angle, cos, sin)
 #endif
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int sub = lane >> 4, ln = lane & 15;
@@ -2052,15 +2053,28 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
         m10 = A;
         m01 = M;
     }
+    float angle, a, b;
 #if ORBX_XBLUR
     // blur across the workgroup: wave w blurs patches 6w .. 6w+5 with 10 lanes each (60 of 64 lanes busy,
-    // 3 waves for 16 patches instead of 4 at 10 of 16), after every wave's IC_Angle read its raw rows
+    // 3 waves for 16 patches instead of 4 at 10 of 16), after every wave's IC_Angle read its raw rows. The
+    // last wave, which has no blur share, computes the 16 keypoints' angle / cos / sin once each meanwhile
+    // (instead of on all 16 lanes of every keypoint in every wave)
+    static_assert((kFusedWaves - 1) * 6 >= kFusedKps, "the last wave has no blur share");
     if (ln == 0) {
         s_bcx[wave * 4 + sub] = cx0;  // negative near the left edge
         s_bve[wave * 4 + sub] = valid ? lv.blur_vec_end : -1;
+        s_trig[wave * 4 + sub] = make_float4((float)m10, (float)m01, 0.f, 0.f);
     }
     __syncthreads();
-    {
+    if (wave == kFusedWaves - 1) {
+        if (lane < kFusedKps) {
+            const float4 m = s_trig[lane];
+            const float ang = fast_atan2(m.y, m.x);
+            float sa, ca;
+            glibc_sincosf(__fmul_rn(ang, (float)(3.14159265358979323846 / 180.f)), &sa, &ca);
+            s_trig[lane] = make_float4(ang, ca, sa, 0.f);
+        }
+    } else {
         const int kq = wave * 6 + lane / 10, gd = lane - 10 * (lane / 10) + 1;
         if (lane < 60 && kq < kFusedKps) {
             const int bve = s_bve[kq];
@@ -2069,17 +2083,26 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     }
     __syncthreads();
     if (!wave_on) return;  // wave-uniform, past the last barrier
+    {
+        const float4 t = s_trig[wave * 4 + sub];
+        angle = t.x;
+        a = t.y;
+        b = t.z;
+    }
 #else
     // blur in place: lanes ln < 10 own output dword g = ln + 1 (columns 4g..4g+3 of the patch)
     if (ln < 10) blur_patch_column(patch, ln + 1, cx0 + 4 * (ln + 1), lv.blur_vec_end);
-#endif
     wave_sync();
-    const float angle = fast_atan2((float)m01, (float)m10);
-    const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    const float theta = __fmul_rn(angle, factorPI);
-    float sa, ca;
-    glibc_sincosf(theta, &sa, &ca);
-    const float a = ca, b = sa;
+    angle = fast_atan2((float)m01, (float)m10);
+    {
+        const float factorPI = (float)(3.14159265358979323846 / 180.f);
+        const float theta = __fmul_rn(angle, factorPI);
+        float sa, ca;
+        glibc_sincosf(theta, &sa, &ca);
+        a = ca;
+        b = sa;
+    }
+#endif
     // blurred row r = image row y-18+r; image column x+dx = patch column 22+pm+dx
     const uint8_t* pc0 = patch + kDescPatchR * kFusedPitch + 22 + pm;
     uint32_t myword = 0;
