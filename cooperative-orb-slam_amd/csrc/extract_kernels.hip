@@ -2179,7 +2179,7 @@ hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int p
     const size_t lds = (size_t)max_rows * sizeof(int4);
     if (bands) {  // row bands: 1024 threads, so a band's rows of a level are one or two passes
         if (nbands < 1) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), dim3(nbands, nframes), dim3(kPyrThreadsMax),
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrUMax, kPyrThreadsMax>), dim3(nbands, nframes), dim3(kPyrThreadsMax),
                            lds, st, frames, fstride, pitch0, pyr, ep, levels, ptab, bands);
         return hipGetLastError();
     }
@@ -2190,7 +2190,7 @@ hipError_t launch_pyramid_frames(const uint8_t* frames, long long fstride, int p
         hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreads>), dim3(nframes), dim3(kPyrThreads), lds, st, frames,
                            fstride, pitch0, pyr, ep, levels, ptab, (const int2*)nullptr);
     else
-        hipLaunchKernelGGL((k_pyramid_frames<kPyrU, kPyrThreadsMax>), dim3(nframes), dim3(kPyrThreadsMax), lds, st,
+        hipLaunchKernelGGL((k_pyramid_frames<kPyrUMax, kPyrThreadsMax>), dim3(nframes), dim3(kPyrThreadsMax), lds, st,
                            frames, fstride, pitch0, pyr, ep, levels, ptab, (const int2*)nullptr);
     return hipGetLastError();
 }

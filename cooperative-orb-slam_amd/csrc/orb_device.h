@@ -37,6 +37,12 @@ constexpr int kPyrMaxRows = 2048;   // k_pyramid_frames: LDS row table capacity 
 // k_pyramid_frames: rows in flight per thread (round 5, with the v_mul_hi vertical pass: 6 beats 2/4/5/7/8 by
 // 0.3-2.5 % at the bench step, pyramid alone -10 % against 4; profiles/r05_ab_pyr_rows.log)
 constexpr int kPyrU = ORBX_PYR_U;
+#ifndef ORBX_PYR_UMAX
+#define ORBX_PYR_UMAX 4
+#endif
+// the same for the kPyrThreadsMax workgroups (wide levels: C4's 1241-column frames; row bands): 4, not 6, holds
+// them at 59 VGPRs (C4 199.3-199.9k against 191-193k at 6, profiles/r05_ab_pyr_rows_c4.log)
+constexpr int kPyrUMax = ORBX_PYR_UMAX;
 // k_pyramid_frames: threads per frame's workgroup. kPyrThreads is used when every level's 4-column
 // group count fits half of it (>= 2 rows per pass); wider levels take kPyrThreadsMax, the limit the
 // whole-frame kernel accepts (>= column groups of every level)
