@@ -46,7 +46,10 @@ constexpr int kPyrUMax = ORBX_PYR_UMAX;
 // k_pyramid_frames: threads per frame's workgroup. kPyrThreads is used when every level's 4-column
 // group count fits half of it (>= 2 rows per pass); wider levels take kPyrThreadsMax, the limit the
 // whole-frame kernel accepts (>= column groups of every level)
-constexpr int kPyrThreads = 512;  // (1024 at the round-5 step: -4.5 %, profiles/r05_ab_pyr1024.log)
+#ifndef ORBX_PYR_THREADS
+#define ORBX_PYR_THREADS 512
+#endif
+constexpr int kPyrThreads = ORBX_PYR_THREADS;  // 384-704 measured at 6 rows in flight: 512 best (profiles/r05_ab_pyr_threads.log)  // (1024 at the round-5 step: -4.5 %, profiles/r05_ab_pyr1024.log)
 constexpr int kPyrThreadsMax = 1024;
 constexpr int kPyrFramesMinBatch = 64;  // batches below this build the pyramid in row bands (below)
 // small batches: k_pyramid_frames over kPyrBands row bands per frame, each band's workgroup computing every level's
