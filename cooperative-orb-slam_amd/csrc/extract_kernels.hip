@@ -550,6 +550,10 @@ __device__ __forceinline__ bool fast_survivor_c(const uint8_t* s, int P, int t, 
 
 /* LDS bytes per wave of k_fast_cells2: ROI + S map (RP x RH each) + candidate list (u16 per
  * band pixel; a band is at most (RP-6) x (RH-6)) + 64 per-lane dummy slots of the compaction */
+#ifndef ORBX_FAST_WAVES
+#define ORBX_FAST_WAVES 4
+#endif
+constexpr int kFastWaves = ORBX_FAST_WAVES;  // cells (one per wave) per k_fast_cells2 workgroup
 __host__ __device__ inline int fast_wave_lds(int RP, int RH) {
     return 2 * RP * RH + ((2 * ((RP - 6) * (RH - 6) + 64) + 15) & ~15);
 }
@@ -559,14 +563,14 @@ __device__ __forceinline__ void fast_cells_body(
     const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
     const ExtractParams& ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
     uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi, int bx,
-    int f, uint8_t* lds) {
+    int f, uint8_t* lds, int wpb) {
     // compile-time ROI pitch for the common geometries: every LDS offset of the ring/NMS reads becomes an
     // instruction immediate
     const int RP = kRP ? kRP : RP_;
     // wave index through readfirstlane: the cell descriptor, loop bounds and addressing are wave-uniform
     // (scalar loads / SALU) instead of per-lane VALU
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int ci = cell_lo + bx * 4 + wave;
+    const int ci = cell_lo + bx * wpb + wave;  // wpb: cells (waves) per workgroup
     if (ci >= cell_hi) return;  // wave-uniform; no block barriers in this kernel
     const int roi_bytes = RP * RH;
     uint8_t* roi = lds + wave * fast_wave_lds(RP, RH);
@@ -772,13 +776,13 @@ __device__ __forceinline__ void fast_cells_body(
 }
 
 template <int kMaxPass, int kRP>
-__global__ __launch_bounds__(256) void k_fast_cells2(
+__global__ __launch_bounds__(64 * kFastWaves) void k_fast_cells2(
     const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
     ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
     uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi) {
     extern __shared__ __align__(16) uint8_t lds[];
     fast_cells_body<kMaxPass, kRP>(frames, fstride, pitch0, pyr, ep, levels, cells, cellkey, cellcnt, RP_, RH, cell_lo,
-                                   cell_hi, blockIdx.x, blockIdx.y, lds);
+                                   cell_hi, blockIdx.x, blockIdx.y, lds, kFastWaves);
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -1498,7 +1502,7 @@ __global__ __launch_bounds__(256) void k_fast_blur(
     extern __shared__ __align__(16) uint8_t lds[];
     if ((int)blockIdx.x < nfast)
         fast_cells_body<kMaxPass, kRP>(frames, fstride, pitch0, pyr, ep, levels, cells, cellkey, cellcnt, RP_, RH,
-                                       cell_lo, cell_hi, blockIdx.x, blockIdx.y, lds);
+                                       cell_lo, cell_hi, blockIdx.x, blockIdx.y, lds, 4);
     else
         blur_strips_body<kAligned, kBlurRowsSmall>(frames, fstride, pitch0, pyr, blur, eb, levels, 0, njobs, nullptr,
                                                    blockIdx.x - nfast, blockIdx.y, (uint8_t(*)[7][kBlurSeg])lds);
@@ -2227,10 +2231,10 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
                               uint32_t* cellkey, int* cellcnt, int RP, int RH, int max_pass, int cell_lo,
                               int cell_hi, int nframes, hipStream_t st) {
     if (cell_hi <= cell_lo) return hipSuccess;
-    dim3 grid((cell_hi - cell_lo + 3) / 4, nframes);
-    const size_t lds = 4 * (size_t)fast_wave_lds(RP, RH);
+    dim3 grid((cell_hi - cell_lo + kFastWaves - 1) / kFastWaves, nframes);
+    const size_t lds = kFastWaves * (size_t)fast_wave_lds(RP, RH);
 #define ORBX_FAST(MP, RPC)                                                                                        \
-    hipLaunchKernelGGL((k_fast_cells2<MP, RPC>), grid, dim3(256), lds, st, frames, fstride, pitch0, pyr, ep, levels, \
+    hipLaunchKernelGGL((k_fast_cells2<MP, RPC>), grid, dim3(64 * kFastWaves), lds, st, frames, fstride, pitch0, pyr, ep, levels, \
                        cells, cellkey, cellcnt, RP, RH, cell_lo, cell_hi)
     if (max_pass <= 8 && RP == 40)
         ORBX_FAST(8, 40);
