@@ -110,6 +110,7 @@ __device__ __forceinline__ v8i fp4_operand(v4i a) {  // fp4 reads only the low 4
 }
 
 constexpr int kMfChunk = 64;  // candidates staged per step (two 32-row tiles)
+constexpr int kMfBufs = 2;   // LDS chunk buffers of k_tri_mfma (staging of chunk c+1 overlaps chunk c's MFMAs)
 constexpr int kMfWaves = 8;    // query waves per workgroup (32 queries each); they share each chunk's expansion
 constexpr int kMfThreads = 64 * kMfWaves;
 
@@ -122,10 +123,10 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
                                                   int32_t* __restrict__ nmatch) {
     static_assert(kMfWaves == 4 || kMfWaves == 8, "fp4 expansion roles: 4 waves (2 dwords per thread) or 8 (1)");
     constexpr int kDw = 512 / kMfThreads;  // descriptor dwords expanded per thread and chunk
-    __shared__ v4i s_frag[2][4][64];  // [tile][step][lane] candidate fragments (fp4 +-1)
+    __shared__ v4i s_frag[kMfBufs][2][4][64];  // [buffer][tile][step][lane] candidate fragments (fp4 +-1)
     // per candidate (x, y, epipolar threshold thf or -1 when it is near the epipole / past n2): one
     // ds_read_b128 per geometric check in the key walk (instead of four b32 reads + a threshold gather)
-    __shared__ float4 s_rec[kMfChunk];
+    __shared__ float4 s_rec[kMfBufs][kMfChunk];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int qblk = blockIdx.x * (32 * kMfWaves);
     if (qblk >= s.n1) return;  // block-uniform
@@ -161,27 +162,36 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
     DwT pd;
     orbx_kp pk;
     load_chunk(0, pd, pk);
-    for (int cb = 0; cb < s.n2; cb += kMfChunk) {
-        {
-            const bool on = cb + ec < s.n2;
-            const int tile = ec >> 5, r = ec & 31;
+    // chunk staging into LDS buffer bw (candidates cbw ..): expansion of the prefetched descriptor dwords and the
+    // per-candidate geometry record
+    auto stage = [&](int cbw, int bw) {
+        const bool on = cbw + ec < s.n2;
+        const int tile = ec >> 5, r = ec & 31;
 #pragma unroll
-            for (int k = 0; k < kDw; k++)
-                s_frag[tile][(ed + k) >> 1][32 * ((ed + k) & 1) + r] = fp4_pm1_dword(on ? pd.w[k] : 0u);
-            if (tid < kMfChunk) {
-                const bool on2 = cb + tid < s.n2 && !near_epipole(g, pk.x, pk.y, pk.octave);
-                s_rec[tid] = make_float4(pk.x, pk.y, on2 ? g.th384f[pk.octave] : -1.0f, 0.0f);
-            }
+        for (int k = 0; k < kDw; k++)
+            s_frag[bw][tile][(ed + k) >> 1][32 * ((ed + k) & 1) + r] = fp4_pm1_dword(on ? pd.w[k] : 0u);
+        if (tid < kMfChunk) {
+            const bool on2 = cbw + tid < s.n2 && !near_epipole(g, pk.x, pk.y, pk.octave);
+            s_rec[bw][tid] = make_float4(pk.x, pk.y, on2 ? g.th384f[pk.octave] : -1.0f, 0.0f);
         }
-        __syncthreads();
-        if (cb + kMfChunk < s.n2) load_chunk(cb + kMfChunk, pd, pk);
+    };
+    // double-buffered: chunk c+1 is expanded into the other buffer before chunk c's MFMAs, so one barrier per chunk
+    // (the one that publishes c+1 and retires c's reads) instead of two
+    stage(0, 0);
+    __syncthreads();
+    if (kMfChunk < s.n2) load_chunk(kMfChunk, pd, pk);
+    for (int cb = 0, bf = 0; cb < s.n2; cb += kMfChunk, bf ^= 1) {
+        if (cb + kMfChunk < s.n2) {
+            stage(cb + kMfChunk, bf ^ 1);
+            if (cb + 2 * kMfChunk < s.n2) load_chunk(cb + 2 * kMfChunk, pd, pk);
+        }
         v16f acc0 = (v16f)0.f, acc1 = (v16f)0.f;
 #pragma unroll
         for (int st = 0; st < 4; st++) {
             // cbsz = blgp = 4: fp4 (e2m1) A and B; E8M0 scales 127 = 2^0
-            acc0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_operand(s_frag[0][st][lane]), fp4_operand(bq[st]),
+            acc0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_operand(s_frag[bf][0][st][lane]), fp4_operand(bq[st]),
                                                                    acc0, 4, 4, 0, 127, 0, 127);
-            acc1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_operand(s_frag[1][st][lane]), fp4_operand(bq[st]),
+            acc1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_operand(s_frag[bf][1][st][lane]), fp4_operand(bq[st]),
                                                                    acc1, 4, 4, 0, 127, 0, 127);
         }
 #pragma unroll
@@ -200,7 +210,7 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
             uint32_t km = key(pmax);
             while (km < best && (km >> 16) <= 50u) {  // TH_LOW (ORBmatcher.cc:715)
                 const int jl = (int)(65535u - (km & 0xFFFFu)) - cb;
-                const float4 c2 = s_rec[jl];
+                const float4 c2 = s_rec[bf][jl];
                 if (epi_ok_f(la, lb, lc, c2.x, c2.y, c2.z)) {
                     best = km;
                     break;
