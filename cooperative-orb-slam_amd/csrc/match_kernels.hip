@@ -235,7 +235,14 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
     }
 }
 
-__global__ __launch_bounds__(kMfThreads) void k_tri_mfma(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
+// 6 waves per SIMD: the compiler fits the kernel in 80 VGPRs (88 unconstrained: 5 waves) without scratch; match-only
+// +19 % (C2 3.50M -> 4.18M pairs/s, 18.2 % -> 21.7 % of the fp4 peak), C2 step +0.5-1 %, C3 +-0, C4 -0.6 %
+// (profiles/r05_ab_match_occupancy.log)
+#ifndef ORBX_MF_WPE
+#define ORBX_MF_WPE 6
+#endif
+#define ORBX_MF_ATTR __attribute__((amdgpu_waves_per_eu(ORBX_MF_WPE)))
+__global__ __launch_bounds__(kMfThreads) ORBX_MF_ATTR void k_tri_mfma(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
                                                   const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
                                                   const int32_t* __restrict__ counts, int kp_stride, MatchGeom g,
                                                   int32_t* __restrict__ match12, int32_t* __restrict__ nmatches) {
