@@ -377,9 +377,6 @@ struct PyrColGroup {
 };
 static_assert(sizeof(PyrColGroup) == 48, "PyrColGroup layout");
 
-#ifndef ORBX_PYR_MULHI
-#define ORBX_PYR_MULHI 1
-#endif
 template <int U, int NT>
 __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict__ frames, long long fstride,
                                                          int pitch0, uint8_t* __restrict__ pyr, ExtractParams ep,
@@ -450,17 +447,11 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
                             const uint32_t pr = __builtin_amdgcn_perm(hw, lw, cg.sel[i]);
-#if ORBX_PYR_MULHI
                             // VOP3P v_dot2_i32_i16 with an inline-zero accumulator (the builtin becomes a v_mov + v_dot2c)
                             asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(h[q][i]) : "v"(pr), "v"(cg.alpha[i]));
-#else
-                            h[q][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr),
-                                                             __builtin_bit_cast(short2v, cg.alpha[i]), 0, false);
-#endif
                         }
                     }
                     uint32_t packed = 0;
-#if ORBX_PYR_MULHI
                     // (b * (h >> 4)) >> 16 as the high word of a 24 x 24-bit product: (h & ~15) * (b << 12) >> 32, one
                     // full-rate v_mul_hi_u32_u24 and an and for the shift-multiply-shift (h < 2^20, b <= 2049 < 2^12).
                     // No clamp: the weights of a row (a0 + a1) and of a column pair (b0 + b1) are >= 0 and sum to at
@@ -475,16 +466,6 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
                             v = (uint32_t)(__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
                         packed |= v << (8 * i);
                     }
-#else
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        // taps < 2^20, weights <= 2048: 24-bit multiplies (full rate) are exact
-                        int v = ((__mul24(h[0][i] >> 4, (int)b.x) >> 16) + (__mul24(h[1][i] >> 4, (int)b.y) >> 16) + 2) >> 2;
-                        if (tail && x0 + i >= lv.simd_end)
-                            v = (__mul24(h[0][i], (int)b.x) + __mul24(h[1][i], (int)b.y) + (1 << 21)) >> 22;
-                        packed |= (uint32_t)iclamp(v, 0, 255) << (8 * i);
-                    }
-#endif
                     if (xg < gw) *(uint32_t*)(dst + (unsigned)(y * lv.pitch + x0)) = packed;
                 }
             }
@@ -1783,11 +1764,12 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
 /*  column cx0 = (x-22) & ~3 is staged in LDS by LDS-DMA (pitch 48; rows REFLECT_101 by   */
 /*  address, columns clamped into the row and the two halo columns on either side        */
 /*  patched as REFLECT_101 for keypoints near an edge). IC_Angle (ORBextractor.cc:77-104) */
-/*  reads its 31x31 window there. Then 10 of the keypoint's 16 lanes blur the patch in    */
-/*  place (ORBextractor.cc:1085-1086): lane = 4 output columns (dword g = 1..10), a 7-row  */
-/*  register window of float row sums walking the 43 rows; output row r (image row        */
-/*  y-18+r) overwrites source row r, which no later row sum reads (the lanes of a wave    */
-/*  issue in lockstep and LDS operations of a wave complete in order). The row sums are    */
+/*  reads its 31x31 window there. After a workgroup barrier waves 0-2 blur the 16 patches  */
+/*  in place (ORBextractor.cc:1085-1086), 6 patches per wave at 10 lanes each: lane = 4    */
+/*  output columns (dword g = 1..10), a 7-row register window of float row sums walking    */
+/*  the 43 rows; output row r (image row y-18+r) overwrites source row r, which no later   */
+/*  row sum reads (a patch's lanes are lanes of one wave: they issue in lockstep and its   */
+/*  LDS operations complete in order); wave 3 computes the 16 angles meanwhile. Row sums:  */
 /*  ten v_dot4 per 4 outputs on the three aligned dwords around them (no alignbyte); the   */
 /*  vertical sums, the rounding (SSE2 column path RNE, scalar tail half-up) are those of   */
 /*  k_blur_strips, so every blurred byte rBRIEF samples equals the whole-level blur's.     */
@@ -1798,15 +1780,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
 constexpr int kFusedRows = 43;   // source rows y-21 .. y+21
 constexpr int kFusedPitch = 48;  // 12 dwords: columns cx0 .. cx0+47 cover x-21 .. x+21 for any (x-22) & 3
 constexpr int kFusedDwords = kFusedRows * kFusedPitch / 4;  // 516 per keypoint
-#ifndef ORBX_XBLUR
-#define ORBX_XBLUR 1
-#endif
 #ifndef ORBX_FUSED_STRIDE
-#if ORBX_XBLUR
 #define ORBX_FUSED_STRIDE 2088  // 522 dwords = 10 banks mod 64: the blur's 60 lanes of a wave hit 60 distinct banks
-#else
-#define ORBX_FUSED_STRIDE (kFusedRows * kFusedPitch)
-#endif
 #endif
 constexpr int kFusedStride = ORBX_FUSED_STRIDE;  // bytes between the keypoints' patches in LDS
 
@@ -1882,10 +1857,8 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     __shared__ PatPt s_pat[256];
     __shared__ int2 s_ic[256];
     __shared__ __align__(16) uint8_t s_patch[kFusedKps][kFusedStride];
-#if ORBX_XBLUR
     __shared__ int s_bcx[kFusedKps], s_bve[kFusedKps];  // per patch: cx0, blur_vec_end (-1: no keypoint)
     __shared__ float4 s_trig[kFusedKps];  // per patch: (m10, m01) after IC_Angle, then (angle, cos, sin)
-#endif
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int sub = lane >> 4, ln = lane & 15;
     // XCD-aware block mapping as k_describe: every workgroup of a frame on one XCD
@@ -1934,9 +1907,6 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
         if (ep.host_out) __threadfence_system();
     }
     __syncthreads();
-#if !ORBX_XBLUR
-    if (__ballot(g < ep.kp_per_frame) == 0) return;  // wave-uniform
-#endif
     const int l = level_of(ep.kp_off, ep.L, gc);
     const int k = gc - ep.kp_off[l];
     int mycnt = 0, outidx = k;
@@ -1947,9 +1917,6 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     }
     const bool valid = g < ep.kp_per_frame && k < mycnt;
     const bool wave_on = __ballot(valid) != 0;  // wave-uniform
-#if !ORBX_XBLUR
-    if (!wave_on) return;
-#endif
     const LevelDesc lv = levels[l];
     const uint32_t kk = valid ? kk_raw : 0u;
     const int x = valid ? (int)(kk & 0xFFF) : 32, y = valid ? (int)((kk >> 12) & 0xFFF) : 32;
@@ -1963,7 +1930,7 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     // row's last valid dword takes the clamped / reflected staging
     const int edge = (y < 21 || y + 21 >= lv.h || x < 22 || x + 21 >= lv.w || cx0 + 44 > lastd) ? 1 : 0;
     uint8_t* patch = s_patch[wave * 4 + sub];
-    if (wave_on) {  // a wave without keypoints (only with ORBX_XBLUR) stages nothing
+    if (wave_on) {  // a wave without keypoints stages nothing (it still reaches the barriers)
         int rq[9], cq[9];
 #pragma unroll
         for (int q = 0; q < 9; q++) {
@@ -2058,7 +2025,6 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
         m01 = M;
     }
     float angle, a, b;
-#if ORBX_XBLUR
     // blur across the workgroup: wave w blurs patches 6w .. 6w+5 with 10 lanes each (60 of 64 lanes busy,
     // 3 waves for 16 patches instead of 4 at 10 of 16), after every wave's IC_Angle read its raw rows. The
     // last wave, which has no blur share, computes the 16 keypoints' angle / cos / sin once each meanwhile
@@ -2093,20 +2059,6 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
         a = t.y;
         b = t.z;
     }
-#else
-    // blur in place: lanes ln < 10 own output dword g = ln + 1 (columns 4g..4g+3 of the patch)
-    if (ln < 10) blur_patch_column(patch, ln + 1, cx0 + 4 * (ln + 1), lv.blur_vec_end);
-    wave_sync();
-    angle = fast_atan2((float)m01, (float)m10);
-    {
-        const float factorPI = (float)(3.14159265358979323846 / 180.f);
-        const float theta = __fmul_rn(angle, factorPI);
-        float sa, ca;
-        glibc_sincosf(theta, &sa, &ca);
-        a = ca;
-        b = sa;
-    }
-#endif
     // blurred row r = image row y-18+r; image column x+dx = patch column 22+pm+dx
     const uint8_t* pc0 = patch + kDescPatchR * kFusedPitch + 22 + pm;
     uint32_t myword = 0;
