@@ -22,7 +22,11 @@ uploaded from pinned host memory on a copy stream, overlapped with the previous 
 (ORBextractor::operator() takes a host image, ORBextractor.cc:1043-1050).
 
 --config c2 (default, the BASELINE metric) | c3 (752x480, 1200 features) | c4 (1241x376, 2000
-features): the BASELINE configs 3 and 4 at their geometries (left images, same step).
+features): the BASELINE configs 3 (EuRoC MH01 stereo) and 4 (KITTI 00 stereo) as the stereo frames they name:
+each frame is a rectified left/right pair (synthetic: the right image is the left crop shifted by a fixed
+disparity), both images extracted, Frame::ComputeStereoMatches on the device, and SearchForTriangulation's stereo
+branch against the previous frame (ORB_SLAM2.1/src/Frame.cc:80-92, 471-645; ORBmatcher.cc:703-749); `value` is
+stereo frames (pairs) per second. --mono runs their left images alone (the rounds 1-5 lines).
 
 Launch (N>1): python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
               --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
@@ -43,14 +47,17 @@ sys.path.insert(0, os.path.join(ROOT, "cooperative-orb-slam_amd"))
 
 VALU_PEAK_GINST = 1228.8  # 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU op (G wave-instr/s)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ALONE_LAUNCHES = 7  # roofline.alone: launches of the priced kernel with nothing else on the GPU (median)
 FP4_MFMA_PEAK_TOPS = 10000.0  # dense fp4 (MX-scaled f8f6f4) MFMA, 4x the 2.5 PF dense bf16 rate (MI355X_MICROARCH.md "Matrix cores")
 
 CONFIGS = {
     "c2": dict(W=640, H=480, nfeatures=1000, name="C2: synthetic 640x480 uint8, nfeatures 1000"),
-    "c3": dict(W=752, H=480, nfeatures=1200, name="C3: synthetic 752x480 uint8 (EuRoC geometry, left images), "
-                                                  "nfeatures 1200"),
-    "c4": dict(W=1241, H=376, nfeatures=2000, name="C4: synthetic 1241x376 uint8 (KITTI geometry, left images), "
-                                                   "nfeatures 2000"),
+    # stereo: the rig (orbamd.device.STEREO_RIGS: Camera.bf and mb = bf / fx of EuRoC.yaml / KITTI00-02.yaml) and the
+    # synthetic right image's disparity in pixels (orbx_synth_scene_frames dx)
+    "c3": dict(W=752, H=480, nfeatures=1200, stereo="euroc", dx=11,
+               name="C3: synthetic 752x480 uint8 (EuRoC geometry), nfeatures 1200"),
+    "c4": dict(W=1241, H=376, nfeatures=2000, stereo="kitti", dx=19,
+               name="C4: synthetic 1241x376 uint8 (KITTI geometry), nfeatures 2000"),
 }
 
 
@@ -139,11 +146,14 @@ def host_cpu_info():
     return info
 
 
-def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000):
+def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000, stereo=None):
     """Oracle ("port") timed on host cores: extract + BF SearchForTriangulation vs the previous
     frame, one independent frame stream per thread (ctypes releases the GIL). Stops after `seconds`
     or once `nframes` frames are done in total. Returns frames/s, frames, seconds, per-stage seconds
-    per frame (oracle stage timers + the matcher timed around its call)."""
+    per frame (oracle stage timers + the matcher timed around its call). stereo=(mbf, mb): frames are
+    [N, 2, H, W] pairs and a frame is the stereo Frame's work: both images extracted (the reference runs the
+    two extractions on two threads, Frame.cc:80-81; here each thread's frame stream runs them in turn, and
+    every core runs its own stream), ComputeStereoMatches, and the stereo SearchForTriangulation."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
     import orbamd
@@ -155,8 +165,11 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000):
     total = [0]
     lock = threading.Lock()
 
+    stereo_s = [0.0] * threads
+
     def work(tid):
         orc = oracle_py.OracleExtractor(nfeatures, 1.2, 8, 20, 7)
+        orr = oracle_py.OracleExtractor(nfeatures, 1.2, 8, 20, 7) if stereo else None
         tabs = orc.tables()
         prev = None
         i = tid
@@ -167,8 +180,16 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000):
                         break
                     total[0] += 1
             img = frames[i % len(frames)]
-            k, d = orc(img)
-            cur = orbamd.KeyFrameView(k, d, tabs["scale"], tabs["sigma2"])
+            ur = None
+            if stereo:
+                k, d = orc(img[0])
+                kr, dr = orr(img[1])
+                ts = time.perf_counter()
+                ur = oracle_py.compute_stereo_matches(orc, orr, k, d, kr, dr, stereo[0], stereo[1])[0]
+                stereo_s[tid] += time.perf_counter() - ts
+            else:
+                k, d = orc(img)
+            cur = orbamd.KeyFrameView(k, d, tabs["scale"], tabs["sigma2"], uright=ur)
             if prev is not None:
                 tm = time.perf_counter()
                 oracle_py.search_for_triangulation(cur, prev, F12, ex, ey, False, False)
@@ -177,6 +198,9 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000):
             count[tid] += 1
             i += threads
         stage[tid] = orc.stage_times()[0]
+        if stereo:  # both extractors' stage timers
+            for k2, v in orr.stage_times()[0].items():
+                stage[tid][k2] = stage[tid].get(k2, 0.0) + v
 
     t0 = time.perf_counter()
     ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
@@ -188,33 +212,44 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000):
     n = max(sum(count), 1)
     per = {k: sum(st[k] for st in stage) / n for k in stage[0]}
     per["match"] = sum(match_s) / max(n - threads, 1)
+    if stereo:
+        per["stereo"] = sum(stereo_s) / n
     return sum(count) / el, sum(count), el, per
 
 
 def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, dist, nstreams=4):
     """The schedule with every step's B frames uploaded from pinned host memory (the frame pool, batch
-    i mod pool at step i) into the device batch the step processes: graph p's frames on copy stream
-    p mod nstreams (several DMA engines in flight), and graph p starts extracting as soon as its own frames
-    have arrived. Upload i waits for step i-pool (the previous user of that device batch), so an upload
-    overlaps the previous step's compute. Returns frames/s over nsteps after `pool` warm-up steps and the
-    H2D rate achieved (W*H bytes per frame, max over ranks)."""
+    i mod pool at step i) into the device batch the step processes, on `nstreams` copy streams whatever the
+    graph count (several DMA engines in flight: round 3's fourth copy stream was +36 %, and tying the streams to
+    the graphs lost it when the step went to 3 graphs): each graph's frames are cut into ceil(nstreams / P)
+    contiguous chunks dealt round-robin over the streams in graph order, and graph p starts extracting as soon
+    as its own chunks have arrived. Upload i waits for step i-pool (the previous user of that device batch), so
+    an upload overlaps the previous step's compute. Returns frames/s over nsteps after `pool` warm-up steps and
+    the H2D rate achieved (bytes per frame uploaded, max over ranks)."""
     P, sub, dev = sched.P, sched.sub, sched.dev
-    host = [torch.from_numpy(frames_np[r * B:(r + 1) * B]).pin_memory() for r in range(pool)]
-    copy_st = [torch.cuda.Stream(dev) for _ in range(max(1, min(nstreams, P)))]
-    up = [[torch.cuda.Event() for _ in range(P)] for _ in range(pool)]
+    per = sched.images_per_frame  # 2 for stereo pairs (left + right image per frame)
+    host = [torch.from_numpy(sched.host_batch(frames_np, r)).pin_memory() for r in range(pool)]
+    nst = max(1, nstreams)
+    copy_st = [torch.cuda.Stream(dev) for _ in range(nst)]
+    k = -(-nst // P)  # chunks per graph
+    imgs = per * sub
+    cuts = [(j * imgs // k, (j + 1) * imgs // k) for j in range(k)]
+    up = [[[torch.cuda.Event() for _ in range(k)] for _ in range(P)] for _ in range(pool)]
     done = [[torch.cuda.Event() for _ in range(P)] for _ in range(pool)]
     used = [False] * pool
 
     def one(i):
         r = i % pool
         for p in range(P):
-            cs = copy_st[p % len(copy_st)]
-            with torch.cuda.stream(cs):
-                if used[r]:
-                    for e in done[r]:
-                        cs.wait_event(e)
-                sched.frames[r][p].copy_(host[r][p * sub:(p + 1) * sub], non_blocking=True)
-                up[r][p].record(cs)
+            dst = sched.device_images(r, p)
+            for j, (a, b) in enumerate(cuts):
+                cs = copy_st[(p * k + j) % nst]
+                with torch.cuda.stream(cs):
+                    if used[r]:
+                        for e in done[r]:
+                            cs.wait_event(e)
+                    dst[a:b].copy_(host[r][p * imgs + a:p * imgs + b], non_blocking=True)
+                    up[r][p][j].record(cs)
         sched.step(batch=r, wait=up[r], first=i == 0)
         for p in range(P):
             done[r][p].record(sched.streams[p])
@@ -236,11 +271,11 @@ def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, 
         el = float(t.item())
     fps = world * B * nsteps / el
     return {"frames_per_s": round(fps, 1), "per_gpu_frames_per_s": round(fps / world, 1),
-            "h2d_GBs_per_gpu": round(B * W * H * nsteps / el / 1e9, 2), "steps": nsteps, "seconds": round(el, 3),
-            "copy_streams": len(copy_st),
+            "h2d_GBs_per_gpu": round(per * B * W * H * nsteps / el / 1e9, 2), "steps": nsteps, "seconds": round(el, 3),
+            "copy_streams": nst, "chunks_per_graph": k,
             "source": "pinned host memory, %d batches of %d frames uploaded round-robin (one batch per step) on %d "
-                      "copy streams, overlapped with the previous step's compute; each graph starts on its own "
-                      "frames' arrival" % (pool, B, len(copy_st))}
+                      "copy streams (%d chunks per graph), overlapped with the previous step's compute; each graph "
+                      "starts on its own frames' arrival" % (pool, B, nst, k)}
 
 
 def launch_ranks(n, argv):
@@ -272,7 +307,10 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
-    ap.add_argument("--batch", type=int, default=3072, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per step per GPU (0: 3072, or 1536 stereo pairs = 3072 images at c3 / c4)")
+    ap.add_argument("--mono", action="store_true",
+                    help="c3 / c4: their left images alone (monocular frames) instead of the stereo pairs the configs name")
     ap.add_argument("--pipes", type=int, default=3,
                     help="concurrent extraction+match graphs per GPU (each over batch/pipes frames, own handle "
                          "and HIP stream), staggered: graph p starts a step when graph p-1 finished extracting it")
@@ -323,12 +361,13 @@ def main():
                          "K-th step after it; pyr_ / fast_: after graph p-1's pyramid / FAST instead (a third of the step "
                          "apart at 3 graphs)")
     ap.add_argument("--launch-frames", action="store_true",
-                    help="print the frames one stage launch processes (--batch / --pipes) and the graph count, and exit "
-                         "(no GPU use)")
+                    help="print the images one stage launch processes (--batch / --pipes frames, x2 for stereo pairs) and "
+                         "the graph count, and exit (no GPU use)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
-    if args.launch_frames:
-        print(args.batch // args.pipes, args.pipes)
+    if args.launch_frames:  # images one stage launch processes (stereo: a graph's left + right images)
+        per = 1 if args.mono or "stereo" not in cfg else 2
+        print(per * ((args.batch or 3072 // per) // args.pipes), args.pipes)
         return
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -362,12 +401,24 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    W, H, B, P = cfg["W"], cfg["H"], args.batch, args.pipes
+    W, H, P = cfg["W"], cfg["H"], args.pipes
+    rig = None if args.mono or "stereo" not in cfg else orbamd.device.STEREO_RIGS[cfg["stereo"]]
+    per = 2 if rig else 1  # images per frame
+    B = args.batch or (3072 // per)
     assert B % P == 0, "--batch must be a multiple of --pipes"
     assert args.pool >= 1
     sub = B // P
+    imgs = per * sub  # images one extraction launch processes
     scene = 0 if args.scene == "shared" else None
-    frames_np = orbamd.synth_frames(rank, 0, args.pool * B, W, H, scene=scene)  # agent = rank; pool batches back to back
+
+    def agent_frames(r, t0, n):
+        """agent r's frames t0 .. t0+n-1: uint8 [n, H, W], or [n, 2, H, W] stereo pairs (the right image: the crop
+        shifted by the config's disparity)"""
+        left = orbamd.synth_frames(r, t0, n, W, H, scene=scene)
+        if not rig:
+            return left
+        return np.stack([left, orbamd.synth_frames(r, t0, n, W, H, dx=cfg["dx"], scene=scene)], axis=1)
+    frames_np = agent_frames(rank, 0, args.pool * B)  # agent = rank; pool batches back to back
     def allgather(out, inp):
         # RCCL over xGMI; gloo (the one-GPU rehearsal): through host memory
         if backend == "nccl":
@@ -384,7 +435,7 @@ def main():
                           allgather=allgather if use_dist else None,
                           stagger=args.stagger, exchange=not args.no_exchange,
                           priorities=[hi_prio if p < n_hi else lo_prio for p in range(P)], nfeatures=cfg["nfeatures"],
-                          pool=args.pool, async_exchange=async_x)
+                          pool=args.pool, async_exchange=async_x, stereo=rig)
     pipes = sched.pipes
     if args.serial_stages:
         for pp in pipes:
@@ -409,6 +460,8 @@ def main():
         evs = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(P)]
                for _ in range(nsteps)]
         xevs = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(nsteps)]
+        sevs = ([[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(P)]
+                 for _ in range(nsteps)] if rig else None)
         if timed and use_dist:
             dist.barrier()
         torch.cuda.synchronize()
@@ -419,7 +472,7 @@ def main():
             if timed:
                 sched.step(first=i == 0)
             else:
-                sched.step(evs[i], xevs[i], first=i == 0)
+                sched.step(evs[i], xevs[i], first=i == 0, sev=sevs[i] if rig else None)
         torch.cuda.synchronize()
         if timed and use_dist:
             dist.barrier()
@@ -438,6 +491,8 @@ def main():
         if timed:
             return elapsed, st
         st["match"] = sum(e[p][0].elapsed_time(e[p][1]) for e in evs for p in range(P)) / (nsteps * P)
+        if rig:
+            st["stereo"] = sum(e[p][0].elapsed_time(e[p][1]) for e in sevs for p in range(P)) / (nsteps * P)
         if not args.no_exchange:
             st["exchange"] = sum(x[0].elapsed_time(x[1]) for x in xevs) / nsteps
             st["allgather"] = sum(a.elapsed_time(b) for a, b in sched.ag_events) / max(len(sched.ag_events), 1)
@@ -477,7 +532,7 @@ def main():
     except RuntimeError as e:
         err_msg = str(e)
     check = None
-    agent_kf = lambda r, t: orbamd.synth_frames(r, t, 1, W, H, scene=scene)[0]  # noqa: E731 (agent r's keyframe image)
+    agent_kf = lambda r, t: agent_frames(r, t, 1)[0]  # noqa: E731 (agent r's keyframe image / stereo pair)
     if not args.no_check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from check_schedule import check_schedule
@@ -488,6 +543,25 @@ def main():
         t = torch.tensor([0 if ok_local else 1], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ok_all = int(t.item()) == 0
+    # 3b) the priced kernels alone (untimed, after the check): graph 0 re-extracts the last batch in stage order with
+    # every other graph idle, one step at a time, the priced stages bracketed by HIP events; the live launch above is
+    # the kernel's share of a chip running the other graphs, this is its own speed (roofline.alone)
+    alone_ms = {}
+    pp0 = pipes[0]
+    lib.orbx_debug_serial(pp0.ext._h, 1)
+    for kern in [dom] + ([co] if co else []):
+        vals = []
+        for _ in range(ALONE_LAUNCHES):
+            lib.orbx_profile_enable(pp0.ext._h, 1 << stages.index(kern))
+            pp0.extract(sched.frames[last_batch][0], sched.streams[0].cuda_stream, stereo=False)
+            torch.cuda.synchronize()
+            ms = (C.c_double * 5)()
+            nc = C.c_int()
+            lib.orbx_profile_read(pp0.ext._h, ms, C.byref(nc))
+            vals.append(ms[stages.index(kern)] / max(nc.value, 1))
+        alone_ms[kern] = sorted(vals)[len(vals) // 2]
+    lib.orbx_profile_enable(pp0.ext._h, 0)
+    lib.orbx_debug_serial(pp0.ext._h, 0)
     # 4) extract-only and match-only rates, untimed breakdown passes; and the box's
     # measured device-to-device copy bandwidth (read + write bytes of a 1 GiB copy) beside the nominal peak
     copy_gbs = None
@@ -558,21 +632,34 @@ def main():
                 pmc = json.load(open(pmc_path))
             except Exception:
                 pmc = {}
-            if pmc.get("frames_per_launch", 256) != sub:  # counters of another launch size do not price this one
+            if pmc.get("frames_per_launch", 256) != imgs:  # counters of another launch size do not price this one
                 pmc = {}
         sel = ("largest stage of this run's stage split (%s)" % ", ".join("%s %.3f ms" % (k, stage_ms[k]) for k in stages)
                if args.roof_kernel == "auto" else "--roof-kernel")
 
         def price(kern):
             """the kernel's roofline at its live launch duration in the timed region (one launch = one graph's
-            sub-batch of B / P frames): VALU issue from the counter pass, algorithmic bytes against HBM"""
+            sub-batch of B / P frames, `imgs` images): VALU issue from the counter pass, algorithmic bytes against
+            HBM; `alone`: the same launch with nothing else on the GPU (its own efficiency, measured after the timed
+            region: graph 0's extraction in stage order, one launch at a time)"""
             k_ms = dom_live[kern]
-            hbm_gbs = per_stage[kern] * sub / (k_ms * 1e-3) / 1e9 if k_ms > 0 and per_stage[kern] > 0 else 0.0
+            hbm_gbs = per_stage[kern] * imgs / (k_ms * 1e-3) / 1e9 if k_ms > 0 and per_stage[kern] > 0 else 0.0
             rec = pmc.get(kern, {})
             traffic, valu_insts = rec.get("hbm_bytes_per_launch"), rec.get("valu_insts_per_launch")
             valu_gs = valu_insts / (k_ms * 1e-3) / 1e9 if valu_insts and k_ms > 0 else None
+            a_ms = alone_ms.get(kern)
+            alone = None
+            if a_ms:
+                alone = {"launch_ms": round(a_ms, 4), "share_of_live": round(a_ms / k_ms, 4) if k_ms > 0 else None,
+                         "alg_hbm_frac": round(per_stage[kern] * imgs / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                         "valu_frac": (round(valu_insts / (a_ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4) if valu_insts
+                                       else None),
+                         "counter_hbm_frac": (round(traffic / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic
+                                              else None),
+                         "how": "graph 0 alone on the GPU (orbx_debug_serial), HIP events around the stage, median of "
+                                "%d launches" % ALONE_LAUNCHES}
             hbm = {"achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": round(hbm_gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": round(per_stage[kern] * sub),
+                   "frac": round(hbm_gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": round(per_stage[kern] * imgs),
                    "measured_copy_GBs": round(copy_gbs, 1) if copy_gbs else None,
                    "frac_vs_copy": round(hbm_gbs / copy_gbs, 5) if copy_gbs else None}
             if valu_gs is not None and valu_gs / VALU_PEAK_GINST > hbm_gbs / HBM_PEAK_GBS:
@@ -580,9 +667,9 @@ def main():
                 return {"bound": "valu", "kernel": kern, "achieved": round(valu_gs, 1), "peak": VALU_PEAK_GINST,
                         "unit": "G wave64 VALU instr/s", "frac": round(valu_gs / VALU_PEAK_GINST, 4),
                         "traffic": traffic, "valu_insts_per_launch": valu_insts, "launch_ms": round(k_ms, 4),
-                        "hbm": hbm}
+                        "hbm": hbm, "alone": alone}
             return {"bound": "hbm", "kernel": kern, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": hbm["frac"], "traffic": traffic, "launch_ms": round(k_ms, 4), "hbm": hbm}
+                    "frac": hbm["frac"], "traffic": traffic, "launch_ms": round(k_ms, 4), "hbm": hbm, "alone": alone}
 
         roof = price(dom)
         roof["selected_by"] = sel
@@ -601,13 +688,13 @@ def main():
         # them; plus the whole step's VALU issue rate (every stage's VALU wave-instructions x P launches per step
         # / ms_per_step)
         stage_roof, step_valu = {}, 0.0
-        for k in stages + ["match"]:
+        for k in stages + ["match"] + (["stereo"] if rig else []):
             if k == "blur" and fused:
                 continue  # no separate blur stage ran (the event pair around nothing reads a few microseconds)
             ms = stage_ms.get(k, 0.0)
             rec = pmc.get(k, {})
             vi, hb = rec.get("valu_insts_per_launch"), rec.get("hbm_bytes_per_launch")
-            alg = round(per_stage.get(k, 0) * sub) if k in per_stage else None
+            alg = round(per_stage.get(k, 0) * imgs) if k in per_stage else None
             row = {"launch_ms": round(ms, 4), "valu_insts_per_launch": vi, "hbm_bytes_per_launch": hb}
             if ms > 0:
                 if vi:
@@ -625,10 +712,12 @@ def main():
                            "peak": VALU_PEAK_GINST, "unit": "G wave64 VALU instr/s",
                            "frac": round(step_valu / step_s / 1e9 / VALU_PEAK_GINST, 4)} if step_valu else None)
         result = {
-            "metric": "frames/sec ORB extract+match, 640x480 mono, 1000 feat/frame" if args.config == "c2" else
-                      "frames/sec ORB extract+match, %dx%d, %d feat/frame" % (W, H, cfg["nfeatures"]),
+            "metric": ("frames/sec ORB extract+match, 640x480 mono, 1000 feat/frame" if args.config == "c2" else
+                       "stereo frames/sec ORB extract(L+R)+stereo match+match, %dx%d, %d feat/image" % (W, H, cfg["nfeatures"])
+                       if rig else "frames/sec ORB extract+match, %dx%d left images, %d feat/frame"
+                       % (W, H, cfg["nfeatures"])),
             "value": round(value, 2),
-            "unit": "frames/s",
+            "unit": "stereo frames/s" if rig else "frames/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -638,11 +727,14 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic textured pan, SURVEY.md 8(d)); resident in HBM",
-            "config": {"workload": cfg["name"] + ", scale 1.2, 8 levels, FAST 20/7; extract + BF "
-                                                 "SearchForTriangulation vs previous frame + per-step keyframe "
-                                                 "BoW + slot all-gather & cross-agent SearchForTriangulation and "
-                                                 "SearchByBoW(KF,KF)",
-                       "config": args.config, "frames_per_step_per_gpu": B, "graphs_per_gpu": P,
+            "config": {"workload": cfg["name"] + ", scale 1.2, 8 levels, FAST 20/7; " +
+                                   ("stereo pairs (right image at disparity %d px; mbf %.4f, mb %.5f): extract left + right "
+                                    "+ ComputeStereoMatches + BF SearchForTriangulation (stereo branch)" % (cfg["dx"], rig[0], rig[1])
+                                    if rig else "extract + BF SearchForTriangulation") +
+                                   " vs previous frame + per-step keyframe BoW + slot all-gather & cross-agent "
+                                   "SearchForTriangulation and SearchByBoW(KF,KF)",
+                       "config": args.config, "stereo": bool(rig), "frames_per_step_per_gpu": B,
+                       "images_per_step_per_gpu": per * B, "graphs_per_gpu": P,
                        "graph_stagger": args.stagger, "scene": args.scene,
                        "exchange_stream": "own" if async_x else "graph 0's",
                        "parallelism": "agent-per-gpu x%d" % world},
@@ -660,13 +752,13 @@ def main():
                                               "what": "whole-GPU rate of the match-only pass (wall clock)"}},
             "stage_rooflines": stage_roof,
             "step_valu_issue": step_valu_roof,
-            "pipeline_hbm": {"bytes_per_frame": b_frame, "achieved_GBs": round(b_frame * value / world / 1e9, 2),
-                             "frac": round(b_frame * value / world / 1e9 / HBM_PEAK_GBS, 5)},
+            "pipeline_hbm": {"bytes_per_image": b_frame, "achieved_GBs": round(b_frame * per * value / world / 1e9, 2),
+                             "frac": round(b_frame * per * value / world / 1e9 / HBM_PEAK_GBS, 5)},
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "per_gpu_frames_per_s": round(value / world, 2),
             "extract_only_frames_per_s_per_gpu": round(extract_fps, 1),
             "match_only_pairs_per_s_per_gpu": round(match_pps, 1),
-            "kp_per_frame": round(nkp, 1),
+            "kp_per_image": round(nkp, 1),
             "matches_per_pair": round(nmatch, 1),
             "sustained": sustained,
             "ingest": ingest,
@@ -691,18 +783,23 @@ def main():
         nf1 = args.cpu_frames_1t or (2000 if args.config == "c2" else 1000)
         # median of 5 short runs on every usable host core (the headline ratio), then the
         # reference's own architecture: one Tracking thread ((i), >= 2000 frames at C2) with the oracle's stage split
-        runs = [cpu_baseline(frames_np, threads, seconds=args.cpu_seconds / 5, nfeatures=cfg["nfeatures"])
+        if rig:
+            nf1 = args.cpu_frames_1t or 500
+        runs = [cpu_baseline(frames_np, threads, seconds=args.cpu_seconds / 5, nfeatures=cfg["nfeatures"], stereo=rig)
                 for _ in range(5)]
         fps = sorted(r[0] for r in runs)[2]
         nfr, sec = sum(r[1] for r in runs), sum(r[2] for r in runs)
-        fps1, nfr1, sec1, per1 = cpu_baseline(frames_np, 1, nframes=nf1, nfeatures=cfg["nfeatures"])
+        fps1, nfr1, sec1, per1 = cpu_baseline(frames_np, 1, nframes=nf1, nfeatures=cfg["nfeatures"], stereo=rig)
         result["cpu_baseline"] = {
-            "value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": "median of 5 runs, %d synthetic %dx%d frames in %.1f s in total (extract + BF triangulation vs "
+            "value": round(fps, 2), "unit": "stereo frames/s" if rig else "frames/s", "cores": threads, "kind": "port",
+            "sample": "median of 5 runs, %d synthetic %dx%d %s in %.1f s in total (%s vs "
                       "previous) on %d threads (every CPU of the affinity set, capped by the cgroup quota), "
                       "oracle/orb_oracle.c -O3 -march=x86-64-v3 -ffp-contract=off (a restatement; cv::FAST in OpenCV's SSE2 "
                       "vector form (detection + cornerScore), the other stages compiler-vectorised, no IPP); "
-                      "1-thread leg: %d frames in %.1f s" % (nfr, W, H, sec, threads, nfr1, sec1),
+                      "1-thread leg: %d frames in %.1f s" % (nfr, W, H, "stereo pairs" if rig else "frames", sec,
+                                                             "extract L + R + ComputeStereoMatches + stereo BF "
+                                                             "triangulation" if rig else "extract + BF triangulation",
+                                                             threads, nfr1, sec1),
             "host": info,
             "value_1thread": round(fps1, 2),
             "frames_1thread": nfr1,

@@ -27,6 +27,7 @@
 #include "orbslam_amd_testing.h"
 #include "launch.h"
 #include "orb_device.h"
+#include "kf_cache.h"
 #include "orb_match.h"
 
 using namespace orbamd;
@@ -519,7 +520,9 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
     const size_t B = (size_t)h->max_batch;
     const void* before[7] = {h->pyr.p, h->blur.p, h->cellkey.p, h->cellcnt.p, h->lvkey.p, h->lvcnt.p, h->gscratch.p};
     const void* err_before = h->err.p;
-    if (h->pyr.ensure(B * ep.pyr_frame_bytes) || h->blur.ensure(B * ep.blur_frame_bytes) ||
+    // the blurred pyramid is only for frames the fused describe cannot take (unaligned level-0 rows): allocated at the
+    // first such call (ensure_blur), and kept sized here once it exists
+    if (h->pyr.ensure(B * ep.pyr_frame_bytes) || (h->blur.p && h->blur.ensure(B * ep.blur_frame_bytes)) ||
         h->cellkey.ensure(B * ep.keys_per_frame * 4) || h->cellcnt.ensure(B * ep.ncells * 4) ||
         h->lvkey.ensure(B * ep.kp_per_frame * 4) || h->lvcnt.ensure((B * ep.L + kMaxLevels) * 4) ||
         h->gscratch.ensure(B * (size_t)ep.keys_per_frame * 8) || h->err.ensure(256))
@@ -531,6 +534,17 @@ static int ensure_geometry(orbx_handle* h, int W, int H, int nframes) {
         HIPR(octree_setup(h->geo.lds_bytes));
         h->lds_attr_set = true;
     }
+    return 0;
+}
+
+/* the separate blur's buffer (k_blur_strips / k_fast_blur + k_describe), allocated at the first extraction of frames whose
+ * level-0 rows are not 4-byte aligned: every aligned frame blurs inside describe's LDS, so most handles never hold the
+ * ~1 MB per 640x480 frame of max_batch (3 GB at the bench's 3 x 1024 frames). A host-call graph captured before holds no
+ * blur launch, so a reallocation only bumps the epoch like any other buffer change. */
+static int ensure_blur(orbx_handle* h) {
+    const void* before = h->blur.p;
+    if (h->blur.ensure((size_t)h->max_batch * h->geo.ep.blur_frame_bytes)) return ORBX_EDEVICE;
+    if (h->blur.p != before) h->epoch++;
     return 0;
 }
 
@@ -632,6 +646,7 @@ static int run_extract_levels(orbx_handle* h, const ExtractParams& ep, int nfram
                                       nframes, st));
         return 0;
     }
+    if (ensure_blur(h)) return ORBX_EDEVICE;
     ExtractParams eb = ep;  // the blur's short-chunk job table
     for (int i = 0; i <= kMaxLevels; i++) eb.bjob_begin[i] = g.bjob_small[i];
     if (!(h->skip_mask & 2) && !(h->skip_mask & 8)) {  // FAST and the blur in one launch
@@ -700,6 +715,7 @@ static int run_extract(orbx_handle* h, int nframes, const uint8_t* d_frames, lon
         return 0;
     }
     const bool fused = use_describe_blur(d_frames, fstride, pitch);
+    if (!fused && ensure_blur(h)) return ORBX_EDEVICE;
     if (!fused && !h->serial && ensure_stream(h, &h->side)) return ORBX_EDEVICE;
     const hipStream_t sd = h->serial ? st : h->side;
     if (prof_mark(h, 0, 0, st)) return ORBX_EDEVICE;
@@ -1086,7 +1102,8 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
         HIPR(hipGraphLaunch(h->gexec, h->stream));
     }
     if (const int rc = wait_until(h->stream, [&] { return __atomic_load_n(done, __ATOMIC_ACQUIRE) != done0; })) return rc;
-    h->host_pyr_valid = copies;
+    // the copy workgroups ride on the octree launch: a skipped octree (orbx_debug_skip_stages bit 2) delivers nothing
+    h->host_pyr_valid = copies && !(h->skip_mask & 4);
     h->last_frames = h->in_frame.as<uint8_t>();
     h->last_fstride = (long long)in_bytes;
     h->last_pitch = width;
@@ -1122,6 +1139,9 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int width, int height, size
         return ORBX_EDEVICE;
     const void* after[4] = {h->in_frame.p, h->out_kps.p, h->out_desc.p, h->out_cnt.p};
     if (memcmp(before, after, sizeof(before))) h->epoch++;
+    // an unaligned frame (width not a multiple of 4) blurs into HBM: allocate that buffer here, never inside a capture
+    if (!use_describe_blur(h->in_frame.as<uint8_t>(), (long long)width * height, width) && ensure_blur(h))
+        return ORBX_EDEVICE;
     // captured graph, except while stage profiling (its events are recorded per call)
     if (!h->prof_on) return extract_graph(h, img, width, height, pitch, kps, desc, cap, n);
     HIPR(hipMemcpy2DAsync(h->in_frame.p, width, img, pitch, width, height, hipMemcpyHostToDevice, h->stream));
@@ -1489,6 +1509,7 @@ struct KfEntry {
     size_t o_dnode = 0, o_rnode = 0;  // descriptors / NodeRecs in FeatureVector order (k_bow_small, k_tri_small)
     float min_x = 0, min_y = 0, gw_inv = 0, gh_inv = 0;  // grid bounds / scale the grid was built with
     const uint8_t* at(size_t o) const { return buf.as<uint8_t>() + o; }
+    size_t bytes() const { return buf.bytes; }  // what it holds against the cache's capacity (KfLru)
 };
 
 struct ViewPlan {
@@ -1969,6 +1990,28 @@ int orbm_triangulation_bf_batch_device(orbm_ctx* ctx, int npairs, const int32_t*
     hipStream_t st = (hipStream_t)stream;
     HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * npairs, st));
     HIPR(launch_tri_bf(npairs, d_q1, d_q2, d_kps, d_desc, d_counts, kp_stride, g, d_match12, d_nmatches, st));
+    if (check_ori)
+        HIPR(launch_rot_filter_pairs(npairs, d_q1, d_q2, d_kps, d_counts, kp_stride, d_match12, d_nmatches, st));
+    return 0;
+}
+
+int orbm_triangulation_bf_stereo_batch_device(orbm_ctx* ctx, int npairs, const int32_t* d_q1, const int32_t* d_q2,
+                                              const orbx_kp* d_kps, const uint8_t* d_desc, const int32_t* d_counts,
+                                              const float* d_uright, int kp_stride, const float F12[9], float ex,
+                                              float ey, int nlevels, const float* scale_factors,
+                                              const float* level_sigma2, int only_stereo, int check_ori,
+                                              int32_t* d_match12, int32_t* d_nmatches, void* stream) {
+    if (!ctx || npairs < 0 || !F12 || nlevels < 1 || nlevels > 16 || !scale_factors || !level_sigma2 ||
+        kp_stride < 1 || (npairs > 0 && !d_uright))
+        return ORBX_EARG;
+    if (npairs == 0) return 0;
+    HIPR(hipSetDevice(ctx->device));
+    MatchGeom g;
+    make_geom(g, F12, ex, ey, nlevels, scale_factors, level_sigma2);
+    hipStream_t st = (hipStream_t)stream;
+    HIPR(hipMemsetAsync(d_nmatches, 0, sizeof(int32_t) * npairs, st));
+    HIPR(launch_tri_bf(npairs, d_q1, d_q2, d_kps, d_desc, d_counts, kp_stride, g, d_match12, d_nmatches, st, d_uright,
+                       only_stereo ? 1 : 0));
     if (check_ori)
         HIPR(launch_rot_filter_pairs(npairs, d_q1, d_q2, d_kps, d_counts, kp_stride, d_match12, d_nmatches, st));
     return 0;
@@ -3087,25 +3130,18 @@ int orbv_transform(orbv_handle* h, const uint8_t* desc, int n, int levelsup, uin
 /* ===================================================================================== */
 struct orbm_kf_cache {
     int device = 0;
-    size_t capacity = 0;
-    std::mutex mu;
     hipStream_t stream = nullptr;
-    struct Slot {
-        std::shared_ptr<KfEntry> e;
-        std::list<std::pair<int, uint64_t>>::iterator lru;
-    };
-    // kind 0: matcher views (orbm_kf_view: + FeatureVector), kind 1: projection views (orbm_frame_view: + grid)
-    std::unordered_map<uint64_t, Slot> map[2];
-    std::list<std::pair<int, uint64_t>> lru;  // front = most recently used
-    size_t bytes = 0;
-    long long hits = 0, misses = 0;
+    // kind 0: matcher views (orbm_kf_view: + FeatureVector), kind 1: projection views (orbm_frame_view: + grid); the
+    // LRU books and their mutex are csrc/kf_cache.h's (also run under ThreadSanitizer by tests/test_sanitizers.py)
+    orbamd::KfLru<KfEntry> lru;
+    explicit orbm_kf_cache(size_t capacity) : lru(capacity) {}
 };
 
 namespace {
 
 /* the cached entry for (kind, key) matching this call's view, uploading (or replacing) it when absent or
  * stale (a different N, FeatureVector size, stereo presence or grid geometry); LRU eviction over the
- * capacity. The lookup and the insertion hold the cache's mutex; a miss builds and uploads its entry on the
+ * capacity (KfLru). The lookup and the insertion hold the cache's mutex; a miss builds and uploads its entry on the
  * calling context's stream with the mutex released, so calls of other threads are not held behind the upload
  * (two threads missing on the same key both upload; the second insertion keeps the first one's entry).
  * Returns nullptr on a device error. */
@@ -3120,22 +3156,7 @@ std::shared_ptr<KfEntry> cache_get(orbm_kf_cache* c, int kind, uint64_t key, con
                (kind == 0 || (e.min_x == fv->min_x && e.min_y == fv->min_y && e.gw_inv == fv->grid_w_inv &&
                               e.gh_inv == fv->grid_h_inv));
     };
-    auto& m = c->map[kind];
-    {
-        std::lock_guard<std::mutex> lock(c->mu);
-        auto it = m.find(key);
-        if (it != m.end()) {
-            if (matches(*it->second.e)) {
-                c->hits++;
-                c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
-                return it->second.e;
-            }
-            c->bytes -= it->second.e->buf.bytes;
-            c->lru.erase(it->second.lru);
-            m.erase(it);  // in-flight calls keep their shared_ptr; the buffer goes with the last one
-        }
-        c->misses++;
-    }
+    if (std::shared_ptr<KfEntry> hit = c->lru.find(kind, key, matches)) return hit;
     auto e = std::make_shared<KfEntry>();
     e->n = n;
     e->n_nodes = n_nodes;
@@ -3206,29 +3227,7 @@ std::shared_ptr<KfEntry> cache_get(orbm_kf_cache* c, int kind, uint64_t key, con
     if (hipMemcpyAsync(e->buf.p, h.data(), cv.off, hipMemcpyHostToDevice, st) != hipSuccess) return nullptr;
     if (kind == 1 && launch_projection((const ProjCall*)e->at(o_call), 1, 0, st, false) != hipSuccess) return nullptr;
     if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lock(c->mu);
-    auto it = m.find(key);
-    if (it != m.end()) {
-        if (matches(*it->second.e)) {  // another thread inserted the same keyframe meanwhile: share its entry
-            c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
-            return it->second.e;
-        }
-        c->bytes -= it->second.e->buf.bytes;
-        c->lru.erase(it->second.lru);
-        m.erase(it);
-    }
-    c->lru.push_front({kind, key});
-    m[key] = orbm_kf_cache::Slot{e, c->lru.begin()};
-    c->bytes += e->buf.bytes;
-    while (c->bytes > c->capacity && c->lru.size() > 1) {  // evict the least recently used, never this one
-        const auto victim = c->lru.back();
-        auto& vm = c->map[victim.first];
-        auto vit = vm.find(victim.second);
-        c->bytes -= vit->second.e->buf.bytes;
-        vm.erase(vit);
-        c->lru.pop_back();
-    }
-    return e;
+    return c->lru.insert(kind, key, e, matches);  // another thread's matching entry, if it inserted one meanwhile
 }
 
 }  // namespace
@@ -3240,9 +3239,8 @@ int orbm_kf_cache_create(int device, size_t capacity_bytes, orbm_kf_cache** out)
     *out = nullptr;
     if (device < 0 || device >= orbx_device_count()) return ORBX_EDEVICE;
     HIPR(hipSetDevice(device));
-    orbm_kf_cache* c = new orbm_kf_cache();
+    orbm_kf_cache* c = new orbm_kf_cache(capacity_bytes ? capacity_bytes : (size_t)1 << 30);
     c->device = device;
-    c->capacity = capacity_bytes ? capacity_bytes : (size_t)1 << 30;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return ORBX_EDEVICE;
@@ -3255,32 +3253,20 @@ void orbm_kf_cache_destroy(orbm_kf_cache* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    c->map[0].clear();
-    c->map[1].clear();
+    c->lru.clear();
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
 int orbm_kf_cache_erase(orbm_kf_cache* c, uint64_t key) {
     if (!c) return ORBX_EARG;
-    std::lock_guard<std::mutex> lock(c->mu);
-    for (auto& m : c->map) {
-        auto it = m.find(key);
-        if (it == m.end()) continue;
-        c->bytes -= it->second.e->buf.bytes;
-        c->lru.erase(it->second.lru);
-        m.erase(it);
-    }
+    c->lru.erase(key);
     return 0;
 }
 
 int orbm_kf_cache_stats(orbm_kf_cache* c, int* entries, size_t* bytes, long long* hits, long long* misses) {
     if (!c) return ORBX_EARG;
-    std::lock_guard<std::mutex> lock(c->mu);
-    if (entries) *entries = (int)(c->map[0].size() + c->map[1].size());
-    if (bytes) *bytes = c->bytes;
-    if (hits) *hits = c->hits;
-    if (misses) *misses = c->misses;
+    c->lru.stats(entries, bytes, hits, misses);
     return 0;
 }
 

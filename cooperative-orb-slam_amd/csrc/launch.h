@@ -53,9 +53,10 @@ hipError_t launch_describe_blur(const uint8_t* frames, long long fstride, int pi
                                 const int* lvcnt, orbx_kp* out_kps, uint8_t* out_desc, int* out_counts, int kp_stride,
                                 const int* ptab, int nframes, hipStream_t st);
 
+/* uright: mvuRight of every frame (uright[f * kp_stride + i], -1 = monocular; nullptr = all monocular) */
 hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
-                         int32_t* nmatches, hipStream_t st);
+                         int32_t* nmatches, hipStream_t st, const float* uright = nullptr, int only_stereo = 0);
 hipError_t launch_tri_nodes_pairs(int npairs, int max_nodes, const int32_t* q1, const int32_t* q2, const orbx_kp* kps,
                                   const uint8_t* desc, int kp_stride, const uint32_t* fv_node, const int32_t* fv_off,
                                   const int32_t* fv_feat, const int32_t* nfv, const MatchGeom& g, int32_t* match12,

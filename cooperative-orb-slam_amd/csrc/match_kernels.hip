@@ -65,10 +65,12 @@ __device__ __forceinline__ bool near_epipole(const MatchGeom& g, float x2, float
 }
 
 /* Pair p: KF1 = (kps1, desc1, n1), KF2 = (kps2, desc2, n2) resolved by the caller-side
- * accessor; every keypoint mono, no MapPoints (BF bench configuration). */
+ * accessor; no MapPoints (BF bench configuration). ur1 / ur2: mvuRight of each keyframe (the stereo
+ * form, k_tri_mfma<true>; unread by the mono form). */
 struct PairSrc {
     const orbx_kp* kps1; const uint8_t* desc1; int n1;
     const orbx_kp* kps2; const uint8_t* desc2; int n2;
+    const float* ur1; const float* ur2;
 };
 
 /* ----------------------------------------------------------------------------------- */
@@ -119,8 +121,13 @@ constexpr int kMfThreads = 64 * kMfWaves;
 /* is the f32 accumulator's bit pattern (dot' is an even integer <= 256: its low 14 mantissa bits  */
 /* are zero) OR the tile row, whose signed maximum is the first candidate of maximum dot' =        */
 /* minimum D with ties to the later row.                                                          */
+/* STEREO: keyframes with mvuRight (ORBmatcher.cc:703-749): the epipole-radius test applies only when both the
+ * query and the candidate are monocular (!bStereo1 && !bStereo2), and with only_stereo a monocular query or
+ * candidate takes no part. The candidate record's w is 1 for a monocular candidate near the epipole (rejected for
+ * a monocular query only); the mono form folds that test into the threshold (-1) as before. */
+template <bool STEREO>
 __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchGeom& g, int32_t* __restrict__ out,
-                                                  int32_t* __restrict__ nmatch) {
+                                                  int32_t* __restrict__ nmatch, int only_stereo) {
     static_assert(kMfWaves == 4 || kMfWaves == 8, "fp4 expansion roles: 4 waves (2 dwords per thread) or 8 (1)");
     constexpr int kDw = 512 / kMfThreads;  // descriptor dwords expanded per thread and chunk
     __shared__ v4i s_frag[kMfBufs][2][4][64];  // [buffer][tile][step][lane] candidate fragments (fp4 +-1)
@@ -133,6 +140,9 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
     const int h = lane >> 5;
     const int qi = qblk + wave * 32 + (lane & 31);
     const bool qon = qi < s.n1;
+    // bStereo1 (ORBmatcher.cc:703); with bOnlyStereo a monocular query is skipped (:705-707): output -1
+    const bool st1 = STEREO && qon && s.ur1[qi] >= 0.f;
+    const bool qact = qon && (!STEREO || !only_stereo || st1);
     // query fragments: step st covers descriptor bits 64 st .. 64 st + 63, lane half h dword 2 st + h
     v4i bq[4];
     float la = 0.f, lb = 0.f, lc = 0.f;
@@ -154,14 +164,17 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
     const int ec = (tid >> 6) * (64 / kMfWaves) + (tid & 7) + (kDw == 1 ? 0 : 8 * ((tid >> 5) & 1));
     const int ed = kDw == 1 ? (tid >> 3) & 7 : 2 * ((tid >> 3) & 3);
     struct DwT { uint32_t w[kDw]; };
-    auto load_chunk = [&](int cb, DwT& d, orbx_kp& k2) {
+    auto load_chunk = [&](int cb, DwT& d, orbx_kp& k2, float& u2) {
         const int c = min(cb + ec, s.n2 - 1);
         d = *(const DwT*)(s.desc2 + (long long)c * 32 + 4 * ed);
-        k2 = s.kps2[min(cb + (tid & (kMfChunk - 1)), s.n2 - 1)];
+        const int c2 = min(cb + (tid & (kMfChunk - 1)), s.n2 - 1);
+        k2 = s.kps2[c2];
+        if (STEREO) u2 = s.ur2[c2];
     };
     DwT pd;
     orbx_kp pk;
-    load_chunk(0, pd, pk);
+    float pu = -1.f;
+    load_chunk(0, pd, pk, pu);
     // chunk staging into LDS buffer bw (candidates cbw ..): expansion of the prefetched descriptor dwords and the
     // per-candidate geometry record
     auto stage = [&](int cbw, int bw) {
@@ -171,19 +184,26 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
         for (int k = 0; k < kDw; k++)
             s_frag[bw][tile][(ed + k) >> 1][32 * ((ed + k) & 1) + r] = fp4_pm1_dword(on ? pd.w[k] : 0u);
         if (tid < kMfChunk) {
-            const bool on2 = cbw + tid < s.n2 && !near_epipole(g, pk.x, pk.y, pk.octave);
-            s_rec[bw][tid] = make_float4(pk.x, pk.y, on2 ? g.th384f[pk.octave] : -1.0f, 0.0f);
+            if (STEREO) {
+                const bool st2 = pu >= 0.f;  // bStereo2 (:727); only_stereo skips a monocular candidate (:729-731)
+                const bool on2 = cbw + tid < s.n2 && (!only_stereo || st2);
+                const bool near = !st2 && near_epipole(g, pk.x, pk.y, pk.octave);
+                s_rec[bw][tid] = make_float4(pk.x, pk.y, on2 ? g.th384f[pk.octave] : -1.0f, near ? 1.0f : 0.0f);
+            } else {
+                const bool on2 = cbw + tid < s.n2 && !near_epipole(g, pk.x, pk.y, pk.octave);
+                s_rec[bw][tid] = make_float4(pk.x, pk.y, on2 ? g.th384f[pk.octave] : -1.0f, 0.0f);
+            }
         }
     };
     // double-buffered: chunk c+1 is expanded into the other buffer before chunk c's MFMAs, so one barrier per chunk
     // (the one that publishes c+1 and retires c's reads) instead of two
     stage(0, 0);
     __syncthreads();
-    if (kMfChunk < s.n2) load_chunk(kMfChunk, pd, pk);
+    if (kMfChunk < s.n2) load_chunk(kMfChunk, pd, pk, pu);
     for (int cb = 0, bf = 0; cb < s.n2; cb += kMfChunk, bf ^= 1) {
         if (cb + kMfChunk < s.n2) {
             stage(cb + kMfChunk, bf ^ 1);
-            if (cb + 2 * kMfChunk < s.n2) load_chunk(cb + 2 * kMfChunk, pd, pk);
+            if (cb + 2 * kMfChunk < s.n2) load_chunk(cb + 2 * kMfChunk, pd, pk, pu);
         }
         v16f acc0 = (v16f)0.f, acc1 = (v16f)0.f;
 #pragma unroll
@@ -211,7 +231,7 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
             while (km < best && (km >> 16) <= 50u) {  // TH_LOW (ORBmatcher.cc:715)
                 const int jl = (int)(65535u - (km & 0xFFFFu)) - cb;
                 const float4 c2 = s_rec[bf][jl];
-                if (epi_ok_f(la, lb, lc, c2.x, c2.y, c2.z)) {
+                if ((!STEREO || st1 || c2.w == 0.0f) && epi_ok_f(la, lb, lc, c2.x, c2.y, c2.z)) {
                     best = km;
                     break;
                 }
@@ -229,7 +249,7 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
     }
     best = min(best, (uint32_t)__shfl_xor((int)best, 32, 64));
     if (qon && h == 0) {
-        const int idx2 = (best >> 16) <= 50u ? (int)(65535u - (best & 0xFFFFu)) : -1;
+        const int idx2 = qact && (best >> 16) <= 50u ? (int)(65535u - (best & 0xFFFFu)) : -1;
         out[qi] = idx2;
         if (idx2 >= 0) atomicAdd(nmatch, 1);
     }
@@ -242,16 +262,20 @@ __device__ __forceinline__ void tri_mfma_body_fp4(const PairSrc& s, const MatchG
 #define ORBX_MF_WPE 6
 #endif
 #define ORBX_MF_ATTR __attribute__((amdgpu_waves_per_eu(ORBX_MF_WPE)))
+template <bool STEREO>
 __global__ __launch_bounds__(kMfThreads) ORBX_MF_ATTR void k_tri_mfma(const int32_t* __restrict__ q1, const int32_t* __restrict__ q2,
                                                   const orbx_kp* __restrict__ kps, const uint8_t* __restrict__ desc,
-                                                  const int32_t* __restrict__ counts, int kp_stride, MatchGeom g,
+                                                  const int32_t* __restrict__ counts, const float* __restrict__ uright,
+                                                  int kp_stride, MatchGeom g, int only_stereo,
                                                   int32_t* __restrict__ match12, int32_t* __restrict__ nmatches) {
     const int p = blockIdx.y;
     const int f1 = q1[p], f2 = q2[p];
     PairSrc s;
     s.kps1 = kps + (long long)f1 * kp_stride; s.desc1 = desc + (long long)f1 * kp_stride * 32; s.n1 = counts[f1];
     s.kps2 = kps + (long long)f2 * kp_stride; s.desc2 = desc + (long long)f2 * kp_stride * 32; s.n2 = counts[f2];
-    tri_mfma_body_fp4(s, g, match12 + (long long)p * kp_stride, nmatches + p);
+    s.ur1 = STEREO ? uright + (long long)f1 * kp_stride : nullptr;
+    s.ur2 = STEREO ? uright + (long long)f2 * kp_stride : nullptr;
+    tri_mfma_body_fp4<STEREO>(s, g, match12 + (long long)p * kp_stride, nmatches + p, only_stereo);
 }
 
 /* rotation bin of a match (ORBmatcher.cc:236-246): rot = angA[a] - angB[b], (a,b) = (i, j) or,
@@ -1006,11 +1030,15 @@ namespace orbamd {
 
 hipError_t launch_tri_bf(int npairs, const int32_t* q1, const int32_t* q2, const orbx_kp* kps, const uint8_t* desc,
                          const int32_t* counts, int kp_stride, const MatchGeom& g, int32_t* match12,
-                         int32_t* nmatches, hipStream_t st) {
+                         int32_t* nmatches, hipStream_t st, const float* uright, int only_stereo) {
     if (npairs == 0) return hipSuccess;
     dim3 grid((kp_stride + 32 * kMfWaves - 1) / (32 * kMfWaves), npairs);
-    hipLaunchKernelGGL(k_tri_mfma, grid, dim3(kMfThreads), 0, st, q1, q2, kps, desc, counts, kp_stride, g, match12,
-                       nmatches);
+    if (uright)
+        hipLaunchKernelGGL(k_tri_mfma<true>, grid, dim3(kMfThreads), 0, st, q1, q2, kps, desc, counts, uright, kp_stride,
+                           g, only_stereo, match12, nmatches);
+    else
+        hipLaunchKernelGGL(k_tri_mfma<false>, grid, dim3(kMfThreads), 0, st, q1, q2, kps, desc, counts, uright,
+                           kp_stride, g, 0, match12, nmatches);
     return hipGetLastError();
 }
 

@@ -14,7 +14,12 @@ extern "C" {
 /* Test hook: the stages in `mask` (bit k of {pyramid, fast_cells, octree, blur, describe}) are not
  * launched by subsequent batched extractions of this handle (0 = every stage runs, the default). A
  * skipped stage leaves its buffers as the previous call left them; the tests use it to prove that
- * the bench's self-check detects a stage that stopped launching. */
+ * the bench's self-check detects a stage that stopped launching. Bit 3 (blur) only acts on frames that
+ * take the separate blur (level-0 rows not 4-byte aligned); frames with aligned rows blur inside
+ * describe (k_describe_blur), so for them skipping the blur means skipping describe (bit 4), and a
+ * test that skips bit 3 alone on such frames must expect every output to stay correct. Skipping the
+ * octree (bit 2) also skips the host path's pyramid copy that rides on its launch, so
+ * orbx_host_pyramid_level reports no pyramid for that call. */
 int orbx_debug_skip_stages(orbx_handle* h, int mask);
 
 /* Measurement hook: on != 0 runs every stage of this handle's subsequent extractions in order on the

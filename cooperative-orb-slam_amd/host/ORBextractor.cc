@@ -144,6 +144,9 @@ const std::vector<cv::Mat>& ORBextractor::SyncImagePyramid() {
         int w = 0, h = 0;
         int rc = mpHandle ? orbx_pyramid_level(mpHandle, 0, l, nullptr, 0, &w, &h) : ORBX_EDEVICE;
         if (rc == ORBX_OK) {
+            // an earlier eager call left a header over the handle's pinned memory here: drop it, so create() allocates
+            // storage this member owns instead of writing into (possibly freed) handle memory
+            mvImagePyramid[l].release();
             mvImagePyramid[l].create(h, w, CV_8U);
             rc = orbx_pyramid_level(mpHandle, 0, l, mvImagePyramid[l].data, mvImagePyramid[l].step, &w, &h);
         }

@@ -121,6 +121,8 @@ SIGNATURES = {
     "orbm_search_by_bow_kf_kf": (_I, [_P, C.POINTER(OrbmKfView), C.POINTER(OrbmKfView), _F, _I, _P, C.POINTER(_I)]),
     "orbm_triangulation_bf_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _F, _F, _I, _P, _P, _I, _P, _P,
                                                 _P]),
+    "orbm_triangulation_bf_stereo_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _F, _F, _I, _P, _P, _I,
+                                                       _I, _P, _P, _P]),
     "orbm_search_for_triangulation_slots_device": (_I, [_P, C.POINTER(OrbxKfSource), _I, _I, _P, _SZ,
                                                         C.POINTER(OrbmSlotGeom), _I, _I, _P, _P, _P]),
     "orbm_search_by_bow_slots_device": (_I, [_P, C.POINTER(OrbxKfSource), _I, _I, _P, _SZ, _F, _I, _I, _P, _P, _P]),

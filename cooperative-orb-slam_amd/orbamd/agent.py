@@ -12,6 +12,11 @@ orbx handle, matcher ctx and HIP stream each):
     N > 1, a local copy at N = 1), and matched against every agent's slot straight from the receive
     buffer: SearchForTriangulation (orbm_search_for_triangulation_slots_device, LocalMapping) and the
     loop-candidate SearchByBoW(KF,KF) (orbm_search_by_bow_slots_device, LoopClosing).
+Stereo (stereo=(mbf, mb), BASELINE configs 3 and 4): every frame is a rectified stereo pair, as the stereo Frame
+constructor builds it (ORB_SLAM2.1/src/Frame.cc:80-98): both images extracted (one batch per graph: its left
+images, then its right ones), Frame::ComputeStereoMatches on the device-resident pyramids (mvuRight / mvDepth), and
+SearchForTriangulation's stereo branch against the previous frame (ORBmatcher.cc:703-749); the keyframe slot carries
+mvuRight / mvDepth, so the cross-agent triangulation takes the stereo branch too.
 Graphs are staggered: in a staggered step graph p starts extracting once graph p-1 has finished extracting
 it, so one graph's FAST overlaps another's latency-bound tail (octree, describe, matcher); the offset is
 imposed in the first step of a pass and every 8th step after it (DEFAULT_STAGGER) and persists in between.
@@ -47,11 +52,15 @@ def kf_mp_flags(n):
 class AgentSchedule:
     def __init__(self, torch, frames_np, width, height, pipes, device=0, rank=0, world=1, allgather=None,
                  stagger=DEFAULT_STAGGER, exchange=True, priorities=None, nfeatures=1000, pool=1,
-                 async_exchange=False):
+                 async_exchange=False, stereo=None):
         """frames_np: uint8 [pool*B, H, W] host frames of this agent (copied to HBM once), batch r = frames
-        [r*B, (r+1)*B); allgather(out, inp): all-gather of equal-sized device byte tensors across agents
-        (None: no collective, only possible at world 1, where the slot is packed in place)."""
+        [r*B, (r+1)*B); with stereo=(mbf, mb) uint8 [pool*B, 2, H, W] (left, right image of each frame);
+        allgather(out, inp): all-gather of equal-sized device byte tensors across agents (None: no collective,
+        only possible at world 1, where the slot is packed in place)."""
         assert len(frames_np) % pool == 0
+        assert (frames_np.ndim == 4 and frames_np.shape[1] == 2) == bool(stereo), "stereo frames are [N, 2, H, W]"
+        self.stereo = stereo
+        self.images_per_frame = 2 if stereo else 1
         B = len(frames_np) // pool
         assert B % pipes == 0, "frames per step must be a multiple of the graph count"
         assert allgather is not None or world == 1
@@ -77,18 +86,18 @@ class AgentSchedule:
         # (C4's 1241), so every row starts 4-aligned and the whole-frame pyramid kernel applies
         pitch = width if width % 4 == 0 else (width + 63) // 64 * 64
         self.pitch = pitch
-        self.frames = []  # [batch r][graph p] -> device view [sub, H, W]
+        self.frames = []  # [batch r][graph p] -> device view [sub * images_per_frame, H, W]
+        per = self.images_per_frame
         for r in range(pool):
             row = []
             for p in range(pipes):
-                buf = torch.zeros((sub, height, pitch), dtype=torch.uint8, device=dev)
+                buf = torch.zeros((per * sub, height, pitch), dtype=torch.uint8, device=dev)
                 view = buf[:, :, :width]
-                lo = r * B + p * sub
-                view.copy_(torch.from_numpy(frames_np[lo:lo + sub]).to(dev))
+                view.copy_(torch.from_numpy(self.graph_images(frames_np, r, p)).to(dev))
                 row.append(view)
             self.frames.append(row)
         self.nfeatures = nfeatures
-        self.pipes = [BatchPipeline(torch, width, height, sub, nfeatures=nfeatures, device=device)
+        self.pipes = [BatchPipeline(torch, width, height, sub, nfeatures=nfeatures, device=device, stereo=stereo)
                       for _ in range(pipes)]
         prio = priorities or [0] * pipes
         self.streams = [torch.cuda.Stream(dev, priority=prio[p]) for p in range(pipes)]
@@ -133,6 +142,12 @@ class AgentSchedule:
             kps, desc, count = self.q_kps, self.q_desc, self.q_count
             self.kf_released = torch.cuda.Event()
             self.kf_pending = False
+        self.kf_stereo = (None, None)
+        if stereo:
+            self.kf_stereo = (p0.uright[0], p0.depth[0])
+            if self.xstream is not None:
+                self.q_uright, self.q_depth = torch.empty_like(p0.uright[0]), torch.empty_like(p0.depth[0])
+                self.kf_stereo = (self.q_uright, self.q_depth)
         self.kf_arrays = (kps, desc, count)
         # the keyframe as a KeyFrame of the map: Frame::ComputeBoW on the device against the vocabulary (a
         # deterministic synthetic one of ORBvoc.txt's shape, k = 10, L = 6: ORBvoc.txt is absent; levelsup 4,
@@ -150,11 +165,33 @@ class AgentSchedule:
             self.kf_fv_node, self.kf_fv_off, self.kf_fv_feat, self.kf_nfv = z(S), z(S + 1), z(S), z(1)
             self.kf_mpf = torch.from_numpy(kf_mp_flags(S)).to(dev)
             self.bow_max_nodes = int(min(S, k ** max(L - KF_LEVELSUP, 0)))
-            self.kf_src = kf_source(kps, desc, count, mp_flags=self.kf_mpf, bow_word=self.kf_bow_word,
+            self.kf_src = kf_source(kps, desc, count, uright=self.kf_stereo[0], depth=self.kf_stereo[1],
+                                    mp_flags=self.kf_mpf, bow_word=self.kf_bow_word,
                                     bow_value=self.kf_bow_val, nbow=self.kf_nbow, fv_node=self.kf_fv_node,
                                     fv_off=self.kf_fv_off, fv_feat=self.kf_fv_feat, nfv=self.kf_nfv)
 
     # ------------------------------------------------------------------------------------------
+    def graph_images(self, frames_np, r, p):
+        """host images of graph p in pool batch r, in the device batch's order (stereo: the graph's left images,
+        then its right ones)"""
+        lo = r * self.B + p * self.sub
+        f = frames_np[lo:lo + self.sub]
+        if not self.stereo:
+            return f
+        import numpy as np
+        return np.ascontiguousarray(np.concatenate([f[:, 0], f[:, 1]]))
+
+    def host_batch(self, frames_np, r):
+        """every graph's images of pool batch r back to back (graph order; the ingest leg's pinned source)"""
+        import numpy as np
+        if not self.stereo:
+            return frames_np[r * self.B:(r + 1) * self.B]
+        return np.ascontiguousarray(np.concatenate([self.graph_images(frames_np, r, p) for p in range(self.P)]))
+
+    def device_images(self, r, p):
+        """the device images graph p extracts in pool batch r ([sub * images_per_frame, H, W] view)"""
+        return self.frames[r][p]
+
     def exchange_stream(self):
         """the stream the exchange runs on"""
         return self.xstream if self.xstream is not None else self.streams[0]
@@ -176,6 +213,9 @@ class AgentSchedule:
                 kps.copy_(p0.kps[0])
                 desc.copy_(p0.desc[0])
                 count.copy_(p0.counts[0:1])
+                if self.stereo:
+                    self.q_uright.copy_(p0.uright[0])
+                    self.q_depth.copy_(p0.depth[0])
                 self.kf_released.record(st)  # graph 0 may overwrite its buffers from here on
                 self.kf_pending = True
             S = p0.stride
@@ -196,10 +236,11 @@ class AgentSchedule:
             bow_slots_device(p0.mh, self.kf_src, S, self.world, self.all_slots, self.slot_bytes, self.xbow, self.xbn,
                              LOOP_NNRATIO, True, self.bow_max_nodes, st.cuda_stream)
 
-    def step(self, ev=None, xev=None, extract=True, match=True, xchg=True, first=True, batch=None, wait=None):
+    def step(self, ev=None, xev=None, extract=True, match=True, xchg=True, first=True, batch=None, wait=None, sev=None):
         """enqueue one step over the next pool batch (or `batch`); ev[p] = (start, end) events around graph
-        p's matcher, xev around the exchange; wait: an event every graph waits for before extracting, or one
-        event per graph (the ingest leg's upload of that graph's frames)"""
+        p's matcher, xev around the exchange, sev[p] around graph p's ComputeStereoMatches (stereo); wait: an event
+        every graph waits for before extracting, or per graph an event or a list of events (the ingest leg's
+        uploads of that graph's frames)"""
         torch = self.torch
         r = self.cursor % self.pool if batch is None else batch
         self.cursor += 1
@@ -213,12 +254,20 @@ class AgentSchedule:
             st = self.streams[p].cuda_stream
             if extract:
                 if wait is not None:
-                    self.streams[p].wait_event(wait[p] if isinstance(wait, (list, tuple)) else wait)
+                    w = wait[p] if isinstance(wait, (list, tuple)) else wait
+                    for e in (w if isinstance(w, (list, tuple)) else (w,)):
+                        self.streams[p].wait_event(e)
                 if p > 0 and stagger_now:
                     self.streams[p].wait_event(self.pyr_done[p - 1] if self.stagger_pyr else self.done[p - 1])
                 if p == 0 and self.xstream is not None and self.kf_pending:
                     self.streams[0].wait_event(self.kf_released)  # the previous exchange has copied the keyframe
-                self.pipes[p].extract(self.frames[r][p], st)
+                self.pipes[p].extract(self.frames[r][p], st, stereo=False)
+                if self.stereo:  # Frame::ComputeStereoMatches of the graph's pairs (Frame.cc:92)
+                    if sev is not None:
+                        sev[p][0].record(self.streams[p])
+                    self.pipes[p].stereo_matches(st)
+                    if sev is not None:
+                        sev[p][1].record(self.streams[p])
                 self.done[p].record(self.streams[p])
             if match:
                 if ev is not None:
@@ -256,8 +305,14 @@ class AgentSchedule:
         return (self.last_batch or 0) * self.B + p * self.sub + b
 
     def frame_results(self, p, b):
-        """(keypoints, descriptors, match12 vs frame b-1 of the same graph) of frame b of graph p"""
+        """(keypoints, descriptors, match12 vs frame b-1 of the same graph) of frame b of graph p (stereo: its left
+        image)"""
         return self.pipes[p].host_results(b)
+
+    def stereo_results(self, p, b):
+        """stereo: ((right keypoints, right descriptors), (mvuRight, mvDepth, kept)) of frame b of graph p"""
+        pp = self.pipes[p]
+        return pp.host_keypoints(self.sub + b), pp.host_stereo(b)
 
     def exchange_results(self):
         """(triangulation rows [world, n], counts [world], SearchByBoW rows [world, n], counts [world]) of this agent's

@@ -16,6 +16,12 @@ from .extractor import ORBextractor
 # camera of the reference config (ORB_SLAM2/my.yaml:8-11)
 FX, FY, CX, CY = 715.092024, 719.025258, 334.298489, 256.326097
 
+# stereo rigs of the BASELINE stereo configs: Camera.bf and the baseline mb = mbf / fx (Frame.cc:501-503, Tracking.cc
+# reads Camera.bf). EuRoC (EuRoC.yaml: fx 435.2047, bf 47.90639384423901) and KITTI 00-02 (KITTI00-02.yaml: fx 718.856,
+# bf 386.1448)
+STEREO_RIGS = {"euroc": (47.90639384423901, 47.90639384423901 / 435.2046959714599),
+               "kitti": (386.1448, 386.1448 / 718.856)}
+
 
 def default_geometry():
     """KF2 pose relative to KF1: R = I, t = (0.05, 0, 0.01); returns (F12, ex, ey)."""
@@ -32,25 +38,40 @@ def default_geometry():
 
 
 class BatchPipeline:
-    """Extract + match over batches of frames on one GPU."""
+    """Extract + match over batches of frames on one GPU.
+
+    stereo=(mbf, mb): every frame is a rectified stereo pair (the stereo Frame constructor, ORB_SLAM2.1/src/Frame.cc:
+    80-98): the extraction batch holds the B left images (images 0..B-1) and then the B right images (B..2B-1),
+    one orbx_extract_batch_device over all 2B (the two ORBextractor instances share the parameters,
+    Tracking.cc:119-125); Frame::ComputeStereoMatches gives every left keypoint its mvuRight / mvDepth
+    (orbx_stereo_matches_batch_device), and SearchForTriangulation of frame b against b-1 takes the stereo branch
+    (orbm_triangulation_bf_stereo_batch_device)."""
 
     def __init__(self, torch, width=640, height=480, batch=64, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mini=7,
-                 device=0, check_ori=False):
+                 device=0, check_ori=False, stereo=None):
         self.torch = torch
         self.W, self.H, self.B = width, height, batch
+        self.stereo = stereo
+        self.nimg = 2 * batch if stereo else batch
+        nimg = self.nimg
         self.ext = ORBextractor(nfeatures, scale, nlevels, ini, mini, device=device, max_width=width,
-                                max_height=height, max_batch=batch)
+                                max_height=height, max_batch=nimg)
         self.lib = load()
         self.stride = self.ext.max_keypoints(width, height)
         dev = torch.device("cuda", device)
         self.dev = dev
-        self.kps = torch.empty((batch, self.stride, 6), dtype=torch.float32, device=dev)
-        self.desc = torch.empty((batch, self.stride, 32), dtype=torch.uint8, device=dev)
-        self.counts = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self.kps = torch.empty((nimg, self.stride, 6), dtype=torch.float32, device=dev)
+        self.desc = torch.empty((nimg, self.stride, 32), dtype=torch.uint8, device=dev)
+        self.counts = torch.zeros(nimg, dtype=torch.int32, device=dev)
         self.match = torch.empty((batch, self.stride), dtype=torch.int32, device=dev)
         self.nmatch = torch.zeros(batch, dtype=torch.int32, device=dev)
         self.q1 = torch.arange(batch, dtype=torch.int32, device=dev)
         self.q2 = ((self.q1 + batch - 1) % batch).to(torch.int32)
+        if stereo:
+            self.uright = torch.empty((batch, self.stride), dtype=torch.float32, device=dev)
+            self.depth = torch.empty((batch, self.stride), dtype=torch.float32, device=dev)
+            self.nstereo = torch.zeros(batch, dtype=torch.int32, device=dev)
+            self.fr = (self.q1 + batch).to(torch.int32)
         h = C.c_void_p()
         check(self.lib.orbm_create(device, C.byref(h)), "orbm_create")
         self.mh = h
@@ -62,9 +83,23 @@ class BatchPipeline:
     def stream_ptr(self):
         return self.torch.cuda.current_stream(self.dev).cuda_stream
 
-    def extract(self, frames, stream=None):
+    def extract(self, frames, stream=None, stereo=True):
+        """frames: [nimg, H, W] device images (stereo: the B left images, then the B right ones); a stereo pipeline
+        then runs ComputeStereoMatches for every pair on the same stream (stereo=False: the caller does)"""
         st = self.stream_ptr() if stream is None else stream
         self.ext.extract_batch_device(frames, self.kps, self.desc, self.counts, st)
+        if self.stereo and stereo:
+            self.stereo_matches(st)
+
+    def stereo_matches(self, stream=None):
+        """Frame::ComputeStereoMatches of every pair (left image b, right image B + b) on the device"""
+        st = self.stream_ptr() if stream is None else stream
+        mbf, mb = self.stereo
+        check(self.lib.orbx_stereo_matches_batch_device(
+            self.ext._h, self.ext._h, self.B, self.q1.data_ptr(), self.fr.data_ptr(), self.kps.data_ptr(),
+            self.desc.data_ptr(), self.counts.data_ptr(), self.kps.data_ptr(), self.desc.data_ptr(),
+            self.counts.data_ptr(), self.stride, float(mbf), float(mb), self.uright.data_ptr(), self.depth.data_ptr(),
+            self.nstereo.data_ptr(), st), "orbx_stereo_matches_batch_device")
 
     def check_error(self, stream=None):
         st = self.stream_ptr() if stream is None else stream
@@ -73,6 +108,13 @@ class BatchPipeline:
     def match_pairs(self, stream=None):
         st = self.stream_ptr() if stream is None else stream
         F = np.ascontiguousarray(self.F12.reshape(9))
+        if self.stereo:
+            check(self.lib.orbm_triangulation_bf_stereo_batch_device(
+                self.mh, self.B, self.q1.data_ptr(), self.q2.data_ptr(), self.kps.data_ptr(), self.desc.data_ptr(),
+                self.counts.data_ptr(), self.uright.data_ptr(), self.stride, F.ctypes.data, self.ex, self.ey,
+                len(self.scale), self.scale.ctypes.data, self.sigma2.ctypes.data, 0, self.check_ori,
+                self.match.data_ptr(), self.nmatch.data_ptr(), st), "orbm_triangulation_bf_stereo_batch_device")
+            return
         check(self.lib.orbm_triangulation_bf_batch_device(
             self.mh, self.B, self.q1.data_ptr(), self.q2.data_ptr(), self.kps.data_ptr(), self.desc.data_ptr(),
             self.counts.data_ptr(), self.stride, F.ctypes.data, self.ex, self.ey, len(self.scale),
@@ -141,6 +183,8 @@ class BatchPipeline:
         with_bow; optional per-keypoint uright/depth/MapPoint device tensors)."""
         from .exchange import kf_source
         f, S = frame_idx, self.stride
+        if self.stereo and uright is None:  # a stereo keyframe carries its mvuRight / mvDepth
+            uright, depth = self.uright[f], self.depth[f]
         kw = {}
         if with_bow:
             kw = dict(bow_word=self.bow_word[f], bow_value=self.bow_val[f], nbow=self.nbow[f:f + 1],
@@ -175,13 +219,24 @@ class BatchPipeline:
         check(self.lib.orbm_check_error(self.mh, st), "orbm_check_error")
 
     def host_results(self, b):
-        """(keypoints structured array, descriptors uint8 [n,32], match12 int32 [n]) of frame b."""
-        from .extractor import kp_dtype
-        n = int(self.counts[b].item())
-        k = self.kps[b, :n].cpu().numpy().copy().view(np.uint8).view(kp_dtype).reshape(n)
-        d = self.desc[b, :n].cpu().numpy()
-        m = self.match[b, :n].cpu().numpy()
+        """(keypoints structured array, descriptors uint8 [n,32], match12 int32 [n]) of frame b (stereo: its left
+        image)."""
+        k, d = self.host_keypoints(b)
+        m = self.match[b, :len(k)].cpu().numpy()
         return k, d, m
+
+    def host_keypoints(self, i):
+        """(keypoints, descriptors) of extraction image i (stereo: i >= B is the right image of frame i - B)"""
+        from .extractor import kp_dtype
+        n = int(self.counts[i].item())
+        k = self.kps[i, :n].cpu().numpy().copy().view(np.uint8).view(kp_dtype).reshape(n)
+        d = self.desc[i, :n].cpu().numpy()
+        return k, d
+
+    def host_stereo(self, b):
+        """(mvuRight float32 [n], mvDepth float32 [n], stereo matches kept) of stereo frame b"""
+        n = int(self.counts[b].item())
+        return (self.uright[b, :n].cpu().numpy(), self.depth[b, :n].cpu().numpy(), int(self.nstereo[b].item()))
 
     def close(self):
         if getattr(self, "mh", None):

@@ -189,6 +189,19 @@ int orbm_triangulation_bf_batch_device(orbm_ctx* ctx, int npairs, const int32_t*
                                        int nlevels, const float* scale_factors,
                                        const float* level_sigma2, int check_ori,
                                        int32_t* d_match12, int32_t* d_nmatches, void* stream);
+/* The stereo form of the same batch (ORBmatcher.cc:657-823 with mvuRight, as LocalMapping::CreateNewMapPoints
+ * calls it between stereo keyframes): d_uright[f*kp_stride + i] = mvuRight of keypoint i of frame f (-1 =
+ * monocular), e.g. the output of orbx_stereo_matches_batch_device for the left frames. The epipole-radius test
+ * applies to monocular-monocular pairs only (:743-749); only_stereo = bOnlyStereo (:705-707, :729-731). No
+ * MapPoints, one F12/(ex,ey) and scale table for all pairs, match12 / nmatches as above. */
+int orbm_triangulation_bf_stereo_batch_device(orbm_ctx* ctx, int npairs, const int32_t* d_q1,
+                                              const int32_t* d_q2, const orbx_kp* d_kps,
+                                              const uint8_t* d_desc, const int32_t* d_counts,
+                                              const float* d_uright, int kp_stride, const float F12[9],
+                                              float ex, float ey, int nlevels,
+                                              const float* scale_factors, const float* level_sigma2,
+                                              int only_stereo, int check_ori, int32_t* d_match12,
+                                              int32_t* d_nmatches, void* stream);
 /* The same batch over common BoW nodes (SearchForTriangulation's own merge walk,
  * ORBmatcher.cc:691-789, as LocalMapping::CreateNewMapPoints calls it with a real vocabulary):
  * the FeatureVectors are orbv_transform_batch_device's device output for the same frames

@@ -8,6 +8,9 @@ SearchForTriangulation and SearchByBoW(KF,KF) of this agent's keyframe against e
 (their FeatureVectors from the oracle vocabulary transform, their MapPoint records from
 orbamd.agent.kf_mp_flags), and compares
 every keypoint field (raw float bits), descriptor byte and match index with the device results.
+A stereo schedule (sched.stereo = (mbf, mb)) also recomputes each sampled frame's right image and
+Frame::ComputeStereoMatches (oracle/orb_oracle_frame.c) and compares the right keypoints, mvuRight /
+mvDepth (raw float bits) and the kept count; the matchers then see both keyframes' mvuRight.
 """
 import os
 import sys
@@ -55,9 +58,20 @@ def check_schedule(sched, frames_np, samples=None, agent_frames=None, threads=No
     need = sorted(need)
     local = {}
 
+    stereo = getattr(sched, "stereo", None)
+
     def extract(img):
+        """(keypoints, descriptors, stereo) of one frame; stereo (img = [2, H, W]): (right keypoints, right
+        descriptors, mvuRight, mvDepth, kept) from two extractors as the stereo Frame holds them (Frame.cc:80-92)"""
         orc = oracle_py.OracleExtractor(nfeat, 1.2, 8, 20, 7)
-        return orc(img)
+        if not stereo:
+            k, d = orc(img)
+            return k, d, None
+        k, d = orc(img[0])
+        orr = oracle_py.OracleExtractor(nfeat, 1.2, 8, 20, 7)
+        kr, dr = orr(img[1])
+        ur, dp, ns = oracle_py.compute_stereo_matches(orc, orr, k, d, kr, dr, stereo[0], stereo[1])
+        return k, d, (kr, dr, ur, dp, ns)
 
     threads = threads or host_threads()
     with ThreadPoolExecutor(max_workers=threads) as ex_pool:
@@ -65,15 +79,29 @@ def check_schedule(sched, frames_np, samples=None, agent_frames=None, threads=No
     for pb, o in zip(need, outs):
         local[pb] = o
     mism = []
+
+    def bits_differ(a, b):
+        a, b = np.ascontiguousarray(a, np.float32), np.ascontiguousarray(b, np.float32)
+        return a.shape != b.shape or not np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
     for p, b in samples:
         kg, dg, mg = sched.frame_results(p, b)
-        ko, do = local[(p, b)]
+        ko, do, so = local[(p, b)]
         if len(kg) != len(ko) or kg.tobytes() != ko.tobytes() or not np.array_equal(dg, do):
             mism.append("frame p=%d b=%d: %d vs %d keypoints or differing fields" % (p, b, len(kg), len(ko)))
             continue
-        kp, dp = local[(p, (b - 1) % sub)]
-        v1 = orbamd.KeyFrameView(ko, do, tabs["scale"], tabs["sigma2"])
-        v2 = orbamd.KeyFrameView(kp, dp, tabs["scale"], tabs["sigma2"])
+        if stereo:
+            (krg, drg), (urg, dpg, nsg) = sched.stereo_results(p, b)
+            kro, dro, uro, dpo, nso = so
+            if len(krg) != len(kro) or krg.tobytes() != kro.tobytes() or not np.array_equal(drg, dro):
+                mism.append("right image p=%d b=%d: %d vs %d keypoints or differing fields" % (p, b, len(krg), len(kro)))
+                continue
+            if bits_differ(urg, uro) or bits_differ(dpg, dpo) or nsg != nso:
+                mism.append("stereo p=%d b=%d: mvuRight / mvDepth / kept (%d vs %d) differ" % (p, b, nsg, nso))
+                continue
+        kp, dp, sp = local[(p, (b - 1) % sub)]
+        v1 = orbamd.KeyFrameView(ko, do, tabs["scale"], tabs["sigma2"], uright=so[2] if stereo else None)
+        v2 = orbamd.KeyFrameView(kp, dp, tabs["scale"], tabs["sigma2"], uright=sp[2] if stereo else None)
         _, mo = oracle_py.search_for_triangulation(v1, v2, F12, ex, ey, False, False)
         if not np.array_equal(mg, mo):
             mism.append("match p=%d b=%d vs b-1: %s" % (p, b, "%d entries differ" % int((mg != mo).sum())
@@ -84,21 +112,22 @@ def check_schedule(sched, frames_np, samples=None, agent_frames=None, threads=No
         from orbamd.agent import KF_LEVELSUP, LOOP_NNRATIO, kf_mp_flags
         xm, xn, xb, xbn = sched.exchange_results()
         t_kf = sched.frame_index(0, 0)
-        kq, dq = local.get((0, 0)) or extract(frames_np[t_kf])
+        kq, dq, sq = local.get((0, 0)) or extract(frames_np[t_kf])
         voc = _oracle_vocabulary(sched)
 
-        def kf_view(k, d, with_fv):
-            """the keyframe as the slot carries it: MapPoint records (kf_mp_flags) and, for SearchByBoW, the
-            FeatureVector of the vocabulary transform (KeyFrame::ComputeBoW, levelsup 4)"""
+        def kf_view(k, d, s, with_fv):
+            """the keyframe as the slot carries it: MapPoint records (kf_mp_flags), mvuRight when stereo and, for
+            SearchByBoW, the FeatureVector of the vocabulary transform (KeyFrame::ComputeBoW, levelsup 4)"""
             f = kf_mp_flags(len(k))
             fv = voc.transform(d, KF_LEVELSUP)[1] if with_fv else None
             return orbamd.KeyFrameView(k, d, tabs["scale"], tabs["sigma2"], feat_vec=fv, has_mp=(f & 1).astype(bool),
-                                       mp_bad=((f >> 1) & 1).astype(bool))
-        vq, vq_bow = kf_view(kq, dq, False), kf_view(kq, dq, True)
+                                       mp_bad=((f >> 1) & 1).astype(bool), uright=s[2] if s is not None else None)
+        vq, vq_bow = kf_view(kq, dq, sq, False), kf_view(kq, dq, sq, True)
         for r in range(sched.world):
             img = frames_np[t_kf] if agent_frames is None else agent_frames(r, t_kf)
-            kr, dr = extract(img) if agent_frames is not None else (kq, dq)
-            vr, vr_bow = (vq, vq_bow) if agent_frames is None else (kf_view(kr, dr, False), kf_view(kr, dr, True))
+            kr, dr, sr = extract(img) if agent_frames is not None else (kq, dq, sq)
+            vr, vr_bow = ((vq, vq_bow) if agent_frames is None else
+                          (kf_view(kr, dr, sr, False), kf_view(kr, dr, sr, True)))
             # LocalMapping's SearchForTriangulation (features with a MapPoint skipped on both sides, :699-726)
             n_o, mo = oracle_py.search_for_triangulation(vq, vr, F12, ex, ey, False, False)
             if not np.array_equal(xm[r], mo) or int(xn[r]) != int(n_o):

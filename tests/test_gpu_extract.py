@@ -124,6 +124,37 @@ def test_large_batch_whole_frame_pyramid(W, H, nf):
     pipe.close()
 
 
+@pytest.mark.parametrize("W,offset", [(641, 0), (640, 1)])
+def test_large_batch_unaligned_rows_separate_blur(W, offset):
+    """A >= 64-frame batch whose level-0 rows are not 4-byte aligned (a 641-byte row pitch, or frames starting one
+    byte into the buffer) cannot take the fused describe (k_describe_blur's LDS-DMA moves dwords): the pyramid falls
+    back to the per-level kernels, the blur runs in k_blur_strips on the handle's lazily created side stream (its
+    buffer allocated at this first unaligned call) and k_describe joins it. Keypoints, descriptors and every pyramid
+    level against the oracle, over two steps on one pipeline (the second reuses the side stream and blur buffer)."""
+    torch = pytest.importorskip("torch")
+    lib = orbamd.load()
+    H, B = 480, 64
+    frames = orbamd.synth_frames(6, 4, B, W, H)
+    buf = torch.zeros(B * H * W + offset, dtype=torch.uint8, device="cuda")
+    fr = buf[offset:].view(B, H, W)
+    fr.copy_(torch.from_numpy(frames).cuda())
+    assert lib.orbx_describe_blur_fused(fr.data_ptr(), fr.stride(0), fr.stride(1)) == 0
+    pipe = orbamd.device.BatchPipeline(torch, W, H, B)
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    for step in range(2):
+        pipe.extract(fr)
+        pipe.check_error()
+        torch.cuda.synchronize()
+        for b in (0, 29, B - 1):
+            kg, dg, _ = pipe.host_results(b)
+            ko, do = orc(frames[b])
+            _compare(kg, dg, ko, do)
+            for l in range(8):
+                np.testing.assert_array_equal(pipe.ext.pyramid_level(l, frame=b), orc.pyramid(l),
+                                              err_msg="step %d frame %d pyramid level %d" % (step, b, l))
+    pipe.close()
+
+
 PARAMS = [
     # (W, H, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST): other my.yaml settings / odd sizes
     (641, 479, 1000, 1.2, 8, 20, 7),

@@ -6,7 +6,7 @@ error flags, then EVERY frame's keypoints and
 descriptors (raw bits), every frame's SearchForTriangulation row against its predecessor, and the
 cross-agent match row are compared with the oracle (ORBextractor.cc:1043-1105,
 ORBmatcher.cc:657-823). The BASELINE configs C3 (752x480, 1200 features) and C4 (1241x376, 2000
-features) run the same schedule on smaller batches."""
+features) run the same schedule on smaller batches, and as the stereo frames those configs name."""
 import pytest
 
 import orbamd
@@ -39,6 +39,36 @@ def test_bench_schedule_bit_exact(W, H, nf, B, P, stagger, async_x):
     assert res["checked_frames"] == B and res["checked_slots"] == 1
     assert res["slot_bow_matches"][0] > 100  # SearchByBoW(KF,KF) of the keyframe against its own slot
     assert all(int(pp.nmatch.min().item()) > 0 for pp in sched.pipes)
+    sched.close()
+
+
+@pytest.mark.parametrize("cfg,B,P,async_x", [("c3", 256, 2, False), ("c4", 128, 2, False), ("c3", 192, 3, True)])
+def test_stereo_schedule_bit_exact(cfg, B, P, async_x):
+    """BASELINE configs 3 and 4 as stereo frames (bench.py --config c3 / c4): every frame's left and right
+    keypoints / descriptors, mvuRight / mvDepth (raw bits) and kept count of ComputeStereoMatches (Frame.cc:471-645),
+    the stereo SearchForTriangulation row against its predecessor (ORBmatcher.cc:703-749) and the cross-agent rows of
+    the stereo keyframe slot, against the oracle"""
+    torch = pytest.importorskip("torch")
+    import numpy as np
+    import bench
+    from orbamd.agent import AgentSchedule
+    from orbamd.device import STEREO_RIGS
+    c = bench.CONFIGS[cfg]
+    W, H, nf, rig = c["W"], c["H"], c["nfeatures"], STEREO_RIGS[c["stereo"]]
+    frames = np.stack([orbamd.synth_frames(0, 0, B, W, H, scene=0),
+                       orbamd.synth_frames(0, 0, B, W, H, dx=c["dx"], scene=0)], axis=1)
+    sched = AgentSchedule(torch, frames, W, H, P, device=0, nfeatures=nf, async_exchange=async_x, stereo=rig)
+    for i in range(3):
+        sched.step(first=i == 0)
+    torch.cuda.synchronize()
+    sched.check_errors()
+    samples = [(p, b) for p in range(P) for b in range(B // P)]  # every frame
+    res = check_schedule(sched, frames, samples=samples, nfeatures=nf)
+    assert res["bit_exact"], res["mismatches"]
+    assert res["checked_frames"] == B and res["checked_slots"] == 1
+    for pp in sched.pipes:  # the stereo branch has work: most left keypoints find their right partner
+        assert int(pp.nstereo.min().item()) > int(pp.counts[:pp.B].min().item()) // 4
+        assert int(pp.nmatch.min().item()) > 0
     sched.close()
 
 
