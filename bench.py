@@ -217,7 +217,7 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000, st
     return sum(count) / el, sum(count), el, per
 
 
-def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, dist, nstreams=4):
+def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, dist, reduce_max, nstreams=4):
     """The schedule with every step's B frames uploaded from pinned host memory (the frame pool, batch
     i mod pool at step i) into the device batch the step processes, on `nstreams` copy streams whatever the
     graph count (several DMA engines in flight: round 3's fourth copy stream was +36 %, and tying the streams to
@@ -264,11 +264,7 @@ def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, 
     for i in range(nsteps):
         one(pool + i)
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if use_dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = reduce_max(time.perf_counter() - t0)
     fps = world * B * nsteps / el
     return {"frames_per_s": round(fps, 1), "per_gpu_frames_per_s": round(fps / world, 1),
             "h2d_GBs_per_gpu": round(per * B * W * H * nsteps / el / 1e9, 2), "steps": nsteps, "seconds": round(el, 3),
@@ -344,7 +340,12 @@ def main():
     ap.add_argument("--pool", type=int, default=2,
                     help="resident batches of distinct frames; step k processes batch k mod pool (stale-output guard)")
     ap.add_argument("--dist", action="store_true",
-                    help="use torch.distributed (RCCL) and the out-of-place all-gather even at world 1")
+                    help="use torch.distributed and the out-of-place RCCL all-gather even at world 1")
+    ap.add_argument("--collective", choices=("rccl", "torch"), default="rccl",
+                    help="the keyframe all-gather across ranks: rccl = liborbamd's RCCL communicator (orbx_comm_allgather: "
+                         "ncclAllGather on the exchange's own HIP stream, no collective-owned stream; torch.distributed runs "
+                         "the gloo control plane: unique-id broadcast, barriers, max-over-ranks timing), torch = "
+                         "torch.distributed's ProcessGroupNCCL all_gather_into_tensor (its internal RCCL stream)")
     ap.add_argument("--ingest-streams", type=int, default=4, help="copy streams of the ingest leg (<= --pipes)")
     ap.add_argument("--ingest-steps", type=int, default=100,
                     help="steps of the ingest leg (frames uploaded from pinned host memory each step; 0: skip)")
@@ -378,6 +379,7 @@ def main():
     import torch
     import torch.distributed as dist
     import orbamd
+    from orbamd._lib import check as lib_check
     from orbamd.agent import AgentSchedule
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -391,15 +393,40 @@ def main():
     if world != args.gpus:
         print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr, flush=True)
         sys.exit(2)
+    # the data-path collective: liborbamd's RCCL communicator (default), torch's ProcessGroupNCCL, or (one-GPU
+    # rehearsals, ORBAMD_DIST_BACKEND=gloo) gloo through host memory
+    coll = args.collective if backend == "nccl" else "gloo"
     if use_dist:
         torch.cuda.set_device(local)
-        if backend == "nccl":
+        if coll == "torch":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        else:  # control plane only: barriers, max-over-ranks timing, the RCCL unique id
+            dist.init_process_group("gloo")
         assert dist.get_world_size() == world
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    ctl_dev = dev if coll == "torch" else torch.device("cpu")
+
+    def reduce_max(v, dtype=None):
+        """max over ranks of a host number (the whole job's time is its slowest rank's)"""
+        if not use_dist:
+            return v
+        t = torch.tensor([v], dtype=dtype or torch.float64, device=ctl_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item()
+    comm = None
+    if use_dist and coll == "rccl":
+        import ctypes as C
+        lib0 = orbamd.load()
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            lib_check(lib0.orbx_comm_unique_id(uid), "orbx_comm_unique_id")
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0)
+        uid = (C.c_uint8 * 128).from_buffer_copy(box[0])
+        h = C.c_void_p()
+        lib_check(lib0.orbx_comm_create(uid, world, rank, local, C.byref(h)), "orbx_comm_create")
+        comm = h
 
     W, H, P = cfg["W"], cfg["H"], args.pipes
     rig = None if args.mono or "stereo" not in cfg else orbamd.device.STEREO_RIGS[cfg["stereo"]]
@@ -420,8 +447,11 @@ def main():
         return np.stack([left, orbamd.synth_frames(r, t0, n, W, H, dx=cfg["dx"], scene=scene)], axis=1)
     frames_np = agent_frames(rank, 0, args.pool * B)  # agent = rank; pool batches back to back
     def allgather(out, inp):
-        # RCCL over xGMI; gloo (the one-GPU rehearsal): through host memory
-        if backend == "nccl":
+        # RCCL over xGMI on the current (exchange) stream; gloo (the one-GPU rehearsal): through host memory
+        if coll == "rccl":
+            lib_check(orbamd.load().orbx_comm_allgather(comm, inp.data_ptr(), out.data_ptr(), inp.numel(),
+                                                        torch.cuda.current_stream(dev).cuda_stream), "orbx_comm_allgather")
+        elif coll == "torch":
             dist.all_gather_into_tensor(out, inp)
         else:
             o = torch.empty(out.numel(), dtype=torch.uint8)
@@ -430,7 +460,9 @@ def main():
 
     lo_prio, hi_prio = torch.cuda.Stream.priority_range()
     n_hi = {"none": 0, "lead": P // 2, "lead1": 1}[args.prio]
-    async_x = args.exchange_stream == "own" or (args.exchange_stream == "auto" and use_dist)
+    # auto: torch's collective on the exchange's own stream (off graph 0's chain while it waits on its internal stream);
+    # liborbamd's RCCL in order on graph 0's stream, as the N = 1 exchange (no stream beyond the graphs')
+    async_x = args.exchange_stream == "own" or (args.exchange_stream == "auto" and use_dist and coll == "torch")
     sched = AgentSchedule(torch, frames_np, W, H, P, device=local, rank=rank, world=world,
                           allgather=allgather if use_dist else None,
                           stagger=args.stagger, exchange=not args.no_exchange,
@@ -482,7 +514,8 @@ def main():
         for pp in pipes:
             ms = (C.c_double * 5)()
             nc = C.c_int()
-            lib.orbx_profile_read(pp.ext._h, ms, C.byref(nc))
+            # a failing read (an unrecorded stage event pair) must stop the run, not leave a HIP error behind
+            lib_check(lib.orbx_profile_read(pp.ext._h, ms, C.byref(nc)), "orbx_profile_read")
             lib.orbx_profile_enable(pp.ext._h, 0)
             for i in range(5):
                 acc[i] += ms[i]
@@ -520,10 +553,7 @@ def main():
     # 2) timed region: only the priced kernels bracketed (their live launch durations for the roofline)
     el, dom_live = run_profiled((1 << stages.index(dom)) | ((1 << stages.index(co)) if co else 0), args.steps, True)
     last_batch, prev_batch = sched.last_batch, (sched.last_batch - 1) % args.pool
-    if use_dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = reduce_max(el)
     # 3) self-check of the last timed step (error flags on every rank; oracle bit-compare of sampled frames,
     # their match rows and the cross-agent matches)
     err_msg = None
@@ -540,9 +570,7 @@ def main():
     ok_local = err_msg is None and (check is None or check["bit_exact"])
     ok_all = ok_local
     if use_dist:
-        t = torch.tensor([0 if ok_local else 1], dtype=torch.int32, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ok_all = int(t.item()) == 0
+        ok_all = int(reduce_max(0 if ok_local else 1, torch.int32)) == 0
     # 3b) the priced kernels alone (untimed, after the check): graph 0 re-extracts the last batch in stage order with
     # every other graph idle, one step at a time, the priced stages bracketed by HIP events; the live launch above is
     # the kernel's share of a chip running the other graphs, this is its own speed (roofline.alone)
@@ -557,7 +585,7 @@ def main():
             torch.cuda.synchronize()
             ms = (C.c_double * 5)()
             nc = C.c_int()
-            lib.orbx_profile_read(pp0.ext._h, ms, C.byref(nc))
+            lib_check(lib.orbx_profile_read(pp0.ext._h, ms, C.byref(nc)), "orbx_profile_read")
             vals.append(ms[stages.index(kern)] / max(nc.value, 1))
         alone_ms[kern] = sorted(vals)[len(vals) // 2]
     lib.orbx_profile_enable(pp0.ext._h, 0)
@@ -587,7 +615,7 @@ def main():
         if use_dist:
             dist.barrier()
         ingest = run_ingest(torch, sched, frames_np, args.pool, args.ingest_steps, B, W, H, world, use_dist, dist,
-                            args.ingest_streams)
+                            reduce_max, args.ingest_streams)
         if not args.no_check:
             chk = check_schedule(sched, frames_np, nfeatures=cfg["nfeatures"], agent_frames=agent_kf)
             ingest["bit_exact"] = bool(chk["bit_exact"])
@@ -601,11 +629,7 @@ def main():
         n_sus = max(1, int(math.ceil(args.sustain / (el / args.steps))))
         if use_dist:
             dist.barrier()
-        sus_s = run_part(n_sus)
-        if use_dist:
-            t = torch.tensor([sus_s], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            sus_s = float(t.item())
+        sus_s = reduce_max(run_part(n_sus))
         sustained = {"seconds": round(sus_s, 3), "steps": n_sus, "frames_per_s": round(world * B * n_sus / sus_s, 1)}
     nkp = float(sum(pp.counts.float().mean().item() for pp in pipes) / P)
     nmatch = float(sum(pp.nmatch.float().mean().item() for pp in pipes) / P)
@@ -768,7 +792,11 @@ def main():
                                     "launch in the checked (last timed) step leaves the previous batch's outputs and "
                                     "fails the oracle check" if args.pool > 1 else
                                     "pool of 1: repeated frames, a skipped launch would not be detected"},
-            "collective": ("rccl all_gather_into_tensor (out-of-place slot buffer)" if use_dist and backend == "nccl"
+            "collective": ("rccl ncclAllGather by liborbamd (orbx_comm_allgather) on %s stream, out-of-place slot "
+                           "buffer; gloo control plane" % ("the exchange's own" if async_x else "graph 0's")
+                           if use_dist and coll == "rccl" else
+                           "rccl all_gather_into_tensor (torch ProcessGroupNCCL, out-of-place slot buffer)"
+                           if use_dist and coll == "torch"
                            else "gloo all_gather through host memory (rehearsal)" if use_dist
                            else "none (N=1: the keyframe slot is packed in place)"),
         }
@@ -813,6 +841,8 @@ def main():
     sched.close()
     if use_dist:
         dist.barrier()
+        if comm is not None:
+            orbamd.load().orbx_comm_destroy(comm)
         dist.destroy_process_group()
     if not ok_all:
         sys.exit(3)

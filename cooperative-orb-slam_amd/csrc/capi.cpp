@@ -32,12 +32,19 @@
 
 using namespace orbamd;
 
+/* A failing HIP call is reported once, through the entry point's status (ORBX_EDEVICE), and then cleared from the
+ * calling thread's HIP error state: hipGetLastError returns the last error of ANY runtime call on the thread, so a
+ * failure left there would be raised again by the caller's next launch check, far from its cause (round 5's first GPU
+ * run: hipEventElapsedTime over a never-recorded stage event pair in orbx_profile_read, whose status bench.py did not
+ * read, surfaced as "HIP error: invalid resource handle" in torch's dist.barrier; tests/test_gpu_cache.py
+ * ::test_library_hip_failure_does_not_leak pins this). */
 #define HIPR(expr)                                                                    \
     do {                                                                              \
         hipError_t e_ = (expr);                                                       \
         if (e_ != hipSuccess) {                                                       \
             if (getenv("ORBX_DEBUG")) fprintf(stderr, "HIP error %s at %s:%d\n",     \
                                               hipGetErrorString(e_), __FILE__, __LINE__); \
+            (void)hipGetLastError();                                                  \
             return ORBX_EDEVICE;                                                      \
         }                                                                             \
     } while (0)
@@ -870,6 +877,23 @@ int orbx_set_stage_event(orbx_handle* h, int stage, void* event) {
 
 int orbx_describe_blur_fused(const void* frames, size_t frame_stride, size_t pitch) {
     return use_describe_blur((const uint8_t*)frames, (long long)frame_stride, (int)pitch) ? 1 : 0;
+}
+
+int orbx_debug_hip_failure(void) {
+    // two events that were never recorded: hipEventElapsedTime fails (invalid resource handle), as an unrecorded
+    // stage pair did in round 5's orbx_profile_read
+    hipEvent_t a = nullptr, b = nullptr;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+        if (a) (void)hipEventDestroy(a);
+        (void)hipGetLastError();
+        return ORBX_EDEVICE;
+    }
+    float t = 0;
+    const hipError_t e = hipEventElapsedTime(&t, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    HIPR(e);
+    return 0;
 }
 
 int orbx_debug_skip_stages(orbx_handle* h, int mask) {

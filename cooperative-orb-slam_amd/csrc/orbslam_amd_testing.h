@@ -38,6 +38,11 @@ int orbx_debug_alias_frames(orbx_handle* h, int on);
  * and that orbx_check_error reports and clears it once. */
 int orbx_debug_raise_error(orbx_handle* h, int flag, void* stream);
 
+/* Test hook: one HIP runtime call that fails (hipEventElapsedTime over two never-recorded events) inside the
+ * library's error handling; returns ORBX_EDEVICE, and the calling thread's HIP error state (hipGetLastError) must be
+ * clean afterwards, so the failure does not resurface in the caller's next launch check. */
+int orbx_debug_hip_failure(void);
+
 /* Measurement query (host-only): 1 if a batched extraction of frames at `frames` (device pointer value, frame stride
  * and row pitch in bytes) blurs inside describe (k_describe_blur: level-0 rows 4-aligned), 0 if it takes the separate
  * blur (k_blur_strips + k_describe); bench.py prices describe's bytes by the form that ran. */

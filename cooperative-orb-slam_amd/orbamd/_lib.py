@@ -108,6 +108,11 @@ SIGNATURES = {
     "orbx_set_pyramid_event": (_I, [_P, _P]),
     "orbx_set_stage_event": (_I, [_P, _I, _P]),
     "orbx_debug_skip_stages": (_I, [_P, _I]),
+    "orbx_debug_hip_failure": (_I, []),
+    "orbx_comm_unique_id": (_I, [_P]),
+    "orbx_comm_create": (_I, [_P, _I, _I, _I, _P]),
+    "orbx_comm_allgather": (_I, [_P, _P, _P, _SZ, _P]),
+    "orbx_comm_destroy": (None, [_P]),
     "orbx_describe_blur_fused": (_I, [_P, _SZ, _SZ]),
     "orbx_debug_serial": (_I, [_P, _I]),
     "orbx_debug_alias_frames": (_I, [_P, _I]),

@@ -626,6 +626,24 @@ int orbm_search_by_bow_slots_device(orbm_ctx* ctx, const orbx_kf_source* query, 
                                     int max_nodes, int32_t* d_match, int32_t* d_nmatches, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * Cross-agent collective -- replaces the LCM keyframe publish / subscribe between the agents
+ * (ORB_SLAM2.1/Examples/ROS/ORB_SLAM2/src/ros_mono.cc:2399, ORB_SLAM2/Examples/ROS/ORB_SLAM2/
+ * src/ros_mono.cc:602): one RCCL all-gather over xGMI of every agent's keyframe slot
+ * (orbx_pack_keyframe_device), enqueued on the caller's stream (no collective-owned stream), one
+ * process = one agent = one GPU. RCCL is bound at run time (the process's librccl.so.1 if one
+ * is loaded, else ROCm's); ORBX_EDEVICE without it.
+ * ---------------------------------------------------------------------------------- */
+#define ORBX_COMM_ID_BYTES 128
+typedef struct orbx_comm orbx_comm;
+/* rank 0 creates the id (ncclGetUniqueId); the caller hands it to every rank (any transport) */
+int orbx_comm_unique_id(uint8_t* id);
+/* collective over the world: every rank calls it with the same id, its rank and its device */
+int orbx_comm_create(const uint8_t* id, int world, int rank, int device, orbx_comm** out);
+/* d_recv[r*bytes .. (r+1)*bytes) = rank r's d_send[0 .. bytes), on `stream` (ncclAllGather, uint8) */
+int orbx_comm_allgather(orbx_comm* c, const void* d_send, void* d_recv, size_t bytes, void* stream);
+void orbx_comm_destroy(orbx_comm* c);
+
+/* ------------------------------------------------------------------------------------
  * Stereo -- replaces Frame::ComputeStereoMatches (ORB_SLAM2.1/src/Frame.cc:470-641, the
  * stereo Frame constructor's step after ExtractORB(0/1), Frame.cc:80-98), reading the two
  * extractors' pyramids (mpORBextractorLeft/Right->mvImagePyramid) where they already live.

@@ -167,3 +167,38 @@ def test_small_bow_and_projection_alternate_on_one_context():
             F, mps, 3.0, 0.75)
         assert gn == on
         np.testing.assert_array_equal(gm, om)
+
+
+def test_library_hip_failure_does_not_leak():
+    """A HIP runtime call that fails inside liborbamd is reported through the entry point's status and cleared from
+    the calling thread's HIP error state (capi.cpp HIPR). Round 5's first GPU run raised a library-internal
+    hipEventElapsedTime failure (an unrecorded stage event pair in orbx_profile_read, whose status bench.py ignored)
+    as "HIP error: invalid resource handle" inside torch's next launch check (dist.barrier); with the failure left in
+    the thread's error state the torch launch below raises the same way."""
+    import ctypes
+    torch = pytest.importorskip("torch")
+    lib = orbamd.load()
+    x = torch.ones(16, device="cuda")
+    torch.cuda.synchronize()
+    hip = ctypes.CDLL("libamdhip64.so")  # the HIP runtime torch and liborbamd share in this process
+    hip.hipGetLastError.restype = ctypes.c_int
+    assert hip.hipGetLastError() == 0
+    assert lib.orbx_debug_hip_failure() == -2  # ORBX_EDEVICE: the call did fail
+    assert hip.hipGetLastError() == 0, "the library left its HIP failure in the caller's error state"
+    y = (x * 2).sum()  # torch's launch check sees no stale error
+    torch.cuda.synchronize()
+    assert float(y.item()) == 32.0
+    # the bench's stage profiling in both describe forms: every stage's event pair is recorded, the read succeeds and
+    # leaves no error behind
+    import ctypes as C
+    for W in (640, 641):
+        pipe = orbamd.device.BatchPipeline(torch, W, 480, 64)
+        fr = torch.from_numpy(orbamd.synth_frames(1, 2, 64, W, 480)).cuda()
+        assert lib.orbx_profile_enable(pipe.ext._h, 0x1F) == 0
+        pipe.extract(fr)
+        ms = (C.c_double * 5)()
+        nc = C.c_int()
+        assert lib.orbx_profile_read(pipe.ext._h, ms, C.byref(nc)) == 0 and nc.value == 1
+        assert hip.hipGetLastError() == 0
+        lib.orbx_profile_enable(pipe.ext._h, 0)
+        pipe.close()

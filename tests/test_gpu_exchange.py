@@ -290,14 +290,17 @@ def test_eight_agent_slots_equal_oracle(use_bow):
     mh.close()
 
 
-def test_bench_rccl_world1():
-    """bench.py under torch.distributed.run with one rank and --dist: the RCCL process group (init with
-    device_id), the out-of-place all_gather_into_tensor of the keyframe slot on the graph stream and the
-    cross-agent match from the receive buffer, as at N>1; the run's self-check must be bit-exact."""
+@pytest.mark.parametrize("collective", ["rccl", "torch"])
+def test_bench_rccl_world1(collective):
+    """bench.py under torch.distributed.run with one rank and --dist, as at N>1: the keyframe slot's out-of-place RCCL
+    all-gather (rccl: liborbamd's communicator, ncclAllGather on graph 0's stream, gloo control plane; torch: the
+    ProcessGroupNCCL all_gather_into_tensor on the exchange's own stream) and the cross-agent match from the receive
+    buffer; the run's self-check must be bit-exact."""
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--dist", "--steps", "4",
-           "--warmup", "2", "--batch", "256", "--pipes", "2", "--no-cpu", "--sustain", "0", "--ingest-steps", "4"]
+           "--warmup", "2", "--batch", "256", "--pipes", "2", "--no-cpu", "--sustain", "0", "--ingest-steps", "4",
+           "--collective", collective]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT,
                        env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
     print(r.stdout[-3000:], r.stderr[-3000:])
@@ -306,6 +309,7 @@ def test_bench_rccl_world1():
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
     assert res["collective"].startswith("rccl"), res["collective"]
+    assert ("liborbamd" in res["collective"]) == (collective == "rccl"), res["collective"]
     assert res["bit_exact"] is True and res["checked_slots"] == 1 and res["device_errors"] is None
     assert res["ingest"]["bit_exact"] is True
     assert res["stage_ms_per_step"]["allgather"] > 0
