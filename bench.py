@@ -217,7 +217,8 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000, st
     return sum(count) / el, sum(count), el, per
 
 
-def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, dist, reduce_max, nstreams=4):
+def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, dist, reduce_max, nstreams=4,
+               chunks=0):
     """The schedule with every step's B frames uploaded from pinned host memory (the frame pool, batch
     i mod pool at step i) into the device batch the step processes, on `nstreams` copy streams whatever the
     graph count (several DMA engines in flight: round 3's fourth copy stream was +36 %, and tying the streams to
@@ -225,13 +226,13 @@ def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, 
     contiguous chunks dealt round-robin over the streams in graph order, and graph p starts extracting as soon
     as its own chunks have arrived. Upload i waits for step i-pool (the previous user of that device batch), so
     an upload overlaps the previous step's compute. Returns frames/s over nsteps after `pool` warm-up steps and
-    the H2D rate achieved (bytes per frame uploaded, max over ranks)."""
+    the H2D rate achieved (bytes per frame uploaded, max over ranks). chunks: chunks per graph (0: ceil(nstreams / P))."""
     P, sub, dev = sched.P, sched.sub, sched.dev
     per = sched.images_per_frame  # 2 for stereo pairs (left + right image per frame)
     host = [torch.from_numpy(sched.host_batch(frames_np, r)).pin_memory() for r in range(pool)]
     nst = max(1, nstreams)
     copy_st = [torch.cuda.Stream(dev) for _ in range(nst)]
-    k = -(-nst // P)  # chunks per graph
+    k = chunks or -(-nst // P)  # chunks per graph (default: enough to give every copy stream one)
     imgs = per * sub
     cuts = [(j * imgs // k, (j + 1) * imgs // k) for j in range(k)]
     up = [[[torch.cuda.Event() for _ in range(k)] for _ in range(P)] for _ in range(pool)]

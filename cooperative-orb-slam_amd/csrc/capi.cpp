@@ -463,6 +463,7 @@ struct orbx_handle {
     DevBuf in_frame, out_kps, out_desc, out_cnt;
     // orbx_compute_stereo_matches staging (host path) and k_stereo's LDS attribute
     DevBuf st_buf;
+    DevBuf stereo_sad;  // orbx_stereo_matches_batch_device: each left keypoint's SAD for the median pass
     int stereo_lds_set = 0;
     // last extraction, for orbx_pyramid_level
     const uint8_t* last_frames = nullptr;
@@ -831,7 +832,7 @@ void orbx_destroy(orbx_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->side) (void)hipStreamSynchronize(h->side);
     for (DevBuf* b : {&h->pyr, &h->blur, &h->cellkey, &h->cellcnt, &h->lvkey, &h->lvcnt, &h->gscratch, &h->err,
-                      &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt, &h->st_buf})
+                      &h->in_frame, &h->out_kps, &h->out_desc, &h->out_cnt, &h->st_buf, &h->stereo_sad})
         b->release();
     h->geo.release();
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1329,8 +1330,9 @@ int orbx_stereo_matches_batch_device(orbx_handle* left, orbx_handle* right, int 
     if (npairs == 0) return 0;
     HIPR(hipSetDevice(left->device));
     if ((rc = stereo_prepare(left, kp_stride))) return rc;
+    if (left->stereo_sad.ensure((size_t)npairs * kp_stride * 4)) return ORBX_EDEVICE;
     HIPR(launch_stereo(a, npairs, d_fl, d_fr, d_kpsL, d_descL, d_cntL, d_kpsR, d_descR, d_cntR, kp_stride, d_uright,
-                       d_depth, d_nstereo, left->err.as<int>(), (hipStream_t)stream));
+                       d_depth, d_nstereo, left->stereo_sad.as<int32_t>(), left->err.as<int>(), (hipStream_t)stream));
     return 0;
 }
 
@@ -1349,9 +1351,9 @@ int orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orb
     HIPR(hipSetDevice(left->device));
     const int stride = (int)align_up(std::max(nL, nR), 4);
     if ((rc = stereo_prepare(left, stride))) return rc;
-    // staging: kpsL | kpsR | descL | descR | uright | depth | {fl=0, fr=0, cntL, cntR, nstereo}
+    // staging: kpsL | kpsR | descL | descR | uright | depth | {fl=0, fr=0, cntL, cntR, nstereo} | sad scratch
     const size_t kb = sizeof(orbx_kp) * stride, db = 32 * (size_t)stride, fb = 4 * (size_t)stride;
-    if (left->st_buf.ensure(2 * kb + 2 * db + 2 * fb + 64)) return ORBX_EDEVICE;
+    if (left->st_buf.ensure(2 * kb + 2 * db + 3 * fb + 64)) return ORBX_EDEVICE;
     uint8_t* base = left->st_buf.as<uint8_t>();
     orbx_kp* dkL = (orbx_kp*)base;
     orbx_kp* dkR = (orbx_kp*)(base + kb);
@@ -1378,7 +1380,7 @@ int orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orb
     HIPR(hipMemsetAsync(cerr, 0, sizeof(int), st));
     a.left.nframes = a.right.nframes = 1;
     HIPR(launch_stereo(a, 1, misc, misc + 1, dkL, ddL, misc + 2, dkR, ddR, misc + 3, stride, dur, ddp, misc + 4,
-                       cerr, st));
+                       (int32_t*)((uint8_t*)misc + 64), cerr, st));
     int flag = 0, ns = 0;
     HIPR(hipMemcpyAsync(uright, dur, 4 * (size_t)nL, hipMemcpyDeviceToHost, st));
     HIPR(hipMemcpyAsync(depth, ddp, 4 * (size_t)nL, hipMemcpyDeviceToHost, st));

@@ -2,15 +2,16 @@
  * frame_kernels.hip -- gfx950 kernels for the Frame-level consumers of the extractor output
  * (SURVEY.md 8(f)).
  *
- *   k_stereo   Frame::ComputeStereoMatches (ORB_SLAM2.1/src/Frame.cc:470-641), one workgroup
- *              per stereo pair of a batch: right keypoints bucketed by their row band in LDS
- *              (counting sort replaces vRowIndices, Frame.cc:477-498), one wave per left
+ *   k_stereo   Frame::ComputeStereoMatches (ORB_SLAM2.1/src/Frame.cc:470-641), 4 workgroups of
+ *              256 threads per stereo pair of a batch: right keypoints bucketed by their row band in
+ *              LDS (counting sort replaces vRowIndices, Frame.cc:477-498), 16 lanes per left
  *              keypoint for the band/octave/disparity-filtered Hamming search (the minimum of
  *              (dist, iR) is the reference's first-strict-minimum, so bucket order is free),
- *              the 11x11 SAD over 11 shifts on the device-resident pyramids staged per wave in
- *              LDS (integers: exact, as cv::norm's double sum of integer-valued floats is),
- *              the parabola fit in IEEE float (no contraction), then the per-frame median
- *              rejection (Frame.cc:636-650) as an LDS radix select.
+ *              the 11x11 SAD over 11 shifts (a lane per shift) on the device-resident pyramids
+ *              staged per keypoint in LDS (integers: exact, as cv::norm's double sum of
+ *              integer-valued floats is), the parabola fit in IEEE float (no contraction);
+ *   k_stereo_median
+ *              then the per-frame median rejection (Frame.cc:636-650) as an LDS radix select.
  *   k_grid     Frame::AssignFeaturesToGrid (Frame.cc:235-250, PosInGrid 391-401): CSR cell lists
  *              (counting sort in LDS; order inside a cell is free, see k_proj_scan).
  *   k_proj_scan / k_proj_resolve
@@ -44,25 +45,27 @@
 
 namespace orbamd {
 
-constexpr int kStereoThreads = 1024;
+/* k_stereo: kStereoSplit workgroups of kStereoThreads per stereo pair, each over every kStereoSplit-th block of 16 left
+ * keypoints; 16 lanes per left keypoint, so a wave carries 4 keypoints through the band search and the SAD at once
+ * (round 5's form: one wave per keypoint and one 1024-thread workgroup per pair, a long dependent chain per keypoint
+ * and a workgroup that needs a whole CU's wave slots beside the other graphs' kernels). Every workgroup buckets the
+ * pair's right keypoints by row band itself (nR records, cheap beside the search); the median rejection, which needs
+ * every keypoint of the pair, is k_stereo_median's. */
+constexpr int kStereoThreads = 256;
 constexpr int kStereoWaves = kStereoThreads / 64;
-constexpr int kStereoWaveBytes = 124 + 232 + 4 * 56 + 4 * 12;  // IL 11x11, IR 11x21, SAD parts, totals
+constexpr int kStereoGroups = kStereoThreads / 16;  // left keypoints in flight per workgroup
+constexpr int kStereoSplit = 4;                     // workgroups per pair
+constexpr int kStereoIL = 12, kStereoIR = 24;       // LDS row pitch of the 11x11 window / the 11x21 strip
+constexpr int kStereoWinBytes = 11 * kStereoIL + 11 * kStereoIR + 4;  // + 4: IR's last dword read past column 23
 
 /* dynamic LDS layout of k_stereo for kp capacity `cap` and `nrows` level-0 rows */
 struct StereoLds {
-    int rx, rband, roct, sorted, row, sad, wave, hist, misc, total;
+    int rec, row, win, total;
     __host__ __device__ StereoLds(int cap, int nrows) {
-        const int c4 = (cap + 3) & ~3;
-        rx = 0;
-        rband = rx + 4 * c4;
-        roct = rband + 4 * c4;
-        sorted = roct + c4;
-        row = sorted + 2 * c4;
-        sad = row + 4 * ((nrows + 2 + 3) & ~3);
-        wave = sad + 4 * c4;
-        hist = wave + kStereoWaves * kStereoWaveBytes;
-        misc = hist + 4 * 512;
-        total = misc + 4 * 8;
+        rec = 0;                                            // one float4 per right keypoint, in bucket order
+        row = rec + 16 * ((cap + 3) & ~3);                  // bucket offsets (nrows + 2)
+        win = row + 4 * ((nrows + 2 + 3) & ~3);             // per 16-lane group: IL (11 x 12) | IR (11 x 24)
+        total = win + kStereoGroups * ((kStereoWinBytes + 15) & ~15);
     }
 };
 
@@ -72,6 +75,14 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+/* minimum over each row of 16 lanes (DPP quad butterfly + row rotations), every lane of the row holds it */
+__device__ __forceinline__ uint32_t row16_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
+    return v;
+}
 
 __device__ __forceinline__ const uint8_t* level_base(const PyrSide& s, const StereoArgs& a, int f, int l,
                                                      int* pitch) {
@@ -92,19 +103,13 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
                                                            const uint8_t* __restrict__ descR,
                                                            const int32_t* __restrict__ cntR, int stride,
                                                            float* __restrict__ uright, float* __restrict__ depth,
-                                                           int32_t* __restrict__ nstereo, int* __restrict__ err) {
+                                                           int32_t* __restrict__ sad, int* __restrict__ err) {
     extern __shared__ __align__(16) uint8_t lds[];
     const StereoLds o(stride, a.nrows);
-    float* s_rx = (float*)(lds + o.rx);
-    int* s_rband = (int*)(lds + o.rband);
-    int8_t* s_roct = (int8_t*)(lds + o.roct);
-    uint16_t* s_sorted = (uint16_t*)(lds + o.sorted);
+    float4* s_rec = (float4*)(lds + o.rec);  // {uR, band (minr | maxr << 16, clamped to the rows), octave, iR}
     int* s_row = (int*)(lds + o.row);
-    int* s_sad = (int*)(lds + o.sad);
-    int* s_hist = (int*)(lds + o.hist);
-    int* s_misc = (int*)(lds + o.misc);
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int p = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = tid >> 4, li = tid & 15;
+    const int p = blockIdx.x / kStereoSplit, part = blockIdx.x % kStereoSplit;
     const int fl = fl_idx[p], fr = fr_idx[p];
     if (fl < 0 || fl >= a.left.nframes || fr < 0 || fr >= a.right.nframes) {
         if (tid == 0) atomicOr(err, 4);
@@ -121,33 +126,20 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
     const uint8_t* dR = descR + (long long)fr * stride * 32;
     float* ur = uright + (long long)p * stride;
     float* dp = depth + (long long)p * stride;
+    int32_t* sd = sad + (long long)p * stride;
     const int nrows = a.nrows;
 
-    // mvuRight = mvDepth = -1 (Frame.cc:472-473); row-bucket counts
-    for (int i = tid; i < nL; i += kStereoThreads) {
-        ur[i] = -1.0f;
-        dp[i] = -1.0f;
-        s_sad[i] = -1;
-    }
+    // vRowIndices (Frame.cc:477-498) as buckets by the first row of each right keypoint's band: counts, scan, scatter
     for (int i = tid; i <= nrows + 1; i += kStereoThreads) s_row[i] = 0;
-    for (int i = tid; i < 512; i += kStereoThreads) s_hist[i] = 0;
-    if (tid < 8) s_misc[tid] = 0;
     __syncthreads();
-    // row band of each right keypoint (Frame.cc:487-498): rows minr..maxr
     for (int iR = tid; iR < nR; iR += kStereoThreads) {
         const orbx_kp k = kR[iR];
         const float r = __fmul_rn(2.0f, a.scale[k.octave]);
-        const int maxr = (int)ceilf(__fadd_rn(k.y, r));
         const int minr = (int)floorf(__fsub_rn(k.y, r));
-        s_rx[iR] = k.x;
-        s_rband[iR] = (minr & 0xffff) | (maxr << 16);
-        s_roct[iR] = (int8_t)k.octave;
-        const int b = min(max(minr, 0), nrows - 1);
-        atomicAdd(&s_row[b + 1], 1);
+        atomicAdd(&s_row[min(max(minr, 0), nrows - 1) + 1], 1);
     }
     __syncthreads();
-    // exclusive scan of the bucket counts (s_row[b+1] = count of bucket b) by wave 0
-    if (wv == 0) {
+    if (wv == 0) {  // exclusive scan of the bucket counts (s_row[b+1] = count of bucket b)
         const int C = (nrows + 63) / 64;
         const int b0 = min(lane * C, nrows), b1 = min(b0 + C, nrows);
         int sum = 0;
@@ -166,41 +158,46 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
         }
     }
     __syncthreads();
-    // scatter: afterwards bucket b = s_sorted[s_row[b] .. s_row[b+1])
     for (int iR = tid; iR < nR; iR += kStereoThreads) {
-        const int minr = (int)(int16_t)(s_rband[iR] & 0xffff);
-        const int b = min(max(minr, 0), nrows - 1);
-        const int pos = atomicAdd(&s_row[b + 1], 1);
-        s_sorted[pos] = (uint16_t)iR;
+        const orbx_kp k = kR[iR];
+        const float r = __fmul_rn(2.0f, a.scale[k.octave]);
+        const int maxr = (int)ceilf(__fadd_rn(k.y, r));
+        const int minr = (int)floorf(__fsub_rn(k.y, r));
+        // a band test minr <= v <= maxr for 0 <= v < nrows is unchanged by clamping both ends to [0, nrows]
+        const int band = min(max(minr, 0), nrows) | (min(max(maxr, 0), nrows) << 16);
+        const int pos = atomicAdd(&s_row[min(max(minr, 0), nrows - 1) + 1], 1);
+        s_rec[pos] = make_float4(k.x, __int_as_float(band), __int_as_float(k.octave), __int_as_float(iR));
     }
     __syncthreads();
 
-    uint8_t* s_il = lds + o.wave + wv * kStereoWaveBytes;
-    uint8_t* s_ir = s_il + 124;
-    int* s_part = (int*)(s_ir + 232);
-    int* s_tot = s_part + 56;
-    for (int iL = wv; iL < nL; iL += kStereoWaves) {
-        const orbx_kp kpL = kL[iL];
+    uint8_t* s_il = lds + o.win + g * ((kStereoWinBytes + 15) & ~15);
+    uint8_t* s_ir = s_il + 11 * kStereoIL;
+    const int gbase = lane & ~15;
+    const int nblk = (nL + kStereoGroups - 1) / kStereoGroups;
+    for (int blk = part; blk < nblk; blk += kStereoSplit) {  // wave-uniform trip count
+        const int iL = blk * kStereoGroups + g;
+        const bool on = iL < nL;
+        orbx_kp kpL;
+        kpL.x = kpL.y = 0.f;
+        kpL.octave = 0;
+        if (on) kpL = kL[iL];
         const int levelL = kpL.octave;
         const float vL = kpL.y, uL = kpL.x;
         const int v = (int)vL;  // vRowIndices[vL] (Frame.cc:514)
-        if (!(vL >= 0.f) || v >= nrows) continue;
         const float minU = __fsub_rn(uL, a.maxD);
         const float maxU = __fsub_rn(uL, 0.0f);
-        if (maxU < 0) continue;
-        const uint4* qd = (const uint4*)(dL + (long long)iL * 32);
-        const uint4 q0 = qd[0], q1 = qd[1];
-        const int cb = s_row[max(v - a.rspan, 0)], ce = s_row[v + 1];
+        const bool search = on && vL >= 0.f && v < nrows && !(maxU < 0);
         uint32_t best = 0xffffffffu;
-        for (int c0 = cb; c0 < ce; c0 += 64) {  // Frame.cc:531-550
-            const int c = c0 + lane;
-            if (c < ce) {
-                const int iR = s_sorted[c];
-                const int band = s_rband[iR];
-                const int minr = (int)(int16_t)(band & 0xffff), maxr = band >> 16;
-                const int oct = s_roct[iR];
-                const float uR = s_rx[iR];
-                if (minr <= v && v <= maxr && oct >= levelL - 1 && oct <= levelL + 1 && uR >= minU && uR <= maxU) {
+        if (search) {  // Frame.cc:531-550: the first strict minimum over the band = the minimum of (dist, iR)
+            const uint4* qd = (const uint4*)(dL + (long long)iL * 32);
+            const uint4 q0 = qd[0], q1 = qd[1];
+            const int cb = s_row[max(v - a.rspan, 0)], ce = s_row[v + 1];
+            for (int c = cb + li; c < ce; c += 16) {
+                const float4 rc = s_rec[c];
+                const int band = __float_as_int(rc.y), oct = __float_as_int(rc.z);
+                if ((band & 0xffff) <= v && v <= (band >> 16) && oct >= levelL - 1 && oct <= levelL + 1 && rc.x >= minU &&
+                    rc.x <= maxU) {
+                    const int iR = __float_as_int(rc.w);
                     const uint4* cd = (const uint4*)(dR + (long long)iR * 32);
                     const uint4 c0v = cd[0], c1v = cd[1];
                     const int dist = __popc(q0.x ^ c0v.x) + __popc(q0.y ^ c0v.y) + __popc(q0.z ^ c0v.z) +
@@ -210,11 +207,11 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
                 }
             }
         }
-        best = wave_min_u32(best);
-        if (best == 0xffffffffu || (int)(best >> 16) >= 75) continue;  // thOrbDist (Frame.cc:475, 553)
+        best = row16_min_u32(best);
+        // sub-pixel match by correlation (Frame.cc:555-621) for best distance < thOrbDist (Frame.cc:475, 553)
+        bool corr = search && best != 0xffffffffu && (int)(best >> 16) < 75;
         const int bestIdxR = (int)(best & 0xffff);
-        // sub-pixel match by correlation (Frame.cc:555-621)
-        const float uR0 = s_rx[bestIdxR];
+        const float uR0 = corr ? kR[bestIdxR].x : 0.f;
         const float sf = a.inv_scale[levelL];
         const float suL = roundf(__fmul_rn(uL, sf));
         const float svL = roundf(__fmul_rn(vL, sf));
@@ -222,64 +219,108 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
         const float iniu = __fsub_rn(__fadd_rn(suR0, 5.0f), 5.0f);
         const float endu = __fadd_rn(__fadd_rn(__fadd_rn(suR0, 5.0f), 5.0f), 1.0f);
         const int lw = a.lw[levelL], lh = a.lh[levelL];
-        if (iniu < 0 || endu >= (float)lw) continue;
+        corr = corr && !(iniu < 0 || endu >= (float)lw);
         const int r0 = (int)__fsub_rn(svL, 5.0f), c0l = (int)__fsub_rn(suL, 5.0f), c0r = (int)__fsub_rn(suR0, 10.0f);
-        if (r0 < 0 || r0 + 11 > lh || c0l < 0 || c0l + 11 > lw || c0r < 0 || c0r + 21 > lw) {
-            if (lane == 0) atomicOr(err, 2);  // the reference's cv::Mat::colRange/rowRange would assert
-            continue;
+        if (corr && (r0 < 0 || r0 + 11 > lh || c0l < 0 || c0l + 11 > lw || c0r < 0 || c0r + 21 > lw)) {
+            if (li == 0) atomicOr(err, 2);  // the reference's cv::Mat::colRange/rowRange would assert
+            corr = false;
         }
-        int pitchL, pitchR;
-        const uint8_t* PL = level_base(a.left, a, fl, levelL, &pitchL) + (long long)r0 * pitchL + c0l;
-        const uint8_t* PR = level_base(a.right, a, fr, levelL, &pitchR) + (long long)r0 * pitchR + c0r;
-        for (int k = lane; k < 121; k += 64) s_il[k] = PL[(k / 11) * pitchL + k % 11];
-        for (int k = lane; k < 231; k += 64) s_ir[k] = PR[(k / 21) * pitchR + k % 21];
-        wave_lds_sync();
-        int part = 0;
-        if (lane < 55) {
-            const int s = lane % 11, g = lane / 11;
-            const int cL = s_il[5 * 11 + 5], cR = s_ir[5 * 21 + s + 5];
-            for (int r = g; r < 11; r += 5)
+        if (corr) {  // the 11x11 window and the 11x21 strip, one byte per load, 22 per lane in one round trip
+            int pitchL, pitchR;
+            const uint8_t* PL = level_base(a.left, a, fl, levelL, &pitchL) + (long long)r0 * pitchL + c0l;
+            const uint8_t* PR = level_base(a.right, a, fr, levelL, &pitchR) + (long long)r0 * pitchR + c0r;
 #pragma unroll
-                for (int c = 0; c < 11; c++)
-                    part += abs((s_il[r * 11 + c] - cL) - (s_ir[r * 21 + s + c] - cR));
-            s_part[lane] = part;
+            for (int k = li; k < 121 + 231; k += 16) {
+                if (k < 121) {
+                    const int rr = k / 11, cc = k - 11 * rr;
+                    s_il[rr * kStereoIL + cc] = PL[rr * pitchL + cc];
+                } else {
+                    const int k2 = k - 121, rr = k2 / 21, cc = k2 - 21 * rr;
+                    s_ir[rr * kStereoIR + cc] = PR[rr * pitchR + cc];
+                }
+            }
         }
         wave_lds_sync();
-        if (lane < 11)
-            s_tot[lane] = s_part[lane] + s_part[lane + 11] + s_part[lane + 22] + s_part[lane + 33] + s_part[lane + 44];
-        wave_lds_sync();
-        int bestS = 0x7fffffff, bi = 0;
-        for (int s = 0; s < 11; s++) {
-            const int d = s_tot[s];
-            if (d < bestS) {
-                bestS = d;
-                bi = s;
+        // lane li < 11: the L1 distance at shift incR = li - 5 (cv::norm(IL, IR, NORM_L1) of the centre-subtracted
+        // windows: integers, exact)
+        int tot = 0x7fffffff;
+        if (corr && li < 11) {
+            const int cL = s_il[5 * kStereoIL + 5], cR = s_ir[5 * kStereoIR + li + 5];
+            const int dlt = cR - cL;
+            int acc = 0;
+            for (int r = 0; r < 11; r++) {
+                const uint32_t* rl = (const uint32_t*)(s_il + r * kStereoIL);
+                const uint32_t* rr = (const uint32_t*)(s_ir + r * kStereoIR + (li & ~3));
+                const uint32_t l0 = rl[0], l1 = rl[1], l2 = rl[2];
+                const uint32_t w0 = rr[0], w1 = rr[1], w2 = rr[2], w3 = rr[3];
+                const int sh = li & 3;
+                const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
+                               x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+#pragma unroll
+                for (int c = 0; c < 11; c++) {
+                    const uint32_t lw4 = c < 4 ? l0 : c < 8 ? l1 : l2, rw4 = c < 4 ? x0 : c < 8 ? x1 : x2;
+                    const int il = (int)((lw4 >> (8 * (c & 3))) & 255u), ir = (int)((rw4 >> (8 * (c & 3))) & 255u);
+                    acc += abs(il - ir + dlt);
+                }
+            }
+            tot = acc;
+        }
+        // first strict minimum over the 11 shifts (Frame.cc:594-602) and its neighbours for the parabola
+        const uint32_t key = row16_min_u32(tot == 0x7fffffff ? 0xffffffffu : ((uint32_t)tot << 4) | (uint32_t)li);
+        const int bi = (int)(key & 15u), bestS = (int)(key >> 4);
+        const float d1 = (float)__shfl(tot, gbase + max(bi - 1, 0)), d2 = (float)bestS,
+                    d3 = (float)__shfl(tot, gbase + min(bi + 1, 10));
+        wave_lds_sync();  // this group's window is rewritten by its next keypoint
+        if (!on || li != 0) continue;
+        float u_out = -1.0f, d_out = -1.0f;
+        int s_out = -1;
+        if (corr && bi != 0 && bi != 10) {
+            const float deltaR =
+                __fdiv_rn(__fsub_rn(d1, d3), __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2))));
+            if (!(deltaR < -1 || deltaR > 1)) {
+                float bestuR = __fmul_rn(a.scale[levelL], __fadd_rn(__fadd_rn(suR0, (float)(bi - 5)), deltaR));
+                float disparity = __fsub_rn(uL, bestuR);
+                if (disparity >= 0.0f && disparity < a.maxD) {  // Frame.cc:623-633
+                    if (disparity <= 0) {
+                        disparity = 0.01f;
+                        bestuR = (float)((double)uL - 0.01);
+                    }
+                    d_out = __fdiv_rn(a.bf, disparity);
+                    u_out = bestuR;
+                    s_out = bestS;
+                }
             }
         }
-        const float d1 = (float)s_tot[max(bi - 1, 0)], d2 = (float)s_tot[bi], d3 = (float)s_tot[min(bi + 1, 10)];
-        wave_lds_sync();  // s_tot/s_il/s_ir are rewritten by this wave's next keypoint
-        if (bi == 0 || bi == 10) continue;
-        const float deltaR = __fdiv_rn(__fsub_rn(d1, d3), __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2))));
-        if (deltaR < -1 || deltaR > 1) continue;
-        float bestuR = __fmul_rn(a.scale[levelL], __fadd_rn(__fadd_rn(suR0, (float)(bi - 5)), deltaR));
-        float disparity = __fsub_rn(uL, bestuR);
-        if (disparity >= 0.0f && disparity < a.maxD) {  // Frame.cc:623-633
-            if (disparity <= 0) {
-                disparity = 0.01f;
-                bestuR = (float)((double)uL - 0.01);
-            }
-            if (lane == 0) {
-                dp[iL] = __fdiv_rn(a.bf, disparity);
-                ur[iL] = bestuR;
-                s_sad[iL] = bestS;
-            }
-        }
+        ur[iL] = u_out;  // mvuRight = mvDepth = -1 unless matched (Frame.cc:472-473)
+        dp[iL] = d_out;
+        sd[iL] = s_out;
     }
+}
+
+/* the median rejection of a pair's stereo matches (Frame.cc:636-650), one workgroup per pair after k_stereo: the
+ * n/2-th smallest SAD (sort(vDistIdx), vDistIdx[n/2]) by a two-digit radix select in LDS, thDist = 1.5f*1.4f*median,
+ * every match at or above it reset to -1; d_nstereo = the matches kept */
+__global__ __launch_bounds__(256) void k_stereo_median(const int32_t* __restrict__ fl_idx, const int32_t* __restrict__ fr_idx,
+                                                      const int32_t* __restrict__ cntL, const int32_t* __restrict__ cntR,
+                                                      int left_nframes, int right_nframes, int stride, float thc,
+                                                      float* __restrict__ uright, float* __restrict__ depth,
+                                                      const int32_t* __restrict__ sad, int32_t* __restrict__ nstereo) {
+    __shared__ int s_hist[512];
+    __shared__ int s_misc[8];
+    const int tid = threadIdx.x, p = blockIdx.x;
+    const int fl = fl_idx[p], fr = fr_idx[p];
+    if (fl < 0 || fl >= left_nframes || fr < 0 || fr >= right_nframes) return;  // k_stereo raised the error flag
+    const int nL = cntL[fl], nR = cntR[fr];
+    if (nL < 0 || nL > stride || nR < 0 || nR > stride) return;
+    float* ur = uright + (long long)p * stride;
+    float* dp = depth + (long long)p * stride;
+    const int32_t* sd = sad + (long long)p * stride;
+    for (int i = tid; i < 512; i += 256) s_hist[i] = 0;
+    if (tid < 8) s_misc[tid] = 0;
     __syncthreads();
-    // median rejection (Frame.cc:636-650): k-th smallest SAD, k = n/2, by a two-digit radix select
     int nloc = 0;
-    for (int i = tid; i < nL; i += kStereoThreads) {
-        const int d = s_sad[i];
+    for (int i = tid; i < nL; i += 256) {
+        const int d = sd[i];
         if (d >= 0) {
             nloc++;
             atomicAdd(&s_hist[d >> 8], 1);
@@ -300,8 +341,8 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
     }
     __syncthreads();
     const int hb = s_misc[1];
-    for (int i = tid; i < nL; i += kStereoThreads) {
-        const int d = s_sad[i];
+    for (int i = tid; i < nL; i += 256) {
+        const int d = sd[i];
         if (d >= 0 && (d >> 8) == hb) atomicAdd(&s_hist[256 + (d & 255)], 1);
     }
     __syncthreads();
@@ -312,10 +353,10 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
     }
     __syncthreads();
     const float median = (float)s_misc[3];
-    const float thDist = __fmul_rn(a.thc, median);
+    const float thDist = __fmul_rn(thc, median);
     int kept = 0;
-    for (int i = tid; i < nL; i += kStereoThreads) {
-        const int d = s_sad[i];
+    for (int i = tid; i < nL; i += 256) {
+        const int d = sd[i];
         if (d < 0) continue;
         if ((float)d < thDist) {
             kept++;
@@ -1059,11 +1100,13 @@ hipError_t stereo_setup(int lds_bytes) {
 
 hipError_t launch_stereo(const StereoArgs& a, int npairs, const int32_t* fl, const int32_t* fr, const orbx_kp* kpsL,
                          const uint8_t* descL, const int32_t* cntL, const orbx_kp* kpsR, const uint8_t* descR,
-                         const int32_t* cntR, int stride, float* uright, float* depth, int32_t* nstereo, int* err,
-                         hipStream_t st) {
+                         const int32_t* cntR, int stride, float* uright, float* depth, int32_t* nstereo, int32_t* sad,
+                         int* err, hipStream_t st) {
     const int lds = stereo_lds_bytes(stride, a.nrows);
-    hipLaunchKernelGGL(k_stereo, dim3(npairs), dim3(kStereoThreads), lds, st, a, fl, fr, kpsL, descL, cntL, kpsR,
-                       descR, cntR, stride, uright, depth, nstereo, err);
+    hipLaunchKernelGGL(k_stereo, dim3(npairs * kStereoSplit), dim3(kStereoThreads), lds, st, a, fl, fr, kpsL, descL, cntL,
+                       kpsR, descR, cntR, stride, uright, depth, sad, err);
+    hipLaunchKernelGGL(k_stereo_median, dim3(npairs), dim3(256), 0, st, fl, fr, cntL, cntR, a.left.nframes,
+                       a.right.nframes, stride, a.thc, uright, depth, sad, nstereo);
     return hipGetLastError();
 }
 

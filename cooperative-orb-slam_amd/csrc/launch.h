@@ -99,7 +99,7 @@ int stereo_lds_bytes(int cap, int nrows);
 hipError_t stereo_setup(int lds_bytes);
 hipError_t launch_stereo(const StereoArgs& a, int npairs, const int32_t* fl, const int32_t* fr, const orbx_kp* kpsL,
                          const uint8_t* descL, const int32_t* cntL, const orbx_kp* kpsR, const uint8_t* descR,
-                         const int32_t* cntR, int stride, float* uright, float* depth, int32_t* nstereo, int* err,
-                         hipStream_t st);
+                         const int32_t* cntR, int stride, float* uright, float* depth, int32_t* nstereo, int32_t* sad,
+                         int* err, hipStream_t st);  // sad: npairs * stride ints of scratch (k_stereo -> k_stereo_median)
 
 }  // namespace orbamd
