@@ -347,7 +347,10 @@ def main():
                          "ncclAllGather on the exchange's own HIP stream, no collective-owned stream; torch.distributed runs "
                          "the gloo control plane: unique-id broadcast, barriers, max-over-ranks timing), torch = "
                          "torch.distributed's ProcessGroupNCCL all_gather_into_tensor (its internal RCCL stream)")
-    ap.add_argument("--ingest-streams", type=int, default=4, help="copy streams of the ingest leg (<= --pipes)")
+    ap.add_argument("--ingest-streams", type=int, default=4, help="copy streams of the ingest leg")
+    ap.add_argument("--ingest-chunks", type=int, default=8,
+                    help="upload chunks per graph in the ingest leg, dealt round-robin over the copy streams (4 streams x 8 "
+                         "chunks: 53.7 GB/s of the box's 54 GB/s pinned H2D, profiles/r06c_exp_ingest.log)")
     ap.add_argument("--ingest-steps", type=int, default=100,
                     help="steps of the ingest leg (frames uploaded from pinned host memory each step; 0: skip)")
     ap.add_argument("--scene", choices=("shared", "private"), default="shared",
@@ -616,7 +619,7 @@ def main():
         if use_dist:
             dist.barrier()
         ingest = run_ingest(torch, sched, frames_np, args.pool, args.ingest_steps, B, W, H, world, use_dist, dist,
-                            reduce_max, args.ingest_streams)
+                            reduce_max, args.ingest_streams, args.ingest_chunks)
         if not args.no_check:
             chk = check_schedule(sched, frames_np, nfeatures=cfg["nfeatures"], agent_frames=agent_kf)
             ingest["bit_exact"] = bool(chk["bit_exact"])

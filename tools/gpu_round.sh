@@ -30,7 +30,7 @@ for step in "$@"; do
       tools/prof_round.sh $T || exit $?
       kt=$(find gpurun_out/${T}_kt -name '*kernel_trace.csv' | head -n 1)
       read sub pipes < <(python3 bench.py --launch-frames)
-      python3 tools/trace_segments.py "$kt" 10 2 $pipes > gpurun_out/${T}_timed_region_kernels.txt || exit $?
+      python3 tools/trace_segments.py "$kt" 10 2 $pipes 7 > gpurun_out/${T}_timed_region_kernels.txt || exit $?
       python3 tools/exchange_kernels.py "$kt" > gpurun_out/${T}_exchange_kernels.txt || exit $?
       python3 tools/queue_map.py "$kt" > gpurun_out/${T}_queue_map.txt || exit $?
       tools/prof_reduce.sh $T $sub

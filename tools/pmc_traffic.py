@@ -42,7 +42,8 @@ for st in STAGES:
     g = grids[-1]
     f = 2.0 * sum(fetch[(st, g)]) / len(fetch[(st, g)])  # calibrated: FETCH_SIZE tallies half the bytes
     w = sum(write.get((st, g), [0.0])) / max(len(write.get((st, g), [0.0])), 1)
-    out[st] = {"grid": g, "dispatches": len(fetch[(st, g)]), "fetch_KiB_avg_per_dispatch_corrected": f,
+    out[st] = {"grid": g, "dispatches": len(fetch[(st, g)]), "FETCH_SIZE_KiB_raw_avg_per_dispatch": f / 2.0,
+               "fetch_KiB_avg_per_dispatch_corrected": f,
                "WRITE_SIZE_KiB_avg_per_dispatch": w, "hbm_bytes_per_launch": (f + w) * 1024.0}
     if (st, g) in valu:
         out[st]["valu_insts_per_launch"] = sum(valu[(st, g)]) / len(valu[(st, g)])
