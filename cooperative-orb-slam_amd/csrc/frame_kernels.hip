@@ -55,17 +55,24 @@ constexpr int kStereoThreads = 256;
 constexpr int kStereoWaves = kStereoThreads / 64;
 constexpr int kStereoGroups = kStereoThreads / 16;  // left keypoints in flight per workgroup
 constexpr int kStereoSplit = 4;                     // workgroups per pair
-constexpr int kStereoIL = 12, kStereoIR = 24;       // LDS row pitch of the 11x11 window / the 11x21 strip
-constexpr int kStereoWinBytes = 11 * kStereoIL + 11 * kStereoIR + 4;  // + 4: IR's last dword read past column 23
+/* the correlation windows of one keypoint in LDS, as whole dwords from the dword that holds their first column: the
+ * 11x11 IL window as 11 rows x 4 dwords (columns (c0l & ~3) .. +15), the 11x21 IR strip as 11 rows x 6 dwords
+ * ((c0r & ~3) .. +23): 110 dwords, dword t of group g at (64 (t >> 4) + 16 g + (t & 15)) of its wave's area, which is
+ * exactly where 7 LDS-DMA rounds of the wave's 64 lanes (lane 16 g + j carries t = 16 q + j) put them */
+constexpr int kStereoILd = 4, kStereoIRd = 6;
+constexpr int kStereoStageQ = (11 * (kStereoILd + kStereoIRd) + 15) / 16;  // 7 rounds
+constexpr int kStereoWaveStage = kStereoStageQ * 64 * 4;                   // bytes per wave
 
 /* dynamic LDS layout of k_stereo for kp capacity `cap` and `nrows` level-0 rows */
 struct StereoLds {
-    int rec, row, win, total;
+    int rec, idx, row, stage, total;
     __host__ __device__ StereoLds(int cap, int nrows) {
-        rec = 0;                                            // one float4 per right keypoint, in bucket order
-        row = rec + 16 * ((cap + 3) & ~3);                  // bucket offsets (nrows + 2)
-        win = row + 4 * ((nrows + 2 + 3) & ~3);             // per 16-lane group: IL (11 x 12) | IR (11 x 24)
-        total = win + kStereoGroups * ((kStereoWinBytes + 15) & ~15);
+        const int c4 = (cap + 3) & ~3;
+        rec = 0;                                  // per right keypoint in bucket order: {uR, minr | maxr << 12 | oct << 24}
+        idx = rec + 8 * c4;                       // its index iR (u16)
+        row = idx + ((2 * c4 + 15) & ~15);        // bucket offsets (nrows + 2)
+        stage = row + ((4 * (nrows + 2) + 15) & ~15);
+        total = stage + kStereoWaves * kStereoWaveStage;
     }
 };
 
@@ -94,6 +101,20 @@ __device__ __forceinline__ const uint8_t* level_base(const PyrSide& s, const Ste
     return s.pyr + (long long)f * s.pyr_fstride + a.pyr_off[l];
 }
 
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+/* sum over 4 pixel pairs of |a - b + d| (bytes of a and b; d in each 16-bit half of d2), as two u16 partial sums:
+ * bytes 0, 2 and 1, 3 of each word spread into 16-bit lanes by v_perm; keep3 drops byte 3 (the 12th column) */
+__device__ __forceinline__ short2v sad4(uint32_t a, uint32_t b, short2v d2, short2v acc, bool keep3) {
+    const uint32_t alo = __builtin_amdgcn_perm(0u, a, 0x0c020c00u), ahi = __builtin_amdgcn_perm(0u, a, 0x0c030c01u);
+    const uint32_t blo = __builtin_amdgcn_perm(0u, b, 0x0c020c00u), bhi = __builtin_amdgcn_perm(0u, b, 0x0c030c01u);
+    short2v xlo = __builtin_bit_cast(short2v, alo) - __builtin_bit_cast(short2v, blo) + d2;
+    short2v xhi = __builtin_bit_cast(short2v, ahi) - __builtin_bit_cast(short2v, bhi) + d2;
+    if (!keep3) xhi = (short2v){xhi.x, 0};
+    return acc + __builtin_elementwise_max(xlo, -xlo) + __builtin_elementwise_max(xhi, -xhi);
+}
+
+template <bool kDwordRows>
 __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const int32_t* __restrict__ fl_idx,
                                                            const int32_t* __restrict__ fr_idx,
                                                            const orbx_kp* __restrict__ kpsL,
@@ -106,7 +127,8 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
                                                            int32_t* __restrict__ sad, int* __restrict__ err) {
     extern __shared__ __align__(16) uint8_t lds[];
     const StereoLds o(stride, a.nrows);
-    float4* s_rec = (float4*)(lds + o.rec);  // {uR, band (minr | maxr << 16, clamped to the rows), octave, iR}
+    uint2* s_rec = (uint2*)(lds + o.rec);
+    uint16_t* s_idx = (uint16_t*)(lds + o.idx);
     int* s_row = (int*)(lds + o.row);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = tid >> 4, li = tid & 15;
     const int p = blockIdx.x / kStereoSplit, part = blockIdx.x % kStereoSplit;
@@ -163,15 +185,19 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
         const float r = __fmul_rn(2.0f, a.scale[k.octave]);
         const int maxr = (int)ceilf(__fadd_rn(k.y, r));
         const int minr = (int)floorf(__fsub_rn(k.y, r));
-        // a band test minr <= v <= maxr for 0 <= v < nrows is unchanged by clamping both ends to [0, nrows]
-        const int band = min(max(minr, 0), nrows) | (min(max(maxr, 0), nrows) << 16);
+        // a band test minr <= v <= maxr for 0 <= v < nrows (< 4096) is unchanged by clamping both ends to [0, nrows]
+        const uint32_t band = (uint32_t)min(max(minr, 0), nrows) | ((uint32_t)min(max(maxr, 0), nrows) << 12) |
+                              ((uint32_t)k.octave << 24);
         const int pos = atomicAdd(&s_row[min(max(minr, 0), nrows - 1) + 1], 1);
-        s_rec[pos] = make_float4(k.x, __int_as_float(band), __int_as_float(k.octave), __int_as_float(iR));
+        s_rec[pos] = make_uint2(__float_as_uint(k.x), band);
+        s_idx[pos] = (uint16_t)iR;
     }
     __syncthreads();
 
-    uint8_t* s_il = lds + o.win + g * ((kStereoWinBytes + 15) & ~15);
-    uint8_t* s_ir = s_il + 11 * kStereoIL;
+    uint8_t* stage = lds + o.stage + wv * kStereoWaveStage;
+    const uint32_t* sg = (const uint32_t*)stage + 16 * (g & 3);  // this group's dwords: sg[64 (t >> 4) + (t & 15)]
+    auto sdw = [&](int t) { return sg[64 * (t >> 4) + (t & 15)]; };
+    auto sbyte = [&](int t, int b) { return (int)((const uint8_t*)sg)[4 * (64 * (t >> 4) + (t & 15)) + b]; };
     const int gbase = lane & ~15;
     const int nblk = (nL + kStereoGroups - 1) / kStereoGroups;
     for (int blk = part; blk < nblk; blk += kStereoSplit) {  // wave-uniform trip count
@@ -193,11 +219,11 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
             const uint4 q0 = qd[0], q1 = qd[1];
             const int cb = s_row[max(v - a.rspan, 0)], ce = s_row[v + 1];
             for (int c = cb + li; c < ce; c += 16) {
-                const float4 rc = s_rec[c];
-                const int band = __float_as_int(rc.y), oct = __float_as_int(rc.z);
-                if ((band & 0xffff) <= v && v <= (band >> 16) && oct >= levelL - 1 && oct <= levelL + 1 && rc.x >= minU &&
-                    rc.x <= maxU) {
-                    const int iR = __float_as_int(rc.w);
+                const uint2 rc = s_rec[c];
+                const int minr = (int)(rc.y & 0xfffu), maxr = (int)((rc.y >> 12) & 0xfffu), oct = (int)(rc.y >> 24);
+                const float uR = __uint_as_float(rc.x);
+                if (minr <= v && v <= maxr && oct >= levelL - 1 && oct <= levelL + 1 && uR >= minU && uR <= maxU) {
+                    const int iR = s_idx[c];
                     const uint4* cd = (const uint4*)(dR + (long long)iR * 32);
                     const uint4 c0v = cd[0], c1v = cd[1];
                     const int dist = __popc(q0.x ^ c0v.x) + __popc(q0.y ^ c0v.y) + __popc(q0.z ^ c0v.z) +
@@ -225,50 +251,70 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
             if (li == 0) atomicOr(err, 2);  // the reference's cv::Mat::colRange/rowRange would assert
             corr = false;
         }
-        if (corr) {  // the 11x11 window and the 11x21 strip, one byte per load, 22 per lane in one round trip
-            int pitchL, pitchR;
-            const uint8_t* PL = level_base(a.left, a, fl, levelL, &pitchL) + (long long)r0 * pitchL + c0l;
-            const uint8_t* PR = level_base(a.right, a, fr, levelL, &pitchR) + (long long)r0 * pitchR + c0r;
+        int pitchL = 0, pitchR = 0;
+        const uint8_t* PL = level_base(a.left, a, fl, levelL, &pitchL) + (long long)r0 * pitchL;
+        const uint8_t* PR = level_base(a.right, a, fr, levelL, &pitchR) + (long long)r0 * pitchR;
+        if (kDwordRows) {
+            // every row 4-aligned: 7 LDS-DMA rounds per wave, lane (g, j) carrying dword t = 16 q + j of its keypoint;
+            // a dword past the level's last one is clamped to it (its bytes lie past column lw - 1: never read)
+            const int lastd = (lw - 1) & ~3;
+            const bool any = __ballot(corr) != 0;  // wave-uniform: a wave with no window to stage issues nothing
+            // lanes without a window load a valid dummy (their keypoint array); r0 / c0 of such a lane are arbitrary
+            const uint8_t* dummy = (const uint8_t*)kL;
 #pragma unroll
-            for (int k = li; k < 121 + 231; k += 16) {
-                if (k < 121) {
-                    const int rr = k / 11, cc = k - 11 * rr;
-                    s_il[rr * kStereoIL + cc] = PL[rr * pitchL + cc];
-                } else {
-                    const int k2 = k - 121, rr = k2 / 21, cc = k2 - 21 * rr;
-                    s_ir[rr * kStereoIR + cc] = PR[rr * pitchR + cc];
-                }
+            for (int q = 0; q < kStereoStageQ; q++) {
+                const int t = 16 * q + li;
+                const bool il = t < 11 * kStereoILd;
+                const int tt = il ? t : t - 11 * kStereoILd;
+                const int rr = il ? tt >> 2 : tt / kStereoIRd, dd = il ? tt & 3 : tt - kStereoIRd * rr;
+                const int col = min(((il ? c0l : c0r) & ~3) + 4 * dd, lastd);
+                const uint8_t* src = (il ? PL + rr * pitchL : PR + min(rr, 10) * pitchR) + col;
+                if (any)
+                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(corr ? src : dummy),
+                                                     (__attribute__((address_space(3))) void*)(stage + 256 * q), 4, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (corr) {  // unaligned rows (a packed odd-width level 0): the same layout a byte at a time
+            for (int k = li; k < 11 * 4 * (kStereoILd + kStereoIRd); k += 16) {
+                const bool il = k < 11 * 4 * kStereoILd;
+                const int kk = il ? k : k - 11 * 4 * kStereoILd;
+                const int rr = il ? kk >> 4 : kk / (4 * kStereoIRd), bb = il ? kk & 15 : kk - 4 * kStereoIRd * rr;
+                const int col = min(((il ? c0l : c0r) & ~3) + bb, lw - 1);
+                const int t = il ? 4 * rr + (bb >> 2) : 11 * kStereoILd + kStereoIRd * rr + (bb >> 2);
+                ((uint8_t*)sg)[4 * (64 * (t >> 4) + (t & 15)) + (bb & 3)] =
+                    il ? PL[rr * pitchL + col] : PR[rr * pitchR + col];
             }
         }
         wave_lds_sync();
         // lane li < 11: the L1 distance at shift incR = li - 5 (cv::norm(IL, IR, NORM_L1) of the centre-subtracted
-        // windows: integers, exact)
+        // windows: |IL - IR + (cR - cL)| summed, integers, exact)
         int tot = 0x7fffffff;
         if (corr && li < 11) {
-            const int cL = s_il[5 * kStereoIL + 5], cR = s_ir[5 * kStereoIR + li + 5];
-            const int dlt = cR - cL;
-            int acc = 0;
+            const int shl = c0l & 3, orr = (c0r & 3) + li;
+            const int cL = sbyte(4 * 5 + ((shl + 5) >> 2), (shl + 5) & 3);
+            const int oc = orr + 5;
+            const int cR = sbyte(11 * kStereoILd + kStereoIRd * 5 + (oc >> 2), oc & 3);
+            const short2v d2 = (short2v){(short)(cR - cL), (short)(cR - cL)};
+            short2v acc = (short2v){0, 0};
+            const int shr = orr & 3;
             for (int r = 0; r < 11; r++) {
-                const uint32_t* rl = (const uint32_t*)(s_il + r * kStereoIL);
-                const uint32_t* rr = (const uint32_t*)(s_ir + r * kStereoIR + (li & ~3));
-                const uint32_t l0 = rl[0], l1 = rl[1], l2 = rl[2];
-                const uint32_t w0 = rr[0], w1 = rr[1], w2 = rr[2], w3 = rr[3];
-                const int sh = li & 3;
-                const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
-                               x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-#pragma unroll
-                for (int c = 0; c < 11; c++) {
-                    const uint32_t lw4 = c < 4 ? l0 : c < 8 ? l1 : l2, rw4 = c < 4 ? x0 : c < 8 ? x1 : x2;
-                    const int il = (int)((lw4 >> (8 * (c & 3))) & 255u), ir = (int)((rw4 >> (8 * (c & 3))) & 255u);
-                    acc += abs(il - ir + dlt);
-                }
+                const uint4 lw4 = *(const uint4*)(sg + 64 * (r >> 2) + 4 * (r & 3));  // IL dwords 4r .. 4r+3
+                const int t0 = 11 * kStereoILd + kStereoIRd * r + (orr >> 2);
+                const uint32_t w0 = sdw(t0), w1 = sdw(t0 + 1), w2 = sdw(t0 + 2), w3 = sdw(t0 + 3);
+                const uint32_t l0 = __builtin_amdgcn_alignbyte(lw4.y, lw4.x, shl), l1 = __builtin_amdgcn_alignbyte(lw4.z, lw4.y, shl),
+                               l2 = __builtin_amdgcn_alignbyte(lw4.w, lw4.z, shl);
+                const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, shr), x1 = __builtin_amdgcn_alignbyte(w2, w1, shr),
+                               x2 = __builtin_amdgcn_alignbyte(w3, w2, shr);
+                acc = sad4(l0, x0, d2, acc, true);
+                acc = sad4(l1, x1, d2, acc, true);
+                acc = sad4(l2, x2, d2, acc, false);
             }
-            tot = acc;
+            tot = (int)(uint16_t)acc.x + (int)(uint16_t)acc.y;
         }
         // first strict minimum over the 11 shifts (Frame.cc:594-602) and its neighbours for the parabola
         const uint32_t key = row16_min_u32(tot == 0x7fffffff ? 0xffffffffu : ((uint32_t)tot << 4) | (uint32_t)li);
         const int bi = (int)(key & 15u), bestS = (int)(key >> 4);
-        const float d1 = (float)__shfl(tot, gbase + max(bi - 1, 0)), d2 = (float)bestS,
+        const float d1 = (float)__shfl(tot, gbase + max(bi - 1, 0)), d2f = (float)bestS,
                     d3 = (float)__shfl(tot, gbase + min(bi + 1, 10));
         wave_lds_sync();  // this group's window is rewritten by its next keypoint
         if (!on || li != 0) continue;
@@ -276,7 +322,7 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
         int s_out = -1;
         if (corr && bi != 0 && bi != 10) {
             const float deltaR =
-                __fdiv_rn(__fsub_rn(d1, d3), __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2))));
+                __fdiv_rn(__fsub_rn(d1, d3), __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2f))));
             if (!(deltaR < -1 || deltaR > 1)) {
                 float bestuR = __fmul_rn(a.scale[levelL], __fadd_rn(__fadd_rn(suR0, (float)(bi - 5)), deltaR));
                 float disparity = __fsub_rn(uL, bestuR);
@@ -1095,7 +1141,9 @@ hipError_t launch_distinctive(int npoints, const int32_t* off, const uint8_t* de
 int stereo_lds_bytes(int cap, int nrows) { return StereoLds(cap, nrows).total; }
 
 hipError_t stereo_setup(int lds_bytes) {
-    return hipFuncSetAttribute((const void*)k_stereo, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    hipError_t e = hipFuncSetAttribute((const void*)k_stereo<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)k_stereo<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
 hipError_t launch_stereo(const StereoArgs& a, int npairs, const int32_t* fl, const int32_t* fr, const orbx_kp* kpsL,
@@ -1103,8 +1151,16 @@ hipError_t launch_stereo(const StereoArgs& a, int npairs, const int32_t* fl, con
                          const int32_t* cntR, int stride, float* uright, float* depth, int32_t* nstereo, int32_t* sad,
                          int* err, hipStream_t st) {
     const int lds = stereo_lds_bytes(stride, a.nrows);
-    hipLaunchKernelGGL(k_stereo, dim3(npairs * kStereoSplit), dim3(kStereoThreads), lds, st, a, fl, fr, kpsL, descL, cntL,
-                       kpsR, descR, cntR, stride, uright, depth, sad, err);
+    // level-0 rows of both sides 4-byte aligned (the pyramid levels always are): the windows are staged as dwords
+    auto rows_aligned = [](const PyrSide& s) {
+        return (((uintptr_t)s.l0 | (uintptr_t)s.l0_fstride | (uintptr_t)s.l0_pitch) & 3) == 0;
+    };
+    if (rows_aligned(a.left) && rows_aligned(a.right))
+        hipLaunchKernelGGL(k_stereo<true>, dim3(npairs * kStereoSplit), dim3(kStereoThreads), lds, st, a, fl, fr, kpsL,
+                           descL, cntL, kpsR, descR, cntR, stride, uright, depth, sad, err);
+    else
+        hipLaunchKernelGGL(k_stereo<false>, dim3(npairs * kStereoSplit), dim3(kStereoThreads), lds, st, a, fl, fr, kpsL,
+                           descL, cntL, kpsR, descR, cntR, stride, uright, depth, sad, err);
     hipLaunchKernelGGL(k_stereo_median, dim3(npairs), dim3(256), 0, st, fl, fr, cntL, cntR, a.left.nframes,
                        a.right.nframes, stride, a.thc, uright, depth, sad, nstereo);
     return hipGetLastError();

@@ -314,3 +314,51 @@ def test_per_call_matchers_large_frames(W, H, nf, shift):
                 assert ng == no and (mp_frac < 0.5 or no > 0)
                 np.testing.assert_array_equal(mg, mo)
             m.close()
+
+
+@pytest.mark.parametrize("W,H,nf", CONFIGS[:3])
+@pytest.mark.parametrize("only_stereo,check_ori", [(0, False), (1, False), (0, True)])
+def test_triangulation_bf_stereo_batch(W, H, nf, only_stereo, check_ori):
+    """orbm_triangulation_bf_stereo_batch_device (k_tri_mfma<true>): SearchForTriangulation's stereo branch
+    (ORBmatcher.cc:703-749) over a device batch of frame pairs whose keypoints are a mix of stereo (mvuRight >= 0) and
+    monocular ones: the epipole test only between two monocular keypoints, bOnlyStereo skipping monocular ones on
+    either side, with and without the rotation filter; every pair's row against the oracle"""
+    import ctypes as C
+    torch = pytest.importorskip("torch")
+    B = 4
+    frames = orbamd.synth_frames(3, 5, B, W, H)
+    pipe = orbamd.device.BatchPipeline(torch, W, H, B, nfeatures=nf, check_ori=check_ori)
+    pipe.extract(torch.from_numpy(frames).cuda())
+    S = pipe.stride
+    rng = np.random.default_rng(W + nf + only_stereo)
+    # mvuRight: about 60 % stereo (a plausible disparity), the rest -1; near-epipole keypoints included by the geometry
+    ur = np.full((B, S), -1.0, np.float32)
+    counts = pipe.counts.cpu().numpy()
+    kps = [pipe.host_keypoints(b)[0] for b in range(B)]
+    for b in range(B):
+        n = int(counts[b])
+        st = rng.random(n) < 0.6
+        ur[b, :n] = np.where(st, kps[b]["x"] - rng.uniform(1, 40, n).astype(np.float32), -1.0).astype(np.float32)
+    d_ur = torch.from_numpy(ur).cuda()
+    lib = orbamd.load()
+    F = np.ascontiguousarray(pipe.F12.reshape(9))
+    rc = lib.orbm_triangulation_bf_stereo_batch_device(
+        pipe.mh, B, pipe.q1.data_ptr(), pipe.q2.data_ptr(), pipe.kps.data_ptr(), pipe.desc.data_ptr(),
+        pipe.counts.data_ptr(), d_ur.data_ptr(), S, F.ctypes.data, pipe.ex, pipe.ey, len(pipe.scale),
+        pipe.scale.ctypes.data, pipe.sigma2.ctypes.data, only_stereo, int(check_ori), pipe.match.data_ptr(),
+        pipe.nmatch.data_ptr(), C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    tabs = oracle_py.OracleExtractor(nf, 1.2, 8, 20, 7).tables()
+    for b in range(B):
+        b2 = (b - 1) % B
+        n1 = int(counts[b])
+        k1, d1 = pipe.host_keypoints(b)
+        k2, d2 = pipe.host_keypoints(b2)
+        v1 = _view(k1, d1, tabs, uright=ur[b, :n1])
+        v2 = _view(k2, d2, tabs, uright=ur[b2, :len(k2)])
+        no, mo = oracle_py.search_for_triangulation(v1, v2, pipe.F12, pipe.ex, pipe.ey, bool(only_stereo), check_ori)
+        mg = pipe.match[b, :n1].cpu().numpy()
+        np.testing.assert_array_equal(mg, mo, err_msg="pair %d" % b)
+        assert int(pipe.nmatch[b].item()) == no and no > 0
+    pipe.close()
