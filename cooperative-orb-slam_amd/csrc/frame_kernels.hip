@@ -193,6 +193,9 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
         s_idx[pos] = (uint16_t)iR;
     }
     __syncthreads();
+#if defined(ORBX_STEREO_STOP) && ORBX_STEREO_STOP == 1  // phase cut (A/B timing only): the bucket table alone
+    return;
+#endif
 
     uint8_t* stage = lds + o.stage + wv * kStereoWaveStage;
     const uint32_t* sg = (const uint32_t*)stage + 16 * (g & 3);  // this group's dwords: sg[64 (t >> 4) + (t & 15)]
@@ -214,30 +217,62 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
         const float maxU = __fsub_rn(uL, 0.0f);
         const bool search = on && vL >= 0.f && v < nrows && !(maxU < 0);
         uint32_t best = 0xffffffffu;
+        float bestU = 0.f;  // uR of this lane's best candidate (the winner's is shuffled to the group below)
         if (search) {  // Frame.cc:531-550: the first strict minimum over the band = the minimum of (dist, iR)
             const uint4* qd = (const uint4*)(dL + (long long)iL * 32);
             const uint4 q0 = qd[0], q1 = qd[1];
             const int cb = s_row[max(v - a.rspan, 0)], ce = s_row[v + 1];
-            for (int c = cb + li; c < ce; c += 16) {
-                const uint2 rc = s_rec[c];
-                const int minr = (int)(rc.y & 0xfffu), maxr = (int)((rc.y >> 12) & 0xfffu), oct = (int)(rc.y >> 24);
-                const float uR = __uint_as_float(rc.x);
-                if (minr <= v && v <= maxr && oct >= levelL - 1 && oct <= levelL + 1 && uR >= minU && uR <= maxU) {
-                    const int iR = s_idx[c];
-                    const uint4* cd = (const uint4*)(dR + (long long)iR * 32);
-                    const uint4 c0v = cd[0], c1v = cd[1];
-                    const int dist = __popc(q0.x ^ c0v.x) + __popc(q0.y ^ c0v.y) + __popc(q0.z ^ c0v.z) +
-                                     __popc(q0.w ^ c0v.w) + __popc(q1.x ^ c1v.x) + __popc(q1.y ^ c1v.y) +
-                                     __popc(q1.z ^ c1v.z) + __popc(q1.w ^ c1v.w);
-                    if (dist < 100) best = min(best, ((uint32_t)dist << 16) | (uint32_t)iR);  // TH_HIGH
+            // 4 candidates per lane per round: their records, then all 8 descriptor loads in flight together (a
+            // candidate that fails the tests, or past the bucket range, loads row 0 and is ignored), one memory round
+            // trip per 64 candidates instead of one per 16
+            for (int c0 = cb; c0 < ce; c0 += 64) {
+                uint2 rc[4];
+                int ir[4];
+                bool ok[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int c = c0 + 16 * k + li;
+                    const bool in = c < ce;
+                    rc[k] = s_rec[in ? c : cb];
+                    ir[k] = s_idx[in ? c : cb];
+                    const int minr = (int)(rc[k].y & 0xfffu), maxr = (int)((rc[k].y >> 12) & 0xfffu),
+                              oct = (int)(rc[k].y >> 24);
+                    const float uR = __uint_as_float(rc[k].x);
+                    ok[k] = in && minr <= v && v <= maxr && oct >= levelL - 1 && oct <= levelL + 1 && uR >= minU &&
+                            uR <= maxU;
+                }
+                uint4 cv0[4], cv1[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint4* cd = (const uint4*)(dR + (long long)(ok[k] ? ir[k] : 0) * 32);
+                    cv0[k] = cd[0];
+                    cv1[k] = cd[1];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int dist = __popc(q0.x ^ cv0[k].x) + __popc(q0.y ^ cv0[k].y) + __popc(q0.z ^ cv0[k].z) +
+                                     __popc(q0.w ^ cv0[k].w) + __popc(q1.x ^ cv1[k].x) + __popc(q1.y ^ cv1[k].y) +
+                                     __popc(q1.z ^ cv1[k].z) + __popc(q1.w ^ cv1[k].w);
+                    const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)ir[k];
+                    if (ok[k] && dist < 100 && key < best) {  // TH_HIGH
+                        best = key;
+                        bestU = __uint_as_float(rc[k].x);
+                    }
                 }
             }
         }
+        const uint32_t mine = best;
         best = row16_min_u32(best);
         // sub-pixel match by correlation (Frame.cc:555-621) for best distance < thOrbDist (Frame.cc:475, 553)
         bool corr = search && best != 0xffffffffu && (int)(best >> 16) < 75;
-        const int bestIdxR = (int)(best & 0xffff);
-        const float uR0 = corr ? kR[bestIdxR].x : 0.f;
+#if defined(ORBX_STEREO_STOP) && ORBX_STEREO_STOP == 2  // phase cut (A/B timing only): no correlation
+        corr = false;
+#endif
+        // the winner's uR from the lane that holds it (keys are unique: iR is in the key)
+        const unsigned long long wm = __ballot(mine == best && best != 0xffffffffu) & (0xFFFFull << gbase);
+        const int wl = wm ? (int)__builtin_ctzll(wm) : lane;
+        const float wU = __shfl(bestU, wl);  // every lane takes part (the winner lane is active here)
+        const float uR0 = corr ? wU : 0.f;
         const float sf = a.inv_scale[levelL];
         const float suL = roundf(__fmul_rn(uL, sf));
         const float svL = roundf(__fmul_rn(vL, sf));
