@@ -756,38 +756,14 @@ __device__ __forceinline__ void fast_cells_body(
     if (lane == 0) cellcnt[(long long)f * ep.ncells + ci] = total;
 }
 
-/* XCD-aware grid of k_fast_cells2 (ORBX_FAST_XCD_CHUNK = C > 0): workgroups are dispatched to the 8 XCDs round-robin
- * (block b on XCD b % 8), so the default 2-D grid puts neighbouring cell groups (whose ROIs overlap by 6 px + the FAST
- * border) on different XCDs, each fetching the shared lines into its own L2. The 1-D grid maps block b = 8 (C m + i) + x
- * (XCD x, its k-th block, k = C m + i) to chunk j = 8 m + x, group C (j % (Gp / C)) + i of frame j / (Gp / C): C
- * consecutive groups (a level-0 cell row at C = 5) run on one XCD, and consecutive chunks on consecutive XCDs at the
- * same time, so the frame is still swept in raster order by all XCDs together. Gp = the groups per frame rounded up to
- * a multiple of C; chunks past the frames' (padding to a multiple of 8) and padded groups exit. */
-#ifndef ORBX_FAST_XCD_CHUNK
-#define ORBX_FAST_XCD_CHUNK 0
-#endif
-constexpr int kFastXcdChunk = ORBX_FAST_XCD_CHUNK;
-constexpr int kFastXcdC = kFastXcdChunk > 0 ? kFastXcdChunk : 1;  // the divisor (the mapping is off at 0)
-
 template <int kMaxPass, int kRP>
 __global__ __launch_bounds__(64 * kFastWaves) void k_fast_cells2(
     const uint8_t* __restrict__ frames, long long fstride, int pitch0, const uint8_t* __restrict__ pyr,
     ExtractParams ep, const LevelDesc* __restrict__ levels, const CellDesc* __restrict__ cells,
-    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi, int nframes) {
+    uint32_t* __restrict__ cellkey, int* __restrict__ cellcnt, int RP_, int RH, int cell_lo, int cell_hi) {
     extern __shared__ __align__(16) uint8_t lds[];
-    int bx = blockIdx.x, f = blockIdx.y;
-    if (kFastXcdChunk > 0) {
-        const int G = (cell_hi - cell_lo + kFastWaves - 1) / kFastWaves;
-        const int Gp = (G + kFastXcdC - 1) / kFastXcdC * kFastXcdC;
-        const int b = blockIdx.x, x = b & 7, k = b >> 3;
-        const int j = 8 * (k / kFastXcdC) + x, i = k % kFastXcdC;
-        const int cpf = Gp / kFastXcdC;  // chunks per frame
-        f = j / cpf;
-        bx = (j % cpf) * kFastXcdC + i;
-        if (f >= nframes || bx >= G) return;  // padding
-    }
     fast_cells_body<kMaxPass, kRP>(frames, fstride, pitch0, pyr, ep, levels, cells, cellkey, cellcnt, RP_, RH, cell_lo,
-                                   cell_hi, bx, f, lds, kFastWaves);
+                                   cell_hi, blockIdx.x, blockIdx.y, lds, kFastWaves);
 }
 
 /* ----------------------------------------------------------------------------------- */
@@ -2208,15 +2184,10 @@ hipError_t launch_fast_cells2(const uint8_t* frames, long long fstride, int pitc
                               int cell_hi, int nframes, hipStream_t st) {
     if (cell_hi <= cell_lo) return hipSuccess;
     dim3 grid((cell_hi - cell_lo + kFastWaves - 1) / kFastWaves, nframes);
-    if (kFastXcdChunk > 0) {  // 1-D XCD-aware grid (see k_fast_cells2)
-        const long long Gp = (grid.x + kFastXcdC - 1) / kFastXcdC * kFastXcdC;
-        const long long nchunks = ((long long)nframes * (Gp / kFastXcdC) + 7) / 8 * 8;
-        grid = dim3((unsigned)(nchunks * kFastXcdC), 1);
-    }
     const size_t lds = kFastWaves * (size_t)fast_wave_lds(RP, RH);
 #define ORBX_FAST(MP, RPC)                                                                                        \
     hipLaunchKernelGGL((k_fast_cells2<MP, RPC>), grid, dim3(64 * kFastWaves), lds, st, frames, fstride, pitch0, pyr, ep, levels, \
-                       cells, cellkey, cellcnt, RP, RH, cell_lo, cell_hi, nframes)
+                       cells, cellkey, cellcnt, RP, RH, cell_lo, cell_hi)
     if (max_pass <= 8 && RP == 40)
         ORBX_FAST(8, 40);
     else if (max_pass <= 8 && RP == 44)

@@ -57,11 +57,18 @@ constexpr int kStereoGroups = kStereoThreads / 16;  // left keypoints in flight 
 constexpr int kStereoSplit = 4;                     // workgroups per pair
 /* the correlation windows of one keypoint in LDS, as whole dwords from the dword that holds their first column: the
  * 11x11 IL window as 11 rows x 4 dwords (columns (c0l & ~3) .. +15), the 11x21 IR strip as 11 rows x 6 dwords
- * ((c0r & ~3) .. +23): 110 dwords, dword t of group g at (64 (t >> 4) + 16 g + (t & 15)) of its wave's area, which is
- * exactly where 7 LDS-DMA rounds of the wave's 64 lanes (lane 16 g + j carries t = 16 q + j) put them */
-constexpr int kStereoILd = 4, kStereoIRd = 6;
-constexpr int kStereoStageQ = (11 * (kStereoILd + kStereoIRd) + 15) / 16;  // 7 rounds
-constexpr int kStereoWaveStage = kStereoStageQ * 64 * 4;                   // bytes per wave
+ * ((c0r & ~3) .. +23). An LDS-DMA round q of a wave writes its 64 lanes' dwords to 64 consecutive LDS dwords, so
+ * group g (lanes 16 g .. 16 g + 15) owns the 16-dword block q of every round: 7 blocks of 16 dwords, and each row is
+ * kept whole inside one block so the SAD reads it at constant offsets: block q < 5 = IL row q | IR row 2q | IR row 2q+1
+ * (4 + 6 + 6 dwords), block 5 = IL rows 5..8, block 6 = IL rows 9, 10 | IR row 10 */
+constexpr int kStereoStageQ = 7;
+constexpr int kStereoWaveStage = kStereoStageQ * 64 * 4 + 16;  // bytes per wave (+16: the IR over-read of group 3)
+__host__ __device__ constexpr int il_dw(int r) {  // block-local dword index of IL row r (block q * 64 + offset)
+    return r < 5 ? 64 * r : r < 9 ? 64 * 5 + 4 * (r - 5) : 64 * 6 + 4 * (r - 9);
+}
+__host__ __device__ constexpr int ir_dw(int r) {
+    return r < 10 ? 64 * (r >> 1) + ((r & 1) ? 10 : 4) : 64 * 6 + 8;
+}
 
 /* dynamic LDS layout of k_stereo for kp capacity `cap` and `nrows` level-0 rows */
 struct StereoLds {
@@ -193,14 +200,9 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
         s_idx[pos] = (uint16_t)iR;
     }
     __syncthreads();
-#if defined(ORBX_STEREO_STOP) && ORBX_STEREO_STOP == 1  // phase cut (A/B timing only): the bucket table alone
-    return;
-#endif
 
     uint8_t* stage = lds + o.stage + wv * kStereoWaveStage;
-    const uint32_t* sg = (const uint32_t*)stage + 16 * (g & 3);  // this group's dwords: sg[64 (t >> 4) + (t & 15)]
-    auto sdw = [&](int t) { return sg[64 * (t >> 4) + (t & 15)]; };
-    auto sbyte = [&](int t, int b) { return (int)((const uint8_t*)sg)[4 * (64 * (t >> 4) + (t & 15)) + b]; };
+    const uint32_t* sg = (const uint32_t*)stage + 16 * (g & 3);  // this group's blocks: sg[64 q + 0..15]
     const int gbase = lane & ~15;
     const int nblk = (nL + kStereoGroups - 1) / kStereoGroups;
     for (int blk = part; blk < nblk; blk += kStereoSplit) {  // wave-uniform trip count
@@ -265,9 +267,6 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
         best = row16_min_u32(best);
         // sub-pixel match by correlation (Frame.cc:555-621) for best distance < thOrbDist (Frame.cc:475, 553)
         bool corr = search && best != 0xffffffffu && (int)(best >> 16) < 75;
-#if defined(ORBX_STEREO_STOP) && ORBX_STEREO_STOP == 2  // phase cut (A/B timing only): no correlation
-        corr = false;
-#endif
         // the winner's uR from the lane that holds it (keys are unique: iR is in the key)
         const unsigned long long wm = __ballot(mine == best && best != 0xffffffffu) & (0xFFFFull << gbase);
         const int wl = wm ? (int)__builtin_ctzll(wm) : lane;
@@ -290,52 +289,64 @@ __global__ __launch_bounds__(kStereoThreads) void k_stereo(StereoArgs a, const i
         const uint8_t* PL = level_base(a.left, a, fl, levelL, &pitchL) + (long long)r0 * pitchL;
         const uint8_t* PR = level_base(a.right, a, fr, levelL, &pitchR) + (long long)r0 * pitchR;
         if (kDwordRows) {
-            // every row 4-aligned: 7 LDS-DMA rounds per wave, lane (g, j) carrying dword t = 16 q + j of its keypoint;
-            // a dword past the level's last one is clamped to it (its bytes lie past column lw - 1: never read)
+            // every row 4-aligned: 7 LDS-DMA rounds per wave, lane j of a group carrying the dword of its block slot
+            // (round q, j); a dword past the level's last one is clamped to it (its bytes lie past column lw - 1: never
+            // read)
             const int lastd = (lw - 1) & ~3;
             const bool any = __ballot(corr) != 0;  // wave-uniform: a wave with no window to stage issues nothing
             // lanes without a window load a valid dummy (their keypoint array); r0 / c0 of such a lane are arbitrary
             const uint8_t* dummy = (const uint8_t*)kL;
 #pragma unroll
             for (int q = 0; q < kStereoStageQ; q++) {
-                const int t = 16 * q + li;
-                const bool il = t < 11 * kStereoILd;
-                const int tt = il ? t : t - 11 * kStereoILd;
-                const int rr = il ? tt >> 2 : tt / kStereoIRd, dd = il ? tt & 3 : tt - kStereoIRd * rr;
+                bool il;
+                int rr, dd;
+                if (q < 5) {
+                    il = li < 4;
+                    rr = il ? q : 2 * q + (li >= 10 ? 1 : 0);
+                    dd = il ? li : (li >= 10 ? li - 10 : li - 4);
+                } else if (q == 5) {
+                    il = true;
+                    rr = 5 + (li >> 2);
+                    dd = li & 3;
+                } else {
+                    il = li < 8;
+                    rr = il ? 9 + (li >> 2) : 10;
+                    dd = il ? (li & 3) : min(li - 8, 5);
+                }
                 const int col = min(((il ? c0l : c0r) & ~3) + 4 * dd, lastd);
-                const uint8_t* src = (il ? PL + rr * pitchL : PR + min(rr, 10) * pitchR) + col;
+                const uint8_t* src = (il ? PL + rr * pitchL : PR + rr * pitchR) + col;
                 if (any)
                     __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(corr ? src : dummy),
                                                      (__attribute__((address_space(3))) void*)(stage + 256 * q), 4, 0, 0);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (corr) {  // unaligned rows (a packed odd-width level 0): the same layout a byte at a time
-            for (int k = li; k < 11 * 4 * (kStereoILd + kStereoIRd); k += 16) {
-                const bool il = k < 11 * 4 * kStereoILd;
-                const int kk = il ? k : k - 11 * 4 * kStereoILd;
-                const int rr = il ? kk >> 4 : kk / (4 * kStereoIRd), bb = il ? kk & 15 : kk - 4 * kStereoIRd * rr;
+            for (int k = li; k < 11 * 16 + 11 * 24; k += 16) {
+                const bool il = k < 11 * 16;
+                const int kk = il ? k : k - 11 * 16;
+                const int rr = il ? kk >> 4 : kk / 24, bb = il ? kk & 15 : kk - 24 * rr;
                 const int col = min(((il ? c0l : c0r) & ~3) + bb, lw - 1);
-                const int t = il ? 4 * rr + (bb >> 2) : 11 * kStereoILd + kStereoIRd * rr + (bb >> 2);
-                ((uint8_t*)sg)[4 * (64 * (t >> 4) + (t & 15)) + (bb & 3)] =
-                    il ? PL[rr * pitchL + col] : PR[rr * pitchR + col];
+                ((uint8_t*)sg)[4 * (il ? il_dw(rr) : ir_dw(rr)) + bb] = il ? PL[rr * pitchL + col] : PR[rr * pitchR + col];
             }
         }
         wave_lds_sync();
         // lane li < 11: the L1 distance at shift incR = li - 5 (cv::norm(IL, IR, NORM_L1) of the centre-subtracted
-        // windows: |IL - IR + (cR - cL)| summed, integers, exact)
+        // windows: |IL - IR + (cR - cL)| summed, integers, exact); every row read at constant offsets
         int tot = 0x7fffffff;
         if (corr && li < 11) {
             const int shl = c0l & 3, orr = (c0r & 3) + li;
-            const int cL = sbyte(4 * 5 + ((shl + 5) >> 2), (shl + 5) & 3);
-            const int oc = orr + 5;
-            const int cR = sbyte(11 * kStereoILd + kStereoIRd * 5 + (oc >> 2), oc & 3);
+            const uint8_t* sb = (const uint8_t*)sg;
+            const int cL = sb[4 * il_dw(5) + shl + 5];
+            const int cR = sb[4 * ir_dw(5) + orr + 5];
             const short2v d2 = (short2v){(short)(cR - cL), (short)(cR - cL)};
             short2v acc = (short2v){0, 0};
             const int shr = orr & 3;
+            const uint32_t* irb = sg + (orr >> 2);  // this lane's IR rows start (orr >> 2) dwords in
+#pragma unroll
             for (int r = 0; r < 11; r++) {
-                const uint4 lw4 = *(const uint4*)(sg + 64 * (r >> 2) + 4 * (r & 3));  // IL dwords 4r .. 4r+3
-                const int t0 = 11 * kStereoILd + kStereoIRd * r + (orr >> 2);
-                const uint32_t w0 = sdw(t0), w1 = sdw(t0 + 1), w2 = sdw(t0 + 2), w3 = sdw(t0 + 3);
+                const uint4 lw4 = *(const uint4*)(sg + il_dw(r));
+                const uint32_t* rw = irb + ir_dw(r);
+                const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
                 const uint32_t l0 = __builtin_amdgcn_alignbyte(lw4.y, lw4.x, shl), l1 = __builtin_amdgcn_alignbyte(lw4.z, lw4.y, shl),
                                l2 = __builtin_amdgcn_alignbyte(lw4.w, lw4.z, shl);
                 const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, shr), x1 = __builtin_amdgcn_alignbyte(w2, w1, shr),

@@ -17,7 +17,7 @@ import sys
 
 STAGES = {"pyramid": ("k_pyramid_frames", "k_resize_tiled", "k_resize_level"), "fast_cells": ("k_fast_cells2",),
           "octree": ("k_octree",), "blur": ("k_blur_strips",), "describe": ("k_describe",),
-          "match": ("k_tri_mfma",)}
+          "match": ("k_tri_mfma",), "stereo": ("k_stereo",)}  # k_stereo_median's smaller grid is not the one priced
 
 
 def load(path, counter):
