@@ -218,7 +218,7 @@ def cpu_baseline(frames, threads, seconds=None, nframes=None, nfeatures=1000, st
 
 
 def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, dist, reduce_max, nstreams=4,
-               chunks=0):
+               chunks=0, copy_streams=None, host_wait=False):
     """The schedule with every step's B frames uploaded from pinned host memory (the frame pool, batch
     i mod pool at step i) into the device batch the step processes, on `nstreams` copy streams whatever the
     graph count (several DMA engines in flight: round 3's fourth copy stream was +36 %, and tying the streams to
@@ -226,12 +226,15 @@ def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, 
     contiguous chunks dealt round-robin over the streams in graph order, and graph p starts extracting as soon
     as its own chunks have arrived. Upload i waits for step i-pool (the previous user of that device batch), so
     an upload overlaps the previous step's compute. Returns frames/s over nsteps after `pool` warm-up steps and
-    the H2D rate achieved (bytes per frame uploaded, max over ranks). chunks: chunks per graph (0: ceil(nstreams / P))."""
+    the H2D rate achieved (bytes per frame uploaded, max over ranks). chunks: chunks per graph (0: ceil(nstreams / P)).
+    pool may be below the schedule's batch count (the first `pool` batches are cycled); copy_streams: reuse these
+    streams instead of creating nstreams; host_wait: the host waits for the batch's previous user (step i - pool) to
+    finish before enqueueing its upload, instead of a stream wait on the copy streams."""
     P, sub, dev = sched.P, sched.sub, sched.dev
     per = sched.images_per_frame  # 2 for stereo pairs (left + right image per frame)
     host = [torch.from_numpy(sched.host_batch(frames_np, r)).pin_memory() for r in range(pool)]
-    nst = max(1, nstreams)
-    copy_st = [torch.cuda.Stream(dev) for _ in range(nst)]
+    copy_st = list(copy_streams) if copy_streams else [torch.cuda.Stream(dev) for _ in range(max(1, nstreams))]
+    nst = len(copy_st)
     k = chunks or -(-nst // P)  # chunks per graph (default: enough to give every copy stream one)
     imgs = per * sub
     cuts = [(j * imgs // k, (j + 1) * imgs // k) for j in range(k)]
@@ -241,12 +244,15 @@ def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, 
 
     def one(i):
         r = i % pool
+        if host_wait and used[r]:
+            for e in done[r]:
+                e.synchronize()
         for p in range(P):
             dst = sched.device_images(r, p)
             for j, (a, b) in enumerate(cuts):
                 cs = copy_st[(p * k + j) % nst]
                 with torch.cuda.stream(cs):
-                    if used[r]:
+                    if used[r] and not host_wait:
                         for e in done[r]:
                             cs.wait_event(e)
                     dst[a:b].copy_(host[r][p * imgs + a:p * imgs + b], non_blocking=True)
@@ -269,10 +275,11 @@ def run_ingest(torch, sched, frames_np, pool, nsteps, B, W, H, world, use_dist, 
     fps = world * B * nsteps / el
     return {"frames_per_s": round(fps, 1), "per_gpu_frames_per_s": round(fps / world, 1),
             "h2d_GBs_per_gpu": round(per * B * W * H * nsteps / el / 1e9, 2), "steps": nsteps, "seconds": round(el, 3),
-            "copy_streams": nst, "chunks_per_graph": k,
+            "copy_streams": nst, "chunks_per_graph": k, "upload_waits": "host" if host_wait else "stream",
             "source": "pinned host memory, %d batches of %d frames uploaded round-robin (one batch per step) on %d "
                       "copy streams (%d chunks per graph), overlapped with the previous step's compute; each graph "
-                      "starts on its own frames' arrival" % (pool, B, nst, k)}
+                      "starts on its own frames' arrival; an upload waits for the batch's previous step (%s)"
+                      % (pool, B, nst, k, "on the host" if host_wait else "stream wait on the copy streams")}
 
 
 def launch_ranks(n, argv):
@@ -338,8 +345,9 @@ def main():
                                          "the largest stage of this run's own stage split")
     ap.add_argument("--sustain", type=float, default=6.0,
                     help="seconds of the untimed sustained pass after the timed region (0: skip)")
-    ap.add_argument("--pool", type=int, default=2,
-                    help="resident batches of distinct frames; step k processes batch k mod pool (stale-output guard)")
+    ap.add_argument("--pool", type=int, default=3,
+                    help="resident batches of distinct frames; step k processes batch k mod pool (stale-output guard; "
+                         "the ingest leg re-uploads batch k mod pool, so its upload for step k waits for step k - pool)")
     ap.add_argument("--dist", action="store_true",
                     help="use torch.distributed and the out-of-place RCCL all-gather even at world 1")
     ap.add_argument("--collective", choices=("rccl", "torch"), default="rccl",
@@ -351,6 +359,11 @@ def main():
     ap.add_argument("--ingest-chunks", type=int, default=8,
                     help="upload chunks per graph in the ingest leg, dealt round-robin over the copy streams (4 streams x 8 "
                          "chunks: 53.7 GB/s of the box's 54 GB/s pinned H2D, profiles/r06c_exp_ingest.log)")
+    ap.add_argument("--ingest-wait", choices=("host", "stream"), default="host",
+                    help="how an upload waits for the batch's previous user (step k - pool): host = the enqueueing thread "
+                         "waits on its events before issuing the copies, stream = a stream wait on the copy streams, "
+                         "which holds whichever graph's hardware queue the copy stream shares (pool 3: 175-179k vs "
+                         "145k frames/s, profiles/r06i_exp_ingest2.log)")
     ap.add_argument("--ingest-steps", type=int, default=100,
                     help="steps of the ingest leg (frames uploaded from pinned host memory each step; 0: skip)")
     ap.add_argument("--scene", choices=("shared", "private"), default="shared",
@@ -619,7 +632,8 @@ def main():
         if use_dist:
             dist.barrier()
         ingest = run_ingest(torch, sched, frames_np, args.pool, args.ingest_steps, B, W, H, world, use_dist, dist,
-                            reduce_max, args.ingest_streams, args.ingest_chunks)
+                            reduce_max, args.ingest_streams, args.ingest_chunks,
+                            host_wait=args.ingest_wait == "host")
         if not args.no_check:
             chk = check_schedule(sched, frames_np, nfeatures=cfg["nfeatures"], agent_frames=agent_kf)
             ingest["bit_exact"] = bool(chk["bit_exact"])

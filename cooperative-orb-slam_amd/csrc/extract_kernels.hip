@@ -1607,14 +1607,19 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
     }
     __syncthreads();
     if (__ballot(g < ep.kp_per_frame) == 0) return;  // wave-uniform
-    const int l = level_of(ep.kp_off, ep.L, gc);
-    const int k = gc - ep.kp_off[l];
-    int mycnt = 0, outidx = k;
+    // level, index in the level and output row of the keypoint: one select chain over the frame's L levels
+    int l = 0, koff = 0, mycnt = cl[0], below = 0;
 #pragma unroll
-    for (int q = 0; q < kMaxLevels; q++) {
-        mycnt = q == l ? cl[q] : mycnt;
-        outidx += q < l ? cl[q] : 0;
+    for (int q = 1; q < kMaxLevels; q++) {
+        if (q >= ep.L) break;  // wave-uniform
+        const bool ge = gc >= ep.kp_off[q];
+        l += ge ? 1 : 0;
+        koff = ge ? ep.kp_off[q] : koff;
+        below += ge ? cl[q - 1] : 0;
+        mycnt = ge ? cl[q] : mycnt;
     }
+    const int k = gc - koff;
+    const int outidx = k + below;
     const bool valid = g < ep.kp_per_frame && k < mycnt;
     if (__ballot(valid) == 0) return;  // wave-uniform
     const LevelDesc lv = levels[l];
@@ -1810,14 +1815,18 @@ __device__ __forceinline__ void blur_patch_column(uint8_t* patch, int gd, int co
         auto rowsum = [&](int i, float2v& lo, float2v& hi) {
             const uint32_t a = src[i * (kFusedPitch / 4)], b = src[i * (kFusedPitch / 4) + 1],
                            c = src[i * (kFusedPitch / 4) + 2];
-            const uint32_t o0 = __builtin_amdgcn_udot4(a, A0, __builtin_amdgcn_udot4(b, B0, 0u, false), false);
+            // each dot chain starts at the bit pattern of 2^23, so a row sum s (< 2^16) lands as the float
+            // 2^23 + s; one packed subtract of 2^23 per pair converts two sums exactly (for 4 cvt_f32_u32)
+            constexpr uint32_t Z = 0x4B000000u;
+            const uint32_t o0 = __builtin_amdgcn_udot4(a, A0, __builtin_amdgcn_udot4(b, B0, Z, false), false);
             const uint32_t o1 = __builtin_amdgcn_udot4(
-                a, A1, __builtin_amdgcn_udot4(b, B1, __builtin_amdgcn_udot4(c, C1, 0u, false), false), false);
+                a, A1, __builtin_amdgcn_udot4(b, B1, __builtin_amdgcn_udot4(c, C1, Z, false), false), false);
             const uint32_t o2 = __builtin_amdgcn_udot4(
-                a, A2, __builtin_amdgcn_udot4(b, B2, __builtin_amdgcn_udot4(c, C2, 0u, false), false), false);
-            const uint32_t o3 = __builtin_amdgcn_udot4(b, B3, __builtin_amdgcn_udot4(c, C3, 0u, false), false);
-            lo = (float2v){(float)o0, (float)o1};
-            hi = (float2v){(float)o2, (float)o3};
+                a, A2, __builtin_amdgcn_udot4(b, B2, __builtin_amdgcn_udot4(c, C2, Z, false), false), false);
+            const uint32_t o3 = __builtin_amdgcn_udot4(b, B3, __builtin_amdgcn_udot4(c, C3, Z, false), false);
+            const float2v M23 = {8388608.f, 8388608.f};
+            lo = __builtin_bit_cast(float2v, (uint2v){o0, o1}) - M23;
+            hi = __builtin_bit_cast(float2v, (uint2v){o2, o3}) - M23;
         };
         float2v WL[7], WH[7];
 #pragma unroll
@@ -1859,7 +1868,8 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     __shared__ __align__(16) uint8_t s_patch[kFusedKps][kFusedStride];
     __shared__ int s_bcx[kFusedKps], s_bve[kFusedKps];  // per patch: cx0, blur_vec_end (-1: no keypoint)
     __shared__ float4 s_trig[kFusedKps];  // per patch: (m10, m01) after IC_Angle, then (angle, cos, sin)
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    // wave index through readfirstlane: the LDS-DMA destinations (m0) are scalar
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int sub = lane >> 4, ln = lane & 15;
     // XCD-aware block mapping as k_describe: every workgroup of a frame on one XCD
     const int G = (ep.kp_per_frame + kFusedKps - 1) / kFusedKps;
@@ -1907,14 +1917,20 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
         if (ep.host_out) __threadfence_system();
     }
     __syncthreads();
-    const int l = level_of(ep.kp_off, ep.L, gc);
-    const int k = gc - ep.kp_off[l];
-    int mycnt = 0, outidx = k;
+    // the keypoint's level, its index in the level and its output row (level_of, then the counts of the levels
+    // below): one select chain over the frame's L levels (a uniform trip count), not three over kMaxLevels
+    int l = 0, koff = 0, mycnt = cl[0], below = 0;
 #pragma unroll
-    for (int q = 0; q < kMaxLevels; q++) {
-        mycnt = q == l ? cl[q] : mycnt;
-        outidx += q < l ? cl[q] : 0;
+    for (int q = 1; q < kMaxLevels; q++) {
+        if (q >= ep.L) break;  // wave-uniform
+        const bool ge = gc >= ep.kp_off[q];
+        l += ge ? 1 : 0;
+        koff = ge ? ep.kp_off[q] : koff;
+        below += ge ? cl[q - 1] : 0;
+        mycnt = ge ? cl[q] : mycnt;
     }
+    const int k = gc - koff;
+    const int outidx = k + below;
     const bool valid = g < ep.kp_per_frame && k < mycnt;
     const bool wave_on = __ballot(valid) != 0;  // wave-uniform
     const LevelDesc lv = levels[l];
@@ -1931,12 +1947,16 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
     const int edge = (y < 21 || y + 21 >= lv.h || x < 22 || x + 21 >= lv.w || cx0 + 44 > lastd) ? 1 : 0;
     uint8_t* patch = s_patch[wave * 4 + sub];
     if (wave_on) {  // a wave without keypoints stages nothing (it still reaches the barriers)
-        int rq[9], cq[9];
+        // dword d = 64 q + lane of a window is row rq = d / 12, byte 4 (d - 12 rq): at row pitch sp its source
+        // offset is rq (sp - 48) + 4 d, kept per q for the pitch of the last staged keypoint (the 4 keypoints of a
+        // wave are mostly of one level, so it is computed once per wave and a load is saddr + that voffset)
+        int rq[9], offq[9];
+        int cur_sp = -1;
 #pragma unroll
         for (int q = 0; q < 9; q++) {
             const int d = 64 * q + lane;
             rq[q] = d / 12;
-            cq[q] = 4 * (d - 12 * rq[q]);
+            offq[q] = 0;
         }
         const uint64_t ib = (uint64_t)(uintptr_t)img;
 #pragma unroll
@@ -1949,12 +1969,17 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
             const int scx = __builtin_amdgcn_readlane(cx0, 16 * s);
             uint8_t* dst = s_patch[wave * 4 + s];
             if (__builtin_amdgcn_readlane(edge, 16 * s) == 0) {
+                if (sp != cur_sp) {  // wave-uniform
+                    cur_sp = sp;
+#pragma unroll
+                    for (int q = 0; q < 9; q++) offq[q] = __mul24(rq[q], sp - 48) + 4 * (64 * q + lane);
+                }
                 const uint8_t* b0 = sb + (long long)(sy - 21) * sp + scx;
 #pragma unroll
                 for (int q = 0; q < 9; q++) {
                     if (64 * q + lane < kFusedDwords)
                         __builtin_amdgcn_global_load_lds(
-                            (__attribute__((address_space(1))) void*)(b0 + (unsigned)(rq[q] * sp + cq[q])),
+                            (__attribute__((address_space(1))) void*)(b0 + (unsigned)offq[q]),
                             (__attribute__((address_space(3))) void*)(dst + 256 * q), 4, 0, 0);
                 }
             } else {
@@ -1964,9 +1989,9 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
                 for (int q = 0; q < 9; q++) {
                     if (64 * q + lane < kFusedDwords) {
                         const int rr = reflect101(sy - 21 + rq[q], sh);
-                        const int cc = iclamp(scx + cq[q], 0, sld);
+                        const int cc = iclamp(scx + 4 * (64 * q + lane) - 48 * rq[q], 0, sld);
                         __builtin_amdgcn_global_load_lds(
-                            (__attribute__((address_space(1))) void*)(sb + (long long)rr * sp + cc),
+                            (__attribute__((address_space(1))) void*)(sb + (unsigned)(__mul24(rr, sp) + cc)),
                             (__attribute__((address_space(3))) void*)(dst + 256 * q), 4, 0, 0);
                     }
                 }
