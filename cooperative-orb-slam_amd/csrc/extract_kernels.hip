@@ -20,6 +20,7 @@
 
 #include "../../include/orbslam_amd.h"
 #include "orb_device.h"
+#include "orb_wave.h"
 #include "orb_math.h"
 #include "orb_pattern.h"
 
@@ -427,11 +428,14 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
 #pragma unroll
                     for (int q = 0; q < 2; q++) {
                         const int r = q ? rr[u].y : rr[u].x;
-                        const unsigned off = (unsigned)(r * sp + A);
+                        // (a 24-bit multiply here frees 11 VGPRs, and the 6th wave per SIMD it allows costs the step
+                        // 0.9 %: profiles/r06l_ab_pyramid_mul24.log)
+                        const unsigned rs = (unsigned)(r * sp);
+                        const unsigned off = rs + (unsigned)A;
                         const uint2 lo2 = *(const uint2*)(src + off);
                         w[u][q][0] = lo2.x;
                         w[u][q][1] = lo2.y;
-                        w[u][q][2] = *(const uint32_t*)(src + min(off + 8u, (unsigned)(r * sp + cg.pad[0])));
+                        w[u][q][2] = *(const uint32_t*)(src + min(off + 8u, rs + (unsigned)cg.pad[0]));
                     }
                 }
 #pragma unroll
@@ -566,7 +570,8 @@ __device__ __forceinline__ void fast_cells_body(
         // D dwords per ROI row, 64/D rows per pass; all passes' loads issued before the LDS writes
         const int D = c.D;
         const int rpp = c.rpp;
-        const int lr = (lane * c.magD) >> 16, ld = lane - lr * D;
+        // 24-bit index products (full-rate v_mul_u32_u24 / v_mad_u32_u24; v_mul_lo_u32 is quarter rate)
+        const int lr = __mul24(lane, c.magD) >> 16, ld = lane - __mul24(lr, D);
         const bool on = lane < rpp * D;
         uint32_t v[kMaxPass];  // kMaxPass >= ceil(h / rpp) for every cell (host-chosen)
         const int ldc = on ? ld : 0;
@@ -579,7 +584,7 @@ __device__ __forceinline__ void fast_cells_body(
             const uint8_t* base = img + (long long)c.y0 * pitch;
 #pragma unroll
             for (int kk = 0; kk < kMaxPass; kk++) {
-                const unsigned ro = (unsigned)(min(kk * rpp + lr, c.h - 1) * pitch);
+                const unsigned ro = (unsigned)__mul24(min(kk * rpp + lr, c.h - 1), pitch);
                 const uint32_t w0 = *(const uint32_t*)(base + (ro + o0)), w1 = *(const uint32_t*)(base + (ro + o1));
                 v[kk] = __builtin_amdgcn_alignbyte(w1, w0, k);
             }
@@ -594,8 +599,8 @@ __device__ __forceinline__ void fast_cells_body(
         for (int kk = 0; kk < kMaxPass; kk++) {
             const int r = kk * rpp + lr;
             if (on && r < c.h) {
-                ((uint32_t*)(roi + r * RP))[ld] = v[kk];
-                ((uint32_t*)(str + r * RP))[ld] = 0u;
+                ((uint32_t*)(roi + __mul24(r, RP)))[ld] = v[kk];
+                ((uint32_t*)(str + __mul24(r, RP)))[ld] = 0u;
             }
         }
     }
@@ -612,7 +617,7 @@ __device__ __forceinline__ void fast_cells_body(
         // first pass's candidates and stores the same S for them (S does not depend on t).
         const int G = c.G;  // dword groups covering columns [0, bw+3): (bw + 6) / 4
         const int rpc = c.rpc;
-        const int lr = (lane * c.magG) >> 16, j = lane - lr * G;
+        const int lr = __mul24(lane, c.magG) >> 16, j = lane - __mul24(lr, G);
         const bool lane_ok = lane < rpc * G;
         // band-column mask at the candidate bits: pixel i of this lane's dword -> bit 8 i + 7
         auto colok = [&](int i) { return 4 * j + i >= 3 && 4 * j + i < 3 + bw; };
@@ -638,7 +643,7 @@ __device__ __forceinline__ void fast_cells_body(
                 auto pretest = [&](int r0) -> uint32_t {
                     const int rr = 3 + r0 + lr;
                     const int rrc = min(rr, bh + 2);
-                    const uint8_t* q = roi + rrc * RP + 4 * j;
+                    const uint8_t* q = roi + __mul24(rrc, RP) + 4 * j;
                     const uint32_t xv = *(const uint32_t*)q;
                     const uint32_t xn = *(const uint32_t*)(q + 4);
                     const uint32_t xp = *(const uint32_t*)(q - 4);
@@ -713,7 +718,7 @@ __device__ __forceinline__ void fast_cells_body(
                 const int i = i0 + lane;
                 if (i < ncand) {
                     const int e = i0 == 0 ? e0 : (int)clist[i];
-                    const int o = (e >> 8) * RP + (e & 0xFF);
+                    const int o = __mul24(e >> 8, RP) + (e & 0xFF);
                     const int S = fast_strength_h2(roi, o, RP);
                     if (S > t) str[o] = (uint8_t)S;
                     if (i0 == 0) s0 = S > t ? S : 0;
@@ -730,11 +735,11 @@ __device__ __forceinline__ void fast_cells_body(
                     const uint8_t* sp;
                     if (i0 == 0) {
                         e = e0;
-                        sp = str + (e >> 8) * RP + (e & 0xFF);
+                        sp = str + __mul24(e >> 8, RP) + (e & 0xFF);
                         cS = s0;
                     } else {
                         e = clist[i];
-                        sp = str + (e >> 8) * RP + (e & 0xFF);
+                        sp = str + __mul24(e >> 8, RP) + (e & 0xFF);
                         cS = sp[0];
                     }
                     keep = fast_survivor_c(sp, RP, t, cS);
@@ -779,12 +784,7 @@ __global__ __launch_bounds__(64 * kFastWaves) void k_fast_cells2(
 template <int NW>
 __device__ int block_scan_excl(int v, int* total, int* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += t;
-    }
+    const int inc = wave_scan_incl_i32(v);
     if (lane == 63) red[w] = inc;
     __syncthreads();
     int woff = 0, tot = 0;
@@ -1692,14 +1692,9 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
             S += sI;
             Mp += __umul24(sI, 2u * (uint32_t)p);
         }
-        int A = (int)Ap - 15 * (int)S, M = (int)Mp + (r - 15) * (int)S;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) {
-            A += __shfl_xor(A, o, 16);
-            M += __shfl_xor(M, o, 16);
-        }
-        m10 = A;
-        m01 = M;
+        // 24-bit products (S < 2^24): full-rate v_mad_i32_i24, not a 64-bit / quarter-rate multiply
+        m10 = row16_sum_i32((int)Ap - __mul24(15, (int)S));
+        m01 = row16_sum_i32((int)Mp + __mul24(r - 15, (int)S));
     }
     const float angle = fast_atan2((float)m01, (float)m10);
     // computeOrbDescriptor (ORBextractor.cc:107-147)
@@ -1723,7 +1718,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
         const float2v MAG = {12582912.f, 12582912.f};
         constexpr uint32_t K = 0x400000u * (uint32_t)kDescPatchPitch + 0x4B400000u;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
+        for (int j = 15; j >= 0; j--) {  // bit j is shifted up j times: v_cmp + v_addc per test
             // global table: pairs fetched 4 steps at a time (a scheduling fence per group keeps the compiler
             // from hoisting all 16 loads, i.e. 64 live VGPRs)
             const PatPt pp = s_pat[16 * j + ln];  // pair 16ln + j (transposed)
@@ -1739,7 +1734,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
             const uint32_t o1 = (rb1 & 0xFFFFFFu) * (uint32_t)kDescPatchPitch + cb1 - K;
             const int t0 = pc0[(int)o0];
             const int t1 = pc0[(int)o1];
-            myword |= (uint32_t)(t0 < t1) << j;
+            myword = myword + myword + (uint32_t)(t0 < t1);
         }
     }
     if (valid) {
@@ -2040,14 +2035,9 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
             S += sI;
             Mp += __umul24(sI, 2u * (uint32_t)p);
         }
-        int A = (int)Ap - 15 * (int)S, M = (int)Mp + (r - 15) * (int)S;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) {
-            A += __shfl_xor(A, o, 16);
-            M += __shfl_xor(M, o, 16);
-        }
-        m10 = A;
-        m01 = M;
+        // 24-bit products (S < 2^24): full-rate v_mad_i32_i24, not a 64-bit / quarter-rate multiply
+        m10 = row16_sum_i32((int)Ap - __mul24(15, (int)S));
+        m01 = row16_sum_i32((int)Mp + __mul24(r - 15, (int)S));
     }
     float angle, a, b;
     // blur across the workgroup: wave w blurs patches 6w .. 6w+5 with 10 lanes each (60 of 64 lanes busy,
@@ -2093,7 +2083,7 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
         const float2v MAG = {12582912.f, 12582912.f};
         constexpr uint32_t K = 0x400000u * (uint32_t)kFusedPitch + 0x4B400000u;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
+        for (int j = 15; j >= 0; j--) {  // bit j is shifted up j times: v_cmp + v_addc per test
             const PatPt pp = s_pat[16 * j + ln];
             const float2v X = {pp.x0, pp.x1}, Y = {pp.y0, pp.y1};
             float2v R = (X * B2v + Y * A2v) + MAG;
@@ -2104,7 +2094,7 @@ __global__ __launch_bounds__(64 * kFusedWaves) void k_describe_blur(
             const uint32_t o1 = (RB.y & 0xFFFFFFu) * (uint32_t)kFusedPitch + CB.y - K;
             const int t0 = pc0[(int)o0];
             const int t1 = pc0[(int)o1];
-            myword |= (uint32_t)(t0 < t1) << j;
+            myword = myword + myword + (uint32_t)(t0 < t1);
         }
     }
     if (valid) {
