@@ -488,6 +488,13 @@ struct orbx_handle {
     uint8_t* pin_pyr = nullptr;
     uint8_t* pin_pyr_dev = nullptr;
     size_t pin_pyr_bytes = 0;
+    // orbx_set_host_pyramid_target: caller-owned registered memory receiving the next calls' levels (level 0 at 0,
+    // levels 1..L-1 from host_l0_bytes in the device layout) instead of pin_in / pin_pyr; last_target = the one the
+    // last call filled (what orbx_host_pyramid_level points into)
+    uint8_t* target = nullptr;
+    uint8_t* target_dev = nullptr;
+    size_t target_bytes = 0;
+    uint8_t* last_target = nullptr;
     // stage profiling (orbx_profile_*)
     bool prof_on = false;
     int prof_mask = 0;  // stages with event pairs (bit k = stage k)
@@ -501,6 +508,12 @@ struct orbx_handle {
 
 static const int kProfMaxCalls = 4096;
 static const int kHostCopyBlocks = 16;  // octree-launch workgroups (1024 threads) copying the host path's pyramid
+// pin_out byte offset of the host copy's destination pointer: the captured graph's copy workgroups read it at run time,
+// so a call can deliver its levels into another buffer (orbx_set_host_pyramid_target) without a new capture
+static const int kPinOutCopyDst = 48;
+
+/* bytes of a host pyramid target: level 0 (w x h, contiguous) rounded up to 256, then levels 1..L-1 as on the device */
+static size_t host_l0_bytes(const orbx_handle* h) { return align_up((size_t)h->geo.W * h->geo.H, 256); }
 
 /* stage k = {pyramid, fast_cells, octree, blur, describe}; e = 0 start / 1 end, recorded on the
  * stream the stage's kernel is launched on (the overlapped schedule is kept) */
@@ -1072,7 +1085,12 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
             HIPR(hipHostGetDevicePointer((void**)&h->pin_pyr_dev, h->pin_pyr, 0));
             h->epoch++;
         }
-        hc = HostCopy{(const uint4*)h->pyr.p, (uint4*)h->pin_pyr_dev, (long long)(pb / 16), kHostCopyBlocks};
+        hc = HostCopy{(const uint4*)h->pyr.p, nullptr, (long long)(pb / 16), kHostCopyBlocks,
+                      (uint4* const*)(h->pin_out_dev + kPinOutCopyDst)};
+        if (h->target && h->target_bytes < host_l0_bytes(h) + pb) return ORBX_EARG;
+        // this call's destination of levels 1..L-1, read by the copy workgroups when they run
+        uint8_t* dst = h->target ? h->target_dev + host_l0_bytes(h) : h->pin_pyr_dev;
+        memcpy(h->pin_out + kPinOutCopyDst, &dst, sizeof(dst));
     }
     for (int y = 0; y < height; y++) memcpy(h->pin_in + (size_t)y * width, img + (size_t)y * pitch, width);
     uint8_t* o_kps = h->pin_out + 64;
@@ -1126,9 +1144,12 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int width, int heig
         }
         HIPR(hipGraphLaunch(h->gexec, h->stream));
     }
+    // level 0 of a caller-owned target: the staged input, copied on the host while the device works
+    if (copies && h->target) memcpy(h->target, h->pin_in, in_bytes);
     if (const int rc = wait_until(h->stream, [&] { return __atomic_load_n(done, __ATOMIC_ACQUIRE) != done0; })) return rc;
     // the copy workgroups ride on the octree launch: a skipped octree (orbx_debug_skip_stages bit 2) delivers nothing
     h->host_pyr_valid = copies && !(h->skip_mask & 4);
+    h->last_target = copies ? h->target : nullptr;
     h->last_frames = h->in_frame.as<uint8_t>();
     h->last_fstride = (long long)in_bytes;
     h->last_pitch = width;
@@ -1220,10 +1241,51 @@ int orbx_host_pyramid_level(orbx_handle* h, int level, const uint8_t** data, siz
     if (!h || !data || !pitch || level < 0 || level >= h->T.nlevels || !h->geo.W || !h->host_pyr_valid)
         return ORBX_EARG;
     const LevelDesc& d = h->geo.lv[level];
-    *data = level == 0 ? h->pin_in : h->pin_pyr + d.pyr_off;
+    if (h->last_target)
+        *data = level == 0 ? h->last_target : h->last_target + host_l0_bytes(h) + d.pyr_off;
+    else
+        *data = level == 0 ? h->pin_in : h->pin_pyr + d.pyr_off;
     *pitch = level == 0 ? (size_t)d.w : (size_t)d.pitch;
     if (width) *width = d.w;
     if (height) *height = d.h;
+    return 0;
+}
+
+int orbx_host_pyramid_bytes(orbx_handle* h, int width, int height, size_t* bytes) {
+    if (!h || !bytes || width <= 0 || height <= 0) return ORBX_EARG;
+    *bytes = 0;
+    HIPR(hipSetDevice(h->device));
+    if (const int rc = ensure_geometry(h, width, height, 1)) return rc;
+    *bytes = host_l0_bytes(h) + (size_t)h->geo.ep.pyr_frame_bytes;
+    return 0;
+}
+
+int orbx_host_register(void* p, size_t bytes) {
+    if (!p || !bytes) return ORBX_EARG;
+    HIPR(hipHostRegister(p, bytes, hipHostRegisterMapped));
+    return 0;
+}
+
+int orbx_host_unregister(void* p) {
+    if (!p) return ORBX_EARG;
+    HIPR(hipHostUnregister(p));
+    return 0;
+}
+
+int orbx_set_host_pyramid_target(orbx_handle* h, uint8_t* host, size_t bytes) {
+    if (!h || (host && !bytes)) return ORBX_EARG;
+    if (!host) {
+        h->target = h->target_dev = nullptr;
+        h->target_bytes = 0;
+        return 0;
+    }
+    if (host == h->target && bytes == h->target_bytes) return 0;  // the drop-in sets the same buffer every call
+    HIPR(hipSetDevice(h->device));
+    uint8_t* dev = nullptr;
+    HIPR(hipHostGetDevicePointer((void**)&dev, host, 0));  // fails unless the memory is registered (or pinned) mapped
+    h->target = host;
+    h->target_dev = dev;
+    h->target_bytes = bytes;
     return 0;
 }
 

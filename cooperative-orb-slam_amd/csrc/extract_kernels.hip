@@ -859,8 +859,9 @@ __global__ __launch_bounds__(NT) void k_octree(ExtractParams ep, const LevelDesc
         // memory, beside the octree's few barrier-chained workgroups; visible to the host before the call's done
         // word (k_call_done, a later launch on the same queue)
         const long long stride = (long long)hc.nblocks * NT;
+        uint4* dst = hc.dst_ref ? *(uint4* const volatile*)hc.dst_ref : hc.dst;
         for (long long i = (long long)(blockIdx.x - (gridDim.x - hc.nblocks)) * NT + tid; i < hc.n16; i += stride)
-            hc.dst[i] = hc.src[i];
+            dst[i] = hc.src[i];
         __threadfence_system();
         return;
     }

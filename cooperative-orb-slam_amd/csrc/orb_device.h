@@ -116,6 +116,7 @@ struct HostCopy {
     uint4* dst;
     long long n16;
     int nblocks;
+    uint4* const* dst_ref;  // if set: the destination is read from this (host-mapped) word when the copy runs
 };
 
 /* level containing index g of a per-level prefix table (no dependent loads: unrolled compares

@@ -14,6 +14,39 @@
 
 namespace ORB_SLAM2 {
 
+namespace {
+
+// references to a Mat's storage (the extractor's own one included)
+int storageRefs(const cv::Mat& m) {
+#ifdef CVMIN_CORE_HPP
+    return (int)m.store.use_count();
+#else
+    return m.u ? m.u->refcount : 0;
+#endif
+}
+
+// an h x w header at p inside buf's storage that shares buf's reference count (as Mat(const Mat&, Rect) does)
+cv::Mat storageView(const cv::Mat& buf, const uint8_t* p, int h, int w, size_t step) {
+    cv::Mat m(h, w, CV_8U, (void*)p, step);
+#ifdef CVMIN_CORE_HPP
+    m.store = buf.store;
+#else
+    if (buf.u) {
+        CV_XADD(&buf.u->refcount, 1);
+        m.u = buf.u;
+    }
+#endif
+    return m;
+}
+
+const size_t kPage = 4096;
+const size_t kMaxPyramidSlots = 8;
+
+// the page-aligned registered range inside a slot's storage (whole pages only: no page shared with another allocation)
+uint8_t* slotBase(const cv::Mat& b) { return (uint8_t*)(((uintptr_t)b.data + kPage - 1) & ~(uintptr_t)(kPage - 1)); }
+
+}  // namespace
+
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
     : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
       minThFAST(_minThFAST), mpHandle(nullptr), mHandleW(0), mHandleH(0), mDevice(0), mHostPyramid(-1),
@@ -47,11 +80,61 @@ orbx_params ORBextractor::params() const {
 }
 
 ORBextractor::~ORBextractor() {
+    dropPyramidSlots();  // held levels stay valid as ordinary memory
     if (mpHandle) orbx_destroy(mpHandle);
+}
+
+void ORBextractor::dropPyramidSlots() {
+    if (mpHandle) orbx_set_host_pyramid_target(mpHandle, nullptr, 0);
+    for (size_t i = 0; i < mPyrSlots.size(); i++) amd::StatusOk(orbx_host_unregister(slotBase(mPyrSlots[i])), "orbx_host_unregister");
+    mPyrSlots.clear();
+    mPyrSlotBytes = 0;
+    mPyrCur = -1;
+    mPyrW = mPyrH = 0;
+}
+
+int ORBextractor::selectPyramidSlot(int width, int height) {
+    mPyrCur = -1;
+    size_t need = mPyrSlotBytes;
+    int rc = ORBX_OK;
+    if (width != mPyrW || height != mPyrH || !need) {
+        rc = orbx_host_pyramid_bytes(mpHandle, width, height, &need);
+        if (rc != ORBX_OK) return rc;
+        need = (need + kPage - 1) & ~(kPage - 1);
+    }
+    if (need != mPyrSlotBytes) {
+        dropPyramidSlots();
+        mPyrSlotBytes = need;
+    }
+    mPyrW = width;
+    mPyrH = height;
+    // the member drops the last call's levels first (the reference reassigns it every call), so a slot referenced only
+    // by the extractor is one no caller holds
+    for (size_t l = 0; l < mvImagePyramid.size(); l++) mvImagePyramid[l].release();
+    for (size_t i = 0; i < mPyrSlots.size() && mPyrCur < 0; i++)
+        if (storageRefs(mPyrSlots[i]) == 1) mPyrCur = (int)i;
+    if (mPyrCur < 0) {
+        if (mPyrSlots.size() >= kMaxPyramidSlots) {  // every slot held: the oldest becomes its holders' ordinary memory
+            amd::StatusOk(orbx_host_unregister(slotBase(mPyrSlots.front())), "orbx_host_unregister");
+            mPyrSlots.erase(mPyrSlots.begin());
+        }
+        cv::Mat b(1, (int)(need + kPage), CV_8U);
+        rc = orbx_host_register(slotBase(b), need);
+        if (rc != ORBX_OK) {
+            orbx_set_host_pyramid_target(mpHandle, nullptr, 0);
+            return rc;
+        }
+        mPyrSlots.push_back(b);
+        mPyrCur = (int)mPyrSlots.size() - 1;
+    }
+    rc = orbx_set_host_pyramid_target(mpHandle, slotBase(mPyrSlots[mPyrCur]), need);
+    if (rc != ORBX_OK) mPyrCur = -1;
+    return rc;
 }
 
 int ORBextractor::ensureHandle(int width, int height) {
     if (mpHandle && width <= mHandleW && height <= mHandleH) return ORBX_OK;
+    dropPyramidSlots();
     if (mpHandle) orbx_destroy(mpHandle);
     mpHandle = nullptr;
     mHandleW = mHandleH = 0;
@@ -97,6 +180,12 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask, std::
     mKpBuf.resize(sizeof(orbx_kp) * (size_t)cap);
     mDescBuf.resize(32 * (size_t)cap);
     int n = 0;
+    if (HostPyramidEager()) {
+        // storage for this frame's levels that no caller holds; on failure the handle's own pinned memory
+        // (valid until the next call) serves instead
+        const int sr = selectPyramidSlot(image.cols, image.rows);
+        if (sr != ORBX_OK) amd::StatusOk(sr, "host pyramid storage");
+    }
     rc = orbx_extract(mpHandle, image.data, image.cols, image.rows, image.step, (orbx_kp*)mKpBuf.data(),
                       mDescBuf.data(), cap, &n);
     if (rc != ORBX_OK) return failed(rc, "orbx_extract", _keypoints, _descriptors);
@@ -137,7 +226,7 @@ const std::vector<cv::Mat>& ORBextractor::SyncImagePyramid() {
             mapped = false;
             break;
         }
-        mvImagePyramid[l] = cv::Mat(h, w, CV_8U, (void*)p, step);
+        mvImagePyramid[l] = mPyrCur >= 0 ? storageView(mPyrSlots[mPyrCur], p, h, w, step) : cv::Mat(h, w, CV_8U, (void*)p, step);
     }
     if (mapped) return mvImagePyramid;
     for (int l = 0; l < nlevels; l++) {

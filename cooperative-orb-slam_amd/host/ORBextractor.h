@@ -15,9 +15,13 @@
  * mvImagePyramid: by default every operator() fills the public member with this frame's levels, as the
  * reference does (ORBextractor.cc:1107-1132), so stock readers (Frame::ComputeStereoMatches, A1
  * Frame.cc:474-581) see the current frame: the device writes the levels into the handle's pinned host
- * memory during the call (orbx_set_host_pyramid) and the member's Mats are headers over that memory,
- * holding this frame's levels until the next operator() call on this extractor (a reader that keeps a
- * level past that must clone it). When the drop-in Frame::ComputeStereoMatches
+ * memory during the call (orbx_set_host_pyramid) and the member's Mats are views of refcounted storage
+ * that this extractor registered for device writes. Like the reference, which assigns every level a
+ * freshly allocated Mat in each call (ORBextractor.cc:1114-1115), a level a caller keeps (a shallow
+ * copy of the Mat) keeps this frame's pixels after later calls: each call fills storage no caller
+ * holds (the one buffer of the last call when nobody kept a level, so no copy and no allocation in the
+ * steady state; up to 8 buffers are kept registered, beyond that a held one is handed over to its
+ * holders as ordinary memory). When the drop-in Frame::ComputeStereoMatches
  * (host/Frame_stereo_amd.cc) is linked in, it registers itself as the reader of the device copy and the
  * extractor skips the PCIe copy; the member is then filled lazily by SyncImagePyramid() (once per call).
  * ORBAMD_HOST_PYRAMID=1 / 0 forces the eager / lazy form.
@@ -88,6 +92,14 @@ protected:
     bool mbPyramidStale;  // mvImagePyramid does not hold the last call's levels yet
     int mLastStatus = 0;
     std::vector<unsigned char> mKpBuf, mDescBuf;
+    // eager mvImagePyramid storage: refcounted buffers registered for device writes (orbx_host_register); a call
+    // fills one no caller holds (selectPyramidSlot), the member's Mats are views sharing its reference count
+    std::vector<cv::Mat> mPyrSlots;
+    size_t mPyrSlotBytes = 0;
+    int mPyrCur = -1;  // slot the last call filled
+    int mPyrW = 0, mPyrH = 0;  // frame size mPyrSlotBytes was computed for
+    int selectPyramidSlot(int width, int height);
+    void dropPyramidSlots();
 };
 
 }  // namespace ORB_SLAM2

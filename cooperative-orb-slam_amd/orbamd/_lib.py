@@ -100,6 +100,10 @@ SIGNATURES = {
     "orbx_pyramid_level": (_I, [_P, _I, _I, _P, _SZ, C.POINTER(_I), C.POINTER(_I)]),
     "orbx_set_host_pyramid": (_I, [_P, _I]),
     "orbx_host_pyramid_level": (_I, [_P, _I, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_I), C.POINTER(_I)]),
+    "orbx_host_pyramid_bytes": (_I, [_P, _I, _I, C.POINTER(_SZ)]),
+    "orbx_host_register": (_I, [_P, _SZ]),
+    "orbx_host_unregister": (_I, [_P]),
+    "orbx_set_host_pyramid_target": (_I, [_P, _P, _SZ]),
     "orbx_get_levels": (_I, [_P]),
     "orbx_get_scale_factor": (_F, [_P]),
     "orbx_get_scale_tables": (_I, [_P, _P, _P, _P, _P]),

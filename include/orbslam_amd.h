@@ -108,6 +108,22 @@ int orbx_set_host_pyramid(orbx_handle* h, int on);
 int orbx_host_pyramid_level(orbx_handle* h, int level, const uint8_t** data, size_t* pitch,
                             int* width, int* height);
 
+/* Caller-owned destination of that eager pyramid. The reference assigns every level a freshly
+ * allocated Mat in each call (ORBextractor.cc:1114-1115), so a level a caller keeps is never
+ * overwritten by a later call; the drop-in ORBextractor keeps that by handing each call storage no
+ * caller holds (host/ORBextractor.cc). orbx_host_pyramid_bytes: bytes of one target for a
+ * width x height frame (level 0 contiguous at offset 0, rounded up to 256, then levels 1..L-1 in
+ * the device layout). orbx_host_register / orbx_host_unregister: make caller memory writable by
+ * the device (mapped) and release it again. orbx_set_host_pyramid_target: subsequent
+ * orbx_extract calls on `h` write their levels into `host` (registered, >= bytes of the frame;
+ * ORBX_EARG from orbx_extract otherwise), and orbx_host_pyramid_level then points into the target
+ * the last call filled; host = NULL returns to the handle's own pinned memory. The target stays
+ * the caller's: the library never frees or unregisters it. */
+int orbx_host_pyramid_bytes(orbx_handle* h, int width, int height, size_t* bytes);
+int orbx_host_register(void* p, size_t bytes);
+int orbx_host_unregister(void* p);
+int orbx_set_host_pyramid_target(orbx_handle* h, uint8_t* host, size_t bytes);
+
 /* ORBextractor getters (ORBextractor.h:63-81): GetLevels, GetScaleFactor,
  * GetScaleFactors, GetInverseScaleFactors, GetScaleSigmaSquares,
  * GetInverseScaleSigmaSquares. Arrays have nlevels entries. */

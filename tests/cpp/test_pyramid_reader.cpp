@@ -61,6 +61,55 @@ int main() {
             CHECK(diff == 0, "frame %d: pyramid level %d differs in %d rows", t, l, diff);
         }
     }
+    // A level kept past later calls keeps its frame: the reference assigns every level a new Mat per call
+    // (ORBextractor.cc:1114-1115), so a reader's shallow copy is never overwritten by the next ExtractORB.
+    auto run = [&](int t, std::vector<std::vector<uint8_t> >* lv) {
+        orbx_synth_frame(1, t, W, H, img.data());
+        cv::Mat im(H, W, CV_8U, img.data(), W);
+        std::vector<cv::KeyPoint> kps;
+        cv::Mat desc;
+        ext(im, cv::Mat(), kps, desc);
+        int n = 0;
+        oc_extract(orc, img.data(), W, H, W, okp.data(), odesc.data(), 64 * 1024, &n);
+        lv->assign(ext.GetLevels(), std::vector<uint8_t>());
+        for (int l = 0; l < ext.GetLevels(); l++) {
+            int w, h;
+            oc_level_size(orc, l, &w, &h);
+            (*lv)[l].assign(oc_pyramid(orc, l), oc_pyramid(orc, l) + (size_t)w * h);
+        }
+    };
+    auto same = [&](const cv::Mat& m, const std::vector<uint8_t>& ref) {
+        if (m.empty() || (size_t)m.rows * m.cols != ref.size()) return false;
+        for (int y = 0; y < m.rows; y++)
+            if (memcmp(m.ptr<unsigned char>(y), ref.data() + (size_t)y * m.cols, m.cols)) return false;
+        return true;
+    };
+    std::vector<std::vector<uint8_t> > la, lb;
+    run(10, &la);
+    std::vector<cv::Mat> kept(ext.mvImagePyramid);  // shallow copies, as a reader that stores the Mats holds them
+    run(11, &lb);
+    for (int l = 0; l < ext.GetLevels(); l++) {
+        CHECK(same(ext.mvImagePyramid[l], lb[l]), "member level %d is not the current frame's", l);
+        CHECK(same(kept[l], la[l]), "a kept level %d was overwritten by the next call", l);
+        CHECK(kept[l].data != ext.mvImagePyramid[l].data, "kept level %d shares the current frame's storage", l);
+    }
+    kept.clear();
+    // nobody holds a level: consecutive calls reuse one buffer (no allocation, no copy in the steady state)
+    run(12, &la);
+    const unsigned char* p12 = ext.mvImagePyramid[1].data;
+    run(13, &lb);
+    CHECK(ext.mvImagePyramid[1].data == p12, "steady state: the level storage was not reused");
+    for (int l = 0; l < ext.GetLevels(); l++) CHECK(same(ext.mvImagePyramid[l], lb[l]), "frame 13 level %d", l);
+    // more frames held than the extractor keeps registered (8): every held level keeps its frame
+    std::vector<cv::Mat> held;
+    std::vector<std::vector<uint8_t> > want;
+    for (int t = 20; t < 32; t++) {
+        std::vector<std::vector<uint8_t> > lt;
+        run(t, &lt);
+        held.push_back(ext.mvImagePyramid[t % ext.GetLevels()]);
+        want.push_back(lt[t % ext.GetLevels()]);
+    }
+    for (size_t i = 0; i < held.size(); i++) CHECK(same(held[i], want[i]), "held level of frame %d changed", 20 + (int)i);
     oc_destroy(orc);
     printf(failures ? "FAILURES %d\n" : "ALL PASS\n", failures);
     return failures ? 1 : 0;

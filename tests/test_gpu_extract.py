@@ -256,3 +256,67 @@ def test_host_pyramid_delivery():
     ext(frames[1])
     assert level(1) == -1  # a stage-profiled call delivers none
     ext.close()
+
+
+@pytest.mark.gpu
+def test_host_pyramid_caller_targets():
+    """orbx_set_host_pyramid_target (the storage of the drop-in's refcounted mvImagePyramid, so a level a caller keeps
+    is not overwritten by the next call, as with the reference's per-call Mats, ORBextractor.cc:1114-1115): each call
+    fills the registered target set before it, level 0 at offset 0 and levels 1..L-1 after it, bit-exact against the
+    oracle, captured-graph replays included; a target filled earlier keeps its frame; a target smaller than
+    orbx_host_pyramid_bytes is rejected; NULL returns to the handle's own memory."""
+    import ctypes as C
+    W, H = 640, 480
+    frames = orbamd.synth_frames(4, 3, 5, W, H)
+    ext = orbamd.ORBextractor(1000, 1.2, 8, 20, 7, max_width=W, max_height=H)
+    orc = oracle_py.OracleExtractor(1000, 1.2, 8, 20, 7)
+    lib = orbamd.load()
+    assert lib.orbx_set_host_pyramid(ext._h, 1) == 0
+    nb = C.c_size_t()
+    assert lib.orbx_host_pyramid_bytes(ext._h, W, H, C.byref(nb)) == 0
+    page = 4096
+    need = (nb.value + page - 1) // page * page
+    raw = [np.zeros(need + page, np.uint8) for _ in range(2)]
+    tgt = [r[(-r.ctypes.data) % page:][:need] for r in raw]  # page-aligned views
+    for t in tgt:
+        assert lib.orbx_host_register(t.ctypes.data, need) == 0
+    p, pitch, w, h = C.c_void_p(), C.c_size_t(), C.c_int(), C.c_int()
+
+    def level(lv):
+        assert lib.orbx_host_pyramid_level(ext._h, lv, C.byref(p), C.byref(pitch), C.byref(w), C.byref(h)) == 0
+        buf = (C.c_uint8 * (pitch.value * h.value)).from_address(p.value)
+        return p.value, np.frombuffer(buf, np.uint8).reshape(h.value, pitch.value)[:, :w.value].copy()
+
+    try:
+        want = []
+        for f in range(frames.shape[0]):
+            k = f % 2
+            assert lib.orbx_set_host_pyramid_target(ext._h, tgt[k].ctypes.data, need) == 0
+            kg, dg = ext(frames[f])
+            ko, do = orc(frames[f])
+            _compare(kg, dg, ko, do)
+            lv_f = [orc.pyramid(lv).copy() for lv in range(8)]
+            for lv in range(8):
+                addr, got = level(lv)
+                assert tgt[k].ctypes.data <= addr < tgt[k].ctypes.data + need, (f, lv)
+                np.testing.assert_array_equal(got, lv_f[lv], err_msg="frame %d level %d" % (f, lv))
+            if f:
+                # the other target still holds the previous frame (level 0 at offset 0, w x h contiguous)
+                prev = tgt[1 - k][:W * H].reshape(H, W)
+                np.testing.assert_array_equal(prev, want[-1][0])
+            want.append(lv_f)
+        assert lib.orbx_set_host_pyramid_target(ext._h, tgt[0].ctypes.data, need - page) == 0
+        img = np.ascontiguousarray(frames[0])
+        cap = ext.max_keypoints(W, H)
+        kbuf, dbuf, n = np.empty(cap * 24, np.uint8), np.empty(cap * 32, np.uint8), C.c_int()
+        rc = lib.orbx_extract(ext._h, img.ctypes.data, W, H, W, kbuf.ctypes.data, dbuf.ctypes.data, cap, C.byref(n))
+        assert rc == -1  # ORBX_EARG: the target cannot hold the frame's levels
+        assert lib.orbx_set_host_pyramid_target(ext._h, None, 0) == 0
+        ext(frames[2])
+        addr, got = level(3)
+        assert not (tgt[0].ctypes.data <= addr < tgt[0].ctypes.data + need)
+        np.testing.assert_array_equal(got, want[2][3])
+    finally:
+        ext.close()
+        for t in tgt:
+            assert lib.orbx_host_unregister(t.ctypes.data) == 0
