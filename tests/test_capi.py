@@ -89,3 +89,18 @@ def test_bad_arguments():
     assert lib.orbx_create(None, 0, 640, 480, 1, C.byref(h)) == -1
     p = OrbxParams(1000, 1.2, 99, 20, 7)
     assert lib.orbx_create(C.byref(p), 0, 640, 480, 1, C.byref(h)) == -1
+
+
+def test_host_pyramid_target_arguments():
+    """the caller-owned eager-pyramid storage (orbx_host_register / orbx_set_host_pyramid_target, the drop-in's
+    refcounted mvImagePyramid): argument checks, and no GPU means ORBX_EDEVICE, never a silent success"""
+    lib = orbamd.load()
+    nb = C.c_size_t(7)
+    assert lib.orbx_host_pyramid_bytes(None, 640, 480, C.byref(nb)) == -1
+    assert lib.orbx_set_host_pyramid_target(None, None, 0) == -1
+    assert lib.orbx_host_register(None, 4096) == -1
+    assert lib.orbx_host_unregister(None) == -1
+    buf = np.zeros(8192, np.uint8)
+    assert lib.orbx_host_register(buf.ctypes.data, 0) == -1
+    if lib.orbx_device_count() == 0:
+        assert lib.orbx_host_register(buf.ctypes.data, 4096) == -2  # ORBX_EDEVICE
