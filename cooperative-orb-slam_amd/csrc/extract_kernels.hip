@@ -412,6 +412,7 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
         const int ry = tid / gw, xg = tid - ry * gw;
         const PyrColGroup cg = ((const PyrColGroup*)(ptab + lv.cg_off))[min(xg, gw - 1)];
         const int A = cg.W & ~3, k = cg.W & 3;
+        const int edge4 = A + 8 > cg.pad[0] ? 4 : 0;  // pad[0]: the row's last dword (host: align4(sw) - 4)
         const int x0 = 4 * xg;
         const bool tail = x0 + 3 >= lv.simd_end;
         __syncthreads();
@@ -431,11 +432,15 @@ __global__ __launch_bounds__(NT) void k_pyramid_frames(const uint8_t* __restrict
                         // (a 24-bit multiply here frees 11 VGPRs, and the 6th wave per SIMD it allows costs the step
                         // 0.9 %: profiles/r06l_ab_pyramid_mul24.log)
                         const unsigned rs = (unsigned)(r * sp);
-                        const unsigned off = rs + (unsigned)A;
-                        const uint2 lo2 = *(const uint2*)(src + off);
-                        w[u][q][0] = lo2.x;
-                        w[u][q][1] = lo2.y;
-                        w[u][q][2] = *(const uint32_t*)(src + min(off + 8u, rs + (unsigned)cg.pad[0]));
+                        // the window's 3 dwords by one 12-byte load; the row's last group (whose third dword would
+                        // start past the row's last dword) loads 4 bytes earlier and takes the clamped dword twice.
+                        // The dwordx2 + dword pair requested the window's lines twice: pyramid alone 0.181 -> 0.168
+                        // ms per 256 frames, 80 instead of 85 VGPRs, the step +0.8 % (profiles/r06zc_ab_pyr_x3.log)
+                        typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
+                        const u32x3a4 L3 = *(const u32x3a4*)(src + (rs + (unsigned)(A - edge4)));
+                        w[u][q][0] = edge4 ? L3.y : L3.x;
+                        w[u][q][1] = edge4 ? L3.z : L3.y;
+                        w[u][q][2] = L3.z;
                     }
                 }
 #pragma unroll
@@ -585,8 +590,14 @@ __device__ __forceinline__ void fast_cells_body(
 #pragma unroll
             for (int kk = 0; kk < kMaxPass; kk++) {
                 const unsigned ro = (unsigned)__mul24(min(kk * rpp + lr, c.h - 1), pitch);
-                const uint32_t w0 = *(const uint32_t*)(base + (ro + o0)), w1 = *(const uint32_t*)(base + (ro + o1));
-                v[kk] = __builtin_amdgcn_alignbyte(w1, w0, k);
+                // both dwords by one 8-byte load (an active lane's o0 + 4 is always inside the row: cells end 13
+                // columns before the level's edge, so the clamp to lastd never binds for them). Two dword loads
+                // request every line of the ROI twice, and the staging is bound by those requests: 398.0k -> 403.2k
+                // frames/s, FAST alone 0.220 -> 0.215 ms per 256 frames (profiles/r06zb_ab_fast_x2.log; staging alone with
+                // half the requests 0.46 -> 0.31 ms per 1024 frames, r06z_fast_half_loads.txt)
+                typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+                const u32x2a4 w = *(const u32x2a4*)(base + (ro + o0));
+                v[kk] = __builtin_amdgcn_alignbyte(w.y, w.x, k);
             }
         } else {
 #pragma unroll
