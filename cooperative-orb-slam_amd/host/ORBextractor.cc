@@ -99,7 +99,10 @@ int ORBextractor::selectPyramidSlot(int width, int height) {
     int rc = ORBX_OK;
     if (width != mPyrW || height != mPyrH || !need) {
         rc = orbx_host_pyramid_bytes(mpHandle, width, height, &need);
-        if (rc != ORBX_OK) return rc;
+        if (rc != ORBX_OK) {
+            orbx_set_host_pyramid_target(mpHandle, nullptr, 0);  // never the last call's buffer: a caller may hold it
+            return rc;
+        }
         need = (need + kPage - 1) & ~(kPage - 1);
     }
     if (need != mPyrSlotBytes) {
@@ -128,7 +131,10 @@ int ORBextractor::selectPyramidSlot(int width, int height) {
         mPyrCur = (int)mPyrSlots.size() - 1;
     }
     rc = orbx_set_host_pyramid_target(mpHandle, slotBase(mPyrSlots[mPyrCur]), need);
-    if (rc != ORBX_OK) mPyrCur = -1;
+    if (rc != ORBX_OK) {
+        mPyrCur = -1;
+        orbx_set_host_pyramid_target(mpHandle, nullptr, 0);
+    }
     return rc;
 }
 
