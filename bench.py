@@ -8,7 +8,7 @@ all features = the BASELINE "BF" configuration) + the cooperative exchange: each
 latest keyframe into a keyframe slot, RCCL-all-gathers it, then matches it against every agent's
 slot. One process per GPU = one agent; frames are agent-private, so
 per-GPU work is fixed as N grows ("weak" scaling). The B frames are split over P concurrent,
-staggered extraction+match graphs (default 1024 frames as 4 graphs of 256).
+staggered extraction+match graphs (default 3840 frames as 3 graphs of 1280).
 
 After the timed region the run checks itself: every graph's device error flags, then sampled
 frames (first / middle / last of every graph) with their match rows and the cross-agent matches,
@@ -305,6 +305,13 @@ def launch_ranks(n, argv):
     return subprocess.call(cmd)
 
 
+def default_batch(per):
+    """frames per step per GPU: 3 graphs of 1280 frames (C2; 3 x 1024 measured 2.5 % slower on the round-6 kernels,
+    3 x 1536 equal, 3 x 1792 / 2048 and 2 x 2048 slower: profiles/r06zk_shape*.log), or 1536 stereo pairs (3 x 512 pairs =
+    1024 images per graph at C3 / C4, where 3 x 640 pairs is equal)"""
+    return 3840 if per == 1 else 1536
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -312,7 +319,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
     ap.add_argument("--batch", type=int, default=0,
-                    help="frames per step per GPU (0: 3072, or 1536 stereo pairs = 3072 images at c3 / c4)")
+                    help="frames per step per GPU (0: 3840 = 3 graphs of 1280, or 1536 stereo pairs = 3072 images at "
+                         "c3 / c4)")
     ap.add_argument("--mono", action="store_true",
                     help="c3 / c4: their left images alone (monocular frames) instead of the stereo pairs the configs name")
     ap.add_argument("--pipes", type=int, default=3,
@@ -385,7 +393,7 @@ def main():
     cfg = CONFIGS[args.config]
     if args.launch_frames:  # images one stage launch processes (stereo: a graph's left + right images)
         per = 1 if args.mono or "stereo" not in cfg else 2
-        print(per * ((args.batch or 3072 // per) // args.pipes), args.pipes)
+        print(per * ((args.batch or default_batch(per)) // args.pipes), args.pipes)
         return
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -448,7 +456,7 @@ def main():
     W, H, P = cfg["W"], cfg["H"], args.pipes
     rig = None if args.mono or "stereo" not in cfg else orbamd.device.STEREO_RIGS[cfg["stereo"]]
     per = 2 if rig else 1  # images per frame
-    B = args.batch or (3072 // per)
+    B = args.batch or default_batch(per)
     assert B % P == 0, "--batch must be a multiple of --pipes"
     assert args.pool >= 1
     sub = B // P
